@@ -1,0 +1,984 @@
+"""duckdb.mbt_amd — host-side mirror of the duckdb.mbt MoonBit API over the
+MI355X C-ABI library (libduckdb_mb_amd.so, include/duckdb_mb.h).
+
+The reference's host language (MoonBit, `moon` toolchain) is not available in
+this image, so this module re-states the MoonBit driver layer on top of the
+same 89 `duckdb_mb_*` entry points it binds:
+
+  connect / Connection.query        /root/reference/src/duckdb_native.mbt:429-501
+  Connection.query_stream / next    /root/reference/src/duckdb_native.mbt:504-582
+  Config / connect_with_config      /root/reference/src/duckdb_native.mbt:608-662
+  prepare / bind_* / execute        /root/reference/src/duckdb_native.mbt:760-938
+  create_appender / Appender.*      /root/reference/src/duckdb_native.mbt:955-1076
+  query_arrow / ArrowResult.*       /root/reference/src/duckdb_arrow_native.mbt:123-822
+  QueryResult / Value / ColumnType  /root/reference/src/duckdb.mbt:49-278
+  to_typed / TypedQueryResult       /root/reference/src/duckdb_typed_result.mbt:8-379
+  column_type_from_id / parse_*     /root/reference/src/duckdb_parsing.mbt:8-257
+
+Callbacks are invoked synchronously (as on the reference's native target).
+Results are `Ok(value)` / `Err(DuckDBError)`.  MoonBit `Int` is 32-bit: the
+typed layer saturates integers to int32 exactly like parse_int
+(duckdb_parsing.mbt:203-237), and the Arrow decoders reject more than
+1 000 000 rows (duckdb_arrow_native.mbt:435, :474, ...).
+
+There is no CPU execution path: if the HIP library is missing, importing the
+module raises.
+"""
+from __future__ import annotations
+
+import ctypes
+import math
+import os
+import struct
+from dataclasses import dataclass, field
+from typing import Any, Callable, List, Optional
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.environ.get("DUCKDB_MB_AMD_LIB", os.path.join(_HERE, "libduckdb_mb_amd.so"))
+
+
+def _load():
+    if not os.path.exists(LIB_PATH):
+        raise ImportError(
+            f"libduckdb_mb_amd.so not found at {LIB_PATH}: run `make -C duckdb.mbt_amd` "
+            "(or __graft_entry__.build()); there is no CPU fallback"
+        )
+    return ctypes.CDLL(LIB_PATH)
+
+
+lib = _load()
+
+_P = ctypes.c_void_p
+_B = ctypes.POINTER(ctypes.c_uint8)
+_I = ctypes.c_int32
+_L = ctypes.c_int64
+
+
+def _sig(name, res, *args):
+    f = getattr(lib, name)
+    f.restype = res
+    f.argtypes = list(args)
+    return f
+
+
+# --- MoonBit bytes ----------------------------------------------------------
+_sig("moonbit_make_bytes_raw", _B, _I)
+_sig("duckdb_mbx_bytes_new", _B, ctypes.c_char_p, _I)
+_sig("duckdb_mbx_bytes_len", _I, _B)
+_sig("duckdb_mbx_bytes_free", None, _B)
+_sig("duckdb_mbx_free", None, _P)
+_sig("duckdb_mbx_device_count", _I)
+_sig("duckdb_mbx_explain", ctypes.c_void_p, _P, ctypes.c_char_p, _L)
+_sig("duckdb_mbx_last_profile", ctypes.c_void_p, _P)
+_sig("duckdb_mbx_result_raw", _I, _P, _I, _I, _P, _I)
+_sig("duckdb_mbx_append_column", _I, _P, _I, _P, _P, _L)
+_sig("duckdb_mbx_append_commit", _I, _P, _L)
+
+for _n in ["duckdb_mb_connect"]:
+    _sig(_n, _P, _B)
+_sig("duckdb_mb_connect_with_config", _P, _B, _P)
+_sig("duckdb_mb_disconnect", None, _P)
+_sig("duckdb_mb_is_null_conn", _I, _P)
+_sig("duckdb_mb_last_error", _B)
+_sig("duckdb_mb_query", _P, _P, _B)
+_sig("duckdb_mb_result_destroy", None, _P)
+_sig("duckdb_mb_result_column_count", _I, _P)
+_sig("duckdb_mb_result_row_count", _I, _P)
+_sig("duckdb_mb_result_column_name", _B, _P, _I)
+_sig("duckdb_mb_result_column_type", _I, _P, _I)
+_sig("duckdb_mb_result_is_null", _I, _P, _I, _I)
+_sig("duckdb_mb_result_value", _B, _P, _I, _I)
+_sig("duckdb_mb_is_null_result", _I, _P)
+_sig("duckdb_mb_query_stream", _P, _P, _B)
+_sig("duckdb_mb_execute_prepared_stream", _P, _P)
+_sig("duckdb_mb_stream_destroy", None, _P)
+_sig("duckdb_mb_is_null_stream", _I, _P)
+_sig("duckdb_mb_stream_column_count", _I, _P)
+_sig("duckdb_mb_stream_column_name", _B, _P, _I)
+_sig("duckdb_mb_stream_fetch_chunk", _P, _P)
+_sig("duckdb_mb_chunk_destroy", None, _P)
+_sig("duckdb_mb_is_null_chunk", _I, _P)
+_sig("duckdb_mb_chunk_row_count", _I, _P)
+_sig("duckdb_mb_chunk_column_count", _I, _P)
+_sig("duckdb_mb_chunk_is_null", _I, _P, _I, _I)
+_sig("duckdb_mb_chunk_value", _B, _P, _I, _I)
+_sig("duckdb_mb_config_create", _P)
+_sig("duckdb_mb_config_destroy", None, _P)
+_sig("duckdb_mb_config_error", _B, _P)
+_sig("duckdb_mb_config_set", _I, _P, _B, _B)
+_sig("duckdb_mb_prepare", _P, _P, _B)
+_sig("duckdb_mb_statement_destroy", None, _P)
+_sig("duckdb_mb_statement_error", _B, _P)
+_sig("duckdb_mb_bind_int", _I, _P, _I, _I)
+_sig("duckdb_mb_bind_bigint", _I, _P, _I, _L)
+_sig("duckdb_mb_bind_double", _I, _P, _I, ctypes.c_double)
+_sig("duckdb_mb_bind_varchar", _I, _P, _I, _B)
+_sig("duckdb_mb_bind_bool", _I, _P, _I, ctypes.c_bool)
+_sig("duckdb_mb_bind_null", _I, _P, _I)
+_sig("duckdb_mb_clear_bindings", _I, _P)
+_sig("duckdb_mb_execute_prepared", _P, _P)
+_sig("duckdb_mb_is_null_statement", _I, _P)
+_sig("duckdb_mb_bind_date", _I, _P, _I, _I)
+_sig("duckdb_mb_bind_timestamp", _I, _P, _I, _L)
+_sig("duckdb_mb_bind_decimal", _I, _P, _I, ctypes.c_uint8, ctypes.c_uint8, _L, _L)
+_sig("duckdb_mb_bind_interval", _I, _P, _I, _I, _I, _L)
+_sig("duckdb_mb_appender_create", _P, _P, _B, _B)
+_sig("duckdb_mb_appender_destroy", None, _P)
+_sig("duckdb_mb_appender_error", _B, _P)
+_sig("duckdb_mb_begin_row", _I, _P)
+_sig("duckdb_mb_append_int", _I, _P, _I)
+_sig("duckdb_mb_append_bigint", _I, _P, _L)
+_sig("duckdb_mb_append_double", _I, _P, ctypes.c_double)
+_sig("duckdb_mb_append_varchar", _I, _P, _B)
+_sig("duckdb_mb_append_bool", _I, _P, ctypes.c_bool)
+_sig("duckdb_mb_append_null", _I, _P)
+_sig("duckdb_mb_end_row", _I, _P)
+_sig("duckdb_mb_flush", _I, _P)
+_sig("duckdb_mb_is_null_appender", _I, _P)
+_sig("duckdb_mb_append_date", _I, _P, _I)
+_sig("duckdb_mb_append_timestamp", _I, _P, _L)
+_sig("duckdb_mb_append_decimal", _I, _P, ctypes.c_uint8, ctypes.c_uint8, _L, _L)
+_sig("duckdb_mb_append_interval", _I, _P, _I, _I, _L)
+_sig("duckdb_mb_query_arrow", _P, _P, _B)
+_sig("duckdb_mb_arrow_destroy", None, _P)
+_sig("duckdb_mb_arrow_column_count", _I, _P)
+_sig("duckdb_mb_arrow_row_count", _I, _P)
+_sig("duckdb_mb_arrow_schema", _B, _P)
+for _n in ["int32", "int64", "double", "string", "bool"]:
+    _sig(f"duckdb_mb_arrow_get_column_{_n}", _B, _P, _I)
+    _sig(f"duckdb_mb_arrow_get_column_{_n}_nullable", _B, _P, _I)
+_sig("duckdb_mb_is_null_arrow_result", _I, _P)
+_sig("duckdb_mb_bytes_to_double", ctypes.c_double, ctypes.c_char_p, _I)
+
+
+def _enc(s: str):
+    b = s.encode("utf-8")
+    return lib.duckdb_mbx_bytes_new(b, len(b))
+
+
+def _take(bp) -> bytes:
+    """Copies a returned MoonBit Bytes object and releases it."""
+    if not bp:
+        return b""
+    n = lib.duckdb_mbx_bytes_len(bp)
+    data = ctypes.string_at(bp, n)
+    lib.duckdb_mbx_bytes_free(bp)
+    return data
+
+
+def _str(bp) -> str:
+    return _take(bp).decode("utf-8", errors="replace")  # @encoding/utf8.decode_lossy
+
+
+class _Arg:
+    """A MoonBit Bytes argument owned by the caller (borrowed by the callee)."""
+
+    def __init__(self, s: str):
+        self.p = _enc(s)
+
+    def __del__(self):
+        if self.p:
+            lib.duckdb_mbx_bytes_free(self.p)
+            self.p = None
+
+
+def device_count() -> int:
+    return lib.duckdb_mbx_device_count()
+
+
+# --- public types (src/duckdb.mbt) -----------------------------------------
+class DuckDBError(Exception):
+    """DuckDBError::Message(String)."""
+
+    @property
+    def message(self) -> str:
+        return self.args[0]
+
+
+@dataclass
+class Ok:
+    value: Any
+
+
+@dataclass
+class Err:
+    error: DuckDBError
+
+
+COLUMN_TYPES = {
+    0: "Invalid", 1: "Boolean", 2: "TinyInt", 3: "SmallInt", 4: "Integer", 5: "BigInt", 6: "UTinyInt",
+    7: "USmallInt", 8: "UInteger", 9: "UBigInt", 10: "Float", 11: "Double", 12: "Timestamp", 13: "Date",
+    14: "Time", 15: "Interval", 16: "HugeInt", 17: "Varchar", 18: "Blob", 19: "Decimal", 20: "TimestampS",
+    21: "TimestampMs", 22: "TimestampNs", 23: "Enum", 24: "List", 25: "Struct", 26: "Map", 27: "Uuid",
+    28: "Union", 29: "Bit", 30: "TimeTz", 31: "TimestampTz", 32: "UHugeInt", 33: "Array", 34: "Any",
+    35: "Bignum", 36: "SqlNull", 37: "StringLiteral", 38: "IntegerLiteral", 39: "TimeNs",
+}
+
+
+def column_type_from_id(i: int) -> str:
+    """duckdb_parsing.mbt:8-52; unknown ids map to Unknown(id)."""
+    return COLUMN_TYPES.get(i, f"Unknown({i})")
+
+
+INT_MAX = 2**31 - 1
+INT_MIN = -(2**31)
+
+
+def parse_int(s: str) -> int:
+    """duckdb_parsing.mbt:203-237: digits accumulate negatively, saturating at
+    the 32-bit MoonBit Int range; non-digit characters are skipped."""
+    result = 0
+    negative = False
+    start = 0
+    if s:
+        if s[0] == "-":
+            negative, start = True, 1
+        elif s[0] == "+":
+            start = 1
+    limit = INT_MIN if negative else -INT_MAX
+    multmin = int(limit / 10)  # MoonBit Int division truncates
+    for c in s[start:]:
+        if "0" <= c <= "9":
+            digit = ord(c) - 48
+            if result < multmin:
+                return INT_MIN if negative else INT_MAX
+            result = result * 10
+            nxt = result - digit
+            if nxt < limit:
+                return INT_MIN if negative else INT_MAX
+            result = nxt
+    return result if negative else -result
+
+
+def is_integer(s: str) -> bool:
+    if not s:
+        return False
+    start = 1 if s[0] in "+-" else 0
+    body = s[start:]
+    return len(body) > 0 and all("0" <= c <= "9" for c in body)
+
+
+def is_double(s: str) -> bool:
+    if not s:
+        return False
+    start = 1 if s[0] in "+-" else 0
+    has_dot = has_digit = False
+    for c in s[start:]:
+        if c == ".":
+            if has_dot:
+                return False
+            has_dot = True
+        elif not ("0" <= c <= "9"):
+            return False
+        else:
+            has_digit = True
+    return has_digit and has_dot
+
+
+def _parse_fractional(s: str) -> float:
+    # duckdb_parsing.mbt parse_fractional: digit / 10^k accumulation
+    v, scale = 0.0, 0.1
+    for c in s:
+        if "0" <= c <= "9":
+            v += (ord(c) - 48) * scale
+            scale /= 10.0
+    return v
+
+
+def parse_double(s: str) -> float:
+    """duckdb_parsing.mbt:241-257."""
+    idx = s.find(".")
+    if idx >= 0:
+        int_val = parse_int(s[:idx])
+        frac_val = _parse_fractional(s[idx + 1:])
+        sign = -1.0 if s and s[0] == "-" else 1.0
+        return sign * (float(abs(int_val)) + frac_val)
+    return float(parse_int(s))
+
+
+SPECIAL_FLOATS = {"nan", "NaN", "inf", "Infinity", "-inf", "-Infinity"}
+
+
+@dataclass
+class Value:
+    kind: str  # "Null" | "Bool" | "Int" | "Double" | "String" | "Date" | "Timestamp"
+    value: Any = None
+
+    def __eq__(self, o):
+        return isinstance(o, Value) and self.kind == o.kind and self.value == o.value
+
+
+def parse_value(s: str) -> Value:
+    """duckdb_parsing.mbt:56-78 (date/timestamp detection kept as strings here)."""
+    if s == "true":
+        return Value("Bool", True)
+    if s == "false":
+        return Value("Bool", False)
+    if is_integer(s):
+        return Value("Int", parse_int(s))
+    if is_double(s):
+        return Value("Double", parse_double(s))
+    return Value("String", s)
+
+
+_INT_KINDS = {"TinyInt", "SmallInt", "Integer", "BigInt", "UTinyInt", "USmallInt", "UInteger", "UBigInt"}
+_STR_KINDS = {"Varchar", "Enum", "Uuid", "StringLiteral", "Decimal", "HugeInt", "UHugeInt", "Interval", "List",
+              "Struct", "Map", "Array", "Union", "Bit", "Time", "TimeTz", "TimeNs", "Any", "Bignum", "Blob",
+              "SqlNull", "IntegerLiteral"}
+
+
+def parse_value_with_type(s: str, column_type: str) -> Value:
+    """duckdb_parsing.mbt:82-144."""
+    if column_type == "Boolean":
+        return Value("Bool", True) if s == "true" else Value("Bool", False) if s == "false" else Value("String", s)
+    if column_type in _INT_KINDS:
+        return Value("Int", parse_int(s))
+    if column_type in ("Float", "Double"):
+        return Value("String", s) if s in SPECIAL_FLOATS else Value("Double", parse_double(s))
+    if column_type in _STR_KINDS:
+        return Value("String", s)
+    if column_type in ("Date",):
+        return Value("Date", s)
+    if column_type.startswith("Timestamp"):
+        return Value("Timestamp", s)
+    return parse_value(s)
+
+
+@dataclass
+class QueryResult:
+    """src/duckdb.mbt:49-54: row-major strings + null mask + column types."""
+    columns: List[str]
+    column_types: List[str]
+    rows: List[List[str]]
+    nulls: List[List[bool]]
+
+    def column_count(self) -> int:
+        return len(self.columns)
+
+    def row_count(self) -> int:
+        return len(self.rows)
+
+    def cell(self, row: int, col: int) -> Optional[str]:
+        """duckdb.mbt:214-220: None for NULL / out of range."""
+        if row < 0 or row >= len(self.rows) or col < 0 or col >= len(self.columns):
+            return None
+        if self.nulls[row][col]:
+            return None
+        return self.rows[row][col]
+
+    def get_int(self, row: int, col: int) -> Optional[int]:
+        c = self.cell(row, col)
+        return None if c is None else parse_int(c)
+
+    def to_typed(self) -> "TypedQueryResult":
+        """duckdb_typed_result.mbt:8-43 (row-major strings -> column-major Values)."""
+        cols = []
+        for c in range(len(self.columns)):
+            ct = self.column_types[c] if c < len(self.column_types) else "Invalid"
+            col = []
+            for r in range(len(self.rows)):
+                col.append(Value("Null") if self.nulls[r][c] else parse_value_with_type(self.rows[r][c], ct))
+            cols.append(col)
+        return TypedQueryResult(self.columns, self.column_types, cols, len(self.rows))
+
+
+@dataclass
+class TypedQueryResult:
+    columns: List[str]
+    column_types: List[str]
+    data: List[List[Value]]  # column-major
+    nrows: int
+
+    def get_value(self, row: int, col: int) -> Optional[Value]:
+        if col < 0 or col >= len(self.data) or row < 0 or row >= self.nrows:
+            return None
+        return self.data[col][row]
+
+    def get_int(self, row: int, col: int) -> Optional[int]:
+        v = self.get_value(row, col)
+        return v.value if v is not None and v.kind == "Int" else None
+
+    def get_int_column(self, col: int) -> Optional[List[Optional[int]]]:
+        if col < 0 or col >= len(self.data):
+            return None
+        return [v.value if v.kind == "Int" else None for v in self.data[col]]
+
+    def get_double_column(self, col: int) -> Optional[List[Optional[float]]]:
+        if col < 0 or col >= len(self.data):
+            return None
+        return [v.value if v.kind == "Double" else None for v in self.data[col]]
+
+    def get_string_column(self, col: int) -> Optional[List[Optional[str]]]:
+        if col < 0 or col >= len(self.data):
+            return None
+        return [v.value if v.kind == "String" else None for v in self.data[col]]
+
+
+@dataclass
+class DataChunk:
+    columns: List[str]
+    rows: List[List[str]]
+    nulls: List[List[bool]]
+
+    def row_count(self) -> int:
+        return len(self.rows)
+
+
+def _last_error(fallback: str) -> str:
+    msg = _str(lib.duckdb_mb_last_error())
+    return fallback if msg == "" else msg
+
+
+# --- connection ----------------------------------------------------------------
+class Connection:
+    def __init__(self, handle):
+        self._h = handle
+
+    @property
+    def handle(self):
+        return self._h
+
+    def close(self, on_done: Callable = None):
+        if self._h:
+            lib.duckdb_mb_disconnect(self._h)
+            self._h = None
+        if on_done:
+            on_done(Ok(None))
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    # Connection::query (duckdb_native.mbt:454-501): per-cell row-major pull
+    def query(self, sql: str, on_done: Callable = None):
+        a = _Arg(sql)
+        res = lib.duckdb_mb_query(self._h, a.p)
+        if lib.duckdb_mb_is_null_result(res):
+            out = Err(DuckDBError(_last_error("duckdb_query failed")))
+        else:
+            ncol = lib.duckdb_mb_result_column_count(res)
+            nrow = lib.duckdb_mb_result_row_count(res)
+            columns, types = [], []
+            for c in range(ncol):
+                columns.append(_str(lib.duckdb_mb_result_column_name(res, c)))
+                types.append(column_type_from_id(lib.duckdb_mb_result_column_type(res, c)))
+            rows, nulls = [], []
+            for r in range(nrow):
+                rv, rn = [], []
+                for c in range(ncol):
+                    isnull = bool(lib.duckdb_mb_result_is_null(res, c, r))
+                    rn.append(isnull)
+                    rv.append("" if isnull else _str(lib.duckdb_mb_result_value(res, c, r)))
+                rows.append(rv)
+                nulls.append(rn)
+            lib.duckdb_mb_result_destroy(res)
+            out = Ok(QueryResult(columns, types, rows, nulls))
+        if on_done:
+            on_done(out)
+        return out
+
+    def query_stream(self, sql: str, on_done: Callable = None):
+        a = _Arg(sql)
+        s = lib.duckdb_mb_query_stream(self._h, a.p)
+        out = Err(DuckDBError(_last_error("duckdb_stream failed"))) if lib.duckdb_mb_is_null_stream(s) \
+            else Ok(ResultStream(s))
+        if on_done:
+            on_done(out)
+        return out
+
+    def prepare(self, sql: str, on_done: Callable = None):
+        a = _Arg(sql)
+        st = lib.duckdb_mb_prepare(self._h, a.p)
+        out = Err(DuckDBError(_last_error("duckdb_prepare failed"))) if lib.duckdb_mb_is_null_statement(st) \
+            else Ok(PreparedStatement(st))
+        if on_done:
+            on_done(out)
+        return out
+
+    def create_appender(self, schema: str, table: str, on_done: Callable = None):
+        a, b = _Arg(schema), _Arg(table)
+        ap = lib.duckdb_mb_appender_create(self._h, a.p, b.p)
+        out = Err(DuckDBError("create_appender failed")) if lib.duckdb_mb_is_null_appender(ap) \
+            else Ok(Appender(ap))
+        if on_done:
+            on_done(out)
+        return out
+
+    def query_arrow(self, sql: str, on_done: Callable = None):
+        a = _Arg(sql)
+        r = lib.duckdb_mb_query_arrow(self._h, a.p)
+        out = Err(DuckDBError(_last_error("duckdb_query_arrow failed"))) if lib.duckdb_mb_is_null_arrow_result(r) \
+            else Ok(ArrowResult(r))
+        if on_done:
+            on_done(out)
+        return out
+
+    # extensions
+    def explain(self, sql: str) -> str:
+        b = sql.encode()
+        p = lib.duckdb_mbx_explain(self._h, b, len(b))
+        if not p:
+            raise DuckDBError(_last_error("explain failed"))
+        s = ctypes.string_at(p).decode()
+        lib.duckdb_mbx_free(p)
+        return s
+
+    def last_profile(self) -> dict:
+        import json
+        p = lib.duckdb_mbx_last_profile(self._h)
+        s = ctypes.string_at(p).decode()
+        lib.duckdb_mbx_free(p)
+        return json.loads(s)
+
+    def query_raw(self, sql: str):
+        """Runs a query and returns the raw handle (caller destroys); raises on error."""
+        a = _Arg(sql)
+        res = lib.duckdb_mb_query(self._h, a.p)
+        if lib.duckdb_mb_is_null_result(res):
+            raise DuckDBError(_last_error("duckdb_query failed"))
+        return RawResult(res)
+
+
+class RawResult:
+    """Direct access to a materialized result (no per-row Python lists)."""
+
+    def __init__(self, h):
+        self._h = h
+
+    def close(self):
+        if self._h:
+            lib.duckdb_mb_result_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        self.close()
+
+    def row_count(self):
+        return lib.duckdb_mb_result_row_count(self._h)
+
+    def column_count(self):
+        return lib.duckdb_mb_result_column_count(self._h)
+
+    def column_type(self, c):
+        return lib.duckdb_mb_result_column_type(self._h, c)
+
+    def is_null(self, c, r):
+        return bool(lib.duckdb_mb_result_is_null(self._h, c, r))
+
+    def value(self, c, r) -> str:
+        return _str(lib.duckdb_mb_result_value(self._h, c, r))
+
+    def raw(self, c, r) -> bytes:
+        buf = ctypes.create_string_buffer(16)
+        n = lib.duckdb_mbx_result_raw(self._h, c, r, buf, 16)
+        return buf.raw[:n]
+
+
+def connect(on_ready: Callable = None, path: str = ":memory:"):
+    """connect (duckdb_native.mbt:429-442)."""
+    a = _Arg(path)
+    h = lib.duckdb_mb_connect(a.p)
+    out = Err(DuckDBError(_last_error("duckdb_open failed"))) if lib.duckdb_mb_is_null_conn(h) else Ok(Connection(h))
+    if on_ready:
+        on_ready(out)
+    return out
+
+
+class Config:
+    """Config::create / Config::set (duckdb_native.mbt:608-627)."""
+
+    def __init__(self):
+        self._h = lib.duckdb_mb_config_create()
+
+    @staticmethod
+    def create():
+        return Config()
+
+    def set(self, key: str, value: str):
+        a, b = _Arg(key), _Arg(value)
+        if lib.duckdb_mb_config_set(self._h, a.p, b.p):
+            return Ok(None)
+        msg = _str(lib.duckdb_mb_config_error(self._h))
+        return Err(DuckDBError(msg or "config_set failed"))
+
+    def __del__(self):
+        if getattr(self, "_h", None):
+            lib.duckdb_mb_config_destroy(self._h)
+            self._h = None
+
+
+def connect_with_config(config: Config, on_ready: Callable = None, path: str = ":memory:"):
+    a = _Arg(path)
+    h = lib.duckdb_mb_connect_with_config(a.p, config._h)
+    out = Err(DuckDBError(_last_error("duckdb_open failed"))) if lib.duckdb_mb_is_null_conn(h) else Ok(Connection(h))
+    if on_ready:
+        on_ready(out)
+    return out
+
+
+class ResultStream:
+    def __init__(self, h):
+        self._h = h
+
+    def column_count(self) -> int:
+        return lib.duckdb_mb_stream_column_count(self._h)
+
+    def columns(self) -> List[str]:
+        return [_str(lib.duckdb_mb_stream_column_name(self._h, c)) for c in range(self.column_count())]
+
+    def next(self, on_done: Callable = None):
+        """ResultStream::next (duckdb_native.mbt:535-582)."""
+        ch = lib.duckdb_mb_stream_fetch_chunk(self._h)
+        if lib.duckdb_mb_is_null_chunk(ch):
+            msg = _str(lib.duckdb_mb_last_error())
+            out = Ok(None) if msg == "" else Err(DuckDBError(msg))
+        else:
+            nrow = lib.duckdb_mb_chunk_row_count(ch)
+            ncol = lib.duckdb_mb_chunk_column_count(ch)
+            if nrow <= 0 or ncol <= 0:
+                lib.duckdb_mb_chunk_destroy(ch)
+                out = Ok(None)
+            else:
+                cols = self.columns()
+                rows, nulls = [], []
+                for r in range(nrow):
+                    rv, rn = [], []
+                    for c in range(ncol):
+                        isnull = bool(lib.duckdb_mb_chunk_is_null(ch, c, r))
+                        rn.append(isnull)
+                        rv.append("" if isnull else _str(lib.duckdb_mb_chunk_value(ch, c, r)))
+                    rows.append(rv)
+                    nulls.append(rn)
+                lib.duckdb_mb_chunk_destroy(ch)
+                out = Ok(DataChunk(cols, rows, nulls))
+        if on_done:
+            on_done(out)
+        return out
+
+    def next_count(self) -> Optional[int]:
+        """Row count of the next chunk without per-cell pulls (None at end)."""
+        ch = lib.duckdb_mb_stream_fetch_chunk(self._h)
+        if lib.duckdb_mb_is_null_chunk(ch):
+            msg = _str(lib.duckdb_mb_last_error())
+            if msg:
+                raise DuckDBError(msg)
+            return None
+        n = lib.duckdb_mb_chunk_row_count(ch)
+        lib.duckdb_mb_chunk_destroy(ch)
+        return n
+
+    def close(self, on_done: Callable = None):
+        if self._h:
+            lib.duckdb_mb_stream_destroy(self._h)
+            self._h = None
+        if on_done:
+            on_done(Ok(None))
+
+
+class PreparedStatement:
+    def __init__(self, h):
+        self._h = h
+
+    def _r(self, ok, what):
+        if ok:
+            return Ok(None)
+        msg = _str(lib.duckdb_mb_statement_error(self._h))
+        return Err(DuckDBError(msg or f"{what} failed"))
+
+    def bind_int(self, i, v):
+        return self._r(lib.duckdb_mb_bind_int(self._h, i, v), "bind_int")
+
+    def bind_bigint(self, i, v):
+        return self._r(lib.duckdb_mb_bind_bigint(self._h, i, v), "bind_bigint")
+
+    def bind_double(self, i, v):
+        return self._r(lib.duckdb_mb_bind_double(self._h, i, v), "bind_double")
+
+    def bind_varchar(self, i, v):
+        a = _Arg(v)
+        return self._r(lib.duckdb_mb_bind_varchar(self._h, i, a.p), "bind_varchar")
+
+    def bind_bool(self, i, v):
+        return self._r(lib.duckdb_mb_bind_bool(self._h, i, bool(v)), "bind_bool")
+
+    def bind_null(self, i):
+        return self._r(lib.duckdb_mb_bind_null(self._h, i), "bind_null")
+
+    def bind_date(self, i, days):
+        return self._r(lib.duckdb_mb_bind_date(self._h, i, days), "bind_date")
+
+    def bind_timestamp(self, i, micros):
+        return self._r(lib.duckdb_mb_bind_timestamp(self._h, i, micros), "bind_timestamp")
+
+    def bind_decimal(self, i, width, scale, value: int):
+        lower = value & ((1 << 64) - 1)
+        upper = value >> 64
+        if lower >= 1 << 63:
+            lower -= 1 << 64
+        return self._r(lib.duckdb_mb_bind_decimal(self._h, i, width, scale, lower, upper), "bind_decimal")
+
+    def clear_bindings(self):
+        return self._r(lib.duckdb_mb_clear_bindings(self._h), "clear_bindings")
+
+    def execute(self, on_done: Callable = None):
+        res = lib.duckdb_mb_execute_prepared(self._h)
+        if lib.duckdb_mb_is_null_result(res):
+            out = Err(DuckDBError(_last_error("execute failed")))
+        else:
+            out = Ok(_materialize(res))
+        if on_done:
+            on_done(out)
+        return out
+
+    def execute_stream(self, on_done: Callable = None):
+        s = lib.duckdb_mb_execute_prepared_stream(self._h)
+        out = Err(DuckDBError(_last_error("execute_stream failed"))) if lib.duckdb_mb_is_null_stream(s) \
+            else Ok(ResultStream(s))
+        if on_done:
+            on_done(out)
+        return out
+
+    def close(self, on_done: Callable = None):
+        if self._h:
+            lib.duckdb_mb_statement_destroy(self._h)
+            self._h = None
+        if on_done:
+            on_done(Ok(None))
+
+
+def _materialize(res) -> QueryResult:
+    ncol = lib.duckdb_mb_result_column_count(res)
+    nrow = lib.duckdb_mb_result_row_count(res)
+    columns = [_str(lib.duckdb_mb_result_column_name(res, c)) for c in range(ncol)]
+    types = [column_type_from_id(lib.duckdb_mb_result_column_type(res, c)) for c in range(ncol)]
+    rows, nulls = [], []
+    for r in range(nrow):
+        rn = [bool(lib.duckdb_mb_result_is_null(res, c, r)) for c in range(ncol)]
+        rv = ["" if rn[c] else _str(lib.duckdb_mb_result_value(res, c, r)) for c in range(ncol)]
+        rows.append(rv)
+        nulls.append(rn)
+    lib.duckdb_mb_result_destroy(res)
+    return QueryResult(columns, types, rows, nulls)
+
+
+class Appender:
+    def __init__(self, h):
+        self._h = h
+
+    def _r(self, ok, what):
+        if ok:
+            return Ok(None)
+        msg = _str(lib.duckdb_mb_appender_error(self._h))
+        return Err(DuckDBError(msg or f"{what} failed"))
+
+    def begin_row(self):
+        return self._r(lib.duckdb_mb_begin_row(self._h), "begin_row")
+
+    def append_int(self, v):
+        return self._r(lib.duckdb_mb_append_int(self._h, v), "append_int")
+
+    def append_bigint(self, v):
+        return self._r(lib.duckdb_mb_append_bigint(self._h, v), "append_bigint")
+
+    def append_double(self, v):
+        return self._r(lib.duckdb_mb_append_double(self._h, v), "append_double")
+
+    def append_varchar(self, v):
+        a = _Arg(v)
+        return self._r(lib.duckdb_mb_append_varchar(self._h, a.p), "append_varchar")
+
+    def append_bool(self, v):
+        return self._r(lib.duckdb_mb_append_bool(self._h, bool(v)), "append_bool")
+
+    def append_null(self):
+        return self._r(lib.duckdb_mb_append_null(self._h), "append_null")
+
+    def append_date(self, days):
+        return self._r(lib.duckdb_mb_append_date(self._h, days), "append_date")
+
+    def append_timestamp(self, micros):
+        return self._r(lib.duckdb_mb_append_timestamp(self._h, micros), "append_timestamp")
+
+    def append_decimal(self, width, scale, value: int):
+        lower = value & ((1 << 64) - 1)
+        upper = value >> 64
+        if lower >= 1 << 63:
+            lower -= 1 << 64
+        return self._r(lib.duckdb_mb_append_decimal(self._h, width, scale, lower, upper), "append_decimal")
+
+    def end_row(self):
+        return self._r(lib.duckdb_mb_end_row(self._h), "end_row")
+
+    def flush(self):
+        return self._r(lib.duckdb_mb_flush(self._h), "flush")
+
+    def append_column(self, col: int, array, validity=None):
+        """Columnar bulk ingest (extension): `array` is a contiguous numpy array
+        in the column's physical layout."""
+        vp = validity.ctypes.data if validity is not None else None
+        return self._r(lib.duckdb_mbx_append_column(self._h, col, array.ctypes.data, vp, len(array)), "append_column")
+
+    def commit(self, count: int):
+        return self._r(lib.duckdb_mbx_append_commit(self._h, count), "append_commit")
+
+    def close(self, on_done: Callable = None):
+        if self._h:
+            lib.duckdb_mb_appender_destroy(self._h)
+            self._h = None
+        if on_done:
+            on_done(Ok(None))
+
+
+# --- Arrow-style columnar read-back (duckdb_arrow_native.mbt) ---------------------
+ARROW_MAX_ROWS = 1_000_000  # decoders return [] above this (duckdb_arrow_native.mbt:435, :474, :517, ...)
+
+
+@dataclass
+class ArrowField:
+    name: str
+    type_id: str
+    nullable: bool
+
+
+@dataclass
+class ArrowSchema:
+    fields: List[ArrowField] = field(default_factory=list)
+
+
+def _i32(b: bytes, off: int) -> int:
+    return struct.unpack_from("<i", b, off)[0]
+
+
+def _mb_int(x: int) -> int:
+    """The reference int64 decoder (duckdb_arrow_native.mbt:481-503) assembles
+    8 bytes into a 32-bit MoonBit Int with shifts of 32..56, which MoonBit
+    masks to 0..24: the result is (low word | high word) as Int.  Exact for
+    every value in [-2^31, 2^31) (the range the reference tests use)."""
+    lo = x & 0xFFFFFFFF
+    hi = (x >> 32) & 0xFFFFFFFF
+    v = lo | hi
+    return v - (1 << 32) if v >= 1 << 31 else v
+
+
+class ArrowResult:
+    def __init__(self, h):
+        self._h = h
+
+    def column_count(self):
+        return lib.duckdb_mb_arrow_column_count(self._h)
+
+    def row_count(self):
+        return lib.duckdb_mb_arrow_row_count(self._h)
+
+    def get_schema(self):
+        import json
+        txt = _str(lib.duckdb_mb_arrow_schema(self._h))
+        try:
+            arr = json.loads(txt)
+        except Exception as e:  # parse_arrow_schema_json error path
+            return Err(DuckDBError(f"schema parse failed: {e}"))
+        return Ok(ArrowSchema([ArrowField(f["name"], f["type_id"], f["nullable"]) for f in arr]))
+
+    def _buf(self, kind, col, nullable=False):
+        fn = getattr(lib, f"duckdb_mb_arrow_get_column_{kind}{'_nullable' if nullable else ''}")
+        return _take(fn(self._h, col))
+
+    def get_column_int32(self, col) -> List[int]:
+        b = self._buf("int32", col)
+        if len(b) < 4:
+            return []
+        n = _i32(b, 0)
+        if n <= 0 or n > ARROW_MAX_ROWS:
+            return []
+        return list(struct.unpack_from(f"<{n}i", b, 4))
+
+    def get_column_int64(self, col) -> List[int]:
+        """duckdb_arrow_native.mbt:465-505 assembles each value into a 32-bit
+        Int (low word); values keep their 64-bit wire form in `raw_int64`."""
+        return [_mb_int(v) for v in self.raw_int64(col)]
+
+    def raw_int64(self, col) -> List[int]:
+        b = self._buf("int64", col)
+        if len(b) < 4:
+            return []
+        n = _i32(b, 0)
+        if n <= 0 or n > ARROW_MAX_ROWS:
+            return []
+        return list(struct.unpack_from(f"<{n}q", b, 4))
+
+    def raw_int64_bytes(self, col) -> bytes:
+        """The wire buffer itself: [int32 count][count x int64 LE]."""
+        return self._buf("int64", col)
+
+    def get_column_double(self, col) -> List[float]:
+        b = self._buf("double", col)
+        if len(b) < 4:
+            return []
+        n = _i32(b, 0)
+        if n <= 0 or n > ARROW_MAX_ROWS:
+            return []
+        return list(struct.unpack_from(f"<{n}d", b, 4))
+
+    def get_column_bool(self, col) -> List[bool]:
+        b = self._buf("bool", col)
+        if len(b) < 4:
+            return []
+        n = _i32(b, 0)
+        if n <= 0 or n > ARROW_MAX_ROWS:
+            return []
+        return [x != 0 for x in b[4:4 + n]]
+
+    def get_column_string(self, col) -> List[str]:
+        b = self._buf("string", col)
+        if len(b) < 8:
+            return []
+        n, tot = _i32(b, 0), _i32(b, 4)
+        if n <= 0 or n > ARROW_MAX_ROWS:
+            return []
+        parts = b[8:8 + tot].split(b"\0")
+        return [p.decode("utf-8", errors="replace") for p in parts[:n]]
+
+    def _nullable(self, kind, col, width, fmt):
+        b = self._buf(kind, col, True)
+        if len(b) < 4:
+            return [], []
+        n = _i32(b, 0)
+        if n <= 0 or n > ARROW_MAX_ROWS:
+            return [], []
+        vals = list(struct.unpack_from(f"<{n}{fmt}", b, 4)) if fmt else list(b[4:4 + n])
+        valid = [x != 0 for x in b[4 + n * width:4 + n * width + n]]
+        return vals, valid
+
+    def get_column_int32_nullable(self, col):
+        return self._nullable("int32", col, 4, "i")
+
+    def get_column_int64_nullable(self, col):
+        v, m = self._nullable("int64", col, 8, "q")
+        return [_mb_int(x) for x in v], m
+
+    def get_column_double_nullable(self, col):
+        return self._nullable("double", col, 8, "d")
+
+    def get_column_bool_nullable(self, col):
+        v, m = self._nullable("bool", col, 1, None)
+        return [x != 0 for x in v], m
+
+    def get_column_string_nullable(self, col):
+        b = self._buf("string", col, True)
+        if len(b) < 8:
+            return [], []
+        n, tot = _i32(b, 0), _i32(b, 4)
+        if n <= 0 or n > ARROW_MAX_ROWS:
+            return [], []
+        parts = b[8:8 + tot].split(b"\0")[:n]
+        valid = [x != 0 for x in b[8 + tot:8 + tot + n]]
+        return [p.decode("utf-8", errors="replace") for p in parts], valid
+
+    def close(self, on_done: Callable = None):
+        if self._h:
+            lib.duckdb_mb_arrow_destroy(self._h)
+            self._h = None
+        if on_done:
+            on_done(Ok(None))

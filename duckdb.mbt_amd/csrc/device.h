@@ -1,0 +1,144 @@
+// device.h — host-callable launchers for the gfx950 kernels in kernels.hip.
+// Everything here is asynchronous on the given stream unless stated.
+#pragma once
+#include <hip/hip_runtime_api.h>
+#include <stdint.h>
+
+#include "vm.h"
+
+namespace mbx {
+namespace dev {
+
+struct VmCols {
+  VmCol c[VM_MAX_COLS];
+  int32_t n;
+};
+
+struct VmOuts {
+  void *data[VM_MAX_OUT];
+  uint32_t *valid[VM_MAX_OUT];  // 32-bit-word view of the LSB-first bitmap (zeroed), or null
+  int32_t *anynull;             // per output: set to 1 if a NULL was written
+};
+
+// --- expression VM --------------------------------------------------------
+// Predicate pass: one bit per row into sel_bits (4 x u64 words per 256-row
+// tile) and the selected-row count of every tile into tile_counts.
+void VmFilter(const VmProgram &p, const VmCols &cols, int64_t nrows, int64_t range_start, int64_t range_step,
+              uint64_t *sel_bits, uint32_t *tile_counts, int32_t *err, hipStream_t s);
+// Projection pass over all rows (sel_bits == null) or over the selected rows,
+// written densely at tile_offsets[tile] + rank.
+void VmProject(const VmProgram &p, const VmCols &cols, int64_t nrows, int64_t range_start, int64_t range_step,
+               const uint64_t *sel_bits, const int64_t *tile_offsets, const VmOuts &outs, int32_t *err,
+               hipStream_t s);
+// Exclusive scan of tile counts -> int64 offsets; total written to *total (device).
+void ScanTileCounts(const uint32_t *counts, int64_t *offsets, int64_t n, int64_t *total, hipStream_t s);
+
+// --- aggregate state (one per aggregate and group slot), 64 bytes -------
+struct AggState {
+  unsigned long long count;
+  unsigned long long sum_lo;
+  long long sum_hi;
+  long long min_i, max_i;
+  double sum_f;
+  unsigned long long min_f, max_f;  // order-preserving encoded doubles
+};
+
+// --- fused scan -> filter -> aggregate (no GROUP BY; configs C2, C5) -------
+// Predicate lo <= p[i] <= hi on column p (P_I32 / P_I64, no nulls) or none;
+// aggregate column a (P_I32 / P_I64; == p allowed) or none (COUNT(*) only).
+// count_star += selected rows; st accumulates count/sum/min/max of a.
+void FilterAggStates(const void *pcol, int pphys, int64_t lo, int64_t hi, bool has_pred, const void *acol, int aphys,
+                     int64_t nrows, AggState *st, unsigned long long *cstar, int grid_blocks, hipStream_t s);
+
+// --- fused GROUP BY on a small-range integer key (config C3) -------------
+// key in [kmin, kmin + nk), no nulls; up to 2 value columns of one phys.
+size_t GroupDirectLds(int nk, int R, int nv, bool mm);
+void GroupByDirectStates(const void *kcol, int kphys, int64_t kmin, int nk, const void *v0, const void *v1, int vphys,
+                         int nv, bool mm, int64_t nrows, int64_t seg_rows, int R, unsigned long long *cstar,
+                         AggState *st0, AggState *st1, int grid_blocks, hipStream_t s);
+
+// --- generic aggregation over compacted columns ---------------------------
+// vclass: VC_I64 / VC_I128 / VC_F64 of the input column (phys given)
+void ReduceColumn(const void *col, int phys, const uint64_t *valid, int64_t n, AggState *out, hipStream_t s);
+// min/max of an integer key column (for group planning); writes {min,max,nonnull count}
+void KeyRange(const void *col, int phys, const uint64_t *valid, int64_t n, long long *out3, hipStream_t s);
+// Direct-index grouping: slot = valid ? key - kmin : nslots-1 (NULL group).
+// For every aggregate column: AggState per slot; count_star per slot.
+void GroupAssign(const void *kcol, int kphys, const uint64_t *kvalid, int64_t kmin, int64_t nslots, int64_t n,
+                 int32_t *slot_of_row, unsigned long long *count_star, hipStream_t s);
+void GroupReduceColumn(const int32_t *slot_of_row, const void *col, int phys, const uint64_t *valid, int64_t n,
+                       AggState *states, hipStream_t s);
+void InitAggStates(AggState *st, int64_t n, hipStream_t s);
+// Compact non-empty slots into the aggregate relation (index list).
+void CompactSlots(const unsigned long long *count_star, int64_t nslots, int32_t *slot_list, int64_t *n_out,
+                  hipStream_t s);
+
+// --- sort / gather -------------------------------------------------------
+// Order-preserving u64 keys of a column (asc; desc flips; nulls per flag).
+void SortKeyU64(const void *col, int phys, const uint64_t *valid, int64_t n, const int64_t *perm, bool desc,
+                bool nulls_first, uint64_t *keys, hipStream_t s);
+void SortPairs(uint64_t *keys_in, int64_t *vals_in, uint64_t *keys_out, int64_t *vals_out, int64_t n,
+               hipStream_t s);
+void Iota(int64_t *p, int64_t n, int64_t start, hipStream_t s);
+// out[i] = in[idx[i]] for fixed-width phys; validity likewise (bitmap)
+void GatherFixed(const void *in, int phys, const uint64_t *in_valid, const int64_t *idx, int64_t n, void *out,
+                 uint32_t *out_valid, hipStream_t s);
+void GatherSlots(const void *in, int elem_bytes, const int32_t *idx, int64_t n, void *out, hipStream_t s);
+
+// --- strings ---------------------------------------------------------------
+// codes[i] >= 0: row of the source string column; < 0: -(k+1) into pool.
+void StringLengths(const int64_t *codes, const uint64_t *valid, int64_t n, const int64_t *src_off,
+                   const int64_t *pool_off, int64_t *lens, hipStream_t s);
+void ScanLengths(const int64_t *lens, int64_t *offsets, int64_t n, hipStream_t s);  // offsets[n+1]
+void StringCopy(const int64_t *codes, const uint64_t *valid, int64_t n, const int64_t *src_off, const char *src_chars,
+                const int64_t *pool_off, const char *pool_chars, const int64_t *out_off, char *out_chars,
+                hipStream_t s);
+
+// --- ingest / stats ----------------------------------------------------------
+// min/max/null count over rows [0, n) of a fixed-width integer-like column.
+void ColumnStats(const void *col, int phys, const uint64_t *valid, int64_t n, long long *out3, hipStream_t s);
+// Synthetic column: out[i] = splitmix64(seed + start + i) mod m + add  (int64 or int32)
+void Synth(void *out, int phys, int64_t n, int64_t seed, int64_t start, int64_t m, int64_t add, hipStream_t s);
+// Copy a bitmap range: dst bits [dst_off, dst_off+n) = src bits [0, n) (src null -> all ones)
+void BitmapAppend(uint64_t *dst, int64_t dst_off, const uint64_t *src, int64_t n, hipStream_t s);
+// HBM calibration: out = in (float4 copy), nbytes multiple of 16
+void CopyKernel(const void *in, void *out, int64_t nbytes, hipStream_t s);
+
+int NumCUs();
+
+}  // namespace dev
+}  // namespace mbx
+
+namespace mbx {
+namespace dev {
+
+// --- aggregate relation emission ---------------------------------------------
+struct EmitAgg {
+  int32_t kind;      // AggKind
+  int32_t in_class;  // VClass of the aggregated column
+  int32_t out_phys;  // Phys of the result column
+  int32_t avg_scale; // decimal scale for AVG
+  AggState *states;  // per slot (null for COUNT_STAR)
+  void *out;
+  uint32_t *valid;   // zeroed bitmap words
+};
+#define EMIT_MAX_AGGS 16
+struct EmitDesc {
+  int32_t nagg;
+  EmitAgg a[EMIT_MAX_AGGS];
+  const unsigned long long *cstar;  // per slot
+  const int32_t *slot_list;         // null: slots 0..nslots-1 all emitted
+  const int64_t *n_list;            // device count of slot_list (if slot_list)
+  int64_t nslots;
+  int32_t has_key;
+  int32_t key_phys;
+  int64_t kmin;
+  int64_t null_slot;  // -1 if none
+  void *key_out;
+  uint32_t *key_valid;
+};
+void EmitAggRelation(const EmitDesc &d, hipStream_t s);
+void RebaseOffsets(const int64_t *src, int64_t *dst, int64_t n, int64_t delta, hipStream_t s);
+
+}  // namespace dev
+}  // namespace mbx

@@ -1,0 +1,131 @@
+// engine.h — catalog, device column chunks, results and handles behind the
+// duckdb_mb_* C-ABI (the objects the reference keeps inside libduckdb).
+#pragma once
+
+#include <map>
+#include <memory>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "plan.h"
+#include "types.h"
+
+namespace mbx {
+
+// One column of a device-resident table: Arrow-layout values buffer (256-B
+// aligned, allocated with hipMalloc) and an LSB-first validity bitmap in
+// 64-bit words (bit = 1 -> valid; same bit order as DuckDB's
+// duckdb_validity_row_is_valid, reference duckdb_native.c:530-534).  A null
+// validity pointer means "all rows valid".  Strings keep int64 offsets[n+1]
+// plus a chars buffer.
+struct DevColumn {
+  LogicalType type;
+  Phys phys = P_I64;
+  void *data = nullptr;
+  uint64_t *validity = nullptr;
+  int64_t *offsets = nullptr;  // P_STR
+  char *chars = nullptr;       // P_STR
+  int64_t chars_len = 0, chars_cap = 0;
+  int64_t capacity = 0;  // rows
+  // zone-map statistics over all rows (kept by ingest; used by the planner
+  // to pick overflow-free accumulators and direct-index group tables)
+  bool stats_valid = false;
+  i128 imin = 0, imax = 0;
+  int64_t null_count = 0;
+};
+
+struct Table {
+  std::string name;
+  std::vector<std::string> col_names;
+  std::vector<DevColumn> cols;
+  int64_t nrows = 0;
+  int device = 0;
+  ~Table();
+};
+typedef std::shared_ptr<Table> TablePtr;
+
+struct Catalog {
+  std::map<std::string, TablePtr> tables;  // lower-cased name
+  int device = 0;
+  TablePtr Find(const std::string &name) const;
+};
+
+// Host copy of a result column (after the single D2H of a query).
+struct HostColumn {
+  std::string name;
+  LogicalType type;
+  Phys phys = P_I64;
+  std::vector<uint8_t> data;         // fixed-width values
+  std::vector<uint8_t> valid;        // 1 byte per row (1 = valid)
+  std::vector<int64_t> offsets;      // P_STR
+  std::string chars;                 // P_STR
+  Value Get(int64_t row) const;
+  bool IsNull(int64_t row) const { return !valid.empty() && !valid[row]; }
+};
+
+struct MaterializedResult {
+  std::vector<HostColumn> cols;
+  int64_t nrows = 0;
+  std::vector<std::string> formatted;  // optional cache
+};
+typedef std::shared_ptr<MaterializedResult> ResultPtr;
+
+struct QueryProfile {
+  struct Kernel {
+    std::string name;
+    double ms = 0;
+    double bytes = 0;  // algorithmic bytes moved
+    int64_t rows = 0;
+  };
+  std::vector<Kernel> kernels;
+  double total_ms = 0;
+  std::string plan;
+};
+
+struct Database;
+
+// Options a connection was opened with (Config::set keys, reference
+// duckdb_native.c:714-747 passes them to duckdb_set_config).
+struct Options {
+  int device = -1;            // "gpu_device" (default: current HIP device)
+  bool profile = false;       // "mbx_profile"
+  int threads = 0;            // "threads" (accepted; CPU-side only)
+  bool allow_no_gpu = false;  // "mbx_allow_no_gpu": host-constant queries only (tests)
+  int64_t appender_flush_rows = 1 << 20;  // "mbx_appender_flush_rows"
+  std::map<std::string, std::string> raw;
+};
+
+struct Engine;  // per-connection executor state (device stream, scratch)
+
+struct Connection {
+  Options opts;
+  Catalog catalog;
+  std::shared_ptr<Engine> engine;
+  QueryProfile last_profile;
+  ~Connection();
+};
+
+// Runs one statement; returns a materialized result (empty for DDL).
+ResultPtr RunStatement(Connection &c, const std::string &sql, const std::vector<Value> &params, int *n_params_out);
+ResultPtr RunParsed(Connection &c, const Statement &st, const std::vector<Value> &params);
+std::string Explain(Connection &c, const std::string &sql);
+
+// Executor entry points (executor.cpp).
+std::shared_ptr<Engine> CreateEngine(int device, bool allow_no_gpu);
+ResultPtr ExecuteSelect(Connection &c, const BoundSelect &s);
+void ExecuteInsertSelect(Connection &c, Table &t, const BoundSelect &s, const std::vector<int> &col_map);
+TablePtr CreateDeviceTable(Connection &c, const std::string &name, const std::vector<std::string> &names,
+                           const std::vector<LogicalType> &types);
+void DropDeviceTable(Table &t);
+int DeviceCount();
+
+// Host staging -> device append (appender, INSERT VALUES).
+struct HostBatch {
+  std::vector<HostColumn> cols;
+  int64_t nrows = 0;
+};
+void AppendHostBatch(Connection &c, Table &t, const HostBatch &b);
+void HostColumnPush(HostColumn &col, const Value &v);  // v already of col.type (or NULL)
+
+}  // namespace mbx

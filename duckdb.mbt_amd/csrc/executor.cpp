@@ -1,0 +1,1729 @@
+// executor.cpp — runs bound plans on the MI355X.
+//
+// Replaces the work libduckdb does inside duckdb_query for the recognised
+// shapes (reference call sites /root/reference/src/duckdb_native.c:159, :2246,
+// :1003, :381): scan -> filter -> project -> aggregate -> sort over
+// device-resident column chunks.  Every pass over table rows is a kernel in
+// kernels.hip; the host only plans, allocates and copies the (small) final
+// result back.  There is no CPU execution path: without a device, any plan
+// that touches rows raises.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <chrono>
+#include <cmath>
+#include <cstring>
+#include <functional>
+#include <sstream>
+
+#include "device.h"
+#include "engine.h"
+#include "vm.h"
+
+namespace mbx {
+
+#define HIPCHK(x)                                                                            \
+  do {                                                                                       \
+    hipError_t e_ = (x);                                                                     \
+    if (e_ != hipSuccess) ThrowError("IO", std::string("HIP error: ") + hipGetErrorString(e_) + " at " #x); \
+  } while (0)
+
+// ---------------------------------------------------------------------------
+// engine state
+// ---------------------------------------------------------------------------
+struct ProfEvent {
+  std::string name;
+  hipEvent_t a, b;
+  double bytes;
+  int64_t rows;
+};
+
+struct Engine {
+  int device = 0;
+  bool has_gpu = false;
+  hipStream_t stream = nullptr;
+  int32_t *d_err = nullptr;
+  int64_t *d_scratch = nullptr;  // small device scratch (counts)
+  void *d_small = nullptr;       // 4 KB scratch for small states
+  bool profile = false;
+  std::vector<ProfEvent> events;
+  std::string plan_text;
+  ~Engine() {
+    if (has_gpu) {
+      hipSetDevice(device);
+      if (stream) hipStreamSynchronize(stream);
+      for (auto &e : events) {
+        hipEventDestroy(e.a);
+        hipEventDestroy(e.b);
+      }
+      if (d_err) hipFree(d_err);
+      if (d_scratch) hipFree(d_scratch);
+      if (d_small) hipFree(d_small);
+      if (stream) hipStreamDestroy(stream);
+    }
+  }
+};
+
+int DeviceCount() {
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess) return 0;
+  return n;
+}
+
+std::shared_ptr<Engine> CreateEngine(int device, bool allow_no_gpu) {
+  auto e = std::make_shared<Engine>();
+  int n = DeviceCount();
+  if (n <= 0) {
+    if (!allow_no_gpu)
+      ThrowError("IO", "no AMD GPU visible: the MI355X backend requires a gfx950 device (HIP reports 0 devices)");
+    e->has_gpu = false;
+    return e;
+  }
+  if (device < 0) HIPCHK(hipGetDevice(&device));
+  if (device >= n) ThrowError("IO", "gpu_device " + std::to_string(device) + " out of range (" + std::to_string(n) + " devices)");
+  e->device = device;
+  HIPCHK(hipSetDevice(device));
+  HIPCHK(hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking));
+  HIPCHK(hipMalloc(&e->d_err, 256));
+  HIPCHK(hipMalloc(&e->d_scratch, 4096));
+  HIPCHK(hipMalloc(&e->d_small, 1 << 16));
+  e->has_gpu = true;
+  return e;
+}
+
+static Engine &Eng(Connection &c) {
+  Engine &e = *c.engine;
+  if (!e.has_gpu)
+    ThrowError("IO", "this statement reads table rows and needs the MI355X device, but no GPU is available");
+  hipSetDevice(e.device);
+  return e;
+}
+
+struct ProfScope {
+  Engine &e;
+  bool on;
+  size_t idx;
+  ProfScope(Engine &en, const char *name, double bytes, int64_t rows) : e(en), on(en.profile) {
+    if (!on) return;
+    ProfEvent pe;
+    pe.name = name;
+    pe.bytes = bytes;
+    pe.rows = rows;
+    hipEventCreate(&pe.a);
+    hipEventCreate(&pe.b);
+    hipEventRecord(pe.a, e.stream);
+    e.events.push_back(pe);
+    idx = e.events.size() - 1;
+  }
+  ~ProfScope() {
+    if (on) hipEventRecord(e.events[idx].b, e.stream);
+  }
+};
+
+// ---------------------------------------------------------------------------
+// device buffers and relations
+// ---------------------------------------------------------------------------
+struct DevBuf {
+  void *p = nullptr;
+  hipStream_t s = nullptr;
+  ~DevBuf() {
+    if (p) (void)hipFreeAsync(p, s);
+  }
+};
+typedef std::shared_ptr<DevBuf> DevBufPtr;
+
+static DevBufPtr Alloc(Engine &e, size_t bytes, bool zero = false) {
+  auto b = std::make_shared<DevBuf>();
+  b->s = e.stream;
+  if (bytes == 0) bytes = 16;
+  bytes = (bytes + 255) & ~(size_t)255;
+  HIPCHK(hipMallocAsync(&b->p, bytes, e.stream));
+  if (zero) HIPCHK(hipMemsetAsync(b->p, 0, bytes, e.stream));
+  return b;
+}
+
+struct DCol {
+  LogicalType type;
+  Phys phys = P_I64;
+  void *data = nullptr;
+  uint64_t *validity = nullptr;
+  int64_t *offsets = nullptr;  // strings
+  char *chars = nullptr;
+  int64_t chars_len = 0;
+  std::vector<DevBufPtr> owners;
+  // statistics when the column is a table column
+  const DevColumn *table_col = nullptr;
+};
+
+struct DRel {
+  std::vector<DCol> cols;
+  int64_t n = 0;
+  bool range = false;  // column 0 is the virtual range column
+  int64_t rs = 0, rstep = 1;
+};
+
+static DCol ColFromTable(const DevColumn &c) {
+  DCol d;
+  d.type = c.type;
+  d.phys = c.phys;
+  d.data = c.data;
+  d.validity = c.validity;
+  d.offsets = c.offsets;
+  d.chars = c.chars;
+  d.chars_len = c.chars_len;
+  d.table_col = &c;
+  return d;
+}
+
+static int64_t Words64(int64_t n) { return (n + 63) / 64; }
+
+static void CheckError(Engine &e) {
+  int32_t err = 0;
+  HIPCHK(hipMemcpyAsync(&err, e.d_err, sizeof(int32_t), hipMemcpyDeviceToHost, e.stream));
+  HIPCHK(hipStreamSynchronize(e.stream));
+  if (err) {
+    HIPCHK(hipMemsetAsync(e.d_err, 0, sizeof(int32_t), e.stream));
+    switch (err) {
+      case E_OVF_ADD: ThrowError("Out of Range", "Overflow in addition!");
+      case E_OVF_SUB: ThrowError("Out of Range", "Overflow in subtraction!");
+      case E_OVF_MUL: ThrowError("Out of Range", "Overflow in multiplication!");
+      case E_OVF_NEG: ThrowError("Out of Range", "Overflow in negation!");
+      case E_CAST_RANGE: ThrowError("Conversion", "Value out of range for the destination type in CAST");
+      default: ThrowError("Out of Range", "Decimal value out of range");
+    }
+  }
+}
+
+template <typename T>
+static T ReadDev(Engine &e, const void *p) {
+  T v;
+  HIPCHK(hipMemcpyAsync(&v, p, sizeof(T), hipMemcpyDeviceToHost, e.stream));
+  HIPCHK(hipStreamSynchronize(e.stream));
+  return v;
+}
+
+// ---------------------------------------------------------------------------
+// host -> device upload of constant rows (VALUES, host-constant subqueries)
+// ---------------------------------------------------------------------------
+static void UploadHostColumn(Engine &e, const HostColumn &hc, int64_t n, DCol &d) {
+  d.type = hc.type;
+  d.phys = hc.phys;
+  if (hc.phys == P_STR) {
+    auto ob = Alloc(e, (n + 1) * sizeof(int64_t));
+    auto cb = Alloc(e, std::max<size_t>(hc.chars.size(), 1));
+    HIPCHK(hipMemcpyAsync(ob->p, hc.offsets.data(), (n + 1) * sizeof(int64_t), hipMemcpyHostToDevice, e.stream));
+    if (!hc.chars.empty())
+      HIPCHK(hipMemcpyAsync(cb->p, hc.chars.data(), hc.chars.size(), hipMemcpyHostToDevice, e.stream));
+    d.offsets = (int64_t *)ob->p;
+    d.chars = (char *)cb->p;
+    d.chars_len = (int64_t)hc.chars.size();
+    d.owners.push_back(ob);
+    d.owners.push_back(cb);
+  } else {
+    size_t bytes = (size_t)n * PhysSize(hc.phys);
+    auto db = Alloc(e, bytes);
+    if (bytes) HIPCHK(hipMemcpyAsync(db->p, hc.data.data(), bytes, hipMemcpyHostToDevice, e.stream));
+    d.data = db->p;
+    d.owners.push_back(db);
+  }
+  bool anynull = false;
+  for (int64_t i = 0; i < n; i++)
+    if (hc.IsNull(i)) anynull = true;
+  if (anynull) {
+    std::vector<uint64_t> bm(Words64(n), 0);
+    for (int64_t i = 0; i < n; i++)
+      if (!hc.IsNull(i)) bm[i >> 6] |= 1ull << (i & 63);
+    auto vb = Alloc(e, bm.size() * 8);
+    HIPCHK(hipMemcpyAsync(vb->p, bm.data(), bm.size() * 8, hipMemcpyHostToDevice, e.stream));
+    d.validity = (uint64_t *)vb->p;
+    d.owners.push_back(vb);
+  }
+  // keep host staging alive until the copies are done
+  HIPCHK(hipStreamSynchronize(e.stream));
+}
+
+static DRel UploadRows(Engine &e, const std::vector<std::vector<Value>> &rows, const std::vector<LogicalType> &types) {
+  DRel r;
+  r.n = (int64_t)rows.size();
+  for (size_t c = 0; c < types.size(); c++) {
+    HostColumn hc;
+    hc.type = types[c];
+    hc.phys = PhysOf(types[c]);
+    if (hc.phys == P_STR) hc.offsets.push_back(0);
+    for (auto &row : rows) HostColumnPush(hc, CastValue(row[c], types[c]));
+    DCol d;
+    UploadHostColumn(e, hc, r.n, d);
+    r.cols.push_back(d);
+  }
+  return r;
+}
+
+// ---------------------------------------------------------------------------
+// VM compiler: bound expressions -> tile program
+// ---------------------------------------------------------------------------
+struct StrPool {
+  std::vector<std::string> s;
+  int Add(const std::string &x) {
+    for (size_t i = 0; i < s.size(); i++)
+      if (s[i] == x) return (int)i;
+    s.push_back(x);
+    return (int)s.size() - 1;
+  }
+};
+
+struct VmCompiler {
+  VmProgram P;
+  const DRel &rel;
+  std::vector<int> colmap;  // rel col -> VmCols index
+  dev::VmCols cols;
+  bool used[VM_MAX_REGS] = {};
+  int high = 0;
+  StrPool *pool;
+  int str_src_col = -1;  // the one source string column referenced by string outputs
+
+  VmCompiler(const DRel &r, StrPool *p) : rel(r), pool(p) {
+    memset(&P, 0, sizeof(P));
+    memset(&cols, 0, sizeof(cols));
+    colmap.assign(r.cols.size(), -1);
+  }
+  int Reg() {
+    for (int i = 0; i < VM_MAX_REGS; i++)
+      if (!used[i]) {
+        used[i] = true;
+        high = std::max(high, i + 1);
+        return i;
+      }
+    ThrowError("Not implemented", "expression too complex for the device VM (registers)");
+  }
+  void Free(int r) {
+    if (r >= 0 && r < VM_MAX_REGS) used[r] = false;
+  }
+  void Emit(uint8_t op, int d, int a = 0, int b = 0, int c = 0, int aux = 0) {
+    if (P.n_ins >= VM_MAX_INS) ThrowError("Not implemented", "expression too complex for the device VM (instructions)");
+    VmIns &I = P.ins[P.n_ins++];
+    I.op = op;
+    I.dst = (uint8_t)d;
+    I.a = (uint8_t)a;
+    I.b = (uint8_t)b;
+    I.c = (uint8_t)c;
+    I.aux = (uint16_t)aux;
+  }
+  // unary step consuming register a
+  int Step1(uint8_t op, int a, int b = 0, int c = 0, int aux = 0) {
+    int d = Reg();
+    Emit(op, d, a, b, c, aux);
+    Free(a);
+    return d;
+  }
+  // binary step consuming registers a, b
+  int Step2(uint8_t op, int a, int b, int aux = 0) {
+    int d = Reg();
+    Emit(op, d, a, b, 0, aux);
+    Free(a);
+    Free(b);
+    return d;
+  }
+  int Const(i128 v, bool isnull = false) {
+    int64_t lo = (int64_t)(uint64_t)(u128)v, hi = (int64_t)(uint64_t)((u128)v >> 64);
+    for (int i = 0; i < P.n_const; i++)
+      if (P.consts[i].lo == lo && P.consts[i].hi == hi && P.consts[i].isnull == (int)isnull) return i;
+    if (P.n_const >= VM_MAX_CONST) ThrowError("Not implemented", "too many constants for the device VM");
+    P.consts[P.n_const].lo = lo;
+    P.consts[P.n_const].hi = hi;
+    P.consts[P.n_const].isnull = isnull;
+    return P.n_const++;
+  }
+  int ConstF(double d) {
+    int64_t bits;
+    memcpy(&bits, &d, 8);
+    return Const((i128)bits);
+  }
+  int LoadConst(int k) {
+    int d = Reg();
+    Emit(V_CONST, d, k);
+    return d;
+  }
+  int ColIdx(int c) {
+    if (colmap[c] < 0) {
+      if (cols.n >= VM_MAX_COLS) ThrowError("Not implemented", "too many columns in one device expression program");
+      const DCol &d = rel.cols[c];
+      cols.c[cols.n].data = d.phys == P_STR ? nullptr : d.data;
+      cols.c[cols.n].validity = d.validity;
+      cols.c[cols.n].phys = d.phys;
+      colmap[c] = cols.n++;
+    }
+    return colmap[c];
+  }
+
+  // register class conversion without value checks
+  int ToClass(int r, VClass from, VClass to) {
+    if (from == to) return r;
+    if (from == VC_I64 && to == VC_I128) return Step1(V_I2L, r);
+    if (from == VC_I128 && to == VC_I64) return Step1(V_L2I, r, 255, 255);
+    if (from == VC_I64 && to == VC_F64) return Step1(V_I2F, r);
+    if (from == VC_I128 && to == VC_F64) return Step1(V_L2F, r);
+    ThrowError("Not implemented", "unsupported register class conversion on device");
+  }
+
+  int RangeCheck(int r, VClass vc, i128 lo, i128 hi) {
+    return Step1(vc == VC_I128 ? V_CHECK_L : V_CHECK_I, r, Const(lo), Const(hi));
+  }
+
+  int ToFloat32(int r) {
+    int z = LoadConst(ConstF(0.0));
+    return Step2(V_ADD_F, r, z, 1);
+  }
+
+  int CompileCast(const BExpr &e) {
+    const LogicalType &from = e.ch[0]->type, &to = e.type;
+    VClass fc = ClassOf(from), tc = ClassOf(to);
+    if (fc == VC_STR || tc == VC_STR) {
+      if (fc == VC_STR && tc == VC_STR) return Compile(*e.ch[0]);
+      ThrowError("Not implemented", "casts between VARCHAR and " + (fc == VC_STR ? to : from).ToString() +
+                                         " are not supported on the MI355X device path");
+    }
+    if (from.id == T_DATE || from.id == T_TIMESTAMP || from.id == T_TIME || to.id == T_DATE || to.id == T_TIMESTAMP ||
+        to.id == T_TIME || from.id == T_INTERVAL || to.id == T_INTERVAL) {
+      if (from.id == T_DATE && to.id == T_TIMESTAMP) {
+        int r = Compile(*e.ch[0]);
+        int k = LoadConst(Const(86400000000LL));
+        return Step2(V_MUL_I, r, k);
+      }
+      ThrowError("Not implemented", "cast " + from.ToString() + " -> " + to.ToString() + " is not supported on device");
+    }
+    int r = Compile(*e.ch[0]);
+    bool fint = IsIntegral(from.id) || from.id == T_BOOLEAN, tint = IsIntegral(to.id);
+    bool fdec = from.id == T_DECIMAL, tdec = to.id == T_DECIMAL;
+    bool ff = from.id == T_FLOAT || from.id == T_DOUBLE, tf = to.id == T_FLOAT || to.id == T_DOUBLE;
+    if (to.id == T_BOOLEAN) return Step1(ff ? V_TOBOOL_F : V_TOBOOL_I, r);
+    if (fint && tint) {
+      i128 lo, hi, flo, fhi;
+      IntegralRange(to.id, &lo, &hi);
+      IntegralRange(from.id, &flo, &fhi);
+      if (flo >= lo && fhi <= hi) {
+        if (from.id == T_UBIGINT) return r;  // already 128-bit class
+        return ToClass(r, fc, tc);
+      }
+      if (fc == VC_I128 && tc == VC_I64) return Step1(V_L2I, r, Const(lo), Const(hi));
+      int x = ToClass(r, fc, tc);
+      return RangeCheck(x, tc, lo, hi);
+    }
+    if ((fint || fdec) && tdec) {
+      int fs = fdec ? from.scale : 0;
+      int x = ToClass(r, fc, tc);
+      int ds = to.scale - fs;
+      if (ds > 0) x = Step1(tc == VC_I128 ? V_SCALEUP_L : V_SCALEUP_I, x, 0, 0, ds);
+      else if (ds < 0) x = Step1(tc == VC_I128 ? V_SCALEDN_L : V_SCALEDN_I, x, 0, 0, -ds);
+      i128 lim = Pow10(to.width) - 1;
+      return RangeCheck(x, tc, -lim, lim);
+    }
+    if (fdec && tint) {
+      int x = r;
+      if (from.scale) x = Step1(fc == VC_I128 ? V_SCALEDN_L : V_SCALEDN_I, x, 0, 0, from.scale);
+      i128 lo, hi;
+      IntegralRange(to.id, &lo, &hi);
+      if (fc == VC_I128 && tc == VC_I64) return Step1(V_L2I, x, Const(lo), Const(hi));
+      x = ToClass(x, fc, tc);
+      return RangeCheck(x, tc, lo, hi);
+    }
+    if ((fint || fdec) && tf) {
+      int d;
+      if (fdec) d = Step1(fc == VC_I128 ? V_DEC2F_L : V_DEC2F_I, r, 0, 0, from.scale);
+      else d = Step1(fc == VC_I128 ? V_L2F : V_I2F, r);
+      return to.id == T_FLOAT ? ToFloat32(d) : d;
+    }
+    if (ff && tf) return to.id == T_FLOAT ? ToFloat32(r) : r;
+    if (ff && tint) {
+      i128 lo, hi;
+      IntegralRange(to.id, &lo, &hi);
+      return Step1(tc == VC_I128 ? V_F2L : V_F2I, r, Const(lo), Const(hi));
+    }
+    if (ff && tdec) {
+      i128 lim = Pow10(to.width) - 1;
+      return Step1(tc == VC_I128 ? V_F2DEC_L : V_F2DEC_I, r, Const(-lim), Const(lim), to.scale);
+    }
+    ThrowError("Not implemented", "cast " + from.ToString() + " -> " + to.ToString() + " is not supported on device");
+  }
+
+  int Compile(const BExpr &e) {
+    switch (e.kind) {
+      case BExpr::CONST: {
+        const Value &v = e.cval;
+        VClass vc = ClassOf(e.type);
+        if (v.is_null) return LoadConst(Const(0, true));
+        if (vc == VC_F64) return LoadConst(ConstF(v.d));
+        if (vc == VC_STR) {
+          if (!pool) ThrowError("Not implemented", "string constants are not supported in this device context");
+          return LoadConst(Const(-(i128)(pool->Add(v.s) + 1)));
+        }
+        if (e.type.id == T_INTERVAL) ThrowError("Not implemented", "INTERVAL values are not supported on device");
+        return LoadConst(Const(v.i));
+      }
+      case BExpr::COL: {
+        int d = Reg();
+        if (rel.range && e.col == 0) {
+          Emit(V_LOADRANGE, d);
+          return d;
+        }
+        const DCol &c = rel.cols[e.col];
+        if (c.phys == P_STR) {
+          if (str_src_col >= 0 && str_src_col != e.col)
+            ThrowError("Not implemented", "an expression mixing two VARCHAR columns is not supported on device");
+          str_src_col = e.col;
+        }
+        if (c.phys == P_INTERVAL) ThrowError("Not implemented", "INTERVAL columns are not supported on device");
+        Emit(V_LOADCOL, d, ColIdx(e.col), 0, 0, c.phys);
+        return d;
+      }
+      default:
+        break;
+    }
+    const LogicalType &t = e.type;
+    VClass vc = ClassOf(t);
+    switch (e.op) {
+      case B_CAST: return CompileCast(e);
+      case B_CASE: {
+        size_t n = e.ch.size();
+        int acc = (n % 2 == 1) ? Compile(*e.ch[n - 1]) : LoadConst(Const(0, true));
+        for (int i = (int)(n / 2) - 1; i >= 0; i--) {
+          int c = Compile(*e.ch[2 * i]);
+          int v = Compile(*e.ch[2 * i + 1]);
+          int d = Reg();
+          Emit(V_SELECT, d, c, v, acc);
+          Free(c);
+          Free(v);
+          Free(acc);
+          acc = d;
+        }
+        return acc;
+      }
+      case B_COALESCE: {
+        int acc = Compile(*e.ch.back());
+        for (int i = (int)e.ch.size() - 2; i >= 0; i--) {
+          int a = Compile(*e.ch[i]);
+          acc = Step2(V_COALESCE, a, acc);
+        }
+        return acc;
+      }
+      case B_AND: case B_OR: {
+        int a = Compile(*e.ch[0]), b = Compile(*e.ch[1]);
+        return Step2(e.op == B_AND ? V_AND : V_OR, a, b);
+      }
+      case B_NOT: return Step1(V_NOT, Compile(*e.ch[0]));
+      case B_ISNULL: return Step1(V_ISNULL, Compile(*e.ch[0]));
+      case B_ISNOTNULL: return Step1(V_ISNOTNULL, Compile(*e.ch[0]));
+      case B_SYNTH: {
+        int a = Compile(*e.ch[0]), b = Compile(*e.ch[1]), c = Compile(*e.ch[2]);
+        int d = Reg();
+        Emit(V_SYNTH, d, a, b, c);
+        Free(a);
+        Free(b);
+        Free(c);
+        return d;
+      }
+      case B_EQ: case B_NE: case B_LT: case B_LE: case B_GT: case B_GE:
+      case B_DISTINCT: case B_NOT_DISTINCT: {
+        VClass cc = ClassOf(e.ch[0]->type);
+        if (cc == VC_STR) ThrowError("Not implemented", "VARCHAR comparisons are not supported on the MI355X device path");
+        if (e.ch[0]->type.id == T_INTERVAL) ThrowError("Not implemented", "INTERVAL comparisons are not supported on device");
+        int a = Compile(*e.ch[0]), b = Compile(*e.ch[1]);
+        if (e.op == B_DISTINCT || e.op == B_NOT_DISTINCT)
+          return Step2(cc == VC_F64 ? V_DISTINCT_F : cc == VC_I128 ? V_DISTINCT_L : V_DISTINCT_I, a, b,
+                       e.op == B_NOT_DISTINCT ? 1 : 0);
+        int k = e.op == B_EQ ? 0 : e.op == B_NE ? 1 : e.op == B_LT ? 2 : e.op == B_LE ? 3 : e.op == B_GT ? 4 : 5;
+        return Step2(cc == VC_F64 ? V_CMP_F : cc == VC_I128 ? V_CMP_L : V_CMP_I, a, b, k);
+      }
+      case B_NEG: case B_ABS: {
+        int a = Compile(*e.ch[0]);
+        uint8_t op = e.op == B_NEG ? (vc == VC_F64 ? V_NEG_F : vc == VC_I128 ? V_NEG_L : V_NEG_I)
+                                   : (vc == VC_F64 ? V_ABS_F : vc == VC_I128 ? V_ABS_L : V_ABS_I);
+        int d = Step1(op, a);
+        if (vc == VC_I64 && IsIntegral(t.id) && t.id != T_BIGINT) {
+          i128 lo, hi;
+          IntegralRange(t.id, &lo, &hi);
+          return RangeCheck(d, vc, lo, hi);
+        }
+        return d;
+      }
+      case B_ADD: case B_SUB: case B_MUL: case B_DIV: case B_IDIV: case B_MOD: {
+        if (t.id == T_DATE || t.id == T_TIMESTAMP || t.id == T_INTERVAL)
+          ThrowError("Not implemented", "date/interval arithmetic is not supported on the MI355X device path");
+        if (vc == VC_STR) ThrowError("Not implemented", "string arithmetic is not supported on device");
+        int a = Compile(*e.ch[0]);
+        a = ToClass(a, ClassOf(e.ch[0]->type), vc);
+        int b = Compile(*e.ch[1]);
+        b = ToClass(b, ClassOf(e.ch[1]->type), vc);
+        uint8_t op;
+        if (vc == VC_F64) {
+          op = e.op == B_ADD ? V_ADD_F : e.op == B_SUB ? V_SUB_F : e.op == B_MUL ? V_MUL_F : e.op == B_DIV ? V_DIV_F
+               : e.op == B_MOD ? V_MOD_F : V_IDIV_F;
+          return Step2(op, a, b, t.id == T_FLOAT ? 1 : 0);
+        }
+        if (vc == VC_I128) op = e.op == B_ADD ? V_ADD_L : e.op == B_SUB ? V_SUB_L : e.op == B_MUL ? V_MUL_L
+                                : e.op == B_MOD ? V_MOD_L : V_DIV_L;
+        else op = e.op == B_ADD ? V_ADD_I : e.op == B_SUB ? V_SUB_I : e.op == B_MUL ? V_MUL_I
+                  : e.op == B_MOD ? V_MOD_I : V_DIV_I;
+        int d = Step2(op, a, b);
+        if (vc == VC_I64 && IsIntegral(t.id) && t.id != T_BIGINT) {
+          i128 lo, hi;
+          IntegralRange(t.id, &lo, &hi);
+          return RangeCheck(d, vc, lo, hi);
+        }
+        return d;
+      }
+      default:
+        ThrowError("Not implemented", "function " + ExprToString(e) + " is not supported on the MI355X device path");
+    }
+  }
+};
+
+// Does the expression (transitively) only reference columns, and which?
+static void CollectCols(const BExpr &e, std::vector<int> &out) {
+  if (e.kind == BExpr::COL) out.push_back(e.col);
+  for (auto &c : e.ch) CollectCols(*c, out);
+}
+
+// ---------------------------------------------------------------------------
+// filter + project
+// ---------------------------------------------------------------------------
+struct StrOut {
+  int out_idx;
+  int src_col;  // -1: pool only
+};
+
+static DCol AllocOut(Engine &e, const LogicalType &t, int64_t n, bool with_valid) {
+  DCol d;
+  d.type = t;
+  d.phys = PhysOf(t);
+  int sz = d.phys == P_STR ? 8 : PhysSize(d.phys);
+  auto b = Alloc(e, (size_t)std::max<int64_t>(n, 1) * sz);
+  d.data = b->p;
+  d.owners.push_back(b);
+  if (with_valid) {
+    auto v = Alloc(e, Words64(std::max<int64_t>(n, 1)) * 8, true);
+    d.validity = (uint64_t *)v->p;
+    d.owners.push_back(v);
+  }
+  return d;
+}
+
+static void MaterializeStrings(Engine &e, DCol &out, const DCol *src, const StrPool &pool, int64_t n) {
+  // out.data holds int64 codes; build offsets + chars
+  std::vector<int64_t> poff(1, 0);
+  std::string pchars;
+  for (auto &s : pool.s) {
+    pchars += s;
+    poff.push_back((int64_t)pchars.size());
+  }
+  auto pob = Alloc(e, poff.size() * 8);
+  auto pcb = Alloc(e, std::max<size_t>(pchars.size(), 1));
+  HIPCHK(hipMemcpyAsync(pob->p, poff.data(), poff.size() * 8, hipMemcpyHostToDevice, e.stream));
+  if (!pchars.empty()) HIPCHK(hipMemcpyAsync(pcb->p, pchars.data(), pchars.size(), hipMemcpyHostToDevice, e.stream));
+  auto lens = Alloc(e, std::max<int64_t>(n, 1) * 8);
+  auto offs = Alloc(e, (n + 1) * 8);
+  const int64_t *soff = src ? src->offsets : nullptr;
+  const char *schars = src ? src->chars : nullptr;
+  dev::StringLengths((const int64_t *)out.data, out.validity, n, soff, (const int64_t *)pob->p, (int64_t *)lens->p,
+                     e.stream);
+  dev::ScanLengths((const int64_t *)lens->p, (int64_t *)offs->p, n, e.stream);
+  int64_t total = ReadDev<int64_t>(e, (int64_t *)offs->p + n);
+  auto chars = Alloc(e, std::max<int64_t>(total, 1));
+  dev::StringCopy((const int64_t *)out.data, out.validity, n, soff, schars, (const int64_t *)pob->p,
+                  (const char *)pcb->p, (const int64_t *)offs->p, (char *)chars->p, e.stream);
+  HIPCHK(hipStreamSynchronize(e.stream));  // pool staging buffers go out of scope
+  out.offsets = (int64_t *)offs->p;
+  out.chars = (char *)chars->p;
+  out.chars_len = total;
+  out.owners.push_back(offs);
+  out.owners.push_back(chars);
+  out.data = nullptr;
+}
+
+// Evaluates `pred` (may be null) and `exprs` over `rel`; returns the
+// projected relation of the selected rows.
+static DRel FilterProject(Engine &e, const DRel &rel, const BExprPtr &pred, const std::vector<BExprPtr> &exprs) {
+  const int64_t n = rel.n;
+  // pure column passthrough, no predicate, no virtual range column
+  bool passthrough = !pred;
+  for (auto &x : exprs)
+    if (x->kind != BExpr::COL || (rel.range && x->col == 0)) passthrough = false;
+  if (passthrough) {
+    DRel out;
+    out.n = n;
+    for (auto &x : exprs) out.cols.push_back(rel.cols[x->col]);
+    return out;
+  }
+  const int64_t ntiles = (n + VM_TILE - 1) / VM_TILE;
+  DevBufPtr bits, offs;
+  int64_t nsel = n;
+  if (pred) {
+    if (pred->kind == BExpr::CONST) {
+      bool keep = !pred->cval.is_null && pred->cval.i;
+      if (!keep) nsel = 0;
+    } else {
+      StrPool dummy;
+      VmCompiler vc(rel, nullptr);
+      int r = vc.Compile(*pred);
+      vc.P.pred_reg = (uint8_t)r;
+      vc.P.n_regs = vc.high;
+      bits = Alloc(e, std::max<int64_t>(ntiles, 1) * 4 * 8);
+      auto counts = Alloc(e, std::max<int64_t>(ntiles, 1) * 4);
+      offs = Alloc(e, std::max<int64_t>(ntiles, 1) * 8);
+      {
+        ProfScope ps(e, "vm_filter", 0, n);
+        dev::VmFilter(vc.P, vc.cols, n, rel.rs, rel.rstep, (uint64_t *)bits->p, (uint32_t *)counts->p, e.d_err,
+                      e.stream);
+      }
+      dev::ScanTileCounts((const uint32_t *)counts->p, (int64_t *)offs->p, ntiles, e.d_scratch, e.stream);
+      nsel = ReadDev<int64_t>(e, e.d_scratch);
+      CheckError(e);
+    }
+  }
+  DRel out;
+  out.n = nsel;
+  if (exprs.empty()) return out;
+  // compile all outputs into one program (split into chunks of VM_MAX_OUT)
+  for (size_t base = 0; base < exprs.size(); base += VM_MAX_OUT) {
+    size_t cnt = std::min<size_t>(VM_MAX_OUT, exprs.size() - base);
+    StrPool pool;
+    std::vector<DCol> outs;
+    std::vector<StrOut> strs;
+    // one program per chunk; string outputs each need their own program (src column tracking)
+    VmCompiler vc(rel, &pool);
+    std::vector<int> src_cols(cnt, -1);
+    for (size_t k = 0; k < cnt; k++) {
+      const BExpr &x = *exprs[base + k];
+      int prev_src = vc.str_src_col;
+      if (ClassOf(x.type) == VC_STR) vc.str_src_col = -1;
+      int r = vc.Compile(x);
+      if (ClassOf(x.type) == VC_STR) {
+        src_cols[k] = vc.str_src_col;
+      }
+      vc.str_src_col = prev_src < 0 ? vc.str_src_col : prev_src;
+      vc.P.out_reg[k] = (uint8_t)r;
+      vc.P.out_phys[k] = ClassOf(x.type) == VC_STR ? (uint8_t)P_I64 : (uint8_t)PhysOf(x.type);
+      vc.P.out_class[k] = ClassOf(x.type);
+      // r stays allocated (pinned) until the end of the program
+    }
+    vc.P.n_out = (int)cnt;
+    vc.P.n_regs = vc.high;
+    auto anynull = Alloc(e, VM_MAX_OUT * 4, true);
+    dev::VmOuts vo;
+    memset(&vo, 0, sizeof(vo));
+    vo.anynull = (int32_t *)anynull->p;
+    for (size_t k = 0; k < cnt; k++) {
+      DCol d = AllocOut(e, exprs[base + k]->type, nsel, true);
+      vo.data[k] = d.data;
+      vo.valid[k] = (uint32_t *)d.validity;
+      outs.push_back(d);
+    }
+    if (nsel > 0) {
+      ProfScope ps(e, "vm_project", 0, n);
+      dev::VmProject(vc.P, vc.cols, n, rel.rs, rel.rstep, bits ? (const uint64_t *)bits->p : nullptr,
+                     offs ? (const int64_t *)offs->p : nullptr, vo, e.d_err, e.stream);
+    }
+    int32_t an[VM_MAX_OUT];
+    HIPCHK(hipMemcpyAsync(an, anynull->p, sizeof(an), hipMemcpyDeviceToHost, e.stream));
+    CheckError(e);
+    for (size_t k = 0; k < cnt; k++) {
+      DCol &d = outs[k];
+      if (!an[k]) d.validity = nullptr;  // all valid: drop the bitmap (owner freed with the column)
+      if (ClassOf(exprs[base + k]->type) == VC_STR) {
+        const DCol *src = src_cols[k] >= 0 ? &rel.cols[src_cols[k]] : nullptr;
+        MaterializeStrings(e, d, src, pool, nsel);
+        d.phys = P_STR;
+      }
+      out.cols.push_back(d);
+    }
+  }
+  return out;
+}
+
+// ---------------------------------------------------------------------------
+// aggregation
+// ---------------------------------------------------------------------------
+// Column-vs-constant predicate that is a conjunction of comparisons on ONE
+// integer column: folded to lo <= col <= hi (inclusive).
+static const BExpr *StripWidening(const BExpr *x) {
+  while (x->kind == BExpr::FUNC && x->op == B_CAST) {
+    const LogicalType &f = x->ch[0]->type, &t = x->type;
+    bool ok = false;
+    if ((IsIntegral(f.id) || f.id == T_BOOLEAN) && IsIntegral(t.id)) {
+      i128 a, b, c, d;
+      IntegralRange(f.id, &a, &b);
+      IntegralRange(t.id, &c, &d);
+      ok = a >= c && b <= d;
+    } else if (f.id == T_DECIMAL && t.id == T_DECIMAL && f.scale == t.scale && t.width >= f.width) {
+      ok = true;
+    }
+    if (!ok) return x;
+    x = x->ch[0].get();
+  }
+  return x;
+}
+
+static bool RangePredicate(const BExpr &p, int *col, i128 *lo, i128 *hi) {
+  if (p.kind == BExpr::FUNC && p.op == B_AND) {
+    return RangePredicate(*p.ch[0], col, lo, hi) && RangePredicate(*p.ch[1], col, lo, hi);
+  }
+  if (p.kind != BExpr::FUNC) return false;
+  if (p.op != B_EQ && p.op != B_LT && p.op != B_LE && p.op != B_GT && p.op != B_GE) return false;
+  const BExpr *a = StripWidening(p.ch[0].get()), *b = StripWidening(p.ch[1].get());
+  BOp op = p.op;
+  if (a->kind == BExpr::CONST && b->kind == BExpr::COL) {
+    std::swap(a, b);
+    op = op == B_LT ? B_GT : op == B_LE ? B_GE : op == B_GT ? B_LT : op == B_GE ? B_LE : op;
+  }
+  if (a->kind != BExpr::COL || b->kind != BExpr::CONST) return false;
+  if (ClassOf(p.ch[0]->type) != VC_I64 && ClassOf(p.ch[0]->type) != VC_I128) return false;
+  if (p.ch[0]->type.id == T_DOUBLE || p.ch[0]->type.id == T_FLOAT) return false;
+  if (*col >= 0 && *col != a->col) return false;
+  *col = a->col;
+  if (b->cval.is_null) {  // comparison with NULL selects nothing
+    *lo = 1;
+    *hi = 0;
+    return true;
+  }
+  i128 c = b->cval.i;
+  switch (op) {
+    case B_EQ: *lo = std::max(*lo, c); *hi = std::min(*hi, c); break;
+    case B_GT: *lo = std::max(*lo, c + 1); break;
+    case B_GE: *lo = std::max(*lo, c); break;
+    case B_LT: *hi = std::min(*hi, c - 1); break;
+    case B_LE: *hi = std::min(*hi, c); break;
+    default: return false;
+  }
+  return true;
+}
+
+static bool FastIntCol(const DRel &rel, int c) {
+  if (rel.range && c == 0) return false;
+  const DCol &d = rel.cols[c];
+  return d.validity == nullptr && (d.phys == P_I32 || d.phys == P_I64) && d.data != nullptr;
+}
+
+static dev::EmitAgg EmitFor(const AggSpec &a, VClass in_class, dev::AggState *states, DCol &out) {
+  dev::EmitAgg ea;
+  memset(&ea, 0, sizeof(ea));
+  ea.kind = a.kind;
+  ea.in_class = in_class;
+  ea.out_phys = PhysOf(a.type);
+  ea.avg_scale = a.arg && a.arg->type.id == T_DECIMAL ? a.arg->type.scale : 0;
+  ea.states = states;
+  ea.out = out.data;
+  ea.valid = (uint32_t *)out.validity;
+  return ea;
+}
+
+static void DropEmptyValidity(Engine &e, DRel &r) {
+  // aggregates: keep bitmaps (cheap, tiny relations); nothing to do
+  (void)e;
+  (void)r;
+}
+
+static DRel Aggregate(Engine &e, const DRel &src, const BoundSelect &s) {
+  const int ng = (int)s.groups.size();
+  const int na = (int)s.aggs.size();
+  if (na > EMIT_MAX_AGGS) ThrowError("Not implemented", "too many aggregates in one query for the device path");
+  DRel out;
+  // ---- fast path F1: no GROUP BY, range predicate on one int column, all
+  //      aggregates over one int column (or COUNT(*)).
+  if (ng == 0 && !src.range) {
+    int pcol = -1;
+    i128 lo = (i128)INT64_MIN, hi = (i128)INT64_MAX;
+    bool pred_ok = !s.where || RangePredicate(*s.where, &pcol, &lo, &hi);
+    if (pred_ok && pcol >= 0 && !FastIntCol(src, pcol)) pred_ok = false;
+    int acol = -1;
+    bool aggs_ok = pred_ok;
+    for (auto &a : s.aggs) {
+      if (a.kind == A_COUNT_STAR) continue;
+      if (a.distinct) aggs_ok = false;
+      const BExpr *x = a.arg ? StripWidening(a.arg.get()) : nullptr;
+      if (!x || x->kind != BExpr::COL || !FastIntCol(src, x->col)) {
+        aggs_ok = false;
+        break;
+      }
+      if (a.arg->type.id == T_DOUBLE || a.arg->type.id == T_FLOAT) aggs_ok = false;
+      if (acol >= 0 && acol != x->col) aggs_ok = false;
+      acol = x->col;
+    }
+    if (aggs_ok && src.n > 0) {
+      if (lo < (i128)INT64_MIN) lo = INT64_MIN;
+      if (hi > (i128)INT64_MAX) hi = INT64_MAX;
+      bool empty = lo > hi;
+      dev::AggState *st = (dev::AggState *)e.d_small;
+      unsigned long long *cstar = (unsigned long long *)((char *)e.d_small + 1024);
+      dev::InitAggStates(st, 1, e.stream);
+      HIPCHK(hipMemsetAsync(cstar, 0, 8, e.stream));
+      if (!empty) {
+        const DCol *P = pcol >= 0 ? &src.cols[pcol] : nullptr;
+        const DCol *A = acol >= 0 ? &src.cols[acol] : nullptr;
+        if (!P && A) {
+          // no predicate: use the aggregate column as the (always-true) predicate column
+          P = A;
+        }
+        if (!P) P = nullptr;
+        double bytes = 0;
+        if (P) bytes += (double)src.n * PhysSize(P->phys);
+        if (A && A != P) bytes += (double)src.n * PhysSize(A->phys);
+        if (P) {
+          ProfScope ps(e, "filter_agg", bytes, src.n);
+          dev::FilterAggStates(P->data, P->phys, (int64_t)lo, (int64_t)hi, pcol >= 0, A ? A->data : nullptr,
+                               A ? A->phys : P_I64, src.n, st, cstar, 0, e.stream);
+        } else {
+          // COUNT(*) without predicate: the row count is known
+          unsigned long long c = (unsigned long long)src.n;
+          HIPCHK(hipMemcpyAsync(cstar, &c, 8, hipMemcpyHostToDevice, e.stream));
+          HIPCHK(hipStreamSynchronize(e.stream));
+        }
+      }
+      out.n = 1;
+      dev::EmitDesc D;
+      memset(&D, 0, sizeof(D));
+      D.nagg = na;
+      D.cstar = cstar;
+      D.nslots = 1;
+      D.null_slot = -1;
+      for (int j = 0; j < na; j++) {
+        DCol oc = AllocOut(e, s.aggs[j].type, 1, true);
+        D.a[j] = EmitFor(s.aggs[j], VC_I64, s.aggs[j].kind == A_COUNT_STAR ? nullptr : st, oc);
+        out.cols.push_back(oc);
+      }
+      dev::EmitAggRelation(D, e.stream);
+      return out;
+    }
+  }
+  // ---- fast path F2: GROUP BY one small-range int key column, aggregates
+  //      over <= 2 int columns of one phys, no predicate.
+  if (ng == 1 && !s.where && !src.range && s.groups[0]->kind == BExpr::COL && FastIntCol(src, s.groups[0]->col)) {
+    const DCol &K = src.cols[s.groups[0]->col];
+    const DevColumn *ks = K.table_col;
+    std::vector<int> vcols;
+    bool ok = ks && ks->stats_valid && ks->null_count == 0 && src.n > 0;
+    bool mm = false;
+    for (auto &a : s.aggs) {
+      if (a.kind == A_COUNT_STAR) continue;
+      if (a.distinct) ok = false;
+      const BExpr *x = a.arg ? StripWidening(a.arg.get()) : nullptr;
+      if (!x || x->kind != BExpr::COL || !FastIntCol(src, x->col) || a.arg->type.id == T_DOUBLE) {
+        ok = false;
+        break;
+      }
+      if (a.kind == A_MIN || a.kind == A_MAX) mm = true;
+      if (std::find(vcols.begin(), vcols.end(), x->col) == vcols.end()) vcols.push_back(x->col);
+    }
+    if (ok && vcols.size() <= 2) {
+      if (vcols.size() == 2 && src.cols[vcols[0]].phys != src.cols[vcols[1]].phys) ok = false;
+      i128 range = ks->imax - ks->imin + 1;
+      if (range > 1024 || range < 1) ok = false;
+      // overflow-free int64 partial sums: seg_rows / R rows per replica
+      i128 maxabs = 0;
+      for (int c : vcols) {
+        const DevColumn *vs = src.cols[c].table_col;
+        if (!vs || !vs->stats_valid) ok = false;
+        else maxabs = std::max(maxabs, std::max(vs->imax < 0 ? -vs->imax : vs->imax, vs->imin < 0 ? -vs->imin : vs->imin));
+      }
+      if (ok) {
+        int nk = (int)range;
+        int nv = (int)vcols.size();
+        int R = 64;
+        while (R > 1 && dev::GroupDirectLds(nk, R, nv, mm) > 48 * 1024) R >>= 1;
+        if (dev::GroupDirectLds(nk, R, nv, mm) > 64 * 1024) ok = false;
+        int64_t seg = 0;  // whole chunk
+        if (maxabs > 0) {
+          i128 per_rep = ((i128)1 << 62) / maxabs;  // rows one replica may absorb
+          i128 seg128 = per_rep * R;
+          if (seg128 < 4096) ok = false;
+          if (seg128 < (i128)INT64_MAX / 2) seg = (int64_t)seg128;
+        }
+        if ((int64_t)R * ((int64_t)1 << 31) < seg || seg == 0) {
+          // u32 replica counts: cap segment length
+          int64_t cap = (int64_t)R * ((int64_t)1 << 30);
+          if (seg == 0 || seg > cap) seg = cap;
+        }
+        if (ok) {
+          int64_t nslots = nk;
+          size_t st_bytes = (size_t)nslots * sizeof(dev::AggState);
+          auto cs = Alloc(e, nslots * 8, true);
+          auto s0 = Alloc(e, st_bytes), s1 = Alloc(e, st_bytes);
+          dev::InitAggStates((dev::AggState *)s0->p, nslots, e.stream);
+          dev::InitAggStates((dev::AggState *)s1->p, nslots, e.stream);
+          Phys vphys = nv ? src.cols[vcols[0]].phys : P_I64;
+          double bytes = (double)src.n * PhysSize(K.phys);
+          for (int c : vcols) bytes += (double)src.n * PhysSize(src.cols[c].phys);
+          {
+            ProfScope ps(e, "group_direct", bytes, src.n);
+            dev::GroupByDirectStates(K.data, K.phys, (int64_t)ks->imin, nk, nv > 0 ? src.cols[vcols[0]].data : nullptr,
+                                     nv > 1 ? src.cols[vcols[1]].data : nullptr, vphys, nv, mm, src.n, seg, R,
+                                     (unsigned long long *)cs->p, (dev::AggState *)s0->p, (dev::AggState *)s1->p, 0,
+                                     e.stream);
+          }
+          auto list = Alloc(e, nslots * 4);
+          dev::CompactSlots((const unsigned long long *)cs->p, nslots, (int32_t *)list->p, e.d_scratch, e.stream);
+          int64_t ngroups = ReadDev<int64_t>(e, e.d_scratch);
+          dev::EmitDesc D;
+          memset(&D, 0, sizeof(D));
+          D.nagg = na;
+          D.cstar = (const unsigned long long *)cs->p;
+          D.slot_list = (const int32_t *)list->p;
+          D.n_list = e.d_scratch;
+          D.nslots = ngroups;
+          D.has_key = 1;
+          D.key_phys = PhysOf(s.groups[0]->type);
+          D.kmin = (int64_t)ks->imin;
+          D.null_slot = -1;
+          DCol kc = AllocOut(e, s.groups[0]->type, ngroups, true);
+          D.key_out = kc.data;
+          D.key_valid = (uint32_t *)kc.validity;
+          out.n = ngroups;
+          out.cols.push_back(kc);
+          for (int j = 0; j < na; j++) {
+            DCol oc = AllocOut(e, s.aggs[j].type, ngroups, true);
+            dev::AggState *stp = nullptr;
+            if (s.aggs[j].kind != A_COUNT_STAR) {
+              int c = StripWidening(s.aggs[j].arg.get())->col;
+              stp = c == vcols[0] ? (dev::AggState *)s0->p : (dev::AggState *)s1->p;
+            }
+            D.a[j] = EmitFor(s.aggs[j], VC_I64, stp, oc);
+            out.cols.push_back(oc);
+          }
+          dev::EmitAggRelation(D, e.stream);
+          HIPCHK(hipStreamSynchronize(e.stream));  // state buffers released after emit
+          return out;
+        }
+      }
+    }
+  }
+  // ---- generic path: compact [groups..., agg args...] then reduce
+  std::vector<BExprPtr> exprs = s.groups;
+  std::vector<int> arg_idx(na, -1);
+  for (int j = 0; j < na; j++) {
+    if (s.aggs[j].kind == A_COUNT_STAR) continue;
+    arg_idx[j] = (int)exprs.size();
+    exprs.push_back(s.aggs[j].arg);
+  }
+  DRel tmp = FilterProject(e, src, s.where, exprs);
+  if (ng == 0) {
+    size_t st_bytes = std::max(na, 1) * sizeof(dev::AggState);
+    auto sb = Alloc(e, st_bytes);
+    dev::InitAggStates((dev::AggState *)sb->p, std::max(na, 1), e.stream);
+    auto cs = Alloc(e, 8);
+    unsigned long long cn = (unsigned long long)tmp.n;
+    HIPCHK(hipMemcpyAsync(cs->p, &cn, 8, hipMemcpyHostToDevice, e.stream));
+    for (int j = 0; j < na; j++) {
+      if (arg_idx[j] < 0) continue;
+      const DCol &c = tmp.cols[arg_idx[j]];
+      if (c.phys == P_STR) ThrowError("Not implemented", "aggregates over VARCHAR are not supported on device");
+      ProfScope ps(e, "reduce_column", (double)tmp.n * PhysSize(c.phys), tmp.n);
+      dev::ReduceColumn(c.data, c.phys, c.validity, tmp.n, (dev::AggState *)sb->p + j, e.stream);
+    }
+    dev::EmitDesc D;
+    memset(&D, 0, sizeof(D));
+    D.nagg = na;
+    D.cstar = (const unsigned long long *)cs->p;
+    D.nslots = 1;
+    D.null_slot = -1;
+    out.n = 1;
+    for (int j = 0; j < na; j++) {
+      DCol oc = AllocOut(e, s.aggs[j].type, 1, true);
+      VClass ic = arg_idx[j] >= 0 ? ClassOf(tmp.cols[arg_idx[j]].type) : VC_I64;
+      D.a[j] = EmitFor(s.aggs[j], ic, (dev::AggState *)sb->p + j, oc);
+      out.cols.push_back(oc);
+    }
+    dev::EmitAggRelation(D, e.stream);
+    HIPCHK(hipStreamSynchronize(e.stream));
+    return out;
+  }
+  if (ng > 1) ThrowError("Not implemented", "GROUP BY with more than one key is not supported on the MI355X device path yet");
+  const DCol &K = tmp.cols[0];
+  if (ClassOf(K.type) != VC_I64 || K.phys == P_STR || K.phys == P_F64 || K.phys == P_F32)
+    ThrowError("Not implemented", "GROUP BY key of type " + K.type.ToString() + " is not supported on device yet");
+  long long *kr = (long long *)((char *)e.d_small + 2048);
+  dev::KeyRange(K.data, K.phys, K.validity, tmp.n, kr, e.stream);
+  long long krh[3];
+  HIPCHK(hipMemcpyAsync(krh, kr, sizeof(krh), hipMemcpyDeviceToHost, e.stream));
+  HIPCHK(hipStreamSynchronize(e.stream));
+  int64_t kmin = krh[2] ? krh[0] : 0;
+  i128 range = krh[2] ? (i128)krh[1] - krh[0] + 1 : 0;
+  if (range > (1 << 24)) ThrowError("Not implemented", "GROUP BY key range too wide for the direct-index device path");
+  int64_t nslots = (int64_t)range + 1;  // + NULL group
+  auto slot_of = Alloc(e, std::max<int64_t>(tmp.n, 1) * 4);
+  auto cs = Alloc(e, nslots * 8, true);
+  {
+    ProfScope ps(e, "group_assign", (double)tmp.n * PhysSize(K.phys), tmp.n);
+    dev::GroupAssign(K.data, K.phys, K.validity, kmin, nslots, tmp.n, (int32_t *)slot_of->p,
+                     (unsigned long long *)cs->p, e.stream);
+  }
+  std::vector<DevBufPtr> states(na);
+  for (int j = 0; j < na; j++) {
+    if (arg_idx[j] < 0) continue;
+    const DCol &c = tmp.cols[arg_idx[j]];
+    if (c.phys == P_STR) ThrowError("Not implemented", "aggregates over VARCHAR are not supported on device");
+    states[j] = Alloc(e, nslots * sizeof(dev::AggState));
+    dev::InitAggStates((dev::AggState *)states[j]->p, nslots, e.stream);
+    ProfScope ps(e, "group_reduce", (double)tmp.n * (PhysSize(c.phys) + 4), tmp.n);
+    dev::GroupReduceColumn((const int32_t *)slot_of->p, c.data, c.phys, c.validity, tmp.n,
+                           (dev::AggState *)states[j]->p, e.stream);
+  }
+  auto list = Alloc(e, nslots * 4);
+  dev::CompactSlots((const unsigned long long *)cs->p, nslots, (int32_t *)list->p, e.d_scratch, e.stream);
+  int64_t ngroups = ReadDev<int64_t>(e, e.d_scratch);
+  dev::EmitDesc D;
+  memset(&D, 0, sizeof(D));
+  D.nagg = na;
+  D.cstar = (const unsigned long long *)cs->p;
+  D.slot_list = (const int32_t *)list->p;
+  D.n_list = e.d_scratch;
+  D.nslots = ngroups;
+  D.has_key = 1;
+  D.key_phys = PhysOf(s.groups[0]->type);
+  D.kmin = kmin;
+  D.null_slot = nslots - 1;
+  DCol kc = AllocOut(e, s.groups[0]->type, ngroups, true);
+  D.key_out = kc.data;
+  D.key_valid = (uint32_t *)kc.validity;
+  out.n = ngroups;
+  out.cols.push_back(kc);
+  for (int j = 0; j < na; j++) {
+    DCol oc = AllocOut(e, s.aggs[j].type, ngroups, true);
+    VClass ic = arg_idx[j] >= 0 ? ClassOf(tmp.cols[arg_idx[j]].type) : VC_I64;
+    D.a[j] = EmitFor(s.aggs[j], ic, states[j] ? (dev::AggState *)states[j]->p : nullptr, oc);
+    out.cols.push_back(oc);
+  }
+  dev::EmitAggRelation(D, e.stream);
+  HIPCHK(hipStreamSynchronize(e.stream));
+  DropEmptyValidity(e, out);
+  return out;
+}
+
+// ---------------------------------------------------------------------------
+// sort, limit, union
+// ---------------------------------------------------------------------------
+static DRel GatherRel(Engine &e, const DRel &r, const int64_t *perm, int64_t n) {
+  DRel out;
+  out.n = n;
+  for (const DCol &c : r.cols) {
+    if (c.phys == P_STR) {
+      // gather codes = perm, then materialize strings from the source column
+      DCol d;
+      d.type = c.type;
+      d.phys = P_STR;
+      auto codes = Alloc(e, std::max<int64_t>(n, 1) * 8);
+      HIPCHK(hipMemcpyAsync(codes->p, perm, n * 8, hipMemcpyDeviceToDevice, e.stream));
+      d.data = codes->p;
+      d.owners.push_back(codes);
+      if (c.validity) {
+        auto v = Alloc(e, Words64(std::max<int64_t>(n, 1)) * 8, true);
+        // validity gather through a fixed-width gather of a dummy u8 column
+        auto dummy = Alloc(e, std::max<int64_t>(r.n, 1));
+        auto dout = Alloc(e, std::max<int64_t>(n, 1));
+        dev::GatherFixed(dummy->p, P_U8, c.validity, perm, n, dout->p, (uint32_t *)v->p, e.stream);
+        d.validity = (uint64_t *)v->p;
+        d.owners.push_back(v);
+        d.owners.push_back(dummy);
+        d.owners.push_back(dout);
+      }
+      StrPool empty;
+      MaterializeStrings(e, d, &c, empty, n);
+      out.cols.push_back(d);
+      continue;
+    }
+    DCol d = AllocOut(e, c.type, n, c.validity != nullptr);
+    dev::GatherFixed(c.data, c.phys, c.validity, perm, n, d.data, (uint32_t *)d.validity, e.stream);
+    out.cols.push_back(d);
+  }
+  return out;
+}
+
+static DRel SortRel(Engine &e, const DRel &r, const std::vector<BoundOrder> &order) {
+  int64_t n = r.n;
+  if (n <= 1 || order.empty()) return r;
+  auto perm = Alloc(e, n * 8), perm2 = Alloc(e, n * 8);
+  auto keys = Alloc(e, n * 8), keys2 = Alloc(e, n * 8);
+  dev::Iota((int64_t *)perm->p, n, 0, e.stream);
+  for (int k = (int)order.size() - 1; k >= 0; k--) {
+    const BoundOrder &o = order[k];
+    const DCol &c = r.cols[o.expr->col];
+    if (c.phys == P_STR) ThrowError("Not implemented", "ORDER BY a VARCHAR column is not supported on device yet");
+    if (c.phys == P_I128 || c.phys == P_INTERVAL)
+      ThrowError("Not implemented", "ORDER BY a " + c.type.ToString() + " column is not supported on device yet");
+    bool nulls_first = o.nulls_first;
+    dev::SortKeyU64(c.data, c.phys, c.validity, n, (const int64_t *)perm->p, o.desc, nulls_first,
+                    (uint64_t *)keys->p, e.stream);
+    ProfScope ps(e, "radix_sort", (double)n * 16, n);
+    dev::SortPairs((uint64_t *)keys->p, (int64_t *)perm->p, (uint64_t *)keys2->p, (int64_t *)perm2->p, n, e.stream);
+    std::swap(perm, perm2);
+  }
+  DRel out = GatherRel(e, r, (const int64_t *)perm->p, n);
+  HIPCHK(hipStreamSynchronize(e.stream));
+  return out;
+}
+
+static DRel ConcatRels(Engine &e, std::vector<DRel> &parts) {
+  DRel out;
+  int64_t total = 0;
+  for (auto &p : parts) total += p.n;
+  out.n = total;
+  size_t nc = parts[0].cols.size();
+  for (size_t c = 0; c < nc; c++) {
+    const DCol &c0 = parts[0].cols[c];
+    bool anyv = false;
+    for (auto &p : parts)
+      if (p.cols[c].validity) anyv = true;
+    DCol d;
+    d.type = c0.type;
+    d.phys = c0.phys;
+    if (anyv) {
+      auto v = Alloc(e, Words64(std::max<int64_t>(total, 1)) * 8, true);
+      d.validity = (uint64_t *)v->p;
+      d.owners.push_back(v);
+    }
+    if (c0.phys == P_STR) {
+      int64_t chars = 0;
+      for (auto &p : parts) chars += p.cols[c].chars_len;
+      auto ob = Alloc(e, (total + 1) * 8), cb = Alloc(e, std::max<int64_t>(chars, 1));
+      int64_t row = 0, cpos = 0;
+      for (auto &p : parts) {
+        const DCol &s = p.cols[c];
+        if (p.n) {
+          dev::RebaseOffsets(s.offsets, (int64_t *)ob->p + row, p.n + 1, cpos, e.stream);
+          if (s.chars_len)
+            HIPCHK(hipMemcpyAsync((char *)cb->p + cpos, s.chars, s.chars_len, hipMemcpyDeviceToDevice, e.stream));
+        }
+        row += p.n;
+        cpos += s.chars_len;
+      }
+      if (total == 0) HIPCHK(hipMemsetAsync(ob->p, 0, 8, e.stream));
+      d.offsets = (int64_t *)ob->p;
+      d.chars = (char *)cb->p;
+      d.chars_len = chars;
+      d.owners.push_back(ob);
+      d.owners.push_back(cb);
+    } else {
+      int sz = PhysSize(c0.phys);
+      auto db = Alloc(e, std::max<int64_t>(total, 1) * sz);
+      int64_t row = 0;
+      for (auto &p : parts) {
+        if (p.n) HIPCHK(hipMemcpyAsync((char *)db->p + row * sz, p.cols[c].data, p.n * sz, hipMemcpyDeviceToDevice, e.stream));
+        row += p.n;
+      }
+      d.data = db->p;
+      d.owners.push_back(db);
+    }
+    if (anyv) {
+      int64_t row = 0;
+      for (auto &p : parts) {
+        dev::BitmapAppend(d.validity, row, p.cols[c].validity, p.n, e.stream);
+        row += p.n;
+      }
+    }
+    out.cols.push_back(d);
+  }
+  HIPCHK(hipStreamSynchronize(e.stream));
+  return out;
+}
+
+// ---------------------------------------------------------------------------
+// device -> host
+// ---------------------------------------------------------------------------
+static ResultPtr ToHost(Engine &e, const DRel &r, const std::vector<std::string> &names, int64_t offset, int64_t limit,
+                        size_t ncols) {
+  auto res = std::make_shared<MaterializedResult>();
+  int64_t start = std::min(std::max<int64_t>(offset, 0), r.n);
+  int64_t n = r.n - start;
+  if (limit >= 0) n = std::min(n, limit);
+  res->nrows = n;
+  for (size_t c = 0; c < ncols; c++) {
+    const DCol &d = r.cols[c];
+    HostColumn hc;
+    hc.name = names[c];
+    hc.type = d.type;
+    hc.phys = d.phys;
+    if (d.phys == P_STR) {
+      std::vector<int64_t> off(n + 1);
+      if (n > 0) {
+        HIPCHK(hipMemcpyAsync(off.data(), d.offsets + start, (n + 1) * 8, hipMemcpyDeviceToHost, e.stream));
+        HIPCHK(hipStreamSynchronize(e.stream));
+        int64_t base = off[0], len = off[n] - off[0];
+        hc.chars.resize(len);
+        if (len) HIPCHK(hipMemcpyAsync(&hc.chars[0], d.chars + base, len, hipMemcpyDeviceToHost, e.stream));
+        for (auto &o : off) o -= base;
+      } else {
+        off[0] = 0;
+      }
+      hc.offsets = off;
+    } else {
+      int sz = PhysSize(d.phys);
+      hc.data.resize((size_t)n * sz);
+      if (n > 0) HIPCHK(hipMemcpyAsync(hc.data.data(), (char *)d.data + start * sz, (size_t)n * sz, hipMemcpyDeviceToHost, e.stream));
+    }
+    if (d.validity && n > 0) {
+      int64_t w0 = start >> 6, w1 = (start + n + 63) >> 6;
+      std::vector<uint64_t> bm(w1 - w0);
+      HIPCHK(hipMemcpyAsync(bm.data(), d.validity + w0, bm.size() * 8, hipMemcpyDeviceToHost, e.stream));
+      HIPCHK(hipStreamSynchronize(e.stream));
+      hc.valid.resize(n);
+      for (int64_t i = 0; i < n; i++) {
+        int64_t b = start + i - (w0 << 6);
+        hc.valid[i] = (bm[b >> 6] >> (b & 63)) & 1;
+      }
+    }
+    res->cols.push_back(std::move(hc));
+  }
+  HIPCHK(hipStreamSynchronize(e.stream));
+  return res;
+}
+
+// ---------------------------------------------------------------------------
+// select
+// ---------------------------------------------------------------------------
+static ResultPtr HostConstantSelect(const BoundSelect &s);
+
+static DRel RunSelectDev(Engine &e, Connection &c, const BoundSelect &s);
+
+static DRel SourceRel(Engine &e, Connection &c, const BoundSource &src) {
+  DRel r;
+  switch (src.kind) {
+    case BoundSource::ONE_ROW:
+      r.n = 1;
+      break;
+    case BoundSource::RANGE: {
+      r.n = src.RangeCount();
+      r.range = true;
+      r.rs = src.range_start;
+      r.rstep = src.range_step;
+      DCol d;
+      d.type = LogicalType(T_BIGINT);
+      d.phys = P_I64;
+      r.cols.push_back(d);
+      break;
+    }
+    case BoundSource::TABLE: {
+      r.n = src.table->nrows;
+      for (auto &col : src.table->cols) r.cols.push_back(ColFromTable(col));
+      break;
+    }
+    case BoundSource::VALUES:
+      r = UploadRows(e, src.rows, src.col_types);
+      break;
+    case BoundSource::SUBQUERY:
+      r = RunSelectDev(e, c, *src.sub);
+      // hidden order keys of the subquery are dropped by RunSelectDev
+      break;
+  }
+  return r;
+}
+
+static DRel RunBranch(Engine &e, Connection &c, const BoundSelect &s) {
+  if (IsHostConstantSelect(s) && s.union_all.empty()) {
+    ResultPtr hr = HostConstantSelect(s);
+    DRel r;
+    r.n = hr->nrows;
+    for (auto &hc : hr->cols) {
+      DCol d;
+      UploadHostColumn(e, hc, hr->nrows, d);
+      r.cols.push_back(d);
+    }
+    return r;
+  }
+  DRel src = SourceRel(e, c, s.src);
+  if (s.is_agg) {
+    DRel agg = Aggregate(e, src, s);
+    return FilterProject(e, agg, s.having, s.outputs);
+  }
+  return FilterProject(e, src, s.where, s.outputs);
+}
+
+static size_t VisibleCols(const BoundSelect &s) {
+  size_t n = 0;
+  for (auto &nm : s.names)
+    if (nm.rfind("__order_", 0) != 0) n++;
+  return n;
+}
+
+static DRel RunSelectDev(Engine &e, Connection &c, const BoundSelect &s) {
+  DRel r = RunBranch(e, c, s);
+  if (!s.union_all.empty()) {
+    std::vector<DRel> parts;
+    parts.push_back(r);
+    for (auto &u : s.union_all) parts.push_back(RunBranch(e, c, *u));
+    r = ConcatRels(e, parts);
+  }
+  if (!s.order.empty()) r = SortRel(e, r, s.order);
+  if (s.limit >= 0 || s.offset > 0) {
+    int64_t start = std::min(s.offset, r.n);
+    int64_t n = r.n - start;
+    if (s.limit >= 0) n = std::min(n, s.limit);
+    auto perm = Alloc(e, std::max<int64_t>(n, 1) * 8);
+    dev::Iota((int64_t *)perm->p, n, start, e.stream);
+    r = GatherRel(e, r, (const int64_t *)perm->p, n);
+  }
+  r.cols.resize(VisibleCols(s));
+  return r;
+}
+
+// ---- host-constant selects (no FROM): the binder folded every expression
+static ResultPtr HostConstantSelect(const BoundSelect &s) {
+  std::vector<std::vector<Value>> rows;
+  std::function<void(const BoundSelect &)> add = [&](const BoundSelect &b) {
+    bool keep = true;
+    if (b.where) {
+      Value w = EvalConst(*b.where);
+      keep = !w.is_null && w.i;
+    }
+    if (b.is_agg) {
+      // aggregates over the single constant row
+      std::vector<Value> aggvals;
+      for (auto &g : b.groups) aggvals.push_back(EvalConst(*g));
+      for (auto &a : b.aggs) {
+        Value v;
+        Value x = a.arg ? EvalConst(*a.arg) : Value::Int(T_BIGINT, 1);
+        bool has = keep && (!a.arg || !x.is_null);
+        switch (a.kind) {
+          case A_COUNT_STAR: v = Value::Int(T_BIGINT, keep ? 1 : 0); break;
+          case A_COUNT: v = Value::Int(T_BIGINT, has ? 1 : 0); break;
+          case A_AVG: v = has ? CastValue(x, LogicalType(T_DOUBLE)) : Value::Null(a.type); break;
+          default: v = has ? CastValue(x, a.type) : Value::Null(a.type); break;
+        }
+        aggvals.push_back(v);
+      }
+      if (!b.groups.empty() && !keep) return;
+      // bind outputs over the aggregate row
+      std::function<Value(const BExpr &)> ev = [&](const BExpr &x) -> Value {
+        if (x.kind == BExpr::COL) return aggvals[x.col];
+        if (x.kind == BExpr::CONST) return EvalConst(x);
+        BExpr copy = x;
+        for (auto &ch : copy.ch) {
+          Value v = ev(*ch);
+          auto c = std::make_shared<BExpr>();
+          c->kind = BExpr::CONST;
+          c->cval = v;
+          c->type = ch->type;
+          ch = c;
+        }
+        return EvalConst(copy);
+      };
+      if (b.having) {
+        Value h = ev(*b.having);
+        if (h.is_null || !h.i) return;
+      }
+      std::vector<Value> row;
+      for (auto &o : b.outputs) row.push_back(CastValue(ev(*o), o->type));
+      rows.push_back(row);
+      return;
+    }
+    if (!keep) return;
+    std::vector<Value> row;
+    for (auto &o : b.outputs) row.push_back(CastValue(EvalConst(*o), o->type));
+    rows.push_back(row);
+  };
+  add(s);
+  for (auto &u : s.union_all) add(*u);
+  // ORDER BY / LIMIT over constant rows (tiny): the rows are already values
+  if (!s.order.empty()) {
+    std::stable_sort(rows.begin(), rows.end(), [&](const std::vector<Value> &a, const std::vector<Value> &b) {
+      for (auto &o : s.order) {
+        const Value &x = a[o.expr->col], &y = b[o.expr->col];
+        if (x.is_null || y.is_null) {
+          if (x.is_null && y.is_null) continue;
+          bool xfirst = x.is_null == o.nulls_first;
+          return xfirst;
+        }
+        Value xc = x, yc = y;
+        int c;
+        if (ClassOf(x.type) == VC_F64) c = x.d < y.d ? -1 : x.d > y.d ? 1 : 0;
+        else if (ClassOf(x.type) == VC_STR) c = x.s < y.s ? -1 : x.s > y.s ? 1 : 0;
+        else c = x.i < y.i ? -1 : x.i > y.i ? 1 : 0;
+        if (c) return o.desc ? c > 0 : c < 0;
+      }
+      return false;
+    });
+  }
+  int64_t start = std::min<int64_t>(s.offset, (int64_t)rows.size());
+  int64_t n = (int64_t)rows.size() - start;
+  if (s.limit >= 0) n = std::min(n, s.limit);
+  auto res = std::make_shared<MaterializedResult>();
+  res->nrows = n;
+  size_t nvis = VisibleCols(s);
+  for (size_t c = 0; c < nvis; c++) {
+    HostColumn hc;
+    hc.name = s.names[c];
+    hc.type = s.outputs[c]->type;
+    hc.phys = PhysOf(hc.type);
+    if (hc.phys == P_STR) hc.offsets.push_back(0);
+    for (int64_t i = 0; i < n; i++) HostColumnPush(hc, rows[start + i][c]);
+    res->cols.push_back(std::move(hc));
+  }
+  return res;
+}
+
+static void FinishProfile(Connection &c, Engine &e, double total_ms) {
+  QueryProfile &p = c.last_profile;
+  p.kernels.clear();
+  p.total_ms = total_ms;
+  p.plan = e.plan_text;
+  if (!e.profile) return;
+  hipStreamSynchronize(e.stream);
+  for (auto &ev : e.events) {
+    float ms = 0;
+    hipEventElapsedTime(&ms, ev.a, ev.b);
+    QueryProfile::Kernel k;
+    k.name = ev.name;
+    k.ms = ms;
+    k.bytes = ev.bytes;
+    k.rows = ev.rows;
+    p.kernels.push_back(k);
+    hipEventDestroy(ev.a);
+    hipEventDestroy(ev.b);
+  }
+  e.events.clear();
+}
+
+ResultPtr ExecuteSelect(Connection &c, const BoundSelect &s) {
+  auto t0 = std::chrono::steady_clock::now();
+  if (IsHostConstantSelect(s)) {
+    ResultPtr r = HostConstantSelect(s);
+    c.last_profile = QueryProfile();
+    return r;
+  }
+  Engine &e = Eng(c);
+  e.profile = c.opts.profile;
+  e.events.clear();
+  e.plan_text = c.opts.profile ? ExplainSelect(s) : "";
+  DRel r = RunSelectDev(e, c, s);
+  std::vector<std::string> names(s.names.begin(), s.names.begin() + VisibleCols(s));
+  ResultPtr res = ToHost(e, r, names, 0, -1, names.size());
+  CheckError(e);
+  double ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+  FinishProfile(c, e, ms);
+  return res;
+}
+
+// ---------------------------------------------------------------------------
+// tables: creation, append, stats
+// ---------------------------------------------------------------------------
+Table::~Table() {
+  hipSetDevice(device);
+  for (auto &c : cols) {
+    if (c.data) hipFree(c.data);
+    if (c.validity) hipFree(c.validity);
+    if (c.offsets) hipFree(c.offsets);
+    if (c.chars) hipFree(c.chars);
+  }
+}
+
+TablePtr CreateDeviceTable(Connection &c, const std::string &name, const std::vector<std::string> &names,
+                           const std::vector<LogicalType> &types) {
+  auto t = std::make_shared<Table>();
+  t->name = name;
+  t->col_names = names;
+  t->device = c.engine->device;
+  for (auto &ty : types) {
+    DevColumn dc;
+    dc.type = ty;
+    dc.phys = PhysOf(ty);
+    dc.stats_valid = true;
+    dc.imin = 0;
+    dc.imax = 0;
+    t->cols.push_back(dc);
+  }
+  return t;
+}
+
+void DropDeviceTable(Table &t) { (void)t; }
+
+static void Grow(Engine &e, DevColumn &c, int64_t nrows_old, int64_t need) {
+  if (need <= c.capacity && (c.phys != P_STR || c.offsets)) return;
+  int64_t cap = std::max<int64_t>(need, std::max<int64_t>(1024, c.capacity * 2));
+  if (c.phys == P_STR) {
+    int64_t *no = nullptr;
+    HIPCHK(hipMalloc(&no, (cap + 1) * 8));
+    if (c.offsets) HIPCHK(hipMemcpyAsync(no, c.offsets, (nrows_old + 1) * 8, hipMemcpyDeviceToDevice, e.stream));
+    else HIPCHK(hipMemsetAsync(no, 0, 8, e.stream));
+    HIPCHK(hipStreamSynchronize(e.stream));
+    if (c.offsets) HIPCHK(hipFree(c.offsets));
+    c.offsets = no;
+  } else {
+    void *nd = nullptr;
+    int sz = PhysSize(c.phys);
+    HIPCHK(hipMalloc(&nd, (size_t)cap * sz));
+    if (c.data && nrows_old) HIPCHK(hipMemcpyAsync(nd, c.data, (size_t)nrows_old * sz, hipMemcpyDeviceToDevice, e.stream));
+    HIPCHK(hipStreamSynchronize(e.stream));
+    if (c.data) HIPCHK(hipFree(c.data));
+    c.data = nd;
+  }
+  if (c.validity) {
+    uint64_t *nv = nullptr;
+    HIPCHK(hipMalloc(&nv, Words64(cap) * 8));
+    HIPCHK(hipMemsetAsync(nv, 0xFF, Words64(cap) * 8, e.stream));
+    HIPCHK(hipMemcpyAsync(nv, c.validity, Words64(nrows_old) * 8, hipMemcpyDeviceToDevice, e.stream));
+    HIPCHK(hipStreamSynchronize(e.stream));
+    HIPCHK(hipFree(c.validity));
+    c.validity = nv;
+  }
+  c.capacity = cap;
+}
+
+static void EnsureValidity(Engine &e, DevColumn &c, int64_t nrows_old) {
+  if (c.validity) return;
+  int64_t cap = std::max<int64_t>(c.capacity, 1);
+  HIPCHK(hipMalloc(&c.validity, Words64(cap) * 8));
+  HIPCHK(hipMemsetAsync(c.validity, 0xFF, Words64(cap) * 8, e.stream));
+  (void)nrows_old;
+}
+
+static void UpdateStats(Engine &e, DevColumn &c, int64_t off, int64_t n, bool first_rows) {
+  if (n <= 0) return;
+  if (c.phys == P_STR || c.phys == P_F32 || c.phys == P_F64 || c.phys == P_I128 || c.phys == P_U64 ||
+      c.phys == P_INTERVAL) {
+    c.stats_valid = false;
+    return;
+  }
+  long long *o3 = (long long *)((char *)e.d_small + 3072);
+  int sz = PhysSize(c.phys);
+  // stats over the appended range; validity offsets are bit offsets, so use a
+  // validity-free pass when the column has no NULLs
+  const uint64_t *v = nullptr;
+  if (c.validity && (off & 63) == 0) v = c.validity + (off >> 6);
+  else if (c.validity) {
+    c.stats_valid = false;
+    return;
+  }
+  dev::ColumnStats((const char *)c.data + off * sz, c.phys, v, n, o3, e.stream);
+  long long h[3];
+  HIPCHK(hipMemcpyAsync(h, o3, sizeof(h), hipMemcpyDeviceToHost, e.stream));
+  HIPCHK(hipStreamSynchronize(e.stream));
+  c.null_count += n - h[2];
+  if (h[2] > 0) {
+    if (first_rows || !c.stats_valid) {
+      c.imin = h[0];
+      c.imax = h[1];
+    } else {
+      c.imin = std::min<i128>(c.imin, h[0]);
+      c.imax = std::max<i128>(c.imax, h[1]);
+    }
+  }
+}
+
+static void AppendDRel(Engine &e, Table &t, const DRel &r, const std::vector<int> &col_map) {
+  int64_t n = r.n, old = t.nrows;
+  if (n <= 0) return;
+  for (size_t tc = 0; tc < t.cols.size(); tc++) {
+    DevColumn &c = t.cols[tc];
+    Grow(e, c, old, old + n);
+    int src = col_map[tc];
+    if (src < 0) {
+      // column not provided: NULLs
+      EnsureValidity(e, c, old);
+      auto zeros = Alloc(e, Words64(n) * 8, true);
+      dev::BitmapAppend(c.validity, old, (const uint64_t *)zeros->p, n, e.stream);
+      if (c.phys == P_STR) {
+        std::vector<int64_t> offs(n + 1, c.chars_len);
+        // offsets already hold old entries; append n equal offsets
+        HIPCHK(hipMemcpyAsync(c.offsets + old + 1, offs.data(), n * 8, hipMemcpyHostToDevice, e.stream));
+      }
+      HIPCHK(hipStreamSynchronize(e.stream));
+      c.null_count += n;
+      continue;
+    }
+    const DCol &d = r.cols[src];
+    if (d.phys != c.phys) ThrowError("Internal", "append: physical type mismatch");
+    if (c.phys == P_STR) {
+      int64_t need = c.chars_len + d.chars_len;
+      if (need > c.chars_cap) {
+        int64_t cap = std::max<int64_t>(need, std::max<int64_t>(4096, c.chars_cap * 2));
+        char *nc = nullptr;
+        HIPCHK(hipMalloc(&nc, cap));
+        if (c.chars_len) HIPCHK(hipMemcpyAsync(nc, c.chars, c.chars_len, hipMemcpyDeviceToDevice, e.stream));
+        HIPCHK(hipStreamSynchronize(e.stream));
+        if (c.chars) HIPCHK(hipFree(c.chars));
+        c.chars = nc;
+        c.chars_cap = cap;
+      }
+      if (d.chars_len) HIPCHK(hipMemcpyAsync(c.chars + c.chars_len, d.chars, d.chars_len, hipMemcpyDeviceToDevice, e.stream));
+      dev::RebaseOffsets(d.offsets + 1, c.offsets + old + 1, n, c.chars_len, e.stream);
+      c.chars_len += d.chars_len;
+    } else {
+      int sz = PhysSize(c.phys);
+      HIPCHK(hipMemcpyAsync((char *)c.data + old * sz, d.data, (size_t)n * sz, hipMemcpyDeviceToDevice, e.stream));
+    }
+    if (d.validity) {
+      EnsureValidity(e, c, old);
+      dev::BitmapAppend(c.validity, old, d.validity, n, e.stream);
+    } else if (c.validity) {
+      dev::BitmapAppend(c.validity, old, nullptr, n, e.stream);
+    }
+    UpdateStats(e, c, old, n, old == 0);
+  }
+  HIPCHK(hipStreamSynchronize(e.stream));
+  t.nrows = old + n;
+}
+
+void ExecuteInsertSelect(Connection &c, Table &t, const BoundSelect &s, const std::vector<int> &col_map) {
+  Engine &e = Eng(c);
+  e.profile = false;
+  DRel r;
+  if (IsHostConstantSelect(s)) {
+    ResultPtr hr = HostConstantSelect(s);
+    r.n = hr->nrows;
+    for (auto &hc : hr->cols) {
+      DCol d;
+      UploadHostColumn(e, hc, hr->nrows, d);
+      r.cols.push_back(d);
+    }
+  } else {
+    r = RunSelectDev(e, c, s);
+  }
+  // cast columns to the table types on device when they differ
+  std::vector<BExprPtr> casts;
+  bool need = false;
+  for (size_t tc = 0; tc < t.cols.size(); tc++) {
+    int src = col_map[tc];
+    if (src < 0) continue;
+    if (!(r.cols[src].type == t.cols[tc].type)) need = true;
+  }
+  if (need) {
+    std::vector<BExprPtr> exprs;
+    std::vector<int> map2(t.cols.size(), -1);
+    for (size_t tc = 0; tc < t.cols.size(); tc++) {
+      int src = col_map[tc];
+      if (src < 0) continue;
+      auto col = std::make_shared<BExpr>();
+      col->kind = BExpr::COL;
+      col->col = src;
+      col->type = r.cols[src].type;
+      BExprPtr x = col;
+      if (!(col->type == t.cols[tc].type)) {
+        auto cst = std::make_shared<BExpr>();
+        cst->kind = BExpr::FUNC;
+        cst->op = B_CAST;
+        cst->type = t.cols[tc].type;
+        cst->ch = {col};
+        x = cst;
+      }
+      map2[tc] = (int)exprs.size();
+      exprs.push_back(x);
+    }
+    r = FilterProject(e, r, nullptr, exprs);
+    AppendDRel(e, t, r, map2);
+  } else {
+    AppendDRel(e, t, r, col_map);
+  }
+  CheckError(e);
+}
+
+void AppendHostBatch(Connection &c, Table &t, const HostBatch &b) {
+  Engine &e = Eng(c);
+  DRel r;
+  r.n = b.nrows;
+  std::vector<int> map;
+  for (size_t i = 0; i < b.cols.size(); i++) {
+    DCol d;
+    UploadHostColumn(e, b.cols[i], b.nrows, d);
+    r.cols.push_back(d);
+    map.push_back((int)i);
+  }
+  AppendDRel(e, t, r, map);
+}
+
+}  // namespace mbx

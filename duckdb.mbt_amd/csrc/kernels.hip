@@ -1,0 +1,1406 @@
+// kernels.hip — hand-written gfx950 (CDNA4) kernels of the columnar backend.
+//
+// All of this is HBM-bound integer/byte work: no MFMA.  Design rules applied
+// (cdna_hip_programming.md §6 G2/G7/G11/G12/G13):
+//   * 16-byte vector loads (global_load_dwordx4), several in flight per lane;
+//   * wave64 ballot / mbcnt for predicate compaction and bit packing;
+//   * per-thread -> per-wave (DPP/shuffle) -> per-block (LDS) reduction and
+//     ONE global atomic per block and aggregate (128-bit sums as a carry-correct
+//     pair of 64-bit atomics, exact in any order);
+//   * GROUP BY on small key ranges in LDS-privatised replicated tables
+//     (one replica per lane index -> no same-address conflicts inside a wave).
+#include <hip/hip_runtime.h>
+#include <hipcub/hipcub.hpp>
+#include <stdint.h>
+
+#include "device.h"
+#include "types.h"
+#include "vm.h"
+
+namespace mbx {
+namespace dev {
+
+typedef __int128 i128;
+typedef unsigned __int128 u128;
+
+#define CHECK_LAUNCH() (void)hipGetLastError()
+
+static int g_num_cus = 0;
+int NumCUs() {
+  if (!g_num_cus) {
+    int d = 0;
+    (void)hipGetDevice(&d);
+    hipDeviceProp_t pr;
+    if (hipGetDeviceProperties(&pr, d) == hipSuccess) g_num_cus = pr.multiProcessorCount;
+    if (g_num_cus <= 0) g_num_cus = 256;
+  }
+  return g_num_cus;
+}
+
+static inline int GridFor(int64_t work_items, int per_block, int max_blocks) {
+  int64_t b = (work_items + per_block - 1) / per_block;
+  if (b < 1) b = 1;
+  if (b > max_blocks) b = max_blocks;
+  return (int)b;
+}
+
+// ---------------------------------------------------------------------------
+// small device helpers
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ bool bit_valid(const uint64_t *v, int64_t row) {
+  return v == nullptr || ((v[row >> 6] >> (row & 63)) & 1ull);
+}
+
+__device__ __forceinline__ void load_phys(const void *data, int phys, int64_t row, int64_t &lo, int64_t &hi) {
+  switch (phys) {
+    case P_U8: lo = ((const uint8_t *)data)[row]; hi = 0; break;
+    case P_I8: lo = ((const int8_t *)data)[row]; hi = lo >> 63; break;
+    case P_I16: lo = ((const int16_t *)data)[row]; hi = lo >> 63; break;
+    case P_U16: lo = ((const uint16_t *)data)[row]; hi = 0; break;
+    case P_I32: lo = ((const int32_t *)data)[row]; hi = lo >> 63; break;
+    case P_U32: lo = ((const uint32_t *)data)[row]; hi = 0; break;
+    case P_I64: lo = ((const int64_t *)data)[row]; hi = lo >> 63; break;
+    case P_U64: lo = (int64_t)((const uint64_t *)data)[row]; hi = 0; break;
+    case P_I128: {
+      const int64_t *p = (const int64_t *)data + 2 * row;
+      lo = p[0];
+      hi = p[1];
+      break;
+    }
+    case P_F32: {
+      double d = ((const float *)data)[row];
+      lo = __double_as_longlong(d);
+      hi = 0;
+      break;
+    }
+    case P_F64: lo = ((const int64_t *)data)[row]; hi = 0; break;
+    default: lo = row; hi = 0; break;  // P_STR: the row index is the string code
+  }
+}
+
+__device__ __forceinline__ void store_phys(void *data, int phys, int64_t row, int64_t lo, int64_t hi) {
+  switch (phys) {
+    case P_U8: ((uint8_t *)data)[row] = (uint8_t)lo; break;
+    case P_I8: ((int8_t *)data)[row] = (int8_t)lo; break;
+    case P_I16: ((int16_t *)data)[row] = (int16_t)lo; break;
+    case P_U16: ((uint16_t *)data)[row] = (uint16_t)lo; break;
+    case P_I32: ((int32_t *)data)[row] = (int32_t)lo; break;
+    case P_U32: ((uint32_t *)data)[row] = (uint32_t)lo; break;
+    case P_I64: case P_U64: case P_F64: case P_STR: ((int64_t *)data)[row] = lo; break;
+    case P_I128: {
+      int64_t *p = (int64_t *)data + 2 * row;
+      p[0] = lo;
+      p[1] = hi;
+      break;
+    }
+    case P_F32: ((float *)data)[row] = (float)__longlong_as_double(lo); break;
+    default: break;
+  }
+}
+
+__device__ __forceinline__ i128 mk128(int64_t lo, int64_t hi) { return (i128)(((u128)(uint64_t)hi << 64) | (uint64_t)lo); }
+__device__ __forceinline__ void sp128(i128 v, int64_t &lo, int64_t &hi) {
+  lo = (int64_t)(uint64_t)(u128)v;
+  hi = (int64_t)(uint64_t)((u128)v >> 64);
+}
+
+__device__ __forceinline__ bool add_ovf128(i128 a, i128 b, i128 &r) {
+  r = (i128)((u128)a + (u128)b);
+  return ((a ^ r) & (b ^ r)) < 0;
+}
+__device__ __forceinline__ bool sub_ovf128(i128 a, i128 b, i128 &r) {
+  r = (i128)((u128)a - (u128)b);
+  return ((a ^ b) & (a ^ r)) < 0;
+}
+__device__ __forceinline__ bool mul_ovf128(i128 a, i128 b, i128 &r) {
+  bool neg = (a < 0) != (b < 0);
+  u128 ua = a < 0 ? (u128)0 - (u128)a : (u128)a;
+  u128 ub = b < 0 ? (u128)0 - (u128)b : (u128)b;
+  uint64_t ah = (uint64_t)(ua >> 64), al = (uint64_t)ua, bh = (uint64_t)(ub >> 64), bl = (uint64_t)ub;
+  if (ah && bh) return true;
+  u128 lo = (u128)al * bl;
+  u128 mid = (u128)ah * bl + (u128)al * bh;
+  if (mid >> 64) return true;
+  u128 res = lo + (mid << 64);
+  if (res < lo) return true;
+  u128 lim = neg ? ((u128)1 << 127) : (((u128)1 << 127) - 1);
+  if (res > lim) return true;
+  r = neg ? (i128)((u128)0 - res) : (i128)res;
+  return false;
+}
+__device__ __forceinline__ u128 udiv128(u128 n, u128 d) {
+  // shift-subtract division (rare path: HUGEINT / DECIMAL(>18) division)
+  if (d == 0) return 0;
+  if ((n >> 64) == 0 && (d >> 64) == 0) return (u128)((uint64_t)n / (uint64_t)d);
+  u128 q = 0, r = 0;
+  for (int i = 127; i >= 0; i--) {
+    r = (r << 1) | ((n >> i) & 1);
+    if (r >= d) {
+      r -= d;
+      q |= (u128)1 << i;
+    }
+  }
+  return q;
+}
+__device__ __forceinline__ i128 sdiv128(i128 a, i128 b) {
+  bool neg = (a < 0) != (b < 0);
+  u128 ua = a < 0 ? (u128)0 - (u128)a : (u128)a;
+  u128 ub = b < 0 ? (u128)0 - (u128)b : (u128)b;
+  u128 q = udiv128(ua, ub);
+  return neg ? (i128)((u128)0 - q) : (i128)q;
+}
+__device__ __forceinline__ i128 smod128(i128 a, i128 b) { return a - sdiv128(a, b) * b; }
+
+__device__ __forceinline__ i128 pow10_128(int k) {
+  i128 r = 1;
+  for (int i = 0; i < k; i++) r *= 10;
+  return r;
+}
+__device__ __forceinline__ int64_t pow10_64(int k) {
+  int64_t r = 1;
+  for (int i = 0; i < k; i++) r *= 10;
+  return r;
+}
+
+__device__ __forceinline__ double i128_to_double(i128 v) {
+  int64_t lo, hi;
+  sp128(v, lo, hi);
+  return (double)hi * 18446744073709551616.0 + (double)(uint64_t)lo;
+}
+
+__device__ __forceinline__ uint64_t splitmix64(uint64_t z) {
+  z += 0x9E3779B97F4A7C15ull;
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  return z ^ (z >> 31);
+}
+
+__device__ __forceinline__ void raise_err(int32_t *err, int32_t code) {
+  if (err) atomicCAS(err, 0, code);
+}
+
+__device__ __forceinline__ uint64_t f64_order(double d) {
+  uint64_t u = (uint64_t)__double_as_longlong(d);
+  if (d != d) return 0xFFFFFFFFFFFFFFFFull;  // NaN sorts last
+  return (u >> 63) ? ~u : (u | 0x8000000000000000ull);
+}
+__device__ __forceinline__ double f64_unorder(uint64_t k) {
+  uint64_t u = (k >> 63) ? (k & 0x7FFFFFFFFFFFFFFFull) : ~k;
+  return __longlong_as_double((long long)u);
+}
+
+// ---------------------------------------------------------------------------
+// expression VM (tile interpreter)
+// ---------------------------------------------------------------------------
+struct VmLds {
+  int64_t lo[VM_MAX_REGS][VM_TILE];
+  int64_t hi[VM_MAX_REGS][VM_TILE];
+  uint8_t nl[VM_MAX_REGS][VM_TILE];
+};
+
+__device__ __forceinline__ bool cmp_res(int c, int k) {
+  // c = -1/0/1 comparison, k = cmp kind
+  switch (k) {
+    case 0: return c == 0;
+    case 1: return c != 0;
+    case 2: return c < 0;
+    case 3: return c <= 0;
+    case 4: return c > 0;
+    default: return c >= 0;
+  }
+}
+
+__device__ void vm_exec(const VmProgram &P, const VmCols &C, int64_t row, bool active, int64_t rs, int64_t rstep,
+                        VmLds &R, int t, int32_t *err) {
+  for (int k = 0; k < P.n_ins; k++) {
+    const VmIns I = P.ins[k];
+    const int d = I.dst, a = I.a, b = I.b, c = I.c;
+    int64_t lo = 0, hi = 0;
+    uint8_t nl = 0;
+    switch (I.op) {
+      case V_LOADCOL: {
+        const VmCol &col = C.c[a];
+        if (active) {
+          nl = bit_valid(col.validity, row) ? 0 : 1;
+          load_phys(col.data, col.phys, row, lo, hi);
+        } else {
+          nl = 1;
+        }
+        break;
+      }
+      case V_LOADRANGE: lo = rs + row * rstep; hi = lo >> 63; break;
+      case V_CONST: lo = P.consts[a].lo; hi = P.consts[a].hi; nl = (uint8_t)P.consts[a].isnull; break;
+      case V_MOV: lo = R.lo[a][t]; hi = R.hi[a][t]; nl = R.nl[a][t]; break;
+      case V_SELECT: {
+        bool cond = !R.nl[a][t] && R.lo[a][t] != 0;
+        int s = cond ? b : c;
+        lo = R.lo[s][t]; hi = R.hi[s][t]; nl = R.nl[s][t];
+        break;
+      }
+      case V_COALESCE: {
+        int s = R.nl[a][t] ? b : a;
+        lo = R.lo[s][t]; hi = R.hi[s][t]; nl = R.nl[s][t];
+        break;
+      }
+      case V_AND: {
+        bool an = R.nl[a][t], bn = R.nl[b][t];
+        bool av = R.lo[a][t] != 0, bv = R.lo[b][t] != 0;
+        if ((!an && !av) || (!bn && !bv)) { lo = 0; nl = 0; }
+        else if (an || bn) { nl = 1; }
+        else { lo = 1; }
+        break;
+      }
+      case V_OR: {
+        bool an = R.nl[a][t], bn = R.nl[b][t];
+        bool av = R.lo[a][t] != 0, bv = R.lo[b][t] != 0;
+        if ((!an && av) || (!bn && bv)) { lo = 1; nl = 0; }
+        else if (an || bn) { nl = 1; }
+        else { lo = 0; }
+        break;
+      }
+      case V_ISNULL: lo = R.nl[a][t] ? 1 : 0; break;
+      case V_ISNOTNULL: lo = R.nl[a][t] ? 0 : 1; break;
+      case V_DISTINCT_I: case V_DISTINCT_L: case V_DISTINCT_F: {
+        bool an = R.nl[a][t], bn = R.nl[b][t];
+        bool same;
+        if (an || bn) same = an && bn;
+        else if (I.op == V_DISTINCT_F) {
+          double x = __longlong_as_double(R.lo[a][t]), y = __longlong_as_double(R.lo[b][t]);
+          same = (x == y) || (x != x && y != y);
+        } else same = R.lo[a][t] == R.lo[b][t] && R.hi[a][t] == R.hi[b][t];
+        lo = I.aux ? same : !same;
+        break;
+      }
+      case V_SYNTH: {
+        nl = R.nl[a][t] | R.nl[b][t] | R.nl[c][t];
+        uint64_t m = (uint64_t)R.lo[c][t];
+        if (!nl && m) {
+          lo = (int64_t)(splitmix64((uint64_t)R.lo[a][t] + (uint64_t)R.lo[b][t]) % m);
+        } else {
+          nl = 1;
+        }
+        break;
+      }
+      default: {
+        // null-propagating unary/binary ops
+        nl = R.nl[a][t];
+        if (I.op >= V_ADD_I && I.op != V_NOT && I.op != V_I2L && I.op != V_U2L && I.op != V_L2I && I.op != V_I2F &&
+            I.op != V_L2F && I.op != V_F2I && I.op != V_F2L && I.op != V_CHECK_I && I.op != V_CHECK_L &&
+            I.op != V_SCALEUP_I && I.op != V_SCALEUP_L && I.op != V_SCALEDN_I && I.op != V_SCALEDN_L &&
+            I.op != V_DEC2F_I && I.op != V_DEC2F_L && I.op != V_F2DEC_I && I.op != V_F2DEC_L &&
+            I.op != V_TOBOOL_I && I.op != V_TOBOOL_F && I.op != V_NEG_I && I.op != V_NEG_L && I.op != V_NEG_F &&
+            I.op != V_ABS_I && I.op != V_ABS_L && I.op != V_ABS_F)
+          nl |= R.nl[b][t];
+        const int64_t xa = R.lo[a][t], xah = R.hi[a][t];
+        const int64_t xb = R.lo[b][t], xbh = R.hi[b][t];
+        bool ok = active && !nl;
+        switch (I.op) {
+          case V_ADD_I: if (__builtin_add_overflow(xa, xb, &lo) && ok) raise_err(err, E_OVF_ADD); break;
+          case V_SUB_I: if (__builtin_sub_overflow(xa, xb, &lo) && ok) raise_err(err, E_OVF_SUB); break;
+          case V_MUL_I: if (__builtin_mul_overflow(xa, xb, &lo) && ok) raise_err(err, E_OVF_MUL); break;
+          case V_DIV_I:
+            if (xb == 0) nl = 1;
+            else if (xa == INT64_MIN && xb == -1) { if (ok) raise_err(err, E_OVF_MUL); }
+            else lo = xa / xb;
+            break;
+          case V_MOD_I:
+            if (xb == 0) nl = 1;
+            else if (xb == -1) lo = 0;
+            else lo = xa % xb;
+            break;
+          case V_NEG_I: if (__builtin_sub_overflow((int64_t)0, xa, &lo) && ok) raise_err(err, E_OVF_NEG); break;
+          case V_ABS_I:
+            if (xa == INT64_MIN && ok) raise_err(err, E_OVF_NEG);
+            lo = xa < 0 ? -xa : xa;
+            break;
+          case V_ADD_L: case V_SUB_L: case V_MUL_L: {
+            i128 r, x = mk128(xa, xah), y = mk128(xb, xbh);
+            bool o = I.op == V_ADD_L ? add_ovf128(x, y, r) : I.op == V_SUB_L ? sub_ovf128(x, y, r) : mul_ovf128(x, y, r);
+            if (o && ok) raise_err(err, I.op == V_ADD_L ? E_OVF_ADD : I.op == V_SUB_L ? E_OVF_SUB : E_OVF_MUL);
+            sp128(r, lo, hi);
+            break;
+          }
+          case V_DIV_L: case V_MOD_L: {
+            i128 x = mk128(xa, xah), y = mk128(xb, xbh);
+            if (y == 0) { nl = 1; break; }
+            i128 r = I.op == V_DIV_L ? sdiv128(x, y) : smod128(x, y);
+            sp128(r, lo, hi);
+            break;
+          }
+          case V_NEG_L: {
+            i128 r;
+            if (sub_ovf128((i128)0, mk128(xa, xah), r) && ok) raise_err(err, E_OVF_NEG);
+            sp128(r, lo, hi);
+            break;
+          }
+          case V_ABS_L: {
+            i128 x = mk128(xa, xah);
+            sp128(x < 0 ? -x : x, lo, hi);
+            break;
+          }
+          case V_ADD_F: case V_SUB_F: case V_MUL_F: case V_DIV_F: case V_MOD_F: case V_IDIV_F: {
+            double x = __longlong_as_double(xa), y = __longlong_as_double(xb), r = 0;
+            switch (I.op) {
+              case V_ADD_F: r = x + y; break;
+              case V_SUB_F: r = x - y; break;
+              case V_MUL_F: r = x * y; break;
+              case V_DIV_F: if (y == 0) nl = 1; else r = x / y; break;
+              case V_MOD_F: if (y == 0) nl = 1; else r = fmod(x, y); break;
+              default: if (y == 0) nl = 1; else r = trunc(x / y); break;
+            }
+            if (I.aux == 1) r = (double)(float)r;  // FLOAT result
+            lo = __double_as_longlong(r);
+            break;
+          }
+          case V_NEG_F: lo = __double_as_longlong(-__longlong_as_double(xa)); break;
+          case V_ABS_F: lo = __double_as_longlong(fabs(__longlong_as_double(xa))); break;
+          case V_CMP_I: lo = cmp_res(xa < xb ? -1 : xa > xb ? 1 : 0, I.aux); break;
+          case V_CMP_L: {
+            i128 x = mk128(xa, xah), y = mk128(xb, xbh);
+            lo = cmp_res(x < y ? -1 : x > y ? 1 : 0, I.aux);
+            break;
+          }
+          case V_CMP_F: {
+            double x = __longlong_as_double(xa), y = __longlong_as_double(xb);
+            bool nx = x != x, ny = y != y;
+            int cc = (nx || ny) ? (nx == ny ? 0 : (nx ? 1 : -1)) : (x < y ? -1 : x > y ? 1 : 0);
+            lo = cmp_res(cc, I.aux);
+            break;
+          }
+          case V_NOT: lo = xa == 0; break;
+          case V_TOBOOL_I: lo = (xa != 0 || xah != 0); break;
+          case V_TOBOOL_F: lo = __longlong_as_double(xa) != 0.0; break;
+          case V_I2L: lo = xa; hi = xa >> 63; break;
+          case V_U2L: lo = xa; hi = 0; break;
+          case V_L2I: {
+            i128 x = mk128(xa, xah);
+            i128 mn = b == 255 ? (i128)INT64_MIN : mk128(P.consts[b].lo, P.consts[b].hi);
+            i128 mx = c == 255 ? (i128)INT64_MAX : mk128(P.consts[c].lo, P.consts[c].hi);
+            if ((x < mn || x > mx) && ok) raise_err(err, E_CAST_RANGE);
+            lo = xa;
+            break;
+          }
+          case V_CHECK_I: {
+            if ((xa < P.consts[b].lo || xa > P.consts[c].lo) && ok) raise_err(err, E_CAST_RANGE);
+            lo = xa;
+            break;
+          }
+          case V_CHECK_L: {
+            i128 x = mk128(xa, xah);
+            if ((x < mk128(P.consts[b].lo, P.consts[b].hi) || x > mk128(P.consts[c].lo, P.consts[c].hi)) && ok)
+              raise_err(err, E_CAST_RANGE);
+            lo = xa;
+            hi = xah;
+            break;
+          }
+          case V_I2F: lo = __double_as_longlong((double)xa); break;
+          case V_L2F: lo = __double_as_longlong(i128_to_double(mk128(xa, xah))); break;
+          case V_F2I: case V_F2L: {
+            double x = rint(__longlong_as_double(xa));
+            bool bad = !(x >= -1.7014118346046923e38 && x < 1.7014118346046923e38);
+            i128 v = bad ? 0 : (i128)x;
+            i128 mn = mk128(P.consts[b].lo, P.consts[b].hi), mx = mk128(P.consts[c].lo, P.consts[c].hi);
+            if ((bad || v < mn || v > mx) && ok) raise_err(err, E_CAST_RANGE);
+            sp128(v, lo, hi);
+            break;
+          }
+          case V_SCALEUP_I: if (__builtin_mul_overflow(xa, pow10_64(I.aux), &lo) && ok) raise_err(err, E_DEC_OVF); break;
+          case V_SCALEUP_L: {
+            i128 r;
+            if (mul_ovf128(mk128(xa, xah), pow10_128(I.aux), r) && ok) raise_err(err, E_DEC_OVF);
+            sp128(r, lo, hi);
+            break;
+          }
+          case V_SCALEDN_I: {
+            int64_t p = pow10_64(I.aux), q = xa / p, r = xa % p;
+            int64_t ar = r < 0 ? -r : r;
+            if (2 * ar >= p) q += xa < 0 ? -1 : 1;
+            lo = q;
+            break;
+          }
+          case V_SCALEDN_L: {
+            i128 x = mk128(xa, xah), p = pow10_128(I.aux);
+            i128 q = sdiv128(x, p), r = x - q * p;
+            i128 ar = r < 0 ? -r : r;
+            if (2 * ar >= p) q += x < 0 ? -1 : 1;
+            sp128(q, lo, hi);
+            break;
+          }
+          case V_DEC2F_I: lo = __double_as_longlong((double)xa / (double)pow10_64(I.aux)); break;
+          case V_DEC2F_L: lo = __double_as_longlong(i128_to_double(mk128(xa, xah)) / (double)pow10_128(I.aux)); break;
+          case V_F2DEC_I: case V_F2DEC_L: {
+            double x = rint(__longlong_as_double(xa) * (double)pow10_128(I.aux));
+            bool bad = !(x >= -1.7014118346046923e38 && x < 1.7014118346046923e38);
+            i128 v = bad ? 0 : (i128)x;
+            i128 mn = mk128(P.consts[b].lo, P.consts[b].hi), mx = mk128(P.consts[c].lo, P.consts[c].hi);
+            if ((bad || v < mn || v > mx) && ok) raise_err(err, E_CAST_RANGE);
+            sp128(v, lo, hi);
+            break;
+          }
+          default: break;
+        }
+        break;
+      }
+    }
+    R.lo[d][t] = lo;
+    R.hi[d][t] = hi;
+    R.nl[d][t] = nl;
+  }
+}
+
+__global__ __launch_bounds__(256) void vm_filter_kernel(VmProgram P, VmCols C, int64_t nrows, int64_t rs,
+                                                        int64_t rstep, uint64_t *__restrict__ bits,
+                                                        uint32_t *__restrict__ tile_counts, int32_t *err) {
+  __shared__ VmLds R;
+  __shared__ uint32_t wcnt[4];
+  const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+  const int64_t ntiles = (nrows + VM_TILE - 1) / VM_TILE;
+  for (int64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+    int64_t row = tile * VM_TILE + t;
+    bool active = row < nrows;
+    vm_exec(P, C, row, active, rs, rstep, R, t, err);
+    const int pr = P.pred_reg;
+    bool sel = active && !R.nl[pr][t] && R.lo[pr][t] != 0;
+    uint64_t m = __ballot(sel);
+    if (lane == 0) {
+      bits[tile * 4 + w] = m;
+      wcnt[w] = (uint32_t)__popcll(m);
+    }
+    __syncthreads();
+    if (t == 0) tile_counts[tile] = wcnt[0] + wcnt[1] + wcnt[2] + wcnt[3];
+    __syncthreads();
+  }
+}
+
+__global__ __launch_bounds__(256) void vm_project_kernel(VmProgram P, VmCols C, int64_t nrows, int64_t rs,
+                                                         int64_t rstep, const uint64_t *__restrict__ bits,
+                                                         const int64_t *__restrict__ tile_off, VmOuts O,
+                                                         int32_t *err) {
+  __shared__ VmLds R;
+  const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+  const int64_t ntiles = (nrows + VM_TILE - 1) / VM_TILE;
+  for (int64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+    int64_t row = tile * VM_TILE + t;
+    bool sel;
+    int64_t out_idx;
+    if (bits) {
+      const uint64_t *tb = bits + tile * 4;
+      uint64_t b0 = tb[0], b1 = tb[1], b2 = tb[2], b3 = tb[3];
+      if ((b0 | b1 | b2 | b3) == 0) continue;  // uniform across the block
+      uint64_t mine = w == 0 ? b0 : w == 1 ? b1 : w == 2 ? b2 : b3;
+      int before = (w > 0 ? __popcll(b0) : 0) + (w > 1 ? __popcll(b1) : 0) + (w > 2 ? __popcll(b2) : 0);
+      sel = (mine >> lane) & 1ull;
+      uint64_t lt = lane ? (mine & ((1ull << lane) - 1ull)) : 0ull;
+      out_idx = tile_off[tile] + before + __popcll(lt);
+    } else {
+      sel = row < nrows;
+      out_idx = row;
+    }
+    vm_exec(P, C, row, sel, rs, rstep, R, t, err);
+    if (sel) {
+      for (int o = 0; o < P.n_out; o++) {
+        const int r = P.out_reg[o];
+        store_phys(O.data[o], P.out_phys[o], out_idx, R.lo[r][t], R.hi[r][t]);
+        if (O.valid[o]) {
+          if (!R.nl[r][t]) atomicOr(&O.valid[o][out_idx >> 5], 1u << (out_idx & 31));
+          else if (O.anynull) O.anynull[o] = 1;
+        }
+      }
+    }
+  }
+}
+
+void VmFilter(const VmProgram &p, const VmCols &cols, int64_t nrows, int64_t range_start, int64_t range_step,
+              uint64_t *sel_bits, uint32_t *tile_counts, int32_t *err, hipStream_t s) {
+  if (nrows <= 0) return;
+  int64_t ntiles = (nrows + VM_TILE - 1) / VM_TILE;
+  int grid = GridFor(ntiles, 1, NumCUs() * 8);
+  hipLaunchKernelGGL(vm_filter_kernel, dim3(grid), dim3(256), 0, s, p, cols, nrows, range_start, range_step, sel_bits,
+                     tile_counts, err);
+  CHECK_LAUNCH();
+}
+
+void VmProject(const VmProgram &p, const VmCols &cols, int64_t nrows, int64_t range_start, int64_t range_step,
+               const uint64_t *sel_bits, const int64_t *tile_offsets, const VmOuts &outs, int32_t *err,
+               hipStream_t s) {
+  if (nrows <= 0) return;
+  int64_t ntiles = (nrows + VM_TILE - 1) / VM_TILE;
+  int grid = GridFor(ntiles, 1, NumCUs() * 8);
+  hipLaunchKernelGGL(vm_project_kernel, dim3(grid), dim3(256), 0, s, p, cols, nrows, range_start, range_step,
+                     sel_bits, tile_offsets, outs, err);
+  CHECK_LAUNCH();
+}
+
+__global__ void scan_total_kernel(const uint32_t *counts, const int64_t *offsets, int64_t n, int64_t *total) {
+  *total = n ? offsets[n - 1] + (int64_t)counts[n - 1] : 0;
+}
+
+struct U32ToI64 {
+  __host__ __device__ int64_t operator()(uint32_t x) const { return (int64_t)x; }
+};
+
+void ScanTileCounts(const uint32_t *counts, int64_t *offsets, int64_t n, int64_t *total, hipStream_t s) {
+  if (n <= 0) {
+    (void)hipMemsetAsync(total, 0, sizeof(int64_t), s);
+    return;
+  }
+  hipcub::TransformInputIterator<int64_t, U32ToI64, const uint32_t *> it(counts, U32ToI64());
+  size_t tmp = 0;
+  (void)hipcub::DeviceScan::ExclusiveSum(nullptr, tmp, it, offsets, (int)n, s);
+  void *d_tmp = nullptr;
+  (void)hipMallocAsync(&d_tmp, tmp, s);
+  (void)hipcub::DeviceScan::ExclusiveSum(d_tmp, tmp, it, offsets, (int)n, s);
+  (void)hipFreeAsync(d_tmp, s);
+  hipLaunchKernelGGL(scan_total_kernel, dim3(1), dim3(1), 0, s, counts, offsets, n, total);
+}
+
+// ---------------------------------------------------------------------------
+// fused scan -> filter -> aggregate (configs C2 and C5)
+// ---------------------------------------------------------------------------
+// Per-thread accumulators: count, int128 sum (lo/hi with carry), min, max.
+struct Acc {
+  uint64_t cnt;
+  uint64_t slo;
+  int64_t shi;
+  int64_t mn, mx;
+};
+
+__device__ __forceinline__ void acc_add(Acc &A, bool ok, int64_t v) {
+  A.cnt += ok;
+  int64_t vv = ok ? v : 0;
+  uint64_t nlo = A.slo + (uint64_t)vv;
+  A.shi += (vv >> 63) + (nlo < A.slo ? 1 : 0);
+  A.slo = nlo;
+  A.mn = ok && v < A.mn ? v : A.mn;
+  A.mx = ok && v > A.mx ? v : A.mx;
+}
+
+__device__ __forceinline__ void acc_merge(Acc &A, const Acc &B) {
+  A.cnt += B.cnt;
+  uint64_t nlo = A.slo + B.slo;
+  A.shi += B.shi + (nlo < A.slo ? 1 : 0);
+  A.slo = nlo;
+  A.mn = B.mn < A.mn ? B.mn : A.mn;
+  A.mx = B.mx > A.mx ? B.mx : A.mx;
+}
+
+__device__ __forceinline__ uint64_t shfl_xor_u64(uint64_t v, int m) {
+  return (uint64_t)__shfl_xor((long long)v, m, 64);
+}
+
+__device__ __forceinline__ void acc_wave_reduce(Acc &A) {
+#pragma unroll
+  for (int m = 32; m >= 1; m >>= 1) {
+    Acc B;
+    B.cnt = shfl_xor_u64(A.cnt, m);
+    B.slo = shfl_xor_u64(A.slo, m);
+    B.shi = (int64_t)shfl_xor_u64((uint64_t)A.shi, m);
+    B.mn = (int64_t)shfl_xor_u64((uint64_t)A.mn, m);
+    B.mx = (int64_t)shfl_xor_u64((uint64_t)A.mx, m);
+    acc_merge(A, B);
+  }
+}
+
+__device__ __forceinline__ void agg_state_atomic(AggState *st, const Acc &A) {
+  atomicAdd(&st->count, (unsigned long long)A.cnt);
+  unsigned long long old = atomicAdd(&st->sum_lo, (unsigned long long)A.slo);
+  unsigned long long carry = (old + (unsigned long long)A.slo) < old ? 1ull : 0ull;
+  atomicAdd((unsigned long long *)&st->sum_hi, (unsigned long long)A.shi + carry);
+  atomicMin(&st->min_i, (long long)A.mn);
+  atomicMax(&st->max_i, (long long)A.mx);
+}
+
+// Block-level finish: wave shuffle reduction, LDS across the 4 waves, one
+// set of atomics per block.
+__device__ __forceinline__ void acc_block_commit(Acc &A, AggState *st, unsigned long long *cstar, bool count_is_star) {
+  __shared__ Acc part[4];
+  acc_wave_reduce(A);
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  if (lane == 0) part[w] = A;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    Acc T = part[0];
+    for (int i = 1; i < (int)(blockDim.x >> 6); i++) acc_merge(T, part[i]);
+    if (cstar) atomicAdd(cstar, (unsigned long long)T.cnt);
+    if (st) agg_state_atomic(st, T);
+  }
+  (void)count_is_star;
+}
+
+typedef long long v2i64 __attribute__((ext_vector_type(2)));
+typedef int v4i32 __attribute__((ext_vector_type(4)));
+template <typename T>
+struct Vec4;  // 4 consecutive elements through 16-byte loads
+template <>
+struct Vec4<int64_t> {
+  static __device__ __forceinline__ void load(const int64_t *__restrict__ p, int64_t g, int64_t v[4]) {
+    const v2i64 *q = (const v2i64 *)p + 2 * g;
+    v2i64 a = __builtin_nontemporal_load(q);
+    v2i64 b = __builtin_nontemporal_load(q + 1);
+    v[0] = a.x; v[1] = a.y; v[2] = b.x; v[3] = b.y;
+  }
+};
+template <>
+struct Vec4<int32_t> {
+  static __device__ __forceinline__ void load(const int32_t *__restrict__ p, int64_t g, int64_t v[4]) {
+    v4i32 a = __builtin_nontemporal_load((const v4i32 *)p + g);
+    v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w;
+  }
+};
+
+// MODE 0: aggregate over the predicate column; 1: over a second column;
+// 2: COUNT only.
+template <typename TP, typename TA, int MODE, int UNROLL>
+__global__ __launch_bounds__(256) void filter_agg_kernel(const TP *__restrict__ p, const TA *__restrict__ a, int64_t n,
+                                                         int64_t lo, uint64_t span, AggState *st,
+                                                         unsigned long long *cstar) {
+  Acc A;
+  A.cnt = 0; A.slo = 0; A.shi = 0; A.mn = INT64_MAX; A.mx = INT64_MIN;
+  Acc S = A;  // count_star accumulator when MODE == 1 (aggregate col differs)
+  const int64_t ngroups = n >> 2;  // groups of 4 elements
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  for (; g + (UNROLL - 1) * stride < ngroups; g += UNROLL * stride) {
+    int64_t pv[UNROLL][4], av[UNROLL][4];
+#pragma unroll
+    for (int u = 0; u < UNROLL; u++) {
+      Vec4<TP>::load(p, g + u * stride, pv[u]);
+      if (MODE == 1) Vec4<TA>::load(a, g + u * stride, av[u]);
+    }
+#pragma unroll
+    for (int u = 0; u < UNROLL; u++)
+#pragma unroll
+      for (int e = 0; e < 4; e++) {
+        int64_t x = pv[u][e];
+        bool ok = (uint64_t)(x - lo) <= span;
+        if (MODE == 1) acc_add(A, ok, av[u][e]);
+        else acc_add(A, ok, x);
+      }
+  }
+  for (; g < ngroups; g += stride) {
+    int64_t pv[4], av[4];
+    Vec4<TP>::load(p, g, pv);
+    if (MODE == 1) Vec4<TA>::load(a, g, av);
+#pragma unroll
+    for (int e = 0; e < 4; e++) {
+      bool ok = (uint64_t)(pv[e] - lo) <= span;
+      acc_add(A, ok, MODE == 1 ? av[e] : pv[e]);
+    }
+  }
+  // tail (n % 4 elements)
+  int64_t tail = (ngroups << 2) + (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (tail < n && tail < (ngroups << 2) + 4) {
+    int64_t x = p[tail];
+    bool ok = (uint64_t)(x - lo) <= span;
+    acc_add(A, ok, MODE == 1 ? (int64_t)a[tail] : x);
+  }
+  (void)S;
+  acc_block_commit(A, MODE == 2 ? nullptr : st, cstar, true);
+}
+
+__global__ void init_agg_states_kernel(AggState *st, int64_t n) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    AggState z;
+    z.count = 0; z.sum_lo = 0; z.sum_hi = 0;
+    z.min_i = INT64_MAX; z.max_i = INT64_MIN;
+    z.sum_f = 0; z.min_f = 0xFFFFFFFFFFFFFFFFull; z.max_f = 0;
+    st[i] = z;
+  }
+}
+
+void InitAggStates(AggState *st, int64_t n, hipStream_t s) {
+  if (n <= 0) return;
+  hipLaunchKernelGGL(init_agg_states_kernel, dim3(GridFor(n, 256, 1024)), dim3(256), 0, s, st, n);
+  CHECK_LAUNCH();
+}
+
+template <typename TP, typename TA, int MODE>
+static void LaunchFilterAgg(const void *p, const void *a, int64_t n, int64_t lo, uint64_t span, AggState *st,
+                            unsigned long long *cstar, int grid, hipStream_t s) {
+  hipLaunchKernelGGL((filter_agg_kernel<TP, TA, MODE, 4>), dim3(grid), dim3(256), 0, s, (const TP *)p, (const TA *)a,
+                     n, lo, span, st, cstar);
+  CHECK_LAUNCH();
+}
+
+// FilterAgg: exported with AggState output (count_star separately).
+void FilterAggStates(const void *pcol, int pphys, int64_t lo, int64_t hi, bool has_pred, const void *acol, int aphys,
+                     int64_t nrows, AggState *st, unsigned long long *cstar, int grid_blocks, hipStream_t s) {
+  if (nrows <= 0) return;
+  uint64_t span = has_pred ? (uint64_t)hi - (uint64_t)lo : ~0ull;
+  if (!has_pred) lo = INT64_MIN;
+  int grid = grid_blocks > 0 ? grid_blocks : NumCUs() * 8;
+  int mode = acol == nullptr ? 2 : (acol == pcol ? 0 : 1);
+  if (pphys == P_I64) {
+    if (mode == 0) LaunchFilterAgg<int64_t, int64_t, 0>(pcol, acol, nrows, lo, span, st, cstar, grid, s);
+    else if (mode == 2) LaunchFilterAgg<int64_t, int64_t, 2>(pcol, acol, nrows, lo, span, st, cstar, grid, s);
+    else if (aphys == P_I64) LaunchFilterAgg<int64_t, int64_t, 1>(pcol, acol, nrows, lo, span, st, cstar, grid, s);
+    else LaunchFilterAgg<int64_t, int32_t, 1>(pcol, acol, nrows, lo, span, st, cstar, grid, s);
+  } else {
+    if (mode == 0) LaunchFilterAgg<int32_t, int32_t, 0>(pcol, acol, nrows, lo, span, st, cstar, grid, s);
+    else if (mode == 2) LaunchFilterAgg<int32_t, int32_t, 2>(pcol, acol, nrows, lo, span, st, cstar, grid, s);
+    else if (aphys == P_I64) LaunchFilterAgg<int32_t, int64_t, 1>(pcol, acol, nrows, lo, span, st, cstar, grid, s);
+    else LaunchFilterAgg<int32_t, int32_t, 1>(pcol, acol, nrows, lo, span, st, cstar, grid, s);
+  }
+}
+
+// ---------------------------------------------------------------------------
+// fused GROUP BY on a small integer key range (config C3)
+// ---------------------------------------------------------------------------
+// LDS table with R replicas per key: replica = lane % R, so the 64 lanes of a
+// wave never hit the same address in one ds_add.  Partial sums are int64
+// (the host sizes seg_rows from the column statistics so they cannot
+// overflow) and are folded into int128 global slots at every segment flush.
+template <typename TK, typename TV, int NV, bool MM>
+__global__ __launch_bounds__(256) void group_direct_kernel(const TK *__restrict__ keys, const TV *__restrict__ v0,
+                                                           const TV *__restrict__ v1, int64_t n, int64_t kmin, int nk,
+                                                           int R, int64_t chunk, int64_t seg_rows,
+                                                           unsigned long long *cstar, AggState *st0, AggState *st1) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char lds_raw[];
+  const int nslot = nk * R;
+  unsigned int *cnt = (unsigned int *)lds_raw;
+  long long *sum0 = (long long *)(lds_raw + ((nslot * 4 + 15) & ~15));
+  long long *sum1 = sum0 + nslot;
+  long long *mn0 = sum0 + (NV >= 2 ? 2 : 1) * nslot;
+  long long *mx0 = mn0 + nslot;
+  long long *mn1 = mx0 + nslot;
+  long long *mx1 = mn1 + nslot;
+  const int t = threadIdx.x, lane = t & 63;
+  const int rep = lane % R;
+  auto zero = [&]() {
+    for (int i = t; i < nslot; i += blockDim.x) {
+      cnt[i] = 0;
+      if (NV >= 1) sum0[i] = 0;
+      if (NV >= 2) sum1[i] = 0;
+      if (MM) {
+        mn0[i] = INT64_MAX; mx0[i] = INT64_MIN;
+        if (NV >= 2) { mn1[i] = INT64_MAX; mx1[i] = INT64_MIN; }
+      }
+    }
+  };
+  auto flush = [&]() {
+    __syncthreads();
+    for (int k = t; k < nk; k += blockDim.x) {
+      unsigned long long c = 0;
+      i128 s0 = 0, s1 = 0;
+      long long a0 = INT64_MAX, b0 = INT64_MIN, a1 = INT64_MAX, b1 = INT64_MIN;
+      for (int r = 0; r < R; r++) {
+        int sl = k * R + r;
+        c += cnt[sl];
+        if (NV >= 1) s0 += (i128)sum0[sl];
+        if (NV >= 2) s1 += (i128)sum1[sl];
+        if (MM) {
+          a0 = mn0[sl] < a0 ? mn0[sl] : a0; b0 = mx0[sl] > b0 ? mx0[sl] : b0;
+          if (NV >= 2) { a1 = mn1[sl] < a1 ? mn1[sl] : a1; b1 = mx1[sl] > b1 ? mx1[sl] : b1; }
+        }
+      }
+      if (c) {
+        atomicAdd(&cstar[k], c);
+        Acc A;
+        A.cnt = c;
+        if (NV >= 1) {
+          int64_t lo, hi;
+          sp128(s0, lo, hi);
+          A.slo = (uint64_t)lo; A.shi = hi; A.mn = MM ? a0 : INT64_MAX; A.mx = MM ? b0 : INT64_MIN;
+          agg_state_atomic(&st0[k], A);
+        }
+        if (NV >= 2) {
+          int64_t lo, hi;
+          sp128(s1, lo, hi);
+          A.slo = (uint64_t)lo; A.shi = hi; A.mn = MM ? a1 : INT64_MAX; A.mx = MM ? b1 : INT64_MIN;
+          agg_state_atomic(&st1[k], A);
+        }
+      }
+    }
+    __syncthreads();
+    zero();
+    __syncthreads();
+  };
+  zero();
+  __syncthreads();
+  int64_t begin = (int64_t)blockIdx.x * chunk;
+  int64_t end = begin + chunk < n ? begin + chunk : n;
+  for (int64_t seg = begin; seg < end; seg += seg_rows) {
+    int64_t seg_end = seg + seg_rows < end ? seg + seg_rows : end;
+    // vectorised body: groups of 4 rows, chunk/seg boundaries are multiples of 4
+    int64_t g0 = seg >> 2, g1 = seg_end >> 2;
+    for (int64_t g = g0 + t; g < g1; g += blockDim.x) {
+      int64_t kv[4], x0[4], x1[4];
+      Vec4<TK>::load(keys, g, kv);
+      if (NV >= 1) Vec4<TV>::load(v0, g, x0);
+      if (NV >= 2) Vec4<TV>::load(v1, g, x1);
+#pragma unroll
+      for (int e = 0; e < 4; e++) {
+        int sl = (int)(kv[e] - kmin) * R + rep;
+        atomicAdd(&cnt[sl], 1u);
+        if (NV >= 1) atomicAdd((unsigned long long *)&sum0[sl], (unsigned long long)x0[e]);
+        if (NV >= 2) atomicAdd((unsigned long long *)&sum1[sl], (unsigned long long)x1[e]);
+        if (MM) {
+          atomicMin(&mn0[sl], (long long)x0[e]); atomicMax(&mx0[sl], (long long)x0[e]);
+          if (NV >= 2) { atomicMin(&mn1[sl], (long long)x1[e]); atomicMax(&mx1[sl], (long long)x1[e]); }
+        }
+      }
+    }
+    // scalar tail of the last segment (end not multiple of 4 only at n)
+    for (int64_t i = (g1 << 2) + t; i < seg_end; i += blockDim.x) {
+      int sl = (int)((int64_t)keys[i] - kmin) * R + rep;
+      atomicAdd(&cnt[sl], 1u);
+      if (NV >= 1) atomicAdd((unsigned long long *)&sum0[sl], (unsigned long long)(int64_t)v0[i]);
+      if (NV >= 2) atomicAdd((unsigned long long *)&sum1[sl], (unsigned long long)(int64_t)v1[i]);
+      if (MM) {
+        atomicMin(&mn0[sl], (long long)v0[i]); atomicMax(&mx0[sl], (long long)v0[i]);
+        if (NV >= 2) { atomicMin(&mn1[sl], (long long)v1[i]); atomicMax(&mx1[sl], (long long)v1[i]); }
+      }
+    }
+    flush();
+  }
+}
+
+template <typename TK, typename TV, int NV, bool MM>
+static void LaunchGroupDirect(const void *k, const void *v0, const void *v1, int64_t n, int64_t kmin, int nk, int R,
+                              int64_t chunk, int64_t seg, unsigned long long *cstar, AggState *s0, AggState *s1,
+                              int grid, size_t lds, hipStream_t s) {
+  hipLaunchKernelGGL((group_direct_kernel<TK, TV, NV, MM>), dim3(grid), dim3(256), lds, s, (const TK *)k,
+                     (const TV *)v0, (const TV *)v1, n, kmin, nk, R, chunk, seg, cstar, s0, s1);
+  CHECK_LAUNCH();
+}
+
+size_t GroupDirectLds(int nk, int R, int nv, bool mm) {
+  size_t nslot = (size_t)nk * R;
+  size_t b = (nslot * 4 + 15) & ~(size_t)15;
+  b += nslot * 8 * (size_t)(nv >= 2 ? 2 : 1);
+  if (mm) b += nslot * 8 * 2 * (size_t)(nv >= 2 ? 2 : 1);
+  return b;
+}
+
+void GroupByDirectStates(const void *kcol, int kphys, int64_t kmin, int nk, const void *v0, const void *v1, int vphys,
+                         int nv, bool mm, int64_t nrows, int64_t seg_rows, int R, unsigned long long *cstar,
+                         AggState *st0, AggState *st1, int grid_blocks, hipStream_t s) {
+  if (nrows <= 0) return;
+  int grid = grid_blocks > 0 ? grid_blocks : NumCUs() * 4;
+  int64_t chunk = (nrows + grid - 1) / grid;
+  chunk = (chunk + 3) & ~(int64_t)3;
+  grid = (int)((nrows + chunk - 1) / chunk);
+  if (seg_rows <= 0 || seg_rows > chunk) seg_rows = chunk;
+  seg_rows = (seg_rows + 3) & ~(int64_t)3;
+  size_t lds = GroupDirectLds(nk, R, nv, mm);
+#define GD(TK, TV, NV, MM) LaunchGroupDirect<TK, TV, NV, MM>(kcol, v0, v1, nrows, kmin, nk, R, chunk, seg_rows, cstar, st0, st1, grid, lds, s)
+#define GDV(TK, TV)                         \
+  if (nv == 0) GD(TK, TV, 0, false);        \
+  else if (nv == 1) { if (mm) GD(TK, TV, 1, true); else GD(TK, TV, 1, false); } \
+  else { if (mm) GD(TK, TV, 2, true); else GD(TK, TV, 2, false); }
+  if (kphys == P_I32) {
+    if (vphys == P_I64) { GDV(int32_t, int64_t) } else { GDV(int32_t, int32_t) }
+  } else {
+    if (vphys == P_I64) { GDV(int64_t, int64_t) } else { GDV(int64_t, int32_t) }
+  }
+#undef GDV
+#undef GD
+}
+
+// ---------------------------------------------------------------------------
+// generic aggregation over compacted columns
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void reduce_column_kernel(const void *col, int phys, const uint64_t *valid, int64_t n,
+                                                            AggState *st) {
+  Acc A;
+  A.cnt = 0; A.slo = 0; A.shi = 0; A.mn = INT64_MAX; A.mx = INT64_MIN;
+  double sf = 0;
+  uint64_t fmn = ~0ull, fmx = 0;
+  const bool isf = phys == P_F64 || phys == P_F32;
+  const bool is128 = phys == P_I128 || phys == P_U64;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    if (!bit_valid(valid, i)) continue;
+    int64_t lo, hi;
+    load_phys(col, phys, i, lo, hi);
+    if (isf) {
+      double d = __longlong_as_double(lo);
+      A.cnt++;
+      sf += d;
+      uint64_t k = f64_order(d);
+      fmn = k < fmn ? k : fmn;
+      fmx = k > fmx ? k : fmx;
+    } else if (is128) {
+      A.cnt++;
+      uint64_t nlo = A.slo + (uint64_t)lo;
+      A.shi += hi + (nlo < A.slo ? 1 : 0);
+      A.slo = nlo;
+    } else {
+      acc_add(A, true, lo);
+    }
+  }
+  // floats: reduce separately
+  __shared__ double sfs[4];
+  __shared__ unsigned long long fmns[4], fmxs[4];
+#pragma unroll
+  for (int m = 32; m >= 1; m >>= 1) {
+    sf += __shfl_xor(sf, m, 64);
+    uint64_t o = shfl_xor_u64(fmn, m);
+    fmn = o < fmn ? o : fmn;
+    o = shfl_xor_u64(fmx, m);
+    fmx = o > fmx ? o : fmx;
+  }
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  if (lane == 0) {
+    sfs[w] = sf;
+    fmns[w] = fmn;
+    fmxs[w] = fmx;
+  }
+  acc_block_commit(A, st, nullptr, false);
+  if (threadIdx.x == 0 && isf) {
+    double s = 0;
+    unsigned long long a = ~0ull, b = 0;
+    for (int i = 0; i < (int)(blockDim.x >> 6); i++) {
+      s += sfs[i];
+      a = fmns[i] < a ? fmns[i] : a;
+      b = fmxs[i] > b ? fmxs[i] : b;
+    }
+    atomicAdd(&st->sum_f, s);
+    atomicMin(&st->min_f, a);
+    atomicMax(&st->max_f, b);
+  }
+}
+
+void ReduceColumn(const void *col, int phys, const uint64_t *valid, int64_t n, AggState *out, hipStream_t s) {
+  if (n <= 0) return;
+  hipLaunchKernelGGL(reduce_column_kernel, dim3(GridFor(n, 256 * 16, NumCUs() * 4)), dim3(256), 0, s, col, phys, valid,
+                     n, out);
+  CHECK_LAUNCH();
+}
+
+__global__ void key_range_kernel(const void *col, int phys, const uint64_t *valid, int64_t n, long long *out3) {
+  long long mn = INT64_MAX, mx = INT64_MIN, c = 0;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    if (!bit_valid(valid, i)) continue;
+    int64_t lo, hi;
+    load_phys(col, phys, i, lo, hi);
+    mn = lo < mn ? lo : mn;
+    mx = lo > mx ? lo : mx;
+    c++;
+  }
+#pragma unroll
+  for (int m = 32; m >= 1; m >>= 1) {
+    long long o = __shfl_xor(mn, m, 64);
+    mn = o < mn ? o : mn;
+    o = __shfl_xor(mx, m, 64);
+    mx = o > mx ? o : mx;
+    c += __shfl_xor(c, m, 64);
+  }
+  if ((threadIdx.x & 63) == 0) {
+    atomicMin(&out3[0], mn);
+    atomicMax(&out3[1], mx);
+    atomicAdd((unsigned long long *)&out3[2], (unsigned long long)c);
+  }
+}
+
+__global__ void init3_kernel(long long *o) {
+  o[0] = INT64_MAX;
+  o[1] = INT64_MIN;
+  o[2] = 0;
+}
+
+void KeyRange(const void *col, int phys, const uint64_t *valid, int64_t n, long long *out3, hipStream_t s) {
+  hipLaunchKernelGGL(init3_kernel, dim3(1), dim3(1), 0, s, out3);
+  if (n > 0)
+    hipLaunchKernelGGL(key_range_kernel, dim3(GridFor(n, 256 * 16, NumCUs() * 4)), dim3(256), 0, s, col, phys, valid,
+                       n, out3);
+  CHECK_LAUNCH();
+}
+
+void ColumnStats(const void *col, int phys, const uint64_t *valid, int64_t n, long long *out3, hipStream_t s) {
+  KeyRange(col, phys, valid, n, out3, s);
+}
+
+__global__ void group_assign_kernel(const void *kcol, int kphys, const uint64_t *kvalid, int64_t kmin, int64_t nslots,
+                                    int64_t n, int32_t *slot_of_row, unsigned long long *count_star) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    int32_t sl;
+    if (!bit_valid(kvalid, i)) sl = (int32_t)(nslots - 1);
+    else {
+      int64_t lo, hi;
+      load_phys(kcol, kphys, i, lo, hi);
+      sl = (int32_t)(lo - kmin);
+    }
+    slot_of_row[i] = sl;
+    atomicAdd(&count_star[sl], 1ull);
+  }
+}
+
+void GroupAssign(const void *kcol, int kphys, const uint64_t *kvalid, int64_t kmin, int64_t nslots, int64_t n,
+                 int32_t *slot_of_row, unsigned long long *count_star, hipStream_t s) {
+  if (n <= 0) return;
+  hipLaunchKernelGGL(group_assign_kernel, dim3(GridFor(n, 256 * 8, NumCUs() * 8)), dim3(256), 0, s, kcol, kphys,
+                     kvalid, kmin, nslots, n, slot_of_row, count_star);
+  CHECK_LAUNCH();
+}
+
+__global__ void group_reduce_kernel(const int32_t *slot_of_row, const void *col, int phys, const uint64_t *valid,
+                                    int64_t n, AggState *states) {
+  const bool isf = phys == P_F64 || phys == P_F32;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    if (!bit_valid(valid, i)) continue;
+    AggState *st = &states[slot_of_row[i]];
+    int64_t lo, hi;
+    load_phys(col, phys, i, lo, hi);
+    atomicAdd(&st->count, 1ull);
+    if (isf) {
+      double d = __longlong_as_double(lo);
+      atomicAdd(&st->sum_f, d);
+      uint64_t k = f64_order(d);
+      atomicMin(&st->min_f, (unsigned long long)k);
+      atomicMax(&st->max_f, (unsigned long long)k);
+    } else {
+      unsigned long long old = atomicAdd(&st->sum_lo, (unsigned long long)lo);
+      unsigned long long carry = (old + (unsigned long long)lo) < old ? 1ull : 0ull;
+      atomicAdd((unsigned long long *)&st->sum_hi, (unsigned long long)hi + carry);
+      if (phys != P_I128) {
+        atomicMin(&st->min_i, (long long)lo);
+        atomicMax(&st->max_i, (long long)lo);
+      }
+    }
+  }
+}
+
+void GroupReduceColumn(const int32_t *slot_of_row, const void *col, int phys, const uint64_t *valid, int64_t n,
+                       AggState *states, hipStream_t s) {
+  if (n <= 0) return;
+  hipLaunchKernelGGL(group_reduce_kernel, dim3(GridFor(n, 256 * 8, NumCUs() * 8)), dim3(256), 0, s, slot_of_row, col,
+                     phys, valid, n, states);
+  CHECK_LAUNCH();
+}
+
+__global__ __launch_bounds__(1024) void compact_slots_kernel(const unsigned long long *count_star, int64_t nslots,
+                                                             int32_t *slot_list, int64_t *n_out) {
+  __shared__ int wsum[16];
+  __shared__ long long base;
+  if (threadIdx.x == 0) base = 0;
+  __syncthreads();
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  for (int64_t off = 0; off < nslots; off += blockDim.x) {
+    int64_t i = off + threadIdx.x;
+    bool f = i < nslots && count_star[i] > 0;
+    uint64_t m = __ballot(f);
+    if (lane == 0) wsum[w] = __popcll(m);
+    __syncthreads();
+    int before = 0;
+    for (int k = 0; k < w; k++) before += wsum[k];
+    int total = 0;
+    for (int k = 0; k < (int)(blockDim.x >> 6); k++) total += wsum[k];
+    uint64_t lt = lane ? (m & ((1ull << lane) - 1ull)) : 0ull;
+    if (f) slot_list[base + before + __popcll(lt)] = (int32_t)i;
+    __syncthreads();
+    if (threadIdx.x == 0) base += total;
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) *n_out = base;
+}
+
+void CompactSlots(const unsigned long long *count_star, int64_t nslots, int32_t *slot_list, int64_t *n_out,
+                  hipStream_t s) {
+  hipLaunchKernelGGL(compact_slots_kernel, dim3(1), dim3(1024), 0, s, count_star, nslots, slot_list, n_out);
+  CHECK_LAUNCH();
+}
+
+// ---------------------------------------------------------------------------
+// sort / gather
+// ---------------------------------------------------------------------------
+__global__ void sort_key_kernel(const void *col, int phys, const uint64_t *valid, int64_t n, const int64_t *perm,
+                                bool desc, bool nulls_first, uint64_t *keys) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    int64_t r = perm ? perm[i] : i;
+    uint64_t k;
+    if (!bit_valid(valid, r)) {
+      k = nulls_first ? 0ull : ~0ull;
+    } else {
+      int64_t lo, hi;
+      load_phys(col, phys, r, lo, hi);
+      if (phys == P_F64 || phys == P_F32) k = f64_order(__longlong_as_double(lo));
+      else if (phys == P_U8 || phys == P_U16 || phys == P_U32 || phys == P_U64) k = (uint64_t)lo;
+      else k = (uint64_t)lo ^ 0x8000000000000000ull;
+      if (desc) k = ~k;
+      // keep NULLs at the requested end: squeeze valid keys into [1, 2^64-2]
+      if (k == 0ull) k = 1ull;
+      if (k == ~0ull) k = ~1ull;
+    }
+    keys[i] = k;
+  }
+}
+
+void SortKeyU64(const void *col, int phys, const uint64_t *valid, int64_t n, const int64_t *perm, bool desc,
+                bool nulls_first, uint64_t *keys, hipStream_t s) {
+  if (n <= 0) return;
+  hipLaunchKernelGGL(sort_key_kernel, dim3(GridFor(n, 256 * 4, NumCUs() * 8)), dim3(256), 0, s, col, phys, valid, n,
+                     perm, desc, nulls_first, keys);
+  CHECK_LAUNCH();
+}
+
+void SortPairs(uint64_t *keys_in, int64_t *vals_in, uint64_t *keys_out, int64_t *vals_out, int64_t n, hipStream_t s) {
+  if (n <= 0) return;
+  size_t tmp = 0;
+  (void)hipcub::DeviceRadixSort::SortPairs(nullptr, tmp, keys_in, keys_out, vals_in, vals_out, (int)n, 0, 64, s);
+  void *d_tmp = nullptr;
+  (void)hipMallocAsync(&d_tmp, tmp, s);
+  (void)hipcub::DeviceRadixSort::SortPairs(d_tmp, tmp, keys_in, keys_out, vals_in, vals_out, (int)n, 0, 64, s);
+  (void)hipFreeAsync(d_tmp, s);
+}
+
+__global__ void iota_kernel(int64_t *p, int64_t n, int64_t start) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+    p[i] = start + i;
+}
+
+void Iota(int64_t *p, int64_t n, int64_t start, hipStream_t s) {
+  if (n <= 0) return;
+  hipLaunchKernelGGL(iota_kernel, dim3(GridFor(n, 256 * 4, NumCUs() * 8)), dim3(256), 0, s, p, n, start);
+  CHECK_LAUNCH();
+}
+
+__global__ void gather_fixed_kernel(const void *in, int phys, const uint64_t *in_valid, const int64_t *idx, int64_t n,
+                                    void *out, uint32_t *out_valid) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    int64_t r = idx[i];
+    int64_t lo, hi;
+    load_phys(in, phys, r, lo, hi);
+    if (phys == P_F32) {  // keep exact float bits
+      ((float *)out)[i] = ((const float *)in)[r];
+    } else if (phys == P_INTERVAL) {
+      ((int64_t *)out)[2 * i] = ((const int64_t *)in)[2 * r];
+      ((int64_t *)out)[2 * i + 1] = ((const int64_t *)in)[2 * r + 1];
+    } else {
+      store_phys(out, phys, i, lo, hi);
+    }
+    if (out_valid && bit_valid(in_valid, r)) atomicOr(&out_valid[i >> 5], 1u << (i & 31));
+  }
+}
+
+void GatherFixed(const void *in, int phys, const uint64_t *in_valid, const int64_t *idx, int64_t n, void *out,
+                 uint32_t *out_valid, hipStream_t s) {
+  if (n <= 0) return;
+  hipLaunchKernelGGL(gather_fixed_kernel, dim3(GridFor(n, 256 * 4, NumCUs() * 8)), dim3(256), 0, s, in, phys, in_valid,
+                     idx, n, out, out_valid);
+  CHECK_LAUNCH();
+}
+
+__global__ void gather_slots_kernel(const unsigned char *in, int eb, const int32_t *idx, int64_t n, unsigned char *out) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    const unsigned char *src = in + (int64_t)idx[i] * eb;
+    unsigned char *dst = out + i * eb;
+    for (int k = 0; k < eb; k++) dst[k] = src[k];
+  }
+}
+
+void GatherSlots(const void *in, int elem_bytes, const int32_t *idx, int64_t n, void *out, hipStream_t s) {
+  if (n <= 0) return;
+  hipLaunchKernelGGL(gather_slots_kernel, dim3(GridFor(n, 256, 1024)), dim3(256), 0, s, (const unsigned char *)in,
+                     elem_bytes, idx, n, (unsigned char *)out);
+  CHECK_LAUNCH();
+}
+
+// ---------------------------------------------------------------------------
+// strings
+// ---------------------------------------------------------------------------
+__global__ void str_len_kernel(const int64_t *codes, const uint64_t *valid, int64_t n, const int64_t *src_off,
+                               const int64_t *pool_off, int64_t *lens) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    int64_t c = codes[i];
+    int64_t L = 0;
+    if (bit_valid(valid, i)) {
+      if (c >= 0) L = src_off[c + 1] - src_off[c];
+      else L = pool_off[-c] - pool_off[-c - 1];
+    }
+    lens[i] = L;
+  }
+}
+
+void StringLengths(const int64_t *codes, const uint64_t *valid, int64_t n, const int64_t *src_off,
+                   const int64_t *pool_off, int64_t *lens, hipStream_t s) {
+  if (n <= 0) return;
+  hipLaunchKernelGGL(str_len_kernel, dim3(GridFor(n, 256 * 4, NumCUs() * 8)), dim3(256), 0, s, codes, valid, n, src_off,
+                     pool_off, lens);
+  CHECK_LAUNCH();
+}
+
+void ScanLengths(const int64_t *lens, int64_t *offsets, int64_t n, hipStream_t s) {
+  // offsets[0] = 0, offsets[i+1] = inclusive sum
+  (void)hipMemsetAsync(offsets, 0, sizeof(int64_t), s);
+  if (n <= 0) return;
+  size_t tmp = 0;
+  (void)hipcub::DeviceScan::InclusiveSum(nullptr, tmp, lens, offsets + 1, (int)n, s);
+  void *d_tmp = nullptr;
+  (void)hipMallocAsync(&d_tmp, tmp, s);
+  (void)hipcub::DeviceScan::InclusiveSum(d_tmp, tmp, lens, offsets + 1, (int)n, s);
+  (void)hipFreeAsync(d_tmp, s);
+}
+
+__global__ void str_copy_kernel(const int64_t *codes, const uint64_t *valid, int64_t n, const int64_t *src_off,
+                                const char *src_chars, const int64_t *pool_off, const char *pool_chars,
+                                const int64_t *out_off, char *out_chars) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    if (!bit_valid(valid, i)) continue;
+    int64_t c = codes[i];
+    const char *src;
+    int64_t L;
+    if (c >= 0) {
+      src = src_chars + src_off[c];
+      L = src_off[c + 1] - src_off[c];
+    } else {
+      src = pool_chars + pool_off[-c - 1];
+      L = pool_off[-c] - pool_off[-c - 1];
+    }
+    char *dst = out_chars + out_off[i];
+    for (int64_t k = 0; k < L; k++) dst[k] = src[k];
+  }
+}
+
+void StringCopy(const int64_t *codes, const uint64_t *valid, int64_t n, const int64_t *src_off, const char *src_chars,
+                const int64_t *pool_off, const char *pool_chars, const int64_t *out_off, char *out_chars,
+                hipStream_t s) {
+  if (n <= 0) return;
+  hipLaunchKernelGGL(str_copy_kernel, dim3(GridFor(n, 256 * 4, NumCUs() * 8)), dim3(256), 0, s, codes, valid, n,
+                     src_off, src_chars, pool_off, pool_chars, out_off, out_chars);
+  CHECK_LAUNCH();
+}
+
+// ---------------------------------------------------------------------------
+// ingest helpers
+// ---------------------------------------------------------------------------
+template <typename T>
+__global__ void synth_kernel(T *out, int64_t n, uint64_t seed, int64_t start, uint64_t m, int64_t add) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+    out[i] = (T)((int64_t)(splitmix64(seed + (uint64_t)(start + i)) % m) + add);
+}
+
+void Synth(void *out, int phys, int64_t n, int64_t seed, int64_t start, int64_t m, int64_t add, hipStream_t s) {
+  if (n <= 0) return;
+  int grid = GridFor(n, 256 * 8, NumCUs() * 8);
+  if (phys == P_I32)
+    hipLaunchKernelGGL(synth_kernel<int32_t>, dim3(grid), dim3(256), 0, s, (int32_t *)out, n, (uint64_t)seed, start,
+                       (uint64_t)m, add);
+  else
+    hipLaunchKernelGGL(synth_kernel<int64_t>, dim3(grid), dim3(256), 0, s, (int64_t *)out, n, (uint64_t)seed, start,
+                       (uint64_t)m, add);
+  CHECK_LAUNCH();
+}
+
+__global__ void bitmap_append_kernel(uint64_t *dst, int64_t dst_off, const uint64_t *src, int64_t n) {
+  // one thread per destination word touched
+  int64_t first = dst_off >> 6, last = (dst_off + n - 1) >> 6;
+  for (int64_t wi = first + (int64_t)blockIdx.x * blockDim.x + threadIdx.x; wi <= last;
+       wi += (int64_t)gridDim.x * blockDim.x) {
+    uint64_t word = 0;
+    int64_t b0 = wi << 6;
+    for (int k = 0; k < 64; k++) {
+      int64_t db = b0 + k;
+      if (db < dst_off || db >= dst_off + n) {
+        word |= dst[wi] & (1ull << k);
+        continue;
+      }
+      int64_t sb = db - dst_off;
+      uint64_t bit = src ? ((src[sb >> 6] >> (sb & 63)) & 1ull) : 1ull;
+      word |= bit << k;
+    }
+    dst[wi] = word;
+  }
+}
+
+void BitmapAppend(uint64_t *dst, int64_t dst_off, const uint64_t *src, int64_t n, hipStream_t s) {
+  if (n <= 0) return;
+  int64_t words = ((dst_off + n - 1) >> 6) - (dst_off >> 6) + 1;
+  hipLaunchKernelGGL(bitmap_append_kernel, dim3(GridFor(words, 256, 4096)), dim3(256), 0, s, dst, dst_off, src, n);
+  CHECK_LAUNCH();
+}
+
+__global__ __launch_bounds__(256) void copy_kernel(const float4 *__restrict__ in, float4 *__restrict__ out, int64_t n) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+    out[i] = in[i];
+}
+
+void CopyKernel(const void *in, void *out, int64_t nbytes, hipStream_t s) {
+  int64_t n = nbytes / 16;
+  hipLaunchKernelGGL(copy_kernel, dim3(NumCUs() * 8), dim3(256), 0, s, (const float4 *)in, (float4 *)out, n);
+  CHECK_LAUNCH();
+}
+
+}  // namespace dev
+}  // namespace mbx
+
+namespace mbx {
+namespace dev {
+
+// Writes the aggregate relation [key?, agg0, agg1, ...] from per-slot states.
+__global__ void emit_agg_kernel(EmitDesc D) {
+  const int64_t n = D.slot_list ? *D.n_list : D.nslots;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t sl = D.slot_list ? D.slot_list[i] : i;
+    if (D.has_key) {
+      if (sl == D.null_slot) {
+        store_phys(D.key_out, D.key_phys, i, 0, 0);
+      } else {
+        int64_t k = D.kmin + sl;
+        store_phys(D.key_out, D.key_phys, i, k, k >> 63);
+        atomicOr(&D.key_valid[i >> 5], 1u << (i & 31));
+      }
+    }
+    for (int j = 0; j < D.nagg; j++) {
+      const EmitAgg &A = D.a[j];
+      bool valid = true;
+      int64_t lo = 0, hi = 0;
+      if (A.kind == 0 /*COUNT_STAR*/) {
+        lo = (int64_t)D.cstar[sl];
+      } else {
+        const AggState &S = A.states[sl];
+        switch (A.kind) {
+          case 1: /*COUNT*/ lo = (int64_t)S.count; break;
+          case 2: /*SUM*/
+            if (!S.count) { valid = false; break; }
+            if (A.in_class == VC_F64) lo = __double_as_longlong(S.sum_f);
+            else { lo = (int64_t)S.sum_lo; hi = S.sum_hi; }
+            break;
+          case 3: /*MIN*/
+          case 4: /*MAX*/
+            if (!S.count) { valid = false; break; }
+            if (A.in_class == VC_F64) lo = __double_as_longlong(f64_unorder(A.kind == 3 ? S.min_f : S.max_f));
+            else { lo = A.kind == 3 ? S.min_i : S.max_i; hi = lo >> 63; }
+            break;
+          default: /*AVG*/ {
+            if (!S.count) { valid = false; break; }
+            double v;
+            if (A.in_class == VC_F64) v = S.sum_f / (double)S.count;
+            else {
+              double sum = (double)S.sum_hi * 18446744073709551616.0 + (double)S.sum_lo;
+              double div = (double)S.count;
+              for (int k = 0; k < A.avg_scale; k++) div *= 10.0;
+              v = sum / div;
+            }
+            lo = __double_as_longlong(v);
+            break;
+          }
+        }
+      }
+      if (valid) {
+        store_phys(A.out, A.out_phys, i, lo, hi);
+        atomicOr(&A.valid[i >> 5], 1u << (i & 31));
+      } else {
+        store_phys(A.out, A.out_phys, i, 0, 0);
+      }
+    }
+  }
+}
+
+void EmitAggRelation(const EmitDesc &d, hipStream_t s) {
+  hipLaunchKernelGGL(emit_agg_kernel, dim3(GridFor(d.nslots, 256, 1024)), dim3(256), 0, s, d);
+  CHECK_LAUNCH();
+}
+
+__global__ void rebase_kernel(const int64_t *src, int64_t *dst, int64_t n, int64_t delta) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+    dst[i] = src[i] + delta;
+}
+
+void RebaseOffsets(const int64_t *src, int64_t *dst, int64_t n, int64_t delta, hipStream_t s) {
+  if (n <= 0) return;
+  hipLaunchKernelGGL(rebase_kernel, dim3(GridFor(n, 256 * 4, 4096)), dim3(256), 0, s, src, dst, n, delta);
+  CHECK_LAUNCH();
+}
+
+}  // namespace dev
+}  // namespace mbx

@@ -1,0 +1,946 @@
+// shim.cpp — the 89 duckdb_mb_* C-ABI entry points (include/duckdb_mb.h).
+//
+// Same names, parameter types, ownership and error conventions as the
+// reference shim /root/reference/src/duckdb_native.c (each function cites the
+// definition it replaces).  Instead of forwarding to libduckdb, statements go
+// to the MI355X engine (engine.cpp / executor.cpp / kernels.hip).
+//
+// Deliberate differences (documented in DESIGN.md):
+//  * the last-error string is thread_local (reference: process-global static,
+//    duckdb_native.c:22-40) — identical for the single-threaded MoonBit caller;
+//  * duckdb_mb_query_arrow does not read freed memory on error
+//    (reference use-after-free at duckdb_native.c:2258-2260);
+//  * arrow buffer sizes are computed in 64 bits and refused above INT32_MAX
+//    (reference int32 overflow at duckdb_native.c:2404).
+#include <hip/hip_runtime_api.h>
+
+#include <cmath>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <string>
+
+#include "../../include/duckdb_mb.h"
+#include "engine.h"
+
+using namespace mbx;
+
+// ---------------------------------------------------------------------------
+// MoonBit byte objects.  Layout of the MoonBit runtime (moonbit.h): an 8-byte
+// header {int32 rc; uint32 meta} precedes the payload and the array length is
+// the low 28 bits of meta (Moonbit_array_length).  Inside a MoonBit program
+// the runtime's strong moonbit_make_bytes_raw wins over this weak one.
+// ---------------------------------------------------------------------------
+namespace {
+struct MbHeader {
+  int32_t rc;
+  uint32_t meta;
+};
+inline int32_t MbLen(const uint8_t *b) {
+  if (!b) return 0;
+  return (int32_t)(((const MbHeader *)b - 1)->meta & ((1u << 28) - 1));
+}
+}  // namespace
+
+extern "C" __attribute__((weak)) moonbit_bytes_t moonbit_make_bytes_raw(int32_t len) {
+  if (len < 0) len = 0;
+  MbHeader *h = (MbHeader *)calloc(1, sizeof(MbHeader) + (size_t)len + 1);
+  if (!h) return nullptr;
+  h->rc = 1;
+  h->meta = (uint32_t)len & ((1u << 28) - 1);
+  return (moonbit_bytes_t)(h + 1);
+}
+
+extern "C" moonbit_bytes_t duckdb_mbx_bytes_new(const uint8_t *data, int32_t len) {
+  moonbit_bytes_t b = moonbit_make_bytes_raw(len);
+  if (b && len > 0 && data) memcpy(b, data, (size_t)len);
+  return b;
+}
+extern "C" int32_t duckdb_mbx_bytes_len(moonbit_bytes_t b) { return MbLen(b); }
+extern "C" void duckdb_mbx_bytes_free(moonbit_bytes_t b) {
+  if (b) free((MbHeader *)b - 1);
+}
+
+static moonbit_bytes_t MakeBytes(const char *data, size_t len) {
+  moonbit_bytes_t b = moonbit_make_bytes_raw((int32_t)len);
+  if (b && len && data) memcpy(b, data, len);
+  return b;
+}
+static moonbit_bytes_t MakeBytes(const std::string &s) { return MakeBytes(s.data(), s.size()); }
+static std::string BytesStr(moonbit_bytes_t b) {
+  if (!b) return std::string();
+  return std::string((const char *)b, (size_t)MbLen(b));
+}
+
+// ---------------------------------------------------------------------------
+// handles
+// ---------------------------------------------------------------------------
+struct duckdb_mb_connection {
+  Connection conn;
+};
+struct duckdb_mb_result {
+  ResultPtr r;
+};
+struct duckdb_mb_stream {
+  ResultPtr r;
+  int64_t pos = 0;
+};
+struct duckdb_mb_chunk {
+  ResultPtr r;
+  int64_t start = 0, n = 0;
+  duckdb_mb_stream *stream = nullptr;
+};
+struct duckdb_mb_config {
+  Options opts;
+  char error[256];
+};
+struct duckdb_mb_statement {
+  duckdb_mb_connection *conn = nullptr;
+  Statement st;
+  std::vector<Value> params;
+  char error[256];
+};
+struct duckdb_mb_appender {
+  duckdb_mb_connection *conn = nullptr;
+  TablePtr table;
+  HostBatch batch;
+  std::vector<Value> row;
+  size_t col = 0;
+  char error[256];
+  // columnar bulk ingest
+  std::vector<const void *> raw_vals;
+  std::vector<const uint8_t *> raw_valid;
+  std::vector<int64_t> raw_count;
+};
+struct duckdb_mb_arrow_result {
+  ResultPtr r;
+  char error[256];
+  int32_t column_count = 0, row_count = 0;
+};
+
+static thread_local std::string g_last_error;
+static thread_local bool g_has_error = false;
+
+static void SetError(const char *m) {
+  if (!m) {
+    g_last_error.clear();
+    g_has_error = false;
+    return;
+  }
+  g_last_error = m;
+  g_has_error = true;
+}
+static void SetError(const std::string &m) { SetError(m.c_str()); }
+static void CopyErr(char *dst, const std::string &m) {
+  strncpy(dst, m.c_str(), 255);
+  dst[255] = '\0';
+}
+
+extern "C" {
+
+// ---- connection -------------------------------------------------------------
+static duckdb_mb_connection *OpenConn(moonbit_bytes_t path, const Options &opts) {
+  try {
+    auto *h = new duckdb_mb_connection();
+    h->conn.opts = opts;
+    h->conn.engine = CreateEngine(opts.device, opts.allow_no_gpu);
+    h->conn.catalog.device = opts.device;
+    (void)path;  // ":memory:" and file paths both open a volatile device-resident database
+    return h;
+  } catch (std::exception &e) {
+    SetError(e.what());
+    return nullptr;
+  }
+}
+
+duckdb_mb_connection *duckdb_mb_connect(moonbit_bytes_t path) {  // ref duckdb_native.c:67-131
+  Options o;
+  return OpenConn(path, o);
+}
+
+void duckdb_mb_disconnect(duckdb_mb_connection *h) {  // ref :133-140
+  delete h;
+}
+
+int32_t duckdb_mb_is_null_conn(duckdb_mb_connection *h) { return h == nullptr ? 1 : 0; }  // ref :248
+
+moonbit_bytes_t duckdb_mb_last_error(void) {  // ref :240-246
+  if (!g_has_error) return moonbit_make_bytes_raw(0);
+  return MakeBytes(g_last_error);
+}
+
+// ---- materialized query --------------------------------------------------
+duckdb_mb_result *duckdb_mb_query(duckdb_mb_connection *h, moonbit_bytes_t sql) {  // ref :142-172
+  if (!h) {
+    SetError("connection is null");
+    return nullptr;
+  }
+  try {
+    ResultPtr r = RunStatement(h->conn, BytesStr(sql), {}, nullptr);
+    auto *res = new duckdb_mb_result();
+    res->r = r;
+    return res;
+  } catch (std::exception &e) {
+    SetError(e.what());
+    return nullptr;
+  }
+}
+
+void duckdb_mb_result_destroy(duckdb_mb_result *r) { delete r; }  // ref :174-180
+
+int32_t duckdb_mb_result_column_count(duckdb_mb_result *r) {  // ref :182-187
+  return r ? (int32_t)r->r->cols.size() : 0;
+}
+int32_t duckdb_mb_result_row_count(duckdb_mb_result *r) {  // ref :189-194
+  return r ? (int32_t)r->r->nrows : 0;
+}
+moonbit_bytes_t duckdb_mb_result_column_name(duckdb_mb_result *r, int32_t col) {  // ref :196-206
+  if (!r || col < 0 || col >= (int32_t)r->r->cols.size()) return moonbit_make_bytes_raw(0);
+  return MakeBytes(r->r->cols[col].name);
+}
+int32_t duckdb_mb_result_column_type(duckdb_mb_result *r, int32_t col) {  // ref :208-213
+  if (!r || col < 0 || col >= (int32_t)r->r->cols.size()) return T_INVALID;
+  return r->r->cols[col].type.id;
+}
+static bool InRange(const ResultPtr &r, int32_t col, int64_t row) {
+  return col >= 0 && col < (int32_t)r->cols.size() && row >= 0 && row < r->nrows;
+}
+int32_t duckdb_mb_result_is_null(duckdb_mb_result *r, int32_t col, int32_t row) {  // ref :215-222
+  if (!r || !InRange(r->r, col, row)) return 1;
+  return r->r->cols[col].IsNull(row) ? 1 : 0;
+}
+moonbit_bytes_t duckdb_mb_result_value(duckdb_mb_result *r, int32_t col, int32_t row) {  // ref :224-238
+  if (!r || !InRange(r->r, col, row)) return moonbit_make_bytes_raw(0);
+  const HostColumn &c = r->r->cols[col];
+  if (c.IsNull(row)) return moonbit_make_bytes_raw(0);
+  return MakeBytes(FormatValue(c.Get(row)));
+}
+int32_t duckdb_mb_is_null_result(duckdb_mb_result *r) { return r == nullptr ? 1 : 0; }  // ref :252
+
+// ---- streaming --------------------------------------------------------------
+// Whitelist of streamable types, reference duckdb_native.c:271-303.
+static bool StreamSupported(TypeId t) {
+  switch (t) {
+    case T_BOOLEAN: case T_TINYINT: case T_SMALLINT: case T_INTEGER: case T_BIGINT: case T_UTINYINT:
+    case T_USMALLINT: case T_UINTEGER: case T_UBIGINT: case T_FLOAT: case T_DOUBLE: case T_VARCHAR: case T_BLOB:
+    case T_DATE: case T_TIME: case T_TIMESTAMP: case T_INTERVAL: case T_HUGEINT:
+      return true;
+    default:
+      return false;
+  }
+}
+
+static duckdb_mb_stream *StreamFrom(ResultPtr r) {  // ref :320-353
+  for (auto &c : r->cols)
+    if (!StreamSupported(c.type.id)) {
+      SetError("streaming query has unsupported column type");
+      return nullptr;
+    }
+  auto *s = new duckdb_mb_stream();
+  s->r = r;
+  return s;
+}
+
+duckdb_mb_stream *duckdb_mb_query_stream(duckdb_mb_connection *h, moonbit_bytes_t sql) {  // ref :355-397
+  if (!h) {
+    SetError("connection is null");
+    return nullptr;
+  }
+  try {
+    return StreamFrom(RunStatement(h->conn, BytesStr(sql), {}, nullptr));
+  } catch (std::exception &e) {
+    SetError(e.what());
+    return nullptr;
+  }
+}
+
+void duckdb_mb_stream_destroy(duckdb_mb_stream *s) { delete s; }  // ref :426-438
+int32_t duckdb_mb_is_null_stream(duckdb_mb_stream *s) { return s == nullptr ? 1 : 0; }  // ref :440
+int32_t duckdb_mb_stream_column_count(duckdb_mb_stream *s) {  // ref :444-449
+  return s ? (int32_t)s->r->cols.size() : 0;
+}
+moonbit_bytes_t duckdb_mb_stream_column_name(duckdb_mb_stream *s, int32_t col) {  // ref :451-464
+  if (!s || col < 0 || col >= (int32_t)s->r->cols.size()) return moonbit_make_bytes_raw(0);
+  return MakeBytes(s->r->cols[col].name);
+}
+
+// DuckDB's standard vector size: result chunks carry at most 2048 rows.
+static const int64_t kVectorSize = 2048;
+
+duckdb_mb_chunk *duckdb_mb_stream_fetch_chunk(duckdb_mb_stream *s) {  // ref :466-490
+  if (!s) {
+    SetError("stream is null");
+    return nullptr;
+  }
+  if (s->pos >= s->r->nrows) {
+    SetError(nullptr);  // end of stream: NULL chunk with an empty error
+    return nullptr;
+  }
+  auto *c = new duckdb_mb_chunk();
+  c->r = s->r;
+  c->start = s->pos;
+  c->n = std::min(kVectorSize, s->r->nrows - s->pos);
+  c->stream = s;
+  s->pos += c->n;
+  return c;
+}
+
+void duckdb_mb_chunk_destroy(duckdb_mb_chunk *c) { delete c; }  // ref :492-500
+int32_t duckdb_mb_is_null_chunk(duckdb_mb_chunk *c) { return c == nullptr ? 1 : 0; }  // ref :502
+int32_t duckdb_mb_chunk_row_count(duckdb_mb_chunk *c) { return c ? (int32_t)c->n : 0; }  // ref :506-511
+int32_t duckdb_mb_chunk_column_count(duckdb_mb_chunk *c) {  // ref :513-518
+  return c ? (int32_t)c->r->cols.size() : 0;
+}
+int32_t duckdb_mb_chunk_is_null(duckdb_mb_chunk *c, int32_t col, int32_t row) {  // ref :520-535
+  if (!c || col < 0 || col >= (int32_t)c->r->cols.size() || row < 0 || row >= c->n) return 1;
+  return c->r->cols[col].IsNull(c->start + row) ? 1 : 0;
+}
+moonbit_bytes_t duckdb_mb_chunk_value(duckdb_mb_chunk *c, int32_t col, int32_t row) {  // ref :537-667
+  if (!c || col < 0 || col >= (int32_t)c->r->cols.size() || row < 0 || row >= c->n) return moonbit_make_bytes_raw(0);
+  const HostColumn &hc = c->r->cols[col];
+  if (hc.IsNull(c->start + row)) return moonbit_make_bytes_raw(0);
+  return MakeBytes(FormatValue(hc.Get(c->start + row)));
+}
+
+// ---- configuration -----------------------------------------------------------
+duckdb_mb_config *duckdb_mb_config_create(void) {  // ref :678-695
+  auto *c = new duckdb_mb_config();
+  c->error[0] = '\0';
+  return c;
+}
+void duckdb_mb_config_destroy(duckdb_mb_config *c) { delete c; }  // ref :697-705
+moonbit_bytes_t duckdb_mb_config_error(duckdb_mb_config *c) {  // ref :707-712
+  if (!c) return MakeBytes("", 0);
+  return MakeBytes(c->error, strlen(c->error));
+}
+
+static bool IsInt(const std::string &v, long long *out) {
+  char *end = nullptr;
+  long long x = strtoll(v.c_str(), &end, 10);
+  if (v.empty() || *end) return false;
+  *out = x;
+  return true;
+}
+
+int32_t duckdb_mb_config_set(duckdb_mb_config *c, moonbit_bytes_t key, moonbit_bytes_t value) {  // ref :714-747
+  if (!c) return 0;
+  std::string k = BytesStr(key), v = BytesStr(value);
+  std::string kl = k;
+  for (auto &ch : kl) ch = (char)tolower((unsigned char)ch);
+  long long x;
+  bool ok = true;
+  if (kl == "gpu_device") {
+    ok = IsInt(v, &x) && x >= 0;
+    if (ok) c->opts.device = (int)x;
+  } else if (kl == "mbx_profile") {
+    c->opts.profile = v == "true" || v == "1";
+  } else if (kl == "mbx_allow_no_gpu") {
+    c->opts.allow_no_gpu = v == "true" || v == "1";
+  } else if (kl == "mbx_appender_flush_rows") {
+    ok = IsInt(v, &x) && x > 0;
+    if (ok) c->opts.appender_flush_rows = x;
+  } else if (kl == "threads" || kl == "worker_threads") {
+    ok = IsInt(v, &x) && x > 0;
+    if (ok) c->opts.threads = (int)x;
+  } else if (kl == "access_mode") {
+    std::string vl = v;
+    for (auto &ch : vl) ch = (char)tolower((unsigned char)ch);
+    ok = vl == "automatic" || vl == "read_only" || vl == "read_write";
+  } else if (kl == "memory_limit" || kl == "max_memory" || kl == "default_order" || kl == "default_null_order" ||
+             kl == "enable_external_access" || kl == "allow_unsigned_extensions" || kl == "temp_directory" ||
+             kl == "preserve_insertion_order" || kl == "enable_object_cache" || kl == "max_temp_directory_size" ||
+             kl == "enable_progress_bar" || kl == "autoload_known_extensions" || kl == "autoinstall_known_extensions") {
+    ok = true;
+  } else {
+    ok = false;
+  }
+  if (!ok) {
+    CopyErr(c->error, "duckdb_set_config failed");
+    return 0;
+  }
+  c->opts.raw[kl] = v;
+  return 1;
+}
+
+duckdb_mb_connection *duckdb_mb_connect_with_config(moonbit_bytes_t path, duckdb_mb_config *c) {  // ref :749-806
+  if (!c) {
+    SetError("config is null");
+    return nullptr;
+  }
+  return OpenConn(path, c->opts);
+}
+
+// ---- prepared statements -------------------------------------------------------
+duckdb_mb_statement *duckdb_mb_prepare(duckdb_mb_connection *h, moonbit_bytes_t sql) {  // ref :816-854
+  if (!h) return nullptr;
+  try {
+    auto *s = new duckdb_mb_statement();
+    s->conn = h;
+    s->st = ParseSQL(BytesStr(sql));
+    s->params.assign(s->st.n_params, Value());  // type INVALID = unbound
+    s->error[0] = '\0';
+    return s;
+  } catch (std::exception &e) {
+    SetError(e.what());
+    return nullptr;
+  }
+}
+
+void duckdb_mb_statement_destroy(duckdb_mb_statement *s) { delete s; }  // ref :856-864
+moonbit_bytes_t duckdb_mb_statement_error(duckdb_mb_statement *s) {  // ref :866-871
+  if (!s) return MakeBytes("", 0);
+  return MakeBytes(s->error, strlen(s->error));
+}
+
+static int32_t Bind(duckdb_mb_statement *s, int32_t index, const Value &v) {
+  if (!s) return 0;
+  if (index < 1 || index > (int32_t)s->params.size()) {
+    CopyErr(s->error, "Can not bind to parameter number " + std::to_string(index) + ", statement only has " +
+                          std::to_string(s->params.size()) + " parameter(s)");
+    return 0;
+  }
+  s->params[index - 1] = v;
+  return 1;
+}
+
+int32_t duckdb_mb_bind_int(duckdb_mb_statement *s, int32_t i, int32_t v) { return Bind(s, i, Value::Int(T_INTEGER, v)); }  // ref :873
+int32_t duckdb_mb_bind_bigint(duckdb_mb_statement *s, int32_t i, int64_t v) { return Bind(s, i, Value::Int(T_BIGINT, v)); }  // ref :890
+int32_t duckdb_mb_bind_double(duckdb_mb_statement *s, int32_t i, double v) { return Bind(s, i, Value::Double(v)); }  // ref :907
+int32_t duckdb_mb_bind_varchar(duckdb_mb_statement *s, int32_t i, moonbit_bytes_t v) {  // ref :924
+  return Bind(s, i, Value::Varchar(BytesStr(v)));
+}
+int32_t duckdb_mb_bind_bool(duckdb_mb_statement *s, int32_t i, bool v) { return Bind(s, i, Value::Bool(v)); }  // ref :950
+int32_t duckdb_mb_bind_null(duckdb_mb_statement *s, int32_t i) {  // ref :967
+  return Bind(s, i, Value::Null(LogicalType(T_SQLNULL)));
+}
+int32_t duckdb_mb_clear_bindings(duckdb_mb_statement *s) {  // ref :983-989
+  if (!s) return 0;
+  for (auto &p : s->params) p = Value();
+  return 1;
+}
+
+duckdb_mb_result *duckdb_mb_execute_prepared(duckdb_mb_statement *s) {  // ref :991-1016
+  if (!s) {
+    SetError("statement is null");
+    return nullptr;
+  }
+  try {
+    ResultPtr r = RunParsed(s->conn->conn, s->st, s->params);
+    auto *res = new duckdb_mb_result();
+    res->r = r;
+    return res;
+  } catch (std::exception &e) {
+    SetError(e.what());
+    return nullptr;
+  }
+}
+
+duckdb_mb_stream *duckdb_mb_execute_prepared_stream(duckdb_mb_statement *s) {  // ref :399-424
+  if (!s) {
+    SetError("statement is null");
+    return nullptr;
+  }
+  try {
+    return StreamFrom(RunParsed(s->conn->conn, s->st, s->params));
+  } catch (std::exception &e) {
+    SetError(e.what());
+    return nullptr;
+  }
+}
+
+int32_t duckdb_mb_is_null_statement(duckdb_mb_statement *s) { return s == nullptr ? 1 : 0; }  // ref :1018
+
+int32_t duckdb_mb_bind_date(duckdb_mb_statement *s, int32_t i, int32_t days) {  // ref :1261
+  return Bind(s, i, Value::Int(T_DATE, days));
+}
+int32_t duckdb_mb_bind_timestamp(duckdb_mb_statement *s, int32_t i, int64_t micros) {  // ref :1279
+  return Bind(s, i, Value::Int(T_TIMESTAMP, micros));
+}
+int32_t duckdb_mb_bind_blob(duckdb_mb_statement *s, int32_t i, moonbit_bytes_t data, int32_t length) {  // ref :1377
+  Value v = Value::Varchar(std::string((const char *)data, data ? (size_t)std::max(length, 0) : 0));
+  v.type = LogicalType(T_BLOB);
+  return Bind(s, i, v);
+}
+static i128 HugeFromParts(int64_t lower, int64_t upper) {
+  return (i128)(((u128)(uint64_t)upper << 64) | (uint64_t)lower);
+}
+int32_t duckdb_mb_bind_decimal(duckdb_mb_statement *s, int32_t i, uint8_t width, uint8_t scale, int64_t lower,
+                               int64_t upper) {  // ref :1421-1445
+  if (width < 1 || width > 38 || scale > width) {
+    if (s) CopyErr(s->error, "Invalid Input Error: invalid decimal width/scale");
+    return 0;
+  }
+  return Bind(s, i, Value::Decimal(width, scale, HugeFromParts(lower, upper)));
+}
+int32_t duckdb_mb_bind_interval(duckdb_mb_statement *s, int32_t i, int32_t months, int32_t days, int64_t micros) {  // ref :1487
+  Value v;
+  v.type = LogicalType(T_INTERVAL);
+  v.is_null = false;
+  v.iv.months = months;
+  v.iv.days = days;
+  v.iv.micros = micros;
+  return Bind(s, i, v);
+}
+static int32_t Unsupported(char *err, const char *what) {
+  if (err) CopyErr(err, std::string("Not implemented Error: ") + what + " is not supported by the MI355X backend");
+  return 0;
+}
+int32_t duckdb_mb_bind_list_varchar(duckdb_mb_statement *s, int32_t, moonbit_bytes_t *, int32_t) {  // ref :1539
+  return Unsupported(s ? s->error : nullptr, "LIST parameters");
+}
+int32_t duckdb_mb_bind_struct_varchar(duckdb_mb_statement *s, int32_t, moonbit_bytes_t *, moonbit_bytes_t *, int32_t) {  // ref :1597
+  return Unsupported(s ? s->error : nullptr, "STRUCT parameters");
+}
+int32_t duckdb_mb_bind_map_varchar_varchar(duckdb_mb_statement *s, int32_t, moonbit_bytes_t *, moonbit_bytes_t *, int32_t) {  // ref :1666
+  return Unsupported(s ? s->error : nullptr, "MAP parameters");
+}
+
+// ---- appender ----------------------------------------------------------------
+duckdb_mb_appender *duckdb_mb_appender_create(duckdb_mb_connection *h, moonbit_bytes_t schema, moonbit_bytes_t table) {  // ref :1032-1081
+  if (!h) return nullptr;
+  std::string sc = BytesStr(schema), tn = BytesStr(table);
+  TablePtr t = h->conn.catalog.Find(tn);
+  if (!t || (!sc.empty() && sc != "main")) {
+    SetError("Catalog Error: Table \"" + (sc.empty() ? std::string("main") : sc) + "." + tn + "\" could not be found");
+    return nullptr;
+  }
+  auto *a = new duckdb_mb_appender();
+  a->conn = h;
+  a->table = t;
+  a->error[0] = '\0';
+  for (auto &c : t->cols) {
+    HostColumn hc;
+    hc.type = c.type;
+    hc.phys = c.phys;
+    if (hc.phys == P_STR) hc.offsets.push_back(0);
+    a->batch.cols.push_back(hc);
+  }
+  return a;
+}
+
+static bool FlushAppender(duckdb_mb_appender *a) {
+  if (a->batch.nrows == 0) return true;
+  try {
+    AppendHostBatch(a->conn->conn, *a->table, a->batch);
+  } catch (std::exception &e) {
+    CopyErr(a->error, e.what());
+    return false;
+  }
+  for (auto &hc : a->batch.cols) {
+    hc.data.clear();
+    hc.valid.clear();
+    hc.chars.clear();
+    hc.offsets.clear();
+    if (hc.phys == P_STR) hc.offsets.push_back(0);
+  }
+  a->batch.nrows = 0;
+  return true;
+}
+
+void duckdb_mb_appender_destroy(duckdb_mb_appender *a) {  // ref :1083-1091 (destroy flushes)
+  if (!a) return;
+  FlushAppender(a);
+  delete a;
+}
+moonbit_bytes_t duckdb_mb_appender_error(duckdb_mb_appender *a) {  // ref :1093-1098
+  if (!a) return MakeBytes("", 0);
+  return MakeBytes(a->error, strlen(a->error));
+}
+int32_t duckdb_mb_begin_row(duckdb_mb_appender *a) {  // ref :1100-1114
+  if (!a) return 0;
+  return 1;
+}
+
+static int32_t AppendValue(duckdb_mb_appender *a, const Value &v) {
+  if (!a) return 0;
+  if (a->col >= a->table->cols.size()) {
+    CopyErr(a->error, "Too many appends for chunk!");
+    return 0;
+  }
+  try {
+    a->row.push_back(CastValue(v, a->table->cols[a->col].type));
+  } catch (std::exception &e) {
+    CopyErr(a->error, e.what());
+    return 0;
+  }
+  a->col++;
+  return 1;
+}
+
+int32_t duckdb_mb_append_int(duckdb_mb_appender *a, int32_t v) { return AppendValue(a, Value::Int(T_INTEGER, v)); }  // ref :1116
+int32_t duckdb_mb_append_bigint(duckdb_mb_appender *a, int64_t v) { return AppendValue(a, Value::Int(T_BIGINT, v)); }  // ref :1132
+int32_t duckdb_mb_append_double(duckdb_mb_appender *a, double v) { return AppendValue(a, Value::Double(v)); }  // ref :1148
+int32_t duckdb_mb_append_varchar(duckdb_mb_appender *a, moonbit_bytes_t v) {  // ref :1164
+  return AppendValue(a, Value::Varchar(BytesStr(v)));
+}
+int32_t duckdb_mb_append_bool(duckdb_mb_appender *a, bool v) { return AppendValue(a, Value::Bool(v)); }  // ref :1189
+int32_t duckdb_mb_append_null(duckdb_mb_appender *a) {  // ref :1205
+  if (!a) return 0;
+  if (a->col >= a->table->cols.size()) {
+    CopyErr(a->error, "Too many appends for chunk!");
+    return 0;
+  }
+  a->row.push_back(Value::Null(a->table->cols[a->col].type));
+  a->col++;
+  return 1;
+}
+int32_t duckdb_mb_end_row(duckdb_mb_appender *a) {  // ref :1221-1235
+  if (!a) return 0;
+  if (a->col != a->table->cols.size()) {
+    CopyErr(a->error, "Call to EndRow before all columns have been appended to!");
+    return 0;
+  }
+  for (size_t i = 0; i < a->row.size(); i++) HostColumnPush(a->batch.cols[i], a->row[i]);
+  a->batch.nrows++;
+  a->row.clear();
+  a->col = 0;
+  if (a->batch.nrows >= a->conn->conn.opts.appender_flush_rows) return FlushAppender(a) ? 1 : 0;
+  return 1;
+}
+int32_t duckdb_mb_flush(duckdb_mb_appender *a) {  // ref :1237-1251
+  if (!a) return 0;
+  if (a->col != 0) {
+    CopyErr(a->error, "Failed to flush appender: Incomplete append to row!");
+    return 0;
+  }
+  return FlushAppender(a) ? 1 : 0;
+}
+int32_t duckdb_mb_is_null_appender(duckdb_mb_appender *a) { return a == nullptr ? 1 : 0; }  // ref :1253
+
+int32_t duckdb_mb_append_date(duckdb_mb_appender *a, int32_t days) {  // ref :1313 (reference appends an approximate
+  return AppendValue(a, Value::Int(T_DATE, days));  // "YYYY-MM-DD" string; here the exact DATE)
+}
+int32_t duckdb_mb_append_timestamp(duckdb_mb_appender *a, int64_t micros) {  // ref :1350
+  return AppendValue(a, Value::Int(T_TIMESTAMP, micros));
+}
+int32_t duckdb_mb_append_blob(duckdb_mb_appender *a, moonbit_bytes_t data, int32_t length) {  // ref :1397
+  Value v = Value::Varchar(std::string((const char *)data, data ? (size_t)std::max(length, 0) : 0));
+  v.type = LogicalType(T_BLOB);
+  return AppendValue(a, v);
+}
+int32_t duckdb_mb_append_decimal(duckdb_mb_appender *a, uint8_t width, uint8_t scale, int64_t lower,
+                                 int64_t upper) {  // ref :1447-1481
+  if (width < 1 || width > 38 || scale > width) {
+    if (a) CopyErr(a->error, "failed to create decimal value");
+    return 0;
+  }
+  return AppendValue(a, Value::Decimal(width, scale, HugeFromParts(lower, upper)));
+}
+int32_t duckdb_mb_append_interval(duckdb_mb_appender *a, int32_t months, int32_t days, int64_t micros) {  // ref :1511
+  Value v;
+  v.type = LogicalType(T_INTERVAL);
+  v.is_null = false;
+  v.iv.months = months;
+  v.iv.days = days;
+  v.iv.micros = micros;
+  return AppendValue(a, v);
+}
+int32_t duckdb_mb_append_list_varchar(duckdb_mb_appender *a, moonbit_bytes_t *, int32_t) {  // ref :1735
+  return Unsupported(a ? a->error : nullptr, "LIST values");
+}
+int32_t duckdb_mb_append_struct_varchar(duckdb_mb_appender *a, moonbit_bytes_t *, moonbit_bytes_t *, int32_t) {  // ref :1792
+  return Unsupported(a ? a->error : nullptr, "STRUCT values");
+}
+int32_t duckdb_mb_append_map_varchar_varchar(duckdb_mb_appender *a, moonbit_bytes_t *, moonbit_bytes_t *, int32_t) {  // ref :1860
+  return Unsupported(a ? a->error : nullptr, "MAP values");
+}
+
+// ---- columnar bulk ingest (extension) ---------------------------------------------
+int32_t duckdb_mbx_append_column(duckdb_mb_appender *a, int32_t col, const void *values, const uint8_t *validity,
+                                 int64_t count) {
+  if (!a) return 0;
+  size_t nc = a->table->cols.size();
+  if (col < 0 || (size_t)col >= nc) {
+    CopyErr(a->error, "append_column: column index out of range");
+    return 0;
+  }
+  if (a->table->cols[col].phys == P_STR || a->table->cols[col].phys == P_INTERVAL) {
+    CopyErr(a->error, "append_column: only fixed-width columns are supported");
+    return 0;
+  }
+  if (a->raw_vals.size() != nc) {
+    a->raw_vals.assign(nc, nullptr);
+    a->raw_valid.assign(nc, nullptr);
+    a->raw_count.assign(nc, -1);
+  }
+  a->raw_vals[col] = values;
+  a->raw_valid[col] = validity;
+  a->raw_count[col] = count;
+  return 1;
+}
+
+int32_t duckdb_mbx_append_commit(duckdb_mb_appender *a, int64_t count) {
+  if (!a) return 0;
+  size_t nc = a->table->cols.size();
+  if (a->raw_vals.size() != nc) {
+    CopyErr(a->error, "append_commit: no columns staged");
+    return 0;
+  }
+  for (size_t i = 0; i < nc; i++)
+    if (a->raw_count[i] != count || !a->raw_vals[i]) {
+      CopyErr(a->error, "append_commit: every column must be staged with the same row count");
+      return 0;
+    }
+  if (!FlushAppender(a)) return 0;  // keep row order: staged rows first
+  try {
+    HostBatch b;
+    b.nrows = count;
+    for (size_t i = 0; i < nc; i++) {
+      HostColumn hc;
+      hc.type = a->table->cols[i].type;
+      hc.phys = a->table->cols[i].phys;
+      size_t bytes = (size_t)count * PhysSize(hc.phys);
+      hc.data.resize(bytes);
+      memcpy(hc.data.data(), a->raw_vals[i], bytes);
+      if (a->raw_valid[i]) hc.valid.assign(a->raw_valid[i], a->raw_valid[i] + count);
+      b.cols.push_back(std::move(hc));
+    }
+    AppendHostBatch(a->conn->conn, *a->table, b);
+  } catch (std::exception &e) {
+    CopyErr(a->error, e.what());
+    return 0;
+  }
+  a->raw_vals.clear();
+  a->raw_valid.clear();
+  a->raw_count.clear();
+  return 1;
+}
+
+// ---- "arrow" read-back ---------------------------------------------------------
+duckdb_mb_arrow_result *duckdb_mb_query_arrow(duckdb_mb_connection *h, moonbit_bytes_t sql) {  // ref :2219-2268
+  if (!h) {
+    SetError("invalid connection handle");
+    return nullptr;
+  }
+  try {
+    ResultPtr r = RunStatement(h->conn, BytesStr(sql), {}, nullptr);
+    auto *a = new duckdb_mb_arrow_result();
+    a->r = r;
+    a->error[0] = '\0';
+    a->column_count = (int32_t)r->cols.size();
+    a->row_count = (int32_t)r->nrows;
+    return a;
+  } catch (std::exception &e) {
+    SetError(e.what());
+    return nullptr;
+  }
+}
+
+int32_t duckdb_mb_arrow_column_count(duckdb_mb_arrow_result *a) { return a ? a->column_count : 0; }  // ref :2270
+int32_t duckdb_mb_arrow_row_count(duckdb_mb_arrow_result *a) { return a ? a->row_count : 0; }        // ref :2277
+
+moonbit_bytes_t duckdb_mb_arrow_schema(duckdb_mb_arrow_result *a) {  // ref :2285-2355
+  if (!a || a->column_count <= 0) return MakeBytes("[]", 2);
+  std::string j = "[";
+  for (int32_t i = 0; i < a->column_count; i++) {
+    const HostColumn &c = a->r->cols[i];
+    const char *tid = "string";
+    switch (c.type.id) {
+      case T_BOOLEAN: tid = "bool"; break;
+      case T_TINYINT: case T_SMALLINT: case T_INTEGER: tid = "int32"; break;
+      case T_BIGINT: tid = "int64"; break;
+      case T_FLOAT: case T_DOUBLE: tid = "double"; break;
+      default: tid = "string"; break;
+    }
+    j += std::string(i ? "," : "") + "{\"name\":\"" + c.name + "\",\"nullable\":true,\"type_id\":\"" + tid + "\"}";
+  }
+  j += "]";
+  return MakeBytes(j);
+}
+
+// The per-cell conversions of the reference's duckdb_value_int64 /
+// duckdb_value_double / duckdb_value_boolean: a failed cast yields 0.
+static int64_t CellI64(const HostColumn &c, int64_t row) {
+  Value v = c.Get(row);
+  if (v.is_null) return 0;
+  Value x = CastValue(v, LogicalType(T_BIGINT), true);
+  return x.is_null ? 0 : (int64_t)x.i;
+}
+static double CellF64(const HostColumn &c, int64_t row) {
+  Value v = c.Get(row);
+  if (v.is_null) return 0.0;
+  Value x = CastValue(v, LogicalType(T_DOUBLE), true);
+  return x.is_null ? 0.0 : x.d;
+}
+static uint8_t CellBool(const HostColumn &c, int64_t row) {
+  Value v = c.Get(row);
+  if (v.is_null) return 0;
+  Value x = CastValue(v, LogicalType(T_BOOLEAN), true);
+  return x.is_null ? 0 : (x.i ? 1 : 0);
+}
+
+static bool ArrowOk(duckdb_mb_arrow_result *a, int32_t col) {
+  return a && col >= 0 && col < a->column_count && a->row_count > 0;
+}
+
+static moonbit_bytes_t ArrowFixed(duckdb_mb_arrow_result *a, int32_t col, int width, bool nullable) {
+  if (!ArrowOk(a, col)) return MakeBytes("", 0);
+  int64_t n = a->row_count;
+  int64_t total = 4 + n * width + (nullable ? n : 0);
+  if (total > INT32_MAX) {
+    SetError("arrow column too large for one Bytes object");
+    return MakeBytes("", 0);
+  }
+  moonbit_bytes_t out = moonbit_make_bytes_raw((int32_t)total);
+  int32_t cnt = (int32_t)n;
+  memcpy(out, &cnt, 4);
+  uint8_t *vals = out + 4;
+  uint8_t *valid = out + 4 + n * width;
+  const HostColumn &c = a->r->cols[col];
+  for (int64_t i = 0; i < n; i++) {
+    bool null = c.IsNull(i);
+    if (nullable) valid[i] = null ? 0 : 1;
+    if (width == 4) {
+      int32_t x = null ? 0 : (int32_t)CellI64(c, i);
+      memcpy(vals + 4 * i, &x, 4);
+    } else if (width == 8 && c.type.id != T_DOUBLE && c.type.id != T_FLOAT && c.phys != P_F64) {
+      // int64 getter
+      int64_t x = null ? 0 : CellI64(c, i);
+      memcpy(vals + 8 * i, &x, 8);
+    } else if (width == 8) {
+      double x = null ? 0.0 : CellF64(c, i);
+      memcpy(vals + 8 * i, &x, 8);
+    } else {
+      vals[i] = null ? 0 : CellBool(c, i);
+    }
+  }
+  return out;
+}
+
+static moonbit_bytes_t ArrowF64(duckdb_mb_arrow_result *a, int32_t col, bool nullable) {
+  if (!ArrowOk(a, col)) return MakeBytes("", 0);
+  int64_t n = a->row_count;
+  int64_t total = 4 + n * 8 + (nullable ? n : 0);
+  if (total > INT32_MAX) return MakeBytes("", 0);
+  moonbit_bytes_t out = moonbit_make_bytes_raw((int32_t)total);
+  int32_t cnt = (int32_t)n;
+  memcpy(out, &cnt, 4);
+  const HostColumn &c = a->r->cols[col];
+  for (int64_t i = 0; i < n; i++) {
+    bool null = c.IsNull(i);
+    double x = null ? 0.0 : CellF64(c, i);
+    memcpy(out + 4 + 8 * i, &x, 8);
+    if (nullable) out[4 + n * 8 + i] = null ? 0 : 1;
+  }
+  return out;
+}
+
+static moonbit_bytes_t ArrowStr(duckdb_mb_arrow_result *a, int32_t col, bool nullable) {
+  if (!ArrowOk(a, col)) return MakeBytes("", 0);
+  int64_t n = a->row_count;
+  const HostColumn &c = a->r->cols[col];
+  std::string data;
+  for (int64_t i = 0; i < n; i++) {
+    if (!c.IsNull(i)) data += FormatValue(c.Get(i));
+    data.push_back('\0');
+  }
+  int64_t total = 8 + (int64_t)data.size() + (nullable ? n : 0);
+  if (total > INT32_MAX) return MakeBytes("", 0);
+  moonbit_bytes_t out = moonbit_make_bytes_raw((int32_t)total);
+  int32_t h[2] = {(int32_t)n, (int32_t)data.size()};
+  memcpy(out, h, 8);
+  memcpy(out + 8, data.data(), data.size());
+  if (nullable)
+    for (int64_t i = 0; i < n; i++) out[8 + data.size() + i] = c.IsNull(i) ? 0 : 1;
+  return out;
+}
+
+moonbit_bytes_t duckdb_mb_arrow_get_column_int32(duckdb_mb_arrow_result *a, int32_t col) { return ArrowFixed(a, col, 4, false); }  // ref :2359
+moonbit_bytes_t duckdb_mb_arrow_get_column_int64(duckdb_mb_arrow_result *a, int32_t col) {  // ref :2392
+  if (!ArrowOk(a, col)) return MakeBytes("", 0);
+  int64_t n = a->row_count;
+  if (4 + n * 8 > INT32_MAX) return MakeBytes("", 0);
+  moonbit_bytes_t out = moonbit_make_bytes_raw((int32_t)(4 + n * 8));
+  int32_t cnt = (int32_t)n;
+  memcpy(out, &cnt, 4);
+  const HostColumn &c = a->r->cols[col];
+  if (c.phys == P_I64 && c.type.id == T_BIGINT) {
+    // fast path: the D2H'd column already is the wire layout
+    memcpy(out + 4, c.data.data(), (size_t)n * 8);
+    for (int64_t i = 0; i < n; i++)
+      if (c.IsNull(i)) memset(out + 4 + 8 * i, 0, 8);
+  } else {
+    for (int64_t i = 0; i < n; i++) {
+      int64_t x = c.IsNull(i) ? 0 : CellI64(c, i);
+      memcpy(out + 4 + 8 * i, &x, 8);
+    }
+  }
+  return out;
+}
+moonbit_bytes_t duckdb_mb_arrow_get_column_double(duckdb_mb_arrow_result *a, int32_t col) { return ArrowF64(a, col, false); }  // ref :2424
+moonbit_bytes_t duckdb_mb_arrow_get_column_string(duckdb_mb_arrow_result *a, int32_t col) { return ArrowStr(a, col, false); }  // ref :2456
+moonbit_bytes_t duckdb_mb_arrow_get_column_bool(duckdb_mb_arrow_result *a, int32_t col) { return ArrowFixed(a, col, 1, false); }  // ref :2516
+moonbit_bytes_t duckdb_mb_arrow_get_column_int32_nullable(duckdb_mb_arrow_result *a, int32_t col) { return ArrowFixed(a, col, 4, true); }  // ref :2572
+moonbit_bytes_t duckdb_mb_arrow_get_column_int64_nullable(duckdb_mb_arrow_result *a, int32_t col) {  // ref :2611
+  if (!ArrowOk(a, col)) return MakeBytes("", 0);
+  int64_t n = a->row_count;
+  if (4 + n * 9 > INT32_MAX) return MakeBytes("", 0);
+  moonbit_bytes_t out = moonbit_make_bytes_raw((int32_t)(4 + n * 9));
+  int32_t cnt = (int32_t)n;
+  memcpy(out, &cnt, 4);
+  const HostColumn &c = a->r->cols[col];
+  for (int64_t i = 0; i < n; i++) {
+    bool null = c.IsNull(i);
+    int64_t x = null ? 0 : CellI64(c, i);
+    memcpy(out + 4 + 8 * i, &x, 8);
+    out[4 + 8 * n + i] = null ? 0 : 1;
+  }
+  return out;
+}
+moonbit_bytes_t duckdb_mb_arrow_get_column_double_nullable(duckdb_mb_arrow_result *a, int32_t col) { return ArrowF64(a, col, true); }  // ref :2649
+moonbit_bytes_t duckdb_mb_arrow_get_column_string_nullable(duckdb_mb_arrow_result *a, int32_t col) { return ArrowStr(a, col, true); }  // ref :2687
+moonbit_bytes_t duckdb_mb_arrow_get_column_bool_nullable(duckdb_mb_arrow_result *a, int32_t col) { return ArrowFixed(a, col, 1, true); }  // ref :2761
+
+void duckdb_mb_arrow_destroy(duckdb_mb_arrow_result *a) { delete a; }  // ref :2548
+int32_t duckdb_mb_is_null_arrow_result(duckdb_mb_arrow_result *a) { return a == nullptr ? 1 : 0; }  // ref :2556
+double duckdb_mb_bytes_to_double(const char *bytes, int32_t offset) {  // ref :2561-2565
+  double r;
+  memcpy(&r, bytes + offset, sizeof(double));
+  return r;
+}
+
+// ---- extensions ----------------------------------------------------------------
+int32_t duckdb_mbx_device_count(void) { return DeviceCount(); }
+const char *duckdb_mbx_version(void) { return "duckdb.mbt-amd 0.1.0 (gfx950, HIP)"; }
+
+char *duckdb_mbx_explain(duckdb_mb_connection *h, const char *sql, int64_t len) {
+  if (!h || !sql) {
+    SetError("connection is null");
+    return nullptr;
+  }
+  try {
+    std::string s = Explain(h->conn, std::string(sql, (size_t)len));
+    return strdup(s.c_str());
+  } catch (std::exception &e) {
+    SetError(e.what());
+    return nullptr;
+  }
+}
+void duckdb_mbx_free(void *p) { free(p); }
+
+char *duckdb_mbx_last_profile(duckdb_mb_connection *h) {
+  if (!h) return nullptr;
+  const QueryProfile &p = h->conn.last_profile;
+  std::string j = "{\"total_ms\":" + std::to_string(p.total_ms) + ",\"kernels\":[";
+  for (size_t i = 0; i < p.kernels.size(); i++) {
+    const auto &k = p.kernels[i];
+    char buf[256];
+    snprintf(buf, sizeof(buf), "%s{\"name\":\"%s\",\"ms\":%.6f,\"bytes\":%.0f,\"rows\":%lld}", i ? "," : "",
+             k.name.c_str(), k.ms, k.bytes, (long long)k.rows);
+    j += buf;
+  }
+  j += "]}";
+  return strdup(j.c_str());
+}
+
+int32_t duckdb_mbx_result_raw(duckdb_mb_result *r, int32_t col, int32_t row, void *out, int32_t out_len) {
+  if (!r || !InRange(r->r, col, row) || !out) return 0;
+  const HostColumn &c = r->r->cols[col];
+  if (c.IsNull(row) || c.phys == P_STR) return 0;
+  int sz = PhysSize(c.phys);
+  if (out_len < sz) return 0;
+  memcpy(out, c.data.data() + (size_t)row * sz, sz);
+  return sz;
+}
+
+}  // extern "C"

@@ -1,0 +1,209 @@
+/*
+ * duckdb_mb.h — the drop-in C-ABI boundary of the MI355X columnar backend.
+ *
+ * These are exactly the 89 `duckdb_mb_*` symbols the reference's MoonBit
+ * driver binds with `extern "C" fn ... = "duckdb_mb_*"`:
+ *   72 in /root/reference/src/duckdb_native.mbt:10-411, :669-743
+ *   17 in /root/reference/src/duckdb_arrow_native.mbt:10-104
+ * with the C parameter/return types of their definitions in
+ * /root/reference/src/duckdb_native.c (the line cited on each declaration is
+ * the reference definition this symbol replaces).  The library
+ * `libduckdb_mb_amd.so` (built from duckdb.mbt_amd/csrc) exports all of them;
+ * it links no libduckdb.  Scans, filters, projections and aggregates run as
+ * hand-written gfx950 HIP kernels on device-resident column chunks.
+ *
+ * ABI rules kept from the reference (refs/ffi.md:258-281, :509-547):
+ *   - MoonBit Int/Bool -> int32_t, Int64 -> int64_t, Double -> double,
+ *     Bytes -> uint8_t* with the MoonBit object header in front (the length is
+ *     read with Moonbit_array_length), Array[Bytes] -> uint8_t**.
+ *   - every pointer argument is borrowed; returned Bytes are fresh objects from
+ *     moonbit_make_bytes_raw owned by the caller.
+ *   - failure = NULL handle or 0 status; the message comes from
+ *     duckdb_mb_last_error() (connect/query/stream/arrow) or the per-handle
+ *     *_error() accessor (statement/appender/config).
+ *   - end of stream = NULL chunk with an EMPTY last error
+ *     (reference duckdb_native.c:466-490).
+ *
+ * Extensions (prefix duckdb_mbx_, not part of the reference surface) are
+ * declared at the bottom: helpers for non-MoonBit hosts (Python/ctypes tests)
+ * and the columnar bulk-ingest / profiling entry points.
+ */
+#ifndef DUCKDB_MB_AMD_H
+#define DUCKDB_MB_AMD_H
+
+#include <stdbool.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef uint8_t *moonbit_bytes_t;
+
+/* Opaque handles (the MoonBit side sees them as #external = void*). */
+typedef struct duckdb_mb_connection duckdb_mb_connection;
+typedef struct duckdb_mb_result duckdb_mb_result; /* reference: duckdb_result* */
+typedef struct duckdb_mb_stream duckdb_mb_stream;
+typedef struct duckdb_mb_chunk duckdb_mb_chunk;
+typedef struct duckdb_mb_statement duckdb_mb_statement;
+typedef struct duckdb_mb_appender duckdb_mb_appender;
+typedef struct duckdb_mb_config duckdb_mb_config;
+typedef struct duckdb_mb_arrow_result duckdb_mb_arrow_result;
+
+/* ---- connection (duckdb_native.c:67-140, :248-250) ---------------------- */
+duckdb_mb_connection *duckdb_mb_connect(moonbit_bytes_t path);                  /* :67   */
+void duckdb_mb_disconnect(duckdb_mb_connection *handle);                         /* :133  */
+int32_t duckdb_mb_is_null_conn(duckdb_mb_connection *handle);                    /* :248  */
+moonbit_bytes_t duckdb_mb_last_error(void);                                      /* :240  */
+
+/* ---- materialized query (duckdb_native.c:142-254) ---------------------- */
+duckdb_mb_result *duckdb_mb_query(duckdb_mb_connection *handle, moonbit_bytes_t sql); /* :142 */
+void duckdb_mb_result_destroy(duckdb_mb_result *result);                         /* :174  */
+int32_t duckdb_mb_result_column_count(duckdb_mb_result *result);                 /* :182  */
+int32_t duckdb_mb_result_row_count(duckdb_mb_result *result);                    /* :189  */
+moonbit_bytes_t duckdb_mb_result_column_name(duckdb_mb_result *result, int32_t col); /* :196 */
+int32_t duckdb_mb_result_column_type(duckdb_mb_result *result, int32_t col);     /* :208  */
+int32_t duckdb_mb_result_is_null(duckdb_mb_result *result, int32_t col, int32_t row); /* :215 */
+moonbit_bytes_t duckdb_mb_result_value(duckdb_mb_result *result, int32_t col, int32_t row); /* :224 */
+int32_t duckdb_mb_is_null_result(duckdb_mb_result *result);                      /* :252  */
+
+/* ---- streaming (duckdb_native.c:260-667) ------------------------------- */
+duckdb_mb_stream *duckdb_mb_query_stream(duckdb_mb_connection *handle, moonbit_bytes_t sql); /* :355 */
+duckdb_mb_stream *duckdb_mb_execute_prepared_stream(duckdb_mb_statement *stmt);  /* :399  */
+void duckdb_mb_stream_destroy(duckdb_mb_stream *stream);                         /* :426  */
+int32_t duckdb_mb_is_null_stream(duckdb_mb_stream *stream);                      /* :440  */
+int32_t duckdb_mb_stream_column_count(duckdb_mb_stream *stream);                 /* :444  */
+moonbit_bytes_t duckdb_mb_stream_column_name(duckdb_mb_stream *stream, int32_t col); /* :451 */
+duckdb_mb_chunk *duckdb_mb_stream_fetch_chunk(duckdb_mb_stream *stream);         /* :466  */
+void duckdb_mb_chunk_destroy(duckdb_mb_chunk *chunk);                            /* :492  */
+int32_t duckdb_mb_is_null_chunk(duckdb_mb_chunk *chunk);                         /* :502  */
+int32_t duckdb_mb_chunk_row_count(duckdb_mb_chunk *chunk);                       /* :506  */
+int32_t duckdb_mb_chunk_column_count(duckdb_mb_chunk *chunk);                    /* :513  */
+int32_t duckdb_mb_chunk_is_null(duckdb_mb_chunk *chunk, int32_t col, int32_t row); /* :520 */
+moonbit_bytes_t duckdb_mb_chunk_value(duckdb_mb_chunk *chunk, int32_t col, int32_t row); /* :537 */
+
+/* ---- configuration (duckdb_native.c:673-810) --------------------------- */
+duckdb_mb_config *duckdb_mb_config_create(void);                                 /* :678  */
+void duckdb_mb_config_destroy(duckdb_mb_config *cfg);                            /* :697  */
+moonbit_bytes_t duckdb_mb_config_error(duckdb_mb_config *cfg);                   /* :707  */
+int32_t duckdb_mb_config_set(duckdb_mb_config *cfg, moonbit_bytes_t key, moonbit_bytes_t value); /* :714 */
+duckdb_mb_connection *duckdb_mb_connect_with_config(moonbit_bytes_t path, duckdb_mb_config *cfg); /* :749 */
+
+/* ---- prepared statements (duckdb_native.c:816-1020, :1261-1296) -------- */
+duckdb_mb_statement *duckdb_mb_prepare(duckdb_mb_connection *handle, moonbit_bytes_t sql); /* :816 */
+void duckdb_mb_statement_destroy(duckdb_mb_statement *stmt);                     /* :856  */
+moonbit_bytes_t duckdb_mb_statement_error(duckdb_mb_statement *stmt);            /* :866  */
+int32_t duckdb_mb_bind_int(duckdb_mb_statement *stmt, int32_t index, int32_t value);   /* :873  */
+int32_t duckdb_mb_bind_bigint(duckdb_mb_statement *stmt, int32_t index, int64_t value); /* :890 */
+int32_t duckdb_mb_bind_double(duckdb_mb_statement *stmt, int32_t index, double value);  /* :907 */
+int32_t duckdb_mb_bind_varchar(duckdb_mb_statement *stmt, int32_t index, moonbit_bytes_t value); /* :924 */
+int32_t duckdb_mb_bind_bool(duckdb_mb_statement *stmt, int32_t index, bool value);      /* :950 */
+int32_t duckdb_mb_bind_null(duckdb_mb_statement *stmt, int32_t index);           /* :967  */
+int32_t duckdb_mb_clear_bindings(duckdb_mb_statement *stmt);                     /* :983  */
+duckdb_mb_result *duckdb_mb_execute_prepared(duckdb_mb_statement *stmt);         /* :991  */
+int32_t duckdb_mb_is_null_statement(duckdb_mb_statement *stmt);                  /* :1018 */
+int32_t duckdb_mb_bind_date(duckdb_mb_statement *stmt, int32_t index, int32_t days);    /* :1261 */
+int32_t duckdb_mb_bind_timestamp(duckdb_mb_statement *stmt, int32_t index, int64_t micros); /* :1279 */
+int32_t duckdb_mb_bind_blob(duckdb_mb_statement *stmt, int32_t index, moonbit_bytes_t data, int32_t length); /* :1377 */
+int32_t duckdb_mb_bind_decimal(duckdb_mb_statement *stmt, int32_t index, uint8_t width, uint8_t scale,
+                               int64_t lower, int64_t upper);                    /* :1421 */
+int32_t duckdb_mb_bind_interval(duckdb_mb_statement *stmt, int32_t index, int32_t months, int32_t days,
+                                int64_t micros);                                 /* :1487 */
+int32_t duckdb_mb_bind_list_varchar(duckdb_mb_statement *stmt, int32_t index, moonbit_bytes_t *values,
+                                    int32_t count);                              /* :1539 */
+int32_t duckdb_mb_bind_struct_varchar(duckdb_mb_statement *stmt, int32_t index, moonbit_bytes_t *field_names,
+                                      moonbit_bytes_t *field_values, int32_t field_count); /* :1597 */
+int32_t duckdb_mb_bind_map_varchar_varchar(duckdb_mb_statement *stmt, int32_t index, moonbit_bytes_t *keys,
+                                           moonbit_bytes_t *values, int32_t entry_count); /* :1666 */
+
+/* ---- appender (duckdb_native.c:1026-1255, :1313-1367, :1397-1533, :1735-1922) */
+duckdb_mb_appender *duckdb_mb_appender_create(duckdb_mb_connection *handle, moonbit_bytes_t schema,
+                                              moonbit_bytes_t table);            /* :1032 */
+void duckdb_mb_appender_destroy(duckdb_mb_appender *app);                        /* :1083 */
+moonbit_bytes_t duckdb_mb_appender_error(duckdb_mb_appender *app);               /* :1093 */
+int32_t duckdb_mb_begin_row(duckdb_mb_appender *app);                            /* :1100 */
+int32_t duckdb_mb_append_int(duckdb_mb_appender *app, int32_t value);            /* :1116 */
+int32_t duckdb_mb_append_bigint(duckdb_mb_appender *app, int64_t value);         /* :1132 */
+int32_t duckdb_mb_append_double(duckdb_mb_appender *app, double value);          /* :1148 */
+int32_t duckdb_mb_append_varchar(duckdb_mb_appender *app, moonbit_bytes_t value); /* :1164 */
+int32_t duckdb_mb_append_bool(duckdb_mb_appender *app, bool value);              /* :1189 */
+int32_t duckdb_mb_append_null(duckdb_mb_appender *app);                          /* :1205 */
+int32_t duckdb_mb_end_row(duckdb_mb_appender *app);                              /* :1221 */
+int32_t duckdb_mb_flush(duckdb_mb_appender *app);                                /* :1237 */
+int32_t duckdb_mb_is_null_appender(duckdb_mb_appender *app);                     /* :1253 */
+int32_t duckdb_mb_append_date(duckdb_mb_appender *app, int32_t days);            /* :1313 */
+int32_t duckdb_mb_append_timestamp(duckdb_mb_appender *app, int64_t micros);     /* :1350 */
+int32_t duckdb_mb_append_blob(duckdb_mb_appender *app, moonbit_bytes_t data, int32_t length); /* :1397 */
+int32_t duckdb_mb_append_decimal(duckdb_mb_appender *app, uint8_t width, uint8_t scale, int64_t lower,
+                                 int64_t upper);                                 /* :1447 */
+int32_t duckdb_mb_append_interval(duckdb_mb_appender *app, int32_t months, int32_t days, int64_t micros); /* :1511 */
+int32_t duckdb_mb_append_list_varchar(duckdb_mb_appender *app, moonbit_bytes_t *values, int32_t count); /* :1735 */
+int32_t duckdb_mb_append_struct_varchar(duckdb_mb_appender *app, moonbit_bytes_t *field_names,
+                                        moonbit_bytes_t *field_values, int32_t field_count); /* :1792 */
+int32_t duckdb_mb_append_map_varchar_varchar(duckdb_mb_appender *app, moonbit_bytes_t *keys,
+                                             moonbit_bytes_t *values, int32_t entry_count); /* :1860 */
+
+/* ---- "arrow" columnar read-back (duckdb_native.c:2211-2797) ------------ */
+duckdb_mb_arrow_result *duckdb_mb_query_arrow(duckdb_mb_connection *handle, moonbit_bytes_t sql); /* :2219 */
+void duckdb_mb_arrow_destroy(duckdb_mb_arrow_result *r);                         /* :2548 */
+int32_t duckdb_mb_arrow_column_count(duckdb_mb_arrow_result *r);                 /* :2270 */
+int32_t duckdb_mb_arrow_row_count(duckdb_mb_arrow_result *r);                    /* :2277 */
+moonbit_bytes_t duckdb_mb_arrow_schema(duckdb_mb_arrow_result *r);               /* :2285 */
+moonbit_bytes_t duckdb_mb_arrow_get_column_int32(duckdb_mb_arrow_result *r, int32_t col);  /* :2359 */
+moonbit_bytes_t duckdb_mb_arrow_get_column_int64(duckdb_mb_arrow_result *r, int32_t col);  /* :2392 */
+moonbit_bytes_t duckdb_mb_arrow_get_column_double(duckdb_mb_arrow_result *r, int32_t col); /* :2424 */
+moonbit_bytes_t duckdb_mb_arrow_get_column_string(duckdb_mb_arrow_result *r, int32_t col); /* :2456 */
+moonbit_bytes_t duckdb_mb_arrow_get_column_bool(duckdb_mb_arrow_result *r, int32_t col);   /* :2516 */
+moonbit_bytes_t duckdb_mb_arrow_get_column_int32_nullable(duckdb_mb_arrow_result *r, int32_t col);  /* :2572 */
+moonbit_bytes_t duckdb_mb_arrow_get_column_int64_nullable(duckdb_mb_arrow_result *r, int32_t col);  /* :2611 */
+moonbit_bytes_t duckdb_mb_arrow_get_column_double_nullable(duckdb_mb_arrow_result *r, int32_t col); /* :2649 */
+moonbit_bytes_t duckdb_mb_arrow_get_column_string_nullable(duckdb_mb_arrow_result *r, int32_t col); /* :2687 */
+moonbit_bytes_t duckdb_mb_arrow_get_column_bool_nullable(duckdb_mb_arrow_result *r, int32_t col);   /* :2761 */
+int32_t duckdb_mb_is_null_arrow_result(duckdb_mb_arrow_result *r);               /* :2556 */
+double duckdb_mb_bytes_to_double(const char *bytes, int32_t offset);             /* :2561 */
+
+/* ======================================================================== *
+ * Extensions (not in the reference surface).                                *
+ * ======================================================================== */
+
+/* MoonBit byte objects for hosts that are not a MoonBit program.  Inside a
+ * MoonBit executable the runtime's moonbit_make_bytes_raw is used instead
+ * (ours is a weak definition). */
+moonbit_bytes_t moonbit_make_bytes_raw(int32_t len);
+moonbit_bytes_t duckdb_mbx_bytes_new(const uint8_t *data, int32_t len);
+int32_t duckdb_mbx_bytes_len(moonbit_bytes_t bytes);
+void duckdb_mbx_bytes_free(moonbit_bytes_t bytes);
+
+/* Device / library info: number of visible gfx950 devices (0 without a GPU),
+ * and the library build string. */
+int32_t duckdb_mbx_device_count(void);
+const char *duckdb_mbx_version(void);
+
+/* Plan of a statement as text (binder + planner only, never touches a GPU).
+ * Returns a malloc'd NUL-terminated string (free with duckdb_mbx_free) or NULL
+ * with duckdb_mb_last_error() set. */
+char *duckdb_mbx_explain(duckdb_mb_connection *handle, const char *sql, int64_t sql_len);
+void duckdb_mbx_free(void *p);
+
+/* Columnar bulk ingest (MI355X-native form of the unbound
+ * duckdb_mb_append_data_chunk, reference duckdb_native.c:2109-2132):
+ * appends `count` values of one column from host memory; all columns of a
+ * batch must be appended with the same count before duckdb_mbx_append_commit.
+ * `validity` may be NULL (all valid) or one byte per row (1 = valid). */
+int32_t duckdb_mbx_append_column(duckdb_mb_appender *app, int32_t col, const void *values,
+                                 const uint8_t *validity, int64_t count);
+int32_t duckdb_mbx_append_commit(duckdb_mb_appender *app, int64_t count);
+
+/* Per-query device profile of the last statement run on this connection
+ * (enable with config key "mbx_profile"="true"): JSON text, malloc'd. */
+char *duckdb_mbx_last_profile(duckdb_mb_connection *handle);
+
+/* Partial aggregate export for multi-GPU combine: the i-th cell of the last
+ * materialized result as raw little-endian bytes (HUGEINT: 16 bytes). */
+int32_t duckdb_mbx_result_raw(duckdb_mb_result *result, int32_t col, int32_t row, void *out, int32_t out_len);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* DUCKDB_MB_AMD_H */
