@@ -1,0 +1,100 @@
+"""oracle — TEST INFRASTRUCTURE ONLY (checker for tests/, smoke(), and the
+cpu_baseline leg of bench.py).  Nothing under duckdb.mbt_amd/ imports this.
+
+Contents
+  liboracle_mbx.so (oracle.c): multi-threaded C restatement of the hot-path
+      arithmetic (synthetic generator, filter+COUNT/SUM/MIN/MAX, GROUP BY SUM).
+  wire.py:   byte-exact restatement of the reference shim's "arrow" buffers
+             (/root/reference/src/duckdb_native.c:2285-2797).
+  mb.py:     restatement of the MoonBit-side parsing (duckdb_parsing.mbt) used
+             to pin the typed-result behaviour.
+  fmt.py:    DuckDB text rendering of values (what duckdb_value_varchar
+             returns, pinned by src/duckdb_fixture_cases.mbt).
+
+Parity status: pinned by the reference's own golden vectors — the 35 SQL
+fixtures (tests/golden/fixtures.json, extracted from
+src/duckdb_fixture_cases.mbt by tests/golden/make_fixtures.py), the native and
+arrow test assertions (tests/golden/native_cases.json), and closed forms for
+large N (e.g. COUNT(range(N) WHERE i%2=0) = ceil(N/2)).  libduckdb itself is
+absent from /root/reference and from this image, so it cannot be executed.
+"""
+import ctypes
+import os
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB = os.path.join(HERE, "build", "liboracle_mbx.so")
+
+
+def build():
+    import subprocess
+    subprocess.check_call(["make", "-s", "-C", HERE])
+
+
+def load():
+    if not os.path.exists(LIB):
+        build()
+    lib = ctypes.CDLL(LIB)
+    u64, i64, i32, vp = ctypes.c_uint64, ctypes.c_int64, ctypes.c_int32, ctypes.c_void_p
+    lib.orc_splitmix64.restype = u64
+    lib.orc_splitmix64.argtypes = [u64]
+    lib.orc_synth_i64.argtypes = [vp, i64, u64, i64, u64, i64]
+    lib.orc_synth_i32.argtypes = [vp, i64, u64, i64, u64, i64]
+    lib.orc_filter_agg_i64.argtypes = [vp, i64, i64, i64, ctypes.c_int, vp, vp, vp, vp]
+    lib.orc_synth_filter_count.argtypes = [u64, i64, i64, u64, i64, i64, i64, ctypes.c_int, vp, vp]
+    lib.orc_groupby_sum_i32_i64.argtypes = [vp, vp, i64, i32, ctypes.c_int, ctypes.c_int, vp, vp]
+    lib.orc_range_mod_select.restype = i64
+    lib.orc_range_mod_select.argtypes = [i64, i64, i64, i64, vp, i64]
+    return lib
+
+
+def i128_from(b: bytes) -> int:
+    return int.from_bytes(b, "little", signed=True)
+
+
+class Oracle:
+    def __init__(self):
+        self.lib = load()
+
+    def splitmix64(self, z: int) -> int:
+        return self.lib.orc_splitmix64(z & (2**64 - 1))
+
+    def synth_i64(self, n, seed, start, m, add):
+        import numpy as np
+        out = np.empty(n, dtype=np.int64)
+        self.lib.orc_synth_i64(out.ctypes.data, n, seed, start, m, add)
+        return out
+
+    def synth_i32(self, n, seed, start, m, add):
+        import numpy as np
+        out = np.empty(n, dtype=np.int32)
+        self.lib.orc_synth_i32(out.ctypes.data, n, seed, start, m, add)
+        return out
+
+    def filter_agg_i64(self, x, lo, hi, threads=1):
+        c = ctypes.c_uint64()
+        s = ctypes.create_string_buffer(16)
+        mn, mx = ctypes.c_int64(), ctypes.c_int64()
+        self.lib.orc_filter_agg_i64(x.ctypes.data, len(x), lo, hi, threads, ctypes.byref(c), s,
+                                    ctypes.byref(mn), ctypes.byref(mx))
+        return c.value, i128_from(s.raw), mn.value, mx.value
+
+    def synth_filter_count(self, seed, start, n, m, add, lo, hi, threads=1):
+        c = ctypes.c_uint64()
+        s = ctypes.create_string_buffer(16)
+        self.lib.orc_synth_filter_count(seed, start, n, m, add, lo, hi, threads, ctypes.byref(c), s)
+        return c.value, i128_from(s.raw)
+
+    def groupby_sum(self, k, v, kmin, nk, threads=1):
+        import numpy as np
+        counts = np.zeros(nk, dtype=np.uint64)
+        sums = ctypes.create_string_buffer(16 * nk)
+        self.lib.orc_groupby_sum_i32_i64(k.ctypes.data, v.ctypes.data, len(k), kmin, nk, threads,
+                                         counts.ctypes.data, sums)
+        return [int(c) for c in counts], [i128_from(sums.raw[16 * i:16 * i + 16]) for i in range(nk)]
+
+    def range_mod_select(self, n, k, c, mul):
+        import numpy as np
+        cap = n // k + 2
+        out = np.empty(cap, dtype=np.int64)
+        w = self.lib.orc_range_mod_select(n, k, c, mul, out.ctypes.data, cap)
+        return out[:w]

@@ -1,0 +1,224 @@
+/*
+ * oracle.c — TEST INFRASTRUCTURE ONLY.  CPU restatement of the hot-path
+ * arithmetic the reference delegates to libduckdb (duckdb_query at
+ * /root/reference/src/duckdb_native.c:159, :2246), used by tests/, by
+ * __graft_entry__.smoke() as the checker and by bench.py's cpu_baseline leg.
+ * The product (duckdb.mbt_amd/) never links or calls this file.
+ *
+ * Parity anchor: libduckdb itself is not in /root/reference (it is an
+ * un-vendored dependency, "latest" in .github/workflows/native-ci.yml:31-40;
+ * the JS path pins @duckdb/node-api 1.4.3-r.3, package-lock.json:26-29) and is
+ * not installed in this image.  The semantics restated here are DuckDB's for
+ * the recognised shapes, pinned by the reference's golden fixtures
+ * (src/duckdb_fixture_cases.mbt) and native tests (see tests/golden/):
+ *   COUNT(*) -> BIGINT, SUM(BIGINT/INTEGER) -> HUGEINT (exact int128),
+ *   MIN/MAX -> input type, '%' truncated modulo, range(N) = 0..N-1.
+ *
+ * Synthetic data: x_i = splitmix64(seed + start + i) mod m + add.
+ */
+#include <pthread.h>
+#include <stdint.h>
+#include <stdlib.h>
+#include <string.h>
+
+typedef __int128 i128;
+
+uint64_t orc_splitmix64(uint64_t z) {
+  z += 0x9E3779B97F4A7C15ull;
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  return z ^ (z >> 31);
+}
+
+void orc_synth_i64(int64_t *out, int64_t n, uint64_t seed, int64_t start, uint64_t m, int64_t add) {
+  for (int64_t i = 0; i < n; i++) out[i] = (int64_t)(orc_splitmix64(seed + (uint64_t)(start + i)) % m) + add;
+}
+
+void orc_synth_i32(int32_t *out, int64_t n, uint64_t seed, int64_t start, uint64_t m, int64_t add) {
+  for (int64_t i = 0; i < n; i++) out[i] = (int32_t)((int64_t)(orc_splitmix64(seed + (uint64_t)(start + i)) % m) + add);
+}
+
+/* ---- filter + aggregate over a materialized int64 column --------------- */
+typedef struct {
+  const int64_t *x;
+  int64_t n;
+  int64_t lo, hi;
+  uint64_t count;
+  i128 sum;
+  int64_t mn, mx;
+} fa_job;
+
+static void *fa_run(void *p) {
+  fa_job *j = (fa_job *)p;
+  uint64_t c = 0;
+  i128 s = 0;
+  int64_t mn = INT64_MAX, mx = INT64_MIN;
+  for (int64_t i = 0; i < j->n; i++) {
+    int64_t v = j->x[i];
+    if (v >= j->lo && v <= j->hi) {
+      c++;
+      s += v;
+      if (v < mn) mn = v;
+      if (v > mx) mx = v;
+    }
+  }
+  j->count = c;
+  j->sum = s;
+  j->mn = mn;
+  j->mx = mx;
+  return NULL;
+}
+
+/* COUNT(*), SUM(x), MIN(x), MAX(x) WHERE lo <= x <= hi.  sum -> 16 bytes LE. */
+void orc_filter_agg_i64(const int64_t *x, int64_t n, int64_t lo, int64_t hi, int threads, uint64_t *count,
+                        void *sum16, int64_t *mn, int64_t *mx) {
+  if (threads < 1) threads = 1;
+  if (threads > 256) threads = 256;
+  fa_job jobs[256];
+  pthread_t th[256];
+  int64_t chunk = (n + threads - 1) / threads;
+  for (int t = 0; t < threads; t++) {
+    int64_t b = t * chunk, e = b + chunk < n ? b + chunk : n;
+    if (b > n) b = n;
+    jobs[t].x = x + b;
+    jobs[t].n = e - b;
+    jobs[t].lo = lo;
+    jobs[t].hi = hi;
+    pthread_create(&th[t], NULL, fa_run, &jobs[t]);
+  }
+  uint64_t c = 0;
+  i128 s = 0;
+  int64_t a = INT64_MAX, z = INT64_MIN;
+  for (int t = 0; t < threads; t++) {
+    pthread_join(th[t], NULL);
+    c += jobs[t].count;
+    s += jobs[t].sum;
+    if (jobs[t].mn < a) a = jobs[t].mn;
+    if (jobs[t].mx > z) z = jobs[t].mx;
+  }
+  *count = c;
+  memcpy(sum16, &s, 16);
+  *mn = a;
+  *mx = z;
+}
+
+/* ---- the same over the generator (no materialisation; full-size parity) - */
+typedef struct {
+  uint64_t seed, m;
+  int64_t start, n, add, lo, hi;
+  uint64_t count;
+  i128 sum;
+} sf_job;
+
+static void *sf_run(void *p) {
+  sf_job *j = (sf_job *)p;
+  uint64_t c = 0;
+  i128 s = 0;
+  for (int64_t i = 0; i < j->n; i++) {
+    int64_t v = (int64_t)(orc_splitmix64(j->seed + (uint64_t)(j->start + i)) % j->m) + j->add;
+    if (v >= j->lo && v <= j->hi) {
+      c++;
+      s += v;
+    }
+  }
+  j->count = c;
+  j->sum = s;
+  return NULL;
+}
+
+void orc_synth_filter_count(uint64_t seed, int64_t start, int64_t n, uint64_t m, int64_t add, int64_t lo, int64_t hi,
+                            int threads, uint64_t *count, void *sum16) {
+  if (threads < 1) threads = 1;
+  if (threads > 256) threads = 256;
+  sf_job jobs[256];
+  pthread_t th[256];
+  int64_t chunk = (n + threads - 1) / threads;
+  for (int t = 0; t < threads; t++) {
+    int64_t b = t * chunk, e = b + chunk < n ? b + chunk : n;
+    if (b > n) b = n;
+    jobs[t].seed = seed;
+    jobs[t].m = m;
+    jobs[t].start = start + b;
+    jobs[t].n = e - b;
+    jobs[t].add = add;
+    jobs[t].lo = lo;
+    jobs[t].hi = hi;
+    pthread_create(&th[t], NULL, sf_run, &jobs[t]);
+  }
+  uint64_t c = 0;
+  i128 s = 0;
+  for (int t = 0; t < threads; t++) {
+    pthread_join(th[t], NULL);
+    c += jobs[t].count;
+    s += jobs[t].sum;
+  }
+  *count = c;
+  memcpy(sum16, &s, 16);
+}
+
+/* ---- GROUP BY small integer key, SUM(int64) as int128, COUNT(*) --------- */
+typedef struct {
+  const int32_t *k;
+  const int64_t *v;
+  int64_t n;
+  int32_t kmin;
+  int nk;
+  uint64_t *cnt;
+  i128 *sum;
+} gb_job;
+
+static void *gb_run(void *p) {
+  gb_job *j = (gb_job *)p;
+  for (int64_t i = 0; i < j->n; i++) {
+    int s = j->k[i] - j->kmin;
+    j->cnt[s]++;
+    j->sum[s] += j->v[i];
+  }
+  return NULL;
+}
+
+/* counts[nk], sums16[nk*16] (int128 LE) */
+void orc_groupby_sum_i32_i64(const int32_t *k, const int64_t *v, int64_t n, int32_t kmin, int nk, int threads,
+                             uint64_t *counts, void *sums16) {
+  if (threads < 1) threads = 1;
+  if (threads > 256) threads = 256;
+  gb_job jobs[256];
+  pthread_t th[256];
+  int64_t chunk = (n + threads - 1) / threads;
+  for (int t = 0; t < threads; t++) {
+    int64_t b = t * chunk, e = b + chunk < n ? b + chunk : n;
+    if (b > n) b = n;
+    jobs[t].k = k + b;
+    jobs[t].v = v + b;
+    jobs[t].n = e - b;
+    jobs[t].kmin = kmin;
+    jobs[t].nk = nk;
+    jobs[t].cnt = (uint64_t *)calloc(nk, sizeof(uint64_t));
+    jobs[t].sum = (i128 *)calloc(nk, sizeof(i128));
+    pthread_create(&th[t], NULL, gb_run, &jobs[t]);
+  }
+  i128 *acc = (i128 *)calloc(nk, sizeof(i128));
+  memset(counts, 0, nk * sizeof(uint64_t));
+  for (int t = 0; t < threads; t++) {
+    pthread_join(th[t], NULL);
+    for (int s = 0; s < nk; s++) {
+      counts[s] += jobs[t].cnt[s];
+      acc[s] += jobs[t].sum[s];
+    }
+    free(jobs[t].cnt);
+    free(jobs[t].sum);
+  }
+  memcpy(sums16, acc, (size_t)nk * 16);
+  free(acc);
+}
+
+/* ---- range(N) WHERE i % k = c, projected i*mul (config C1) ------------- */
+int64_t orc_range_mod_select(int64_t n, int64_t k, int64_t c, int64_t mul, int64_t *out, int64_t cap) {
+  int64_t w = 0;
+  for (int64_t i = 0; i < n; i++)
+    if (i % k == c) {
+      if (w < cap) out[w] = i * mul;
+      w++;
+    }
+  return w;
+}
