@@ -63,6 +63,11 @@ def main():
     if world > 1:
         dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
     mbx = load_mbx()
+    import importlib.util
+    spec = importlib.util.spec_from_file_location("duckdb_mbt_amd_distributed",
+                                                  os.path.join(HERE, "duckdb.mbt_amd", "distributed.py"))
+    mbx_dist = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mbx_dist)
 
     cfg = mbx.Config.create()
     cfg.set("gpu_device", str(local_rank))
@@ -117,9 +122,10 @@ def main():
         out = step()
         prof = conn.last_profile()
         kernel_ms.extend(k["ms"] for k in prof["kernels"] if k["name"] == kernel)
-        if world > 1 and args.config in ("c2", "c5"):
-            cnt = torch.tensor([int(out[0])], dtype=torch.int64, device="cuda")
-            dist.all_reduce(cnt)  # RCCL over xGMI: global COUNT(*)
+        if world > 1 and args.config == "c2":
+            gcount = mbx_dist.allreduce_count(int(out[0]), device="cuda")  # RCCL over xGMI: global COUNT(*)
+        elif world > 1 and args.config == "c5":
+            gcount, gsum = mbx_dist.global_count_sum(int(out[0]), int(out[1]) if out[1] else None, device="cuda")
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()

@@ -1013,9 +1013,17 @@ static DRel Aggregate(Engine &e, const DRel &src, const BoundSelect &s) {
     for (int j = 0; j < na; j++) {
       if (arg_idx[j] < 0) continue;
       const DCol &c = tmp.cols[arg_idx[j]];
-      if (c.phys == P_STR) ThrowError("Not implemented", "aggregates over VARCHAR are not supported on device");
-      ProfScope ps(e, "reduce_column", (double)tmp.n * PhysSize(c.phys), tmp.n);
-      dev::ReduceColumn(c.data, c.phys, c.validity, tmp.n, (dev::AggState *)sb->p + j, e.stream);
+      const void *data = c.data;
+      int phys = c.phys;
+      if (c.phys == P_STR) {
+        // COUNT(varchar) only needs the validity: scan the offsets as int64
+        if (s.aggs[j].kind != A_COUNT)
+          ThrowError("Not implemented", "SUM/MIN/MAX/AVG over VARCHAR are not supported on device");
+        data = c.offsets;
+        phys = P_I64;
+      }
+      ProfScope ps(e, "reduce_column", (double)tmp.n * PhysSize((Phys)phys), tmp.n);
+      dev::ReduceColumn(data, phys, c.validity, tmp.n, (dev::AggState *)sb->p + j, e.stream);
     }
     dev::EmitDesc D;
     memset(&D, 0, sizeof(D));
@@ -1058,11 +1066,18 @@ static DRel Aggregate(Engine &e, const DRel &src, const BoundSelect &s) {
   for (int j = 0; j < na; j++) {
     if (arg_idx[j] < 0) continue;
     const DCol &c = tmp.cols[arg_idx[j]];
-    if (c.phys == P_STR) ThrowError("Not implemented", "aggregates over VARCHAR are not supported on device");
+    const void *data = c.data;
+    int phys = c.phys;
+    if (c.phys == P_STR) {
+      if (s.aggs[j].kind != A_COUNT)
+        ThrowError("Not implemented", "SUM/MIN/MAX/AVG over VARCHAR are not supported on device");
+      data = c.offsets;
+      phys = P_I64;
+    }
     states[j] = Alloc(e, nslots * sizeof(dev::AggState));
     dev::InitAggStates((dev::AggState *)states[j]->p, nslots, e.stream);
-    ProfScope ps(e, "group_reduce", (double)tmp.n * (PhysSize(c.phys) + 4), tmp.n);
-    dev::GroupReduceColumn((const int32_t *)slot_of->p, c.data, c.phys, c.validity, tmp.n,
+    ProfScope ps(e, "group_reduce", (double)tmp.n * (PhysSize((Phys)phys) + 4), tmp.n);
+    dev::GroupReduceColumn((const int32_t *)slot_of->p, data, phys, c.validity, tmp.n,
                            (dev::AggState *)states[j]->p, e.stream);
   }
   auto list = Alloc(e, nslots * 4);

@@ -162,10 +162,16 @@ __device__ __forceinline__ int64_t pow10_64(int k) {
   return r;
 }
 
+// int128 -> double through the magnitude (no cancellation between the
+// halves); exact rounding whenever |v| < 2^64.
+__device__ __forceinline__ double u128_to_double(u128 m) {
+  uint64_t hi = (uint64_t)(m >> 64), lo = (uint64_t)m;
+  if (hi == 0) return (double)lo;
+  return (double)hi * 18446744073709551616.0 + (double)lo;
+}
 __device__ __forceinline__ double i128_to_double(i128 v) {
-  int64_t lo, hi;
-  sp128(v, lo, hi);
-  return (double)hi * 18446744073709551616.0 + (double)(uint64_t)lo;
+  if (v < 0) return -u128_to_double((u128)0 - (u128)v);
+  return u128_to_double((u128)v);
 }
 
 __device__ __forceinline__ uint64_t splitmix64(uint64_t z) {
@@ -1366,7 +1372,7 @@ __global__ void emit_agg_kernel(EmitDesc D) {
             double v;
             if (A.in_class == VC_F64) v = S.sum_f / (double)S.count;
             else {
-              double sum = (double)S.sum_hi * 18446744073709551616.0 + (double)S.sum_lo;
+              double sum = i128_to_double(mk128((int64_t)S.sum_lo, S.sum_hi));
               double div = (double)S.count;
               for (int k = 0; k < A.avg_scale; k++) div *= 10.0;
               v = sum / div;
