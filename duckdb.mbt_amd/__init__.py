@@ -73,6 +73,7 @@ _sig("duckdb_mbx_last_profile", ctypes.c_void_p, _P)
 _sig("duckdb_mbx_result_raw", _I, _P, _I, _I, _P, _I)
 _sig("duckdb_mbx_append_column", _I, _P, _I, _P, _P, _L)
 _sig("duckdb_mbx_append_commit", _I, _P, _L)
+_sig("duckdb_mbx_hbm_calibrate", _I, _P, _L, _I, ctypes.POINTER(ctypes.c_double))
 
 for _n in ["duckdb_mb_connect"]:
     _sig(_n, _P, _B)
@@ -531,6 +532,12 @@ class Connection:
         s = ctypes.string_at(p).decode()
         lib.duckdb_mbx_free(p)
         return json.loads(s)
+
+    def hbm_calibrate(self, nbytes: int = 2 << 30, iters: int = 5) -> dict:
+        out = (ctypes.c_double * 3)()
+        if not lib.duckdb_mbx_hbm_calibrate(self._h, nbytes, iters, out):
+            raise DuckDBError(_last_error("hbm_calibrate failed"))
+        return {"copy_gbs": out[0], "read_nt_gbs": out[1], "read_gbs": out[2], "bytes": nbytes}
 
     def query_raw(self, sql: str):
         """Runs a query and returns the raw handle (caller destroys); raises on error."""

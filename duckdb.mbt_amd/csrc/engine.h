@@ -127,5 +127,6 @@ struct HostBatch {
 };
 void AppendHostBatch(Connection &c, Table &t, const HostBatch &b);
 void HostColumnPush(HostColumn &col, const Value &v);  // v already of col.type (or NULL)
+void HbmCalibrateConn(Connection &c, int64_t bytes, int iters, double out[3]);
 
 }  // namespace mbx

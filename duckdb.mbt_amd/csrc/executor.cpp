@@ -1727,6 +1727,20 @@ void ExecuteInsertSelect(Connection &c, Table &t, const BoundSelect &s, const st
   CheckError(e);
 }
 
+void HbmCalibrateConn(Connection &c, int64_t bytes, int iters, double out[3]) {
+  Engine &e = Eng(c);
+  bytes &= ~(int64_t)255;
+  void *a = nullptr, *b = nullptr;
+  HIPCHK(hipMalloc(&a, bytes));
+  HIPCHK(hipMalloc(&b, bytes));
+  HIPCHK(hipMemsetAsync(a, 1, bytes, e.stream));
+  HIPCHK(hipMemsetAsync(b, 0, bytes, e.stream));
+  dev::HbmCalibrate(a, b, bytes, iters, out, e.stream);
+  HIPCHK(hipStreamSynchronize(e.stream));
+  HIPCHK(hipFree(a));
+  HIPCHK(hipFree(b));
+}
+
 void AppendHostBatch(Connection &c, Table &t, const HostBatch &b) {
   Engine &e = Eng(c);
   DRel r;

@@ -635,43 +635,61 @@ __device__ __forceinline__ void acc_block_commit(Acc &A, AggState *st, unsigned 
 
 typedef long long v2i64 __attribute__((ext_vector_type(2)));
 typedef int v4i32 __attribute__((ext_vector_type(4)));
-template <typename T>
-struct Vec4;  // 4 consecutive elements through 16-byte loads
-template <>
-struct Vec4<int64_t> {
+template <typename T, bool NT>
+struct Vec4;  // 4 consecutive elements through 16-byte loads (global_load_dwordx4)
+template <bool NT>
+struct Vec4<int64_t, NT> {
   static __device__ __forceinline__ void load(const int64_t *__restrict__ p, int64_t g, int64_t v[4]) {
     const v2i64 *q = (const v2i64 *)p + 2 * g;
-    v2i64 a = __builtin_nontemporal_load(q);
-    v2i64 b = __builtin_nontemporal_load(q + 1);
+    v2i64 a, b;
+    if (NT) {
+      a = __builtin_nontemporal_load(q);
+      b = __builtin_nontemporal_load(q + 1);
+    } else {
+      a = q[0];
+      b = q[1];
+    }
     v[0] = a.x; v[1] = a.y; v[2] = b.x; v[3] = b.y;
   }
 };
-template <>
-struct Vec4<int32_t> {
+template <bool NT>
+struct Vec4<int32_t, NT> {
   static __device__ __forceinline__ void load(const int32_t *__restrict__ p, int64_t g, int64_t v[4]) {
-    v4i32 a = __builtin_nontemporal_load((const v4i32 *)p + g);
+    v4i32 a = NT ? __builtin_nontemporal_load((const v4i32 *)p + g) : ((const v4i32 *)p)[g];
     v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w;
   }
 };
 
+__device__ __forceinline__ void acc_count(Acc &A, bool ok) { A.cnt += ok; }
+
 // MODE 0: aggregate over the predicate column; 1: over a second column;
-// 2: COUNT only.
-template <typename TP, typename TA, int MODE, int UNROLL>
+// 2: COUNT only (no sum/min/max work in the loop).
+// CHUNK: each workgroup streams one contiguous slice (vs a grid-stride sweep).
+template <typename TP, typename TA, int MODE, int UNROLL, bool NT, bool CHUNK>
 __global__ __launch_bounds__(256) void filter_agg_kernel(const TP *__restrict__ p, const TA *__restrict__ a, int64_t n,
                                                          int64_t lo, uint64_t span, AggState *st,
                                                          unsigned long long *cstar) {
   Acc A;
   A.cnt = 0; A.slo = 0; A.shi = 0; A.mn = INT64_MAX; A.mx = INT64_MIN;
-  Acc S = A;  // count_star accumulator when MODE == 1 (aggregate col differs)
   const int64_t ngroups = n >> 2;  // groups of 4 elements
-  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
-  int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  for (; g + (UNROLL - 1) * stride < ngroups; g += UNROLL * stride) {
+  int64_t g, gend, stride;
+  if (CHUNK) {
+    const int64_t per = (ngroups + gridDim.x - 1) / gridDim.x;
+    g = (int64_t)blockIdx.x * per + threadIdx.x;
+    gend = (int64_t)blockIdx.x * per + per;
+    if (gend > ngroups) gend = ngroups;
+    stride = blockDim.x;
+  } else {
+    g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    gend = ngroups;
+    stride = (int64_t)gridDim.x * blockDim.x;
+  }
+  for (; g + (UNROLL - 1) * stride < gend; g += UNROLL * stride) {
     int64_t pv[UNROLL][4], av[UNROLL][4];
 #pragma unroll
     for (int u = 0; u < UNROLL; u++) {
-      Vec4<TP>::load(p, g + u * stride, pv[u]);
-      if (MODE == 1) Vec4<TA>::load(a, g + u * stride, av[u]);
+      Vec4<TP, NT>::load(p, g + u * stride, pv[u]);
+      if (MODE == 1) Vec4<TA, NT>::load(a, g + u * stride, av[u]);
     }
 #pragma unroll
     for (int u = 0; u < UNROLL; u++)
@@ -679,28 +697,30 @@ __global__ __launch_bounds__(256) void filter_agg_kernel(const TP *__restrict__ 
       for (int e = 0; e < 4; e++) {
         int64_t x = pv[u][e];
         bool ok = (uint64_t)(x - lo) <= span;
-        if (MODE == 1) acc_add(A, ok, av[u][e]);
+        if (MODE == 2) acc_count(A, ok);
+        else if (MODE == 1) acc_add(A, ok, av[u][e]);
         else acc_add(A, ok, x);
       }
   }
-  for (; g < ngroups; g += stride) {
+  for (; g < gend; g += stride) {
     int64_t pv[4], av[4];
-    Vec4<TP>::load(p, g, pv);
-    if (MODE == 1) Vec4<TA>::load(a, g, av);
+    Vec4<TP, NT>::load(p, g, pv);
+    if (MODE == 1) Vec4<TA, NT>::load(a, g, av);
 #pragma unroll
     for (int e = 0; e < 4; e++) {
       bool ok = (uint64_t)(pv[e] - lo) <= span;
-      acc_add(A, ok, MODE == 1 ? av[e] : pv[e]);
+      if (MODE == 2) acc_count(A, ok);
+      else acc_add(A, ok, MODE == 1 ? av[e] : pv[e]);
     }
   }
-  // tail (n % 4 elements)
+  // tail (n % 4 elements): handled by the first threads of block 0
   int64_t tail = (ngroups << 2) + (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (tail < n && tail < (ngroups << 2) + 4) {
+  if (tail < n) {
     int64_t x = p[tail];
     bool ok = (uint64_t)(x - lo) <= span;
-    acc_add(A, ok, MODE == 1 ? (int64_t)a[tail] : x);
+    if (MODE == 2) acc_count(A, ok);
+    else acc_add(A, ok, MODE == 1 ? (int64_t)a[tail] : x);
   }
-  (void)S;
   acc_block_commit(A, MODE == 2 ? nullptr : st, cstar, true);
 }
 
@@ -720,33 +740,150 @@ void InitAggStates(AggState *st, int64_t n, hipStream_t s) {
   CHECK_LAUNCH();
 }
 
-template <typename TP, typename TA, int MODE>
-static void LaunchFilterAgg(const void *p, const void *a, int64_t n, int64_t lo, uint64_t span, AggState *st,
-                            unsigned long long *cstar, int grid, hipStream_t s) {
-  hipLaunchKernelGGL((filter_agg_kernel<TP, TA, MODE, 4>), dim3(grid), dim3(256), 0, s, (const TP *)p, (const TA *)a,
-                     n, lo, span, st, cstar);
+// Launch configuration of the fused filter-aggregate kernel.  The defaults
+// were chosen by the A/B sweep recorded in profiles/ (tools/sweep_filter.py);
+// MBX_FA_VARIANT="u<unroll>_<nt|pl>_<gs|ch>_g<blocks per CU>" overrides them
+// for experiments.
+struct FaVariant {
+  int unroll = 4;
+  bool nt = true;
+  bool chunk = false;
+  int blocks_per_cu = 8;
+};
+
+// Defaults from the interleaved 15-round sweep (profiles/r01_filter_sweep.json):
+// COUNT-only prefers one contiguous slice per workgroup with 8 x 32 B of
+// loads in flight per lane; the SUM/MIN/MAX shape prefers the grid-stride
+// sweep with 2 groups per lane at 4 workgroups per CU.  Plain loads beat
+// non-temporal ones on this path.
+static FaVariant FaConfig(int mode) {
+  FaVariant v;
+  if (mode == 2) {
+    v.unroll = 8; v.nt = false; v.chunk = true; v.blocks_per_cu = 8;
+  } else {
+    v.unroll = 2; v.nt = false; v.chunk = false; v.blocks_per_cu = 4;
+  }
+  const char *e = getenv("MBX_FA_VARIANT");
+  if (!e || !*e) return v;
+  int u = 4, g = 8;
+  char m1[8] = {0}, m2[8] = {0};
+  if (sscanf(e, "u%d_%2s_%2s_g%d", &u, m1, m2, &g) == 4) {
+    v.unroll = u;
+    v.nt = m1[0] == 'n';
+    v.chunk = m2[0] == 'c';
+    v.blocks_per_cu = g;
+  }
+  return v;
+}
+
+template <typename TP, typename TA, int MODE, int U, bool NT, bool CH>
+static void LaunchFA(const void *p, const void *a, int64_t n, int64_t lo, uint64_t span, AggState *st,
+                     unsigned long long *cstar, int grid, hipStream_t s) {
+  hipLaunchKernelGGL((filter_agg_kernel<TP, TA, MODE, U, NT, CH>), dim3(grid), dim3(256), 0, s, (const TP *)p,
+                     (const TA *)a, n, lo, span, st, cstar);
   CHECK_LAUNCH();
 }
 
-// FilterAgg: exported with AggState output (count_star separately).
+template <typename TP, typename TA, int MODE>
+static void LaunchFilterAgg(const FaVariant &v, const void *p, const void *a, int64_t n, int64_t lo, uint64_t span,
+                            AggState *st, unsigned long long *cstar, int grid, hipStream_t s) {
+#define FA(U, NT, CH) LaunchFA<TP, TA, MODE, U, NT, CH>(p, a, n, lo, span, st, cstar, grid, s)
+#define FA_NTCH(U)                                          \
+  if (v.nt) { if (v.chunk) FA(U, true, true); else FA(U, true, false); } \
+  else { if (v.chunk) FA(U, false, true); else FA(U, false, false); }
+  if (v.unroll <= 1) { FA_NTCH(1) }
+  else if (v.unroll <= 2) { FA_NTCH(2) }
+  else if (v.unroll <= 4) { FA_NTCH(4) }
+  else { FA_NTCH(8) }
+#undef FA_NTCH
+#undef FA
+}
+
 void FilterAggStates(const void *pcol, int pphys, int64_t lo, int64_t hi, bool has_pred, const void *acol, int aphys,
                      int64_t nrows, AggState *st, unsigned long long *cstar, int grid_blocks, hipStream_t s) {
   if (nrows <= 0) return;
   uint64_t span = has_pred ? (uint64_t)hi - (uint64_t)lo : ~0ull;
   if (!has_pred) lo = INT64_MIN;
-  int grid = grid_blocks > 0 ? grid_blocks : NumCUs() * 8;
   int mode = acol == nullptr ? 2 : (acol == pcol ? 0 : 1);
-  if (pphys == P_I64) {
-    if (mode == 0) LaunchFilterAgg<int64_t, int64_t, 0>(pcol, acol, nrows, lo, span, st, cstar, grid, s);
-    else if (mode == 2) LaunchFilterAgg<int64_t, int64_t, 2>(pcol, acol, nrows, lo, span, st, cstar, grid, s);
-    else if (aphys == P_I64) LaunchFilterAgg<int64_t, int64_t, 1>(pcol, acol, nrows, lo, span, st, cstar, grid, s);
-    else LaunchFilterAgg<int64_t, int32_t, 1>(pcol, acol, nrows, lo, span, st, cstar, grid, s);
-  } else {
-    if (mode == 0) LaunchFilterAgg<int32_t, int32_t, 0>(pcol, acol, nrows, lo, span, st, cstar, grid, s);
-    else if (mode == 2) LaunchFilterAgg<int32_t, int32_t, 2>(pcol, acol, nrows, lo, span, st, cstar, grid, s);
-    else if (aphys == P_I64) LaunchFilterAgg<int32_t, int64_t, 1>(pcol, acol, nrows, lo, span, st, cstar, grid, s);
-    else LaunchFilterAgg<int32_t, int32_t, 1>(pcol, acol, nrows, lo, span, st, cstar, grid, s);
+  if (mode == 2) {
+    const char *cs = getenv("MBX_FA_COUNT_AS_SUM");  // experiment: COUNT through the SUM-shaped loop
+    if (cs && cs[0] == '1') {
+      mode = 0;
+      acol = pcol;
+      aphys = pphys;
+    }
   }
+  FaVariant v = FaConfig(mode);
+  int grid = grid_blocks > 0 ? grid_blocks : NumCUs() * v.blocks_per_cu;
+  int64_t groups = (nrows >> 2) + 1;
+  if (grid > groups) grid = (int)groups;
+  if (pphys == P_I64) {
+    if (mode == 0) LaunchFilterAgg<int64_t, int64_t, 0>(v, pcol, acol, nrows, lo, span, st, cstar, grid, s);
+    else if (mode == 2) LaunchFilterAgg<int64_t, int64_t, 2>(v, pcol, acol, nrows, lo, span, st, cstar, grid, s);
+    else if (aphys == P_I64) LaunchFilterAgg<int64_t, int64_t, 1>(v, pcol, acol, nrows, lo, span, st, cstar, grid, s);
+    else LaunchFilterAgg<int64_t, int32_t, 1>(v, pcol, acol, nrows, lo, span, st, cstar, grid, s);
+  } else {
+    if (mode == 0) LaunchFilterAgg<int32_t, int32_t, 0>(v, pcol, acol, nrows, lo, span, st, cstar, grid, s);
+    else if (mode == 2) LaunchFilterAgg<int32_t, int32_t, 2>(v, pcol, acol, nrows, lo, span, st, cstar, grid, s);
+    else if (aphys == P_I64) LaunchFilterAgg<int32_t, int64_t, 1>(v, pcol, acol, nrows, lo, span, st, cstar, grid, s);
+    else LaunchFilterAgg<int32_t, int32_t, 1>(v, pcol, acol, nrows, lo, span, st, cstar, grid, s);
+  }
+}
+
+__global__ __launch_bounds__(256) void copy_kernel(const float4 *__restrict__ in, float4 *__restrict__ out, int64_t n) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+    out[i] = in[i];
+}
+
+// ---------------------------------------------------------------------------
+// HBM calibration: a float4 copy and an int64 read-reduce, timed with events
+// ---------------------------------------------------------------------------
+template <bool NT>
+__global__ __launch_bounds__(256) void read_sum_kernel(const v2i64 *__restrict__ in, int64_t n, unsigned long long *out) {
+  long long acc = 0;
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  for (; i + 3 * stride < n; i += 4 * stride) {
+    v2i64 a, b, c, d;
+    if (NT) {
+      a = __builtin_nontemporal_load(in + i);
+      b = __builtin_nontemporal_load(in + i + stride);
+      c = __builtin_nontemporal_load(in + i + 2 * stride);
+      d = __builtin_nontemporal_load(in + i + 3 * stride);
+    } else {
+      a = in[i]; b = in[i + stride]; c = in[i + 2 * stride]; d = in[i + 3 * stride];
+    }
+    acc += a.x ^ a.y ^ b.x ^ b.y ^ c.x ^ c.y ^ d.x ^ d.y;
+  }
+  for (; i < n; i += stride) acc += in[i].x ^ in[i].y;
+  if (acc == 0x123456789) atomicAdd(out, 1ull);  // keeps the loads live
+}
+
+void HbmCalibrate(void *buf_a, void *buf_b, int64_t bytes, int iters, double out[3], hipStream_t s) {
+  hipEvent_t e0, e1;
+  (void)hipEventCreate(&e0);
+  (void)hipEventCreate(&e1);
+  unsigned long long *flag = (unsigned long long *)buf_b;
+  int64_t n16 = bytes / 16;
+  int grid = NumCUs() * 8;
+  for (int k = 0; k < 3; k++) {
+    float best = 1e30f;
+    for (int it = 0; it < iters + 1; it++) {
+      (void)hipEventRecord(e0, s);
+      if (k == 0) hipLaunchKernelGGL(copy_kernel, dim3(grid), dim3(256), 0, s, (const float4 *)buf_a, (float4 *)buf_b, n16);
+      else if (k == 1) hipLaunchKernelGGL(read_sum_kernel<true>, dim3(grid), dim3(256), 0, s, (const v2i64 *)buf_a, n16, flag);
+      else hipLaunchKernelGGL(read_sum_kernel<false>, dim3(grid), dim3(256), 0, s, (const v2i64 *)buf_a, n16, flag);
+      (void)hipEventRecord(e1, s);
+      (void)hipEventSynchronize(e1);
+      float ms = 0;
+      (void)hipEventElapsedTime(&ms, e0, e1);
+      if (it > 0 && ms < best) best = ms;  // first launch is a warm-up
+    }
+    double moved = (k == 0 ? 2.0 : 1.0) * (double)bytes;
+    out[k] = moved / (best * 1e-3) / 1e9;
+  }
+  (void)hipEventDestroy(e0);
+  (void)hipEventDestroy(e1);
 }
 
 // ---------------------------------------------------------------------------
@@ -831,9 +968,9 @@ __global__ __launch_bounds__(256) void group_direct_kernel(const TK *__restrict_
     int64_t g0 = seg >> 2, g1 = seg_end >> 2;
     for (int64_t g = g0 + t; g < g1; g += blockDim.x) {
       int64_t kv[4], x0[4], x1[4];
-      Vec4<TK>::load(keys, g, kv);
-      if (NV >= 1) Vec4<TV>::load(v0, g, x0);
-      if (NV >= 2) Vec4<TV>::load(v1, g, x1);
+      Vec4<TK, true>::load(keys, g, kv);
+      if (NV >= 1) Vec4<TV, true>::load(v0, g, x0);
+      if (NV >= 2) Vec4<TV, true>::load(v1, g, x1);
 #pragma unroll
       for (int e = 0; e < 4; e++) {
         int sl = (int)(kv[e] - kmin) * R + rep;
@@ -1313,11 +1450,6 @@ void BitmapAppend(uint64_t *dst, int64_t dst_off, const uint64_t *src, int64_t n
   int64_t words = ((dst_off + n - 1) >> 6) - (dst_off >> 6) + 1;
   hipLaunchKernelGGL(bitmap_append_kernel, dim3(GridFor(words, 256, 4096)), dim3(256), 0, s, dst, dst_off, src, n);
   CHECK_LAUNCH();
-}
-
-__global__ __launch_bounds__(256) void copy_kernel(const float4 *__restrict__ in, float4 *__restrict__ out, int64_t n) {
-  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
-    out[i] = in[i];
 }
 
 void CopyKernel(const void *in, void *out, int64_t nbytes, hipStream_t s) {

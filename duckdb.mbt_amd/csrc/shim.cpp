@@ -918,6 +918,17 @@ char *duckdb_mbx_explain(duckdb_mb_connection *h, const char *sql, int64_t len) 
 }
 void duckdb_mbx_free(void *p) { free(p); }
 
+int32_t duckdb_mbx_hbm_calibrate(duckdb_mb_connection *h, int64_t bytes, int32_t iters, double *out3) {
+  if (!h || !out3) return 0;
+  try {
+    HbmCalibrateConn(h->conn, bytes, iters, out3);
+    return 1;
+  } catch (std::exception &e) {
+    SetError(e.what());
+    return 0;
+  }
+}
+
 char *duckdb_mbx_last_profile(duckdb_mb_connection *h) {
   if (!h) return nullptr;
   const QueryProfile &p = h->conn.last_profile;

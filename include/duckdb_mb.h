@@ -198,6 +198,11 @@ int32_t duckdb_mbx_append_commit(duckdb_mb_appender *app, int64_t count);
  * (enable with config key "mbx_profile"="true"): JSON text, malloc'd. */
 char *duckdb_mbx_last_profile(duckdb_mb_connection *handle);
 
+/* HBM calibration on the connection's device: best-of-`iters` GB/s of a
+ * float4 copy (read+write bytes), a non-temporal int64 read and a plain int64
+ * read over `bytes`-sized buffers -> out3[0..2].  Returns 1 on success. */
+int32_t duckdb_mbx_hbm_calibrate(duckdb_mb_connection *handle, int64_t bytes, int32_t iters, double *out3);
+
 /* Partial aggregate export for multi-GPU combine: the i-th cell of the last
  * materialized result as raw little-endian bytes (HUGEINT: 16 bytes). */
 int32_t duckdb_mbx_result_raw(duckdb_mb_result *result, int32_t col, int32_t row, void *out, int32_t out_len);
