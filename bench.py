@@ -115,15 +115,13 @@ def main():
     for _ in range(args.warmup):
         out = step()
 
-    kernel_ms = []
+    conn.profile_drain()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     t_start = time.perf_counter()
     for _ in range(args.steps):
         out = step()
-        prof = conn.last_profile()
-        kernel_ms.extend(k["ms"] for k in prof["kernels"] if k["name"] == kernel)
         if world > 1 and args.config == "c2":
             gcount = mbx_dist.allreduce_count(int(out[0]), device="cuda")  # RCCL over xGMI: global COUNT(*)
         elif world > 1 and args.config == "c5":
@@ -133,6 +131,7 @@ def main():
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t_start
 
+    kernel_ms = [k["ms"] for k in conn.profile_drain() if k["name"] == kernel]  # HIP events of the timed loop
     t_all = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
     if world > 1:
         dist.all_reduce(t_all, op=dist.ReduceOp.MAX)

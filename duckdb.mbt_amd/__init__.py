@@ -70,6 +70,7 @@ _sig("duckdb_mbx_free", None, _P)
 _sig("duckdb_mbx_device_count", _I)
 _sig("duckdb_mbx_explain", ctypes.c_void_p, _P, ctypes.c_char_p, _L)
 _sig("duckdb_mbx_last_profile", ctypes.c_void_p, _P)
+_sig("duckdb_mbx_profile_drain", ctypes.c_void_p, _P)
 _sig("duckdb_mbx_result_raw", _I, _P, _I, _I, _P, _I)
 _sig("duckdb_mbx_append_column", _I, _P, _I, _P, _P, _L)
 _sig("duckdb_mbx_append_commit", _I, _P, _L)
@@ -538,6 +539,13 @@ class Connection:
         if not lib.duckdb_mbx_hbm_calibrate(self._h, nbytes, iters, out):
             raise DuckDBError(_last_error("hbm_calibrate failed"))
         return {"copy_gbs": out[0], "read_nt_gbs": out[1], "read_gbs": out[2], "bytes": nbytes}
+
+    def profile_drain(self) -> list:
+        import json
+        p = lib.duckdb_mbx_profile_drain(self._h)
+        s = ctypes.string_at(p).decode()
+        lib.duckdb_mbx_free(p)
+        return json.loads(s)
 
     def query_raw(self, sql: str):
         """Runs a query and returns the raw handle (caller destroys); raises on error."""

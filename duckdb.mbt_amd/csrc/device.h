@@ -69,6 +69,7 @@ void GroupAssign(const void *kcol, int kphys, const uint64_t *kvalid, int64_t km
 void GroupReduceColumn(const int32_t *slot_of_row, const void *col, int phys, const uint64_t *valid, int64_t n,
                        AggState *states, hipStream_t s);
 void InitAggStates(AggState *st, int64_t n, hipStream_t s);
+void InitAggStatesCounts(AggState *st, int64_t n, unsigned long long *cs, int64_t nc, hipStream_t s);
 // Compact non-empty slots into the aggregate relation (index list).
 void CompactSlots(const unsigned long long *count_star, int64_t nslots, int32_t *slot_list, int64_t *n_out,
                   hipStream_t s);

@@ -103,6 +103,7 @@ struct Connection {
   Catalog catalog;
   std::shared_ptr<Engine> engine;
   QueryProfile last_profile;
+  std::vector<QueryProfile::Kernel> profile_history;  // drained by duckdb_mbx_profile_drain
   ~Connection();
 };
 

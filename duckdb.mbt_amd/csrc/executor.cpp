@@ -44,21 +44,37 @@ struct Engine {
   hipStream_t stream = nullptr;
   int32_t *d_err = nullptr;
   int64_t *d_scratch = nullptr;  // small device scratch (counts)
-  void *d_small = nullptr;       // 4 KB scratch for small states
+  void *d_small = nullptr;       // 64 KB scratch for small states
+  // pinned host staging for small results: every D2H of a query lands here
+  // and the query pays ONE stream synchronisation
+  uint8_t *h_pinned = nullptr;
+  size_t h_pinned_bytes = 0;
   bool profile = false;
   std::vector<ProfEvent> events;
+  std::vector<std::pair<hipEvent_t, hipEvent_t>> ev_pool;  // reused across queries
+  size_t ev_used = 0;
   std::string plan_text;
+  std::pair<hipEvent_t, hipEvent_t> NextEvents() {
+    if (ev_used == ev_pool.size()) {
+      hipEvent_t a, b;
+      (void)hipEventCreate(&a);
+      (void)hipEventCreate(&b);
+      ev_pool.push_back({a, b});
+    }
+    return ev_pool[ev_used++];
+  }
   ~Engine() {
     if (has_gpu) {
       hipSetDevice(device);
       if (stream) hipStreamSynchronize(stream);
-      for (auto &e : events) {
-        hipEventDestroy(e.a);
-        hipEventDestroy(e.b);
+      for (auto &e : ev_pool) {
+        hipEventDestroy(e.first);
+        hipEventDestroy(e.second);
       }
       if (d_err) hipFree(d_err);
       if (d_scratch) hipFree(d_scratch);
       if (d_small) hipFree(d_small);
+      if (h_pinned) hipHostFree(h_pinned);
       if (stream) hipStreamDestroy(stream);
     }
   }
@@ -87,6 +103,9 @@ std::shared_ptr<Engine> CreateEngine(int device, bool allow_no_gpu) {
   HIPCHK(hipMalloc(&e->d_err, 256));
   HIPCHK(hipMalloc(&e->d_scratch, 4096));
   HIPCHK(hipMalloc(&e->d_small, 1 << 16));
+  HIPCHK(hipMemset(e->d_err, 0, 256));
+  e->h_pinned_bytes = 1 << 20;
+  HIPCHK(hipHostMalloc((void **)&e->h_pinned, e->h_pinned_bytes, hipHostMallocDefault));
   e->has_gpu = true;
   return e;
 }
@@ -109,8 +128,9 @@ struct ProfScope {
     pe.name = name;
     pe.bytes = bytes;
     pe.rows = rows;
-    hipEventCreate(&pe.a);
-    hipEventCreate(&pe.b);
+    auto ev = e.NextEvents();
+    pe.a = ev.first;
+    pe.b = ev.second;
     hipEventRecord(pe.a, e.stream);
     e.events.push_back(pe);
     idx = e.events.size() - 1;
@@ -177,10 +197,16 @@ static DCol ColFromTable(const DevColumn &c) {
 
 static int64_t Words64(int64_t n) { return (n + 63) / 64; }
 
+static void RaiseDeviceError(Engine &e, int32_t err);
+
 static void CheckError(Engine &e) {
   int32_t err = 0;
   HIPCHK(hipMemcpyAsync(&err, e.d_err, sizeof(int32_t), hipMemcpyDeviceToHost, e.stream));
   HIPCHK(hipStreamSynchronize(e.stream));
+  RaiseDeviceError(e, err);
+}
+
+static void RaiseDeviceError(Engine &e, int32_t err) {
   if (err) {
     HIPCHK(hipMemsetAsync(e.d_err, 0, sizeof(int32_t), e.stream));
     switch (err) {
@@ -853,8 +879,7 @@ static DRel Aggregate(Engine &e, const DRel &src, const BoundSelect &s) {
       bool empty = lo > hi;
       dev::AggState *st = (dev::AggState *)e.d_small;
       unsigned long long *cstar = (unsigned long long *)((char *)e.d_small + 1024);
-      dev::InitAggStates(st, 1, e.stream);
-      HIPCHK(hipMemsetAsync(cstar, 0, 8, e.stream));
+      dev::InitAggStatesCounts(st, 1, cstar, 1, e.stream);
       if (!empty) {
         const DCol *P = pcol >= 0 ? &src.cols[pcol] : nullptr;
         const DCol *A = acol >= 0 ? &src.cols[acol] : nullptr;
@@ -1241,8 +1266,65 @@ static DRel ConcatRels(Engine &e, std::vector<DRel> &parts) {
 // ---------------------------------------------------------------------------
 // device -> host
 // ---------------------------------------------------------------------------
+// Small fixed-width results: every column (values + validity words) and the
+// device error word are copied into the pinned arena and the query waits on
+// the stream once.  Returns nullptr when the result does not qualify.
+static ResultPtr ToHostPinned(Engine &e, const DRel &r, const std::vector<std::string> &names, size_t ncols) {
+  const int64_t n = r.n;
+  size_t need = 64;
+  for (size_t c = 0; c < ncols; c++) {
+    const DCol &d = r.cols[c];
+    if (d.phys == P_STR) return nullptr;
+    need += ((size_t)n * PhysSize(d.phys) + 63) & ~(size_t)63;
+    if (d.validity) need += ((size_t)Words64(n) * 8 + 63) & ~(size_t)63;
+  }
+  if (need > e.h_pinned_bytes) return nullptr;
+  std::vector<size_t> data_off(ncols), valid_off(ncols, 0);
+  size_t at = 64;  // [0, 4): error word
+  HIPCHK(hipMemcpyAsync(e.h_pinned, e.d_err, 4, hipMemcpyDeviceToHost, e.stream));
+  for (size_t c = 0; c < ncols; c++) {
+    const DCol &d = r.cols[c];
+    size_t bytes = (size_t)n * PhysSize(d.phys);
+    data_off[c] = at;
+    if (bytes) HIPCHK(hipMemcpyAsync(e.h_pinned + at, d.data, bytes, hipMemcpyDeviceToHost, e.stream));
+    at += (bytes + 63) & ~(size_t)63;
+    if (d.validity) {
+      valid_off[c] = at;
+      size_t vb = (size_t)Words64(n) * 8;
+      if (vb) HIPCHK(hipMemcpyAsync(e.h_pinned + at, d.validity, vb, hipMemcpyDeviceToHost, e.stream));
+      at += (vb + 63) & ~(size_t)63;
+    }
+  }
+  HIPCHK(hipStreamSynchronize(e.stream));
+  int32_t err;
+  memcpy(&err, e.h_pinned, 4);
+  RaiseDeviceError(e, err);
+  auto res = std::make_shared<MaterializedResult>();
+  res->nrows = n;
+  for (size_t c = 0; c < ncols; c++) {
+    const DCol &d = r.cols[c];
+    HostColumn hc;
+    hc.name = names[c];
+    hc.type = d.type;
+    hc.phys = d.phys;
+    size_t bytes = (size_t)n * PhysSize(d.phys);
+    hc.data.assign(e.h_pinned + data_off[c], e.h_pinned + data_off[c] + bytes);
+    if (d.validity && n > 0) {
+      const uint64_t *bm = (const uint64_t *)(e.h_pinned + valid_off[c]);
+      hc.valid.resize(n);
+      for (int64_t i = 0; i < n; i++) hc.valid[i] = (bm[i >> 6] >> (i & 63)) & 1;
+    }
+    res->cols.push_back(std::move(hc));
+  }
+  return res;
+}
+
 static ResultPtr ToHost(Engine &e, const DRel &r, const std::vector<std::string> &names, int64_t offset, int64_t limit,
                         size_t ncols) {
+  if (offset <= 0 && limit < 0) {
+    ResultPtr p = ToHostPinned(e, r, names, ncols);
+    if (p) return p;
+  }
   auto res = std::make_shared<MaterializedResult>();
   int64_t start = std::min(std::max<int64_t>(offset, 0), r.n);
   int64_t n = r.n - start;
@@ -1286,6 +1368,7 @@ static ResultPtr ToHost(Engine &e, const DRel &r, const std::vector<std::string>
     res->cols.push_back(std::move(hc));
   }
   HIPCHK(hipStreamSynchronize(e.stream));
+  CheckError(e);
   return res;
 }
 
@@ -1488,10 +1571,10 @@ static void FinishProfile(Connection &c, Engine &e, double total_ms) {
     k.bytes = ev.bytes;
     k.rows = ev.rows;
     p.kernels.push_back(k);
-    hipEventDestroy(ev.a);
-    hipEventDestroy(ev.b);
+    if (c.profile_history.size() < 100000) c.profile_history.push_back(k);
   }
   e.events.clear();
+  e.ev_used = 0;
 }
 
 ResultPtr ExecuteSelect(Connection &c, const BoundSelect &s) {
@@ -1505,10 +1588,10 @@ ResultPtr ExecuteSelect(Connection &c, const BoundSelect &s) {
   e.profile = c.opts.profile;
   e.events.clear();
   e.plan_text = c.opts.profile ? ExplainSelect(s) : "";
+  e.ev_used = 0;
   DRel r = RunSelectDev(e, c, s);
   std::vector<std::string> names(s.names.begin(), s.names.begin() + VisibleCols(s));
-  ResultPtr res = ToHost(e, r, names, 0, -1, names.size());
-  CheckError(e);
+  ResultPtr res = ToHost(e, r, names, 0, -1, names.size());  // raises pending device errors
   double ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
   FinishProfile(c, e, ms);
   return res;

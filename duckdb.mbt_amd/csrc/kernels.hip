@@ -734,6 +734,26 @@ __global__ void init_agg_states_kernel(AggState *st, int64_t n) {
   }
 }
 
+__global__ void init_states_counts_kernel(AggState *st, int64_t n, unsigned long long *cs, int64_t nc) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n || i < nc; i += (int64_t)gridDim.x * blockDim.x) {
+    if (i < n) {
+      AggState z;
+      z.count = 0; z.sum_lo = 0; z.sum_hi = 0;
+      z.min_i = INT64_MAX; z.max_i = INT64_MIN;
+      z.sum_f = 0; z.min_f = 0xFFFFFFFFFFFFFFFFull; z.max_f = 0;
+      st[i] = z;
+    }
+    if (i < nc) cs[i] = 0;
+  }
+}
+
+void InitAggStatesCounts(AggState *st, int64_t n, unsigned long long *cs, int64_t nc, hipStream_t s) {
+  int64_t m = n > nc ? n : nc;
+  if (m <= 0) return;
+  hipLaunchKernelGGL(init_states_counts_kernel, dim3(GridFor(m, 256, 1024)), dim3(256), 0, s, st, n, cs, nc);
+  CHECK_LAUNCH();
+}
+
 void InitAggStates(AggState *st, int64_t n, hipStream_t s) {
   if (n <= 0) return;
   hipLaunchKernelGGL(init_agg_states_kernel, dim3(GridFor(n, 256, 1024)), dim3(256), 0, s, st, n);

@@ -944,6 +944,21 @@ char *duckdb_mbx_last_profile(duckdb_mb_connection *h) {
   return strdup(j.c_str());
 }
 
+char *duckdb_mbx_profile_drain(duckdb_mb_connection *h) {
+  if (!h) return nullptr;
+  std::string j = "[";
+  for (size_t i = 0; i < h->conn.profile_history.size(); i++) {
+    const auto &k = h->conn.profile_history[i];
+    char buf[256];
+    snprintf(buf, sizeof(buf), "%s{\"name\":\"%s\",\"ms\":%.6f,\"bytes\":%.0f,\"rows\":%lld}", i ? "," : "",
+             k.name.c_str(), k.ms, k.bytes, (long long)k.rows);
+    j += buf;
+  }
+  j += "]";
+  h->conn.profile_history.clear();
+  return strdup(j.c_str());
+}
+
 int32_t duckdb_mbx_result_raw(duckdb_mb_result *r, int32_t col, int32_t row, void *out, int32_t out_len) {
   if (!r || !InRange(r->r, col, row) || !out) return 0;
   const HostColumn &c = r->r->cols[col];

@@ -197,6 +197,8 @@ int32_t duckdb_mbx_append_commit(duckdb_mb_appender *app, int64_t count);
 /* Per-query device profile of the last statement run on this connection
  * (enable with config key "mbx_profile"="true"): JSON text, malloc'd. */
 char *duckdb_mbx_last_profile(duckdb_mb_connection *handle);
+/* Every kernel timing recorded since the previous drain (JSON array), then clears. */
+char *duckdb_mbx_profile_drain(duckdb_mb_connection *handle);
 
 /* HBM calibration on the connection's device: best-of-`iters` GB/s of a
  * float4 copy (read+write bytes), a non-temporal int64 read and a plain int64
