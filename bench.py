@@ -50,6 +50,8 @@ def main():
     ap.add_argument("--config", default="c2", choices=["c2", "c3", "c4", "c5"])
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
+    ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
+                    help="nccl (= RCCL over xGMI) for real runs; gloo only to rehearse N>1 on fewer GPUs")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -59,9 +61,15 @@ def main():
     import torch
     import torch.distributed as dist
 
-    torch.cuda.set_device(local_rank)
+    ndev = torch.cuda.device_count()
+    device = local_rank % max(ndev, 1)  # == local_rank on a full node; folds ranks when rehearsing
+    torch.cuda.set_device(device)
+    coll_dev = "cuda" if args.dist_backend == "nccl" else "cpu"
     if world > 1:
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+        if args.dist_backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", device))
+        else:
+            dist.init_process_group("gloo")
     mbx = load_mbx()
     import importlib.util
     spec = importlib.util.spec_from_file_location("duckdb_mbt_amd_distributed",
@@ -70,7 +78,7 @@ def main():
     spec.loader.exec_module(mbx_dist)
 
     cfg = mbx.Config.create()
-    cfg.set("gpu_device", str(local_rank))
+    cfg.set("gpu_device", str(device))
     cfg.set("mbx_profile", "true")
     r = mbx.connect_with_config(cfg)
     if isinstance(r, mbx.Err):
@@ -123,16 +131,16 @@ def main():
     for _ in range(args.steps):
         out = step()
         if world > 1 and args.config == "c2":
-            gcount = mbx_dist.allreduce_count(int(out[0]), device="cuda")  # RCCL over xGMI: global COUNT(*)
+            gcount = mbx_dist.allreduce_count(int(out[0]), device=coll_dev)  # RCCL over xGMI: global COUNT(*)
         elif world > 1 and args.config == "c5":
-            gcount, gsum = mbx_dist.global_count_sum(int(out[0]), int(out[1]) if out[1] else None, device="cuda")
+            gcount, gsum = mbx_dist.global_count_sum(int(out[0]), int(out[1]) if out[1] else None, device=coll_dev)
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t_start
 
     kernel_ms = [k["ms"] for k in conn.profile_drain() if k["name"] == kernel]  # HIP events of the timed loop
-    t_all = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+    t_all = torch.tensor([elapsed], dtype=torch.float64, device=coll_dev)
     if world > 1:
         dist.all_reduce(t_all, op=dist.ReduceOp.MAX)
     elapsed = float(t_all.item())
@@ -148,6 +156,15 @@ def main():
         parity = {"gpu_count": int(out[0]), "oracle_count": oc, "match": int(out[0]) == oc}
         if args.config == "c5":
             parity.update({"gpu_sum": int(out[1]), "oracle_sum": osum, "match": parity["match"] and int(out[1]) == osum})
+        if world > 1:
+            # global answer (combined over RCCL in the timed loop) vs the sum of the shard oracles
+            g_oracle, g_osum = mbx_dist.global_count_sum(oc, osum, device=coll_dev)
+            parity["global_count"] = gcount
+            parity["global_oracle_count"] = g_oracle
+            parity["match"] = parity["match"] and gcount == g_oracle
+            if args.config == "c5":
+                parity["global_sum"] = gsum
+                parity["match"] = parity["match"] and gsum == g_osum
 
     result = None
     if rank == 0:
@@ -159,7 +176,9 @@ def main():
         pmc = os.path.join(HERE, "profiles", "pmc_traffic.json")
         if os.path.exists(pmc):
             try:
-                traffic = json.load(open(pmc)).get(kernel, {}).get("hbm_bytes_per_launch")
+                ent = json.load(open(pmc)).get(kernel, {})
+                # PMC pass was taken at the default 1e9-row size; only valid for that size
+                traffic = ent.get("hbm_bytes_per_launch") if n == ent.get("rows", 1_000_000_000) else None
             except Exception:
                 traffic = None
         result = {
@@ -176,7 +195,8 @@ def main():
             "dtype": "int64",
             "data": "synthetic: x = splitmix64(42 + i) mod 50 + 1 generated on device (no dataset)",
             "config": {"workload": workload, "rows_per_gpu": n, "sql": sql,
-                       "parallelism": f"row-range shards x{world}" + (" + RCCL all-reduce" if world > 1 else "")},
+                       "parallelism": f"row-range shards x{world}" + ((" + RCCL all-reduce/all-gather" if args.dist_backend == "nccl"
+                                                                          else " + gloo collectives (rehearsal)") if world > 1 else "")},
             "roofline": {
                 "bound": "hbm",
                 "kernel": kernel,

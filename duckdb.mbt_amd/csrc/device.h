@@ -48,7 +48,8 @@ struct AggState {
 // aggregate column a (P_I32 / P_I64; == p allowed) or none (COUNT(*) only).
 // count_star += selected rows; st accumulates count/sum/min/max of a.
 void FilterAggStates(const void *pcol, int pphys, int64_t lo, int64_t hi, bool has_pred, const void *acol, int aphys,
-                     int64_t nrows, AggState *st, unsigned long long *cstar, int grid_blocks, hipStream_t s);
+                     int64_t nrows, AggState *st, unsigned long long *cstar, int grid_blocks, hipStream_t s,
+                     bool need_minmax = true, uint64_t sum_maxabs = ~0ull);
 
 // --- fused GROUP BY on a small-range integer key (config C3) -------------
 // key in [kmin, kmin + nk), no nulls; up to 2 value columns of one phys.

@@ -893,8 +893,19 @@ static DRel Aggregate(Engine &e, const DRel &src, const BoundSelect &s) {
         if (A && A != P) bytes += (double)src.n * PhysSize(A->phys);
         if (P) {
           ProfScope ps(e, "filter_agg", bytes, src.n);
+          bool need_mm = false;
+          for (auto &a : s.aggs) need_mm |= a.kind == A_MIN || a.kind == A_MAX;
+          // zone-map bound on |value| of the aggregated column (lets the kernel
+          // keep int64 per-lane partial sums; ~0 = unknown)
+          uint64_t maxabs = ~0ull;
+          if (A && A->table_col && A->table_col->stats_valid) {
+            i128 m1 = A->table_col->imin < 0 ? -A->table_col->imin : A->table_col->imin;
+            i128 m2 = A->table_col->imax < 0 ? -A->table_col->imax : A->table_col->imax;
+            i128 m = m1 > m2 ? m1 : m2;
+            if (m <= (i128)INT64_MAX) maxabs = (uint64_t)m;
+          }
           dev::FilterAggStates(P->data, P->phys, (int64_t)lo, (int64_t)hi, pcol >= 0, A ? A->data : nullptr,
-                               A ? A->phys : P_I64, src.n, st, cstar, 0, e.stream);
+                               A ? A->phys : P_I64, src.n, st, cstar, 0, e.stream, need_mm, maxabs);
         } else {
           // COUNT(*) without predicate: the row count is known
           unsigned long long c = (unsigned long long)src.n;

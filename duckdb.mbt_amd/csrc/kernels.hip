@@ -660,13 +660,40 @@ struct Vec4<int32_t, NT> {
   }
 };
 
+// Row-pair loads: lane l of a wave reads rows {2l, 2l+1} of a 128-row wave
+// step, so ONE load instruction covers a contiguous 1 KiB (int64) or 512 B
+// (int32) with no holes — every cache line is requested once.  (Vec4 above
+// makes each lane read 32 contiguous bytes as two 16-B loads: each load then
+// spans 2 KiB with 16-B gaps and every line is requested twice.)
+typedef int v2i32 __attribute__((ext_vector_type(2)));
+template <typename T, bool NT>
+struct Pair;
+template <bool NT>
+struct Pair<int64_t, NT> {
+  static __device__ __forceinline__ void load(const int64_t *__restrict__ p, int64_t pi, int64_t &a, int64_t &b) {
+    const v2i64 *q = (const v2i64 *)p + pi;
+    v2i64 v = NT ? __builtin_nontemporal_load(q) : *q;
+    a = v.x;
+    b = v.y;
+  }
+};
+template <bool NT>
+struct Pair<int32_t, NT> {
+  static __device__ __forceinline__ void load(const int32_t *__restrict__ p, int64_t pi, int64_t &a, int64_t &b) {
+    const v2i32 *q = (const v2i32 *)p + pi;
+    v2i32 v = NT ? __builtin_nontemporal_load(q) : *q;
+    a = v.x;
+    b = v.y;
+  }
+};
+
 __device__ __forceinline__ void acc_count(Acc &A, bool ok) { A.cnt += ok; }
 
 // MODE 0: aggregate over the predicate column; 1: over a second column;
 // 2: COUNT only (no sum/min/max work in the loop).
 // CHUNK: each workgroup streams one contiguous slice (vs a grid-stride sweep).
 template <typename TP, typename TA, int MODE, int UNROLL, bool NT, bool CHUNK>
-__global__ __launch_bounds__(256) void filter_agg_kernel(const TP *__restrict__ p, const TA *__restrict__ a, int64_t n,
+__global__ __launch_bounds__(256) void filter_agg_v4_kernel(const TP *__restrict__ p, const TA *__restrict__ a, int64_t n,
                                                          int64_t lo, uint64_t span, AggState *st,
                                                          unsigned long long *cstar) {
   Acc A;
@@ -724,6 +751,187 @@ __global__ __launch_bounds__(256) void filter_agg_kernel(const TP *__restrict__ 
   acc_block_commit(A, MODE == 2 ? nullptr : st, cstar, true);
 }
 
+// Row-pair version (default): U pair-loads in flight per lane.  Grid-stride
+// over pairs, or one contiguous slice of pairs per workgroup (CHUNK).
+template <typename TP, typename TA, int MODE, int UNROLL, bool NT, bool CHUNK>
+__global__ __launch_bounds__(256) void filter_agg_kernel(const TP *__restrict__ p, const TA *__restrict__ a, int64_t n,
+                                                         int64_t lo, uint64_t span, AggState *st,
+                                                         unsigned long long *cstar) {
+  Acc A;
+  A.cnt = 0; A.slo = 0; A.shi = 0; A.mn = INT64_MAX; A.mx = INT64_MIN;
+  const int64_t npairs = n >> 1;
+  int64_t g, gend, stride;
+  if (CHUNK) {
+    const int64_t per = (npairs + gridDim.x - 1) / gridDim.x;
+    g = (int64_t)blockIdx.x * per + threadIdx.x;
+    gend = (int64_t)blockIdx.x * per + per;
+    if (gend > npairs) gend = npairs;
+    stride = blockDim.x;
+  } else {
+    g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    gend = npairs;
+    stride = (int64_t)gridDim.x * blockDim.x;
+  }
+  for (; g + (UNROLL - 1) * stride < gend; g += UNROLL * stride) {
+    int64_t p0[UNROLL], p1[UNROLL], a0[UNROLL], a1[UNROLL];
+#pragma unroll
+    for (int u = 0; u < UNROLL; u++) {
+      Pair<TP, NT>::load(p, g + u * stride, p0[u], p1[u]);
+      if (MODE == 1) Pair<TA, NT>::load(a, g + u * stride, a0[u], a1[u]);
+    }
+#pragma unroll
+    for (int u = 0; u < UNROLL; u++) {
+      bool ok0 = (uint64_t)(p0[u] - lo) <= span, ok1 = (uint64_t)(p1[u] - lo) <= span;
+      if (MODE == 2) {
+        acc_count(A, ok0);
+        acc_count(A, ok1);
+      } else if (MODE == 1) {
+        acc_add(A, ok0, a0[u]);
+        acc_add(A, ok1, a1[u]);
+      } else {
+        acc_add(A, ok0, p0[u]);
+        acc_add(A, ok1, p1[u]);
+      }
+    }
+  }
+  for (; g < gend; g += stride) {
+    int64_t x0, x1, y0 = 0, y1 = 0;
+    Pair<TP, NT>::load(p, g, x0, x1);
+    if (MODE == 1) Pair<TA, NT>::load(a, g, y0, y1);
+    bool ok0 = (uint64_t)(x0 - lo) <= span, ok1 = (uint64_t)(x1 - lo) <= span;
+    if (MODE == 2) {
+      acc_count(A, ok0);
+      acc_count(A, ok1);
+    } else {
+      acc_add(A, ok0, MODE == 1 ? y0 : x0);
+      acc_add(A, ok1, MODE == 1 ? y1 : x1);
+    }
+  }
+  // odd last row: first thread of block 0
+  if ((n & 1) && blockIdx.x == 0 && threadIdx.x == 0) {
+    int64_t x = p[n - 1];
+    bool ok = (uint64_t)(x - lo) <= span;
+    if (MODE == 2) acc_count(A, ok);
+    else acc_add(A, ok, MODE == 1 ? (int64_t)a[n - 1] : x);
+  }
+  acc_block_commit(A, MODE == 2 ? nullptr : st, cstar, true);
+}
+
+// LDS-DMA streaming version: each wave owns a ring of DEPTH slots of 1 KiB
+// (64 lanes x 16 B, global_load_lds_dwordx4) per column; waves walk the
+// column's 1-KiB pieces grid-stride, so the whole chip streams through one
+// contiguous window.  The oldest slot is consumed once at most DEPTH-1 newer
+// pieces are pending (counted vmcnt, never 0 in the loop).  All LDS — ring
+// and the final block reduction — lives in ONE __shared__ array (a second
+// __shared__ object makes hipcc drain vmcnt before every ds_read).
+// A piece is 128 int64 rows or 256 int32 rows; rows past the last whole
+// piece are handled by wave 0 of block 0.  MODE 1 needs TP == TA here.
+// MM: MIN/MAX requested.  NARROW: the host proved from the column's zone map
+// that no lane's int64 partial sum can overflow, so the per-row int128 carry
+// chain collapses to one int64 add (sign-extended once, before the reduce).
+__device__ __forceinline__ void acc_row(Acc &A, bool ok, int64_t v, bool mm, bool narrow) {
+  if (!narrow) {
+    if (mm) {
+      acc_add(A, ok, v);
+    } else {
+      A.cnt += ok;
+      int64_t vv = ok ? v : 0;
+      uint64_t nlo = A.slo + (uint64_t)vv;
+      A.shi += (vv >> 63) + (nlo < A.slo ? 1 : 0);
+      A.slo = nlo;
+    }
+    return;
+  }
+  A.cnt += ok;
+  A.slo += (uint64_t)(ok ? v : 0);
+  if (mm) {
+    A.mn = ok && v < A.mn ? v : A.mn;
+    A.mx = ok && v > A.mx ? v : A.mx;
+  }
+}
+
+template <typename T, int MODE, int DEPTH, bool MM, bool NARROW>
+__global__ __launch_bounds__(256) void filter_agg_lds_kernel(const T *__restrict__ p, const T *__restrict__ a, int64_t n,
+                                                             int64_t lo, uint64_t span, AggState *st,
+                                                             unsigned long long *cstar) {
+  constexpr int NS = MODE == 1 ? 2 : 1;
+  constexpr int RPL = 16 / (int)sizeof(T);
+  constexpr int64_t RP = 64 * RPL;
+  __shared__ __attribute__((aligned(16))) v2i64 ring[4 * NS * DEPTH * 64];
+  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int64_t npieces = n / RP;
+  const int64_t nw = (int64_t)gridDim.x * 4;
+  int64_t pc = (int64_t)blockIdx.x * 4 + w;
+  v2i64 *slot0 = ring + w * NS * DEPTH * 64;
+  const v2i64 *P = (const v2i64 *)p, *A2 = (const v2i64 *)a;
+  Acc A;
+  A.cnt = 0; A.slo = 0; A.shi = 0; A.mn = INT64_MAX; A.mx = INT64_MIN;
+#pragma unroll
+  for (int d = 0; d < DEPTH; d++) {
+    int64_t q = pc + d * nw;
+    q = q < npieces ? q : 0;  // keep the per-slot load count uniform (dummy piece 0)
+    if (npieces > 0) {
+      __builtin_amdgcn_global_load_lds((const void *)(P + q * 64 + lane), (void *)(slot0 + d * 64), 16, 0, 2);
+      if (NS == 2)
+        __builtin_amdgcn_global_load_lds((const void *)(A2 + q * 64 + lane), (void *)(slot0 + (DEPTH + d) * 64), 16, 0, 2);
+    }
+  }
+  int k = 0;
+  for (; pc < npieces; pc += nw) {
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NS * (DEPTH - 1)) : "memory");
+    v2i64 x = slot0[k * 64 + lane];
+    v2i64 y;
+    if (NS == 2) y = slot0[(DEPTH + k) * 64 + lane];
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    int64_t q = pc + DEPTH * nw;
+    q = q < npieces ? q : pc;  // past the end: re-read the piece just consumed
+    __builtin_amdgcn_global_load_lds((const void *)(P + q * 64 + lane), (void *)(slot0 + k * 64), 16, 0, 2);
+    if (NS == 2)
+      __builtin_amdgcn_global_load_lds((const void *)(A2 + q * 64 + lane), (void *)(slot0 + (DEPTH + k) * 64), 16, 0, 2);
+    if (sizeof(T) == 8) {
+      bool ok0 = (uint64_t)(x.x - lo) <= span, ok1 = (uint64_t)(x.y - lo) <= span;
+      if (MODE == 2) {
+        acc_count(A, ok0);
+        acc_count(A, ok1);
+      } else {
+        acc_row(A, ok0, MODE == 1 ? y.x : x.x, MM, NARROW);
+        acc_row(A, ok1, MODE == 1 ? y.y : x.y, MM, NARROW);
+      }
+    } else {
+      const int *xi = (const int *)&x, *yi = (const int *)&y;
+#pragma unroll
+      for (int e = 0; e < 4; e++) {
+        bool ok = (uint64_t)((int64_t)xi[e] - lo) <= span;
+        if (MODE == 2) acc_count(A, ok);
+        else acc_row(A, ok, (int64_t)(MODE == 1 ? yi[e] : xi[e]), MM, NARROW);
+      }
+    }
+    k = k + 1 == DEPTH ? 0 : k + 1;
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  if (blockIdx.x == 0 && w == 0) {
+    for (int64_t i = npieces * RP + lane; i < n; i += 64) {
+      int64_t xv = p[i];
+      bool ok = (uint64_t)(xv - lo) <= span;
+      if (MODE == 2) acc_count(A, ok);
+      else acc_row(A, ok, MODE == 1 ? (int64_t)a[i] : xv, MM, NARROW);
+    }
+  }
+  if (NARROW) A.shi = (int64_t)A.slo >> 63;
+  // block reduction through the same LDS array
+  acc_wave_reduce(A);
+  __syncthreads();
+  Acc *part = (Acc *)ring;
+  if (lane == 0) part[w] = A;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    Acc T0 = part[0];
+    for (int i = 1; i < 4; i++) acc_merge(T0, part[i]);
+    if (cstar) atomicAdd(cstar, (unsigned long long)T0.cnt);
+    if (MODE != 2 && st) agg_state_atomic(st, T0);
+  }
+}
+
 __global__ void init_agg_states_kernel(AggState *st, int64_t n) {
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
     AggState z;
@@ -765,48 +973,78 @@ void InitAggStates(AggState *st, int64_t n, hipStream_t s) {
 // MBX_FA_VARIANT="u<unroll>_<nt|pl>_<gs|ch>_g<blocks per CU>" overrides them
 // for experiments.
 struct FaVariant {
-  int unroll = 4;
+  int unroll = 8;
   bool nt = true;
-  bool chunk = false;
-  int blocks_per_cu = 8;
+  bool chunk = true;
+  int blocks_per_cu = 1;
+  bool pairs = true;  // row-pair layout (false: the older 32-B-per-lane Vec4 layout)
+  int lds_depth = 8;  // >0: LDS-DMA ring of this depth per wave (blocks_per_cu then counts 256-thread blocks)
 };
 
-// Defaults from the interleaved 15-round sweep (profiles/r01_filter_sweep.json):
-// COUNT-only prefers one contiguous slice per workgroup with 8 x 32 B of
-// loads in flight per lane; the SUM/MIN/MAX shape prefers the grid-stride
-// sweep with 2 groups per lane at 4 workgroups per CU.  Plain loads beat
-// non-temporal ones on this path.
+// Default: the LDS-DMA stream, 8 x 1 KiB slots per wave, one 256-thread
+// workgroup per CU (one wave per SIMD) — 6.84 TB/s median on the 1e9-row
+// COUNT vs 6.06 for the best register-load shape (profiles/r01_filter_sweep_lds.json).
+// MBX_FA_VARIANT overrides it: "d<depth>_g<blocks per CU>" (LDS-DMA) or
+// "u<unroll>_<nt|pl>_<gs|ch>_g<blocks per CU>[_v4]" (register loads).
 static FaVariant FaConfig(int mode) {
   FaVariant v;
-  if (mode == 2) {
-    v.unroll = 8; v.nt = false; v.chunk = true; v.blocks_per_cu = 8;
-  } else {
-    v.unroll = 2; v.nt = false; v.chunk = false; v.blocks_per_cu = 4;
-  }
+  (void)mode;
   const char *e = getenv("MBX_FA_VARIANT");
   if (!e || !*e) return v;
-  int u = 4, g = 8;
+  int u = 8, g = 4;
   char m1[8] = {0}, m2[8] = {0};
-  if (sscanf(e, "u%d_%2s_%2s_g%d", &u, m1, m2, &g) == 4) {
+  if (sscanf(e, "d%d_g%d", &u, &g) == 2) {
+    v.lds_depth = u;
+    v.blocks_per_cu = g;
+  } else if (sscanf(e, "u%d_%2s_%2s_g%d", &u, m1, m2, &g) == 4) {
+    v.lds_depth = 0;
     v.unroll = u;
     v.nt = m1[0] == 'n';
     v.chunk = m2[0] == 'c';
     v.blocks_per_cu = g;
+    v.pairs = strstr(e, "_v4") == nullptr;
   }
   return v;
 }
 
+static bool g_fa_pairs = true;
+static bool g_fa_mm = true, g_fa_narrow = false;  // per launch, set by FilterAggStates
 template <typename TP, typename TA, int MODE, int U, bool NT, bool CH>
 static void LaunchFA(const void *p, const void *a, int64_t n, int64_t lo, uint64_t span, AggState *st,
                      unsigned long long *cstar, int grid, hipStream_t s) {
-  hipLaunchKernelGGL((filter_agg_kernel<TP, TA, MODE, U, NT, CH>), dim3(grid), dim3(256), 0, s, (const TP *)p,
-                     (const TA *)a, n, lo, span, st, cstar);
+  if (g_fa_pairs)
+    hipLaunchKernelGGL((filter_agg_kernel<TP, TA, MODE, U, NT, CH>), dim3(grid), dim3(256), 0, s, (const TP *)p,
+                       (const TA *)a, n, lo, span, st, cstar);
+  else
+    hipLaunchKernelGGL((filter_agg_v4_kernel<TP, TA, MODE, U, NT, CH>), dim3(grid), dim3(256), 0, s, (const TP *)p,
+                       (const TA *)a, n, lo, span, st, cstar);
+  CHECK_LAUNCH();
+}
+
+template <typename T, int MODE, int DEPTH>
+static void LaunchFALds(const void *p, const void *a, int64_t n, int64_t lo, uint64_t span, AggState *st,
+                        unsigned long long *cstar, int grid, hipStream_t s) {
+#define FAL(MM, NW)                                                                                                   \
+  hipLaunchKernelGGL((filter_agg_lds_kernel<T, MODE, DEPTH, MM, NW>), dim3(grid), dim3(256), 0, s, (const T *)p,   \
+                     (const T *)a, n, lo, span, st, cstar)
+  if (MODE == 2) FAL(false, false);
+  else if (g_fa_mm) { if (g_fa_narrow) FAL(true, true); else FAL(true, false); }
+  else { if (g_fa_narrow) FAL(false, true); else FAL(false, false); }
+#undef FAL
   CHECK_LAUNCH();
 }
 
 template <typename TP, typename TA, int MODE>
 static void LaunchFilterAgg(const FaVariant &v, const void *p, const void *a, int64_t n, int64_t lo, uint64_t span,
                             AggState *st, unsigned long long *cstar, int grid, hipStream_t s) {
+  if constexpr (MODE != 1 || sizeof(TP) == sizeof(TA)) {
+    if (v.lds_depth > 0) {
+      if (v.lds_depth <= 4) LaunchFALds<TP, MODE, 4>(p, a, n, lo, span, st, cstar, grid, s);
+      else if (v.lds_depth <= 8) LaunchFALds<TP, MODE, 8>(p, a, n, lo, span, st, cstar, grid, s);
+      else LaunchFALds<TP, MODE, 16>(p, a, n, lo, span, st, cstar, grid, s);
+      return;
+    }
+  }
 #define FA(U, NT, CH) LaunchFA<TP, TA, MODE, U, NT, CH>(p, a, n, lo, span, st, cstar, grid, s)
 #define FA_NTCH(U)                                          \
   if (v.nt) { if (v.chunk) FA(U, true, true); else FA(U, true, false); } \
@@ -820,7 +1058,8 @@ static void LaunchFilterAgg(const FaVariant &v, const void *p, const void *a, in
 }
 
 void FilterAggStates(const void *pcol, int pphys, int64_t lo, int64_t hi, bool has_pred, const void *acol, int aphys,
-                     int64_t nrows, AggState *st, unsigned long long *cstar, int grid_blocks, hipStream_t s) {
+                     int64_t nrows, AggState *st, unsigned long long *cstar, int grid_blocks, hipStream_t s,
+                     bool need_minmax, uint64_t sum_maxabs) {
   if (nrows <= 0) return;
   uint64_t span = has_pred ? (uint64_t)hi - (uint64_t)lo : ~0ull;
   if (!has_pred) lo = INT64_MIN;
@@ -834,9 +1073,22 @@ void FilterAggStates(const void *pcol, int pphys, int64_t lo, int64_t hi, bool h
     }
   }
   FaVariant v = FaConfig(mode);
+  g_fa_pairs = v.pairs;
   int grid = grid_blocks > 0 ? grid_blocks : NumCUs() * v.blocks_per_cu;
   int64_t groups = (nrows >> 2) + 1;
   if (grid > groups) grid = (int)groups;
+  g_fa_mm = need_minmax;
+  // LDS-DMA kernel: a lane sees at most (ceil(pieces / waves) + 1) pieces of
+  // 16 B, i.e. that many times 2 (int64) or 4 (int32) rows, tail included.
+  {
+    const int asz = (mode == 1 ? aphys : pphys) == P_I64 ? 8 : 4;
+    const int64_t rp = 64 * (16 / (pphys == P_I64 ? 8 : 4));
+    const int64_t waves = (int64_t)grid * 4, pieces = nrows / rp;
+    const int64_t rows_per_lane = ((pieces + waves - 1) / waves + 1) * (16 / (pphys == P_I64 ? 8 : 4));
+    (void)asz;
+    g_fa_narrow = sum_maxabs <= (uint64_t)INT64_MAX &&
+                  (unsigned __int128)sum_maxabs * (unsigned __int128)rows_per_lane < ((unsigned __int128)1 << 63);
+  }
   if (pphys == P_I64) {
     if (mode == 0) LaunchFilterAgg<int64_t, int64_t, 0>(v, pcol, acol, nrows, lo, span, st, cstar, grid, s);
     else if (mode == 2) LaunchFilterAgg<int64_t, int64_t, 2>(v, pcol, acol, nrows, lo, span, st, cstar, grid, s);
@@ -984,27 +1236,47 @@ __global__ __launch_bounds__(256) void group_direct_kernel(const TK *__restrict_
   int64_t end = begin + chunk < n ? begin + chunk : n;
   for (int64_t seg = begin; seg < end; seg += seg_rows) {
     int64_t seg_end = seg + seg_rows < end ? seg + seg_rows : end;
-    // vectorised body: groups of 4 rows, chunk/seg boundaries are multiples of 4
-    int64_t g0 = seg >> 2, g1 = seg_end >> 2;
-    for (int64_t g = g0 + t; g < g1; g += blockDim.x) {
-      int64_t kv[4], x0[4], x1[4];
-      Vec4<TK, true>::load(keys, g, kv);
-      if (NV >= 1) Vec4<TV, true>::load(v0, g, x0);
-      if (NV >= 2) Vec4<TV, true>::load(v1, g, x1);
+    // row-pair body (chunk/seg boundaries are multiples of 4): each load
+    // instruction covers a contiguous 512 B (int32) / 1 KiB (int64) span;
+    // GU pairs per lane are loaded before any LDS atomic is issued.
+    constexpr int GU = 4;
+    int64_t g0 = seg >> 1, g1 = seg_end >> 1;
+    auto row = [&](int64_t k, int64_t a, int64_t b) {
+      int sl = (int)(k - kmin) * R + rep;
+      atomicAdd(&cnt[sl], 1u);
+      if (NV >= 1) atomicAdd((unsigned long long *)&sum0[sl], (unsigned long long)a);
+      if (NV >= 2) atomicAdd((unsigned long long *)&sum1[sl], (unsigned long long)b);
+      if (MM) {
+        atomicMin(&mn0[sl], (long long)a); atomicMax(&mx0[sl], (long long)a);
+        if (NV >= 2) { atomicMin(&mn1[sl], (long long)b); atomicMax(&mx1[sl], (long long)b); }
+      }
+    };
+    int64_t g = g0 + t;
+    for (; g + (GU - 1) * (int64_t)blockDim.x < g1; g += GU * (int64_t)blockDim.x) {
+      int64_t k0[GU], k1[GU], a0[GU], a1[GU], b0[GU], b1[GU];
 #pragma unroll
-      for (int e = 0; e < 4; e++) {
-        int sl = (int)(kv[e] - kmin) * R + rep;
-        atomicAdd(&cnt[sl], 1u);
-        if (NV >= 1) atomicAdd((unsigned long long *)&sum0[sl], (unsigned long long)x0[e]);
-        if (NV >= 2) atomicAdd((unsigned long long *)&sum1[sl], (unsigned long long)x1[e]);
-        if (MM) {
-          atomicMin(&mn0[sl], (long long)x0[e]); atomicMax(&mx0[sl], (long long)x0[e]);
-          if (NV >= 2) { atomicMin(&mn1[sl], (long long)x1[e]); atomicMax(&mx1[sl], (long long)x1[e]); }
-        }
+      for (int u = 0; u < GU; u++) {
+        int64_t gi = g + u * (int64_t)blockDim.x;
+        Pair<TK, true>::load(keys, gi, k0[u], k1[u]);
+        if (NV >= 1) Pair<TV, true>::load(v0, gi, a0[u], a1[u]);
+        if (NV >= 2) Pair<TV, true>::load(v1, gi, b0[u], b1[u]);
+      }
+#pragma unroll
+      for (int u = 0; u < GU; u++) {
+        row(k0[u], NV >= 1 ? a0[u] : 0, NV >= 2 ? b0[u] : 0);
+        row(k1[u], NV >= 1 ? a1[u] : 0, NV >= 2 ? b1[u] : 0);
       }
     }
-    // scalar tail of the last segment (end not multiple of 4 only at n)
-    for (int64_t i = (g1 << 2) + t; i < seg_end; i += blockDim.x) {
+    for (; g < g1; g += blockDim.x) {
+      int64_t k0, k1, a0 = 0, a1 = 0, b0 = 0, b1 = 0;
+      Pair<TK, true>::load(keys, g, k0, k1);
+      if (NV >= 1) Pair<TV, true>::load(v0, g, a0, a1);
+      if (NV >= 2) Pair<TV, true>::load(v1, g, b0, b1);
+      row(k0, a0, b0);
+      row(k1, a1, b1);
+    }
+    // odd last row (end is odd only at n)
+    for (int64_t i = (g1 << 1) + t; i < seg_end; i += blockDim.x) {
       int sl = (int)((int64_t)keys[i] - kmin) * R + rep;
       atomicAdd(&cnt[sl], 1u);
       if (NV >= 1) atomicAdd((unsigned long long *)&sum0[sl], (unsigned long long)(int64_t)v0[i]);

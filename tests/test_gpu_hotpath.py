@@ -227,3 +227,34 @@ def test_ctas_and_types_roundtrip(conn):
     assert res.column_types == ["BigInt", "Integer", "SmallInt", "Double", "Boolean", "Decimal"]
     assert res.rows[0] == ["-5", "-5", "-5", "-1.25", "false", "-5.000"]
     assert res.rows[9] == ["4", "4", "4", "1.0", "true", "4.000"]
+
+
+# ---- every fused filter-aggregate launch shape gives the same bits ----------
+FA_VARIANTS = ["", "u8_nt_ch_g4", "u4_nt_gs_g16", "u2_pl_gs_g4_v4", "u8_nt_ch_g4_v4", "d4_g1", "d8_g1", "d16_g2"]
+
+
+@pytest.mark.parametrize("variant", FA_VARIANTS)
+def test_filter_agg_variants_parity(conn, oracle, monkeypatch, variant):
+    monkeypatch.setenv("MBX_FA_VARIANT", variant)
+    for n in (0, 1, 127, 128, 129, 255, 257, 4099, 1_000_003):
+        x = oracle.synth_i64(n, 42, 0, 50, 1)
+        v = oracle.synth_i64(n, 9, 0, 1000, -500)
+        q(conn, "DROP TABLE IF EXISTS fv")
+        q(conn, f"CREATE TABLE fv AS SELECT mbx_synth(42, i, 50) + 1 AS x, CAST(mbx_synth(42, i, 50) + 1 AS INTEGER) AS y, "
+                f"mbx_synth(9, i, 1000) - 500 AS v, CAST(mbx_synth(9, i, 1000) - 500 AS INTEGER) AS w "
+                f"FROM range({n}) tbl(i)")
+        m = x > 24
+        exp_cnt = int(m.sum())
+        for sql, vals in [("SELECT COUNT(*) FROM fv WHERE x > 24", None),
+                          ("SELECT COUNT(*), SUM(x), MIN(x), MAX(x) FROM fv WHERE x > 24", x),
+                          ("SELECT COUNT(*), SUM(v), MIN(v), MAX(v) FROM fv WHERE x > 24", v),
+                          ("SELECT COUNT(*) FROM fv WHERE y > 24", None),
+                          ("SELECT COUNT(*), SUM(y), MIN(y), MAX(y) FROM fv WHERE y > 24", x),
+                          ("SELECT COUNT(*), SUM(w), MIN(w), MAX(w) FROM fv WHERE y > 24", v),
+                          ("SELECT COUNT(*), SUM(v) FROM fv WHERE y > 24", v)]:
+            got = one(conn, sql)
+            assert int(got[0]) == exp_cnt, (variant, n, sql)
+            if vals is not None and exp_cnt:
+                sel = vals[m]
+                want = [int(sel.sum(dtype=np.int64)), int(sel.min()), int(sel.max())][:len(got) - 1]
+                assert [int(g) for g in got[1:]] == want, (variant, n, sql)

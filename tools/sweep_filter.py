@@ -23,7 +23,10 @@ variants = [f"u{u}_{nt}_{ch}_g{g}" for u in (2, 4, 8) for nt in ("nt", "pl") for
 if os.environ.get("SWEEP_VARIANTS"):
     variants = os.environ["SWEEP_VARIANTS"].split(",")
 rounds = int(os.environ.get("SWEEP_ROUNDS", "5"))
-sqls = {"count": "SELECT COUNT(*) FROM t WHERE x > 24", "count_sum": "SELECT COUNT(*), SUM(x), MIN(x), MAX(x) FROM t WHERE x > 24"}
+sqls = {"count": "SELECT COUNT(*) FROM t WHERE x > 24", "count_sum": "SELECT COUNT(*), SUM(x) FROM t WHERE x > 24",
+        "count_sum_min_max": "SELECT COUNT(*), SUM(x), MIN(x), MAX(x) FROM t WHERE x > 24"}
+if os.environ.get("SWEEP_SQLS"):
+    sqls = {k: v for k, v in sqls.items() if k in os.environ["SWEEP_SQLS"].split(",")}
 res = {}
 for name, sql in sqls.items():
     times = {v: [] for v in variants}
