@@ -116,7 +116,12 @@ def main():
 
     def step():
         rr = conn.query_raw(sql)
-        cells = [rr.value(c, 0) for c in range(rr.column_count())] if rr.row_count() == 1 else rr.row_count()
+        if args.config == "c3":
+            # (k, COUNT(*), SUM(v)) per group, read through the result accessors
+            cells = [(None if rr.is_null(0, r) else int(rr.value(0, r)), int(rr.value(2, r)),
+                      None if rr.is_null(1, r) else int(rr.value(1, r))) for r in range(rr.row_count())]
+        else:
+            cells = [rr.value(c, 0) for c in range(rr.column_count())]
         rr.close()
         return cells
 
@@ -134,6 +139,8 @@ def main():
             gcount = mbx_dist.allreduce_count(int(out[0]), device=coll_dev)  # RCCL over xGMI: global COUNT(*)
         elif world > 1 and args.config == "c5":
             gcount, gsum = mbx_dist.global_count_sum(int(out[0]), int(out[1]) if out[1] else None, device=coll_dev)
+        elif world > 1 and args.config == "c3":
+            ggroups = mbx_dist.global_group_count_sum(out, device=coll_dev)  # 32 x (key, count, int128 sum)
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
@@ -166,6 +173,20 @@ def main():
                 parity["global_sum"] = gsum
                 parity["match"] = parity["match"] and gsum == g_osum
 
+    if args.config == "c3":
+        sys.path.insert(0, HERE)
+        from oracle import Oracle  # test infrastructure: checker only
+        orc = Oracle()
+        threads = min(16, len(os.sched_getaffinity(0)))
+        oc, osum = orc.synth_groupby(7, 9, start, n, 32, 1 << 40, -(1 << 39), threads)
+        exp = [(k, oc[k], osum[k]) for k in range(32) if oc[k]]
+        got = sorted(out, key=lambda g: (g[0] is None, g[0]))
+        parity = {"groups": len(got), "oracle_groups": len(exp), "match": got == exp}
+        if world > 1:
+            g_exp = mbx_dist.global_group_count_sum(exp, device=coll_dev)
+            parity["global_groups"] = len(ggroups)
+            parity["match"] = parity["match"] and ggroups == g_exp
+
     result = None
     if rank == 0:
         total_rows = n * world * args.steps
@@ -193,7 +214,9 @@ def main():
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": "int64",
-            "data": "synthetic: x = splitmix64(42 + i) mod 50 + 1 generated on device (no dataset)",
+            "data": ("synthetic: k = splitmix64(7 + i) mod 32 (INT32), v = splitmix64(9 + i) mod 2^40 - 2^39 (INT64), "
+                     "generated on device (no dataset)" if args.config == "c3" else
+                     "synthetic: x = splitmix64(42 + i) mod 50 + 1 generated on device (no dataset)"),
             "config": {"workload": workload, "rows_per_gpu": n, "sql": sql,
                        "parallelism": f"row-range shards x{world}" + ((" + RCCL all-reduce/all-gather" if args.dist_backend == "nccl"
                                                                           else " + gloo collectives (rehearsal)") if world > 1 else "")},

@@ -978,12 +978,13 @@ struct FaVariant {
   bool chunk = true;
   int blocks_per_cu = 1;
   bool pairs = true;  // row-pair layout (false: the older 32-B-per-lane Vec4 layout)
-  int lds_depth = 8;  // >0: LDS-DMA ring of this depth per wave (blocks_per_cu then counts 256-thread blocks)
+  int lds_depth = 6;  // >0: LDS-DMA ring of this depth per wave (blocks_per_cu then counts 256-thread blocks)
 };
 
-// Default: the LDS-DMA stream, 8 x 1 KiB slots per wave, one 256-thread
-// workgroup per CU (one wave per SIMD) — 6.84 TB/s median on the 1e9-row
-// COUNT vs 6.06 for the best register-load shape (profiles/r01_filter_sweep_lds.json).
+// Default: the LDS-DMA stream, 6 x 1 KiB slots per wave, one 256-thread
+// workgroup per CU (one wave per SIMD) — 6.90 TB/s median on the 1e9-row
+// COUNT vs 6.80 at depth 8 and 6.06 for the best register-load shape
+// (profiles/r01_filter_sweep_lds.json, r01_filter_sweep_depth.json).
 // MBX_FA_VARIANT overrides it: "d<depth>_g<blocks per CU>" (LDS-DMA) or
 // "u<unroll>_<nt|pl>_<gs|ch>_g<blocks per CU>[_v4]" (register loads).
 static FaVariant FaConfig(int mode) {
@@ -1039,9 +1040,14 @@ static void LaunchFilterAgg(const FaVariant &v, const void *p, const void *a, in
                             AggState *st, unsigned long long *cstar, int grid, hipStream_t s) {
   if constexpr (MODE != 1 || sizeof(TP) == sizeof(TA)) {
     if (v.lds_depth > 0) {
-      if (v.lds_depth <= 4) LaunchFALds<TP, MODE, 4>(p, a, n, lo, span, st, cstar, grid, s);
-      else if (v.lds_depth <= 8) LaunchFALds<TP, MODE, 8>(p, a, n, lo, span, st, cstar, grid, s);
-      else LaunchFALds<TP, MODE, 16>(p, a, n, lo, span, st, cstar, grid, s);
+      switch (v.lds_depth) {
+        case 1: case 2: case 3: case 4: LaunchFALds<TP, MODE, 4>(p, a, n, lo, span, st, cstar, grid, s); break;
+        case 5: LaunchFALds<TP, MODE, 5>(p, a, n, lo, span, st, cstar, grid, s); break;
+        case 6: LaunchFALds<TP, MODE, 6>(p, a, n, lo, span, st, cstar, grid, s); break;
+        case 7: LaunchFALds<TP, MODE, 7>(p, a, n, lo, span, st, cstar, grid, s); break;
+        case 8: LaunchFALds<TP, MODE, 8>(p, a, n, lo, span, st, cstar, grid, s); break;
+        default: LaunchFALds<TP, MODE, 16>(p, a, n, lo, span, st, cstar, grid, s); break;
+      }
       return;
     }
   }

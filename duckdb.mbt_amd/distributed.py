@@ -4,10 +4,12 @@ One process per GPU, each owning a contiguous row-range shard of the table.
 The only exchange is the final combine of the global aggregates: COUNT is an
 int64 all-reduce; SUM is an exact int128 (DuckDB HUGEINT), which no RCCL
 reduction op supports, so every rank all-gathers its partial as two int64
-lanes (lo, hi) and combines them exactly (carry-correct) afterwards.  On
-ROCm, backend "nccl" is RCCL (over xGMI); tests use "gloo" on the CPU.
+lanes (lo, hi) and combines them exactly (carry-correct) afterwards.  A
+GROUP BY (config C3) exchanges its per-shard group table the same way: one
+fixed-width row per group ("32 x 24 B per GPU").  On ROCm,
+backend "nccl" is RCCL (over xGMI); tests use "gloo" on the CPU.
 """
-from typing import List, Sequence
+from typing import List, Optional, Sequence, Tuple
 
 import torch
 import torch.distributed as dist
@@ -60,3 +62,44 @@ def allreduce_count(local_count: int, device="cpu", group=None) -> int:
     t = torch.tensor([int(local_count)], dtype=torch.int64, device=device)
     dist.all_reduce(t, group=group)
     return int(t.item())
+
+
+# One exchanged row per group: [flags, key, count, sum_lo, sum_hi]
+#   flags bit0 = row present (ranks pad to the largest group table),
+#         bit1 = key is NULL, bit2 = the SUM is non-NULL.
+_GROUP_W = 5
+
+
+def global_group_count_sum(groups: Sequence[Tuple[Optional[int], int, Optional[int]]], device="cpu",
+                           group=None) -> List[Tuple[Optional[int], int, Optional[int]]]:
+    """Exact global ``SELECT k, COUNT(*), SUM(v) ... GROUP BY k`` from per-shard
+    partials.  ``groups`` holds (key | None, count, sum | None) for this rank's
+    shard; the result is ordered by key with the NULL group last (DuckDB's
+    NULLS LAST).  Keys and counts are int64; sums are int128 (HUGEINT)."""
+    world = dist.get_world_size(group)
+    g = torch.tensor([len(groups)], dtype=torch.int64, device=device)
+    if world > 1:
+        dist.all_reduce(g, op=dist.ReduceOp.MAX, group=group)
+    width = max(int(g.item()), 1)
+    rows = [[0] * _GROUP_W for _ in range(width)]
+    for i, (k, c, sm) in enumerate(groups):
+        lo, hi = encode_i128(0 if sm is None else int(sm))
+        rows[i] = [1 | (2 if k is None else 0) | (0 if sm is None else 4), 0 if k is None else int(k), int(c), lo, hi]
+    t = torch.tensor(rows, dtype=torch.int64, device=device)
+    outs = [torch.empty_like(t) for _ in range(world)]
+    if world > 1:
+        dist.all_gather(outs, t, group=group)
+    else:
+        outs = [t]
+    acc = {}
+    for o in outs:
+        for flags, k, c, lo, hi in o.cpu().tolist():
+            if not flags & 1:
+                continue
+            key = None if flags & 2 else k
+            cc, ss = acc.get(key, (0, None))
+            if flags & 4:
+                ss = (ss or 0) + decode_i128(lo, hi)
+            acc[key] = (cc + c, ss)
+    keys = sorted(k for k in acc if k is not None) + ([None] if None in acc else [])
+    return [(k, acc[k][0], acc[k][1]) for k in keys]

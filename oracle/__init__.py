@@ -42,6 +42,7 @@ def load():
     lib.orc_filter_agg_i64.argtypes = [vp, i64, i64, i64, ctypes.c_int, vp, vp, vp, vp]
     lib.orc_synth_filter_count.argtypes = [u64, i64, i64, u64, i64, i64, i64, ctypes.c_int, vp, vp]
     lib.orc_groupby_sum_i32_i64.argtypes = [vp, vp, i64, i32, ctypes.c_int, ctypes.c_int, vp, vp]
+    lib.orc_synth_groupby.argtypes = [u64, u64, i64, i64, ctypes.c_int, u64, i64, ctypes.c_int, vp, vp]
     lib.orc_range_mod_select.restype = i64
     lib.orc_range_mod_select.argtypes = [i64, i64, i64, i64, vp, i64]
     return lib
@@ -90,6 +91,14 @@ class Oracle:
         sums = ctypes.create_string_buffer(16 * nk)
         self.lib.orc_groupby_sum_i32_i64(k.ctypes.data, v.ctypes.data, len(k), kmin, nk, threads,
                                          counts.ctypes.data, sums)
+        return [int(c) for c in counts], [i128_from(sums.raw[16 * i:16 * i + 16]) for i in range(nk)]
+
+    def synth_groupby(self, seed_k, seed_v, start, n, nk, vm, vadd, threads=1):
+        """C3 over the generator: per-key COUNT(*) and exact SUM(v) (no arrays)."""
+        import numpy as np
+        counts = np.zeros(nk, dtype=np.uint64)
+        sums = ctypes.create_string_buffer(16 * nk)
+        self.lib.orc_synth_groupby(seed_k, seed_v, start, n, nk, vm, vadd, threads, counts.ctypes.data, sums)
         return [int(c) for c in counts], [i128_from(sums.raw[16 * i:16 * i + 16]) for i in range(nk)]
 
     def range_mod_select(self, n, k, c, mul):

@@ -212,6 +212,73 @@ void orc_groupby_sum_i32_i64(const int32_t *k, const int64_t *v, int64_t n, int3
   free(acc);
 }
 
+/* ---- the C3 GROUP BY over the generator (no materialisation) -----------
+ * k_i = splitmix64(seed_k + start + i) mod nk (INT32), v_i = splitmix64(seed_v
+ * + start + i) mod vm + vadd (INT64); counts[nk], sums16[nk*16] as above. */
+typedef struct {
+  uint64_t seed_k, seed_v, vm;
+  int64_t start, n, vadd;
+  int nk;
+  uint64_t *cnt;
+  i128 *sum;
+} sg_job;
+
+static void *sg_run(void *p) {
+  sg_job *j = (sg_job *)p;
+  int64_t *part = (int64_t *)calloc(j->nk, sizeof(int64_t));
+  int64_t since = 0;
+  for (int64_t i = 0; i < j->n; i++) {
+    uint64_t r = (uint64_t)(j->start + i);
+    int s = (int)(orc_splitmix64(j->seed_k + r) % (uint64_t)j->nk);
+    int64_t v = (int64_t)(orc_splitmix64(j->seed_v + r) % j->vm) + j->vadd;
+    j->cnt[s]++;
+    part[s] += v; /* |v| < 2^62 / 2^20: flushed every 2^20 rows */
+    if (++since == (1 << 20)) {
+      for (int q = 0; q < j->nk; q++) j->sum[q] += part[q], part[q] = 0;
+      since = 0;
+    }
+  }
+  for (int q = 0; q < j->nk; q++) j->sum[q] += part[q];
+  free(part);
+  return NULL;
+}
+
+void orc_synth_groupby(uint64_t seed_k, uint64_t seed_v, int64_t start, int64_t n, int nk, uint64_t vm, int64_t vadd,
+                       int threads, uint64_t *counts, void *sums16) {
+  if (threads < 1) threads = 1;
+  if (threads > 256) threads = 256;
+  sg_job jobs[256];
+  pthread_t th[256];
+  int64_t chunk = (n + threads - 1) / threads;
+  for (int t = 0; t < threads; t++) {
+    int64_t b = t * chunk, e = b + chunk < n ? b + chunk : n;
+    if (b > n) b = n;
+    jobs[t].seed_k = seed_k;
+    jobs[t].seed_v = seed_v;
+    jobs[t].vm = vm;
+    jobs[t].start = start + b;
+    jobs[t].n = e - b;
+    jobs[t].vadd = vadd;
+    jobs[t].nk = nk;
+    jobs[t].cnt = (uint64_t *)calloc(nk, sizeof(uint64_t));
+    jobs[t].sum = (i128 *)calloc(nk, sizeof(i128));
+    pthread_create(&th[t], NULL, sg_run, &jobs[t]);
+  }
+  i128 *acc = (i128 *)calloc(nk, sizeof(i128));
+  memset(counts, 0, nk * sizeof(uint64_t));
+  for (int t = 0; t < threads; t++) {
+    pthread_join(th[t], NULL);
+    for (int q = 0; q < nk; q++) {
+      counts[q] += jobs[t].cnt[q];
+      acc[q] += jobs[t].sum[q];
+    }
+    free(jobs[t].cnt);
+    free(jobs[t].sum);
+  }
+  memcpy(sums16, acc, (size_t)nk * 16);
+  free(acc);
+}
+
 /* ---- range(N) WHERE i % k = c, projected i*mul (config C1) ------------- */
 int64_t orc_range_mod_select(int64_t n, int64_t k, int64_t c, int64_t mul, int64_t *out, int64_t cap) {
   int64_t w = 0;
