@@ -1296,6 +1296,155 @@ __global__ __launch_bounds__(256) void group_direct_kernel(const TK *__restrict_
   }
 }
 
+// LDS-DMA version of group_direct (the default when one flush at the end is
+// overflow-safe).  A wave step covers 256 consecutive rows: the key slice and
+// every value column's slice are pulled into the wave's ring slot with
+// 16-B/lane global_load_lds (1 KiB per instruction, no VGPR staging); each
+// lane then owns 4 consecutive rows.  Waves walk steps grid-stride.  The
+// replicated LDS tables and the rings share ONE dynamic __shared__ array.
+template <typename TK, typename TV, int NV, bool MM, int DEPTH>
+__global__ __launch_bounds__(256) void group_direct_lds_kernel(const TK *__restrict__ keys, const TV *__restrict__ v0,
+                                                               const TV *__restrict__ v1, int64_t n, int64_t kmin,
+                                                               int nk, int R, size_t ring_off,
+                                                               unsigned long long *cstar, AggState *st0,
+                                                               AggState *st1) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char lds_raw[];
+  constexpr int KB = 256 * (int)sizeof(TK), VB = 256 * (int)sizeof(TV);  // bytes per step
+  constexpr int SB = KB + NV * VB;                                         // slot bytes
+  constexpr int NLD = SB / 1024;                                           // glds per step
+  const int nslot = nk * R;
+  unsigned int *cnt = (unsigned int *)lds_raw;
+  long long *sum0 = (long long *)(lds_raw + ((nslot * 4 + 15) & ~15));
+  long long *sum1 = sum0 + nslot;
+  long long *mn0 = sum0 + (NV >= 2 ? 2 : 1) * nslot;
+  long long *mx0 = mn0 + nslot;
+  long long *mn1 = mx0 + nslot;
+  long long *mx1 = mn1 + nslot;
+  const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+  const int rep = lane % R;
+  unsigned char *ring = lds_raw + ring_off + (size_t)w * DEPTH * SB;
+  for (int i = t; i < nslot; i += blockDim.x) {
+    cnt[i] = 0;
+    if (NV >= 1) sum0[i] = 0;
+    if (NV >= 2) sum1[i] = 0;
+    if (MM) {
+      mn0[i] = INT64_MAX; mx0[i] = INT64_MIN;
+      if (NV >= 2) { mn1[i] = INT64_MAX; mx1[i] = INT64_MIN; }
+    }
+  }
+  __syncthreads();
+  auto row = [&](int64_t k, int64_t a, int64_t b) {
+    int sl = (int)(k - kmin) * R + rep;
+    atomicAdd(&cnt[sl], 1u);
+    if (NV >= 1) atomicAdd((unsigned long long *)&sum0[sl], (unsigned long long)a);
+    if (NV >= 2) atomicAdd((unsigned long long *)&sum1[sl], (unsigned long long)b);
+    if (MM) {
+      atomicMin(&mn0[sl], (long long)a); atomicMax(&mx0[sl], (long long)a);
+      if (NV >= 2) { atomicMin(&mn1[sl], (long long)b); atomicMax(&mx1[sl], (long long)b); }
+    }
+  };
+  const int64_t nsteps = n >> 8;
+  const int64_t nw = (int64_t)gridDim.x * 4;
+  int64_t st = (int64_t)blockIdx.x * 4 + w;
+  // issue one step's glds into slot d: key slice, then each value slice
+  auto issue = [&](int64_t q, int d) {
+    unsigned char *dst = ring + d * SB;
+    const unsigned char *kp = (const unsigned char *)keys + q * KB;
+#pragma unroll
+    for (int j = 0; j < KB / 1024; j++)
+      __builtin_amdgcn_global_load_lds((const void *)(kp + j * 1024 + lane * 16), (void *)(dst + j * 1024), 16, 0, 2);
+    if (NV >= 1) {
+      const unsigned char *vp = (const unsigned char *)v0 + q * VB;
+#pragma unroll
+      for (int j = 0; j < VB / 1024; j++)
+        __builtin_amdgcn_global_load_lds((const void *)(vp + j * 1024 + lane * 16), (void *)(dst + KB + j * 1024), 16, 0, 2);
+    }
+    if (NV >= 2) {
+      const unsigned char *vp = (const unsigned char *)v1 + q * VB;
+#pragma unroll
+      for (int j = 0; j < VB / 1024; j++)
+        __builtin_amdgcn_global_load_lds((const void *)(vp + j * 1024 + lane * 16), (void *)(dst + KB + VB + j * 1024), 16,
+                                         0, 2);
+    }
+  };
+  if (nsteps > 0) {
+#pragma unroll
+    for (int d = 0; d < DEPTH; d++) {
+      int64_t q = st + d * nw;
+      issue(q < nsteps ? q : 0, d);
+    }
+  }
+  int k = 0;
+  for (; st < nsteps; st += nw) {
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NLD * (DEPTH - 1)) : "memory");
+    const unsigned char *src = ring + k * SB;
+    int64_t kk[4], a[4], b[4];
+    if (sizeof(TK) == 4) {
+      v4i32 kv = *(const v4i32 *)(src + lane * 16);
+      kk[0] = kv.x; kk[1] = kv.y; kk[2] = kv.z; kk[3] = kv.w;
+    } else {
+      v2i64 k0 = *(const v2i64 *)(src + lane * 32), k1 = *(const v2i64 *)(src + lane * 32 + 16);
+      kk[0] = k0.x; kk[1] = k0.y; kk[2] = k1.x; kk[3] = k1.y;
+    }
+#pragma unroll
+    for (int c = 0; c < NV; c++) {
+      const unsigned char *vs = src + KB + c * VB;
+      int64_t *o = c == 0 ? a : b;
+      if (sizeof(TV) == 4) {
+        v4i32 x = *(const v4i32 *)(vs + lane * 16);
+        o[0] = x.x; o[1] = x.y; o[2] = x.z; o[3] = x.w;
+      } else {
+        v2i64 x0 = *(const v2i64 *)(vs + lane * 32), x1 = *(const v2i64 *)(vs + lane * 32 + 16);
+        o[0] = x0.x; o[1] = x0.y; o[2] = x1.x; o[3] = x1.y;
+      }
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    int64_t q = st + DEPTH * nw;
+    issue(q < nsteps ? q : st, k);
+#pragma unroll
+    for (int e = 0; e < 4; e++) row(kk[e], NV >= 1 ? a[e] : 0, NV >= 2 ? b[e] : 0);
+    k = k + 1 == DEPTH ? 0 : k + 1;
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  if (blockIdx.x == 0) {
+    for (int64_t i = (nsteps << 8) + t; i < n; i += blockDim.x)
+      row((int64_t)keys[i], NV >= 1 ? (int64_t)v0[i] : 0, NV >= 2 ? (int64_t)v1[i] : 0);
+  }
+  __syncthreads();
+  for (int kq = t; kq < nk; kq += blockDim.x) {
+    unsigned long long c = 0;
+    i128 s0 = 0, s1 = 0;
+    long long a0 = INT64_MAX, b0 = INT64_MIN, a1 = INT64_MAX, b1 = INT64_MIN;
+    for (int r = 0; r < R; r++) {
+      int sl = kq * R + r;
+      c += cnt[sl];
+      if (NV >= 1) s0 += (i128)sum0[sl];
+      if (NV >= 2) s1 += (i128)sum1[sl];
+      if (MM) {
+        a0 = mn0[sl] < a0 ? mn0[sl] : a0; b0 = mx0[sl] > b0 ? mx0[sl] : b0;
+        if (NV >= 2) { a1 = mn1[sl] < a1 ? mn1[sl] : a1; b1 = mx1[sl] > b1 ? mx1[sl] : b1; }
+      }
+    }
+    if (c) {
+      atomicAdd(&cstar[kq], c);
+      Acc A;
+      A.cnt = c;
+      if (NV >= 1) {
+        int64_t lo, hi;
+        sp128(s0, lo, hi);
+        A.slo = (uint64_t)lo; A.shi = hi; A.mn = MM ? a0 : INT64_MAX; A.mx = MM ? b0 : INT64_MIN;
+        agg_state_atomic(&st0[kq], A);
+      }
+      if (NV >= 2) {
+        int64_t lo, hi;
+        sp128(s1, lo, hi);
+        A.slo = (uint64_t)lo; A.shi = hi; A.mn = MM ? a1 : INT64_MAX; A.mx = MM ? b1 : INT64_MIN;
+        agg_state_atomic(&st1[kq], A);
+      }
+    }
+  }
+}
+
 template <typename TK, typename TV, int NV, bool MM>
 static void LaunchGroupDirect(const void *k, const void *v0, const void *v1, int64_t n, int64_t kmin, int nk, int R,
                               int64_t chunk, int64_t seg, unsigned long long *cstar, AggState *s0, AggState *s1,
@@ -1317,6 +1466,50 @@ void GroupByDirectStates(const void *kcol, int kphys, int64_t kmin, int nk, cons
                          int nv, bool mm, int64_t nrows, int64_t seg_rows, int R, unsigned long long *cstar,
                          AggState *st0, AggState *st1, int grid_blocks, hipStream_t s) {
   if (nrows <= 0) return;
+  // LDS-DMA variant: one flush at the end, so a block's whole row share must
+  // fit the overflow bound the host derived (seg_rows) — else the segmented
+  // kernel below.  MBX_GD_VARIANT="d<depth>_g<blocks per CU>" / "seg".
+  // Defaults from profiles/r01_group_sweep.json: d2_g3 for C3 (6.72 TB/s vs
+  // 5.87 segmented); COUNT-only tables (nv == 0) carry 3x the LDS atomics per
+  // byte and stay on the segmented kernel at 4 blocks/CU (6.40 TB/s).
+  {
+    int depth = 2, gpc = 3;
+    bool use = nv > 0;
+    const char *e = getenv("MBX_GD_VARIANT");
+    if (e && *e) use = sscanf(e, "d%d_g%d", &depth, &gpc) == 2;
+    if (use) {
+      int grid = grid_blocks > 0 ? grid_blocks : NumCUs() * gpc;
+      int64_t nsteps = nrows >> 8;
+      int64_t waves = (int64_t)grid * 4;
+      int64_t rows_per_block = ((nsteps + waves - 1) / waves) * 4 * 256 + 256;
+      size_t tab = GroupDirectLds(nk, R, nv, mm);
+      size_t ring_off = (tab + 15) & ~(size_t)15;
+      size_t slot = 256 * (size_t)(kphys == P_I64 ? 8 : 4) + (size_t)nv * 256 * (vphys == P_I64 ? 8 : 4);
+      depth = depth <= 2 ? 2 : depth <= 3 ? 3 : 4;
+      size_t lds = ring_off + 4 * (size_t)depth * slot;
+      if ((seg_rows <= 0 || seg_rows >= rows_per_block) && lds <= 64 * 1024) {
+#define GL(TK, TV, NV, MM, D)                                                                                       \
+  hipLaunchKernelGGL((group_direct_lds_kernel<TK, TV, NV, MM, D>), dim3(grid), dim3(256), lds, s, (const TK *)kcol, \
+                     (const TV *)v0, (const TV *)v1, nrows, kmin, nk, R, ring_off, cstar, st0, st1)
+#define GLD(TK, TV, NV, MM) \
+  if (depth == 2) GL(TK, TV, NV, MM, 2); else if (depth == 3) GL(TK, TV, NV, MM, 3); else GL(TK, TV, NV, MM, 4);
+#define GLV(TK, TV)                                                                      \
+  if (nv == 0) { GLD(TK, TV, 0, false) }                                                 \
+  else if (nv == 1) { if (mm) { GLD(TK, TV, 1, true) } else { GLD(TK, TV, 1, false) } } \
+  else { if (mm) { GLD(TK, TV, 2, true) } else { GLD(TK, TV, 2, false) } }
+        if (kphys == P_I32) {
+          if (vphys == P_I64) { GLV(int32_t, int64_t) } else { GLV(int32_t, int32_t) }
+        } else {
+          if (vphys == P_I64) { GLV(int64_t, int64_t) } else { GLV(int64_t, int32_t) }
+        }
+#undef GLV
+#undef GLD
+#undef GL
+        CHECK_LAUNCH();
+        return;
+      }
+    }
+  }
   int grid = grid_blocks > 0 ? grid_blocks : NumCUs() * 4;
   int64_t chunk = (nrows + grid - 1) / grid;
   chunk = (chunk + 3) & ~(int64_t)3;

@@ -258,3 +258,42 @@ def test_filter_agg_variants_parity(conn, oracle, monkeypatch, variant):
                 sel = vals[m]
                 want = [int(sel.sum(dtype=np.int64)), int(sel.min()), int(sel.max())][:len(got) - 1]
                 assert [int(g) for g in got[1:]] == want, (variant, n, sql)
+
+
+# ---- every fused GROUP BY launch shape gives the same bits ------------------
+GD_VARIANTS = ["", "seg", "d2_g1", "d3_g2", "d4_g2"]
+
+
+@pytest.mark.parametrize("variant", GD_VARIANTS)
+def test_group_direct_variants_parity(conn, oracle, monkeypatch, variant):
+    monkeypatch.setenv("MBX_GD_VARIANT", variant)
+    for n in (1, 255, 256, 257, 1023, 70_001, 1_000_003):
+        k = oracle.synth_i64(n, 7, 0, 40, -20)           # keys -20..19
+        v = oracle.synth_i64(n, 9, 0, 2**40, -2**39)
+        u = oracle.synth_i64(n, 11, 0, 1000, -500)
+        q(conn, "DROP TABLE IF EXISTS gv")
+        q(conn, f"CREATE TABLE gv AS SELECT mbx_synth(7, i, 40) - 20 AS k, CAST(mbx_synth(7, i, 40) - 20 AS INTEGER) AS k4, "
+                f"mbx_synth(9, i, 1099511627776) - 549755813888 AS v, mbx_synth(11, i, 1000) - 500 AS u, "
+                f"CAST(mbx_synth(11, i, 1000) - 500 AS INTEGER) AS u4, CAST(mbx_synth(9, i, 1000000) AS INTEGER) AS w4 "
+                f"FROM range({n}) tbl(i)")
+        w = oracle.synth_i64(n, 9, 0, 1_000_000, 0)
+        keys = sorted(set(k.tolist()))
+        for kc in ("k", "k4"):
+            exp_c = [int((k == kk).sum()) for kk in keys]
+            got = q(conn, f"SELECT {kc}, COUNT(*) FROM gv GROUP BY {kc} ORDER BY {kc}").rows
+            assert [(int(r[0]), int(r[1])) for r in got] == list(zip(keys, exp_c)), (variant, n, kc)
+            for sql, cols in [(f"SELECT {kc}, SUM(v), COUNT(*) FROM gv GROUP BY {kc} ORDER BY {kc}", [v]),
+                              (f"SELECT {kc}, SUM(u), SUM(v), COUNT(*) FROM gv GROUP BY {kc} ORDER BY {kc}", [u, v]),
+                              (f"SELECT {kc}, SUM(u4), MIN(u4), MAX(u4), SUM(w4) FROM gv GROUP BY {kc} ORDER BY {kc}", None),
+                              (f"SELECT {kc}, MIN(v), MAX(v), SUM(v) FROM gv GROUP BY {kc} ORDER BY {kc}", None)]:
+                got = q(conn, sql).rows
+                for r, kk in zip(got, keys):
+                    m = k == kk
+                    assert int(r[0]) == kk
+                    if "SUM(u4), MIN(u4)" in sql:
+                        want = [int(u[m].sum()), int(u[m].min()), int(u[m].max()), int(w[m].sum())]
+                    elif "MIN(v), MAX(v)" in sql:
+                        want = [int(v[m].min()), int(v[m].max()), int(v[m].astype(object).sum())]
+                    else:
+                        want = [int(c[m].astype(object).sum()) for c in cols] + [int(m.sum())]
+                    assert [int(x) for x in r[1:]] == want, (variant, n, sql, kk)
