@@ -244,6 +244,13 @@ def main():
         print(json.dumps(result), flush=True)
 
 
+def one_count(conn):
+    rr = conn.query_raw("SELECT COUNT(*) FROM c4")
+    v = int(rr.value(0, 0))
+    rr.close()
+    return v
+
+
 def bench_c4(mbx, conn, n, args):
     """C4: Appender ingest -> device column -> Arrow read-back (host-link bound).
     Reports H2D ingest GB/s and Arrow int64 read-back GB/s (1e6-row slices,
@@ -261,13 +268,15 @@ def bench_c4(mbx, conn, n, args):
     ap.close()
     t_in = time.perf_counter() - t0
     t0 = time.perf_counter()
-    ok = True
+    slices = []
     for k in range(0, n, 1_000_000):
         a = conn.query_arrow(f"SELECT v FROM c4 LIMIT 1000000 OFFSET {k}").value
-        got = np.frombuffer(a.raw_int64_bytes(0)[4:], dtype=np.int64)
+        slices.append(a.raw_int64_bytes(0))  # [i32 count][int64 LE values]: the get_column_int64 wire buffer
         a.close()
-        ok &= bool(np.array_equal(got, v[k:k + 1_000_000]))
     t_out = time.perf_counter() - t0
+    ok = all(np.array_equal(np.frombuffer(b[4:], dtype=np.int64), v[k:k + 1_000_000])
+             for b, k in zip(slices, range(0, n, 1_000_000)))
+    ok &= one_count(conn) == n
     res = {"metric": "C4 appender ingest + arrow read-back", "value": n / (t_in + t_out), "unit": "rows/s",
            "n_gpus": 1, "ingest_gbs": n * 8 / t_in / 1e9, "readback_gbs": n * 8 / t_out / 1e9,
            "ingest_s": t_in, "readback_s": t_out, "rows": n, "bit_exact": ok,

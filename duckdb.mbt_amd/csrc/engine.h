@@ -127,6 +127,8 @@ struct HostBatch {
   int64_t nrows = 0;
 };
 void AppendHostBatch(Connection &c, Table &t, const HostBatch &b);
+void AppendRawColumns(Connection &c, Table &t, const std::vector<const void *> &vals,
+                      const std::vector<const uint8_t *> &valid, int64_t n);
 void HostColumnPush(HostColumn &col, const Value &v);  // v already of col.type (or NULL)
 void HbmCalibrateConn(Connection &c, int64_t bytes, int iters, double out[3]);
 

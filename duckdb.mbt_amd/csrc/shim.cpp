@@ -683,19 +683,9 @@ int32_t duckdb_mbx_append_commit(duckdb_mb_appender *a, int64_t count) {
     }
   if (!FlushAppender(a)) return 0;  // keep row order: staged rows first
   try {
-    HostBatch b;
-    b.nrows = count;
-    for (size_t i = 0; i < nc; i++) {
-      HostColumn hc;
-      hc.type = a->table->cols[i].type;
-      hc.phys = a->table->cols[i].phys;
-      size_t bytes = (size_t)count * PhysSize(hc.phys);
-      hc.data.resize(bytes);
-      memcpy(hc.data.data(), a->raw_vals[i], bytes);
-      if (a->raw_valid[i]) hc.valid.assign(a->raw_valid[i], a->raw_valid[i] + count);
-      b.cols.push_back(std::move(hc));
-    }
-    AppendHostBatch(a->conn->conn, *a->table, b);
+    std::vector<const void *> vals(a->raw_vals.begin(), a->raw_vals.end());
+    std::vector<const uint8_t *> valid(a->raw_valid.begin(), a->raw_valid.end());
+    AppendRawColumns(a->conn->conn, *a->table, vals, valid, count);
   } catch (std::exception &e) {
     CopyErr(a->error, e.what());
     return 0;
