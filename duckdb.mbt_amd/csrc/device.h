@@ -47,9 +47,24 @@ struct AggState {
 // Predicate lo <= p[i] <= hi on column p (P_I32 / P_I64, no nulls) or none;
 // aggregate column a (P_I32 / P_I64; == p allowed) or none (COUNT(*) only).
 // count_star += selected rows; st accumulates count/sum/min/max of a.
-void FilterAggStates(const void *pcol, int pphys, int64_t lo, int64_t hi, bool has_pred, const void *acol, int aphys,
-                     int64_t nrows, AggState *st, unsigned long long *cstar, int grid_blocks, hipStream_t s,
-                     bool need_minmax = true, uint64_t sum_maxabs = ~0ull);
+// One workgroup's partial of the fused filter-aggregate (count, int128 sum as
+// lo/hi, min, max) — same layout as the kernel's accumulator.
+struct AggPartial {
+  uint64_t cnt;
+  uint64_t slo;
+  int64_t shi;
+  int64_t mn, mx;
+};
+// Launches the fused filter-aggregate.  With `partials` (room for
+// kMaxAggPartials) the default LDS-DMA kernel writes one AggPartial per
+// workgroup and the call returns how many; the emit kernel reduces them
+// (EmitDesc::partials), so no state initialisation and no atomics are
+// needed.  Otherwise (or for shapes the LDS kernel does not take) it zeroes
+// st/cstar itself, accumulates with atomics and returns 0.
+constexpr int kMaxAggPartials = 4096;
+int FilterAggStates(const void *pcol, int pphys, int64_t lo, int64_t hi, bool has_pred, const void *acol, int aphys,
+                    int64_t nrows, AggState *st, unsigned long long *cstar, int grid_blocks, hipStream_t s,
+                    bool need_minmax = true, uint64_t sum_maxabs = ~0ull, AggPartial *partials = nullptr);
 
 // --- fused GROUP BY on a small-range integer key (config C3) -------------
 // key in [kmin, kmin + nk), no nulls; up to 2 value columns of one phys.
@@ -140,8 +155,28 @@ struct EmitDesc {
   int64_t null_slot;  // -1 if none
   void *key_out;
   uint32_t *key_valid;
+  // optional: reduce these per-workgroup partials into slot 0 first
+  // (states of every aggregate and cstar[0]); emit then runs one workgroup
+  const AggPartial *partials;
+  int32_t npartials;
 };
 void EmitAggRelation(const EmitDesc &d, hipStream_t s);
+
+// Small results: one kernel copies every result buffer (and the device error
+// word) into coherent pinned host memory, replacing a DMA per buffer.
+struct HostCopySeg {
+  const void *src;
+  void *dst;
+  int64_t bytes;
+};
+#define HOSTCOPY_MAX 32
+struct HostCopyDesc {
+  int32_t nseg;
+  HostCopySeg seg[HOSTCOPY_MAX];
+  const int32_t *err_src;
+  int32_t *err_dst;
+};
+void HostCopy(const HostCopyDesc &d, hipStream_t s);
 void RebaseOffsets(const int64_t *src, int64_t *dst, int64_t n, int64_t delta, hipStream_t s);
 
 }  // namespace dev

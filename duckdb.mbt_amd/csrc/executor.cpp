@@ -39,13 +39,45 @@ struct ProfEvent {
   int64_t rows;
 };
 
+struct SmallPool {
+  static constexpr int kClasses = 13;  // 256 B .. 1 MiB
+  static constexpr size_t kMaxPerClass = 64;
+  std::vector<void *> free_[kClasses];
+  hipStream_t s = nullptr;
+  static int Class(size_t bytes) {
+    if (bytes > ((size_t)256 << (kClasses - 1))) return -1;
+    int c = 0;
+    while (((size_t)256 << c) < bytes) c++;
+    return c;
+  }
+  static size_t ClassBytes(int c) { return (size_t)256 << c; }
+  void *Get(int c) {
+    if (free_[c].empty()) return nullptr;
+    void *p = free_[c].back();
+    free_[c].pop_back();
+    return p;
+  }
+  bool Put(int c, void *p) {
+    if (free_[c].size() >= kMaxPerClass) return false;
+    free_[c].push_back(p);
+    return true;
+  }
+  ~SmallPool() {
+    for (auto &v : free_)
+      for (void *p : v) (void)hipFreeAsync(p, s);
+    if (s) (void)hipStreamSynchronize(s);
+  }
+};
+
 struct Engine {
   int device = 0;
+  std::shared_ptr<SmallPool> pool;
   bool has_gpu = false;
   hipStream_t stream = nullptr;
   int32_t *d_err = nullptr;
   int64_t *d_scratch = nullptr;  // small device scratch (counts)
   void *d_small = nullptr;       // 64 KB scratch for small states
+  dev::AggPartial *d_partials = nullptr;  // per-workgroup partials of the fused filter-aggregate
   // pinned host staging for small results: every D2H of a query lands here
   // and the query pays ONE stream synchronisation
   uint8_t *h_pinned = nullptr;
@@ -66,6 +98,9 @@ struct Engine {
     h_pinned_bytes = b;
     return true;
   }
+  // coherent pinned buffer for small results, written by host_copy_kernel
+  static constexpr size_t kMappedBytes = (size_t)64 << 10;
+  uint8_t *h_mapped = nullptr;
   // H2D ingest ring: host rows are copied into a pinned slot while the DMA of
   // the previous slot runs (bulk appender path)
   static constexpr int kStageSlots = 4;
@@ -90,6 +125,7 @@ struct Engine {
     if (has_gpu) {
       hipSetDevice(device);
       if (stream) hipStreamSynchronize(stream);
+      pool.reset();  // returns cached buffers before the stream goes away
       for (auto &e : ev_pool) {
         hipEventDestroy(e.first);
         hipEventDestroy(e.second);
@@ -97,7 +133,9 @@ struct Engine {
       if (d_err) hipFree(d_err);
       if (d_scratch) hipFree(d_scratch);
       if (d_small) hipFree(d_small);
+      if (d_partials) hipFree(d_partials);
       if (h_pinned) hipHostFree(h_pinned);
+      if (h_mapped) hipHostFree(h_mapped);
       for (int i = 0; i < kStageSlots; i++) {
         if (h_stage[i]) hipHostFree(h_stage[i]);
         if (stage_ev[i]) hipEventDestroy(stage_ev[i]);
@@ -127,12 +165,16 @@ std::shared_ptr<Engine> CreateEngine(int device, bool allow_no_gpu) {
   e->device = device;
   HIPCHK(hipSetDevice(device));
   HIPCHK(hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking));
+  e->pool = std::make_shared<SmallPool>();
+  e->pool->s = e->stream;
   HIPCHK(hipMalloc(&e->d_err, 256));
   HIPCHK(hipMalloc(&e->d_scratch, 4096));
   HIPCHK(hipMalloc(&e->d_small, 1 << 16));
+  HIPCHK(hipMalloc(&e->d_partials, sizeof(dev::AggPartial) * dev::kMaxAggPartials));
   HIPCHK(hipMemset(e->d_err, 0, 256));
   e->h_pinned_bytes = 1 << 20;
   HIPCHK(hipHostMalloc((void **)&e->h_pinned, e->h_pinned_bytes, hipHostMallocDefault));
+  HIPCHK(hipHostMalloc((void **)&e->h_mapped, Engine::kMappedBytes, hipHostMallocCoherent | hipHostMallocMapped));
   e->has_gpu = true;
   return e;
 }
@@ -170,11 +212,19 @@ struct ProfScope {
 // ---------------------------------------------------------------------------
 // device buffers and relations
 // ---------------------------------------------------------------------------
+// Small intermediate buffers (<= 1 MiB: aggregate states, result columns of
+// aggregates, scan counters) are recycled per power-of-two class instead of
+// going through hipMallocAsync/hipFreeAsync each query.  Reuse is stream-
+// ordered: every user of a connection's buffers runs on its one stream.
 struct DevBuf {
   void *p = nullptr;
   hipStream_t s = nullptr;
+  std::shared_ptr<SmallPool> pool;
+  int cls = -1;
   ~DevBuf() {
-    if (p) (void)hipFreeAsync(p, s);
+    if (!p) return;
+    if (pool && pool->Put(cls, p)) return;
+    (void)hipFreeAsync(p, s);
   }
 };
 typedef std::shared_ptr<DevBuf> DevBufPtr;
@@ -184,7 +234,14 @@ static DevBufPtr Alloc(Engine &e, size_t bytes, bool zero = false) {
   b->s = e.stream;
   if (bytes == 0) bytes = 16;
   bytes = (bytes + 255) & ~(size_t)255;
-  HIPCHK(hipMallocAsync(&b->p, bytes, e.stream));
+  int cls = SmallPool::Class(bytes);
+  if (cls >= 0) {
+    b->pool = e.pool;
+    b->cls = cls;
+    bytes = SmallPool::ClassBytes(cls);
+    b->p = e.pool->Get(cls);
+  }
+  if (!b->p) HIPCHK(hipMallocAsync(&b->p, bytes, e.stream));
   if (zero) HIPCHK(hipMemsetAsync(b->p, 0, bytes, e.stream));
   return b;
 }
@@ -644,7 +701,7 @@ struct StrOut {
   int src_col;  // -1: pool only
 };
 
-static DCol AllocOut(Engine &e, const LogicalType &t, int64_t n, bool with_valid) {
+static DCol AllocOut(Engine &e, const LogicalType &t, int64_t n, bool with_valid, bool zero_valid = true) {
   DCol d;
   d.type = t;
   d.phys = PhysOf(t);
@@ -653,7 +710,7 @@ static DCol AllocOut(Engine &e, const LogicalType &t, int64_t n, bool with_valid
   d.data = b->p;
   d.owners.push_back(b);
   if (with_valid) {
-    auto v = Alloc(e, Words64(std::max<int64_t>(n, 1)) * 8, true);
+    auto v = Alloc(e, Words64(std::max<int64_t>(n, 1)) * 8, zero_valid);
     d.validity = (uint64_t *)v->p;
     d.owners.push_back(v);
   }
@@ -906,7 +963,8 @@ static DRel Aggregate(Engine &e, const DRel &src, const BoundSelect &s) {
       bool empty = lo > hi;
       dev::AggState *st = (dev::AggState *)e.d_small;
       unsigned long long *cstar = (unsigned long long *)((char *)e.d_small + 1024);
-      dev::InitAggStatesCounts(st, 1, cstar, 1, e.stream);
+      int npartials = 0;
+      if (empty) dev::InitAggStatesCounts(st, 1, cstar, 1, e.stream);
       if (!empty) {
         const DCol *P = pcol >= 0 ? &src.cols[pcol] : nullptr;
         const DCol *A = acol >= 0 ? &src.cols[acol] : nullptr;
@@ -931,10 +989,12 @@ static DRel Aggregate(Engine &e, const DRel &src, const BoundSelect &s) {
             i128 m = m1 > m2 ? m1 : m2;
             if (m <= (i128)INT64_MAX) maxabs = (uint64_t)m;
           }
-          dev::FilterAggStates(P->data, P->phys, (int64_t)lo, (int64_t)hi, pcol >= 0, A ? A->data : nullptr,
-                               A ? A->phys : P_I64, src.n, st, cstar, 0, e.stream, need_mm, maxabs);
+          npartials = dev::FilterAggStates(P->data, P->phys, (int64_t)lo, (int64_t)hi, pcol >= 0, A ? A->data : nullptr,
+                                           A ? A->phys : P_I64, src.n, st, cstar, 0, e.stream, need_mm, maxabs,
+                                           e.d_partials);
         } else {
           // COUNT(*) without predicate: the row count is known
+          dev::InitAggStatesCounts(st, 1, cstar, 1, e.stream);
           unsigned long long c = (unsigned long long)src.n;
           HIPCHK(hipMemcpyAsync(cstar, &c, 8, hipMemcpyHostToDevice, e.stream));
           HIPCHK(hipStreamSynchronize(e.stream));
@@ -947,8 +1007,10 @@ static DRel Aggregate(Engine &e, const DRel &src, const BoundSelect &s) {
       D.cstar = cstar;
       D.nslots = 1;
       D.null_slot = -1;
+      D.partials = e.d_partials;
+      D.npartials = npartials;
       for (int j = 0; j < na; j++) {
-        DCol oc = AllocOut(e, s.aggs[j].type, 1, true);
+        DCol oc = AllocOut(e, s.aggs[j].type, 1, true, false);
         D.a[j] = EmitFor(s.aggs[j], VC_I64, s.aggs[j].kind == A_COUNT_STAR ? nullptr : st, oc);
         out.cols.push_back(oc);
       }
@@ -1035,13 +1097,13 @@ static DRel Aggregate(Engine &e, const DRel &src, const BoundSelect &s) {
           D.key_phys = PhysOf(s.groups[0]->type);
           D.kmin = (int64_t)ks->imin;
           D.null_slot = -1;
-          DCol kc = AllocOut(e, s.groups[0]->type, ngroups, true);
+          DCol kc = AllocOut(e, s.groups[0]->type, ngroups, true, false);
           D.key_out = kc.data;
           D.key_valid = (uint32_t *)kc.validity;
           out.n = ngroups;
           out.cols.push_back(kc);
           for (int j = 0; j < na; j++) {
-            DCol oc = AllocOut(e, s.aggs[j].type, ngroups, true);
+            DCol oc = AllocOut(e, s.aggs[j].type, ngroups, true, false);
             dev::AggState *stp = nullptr;
             if (s.aggs[j].kind != A_COUNT_STAR) {
               int c = StripWidening(s.aggs[j].arg.get())->col;
@@ -1096,7 +1158,7 @@ static DRel Aggregate(Engine &e, const DRel &src, const BoundSelect &s) {
     D.null_slot = -1;
     out.n = 1;
     for (int j = 0; j < na; j++) {
-      DCol oc = AllocOut(e, s.aggs[j].type, 1, true);
+      DCol oc = AllocOut(e, s.aggs[j].type, 1, true, false);
       VClass ic = arg_idx[j] >= 0 ? ClassOf(tmp.cols[arg_idx[j]].type) : VC_I64;
       D.a[j] = EmitFor(s.aggs[j], ic, (dev::AggState *)sb->p + j, oc);
       out.cols.push_back(oc);
@@ -1157,13 +1219,13 @@ static DRel Aggregate(Engine &e, const DRel &src, const BoundSelect &s) {
   D.key_phys = PhysOf(s.groups[0]->type);
   D.kmin = kmin;
   D.null_slot = nslots - 1;
-  DCol kc = AllocOut(e, s.groups[0]->type, ngroups, true);
+  DCol kc = AllocOut(e, s.groups[0]->type, ngroups, true, false);
   D.key_out = kc.data;
   D.key_valid = (uint32_t *)kc.validity;
   out.n = ngroups;
   out.cols.push_back(kc);
   for (int j = 0; j < na; j++) {
-    DCol oc = AllocOut(e, s.aggs[j].type, ngroups, true);
+    DCol oc = AllocOut(e, s.aggs[j].type, ngroups, true, false);
     VClass ic = arg_idx[j] >= 0 ? ClassOf(tmp.cols[arg_idx[j]].type) : VC_I64;
     D.a[j] = EmitFor(s.aggs[j], ic, states[j] ? (dev::AggState *)states[j]->p : nullptr, oc);
     out.cols.push_back(oc);
@@ -1319,27 +1381,42 @@ static ResultPtr ToHostPinned(Engine &e, const DRel &r, const std::vector<std::s
     need += ((size_t)n * PhysSize(d.phys) + 63) & ~(size_t)63;
     if (d.validity) need += ((size_t)(w1 - w0) * 8 + 63) & ~(size_t)63;
   }
-  if (!e.EnsurePinned(need)) return nullptr;
+  // small results: one copy kernel into the coherent mapped buffer instead of
+  // one DMA per buffer; larger ones: DMA into the (growable) pinned arena
+  const bool mapped = need <= Engine::kMappedBytes && ncols * 2 <= HOSTCOPY_MAX && !getenv("MBX_NO_HOSTCOPY");
+  if (!mapped && !e.EnsurePinned(need)) return nullptr;
+  uint8_t *const H = mapped ? e.h_mapped : e.h_pinned;
   std::vector<size_t> data_off(ncols), valid_off(ncols, 0);
+  dev::HostCopyDesc hd;
+  memset(&hd, 0, sizeof(hd));
+  auto seg = [&](const void *src, size_t off, size_t bytes) {
+    if (mapped) hd.seg[hd.nseg++] = dev::HostCopySeg{src, H + off, (int64_t)bytes};
+    else HIPCHK(hipMemcpyAsync(H + off, src, bytes, hipMemcpyDeviceToHost, e.stream));
+  };
   size_t at = 64;  // [0, 4): error word
-  HIPCHK(hipMemcpyAsync(e.h_pinned, e.d_err, 4, hipMemcpyDeviceToHost, e.stream));
+  if (!mapped) HIPCHK(hipMemcpyAsync(H, e.d_err, 4, hipMemcpyDeviceToHost, e.stream));
   for (size_t c = 0; c < ncols; c++) {
     const DCol &d = r.cols[c];
     const int sz = PhysSize(d.phys);
     size_t bytes = (size_t)n * sz;
     data_off[c] = at;
-    if (bytes) HIPCHK(hipMemcpyAsync(e.h_pinned + at, (const char *)d.data + (size_t)start * sz, bytes, hipMemcpyDeviceToHost, e.stream));
+    if (bytes) seg((const char *)d.data + (size_t)start * sz, at, bytes);
     at += (bytes + 63) & ~(size_t)63;
     if (d.validity) {
       valid_off[c] = at;
       size_t vb = (size_t)(w1 - w0) * 8;
-      if (n > 0) HIPCHK(hipMemcpyAsync(e.h_pinned + at, d.validity + w0, vb, hipMemcpyDeviceToHost, e.stream));
+      if (n > 0) seg(d.validity + w0, at, vb);
       at += (vb + 63) & ~(size_t)63;
     }
   }
+  if (mapped) {
+    hd.err_src = e.d_err;
+    hd.err_dst = (int32_t *)H;
+    dev::HostCopy(hd, e.stream);
+  }
   HIPCHK(hipStreamSynchronize(e.stream));
   int32_t err;
-  memcpy(&err, e.h_pinned, 4);
+  memcpy(&err, (const void *)H, 4);
   RaiseDeviceError(e, err);
   auto res = std::make_shared<MaterializedResult>();
   res->nrows = n;
@@ -1350,9 +1427,9 @@ static ResultPtr ToHostPinned(Engine &e, const DRel &r, const std::vector<std::s
     hc.type = d.type;
     hc.phys = d.phys;
     size_t bytes = (size_t)n * PhysSize(d.phys);
-    hc.data.assign(e.h_pinned + data_off[c], e.h_pinned + data_off[c] + bytes);
+    hc.data.assign(H + data_off[c], H + data_off[c] + bytes);
     if (d.validity && n > 0) {
-      const uint64_t *bm = (const uint64_t *)(e.h_pinned + valid_off[c]);
+      const uint64_t *bm = (const uint64_t *)(H + valid_off[c]);
       const int64_t sh = start - (w0 << 6);
       hc.valid.resize(n);
       for (int64_t i = 0; i < n; i++) hc.valid[i] = (bm[(i + sh) >> 6] >> ((i + sh) & 63)) & 1;

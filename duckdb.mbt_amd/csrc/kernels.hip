@@ -853,7 +853,7 @@ __device__ __forceinline__ void acc_row(Acc &A, bool ok, int64_t v, bool mm, boo
 template <typename T, int MODE, int DEPTH, bool MM, bool NARROW>
 __global__ __launch_bounds__(256) void filter_agg_lds_kernel(const T *__restrict__ p, const T *__restrict__ a, int64_t n,
                                                              int64_t lo, uint64_t span, AggState *st,
-                                                             unsigned long long *cstar) {
+                                                             unsigned long long *cstar, AggPartial *partials) {
   constexpr int NS = MODE == 1 ? 2 : 1;
   constexpr int RPL = 16 / (int)sizeof(T);
   constexpr int64_t RP = 64 * RPL;
@@ -927,8 +927,12 @@ __global__ __launch_bounds__(256) void filter_agg_lds_kernel(const T *__restrict
   if (threadIdx.x == 0) {
     Acc T0 = part[0];
     for (int i = 1; i < 4; i++) acc_merge(T0, part[i]);
-    if (cstar) atomicAdd(cstar, (unsigned long long)T0.cnt);
-    if (MODE != 2 && st) agg_state_atomic(st, T0);
+    if (partials) {
+      partials[blockIdx.x] = AggPartial{T0.cnt, T0.slo, T0.shi, T0.mn, T0.mx};
+    } else {
+      if (cstar) atomicAdd(cstar, (unsigned long long)T0.cnt);
+      if (MODE != 2 && st) agg_state_atomic(st, T0);
+    }
   }
 }
 
@@ -1010,6 +1014,7 @@ static FaVariant FaConfig(int mode) {
 
 static bool g_fa_pairs = true;
 static bool g_fa_mm = true, g_fa_narrow = false;  // per launch, set by FilterAggStates
+static AggPartial *g_fa_partials = nullptr;
 template <typename TP, typename TA, int MODE, int U, bool NT, bool CH>
 static void LaunchFA(const void *p, const void *a, int64_t n, int64_t lo, uint64_t span, AggState *st,
                      unsigned long long *cstar, int grid, hipStream_t s) {
@@ -1027,12 +1032,17 @@ static void LaunchFALds(const void *p, const void *a, int64_t n, int64_t lo, uin
                         unsigned long long *cstar, int grid, hipStream_t s) {
 #define FAL(MM, NW)                                                                                                   \
   hipLaunchKernelGGL((filter_agg_lds_kernel<T, MODE, DEPTH, MM, NW>), dim3(grid), dim3(256), 0, s, (const T *)p,   \
-                     (const T *)a, n, lo, span, st, cstar)
+                     (const T *)a, n, lo, span, st, cstar, g_fa_partials)
   if (MODE == 2) FAL(false, false);
   else if (g_fa_mm) { if (g_fa_narrow) FAL(true, true); else FAL(true, false); }
   else { if (g_fa_narrow) FAL(false, true); else FAL(false, false); }
 #undef FAL
   CHECK_LAUNCH();
+}
+
+// true when LaunchFilterAgg takes the LDS-DMA kernel for this shape
+static bool FaUsesLds(const FaVariant &v, int mode, int pphys, int aphys) {
+  return v.lds_depth > 0 && (mode != 1 || pphys == aphys);
 }
 
 template <typename TP, typename TA, int MODE>
@@ -1063,10 +1073,13 @@ static void LaunchFilterAgg(const FaVariant &v, const void *p, const void *a, in
 #undef FA
 }
 
-void FilterAggStates(const void *pcol, int pphys, int64_t lo, int64_t hi, bool has_pred, const void *acol, int aphys,
-                     int64_t nrows, AggState *st, unsigned long long *cstar, int grid_blocks, hipStream_t s,
-                     bool need_minmax, uint64_t sum_maxabs) {
-  if (nrows <= 0) return;
+int FilterAggStates(const void *pcol, int pphys, int64_t lo, int64_t hi, bool has_pred, const void *acol, int aphys,
+                    int64_t nrows, AggState *st, unsigned long long *cstar, int grid_blocks, hipStream_t s,
+                    bool need_minmax, uint64_t sum_maxabs, AggPartial *partials) {
+  if (nrows <= 0) {
+    InitAggStatesCounts(st, 1, cstar, 1, s);
+    return 0;
+  }
   uint64_t span = has_pred ? (uint64_t)hi - (uint64_t)lo : ~0ull;
   if (!has_pred) lo = INT64_MIN;
   int mode = acol == nullptr ? 2 : (acol == pcol ? 0 : 1);
@@ -1084,6 +1097,9 @@ void FilterAggStates(const void *pcol, int pphys, int64_t lo, int64_t hi, bool h
   int64_t groups = (nrows >> 2) + 1;
   if (grid > groups) grid = (int)groups;
   g_fa_mm = need_minmax;
+  const bool use_partials = partials && FaUsesLds(v, mode, pphys, aphys) && grid <= kMaxAggPartials;
+  g_fa_partials = use_partials ? partials : nullptr;
+  if (!use_partials) InitAggStatesCounts(st, 1, cstar, 1, s);
   // LDS-DMA kernel: a lane sees at most (ceil(pieces / waves) + 1) pieces of
   // 16 B, i.e. that many times 2 (int64) or 4 (int32) rows, tail included.
   {
@@ -1106,6 +1122,8 @@ void FilterAggStates(const void *pcol, int pphys, int64_t lo, int64_t hi, bool h
     else if (aphys == P_I64) LaunchFilterAgg<int32_t, int64_t, 1>(v, pcol, acol, nrows, lo, span, st, cstar, grid, s);
     else LaunchFilterAgg<int32_t, int32_t, 1>(v, pcol, acol, nrows, lo, span, st, cstar, grid, s);
   }
+  g_fa_partials = nullptr;
+  return use_partials ? grid : 0;
 }
 
 __global__ __launch_bounds__(256) void copy_kernel(const float4 *__restrict__ in, float4 *__restrict__ out, int64_t n) {
@@ -1956,67 +1974,133 @@ namespace mbx {
 namespace dev {
 
 // Writes the aggregate relation [key?, agg0, agg1, ...] from per-slot states.
-__global__ void emit_agg_kernel(EmitDesc D) {
+// Writes the aggregate relation.  Validity bitmaps are written as whole
+// 64-bit words from a wave ballot (each wave owns 64 consecutive output rows),
+// so the output bitmaps need no zeroing and no atomics.
+__global__ __launch_bounds__(256) void emit_agg_kernel(EmitDesc D) {
+  if (D.npartials > 0) {
+    // slot 0 from the filter-aggregate's per-workgroup partials (one workgroup)
+    __shared__ Acc part[4];
+    Acc A;
+    A.cnt = 0; A.slo = 0; A.shi = 0; A.mn = INT64_MAX; A.mx = INT64_MIN;
+    for (int i = threadIdx.x; i < D.npartials; i += blockDim.x) {
+      const AggPartial &q = D.partials[i];
+      Acc B;
+      B.cnt = q.cnt; B.slo = q.slo; B.shi = q.shi; B.mn = q.mn; B.mx = q.mx;
+      acc_merge(A, B);
+    }
+    acc_wave_reduce(A);
+    if ((threadIdx.x & 63) == 0) part[threadIdx.x >> 6] = A;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      Acc T0 = part[0];
+      for (int i = 1; i < (int)(blockDim.x >> 6); i++) acc_merge(T0, part[i]);
+      unsigned long long *cs = (unsigned long long *)D.cstar;
+      cs[0] = T0.cnt;
+      for (int j = 0; j < D.nagg; j++) {
+        AggState *S = D.a[j].states;
+        if (!S) continue;
+        S->count = T0.cnt;
+        S->sum_lo = T0.slo;
+        S->sum_hi = T0.shi;
+        S->min_i = T0.mn;
+        S->max_i = T0.mx;
+      }
+      __threadfence_block();
+    }
+    __syncthreads();
+  }
   const int64_t n = D.slot_list ? *D.n_list : D.nslots;
-  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
-    const int64_t sl = D.slot_list ? D.slot_list[i] : i;
+  const int lane = threadIdx.x & 63;
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t base = (int64_t)blockIdx.x * blockDim.x + (threadIdx.x & ~63); base < n; base += stride) {
+    const int64_t i = base + lane;
+    const bool in = i < n;
+    const int64_t sl = in ? (D.slot_list ? D.slot_list[i] : i) : 0;
     if (D.has_key) {
-      if (sl == D.null_slot) {
-        store_phys(D.key_out, D.key_phys, i, 0, 0);
-      } else {
+      bool kv = in && sl != D.null_slot;
+      if (in) {
         int64_t k = D.kmin + sl;
-        store_phys(D.key_out, D.key_phys, i, k, k >> 63);
-        atomicOr(&D.key_valid[i >> 5], 1u << (i & 31));
+        if (kv) store_phys(D.key_out, D.key_phys, i, k, k >> 63);
+        else store_phys(D.key_out, D.key_phys, i, 0, 0);
+      }
+      uint64_t m = __ballot(kv);
+      if (lane == 0) {
+        D.key_valid[base >> 5] = (uint32_t)m;
+        if (base + 32 < n) D.key_valid[(base >> 5) + 1] = (uint32_t)(m >> 32);
       }
     }
     for (int j = 0; j < D.nagg; j++) {
       const EmitAgg &A = D.a[j];
-      bool valid = true;
+      bool valid = in;
       int64_t lo = 0, hi = 0;
-      if (A.kind == 0 /*COUNT_STAR*/) {
-        lo = (int64_t)D.cstar[sl];
-      } else {
-        const AggState &S = A.states[sl];
-        switch (A.kind) {
-          case 1: /*COUNT*/ lo = (int64_t)S.count; break;
-          case 2: /*SUM*/
-            if (!S.count) { valid = false; break; }
-            if (A.in_class == VC_F64) lo = __double_as_longlong(S.sum_f);
-            else { lo = (int64_t)S.sum_lo; hi = S.sum_hi; }
-            break;
-          case 3: /*MIN*/
-          case 4: /*MAX*/
-            if (!S.count) { valid = false; break; }
-            if (A.in_class == VC_F64) lo = __double_as_longlong(f64_unorder(A.kind == 3 ? S.min_f : S.max_f));
-            else { lo = A.kind == 3 ? S.min_i : S.max_i; hi = lo >> 63; }
-            break;
-          default: /*AVG*/ {
-            if (!S.count) { valid = false; break; }
-            double v;
-            if (A.in_class == VC_F64) v = S.sum_f / (double)S.count;
-            else {
-              double sum = i128_to_double(mk128((int64_t)S.sum_lo, S.sum_hi));
-              double div = (double)S.count;
-              for (int k = 0; k < A.avg_scale; k++) div *= 10.0;
-              v = sum / div;
+      if (in) {
+        if (A.kind == 0 /*COUNT_STAR*/) {
+          lo = (int64_t)D.cstar[sl];
+        } else {
+          const AggState &S = A.states[sl];
+          switch (A.kind) {
+            case 1: /*COUNT*/ lo = (int64_t)S.count; break;
+            case 2: /*SUM*/
+              if (!S.count) { valid = false; break; }
+              if (A.in_class == VC_F64) lo = __double_as_longlong(S.sum_f);
+              else { lo = (int64_t)S.sum_lo; hi = S.sum_hi; }
+              break;
+            case 3: /*MIN*/
+            case 4: /*MAX*/
+              if (!S.count) { valid = false; break; }
+              if (A.in_class == VC_F64) lo = __double_as_longlong(f64_unorder(A.kind == 3 ? S.min_f : S.max_f));
+              else { lo = A.kind == 3 ? S.min_i : S.max_i; hi = lo >> 63; }
+              break;
+            default: /*AVG*/ {
+              if (!S.count) { valid = false; break; }
+              double v;
+              if (A.in_class == VC_F64) v = S.sum_f / (double)S.count;
+              else {
+                double sum = i128_to_double(mk128((int64_t)S.sum_lo, S.sum_hi));
+                double div = (double)S.count;
+                for (int k = 0; k < A.avg_scale; k++) div *= 10.0;
+                v = sum / div;
+              }
+              lo = __double_as_longlong(v);
+              break;
             }
-            lo = __double_as_longlong(v);
-            break;
           }
         }
+        if (valid) store_phys(A.out, A.out_phys, i, lo, hi);
+        else store_phys(A.out, A.out_phys, i, 0, 0);
       }
-      if (valid) {
-        store_phys(A.out, A.out_phys, i, lo, hi);
-        atomicOr(&A.valid[i >> 5], 1u << (i & 31));
-      } else {
-        store_phys(A.out, A.out_phys, i, 0, 0);
+      uint64_t m = __ballot(valid);
+      if (lane == 0) {
+        A.valid[base >> 5] = (uint32_t)m;
+        if (base + 32 < n) A.valid[(base >> 5) + 1] = (uint32_t)(m >> 32);
       }
     }
   }
 }
 
 void EmitAggRelation(const EmitDesc &d, hipStream_t s) {
-  hipLaunchKernelGGL(emit_agg_kernel, dim3(GridFor(d.nslots, 256, 1024)), dim3(256), 0, s, d);
+  hipLaunchKernelGGL(emit_agg_kernel, dim3(d.npartials > 0 ? 1 : GridFor(d.nslots, 256, 1024)), dim3(256), 0, s, d);
+  CHECK_LAUNCH();
+}
+
+__global__ __launch_bounds__(256) void host_copy_kernel(HostCopyDesc D) {
+  if ((int)blockIdx.x < D.nseg) {
+    const HostCopySeg g = D.seg[blockIdx.x];
+    const int64_t words = ((((uintptr_t)g.src | (uintptr_t)g.dst) & 7) == 0) ? g.bytes >> 3 : 0;
+    const uint64_t *s8 = (const uint64_t *)g.src;
+    uint64_t *d8 = (uint64_t *)g.dst;
+    for (int64_t i = threadIdx.x; i < words; i += blockDim.x) d8[i] = s8[i];
+    const uint8_t *s1 = (const uint8_t *)g.src;
+    uint8_t *d1 = (uint8_t *)g.dst;
+    for (int64_t i = (words << 3) + threadIdx.x; i < g.bytes; i += blockDim.x) d1[i] = s1[i];
+  }
+  if (blockIdx.x == 0 && threadIdx.x == 0) *D.err_dst = *D.err_src;
+  __threadfence_system();
+}
+
+void HostCopy(const HostCopyDesc &d, hipStream_t s) {
+  hipLaunchKernelGGL(host_copy_kernel, dim3(d.nseg > 0 ? d.nseg : 1), dim3(256), 0, s, d);
   CHECK_LAUNCH();
 }
 

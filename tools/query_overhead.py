@@ -1,0 +1,37 @@
+#!/usr/bin/env python3
+"""Per-query host overhead of the fused C2 path: end-to-end time of
+duckdb_mb_query (+ result cell read) vs the kernel time, with and without
+the per-kernel event profile.  GPU only.  Usage: query_overhead.py [rows]"""
+import json
+import os
+import statistics
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+import __graft_entry__ as ge  # noqa: E402
+
+m = ge._load()
+n = int(sys.argv[1]) if len(sys.argv) > 1 else 1_000_000
+out = {}
+for prof in ("false", "true"):
+    cfg = m.Config.create()
+    cfg.set("mbx_profile", prof)
+    c = m.connect_with_config(cfg).value
+    c.query(f"CREATE TABLE t AS SELECT mbx_synth(42, i, 50) + 1 AS x FROM range({n}) tbl(i)")
+    for sql in ("SELECT COUNT(*) FROM t WHERE x > 24", "SELECT 1"):
+        ts = []
+        for i in range(300):
+            t0 = time.perf_counter()
+            rr = c.query_raw(sql)
+            rr.value(0, 0)
+            rr.close()
+            ts.append(time.perf_counter() - t0)
+        out[f"profile={prof} {sql}"] = {"median_us": statistics.median(ts[50:]) * 1e6, "min_us": min(ts) * 1e6}
+    if prof == "true":
+        c.profile_drain()
+        c.query_raw("SELECT COUNT(*) FROM t WHERE x > 24").close()
+        out["profile kernels"] = c.last_profile()
+    c.close()
+print(json.dumps(out, indent=1))
