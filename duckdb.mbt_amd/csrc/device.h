@@ -94,8 +94,13 @@ void CompactSlots(const unsigned long long *count_star, int64_t nslots, int32_t 
 // Order-preserving u64 keys of a column (asc; desc flips; nulls per flag).
 void SortKeyU64(const void *col, int phys, const uint64_t *valid, int64_t n, const int64_t *perm, bool desc,
                 bool nulls_first, uint64_t *keys, hipStream_t s);
-void SortPairs(uint64_t *keys_in, int64_t *vals_in, uint64_t *keys_out, int64_t *vals_out, int64_t n,
-               hipStream_t s);
+void SortPairs(uint64_t *keys_in, int64_t *vals_in, uint64_t *keys_out, int64_t *vals_out, int64_t n, hipStream_t s,
+               int end_bit = 64);
+void SortKeyNull(const uint64_t *valid, int64_t n, const int64_t *perm, bool nulls_first, uint64_t *keys,
+                 hipStream_t s);
+void SortKeyStr(const int64_t *offsets, const char *chars, const uint64_t *valid, int64_t n, const int64_t *perm,
+                int64_t chunk, bool desc, uint64_t *keys, hipStream_t s);
+void StrMaxLen(const int64_t *offsets, int64_t n, unsigned long long *out, hipStream_t s);
 void Iota(int64_t *p, int64_t n, int64_t start, hipStream_t s);
 // out[i] = in[idx[i]] for fixed-width phys; validity likewise (bitmap)
 void GatherFixed(const void *in, int phys, const uint64_t *in_valid, const int64_t *idx, int64_t n, void *out,
@@ -161,6 +166,27 @@ struct EmitDesc {
   int32_t npartials;
 };
 void EmitAggRelation(const EmitDesc &d, hipStream_t s);
+
+// ---- hash GROUP BY (any number of fixed-width / VARCHAR keys) --------------
+struct HashKeyCol {
+  const void *data;
+  const uint64_t *validity;
+  const int64_t *offsets;  // P_STR
+  const char *chars;       // P_STR
+  int32_t phys;
+};
+#define HASH_MAX_KEYS 8
+struct HashKeys {
+  int32_t nk;
+  HashKeyCol k[HASH_MAX_KEYS];
+};
+// Open-addressing table (cap = power of two >= 2n, 8 B/entry: 24-bit hash
+// tag | 40-bit representative row).  Produces slot_of_row in [0, ngroups)
+// (dense group ids in table order), rep_row[g], count_star[g] and
+// *ngroups (device).  Scratch: table (cap x 8 B), entry ids (cap x 4 B).
+void HashGroupAssign(const HashKeys &k, int64_t n, unsigned long long *table, int64_t cap, int32_t *slot_of_row,
+                     int32_t *gid_of_entry, int64_t *rep_row, unsigned long long *count_star, int64_t *ngroups,
+                     int32_t *err, hipStream_t s);
 
 // Small results: one kernel copies every result buffer (and the device error
 // word) into coherent pinned host memory, replacing a DMA per buffer.

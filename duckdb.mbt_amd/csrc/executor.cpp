@@ -299,6 +299,7 @@ static void RaiseDeviceError(Engine &e, int32_t err) {
       case E_OVF_MUL: ThrowError("Out of Range", "Overflow in multiplication!");
       case E_OVF_NEG: ThrowError("Out of Range", "Overflow in negation!");
       case E_CAST_RANGE: ThrowError("Conversion", "Value out of range for the destination type in CAST");
+      case E_HASH_FULL: ThrowError("Internal", "hash aggregate table overflow");
       default: ThrowError("Out of Range", "Decimal value out of range");
     }
   }
@@ -931,6 +932,86 @@ static void DropEmptyValidity(Engine &e, DRel &r) {
   (void)r;
 }
 
+static DRel GatherRel(Engine &e, const DRel &r, const int64_t *perm, int64_t n);
+
+// GROUP BY through the device hash table (HashGroupAssign): works for any
+// number of keys of any fixed-width or VARCHAR type.  Keys are emitted by
+// gathering each group's representative row; groups come out in table
+// order (DuckDB's hash aggregate has no defined order either).
+static DRel HashAggregate(Engine &e, const DRel &tmp, const BoundSelect &s, const std::vector<int> &arg_idx) {
+  const int ng = (int)s.groups.size();
+  const int na = (int)s.aggs.size();
+  if (ng > HASH_MAX_KEYS) ThrowError("Not implemented", "GROUP BY with more than 8 keys");
+  dev::HashKeys hk;
+  memset(&hk, 0, sizeof(hk));
+  hk.nk = ng;
+  for (int g = 0; g < ng; g++) {
+    const DCol &c = tmp.cols[g];
+    if (c.phys == P_INTERVAL) ThrowError("Not implemented", "GROUP BY on INTERVAL keys is not supported on device");
+    if (c.phys == P_STR && (!c.offsets || !c.chars))
+      ThrowError("Internal", "GROUP BY VARCHAR key without materialised strings");
+    hk.k[g] = dev::HashKeyCol{c.data, c.validity, c.offsets, c.chars, (int32_t)c.phys};
+  }
+  const int64_t n = tmp.n;
+  int64_t cap = 1024;
+  while (cap < 2 * n) cap <<= 1;
+  if (cap > ((int64_t)1 << 31)) ThrowError("Not implemented", "GROUP BY input above 2^30 rows on the hash path");
+  auto table = Alloc(e, (size_t)cap * 8);
+  HIPCHK(hipMemsetAsync(table->p, 0xFF, (size_t)cap * 8, e.stream));
+  auto slot_of = Alloc(e, (size_t)std::max<int64_t>(n, 1) * 4);
+  auto gid = Alloc(e, (size_t)cap * 4);
+  auto rep = Alloc(e, (size_t)std::max<int64_t>(n, 1) * 8);
+  auto cs = Alloc(e, (size_t)std::max<int64_t>(n, 1) * 8, true);
+  {
+    double kb = 0;
+    for (int g = 0; g < ng; g++) kb += (double)n * (tmp.cols[g].phys == P_STR ? 16 : PhysSize(tmp.cols[g].phys));
+    ProfScope ps(e, "hash_group_assign", kb, n);
+    dev::HashGroupAssign(hk, n, (unsigned long long *)table->p, cap, (int32_t *)slot_of->p, (int32_t *)gid->p,
+                         (int64_t *)rep->p, (unsigned long long *)cs->p, e.d_scratch, e.d_err, e.stream);
+  }
+  const int64_t ngroups = ReadDev<int64_t>(e, e.d_scratch);
+  CheckError(e);
+  std::vector<DevBufPtr> states(na);
+  for (int j = 0; j < na; j++) {
+    if (arg_idx[j] < 0) continue;
+    const DCol &c = tmp.cols[arg_idx[j]];
+    const void *data = c.data;
+    int phys = c.phys;
+    if (c.phys == P_STR) {
+      if (s.aggs[j].kind != A_COUNT)
+        ThrowError("Not implemented", "SUM/MIN/MAX/AVG over VARCHAR are not supported on device");
+      data = c.offsets;
+      phys = P_I64;
+    }
+    states[j] = Alloc(e, (size_t)std::max<int64_t>(ngroups, 1) * sizeof(dev::AggState));
+    dev::InitAggStates((dev::AggState *)states[j]->p, ngroups, e.stream);
+    ProfScope ps(e, "group_reduce", (double)n * (PhysSize((Phys)phys) + 4), n);
+    dev::GroupReduceColumn((const int32_t *)slot_of->p, data, phys, c.validity, n, (dev::AggState *)states[j]->p,
+                           e.stream);
+  }
+  DRel keys;
+  keys.n = n;
+  for (int g = 0; g < ng; g++) keys.cols.push_back(tmp.cols[g]);
+  DRel out = GatherRel(e, keys, (const int64_t *)rep->p, ngroups);
+  for (int g = 0; g < ng; g++) out.cols[g].type = s.groups[g]->type;
+  dev::EmitDesc D;
+  memset(&D, 0, sizeof(D));
+  D.nagg = na;
+  D.cstar = (const unsigned long long *)cs->p;
+  D.nslots = ngroups;
+  D.null_slot = -1;
+  for (int j = 0; j < na; j++) {
+    DCol oc = AllocOut(e, s.aggs[j].type, ngroups, true, false);
+    VClass ic = arg_idx[j] >= 0 ? ClassOf(tmp.cols[arg_idx[j]].type) : VC_I64;
+    D.a[j] = EmitFor(s.aggs[j], ic, states[j] ? (dev::AggState *)states[j]->p : nullptr, oc);
+    out.cols.push_back(oc);
+  }
+  if (ngroups > 0) dev::EmitAggRelation(D, e.stream);
+  HIPCHK(hipStreamSynchronize(e.stream));
+  out.n = ngroups;
+  return out;
+}
+
 static DRel Aggregate(Engine &e, const DRel &src, const BoundSelect &s) {
   const int ng = (int)s.groups.size();
   const int na = (int)s.aggs.size();
@@ -1167,18 +1248,24 @@ static DRel Aggregate(Engine &e, const DRel &src, const BoundSelect &s) {
     HIPCHK(hipStreamSynchronize(e.stream));
     return out;
   }
-  if (ng > 1) ThrowError("Not implemented", "GROUP BY with more than one key is not supported on the MI355X device path yet");
+  // one integer key with a narrow range: direct-index slots; anything else
+  // (several keys, VARCHAR/float keys, wide ranges): the hash table
   const DCol &K = tmp.cols[0];
-  if (ClassOf(K.type) != VC_I64 || K.phys == P_STR || K.phys == P_F64 || K.phys == P_F32)
-    ThrowError("Not implemented", "GROUP BY key of type " + K.type.ToString() + " is not supported on device yet");
-  long long *kr = (long long *)((char *)e.d_small + 2048);
-  dev::KeyRange(K.data, K.phys, K.validity, tmp.n, kr, e.stream);
-  long long krh[3];
-  HIPCHK(hipMemcpyAsync(krh, kr, sizeof(krh), hipMemcpyDeviceToHost, e.stream));
-  HIPCHK(hipStreamSynchronize(e.stream));
-  int64_t kmin = krh[2] ? krh[0] : 0;
-  i128 range = krh[2] ? (i128)krh[1] - krh[0] + 1 : 0;
-  if (range > (1 << 24)) ThrowError("Not implemented", "GROUP BY key range too wide for the direct-index device path");
+  bool direct = ng == 1 && ClassOf(K.type) == VC_I64 && K.phys != P_STR && K.phys != P_F64 && K.phys != P_F32 &&
+                K.phys != P_I128 && K.phys != P_INTERVAL;
+  int64_t kmin = 0;
+  i128 range = 0;
+  if (direct) {
+    long long *kr = (long long *)((char *)e.d_small + 2048);
+    dev::KeyRange(K.data, K.phys, K.validity, tmp.n, kr, e.stream);
+    long long krh[3];
+    HIPCHK(hipMemcpyAsync(krh, kr, sizeof(krh), hipMemcpyDeviceToHost, e.stream));
+    HIPCHK(hipStreamSynchronize(e.stream));
+    kmin = krh[2] ? krh[0] : 0;
+    range = krh[2] ? (i128)krh[1] - krh[0] + 1 : 0;
+    if (range > (1 << 24) || range > 4 * (i128)std::max<int64_t>(tmp.n, 1024)) direct = false;
+  }
+  if (!direct) return HashAggregate(e, tmp, s, arg_idx);
   int64_t nslots = (int64_t)range + 1;  // + NULL group
   auto slot_of = Alloc(e, std::max<int64_t>(tmp.n, 1) * 4);
   auto cs = Alloc(e, nslots * 8, true);
@@ -1281,18 +1368,37 @@ static DRel SortRel(Engine &e, const DRel &r, const std::vector<BoundOrder> &ord
   auto perm = Alloc(e, n * 8), perm2 = Alloc(e, n * 8);
   auto keys = Alloc(e, n * 8), keys2 = Alloc(e, n * 8);
   dev::Iota((int64_t *)perm->p, n, 0, e.stream);
+  // LSD over the ORDER BY keys (last key first); each key is one or more
+  // stable 64-bit radix passes, then a stable 1-bit pass placing its NULLs
+  auto pass = [&](int end_bit) {
+    ProfScope ps(e, "radix_sort", (double)n * 16, n);
+    dev::SortPairs((uint64_t *)keys->p, (int64_t *)perm->p, (uint64_t *)keys2->p, (int64_t *)perm2->p, n, e.stream,
+                   end_bit);
+    std::swap(perm, perm2);
+  };
   for (int k = (int)order.size() - 1; k >= 0; k--) {
     const BoundOrder &o = order[k];
     const DCol &c = r.cols[o.expr->col];
-    if (c.phys == P_STR) ThrowError("Not implemented", "ORDER BY a VARCHAR column is not supported on device yet");
     if (c.phys == P_I128 || c.phys == P_INTERVAL)
       ThrowError("Not implemented", "ORDER BY a " + c.type.ToString() + " column is not supported on device yet");
-    bool nulls_first = o.nulls_first;
-    dev::SortKeyU64(c.data, c.phys, c.validity, n, (const int64_t *)perm->p, o.desc, nulls_first,
-                    (uint64_t *)keys->p, e.stream);
-    ProfScope ps(e, "radix_sort", (double)n * 16, n);
-    dev::SortPairs((uint64_t *)keys->p, (int64_t *)perm->p, (uint64_t *)keys2->p, (int64_t *)perm2->p, n, e.stream);
-    std::swap(perm, perm2);
+    if (c.phys == P_STR) {
+      if (!c.offsets || !c.chars) ThrowError("Internal", "ORDER BY VARCHAR without materialised strings");
+      dev::StrMaxLen(c.offsets, n, (unsigned long long *)e.d_scratch, e.stream);
+      int64_t maxlen = ReadDev<int64_t>(e, e.d_scratch);
+      for (int64_t ch = (maxlen + 7) / 8 - 1; ch >= 0; ch--) {
+        dev::SortKeyStr(c.offsets, c.chars, c.validity, n, (const int64_t *)perm->p, ch, o.desc, (uint64_t *)keys->p,
+                        e.stream);
+        pass(64);
+      }
+    } else {
+      dev::SortKeyU64(c.data, c.phys, c.validity, n, (const int64_t *)perm->p, o.desc, o.nulls_first,
+                      (uint64_t *)keys->p, e.stream);
+      pass(64);
+    }
+    if (c.validity) {
+      dev::SortKeyNull(c.validity, n, (const int64_t *)perm->p, o.nulls_first, (uint64_t *)keys->p, e.stream);
+      pass(1);
+    }
   }
   DRel out = GatherRel(e, r, (const int64_t *)perm->p, n);
   HIPCHK(hipStreamSynchronize(e.stream));

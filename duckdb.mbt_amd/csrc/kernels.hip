@@ -1760,8 +1760,10 @@ __global__ void sort_key_kernel(const void *col, int phys, const uint64_t *valid
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
     int64_t r = perm ? perm[i] : i;
     uint64_t k;
+    // NULL placement is a separate stable 1-bit pass (SortKeyNull), so the
+    // full 64-bit value range stays distinct here
     if (!bit_valid(valid, r)) {
-      k = nulls_first ? 0ull : ~0ull;
+      k = 0ull;
     } else {
       int64_t lo, hi;
       load_phys(col, phys, r, lo, hi);
@@ -1769,10 +1771,8 @@ __global__ void sort_key_kernel(const void *col, int phys, const uint64_t *valid
       else if (phys == P_U8 || phys == P_U16 || phys == P_U32 || phys == P_U64) k = (uint64_t)lo;
       else k = (uint64_t)lo ^ 0x8000000000000000ull;
       if (desc) k = ~k;
-      // keep NULLs at the requested end: squeeze valid keys into [1, 2^64-2]
-      if (k == 0ull) k = 1ull;
-      if (k == ~0ull) k = ~1ull;
     }
+    (void)nulls_first;
     keys[i] = k;
   }
 }
@@ -1785,14 +1785,81 @@ void SortKeyU64(const void *col, int phys, const uint64_t *valid, int64_t n, con
   CHECK_LAUNCH();
 }
 
-void SortPairs(uint64_t *keys_in, int64_t *vals_in, uint64_t *keys_out, int64_t *vals_out, int64_t n, hipStream_t s) {
+void SortPairs(uint64_t *keys_in, int64_t *vals_in, uint64_t *keys_out, int64_t *vals_out, int64_t n, hipStream_t s,
+               int end_bit) {
   if (n <= 0) return;
   size_t tmp = 0;
-  (void)hipcub::DeviceRadixSort::SortPairs(nullptr, tmp, keys_in, keys_out, vals_in, vals_out, (int)n, 0, 64, s);
+  (void)hipcub::DeviceRadixSort::SortPairs(nullptr, tmp, keys_in, keys_out, vals_in, vals_out, (int)n, 0, end_bit, s);
   void *d_tmp = nullptr;
   (void)hipMallocAsync(&d_tmp, tmp, s);
-  (void)hipcub::DeviceRadixSort::SortPairs(d_tmp, tmp, keys_in, keys_out, vals_in, vals_out, (int)n, 0, 64, s);
+  (void)hipcub::DeviceRadixSort::SortPairs(d_tmp, tmp, keys_in, keys_out, vals_in, vals_out, (int)n, 0, end_bit, s);
   (void)hipFreeAsync(d_tmp, s);
+}
+
+// 1-bit NULL-placement key: the last (most significant) pass of each ORDER BY key
+__global__ void sort_key_null_kernel(const uint64_t *valid, int64_t n, const int64_t *perm, bool nulls_first,
+                                     uint64_t *keys) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    bool isnull = !bit_valid(valid, perm ? perm[i] : i);
+    keys[i] = (isnull != nulls_first) ? 1ull : 0ull;
+  }
+}
+
+void SortKeyNull(const uint64_t *valid, int64_t n, const int64_t *perm, bool nulls_first, uint64_t *keys,
+                 hipStream_t s) {
+  if (n <= 0) return;
+  hipLaunchKernelGGL(sort_key_null_kernel, dim3(GridFor(n, 256 * 4, NumCUs() * 8)), dim3(256), 0, s, valid, n, perm,
+                     nulls_first, keys);
+  CHECK_LAUNCH();
+}
+
+// VARCHAR ORDER BY: LSD over 8-byte chunks.  Chunk p of a string is its bytes
+// [8p, 8p+8) big-endian, zero-padded (so a prefix sorts first); sorting the
+// chunks from last to first with stable passes gives byte-wise (C collation)
+// order.
+__global__ void sort_key_str_kernel(const int64_t *offsets, const char *chars, const uint64_t *valid, int64_t n,
+                                    const int64_t *perm, int64_t chunk, bool desc, uint64_t *keys) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    int64_t r = perm ? perm[i] : i;
+    uint64_t k = 0;
+    if (bit_valid(valid, r)) {
+      int64_t b = offsets[r], e = offsets[r + 1];
+      for (int j = 0; j < 8; j++) {
+        int64_t at = b + chunk * 8 + j;
+        k = (k << 8) | (at < e ? (uint8_t)chars[at] : 0u);
+      }
+      if (desc) k = ~k;
+    }
+    keys[i] = k;
+  }
+}
+
+void SortKeyStr(const int64_t *offsets, const char *chars, const uint64_t *valid, int64_t n, const int64_t *perm,
+                int64_t chunk, bool desc, uint64_t *keys, hipStream_t s) {
+  if (n <= 0) return;
+  hipLaunchKernelGGL(sort_key_str_kernel, dim3(GridFor(n, 256 * 4, NumCUs() * 8)), dim3(256), 0, s, offsets, chars,
+                     valid, n, perm, chunk, desc, keys);
+  CHECK_LAUNCH();
+}
+
+__global__ void str_max_len_kernel(const int64_t *offsets, int64_t n, unsigned long long *out) {
+  unsigned long long m = 0;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    unsigned long long l = (unsigned long long)(offsets[i + 1] - offsets[i]);
+    m = l > m ? l : m;
+  }
+  for (int o = 32; o > 0; o >>= 1) {
+    unsigned long long x = __shfl_xor(m, o);
+    m = x > m ? x : m;
+  }
+  if ((threadIdx.x & 63) == 0) atomicMax(out, m);
+}
+
+void StrMaxLen(const int64_t *offsets, int64_t n, unsigned long long *out, hipStream_t s) {
+  (void)hipMemsetAsync(out, 0, 8, s);
+  if (n <= 0) return;
+  hipLaunchKernelGGL(str_max_len_kernel, dim3(GridFor(n, 256 * 4, NumCUs() * 4)), dim3(256), 0, s, offsets, n, out);
+  CHECK_LAUNCH();
 }
 
 __global__ void iota_kernel(int64_t *p, int64_t n, int64_t start) {
@@ -2082,6 +2149,165 @@ __global__ __launch_bounds__(256) void emit_agg_kernel(EmitDesc D) {
 void EmitAggRelation(const EmitDesc &d, hipStream_t s) {
   hipLaunchKernelGGL(emit_agg_kernel, dim3(d.npartials > 0 ? 1 : GridFor(d.nslots, 256, 1024)), dim3(256), 0, s, d);
   CHECK_LAUNCH();
+}
+
+// ---------------------------------------------------------------------------
+// hash GROUP BY
+// ---------------------------------------------------------------------------
+#define HT_EMPTY 0xFFFFFFFFFFFFFFFFull
+#define HT_ROW_MASK ((1ull << 40) - 1)
+
+__device__ __forceinline__ uint64_t hmix(uint64_t z) {
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  return z ^ (z >> 31);
+}
+
+// key value as (up to) 128 bits; floats normalised so -0.0 groups with 0.0
+// and every NaN with every other NaN
+__device__ __forceinline__ void key_bits(const HashKeyCol &c, int64_t r, uint64_t &w0, uint64_t &w1) {
+  int64_t lo, hi;
+  load_phys(c.data, c.phys, r, lo, hi);
+  if (c.phys == P_F64 || c.phys == P_F32) {
+    double d = __longlong_as_double(lo);
+    if (d == 0.0) d = 0.0;
+    if (d != d) d = __longlong_as_double(0x7FF8000000000000ll);
+    lo = __double_as_longlong(d);
+  }
+  w0 = (uint64_t)lo;
+  w1 = (uint64_t)hi;
+}
+
+__device__ uint64_t row_hash(const HashKeys &K, int64_t r) {
+  uint64_t h = 0x9E3779B97F4A7C15ull;
+  for (int j = 0; j < K.nk; j++) {
+    const HashKeyCol &c = K.k[j];
+    if (!bit_valid(c.validity, r)) {
+      h = hmix(h ^ 0x5BD1E9955BD1E995ull);
+      continue;
+    }
+    if (c.phys == P_STR) {
+      int64_t b = c.offsets[r], e = c.offsets[r + 1];
+      uint64_t f = 0xCBF29CE484222325ull ^ (uint64_t)(e - b);
+      for (int64_t i = b; i < e; i++) f = (f ^ (uint8_t)c.chars[i]) * 0x100000001B3ull;
+      h = hmix(h ^ f);
+    } else {
+      uint64_t w0, w1;
+      key_bits(c, r, w0, w1);
+      h = hmix(h ^ w0);
+      h = hmix(h ^ (w1 + 0x632BE59BD9B4E019ull));
+    }
+  }
+  return h;
+}
+
+__device__ bool rows_equal(const HashKeys &K, int64_t a, int64_t b) {
+  for (int j = 0; j < K.nk; j++) {
+    const HashKeyCol &c = K.k[j];
+    bool va = bit_valid(c.validity, a), vb = bit_valid(c.validity, b);
+    if (va != vb) return false;
+    if (!va) continue;
+    if (c.phys == P_STR) {
+      int64_t ab = c.offsets[a], ae = c.offsets[a + 1], bb = c.offsets[b], be = c.offsets[b + 1];
+      if (ae - ab != be - bb) return false;
+      for (int64_t i = 0; i < ae - ab; i++)
+        if (c.chars[ab + i] != c.chars[bb + i]) return false;
+    } else {
+      uint64_t a0, a1, b0, b1;
+      key_bits(c, a, a0, a1);
+      key_bits(c, b, b0, b1);
+      if (a0 != b0 || a1 != b1) return false;
+    }
+  }
+  return true;
+}
+
+__global__ __launch_bounds__(256) void hash_insert_kernel(HashKeys K, int64_t n, unsigned long long *table,
+                                                          uint64_t mask, int32_t *entry_of, int32_t *err) {
+  for (int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; r < n; r += (int64_t)gridDim.x * blockDim.x) {
+    const uint64_t h = row_hash(K, r);
+    const uint64_t tag = h >> 40;
+    const unsigned long long mine = (tag << 40) | (uint64_t)r;
+    uint64_t e = h & mask;
+    int32_t got = -1;
+    for (uint64_t probe = 0; probe <= mask; probe++) {
+      unsigned long long cur = __hip_atomic_load(&table[e], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (cur == HT_EMPTY) {
+        unsigned long long prev = atomicCAS(&table[e], HT_EMPTY, mine);
+        if (prev == HT_EMPTY) {
+          got = (int32_t)e;
+          break;
+        }
+        cur = prev;
+      }
+      if ((cur >> 40) == tag && rows_equal(K, (int64_t)(cur & HT_ROW_MASK), r)) {
+        got = (int32_t)e;
+        break;
+      }
+      e = (e + 1) & mask;
+    }
+    if (got < 0) atomicCAS(err, 0, E_HASH_FULL);  // cannot happen with cap >= 2n; never loops forever
+    entry_of[r] = got < 0 ? 0 : got;
+  }
+}
+
+__global__ void hash_occupancy_kernel(const unsigned long long *table, int64_t cap, int32_t *flag) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < cap; i += (int64_t)gridDim.x * blockDim.x)
+    flag[i] = table[i] != HT_EMPTY;
+}
+
+// pos = exclusive scan of the occupancy flags: entry e (occupied) -> group pos[e]
+__global__ void hash_groups_kernel(const unsigned long long *table, const int32_t *flag, const int32_t *pos,
+                                   int64_t cap, int32_t *gid_of_entry, int64_t *rep_row, int64_t *ngroups) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < cap; i += (int64_t)gridDim.x * blockDim.x) {
+    if (flag[i]) {
+      gid_of_entry[i] = pos[i];
+      rep_row[pos[i]] = (int64_t)(table[i] & HT_ROW_MASK);
+    }
+    if (i == cap - 1) *ngroups = (int64_t)pos[i] + flag[i];
+  }
+}
+
+__global__ void hash_slots_kernel(int32_t *slot_of_row, const int32_t *gid_of_entry, int64_t n,
+                                  unsigned long long *count_star) {
+  for (int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; r < n; r += (int64_t)gridDim.x * blockDim.x) {
+    int32_t g = gid_of_entry[slot_of_row[r]];
+    slot_of_row[r] = g;
+    atomicAdd(&count_star[g], 1ull);
+  }
+}
+
+void HashGroupAssign(const HashKeys &k, int64_t n, unsigned long long *table, int64_t cap, int32_t *slot_of_row,
+                     int32_t *gid_of_entry, int64_t *rep_row, unsigned long long *count_star, int64_t *ngroups,
+                     int32_t *err, hipStream_t s) {
+  // table must hold HT_EMPTY, count_star zeros (caller); gid_of_entry doubles as scan scratch
+  if (n <= 0) {
+    (void)hipMemsetAsync(ngroups, 0, 8, s);
+    return;
+  }
+  const int grid = GridFor(n, 256 * 4, NumCUs() * 8);
+  hipLaunchKernelGGL(hash_insert_kernel, dim3(grid), dim3(256), 0, s, k, n, table, (uint64_t)(cap - 1), slot_of_row,
+                     err);
+  CHECK_LAUNCH();
+  int32_t *flag = nullptr, *pos = nullptr;
+  (void)hipMallocAsync((void **)&flag, (size_t)cap * 4, s);
+  (void)hipMallocAsync((void **)&pos, (size_t)cap * 4, s);
+  const int cgrid = GridFor(cap, 256 * 4, NumCUs() * 8);
+  hipLaunchKernelGGL(hash_occupancy_kernel, dim3(cgrid), dim3(256), 0, s, table, cap, flag);
+  CHECK_LAUNCH();
+  size_t tmp = 0;
+  (void)hipcub::DeviceScan::ExclusiveSum(nullptr, tmp, flag, pos, (int)cap, s);
+  void *d_tmp = nullptr;
+  (void)hipMallocAsync(&d_tmp, tmp ? tmp : 16, s);
+  (void)hipcub::DeviceScan::ExclusiveSum(d_tmp, tmp, flag, pos, (int)cap, s);
+  hipLaunchKernelGGL(hash_groups_kernel, dim3(cgrid), dim3(256), 0, s, table, flag, pos, cap, gid_of_entry, rep_row,
+                     ngroups);
+  CHECK_LAUNCH();
+  hipLaunchKernelGGL(hash_slots_kernel, dim3(grid), dim3(256), 0, s, slot_of_row, gid_of_entry, n, count_star);
+  CHECK_LAUNCH();
+  (void)hipFreeAsync(d_tmp, s);
+  (void)hipFreeAsync(pos, s);
+  (void)hipFreeAsync(flag, s);
 }
 
 __global__ __launch_bounds__(256) void host_copy_kernel(HostCopyDesc D) {

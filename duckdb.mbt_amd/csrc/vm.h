@@ -90,6 +90,7 @@ enum VmErr : int32_t {
   E_OVF_NEG = 4,
   E_CAST_RANGE = 5,
   E_DEC_OVF = 6,
+  E_HASH_FULL = 7,
 };
 
 }  // namespace mbx

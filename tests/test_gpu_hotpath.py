@@ -297,3 +297,91 @@ def test_group_direct_variants_parity(conn, oracle, monkeypatch, variant):
                     else:
                         want = [int(c[m].astype(object).sum()) for c in cols] + [int(m.sum())]
                     assert [int(x) for x in r[1:]] == want, (variant, n, sql, kk)
+
+
+# ---- hash GROUP BY: several keys, VARCHAR / wide-range / NULL keys ---------------
+def _expect_groups(keys, vals):
+    acc = {}
+    for kt, v in zip(keys, vals):
+        c, s, mn, mx = acc.get(kt, (0, 0, None, None))
+        acc[kt] = (c + 1, s + v, v if mn is None else min(mn, v), v if mx is None else max(mx, v))
+    return acc
+
+
+def _sort_key(kt):
+    return tuple((k is None, k if k is not None else 0) for k in kt)
+
+
+@pytest.mark.parametrize("n", [1, 1000, 200_003])
+def test_hash_groupby_multi_key(conn, oracle, n):
+    a = oracle.synth_i64(n, 3, 0, 97, 0)
+    b = oracle.synth_i64(n, 5, 0, 13, -6)
+    v = oracle.synth_i64(n, 9, 0, 2**40, -2**39)
+    q(conn, "DROP TABLE IF EXISTS hg")
+    q(conn, f"CREATE TABLE hg AS SELECT mbx_synth(3, i, 97) AS a, CAST(mbx_synth(5, i, 13) - 6 AS INTEGER) AS b, "
+            f"mbx_synth(9, i, 1099511627776) - 549755813888 AS v FROM range({n}) tbl(i)")
+    exp = _expect_groups(list(zip(a.tolist(), b.tolist())), v.tolist())
+    res = q(conn, "SELECT a, b, COUNT(*), SUM(v), MIN(v), MAX(v) FROM hg GROUP BY a, b ORDER BY a, b")
+    assert res.column_types == ["BigInt", "Integer", "BigInt", "HugeInt", "BigInt", "BigInt"]
+    want = [[str(k[0]), str(k[1])] + [str(x) for x in exp[k]] for k in sorted(exp)]
+    assert res.rows == want
+
+
+def test_hash_groupby_wide_range_and_null_keys(conn, oracle):
+    n = 100_000
+    # wide-range BIGINT keys (range >> rows): hash path; every 7th key NULL
+    q(conn, f"CREATE TABLE wk AS SELECT CASE WHEN i % 7 = 0 THEN NULL ELSE (i % 1000) * 1000000007 END AS k, "
+            f"i AS v FROM range({n}) tbl(i)")
+    keys = [None if i % 7 == 0 else (i % 1000) * 1000000007 for i in range(n)]
+    exp = _expect_groups([(k,) for k in keys], list(range(n)))
+    res = q(conn, "SELECT k, COUNT(*), SUM(v) FROM wk GROUP BY k ORDER BY k")
+    want = [[("" if k[0] is None else str(k[0])), str(exp[k][0]), str(exp[k][1])] for k in sorted(exp, key=_sort_key)]
+    assert [[r[0], r[1], r[2]] for r in res.rows] == want
+    assert res.nulls[-1][0] is True  # NULL group last
+
+
+def test_hash_groupby_varchar_keys(conn):
+    n = 50_000
+    q(conn, f"CREATE TABLE sk AS SELECT CASE WHEN i % 3 = 0 THEN 'alpha' WHEN i % 3 = 1 THEN 'beta' ELSE NULL END AS s, "
+            f"i % 5 AS t, i AS v FROM range({n}) tbl(i)")
+    exp = {}
+    for i in range(n):
+        s = "alpha" if i % 3 == 0 else "beta" if i % 3 == 1 else None
+        kt = (s, i % 5)
+        c, sm = exp.get(kt, (0, 0))
+        exp[kt] = (c + 1, sm + i)
+    res = q(conn, "SELECT s, t, COUNT(*), SUM(v) FROM sk GROUP BY s, t ORDER BY s, t")
+    want = [[("" if k[0] is None else k[0]), str(k[1]), str(c), str(sm)]
+            for k, (c, sm) in sorted(exp.items(), key=lambda kv: _sort_key(kv[0]))]
+    assert res.rows == want
+    # HAVING over the hash path
+    res = q(conn, "SELECT s, COUNT(*) AS c FROM sk GROUP BY s HAVING COUNT(*) > 16666 ORDER BY s")
+    assert res.rows == [["alpha", "16667"], ["beta", "16667"]]
+
+
+def test_hash_groupby_double_keys(conn):
+    q(conn, "CREATE TABLE dk AS SELECT CAST(i % 4 AS DOUBLE) / 2 AS d, i AS v FROM range(1000) tbl(i)")
+    res = q(conn, "SELECT d, COUNT(*), SUM(v) FROM dk GROUP BY d ORDER BY d")
+    assert res.rows == [["0.0", "250", str(sum(range(0, 1000, 4)))], ["0.5", "250", str(sum(range(1, 1000, 4)))],
+                        ["1.0", "250", str(sum(range(2, 1000, 4)))], ["1.5", "250", str(sum(range(3, 1000, 4)))]]
+
+
+def test_order_by_extremes_and_varchar(conn):
+    # adjacent extremes must stay distinct (the NULL pass is separate from the value key)
+    q(conn, "CREATE TABLE ox (x BIGINT, s VARCHAR)")
+    vals = [(-9223372036854775807, "prefix_longer_than_8_b"), (None, None), (-9223372036854775808, "prefix_longer_than_8_a"),
+            (9223372036854775807, "b"), (9223372036854775806, ""), (0, "prefix_longer"), (None, "a")]
+    for x, s in vals:
+        q(conn, "INSERT INTO ox VALUES ({}, {})".format("NULL" if x is None else x, "NULL" if s is None else f"'{s}'"))
+    res = q(conn, "SELECT x FROM ox ORDER BY x")
+    assert [r[0] for r in res.rows] == ["-9223372036854775808", "-9223372036854775807", "0", "9223372036854775806",
+                                        "9223372036854775807", "", ""]
+    res = q(conn, "SELECT x FROM ox ORDER BY x DESC NULLS FIRST")
+    assert [r[0] for r in res.rows][2:] == ["9223372036854775807", "9223372036854775806", "0", "-9223372036854775807",
+                                            "-9223372036854775808"]
+    res = q(conn, "SELECT s FROM ox ORDER BY s")
+    got = [(None if n[0] else r[0]) for r, n in zip(res.rows, res.nulls)]
+    assert got == ["", "a", "b", "prefix_longer", "prefix_longer_than_8_a", "prefix_longer_than_8_b", None]
+    res = q(conn, "SELECT s, x FROM ox ORDER BY s DESC, x")
+    got = [(None if n[0] else r[0]) for r, n in zip(res.rows, res.nulls)]
+    assert got == ["prefix_longer_than_8_b", "prefix_longer_than_8_a", "prefix_longer", "b", "a", "", None]
