@@ -184,6 +184,12 @@ struct HashKeys {
 // tag | 40-bit representative row).  Produces slot_of_row in [0, ngroups)
 // (dense group ids in table order), rep_row[g], count_star[g] and
 // *ngroups (device).  Scratch: table (cap x 8 B), entry ids (cap x 4 B).
+// Scratch allocator the helpers below use (set per call by the executor to
+// the connection's caching pool; the helpers run on that connection's stream).
+typedef void *(*TempAllocFn)(size_t bytes, void *ctx);
+typedef void (*TempFreeFn)(void *p, size_t bytes, void *ctx);
+void SetTempAllocator(TempAllocFn a, TempFreeFn f, void *ctx);
+void CountSlots(const int32_t *slot_of_row, int64_t n, unsigned long long *count_star, hipStream_t s);
 void HashGroupAssign(const HashKeys &k, int64_t n, unsigned long long *table, int64_t cap, int32_t *slot_of_row,
                      int32_t *gid_of_entry, int64_t *rep_row, unsigned long long *count_star, int64_t *ngroups,
                      int32_t *err, hipStream_t s);

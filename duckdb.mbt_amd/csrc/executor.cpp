@@ -14,6 +14,7 @@
 #include <cmath>
 #include <cstring>
 #include <functional>
+#include <map>
 #include <sstream>
 #include <thread>
 
@@ -39,39 +40,66 @@ struct ProfEvent {
   int64_t rows;
 };
 
-struct SmallPool {
-  static constexpr int kClasses = 13;  // 256 B .. 1 MiB
-  static constexpr size_t kMaxPerClass = 64;
-  std::vector<void *> free_[kClasses];
+// Caching device allocator for every intermediate buffer of a connection
+// (hipMalloc underneath; the stream-ordered hipMallocAsync pool is not used).
+// Blocks are bucketed — powers of two up to 1 MiB, then steps of 1/8 of the
+// size's power of two (>= 2 MiB) — and recycled on the connection's single
+// stream, so reuse is stream-ordered by construction.  Cached bytes above
+// kLimit are released after a stream synchronisation.
+struct DevicePool {
+  static constexpr size_t kLimit = (size_t)64 << 30;
+  std::map<size_t, std::vector<void *>> free_;
+  size_t cached = 0;
   hipStream_t s = nullptr;
-  static int Class(size_t bytes) {
-    if (bytes > ((size_t)256 << (kClasses - 1))) return -1;
-    int c = 0;
-    while (((size_t)256 << c) < bytes) c++;
-    return c;
+  static size_t Bucket(size_t bytes) {
+    if (bytes <= 256) return 256;
+    size_t p2 = 256;
+    while (p2 < bytes) p2 <<= 1;
+    if (p2 <= ((size_t)1 << 20)) return p2;
+    size_t step = std::max<size_t>(p2 / 16, (size_t)2 << 20);  // p2/2 < bytes <= p2: steps of p2/16 = (1/8 of floor pow2)
+    return (bytes + step - 1) / step * step;
   }
-  static size_t ClassBytes(int c) { return (size_t)256 << c; }
-  void *Get(int c) {
-    if (free_[c].empty()) return nullptr;
-    void *p = free_[c].back();
-    free_[c].pop_back();
+  void ReleaseAll() {
+    if (s) (void)hipStreamSynchronize(s);
+    for (auto &kv : free_)
+      for (void *p : kv.second) (void)hipFree(p);
+    free_.clear();
+    cached = 0;
+  }
+  void *Get(size_t b) {
+    auto it = free_.find(b);
+    if (it != free_.end() && !it->second.empty()) {
+      void *p = it->second.back();
+      it->second.pop_back();
+      cached -= b;
+      return p;
+    }
+    void *p = nullptr;
+    if (hipMalloc(&p, b) != hipSuccess) {
+      (void)hipGetLastError();
+      ReleaseAll();  // give cached blocks back and retry once
+      if (hipMalloc(&p, b) != hipSuccess) {
+        (void)hipGetLastError();
+        return nullptr;
+      }
+    }
     return p;
   }
-  bool Put(int c, void *p) {
-    if (free_[c].size() >= kMaxPerClass) return false;
-    free_[c].push_back(p);
-    return true;
+  void Put(size_t b, void *p) {
+    if (cached + b > kLimit) {
+      if (s) (void)hipStreamSynchronize(s);
+      (void)hipFree(p);
+      return;
+    }
+    free_[b].push_back(p);
+    cached += b;
   }
-  ~SmallPool() {
-    for (auto &v : free_)
-      for (void *p : v) (void)hipFreeAsync(p, s);
-    if (s) (void)hipStreamSynchronize(s);
-  }
+  ~DevicePool() { ReleaseAll(); }
 };
 
 struct Engine {
   int device = 0;
-  std::shared_ptr<SmallPool> pool;
+  std::shared_ptr<DevicePool> pool;
   bool has_gpu = false;
   hipStream_t stream = nullptr;
   int32_t *d_err = nullptr;
@@ -151,6 +179,16 @@ int DeviceCount() {
   return n;
 }
 
+// scratch for the device helpers (hipcub temp storage, hash flags) from the
+// calling connection's pool
+static void *TempAllocCb(size_t bytes, void *ctx) {
+  DevicePool *p = (DevicePool *)ctx;
+  return p->Get(DevicePool::Bucket(bytes ? bytes : 16));
+}
+static void TempFreeCb(void *ptr, size_t bytes, void *ctx) {
+  if (ptr) ((DevicePool *)ctx)->Put(DevicePool::Bucket(bytes ? bytes : 16), ptr);
+}
+
 std::shared_ptr<Engine> CreateEngine(int device, bool allow_no_gpu) {
   auto e = std::make_shared<Engine>();
   int n = DeviceCount();
@@ -165,8 +203,9 @@ std::shared_ptr<Engine> CreateEngine(int device, bool allow_no_gpu) {
   e->device = device;
   HIPCHK(hipSetDevice(device));
   HIPCHK(hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking));
-  e->pool = std::make_shared<SmallPool>();
+  e->pool = std::make_shared<DevicePool>();
   e->pool->s = e->stream;
+  dev::SetTempAllocator(&TempAllocCb, &TempFreeCb, e->pool.get());
   HIPCHK(hipMalloc(&e->d_err, 256));
   HIPCHK(hipMalloc(&e->d_scratch, 4096));
   HIPCHK(hipMalloc(&e->d_small, 1 << 16));
@@ -184,6 +223,7 @@ static Engine &Eng(Connection &c) {
   if (!e.has_gpu)
     ThrowError("IO", "this statement reads table rows and needs the MI355X device, but no GPU is available");
   hipSetDevice(e.device);
+  dev::SetTempAllocator(&TempAllocCb, &TempFreeCb, e.pool.get());
   return e;
 }
 
@@ -212,37 +252,26 @@ struct ProfScope {
 // ---------------------------------------------------------------------------
 // device buffers and relations
 // ---------------------------------------------------------------------------
-// Small intermediate buffers (<= 1 MiB: aggregate states, result columns of
-// aggregates, scan counters) are recycled per power-of-two class instead of
-// going through hipMallocAsync/hipFreeAsync each query.  Reuse is stream-
-// ordered: every user of a connection's buffers runs on its one stream.
+// Every intermediate device buffer comes from the connection's DevicePool
+// and returns to it when its last owner lets go.
 struct DevBuf {
   void *p = nullptr;
-  hipStream_t s = nullptr;
-  std::shared_ptr<SmallPool> pool;
-  int cls = -1;
+  size_t bytes = 0;
+  std::shared_ptr<DevicePool> pool;
   ~DevBuf() {
-    if (!p) return;
-    if (pool && pool->Put(cls, p)) return;
-    (void)hipFreeAsync(p, s);
+    if (p && pool) pool->Put(bytes, p);
   }
 };
 typedef std::shared_ptr<DevBuf> DevBufPtr;
 
 static DevBufPtr Alloc(Engine &e, size_t bytes, bool zero = false) {
   auto b = std::make_shared<DevBuf>();
-  b->s = e.stream;
   if (bytes == 0) bytes = 16;
-  bytes = (bytes + 255) & ~(size_t)255;
-  int cls = SmallPool::Class(bytes);
-  if (cls >= 0) {
-    b->pool = e.pool;
-    b->cls = cls;
-    bytes = SmallPool::ClassBytes(cls);
-    b->p = e.pool->Get(cls);
-  }
-  if (!b->p) HIPCHK(hipMallocAsync(&b->p, bytes, e.stream));
-  if (zero) HIPCHK(hipMemsetAsync(b->p, 0, bytes, e.stream));
+  b->bytes = DevicePool::Bucket(bytes);
+  b->pool = e.pool;
+  b->p = e.pool->Get(b->bytes);
+  if (!b->p) ThrowError("Out of Memory", "device allocation of " + std::to_string(b->bytes) + " bytes failed");
+  if (zero) HIPCHK(hipMemsetAsync(b->p, 0, b->bytes, e.stream));
   return b;
 }
 
@@ -934,6 +963,117 @@ static void DropEmptyValidity(Engine &e, DRel &r) {
 
 static DRel GatherRel(Engine &e, const DRel &r, const int64_t *perm, int64_t n);
 
+// LDS direct-index reduction (group_direct kernels): rows with an integer key
+// in [kmin, kmin + nk) (no NULL keys) and <= 2 integer value columns of one
+// physical type without NULLs.  Fills cs (COUNT(*) per key) and s0/s1 (one
+// AggState per key for each value column).  maxabs bounds |value| (zone map
+// or a device min/max pass); false = the shape does not fit.
+struct DirectStates {
+  DevBufPtr cs, s0, s1;
+};
+static bool DirectReduce(Engine &e, const void *kdata, Phys kphys, int64_t kmin, int64_t nk, int64_t n,
+                         const std::vector<const DCol *> &vals, i128 maxabs, bool mm, DirectStates &out) {
+  const int nv = (int)vals.size();
+  if (nk < 1 || nk > 1024 || nv > 2 || n <= 0) return false;
+  if (kphys != P_I32 && kphys != P_I64) return false;
+  for (auto *v : vals)
+    if ((v->phys != P_I32 && v->phys != P_I64) || v->validity || v->phys != vals[0]->phys) return false;
+  int R = 64;
+  while (R > 1 && dev::GroupDirectLds((int)nk, R, nv, mm) > 48 * 1024) R >>= 1;
+  if (dev::GroupDirectLds((int)nk, R, nv, mm) > 64 * 1024) return false;
+  int64_t seg = 0;  // whole chunk
+  if (maxabs > 0) {
+    i128 per_rep = ((i128)1 << 62) / maxabs;  // rows one replica may absorb
+    i128 seg128 = per_rep * R;
+    if (seg128 < 4096) return false;
+    if (seg128 < (i128)INT64_MAX / 2) seg = (int64_t)seg128;
+  }
+  if ((int64_t)R * ((int64_t)1 << 31) < seg || seg == 0) {
+    // u32 replica counts: cap segment length
+    int64_t cap = (int64_t)R * ((int64_t)1 << 30);
+    if (seg == 0 || seg > cap) seg = cap;
+  }
+  size_t st_bytes = (size_t)nk * sizeof(dev::AggState);
+  out.cs = Alloc(e, nk * 8, true);
+  out.s0 = Alloc(e, st_bytes);
+  out.s1 = Alloc(e, st_bytes);
+  dev::InitAggStates((dev::AggState *)out.s0->p, nk, e.stream);
+  dev::InitAggStates((dev::AggState *)out.s1->p, nk, e.stream);
+  const Phys vphys = nv ? vals[0]->phys : P_I64;
+  double bytes = (double)n * PhysSize(kphys);
+  for (auto *v : vals) bytes += (double)n * PhysSize(v->phys);
+  ProfScope ps(e, "group_direct", bytes, n);
+  dev::GroupByDirectStates(kdata, kphys, kmin, (int)nk, nv > 0 ? vals[0]->data : nullptr,
+                           nv > 1 ? vals[1]->data : nullptr, vphys, nv, mm, n, seg, R,
+                           (unsigned long long *)out.cs->p, (dev::AggState *)out.s0->p, (dev::AggState *)out.s1->p, 0,
+                           e.stream);
+  return true;
+}
+
+// max |x| over an integer column without NULLs (one device min/max pass)
+static i128 DeviceMaxAbs(Engine &e, const DCol &c, int64_t n) {
+  long long *o3 = (long long *)((char *)e.d_small + 3072);
+  dev::KeyRange(c.data, c.phys, c.validity, n, o3, e.stream);
+  long long h[3];
+  HIPCHK(hipMemcpyAsync(h, o3, sizeof(h), hipMemcpyDeviceToHost, e.stream));
+  HIPCHK(hipStreamSynchronize(e.stream));
+  if (!h[2]) return 0;
+  i128 a = h[0] < 0 ? -(i128)h[0] : (i128)h[0], b = h[1] < 0 ? -(i128)h[1] : (i128)h[1];
+  return a > b ? a : b;
+}
+
+// Value columns of the generic aggregate paths reduced through DirectReduce
+// in pairs; states_of[j] = AggState array of aggregate j (nullptr for
+// COUNT(*)), count_star = the per-key COUNT(*).  false: not applicable.
+static bool DirectReduceAll(Engine &e, const void *kdata, Phys kphys, int64_t kmin, int64_t nk, int64_t n,
+                            const DRel &tmp, const BoundSelect &s, const std::vector<int> &arg_idx,
+                            std::vector<DevBufPtr> &keep, std::vector<dev::AggState *> &states_of,
+                            const unsigned long long **count_star) {
+  const int na = (int)s.aggs.size();
+  std::vector<int> cols;
+  bool mm = false;
+  for (int j = 0; j < na; j++) {
+    if (arg_idx[j] < 0) continue;
+    if (s.aggs[j].distinct) return false;
+    const DCol &c = tmp.cols[arg_idx[j]];
+    if ((c.phys != P_I32 && c.phys != P_I64) || c.validity || ClassOf(c.type) != VC_I64) return false;
+    if (s.aggs[j].kind == A_MIN || s.aggs[j].kind == A_MAX) mm = true;
+    if (std::find(cols.begin(), cols.end(), arg_idx[j]) == cols.end()) cols.push_back(arg_idx[j]);
+  }
+  // pairs of one physical type
+  std::vector<std::vector<int>> groups;
+  for (Phys ph : {P_I32, P_I64}) {
+    std::vector<int> g;
+    for (int c : cols)
+      if (tmp.cols[c].phys == ph) g.push_back(c);
+    for (size_t i = 0; i < g.size(); i += 2)
+      groups.push_back(std::vector<int>(g.begin() + i, g.begin() + std::min(g.size(), i + 2)));
+  }
+  if (groups.empty()) groups.push_back({});
+  states_of.assign(na, nullptr);
+  *count_star = nullptr;
+  for (auto &g : groups) {
+    std::vector<const DCol *> vals;
+    i128 maxabs = 0;
+    for (int c : g) {
+      vals.push_back(&tmp.cols[c]);
+      maxabs = std::max(maxabs, DeviceMaxAbs(e, tmp.cols[c], n));
+    }
+    DirectStates ds;
+    if (!DirectReduce(e, kdata, kphys, kmin, nk, n, vals, maxabs, mm, ds)) return false;
+    keep.push_back(ds.cs);
+    keep.push_back(ds.s0);
+    keep.push_back(ds.s1);
+    if (!*count_star) *count_star = (const unsigned long long *)ds.cs->p;
+    for (int j = 0; j < na; j++) {
+      if (arg_idx[j] < 0) continue;
+      if (!g.empty() && arg_idx[j] == g[0]) states_of[j] = (dev::AggState *)ds.s0->p;
+      if (g.size() > 1 && arg_idx[j] == g[1]) states_of[j] = (dev::AggState *)ds.s1->p;
+    }
+  }
+  return true;
+}
+
 // GROUP BY through the device hash table (HashGroupAssign): works for any
 // number of keys of any fixed-width or VARCHAR type.  Keys are emitted by
 // gathering each group's representative row; groups come out in table
@@ -961,18 +1101,31 @@ static DRel HashAggregate(Engine &e, const DRel &tmp, const BoundSelect &s, cons
   auto slot_of = Alloc(e, (size_t)std::max<int64_t>(n, 1) * 4);
   auto gid = Alloc(e, (size_t)cap * 4);
   auto rep = Alloc(e, (size_t)std::max<int64_t>(n, 1) * 8);
-  auto cs = Alloc(e, (size_t)std::max<int64_t>(n, 1) * 8, true);
   {
     double kb = 0;
     for (int g = 0; g < ng; g++) kb += (double)n * (tmp.cols[g].phys == P_STR ? 16 : PhysSize(tmp.cols[g].phys));
     ProfScope ps(e, "hash_group_assign", kb, n);
     dev::HashGroupAssign(hk, n, (unsigned long long *)table->p, cap, (int32_t *)slot_of->p, (int32_t *)gid->p,
-                         (int64_t *)rep->p, (unsigned long long *)cs->p, e.d_scratch, e.d_err, e.stream);
+                         (int64_t *)rep->p, nullptr, e.d_scratch, e.d_err, e.stream);
   }
   const int64_t ngroups = ReadDev<int64_t>(e, e.d_scratch);
   CheckError(e);
+  table.reset();
+  gid.reset();
   std::vector<DevBufPtr> states(na);
-  for (int j = 0; j < na; j++) {
+  std::vector<DevBufPtr> keep;
+  std::vector<dev::AggState *> st_of(na, nullptr);
+  const unsigned long long *cstar = nullptr;
+  DevBufPtr cs;
+  // few groups: LDS-privatised reduction keyed by the dense group id
+  bool lds = ngroups >= 1 && ngroups <= 1024 &&
+             DirectReduceAll(e, slot_of->p, P_I32, 0, ngroups, n, tmp, s, arg_idx, keep, st_of, &cstar);
+  if (!lds) {
+    cs = Alloc(e, (size_t)std::max<int64_t>(ngroups, 1) * 8, true);
+    dev::CountSlots((const int32_t *)slot_of->p, n, (unsigned long long *)cs->p, e.stream);
+    cstar = (const unsigned long long *)cs->p;
+  }
+  for (int j = 0; j < na && !lds; j++) {
     if (arg_idx[j] < 0) continue;
     const DCol &c = tmp.cols[arg_idx[j]];
     const void *data = c.data;
@@ -988,6 +1141,7 @@ static DRel HashAggregate(Engine &e, const DRel &tmp, const BoundSelect &s, cons
     ProfScope ps(e, "group_reduce", (double)n * (PhysSize((Phys)phys) + 4), n);
     dev::GroupReduceColumn((const int32_t *)slot_of->p, data, phys, c.validity, n, (dev::AggState *)states[j]->p,
                            e.stream);
+    st_of[j] = (dev::AggState *)states[j]->p;
   }
   DRel keys;
   keys.n = n;
@@ -997,13 +1151,13 @@ static DRel HashAggregate(Engine &e, const DRel &tmp, const BoundSelect &s, cons
   dev::EmitDesc D;
   memset(&D, 0, sizeof(D));
   D.nagg = na;
-  D.cstar = (const unsigned long long *)cs->p;
+  D.cstar = cstar;
   D.nslots = ngroups;
   D.null_slot = -1;
   for (int j = 0; j < na; j++) {
     DCol oc = AllocOut(e, s.aggs[j].type, ngroups, true, false);
     VClass ic = arg_idx[j] >= 0 ? ClassOf(tmp.cols[arg_idx[j]].type) : VC_I64;
-    D.a[j] = EmitFor(s.aggs[j], ic, states[j] ? (dev::AggState *)states[j]->p : nullptr, oc);
+    D.a[j] = EmitFor(s.aggs[j], ic, st_of[j], oc);
     out.cols.push_back(oc);
   }
   if (ngroups > 0) dev::EmitAggRelation(D, e.stream);
@@ -1266,6 +1420,42 @@ static DRel Aggregate(Engine &e, const DRel &src, const BoundSelect &s) {
     if (range > (1 << 24) || range > 4 * (i128)std::max<int64_t>(tmp.n, 1024)) direct = false;
   }
   if (!direct) return HashAggregate(e, tmp, s, arg_idx);
+  if (!K.validity && range <= 1024 && range >= 1) {
+    // filtered / projected input, small key range: LDS-privatised reduction
+    std::vector<DevBufPtr> keep;
+    std::vector<dev::AggState *> st_of;
+    const unsigned long long *cstar = nullptr;
+    if (DirectReduceAll(e, K.data, K.phys, kmin, (int64_t)range, tmp.n, tmp, s, arg_idx, keep, st_of, &cstar)) {
+      const int64_t nk = (int64_t)range;
+      auto list = Alloc(e, nk * 4);
+      dev::CompactSlots(cstar, nk, (int32_t *)list->p, e.d_scratch, e.stream);
+      int64_t ngroups = ReadDev<int64_t>(e, e.d_scratch);
+      dev::EmitDesc D;
+      memset(&D, 0, sizeof(D));
+      D.nagg = na;
+      D.cstar = cstar;
+      D.slot_list = (const int32_t *)list->p;
+      D.n_list = e.d_scratch;
+      D.nslots = ngroups;
+      D.has_key = 1;
+      D.key_phys = PhysOf(s.groups[0]->type);
+      D.kmin = kmin;
+      D.null_slot = -1;
+      DCol kc = AllocOut(e, s.groups[0]->type, ngroups, true, false);
+      D.key_out = kc.data;
+      D.key_valid = (uint32_t *)kc.validity;
+      out.n = ngroups;
+      out.cols.push_back(kc);
+      for (int j = 0; j < na; j++) {
+        DCol oc = AllocOut(e, s.aggs[j].type, ngroups, true, false);
+        D.a[j] = EmitFor(s.aggs[j], VC_I64, st_of[j], oc);
+        out.cols.push_back(oc);
+      }
+      if (ngroups > 0) dev::EmitAggRelation(D, e.stream);
+      HIPCHK(hipStreamSynchronize(e.stream));
+      return out;
+    }
+  }
   int64_t nslots = (int64_t)range + 1;  // + NULL group
   auto slot_of = Alloc(e, std::max<int64_t>(tmp.n, 1) * 4);
   auto cs = Alloc(e, nslots * 8, true);

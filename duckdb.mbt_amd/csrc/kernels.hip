@@ -11,6 +11,7 @@
 //     (one replica per lane index -> no same-address conflicts inside a wave).
 #include <hip/hip_runtime.h>
 #include <hipcub/hipcub.hpp>
+#include <stdexcept>
 #include <stdint.h>
 
 #include "device.h"
@@ -19,6 +20,24 @@
 
 namespace mbx {
 namespace dev {
+
+static thread_local TempAllocFn g_talloc = nullptr;
+static thread_local TempFreeFn g_tfree = nullptr;
+static thread_local void *g_tctx = nullptr;
+void SetTempAllocator(TempAllocFn a, TempFreeFn f, void *ctx) {
+  g_talloc = a;
+  g_tfree = f;
+  g_tctx = ctx;
+}
+static void *TempAlloc(size_t bytes) {
+  if (!g_talloc) throw std::runtime_error("device scratch allocator not set");
+  void *p = g_talloc(bytes, g_tctx);
+  if (!p) throw std::runtime_error("device scratch allocation failed");
+  return p;
+}
+static void TempFree(void *p, size_t bytes) {
+  if (p && g_tfree) g_tfree(p, bytes, g_tctx);
+}
 
 typedef __int128 i128;
 typedef unsigned __int128 u128;
@@ -554,9 +573,9 @@ void ScanTileCounts(const uint32_t *counts, int64_t *offsets, int64_t n, int64_t
   size_t tmp = 0;
   (void)hipcub::DeviceScan::ExclusiveSum(nullptr, tmp, it, offsets, (int)n, s);
   void *d_tmp = nullptr;
-  (void)hipMallocAsync(&d_tmp, tmp, s);
+  d_tmp = TempAlloc(tmp);
   (void)hipcub::DeviceScan::ExclusiveSum(d_tmp, tmp, it, offsets, (int)n, s);
-  (void)hipFreeAsync(d_tmp, s);
+  TempFree(d_tmp, tmp);
   hipLaunchKernelGGL(scan_total_kernel, dim3(1), dim3(1), 0, s, counts, offsets, n, total);
 }
 
@@ -1791,9 +1810,9 @@ void SortPairs(uint64_t *keys_in, int64_t *vals_in, uint64_t *keys_out, int64_t 
   size_t tmp = 0;
   (void)hipcub::DeviceRadixSort::SortPairs(nullptr, tmp, keys_in, keys_out, vals_in, vals_out, (int)n, 0, end_bit, s);
   void *d_tmp = nullptr;
-  (void)hipMallocAsync(&d_tmp, tmp, s);
+  d_tmp = TempAlloc(tmp);
   (void)hipcub::DeviceRadixSort::SortPairs(d_tmp, tmp, keys_in, keys_out, vals_in, vals_out, (int)n, 0, end_bit, s);
-  (void)hipFreeAsync(d_tmp, s);
+  TempFree(d_tmp, tmp);
 }
 
 // 1-bit NULL-placement key: the last (most significant) pass of each ORDER BY key
@@ -1945,9 +1964,9 @@ void ScanLengths(const int64_t *lens, int64_t *offsets, int64_t n, hipStream_t s
   size_t tmp = 0;
   (void)hipcub::DeviceScan::InclusiveSum(nullptr, tmp, lens, offsets + 1, (int)n, s);
   void *d_tmp = nullptr;
-  (void)hipMallocAsync(&d_tmp, tmp, s);
+  d_tmp = TempAlloc(tmp);
   (void)hipcub::DeviceScan::InclusiveSum(d_tmp, tmp, lens, offsets + 1, (int)n, s);
-  (void)hipFreeAsync(d_tmp, s);
+  TempFree(d_tmp, tmp);
 }
 
 __global__ void str_copy_kernel(const int64_t *codes, const uint64_t *valid, int64_t n, const int64_t *src_off,
@@ -2273,8 +2292,20 @@ __global__ void hash_slots_kernel(int32_t *slot_of_row, const int32_t *gid_of_en
   for (int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; r < n; r += (int64_t)gridDim.x * blockDim.x) {
     int32_t g = gid_of_entry[slot_of_row[r]];
     slot_of_row[r] = g;
-    atomicAdd(&count_star[g], 1ull);
+    if (count_star) atomicAdd(&count_star[g], 1ull);
   }
+}
+
+__global__ void count_slots_kernel(const int32_t *slot_of_row, int64_t n, unsigned long long *count_star) {
+  for (int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; r < n; r += (int64_t)gridDim.x * blockDim.x)
+    atomicAdd(&count_star[slot_of_row[r]], 1ull);
+}
+
+void CountSlots(const int32_t *slot_of_row, int64_t n, unsigned long long *count_star, hipStream_t s) {
+  if (n <= 0) return;
+  hipLaunchKernelGGL(count_slots_kernel, dim3(GridFor(n, 256 * 4, NumCUs() * 8)), dim3(256), 0, s, slot_of_row, n,
+                     count_star);
+  CHECK_LAUNCH();
 }
 
 void HashGroupAssign(const HashKeys &k, int64_t n, unsigned long long *table, int64_t cap, int32_t *slot_of_row,
@@ -2290,24 +2321,24 @@ void HashGroupAssign(const HashKeys &k, int64_t n, unsigned long long *table, in
                      err);
   CHECK_LAUNCH();
   int32_t *flag = nullptr, *pos = nullptr;
-  (void)hipMallocAsync((void **)&flag, (size_t)cap * 4, s);
-  (void)hipMallocAsync((void **)&pos, (size_t)cap * 4, s);
+  flag = (int32_t *)TempAlloc((size_t)cap * 4);
+  pos = (int32_t *)TempAlloc((size_t)cap * 4);
   const int cgrid = GridFor(cap, 256 * 4, NumCUs() * 8);
   hipLaunchKernelGGL(hash_occupancy_kernel, dim3(cgrid), dim3(256), 0, s, table, cap, flag);
   CHECK_LAUNCH();
   size_t tmp = 0;
   (void)hipcub::DeviceScan::ExclusiveSum(nullptr, tmp, flag, pos, (int)cap, s);
   void *d_tmp = nullptr;
-  (void)hipMallocAsync(&d_tmp, tmp ? tmp : 16, s);
+  d_tmp = TempAlloc(tmp ? tmp : 16);
   (void)hipcub::DeviceScan::ExclusiveSum(d_tmp, tmp, flag, pos, (int)cap, s);
   hipLaunchKernelGGL(hash_groups_kernel, dim3(cgrid), dim3(256), 0, s, table, flag, pos, cap, gid_of_entry, rep_row,
                      ngroups);
   CHECK_LAUNCH();
   hipLaunchKernelGGL(hash_slots_kernel, dim3(grid), dim3(256), 0, s, slot_of_row, gid_of_entry, n, count_star);
   CHECK_LAUNCH();
-  (void)hipFreeAsync(d_tmp, s);
-  (void)hipFreeAsync(pos, s);
-  (void)hipFreeAsync(flag, s);
+  TempFree(d_tmp, tmp ? tmp : 16);
+  TempFree(pos, (size_t)cap * 4);
+  TempFree(flag, (size_t)cap * 4);
 }
 
 __global__ __launch_bounds__(256) void host_copy_kernel(HostCopyDesc D) {

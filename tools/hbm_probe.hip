@@ -82,6 +82,45 @@ __global__ __launch_bounds__(256) void lds_dma_read(const v2i64 *__restrict__ in
   if (acc == 0x5a5a5a5a5a5aLL) atomicAdd(out, 1ull);
 }
 
+// Like lds_dma_read, but each ring step of a wave covers PPS contiguous pieces.
+template <int DEPTH, int PPS>
+__global__ __launch_bounds__(256) void lds_dma_read_pps(const v2i64 *__restrict__ in, long long npieces,
+                                                        unsigned long long *out) {
+  __shared__ __attribute__((aligned(16))) v2i64 lds[4 * DEPTH * PPS * 64];
+  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const long long nsteps = npieces / PPS;
+  const long long nw = (long long)gridDim.x * 4;
+  long long p = (long long)blockIdx.x * 4 + w;
+  v2i64 *slot0 = lds + w * DEPTH * PPS * 64;
+  long long acc = 0;
+#pragma unroll
+  for (int d = 0; d < DEPTH; d++) {
+    long long q = p + d * nw;
+    q = q < nsteps ? q : 0;
+#pragma unroll
+    for (int j = 0; j < PPS; j++)
+      __builtin_amdgcn_global_load_lds((const void *)(in + (q * PPS + j) * 64 + lane), (void *)(slot0 + (d * PPS + j) * 64), 16, 0, 2);
+  }
+  int k = 0;
+  for (; p < nsteps; p += nw) {
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"((DEPTH - 1) * PPS) : "memory");
+    v2i64 v[PPS];
+#pragma unroll
+    for (int j = 0; j < PPS; j++) v[j] = slot0[(k * PPS + j) * 64 + lane];
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    long long q = p + DEPTH * nw;
+    q = q < nsteps ? q : p;
+#pragma unroll
+    for (int j = 0; j < PPS; j++)
+      __builtin_amdgcn_global_load_lds((const void *)(in + (q * PPS + j) * 64 + lane), (void *)(slot0 + (k * PPS + j) * 64), 16, 0, 2);
+#pragma unroll
+    for (int j = 0; j < PPS; j++) acc += v[j].x ^ v[j].y;
+    k = k + 1 == DEPTH ? 0 : k + 1;
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  if (acc == 0x5a5a5a5a5a5aLL) atomicAdd(out, 1ull);
+}
+
 #define CHK(x) do { hipError_t e_ = (x); if (e_) { printf("HIP error %s at %s\n", hipGetErrorString(e_), #x); exit(1); } } while (0)
 
 __global__ void fill_random(long long *p, long long n) {
@@ -144,6 +183,16 @@ int main(int argc, char **argv) {
     fflush(stdout);
   };
   const v2i64 *in = (const v2i64 *)buf;
+  if (mode & 8) {
+#define PPSRUN(D, P, G)                                                                                     \
+  run("ldsdma d" #D " pps" #P " g" #G, [&] {                                                                \
+    hipLaunchKernelGGL((lds_dma_read_pps<D, P>), dim3(cus * G), dim3(256), 0, 0, in, npieces, flag);       \
+  })
+    PPSRUN(8, 1, 1); PPSRUN(4, 2, 1); PPSRUN(8, 2, 1); PPSRUN(4, 4, 1); PPSRUN(2, 4, 1); PPSRUN(16, 1, 1);
+    PPSRUN(2, 8, 1); PPSRUN(6, 1, 1); PPSRUN(12, 1, 1); PPSRUN(3, 2, 2); PPSRUN(4, 1, 2);
+    PPSRUN(8, 1, 1);
+    return 0;
+  }
   if (mode & 4) {
     for (int g : {4, 8}) {
       char nm[64];

@@ -1,0 +1,48 @@
+#!/usr/bin/env python3
+"""Kernel-level timing of query shapes around the hot path (filter -> project
+-> aggregate variants) on a C3-style table.  GPU only.  Usage: shape_bench.py [rows]"""
+import json
+import os
+import statistics
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+import __graft_entry__ as ge  # noqa: E402
+
+m = ge._load()
+n = int(sys.argv[1]) if len(sys.argv) > 1 else 100_000_000
+cfg = m.Config.create()
+cfg.set("mbx_profile", "true")
+c = m.connect_with_config(cfg).value
+c.query(f"CREATE TABLE t AS SELECT CAST(mbx_synth(7, i, 32) AS INTEGER) AS k, CAST(mbx_synth(8, i, 4) AS INTEGER) AS k2, "
+        f"mbx_synth(9, i, 1099511627776) - 549755813888 AS v, mbx_synth(42, i, 50) + 1 AS x FROM range({n}) tbl(i)")
+shapes = {
+    "c2_count": "SELECT COUNT(*) FROM t WHERE x > 24",
+    "c3": "SELECT k, SUM(v), COUNT(*) FROM t GROUP BY k",
+    "c3_where": "SELECT k, SUM(v), COUNT(*) FROM t WHERE x > 24 GROUP BY k",
+    "c3_project": "SELECT k, SUM(v * 2), COUNT(*) FROM t GROUP BY k",
+    "multi_key": "SELECT k, k2, SUM(v), COUNT(*) FROM t GROUP BY k, k2",
+    "filter_sum_expr": "SELECT SUM(v + x) FROM t WHERE x > 24 AND k < 16",
+    "wide_key": "SELECT v % 1000003, COUNT(*) FROM t GROUP BY v % 1000003",
+}
+if os.environ.get("SHAPES"):
+    shapes = {k: v for k, v in shapes.items() if k in os.environ["SHAPES"].split(",")}
+out = {}
+for name, sql in shapes.items():
+    walls, kern = [], []
+    for i in range(5):
+        t0 = time.perf_counter()
+        try:
+            rr = c.query_raw(sql)  # engine time: no per-cell pull of the result
+        except Exception as ex:  # noqa: BLE001
+            out[name] = {"error": str(ex)}
+            break
+        walls.append(time.perf_counter() - t0)
+        rr.close()
+        prof = c.last_profile()
+        kern.append({k["name"]: k["ms"] for k in prof["kernels"]})
+    else:
+        out[name] = {"wall_ms_median": statistics.median(walls[1:]) * 1e3, "kernels_last": kern[-1]}
+    print(name, json.dumps(out[name]), flush=True)
