@@ -1255,7 +1255,12 @@ static DRel Aggregate(Engine &e, const DRel &src, const BoundSelect &s) {
   }
   // ---- fast path F2: GROUP BY one small-range int key column, aggregates
   //      over <= 2 int columns of one phys, no predicate.
-  if (ng == 1 && !s.where && !src.range && s.groups[0]->kind == BExpr::COL && FastIntCol(src, s.groups[0]->col)) {
+  //      (plus: an optional range predicate on one int column, fused)
+  int f2_pcol = -1;
+  i128 f2_lo = (i128)INT64_MIN, f2_hi = (i128)INT64_MAX;
+  bool f2_pred_ok = !s.where || (RangePredicate(*s.where, &f2_pcol, &f2_lo, &f2_hi) && f2_pcol >= 0 &&
+                                 FastIntCol(src, f2_pcol) && f2_lo <= f2_hi);
+  if (ng == 1 && f2_pred_ok && !src.range && s.groups[0]->kind == BExpr::COL && FastIntCol(src, s.groups[0]->col)) {
     const DCol &K = src.cols[s.groups[0]->col];
     const DevColumn *ks = K.table_col;
     std::vector<int> vcols;
@@ -1311,13 +1316,27 @@ static DRel Aggregate(Engine &e, const DRel &src, const BoundSelect &s) {
           Phys vphys = nv ? src.cols[vcols[0]].phys : P_I64;
           double bytes = (double)src.n * PhysSize(K.phys);
           for (int c : vcols) bytes += (double)src.n * PhysSize(src.cols[c].phys);
+          dev::GroupPred gp;
+          memset(&gp, 0, sizeof(gp));
+          if (s.where) {
+            const int kcol = s.groups[0]->col;
+            gp.src = f2_pcol == kcol ? 2 : (nv > 0 && f2_pcol == vcols[0]) ? 3 : 1;
+            gp.phys = src.cols[f2_pcol].phys;
+            gp.col = src.cols[f2_pcol].data;
+            gp.lo = (int64_t)std::max<i128>(f2_lo, INT64_MIN);
+            gp.span = (uint64_t)((int64_t)std::min<i128>(f2_hi, INT64_MAX)) - (uint64_t)gp.lo;
+            if (gp.src == 1) bytes += (double)src.n * PhysSize(src.cols[f2_pcol].phys);
+          }
+          bool launched;
           {
             ProfScope ps(e, "group_direct", bytes, src.n);
-            dev::GroupByDirectStates(K.data, K.phys, (int64_t)ks->imin, nk, nv > 0 ? src.cols[vcols[0]].data : nullptr,
-                                     nv > 1 ? src.cols[vcols[1]].data : nullptr, vphys, nv, mm, src.n, seg, R,
-                                     (unsigned long long *)cs->p, (dev::AggState *)s0->p, (dev::AggState *)s1->p, 0,
-                                     e.stream);
+            launched = dev::GroupByDirectStates(K.data, K.phys, (int64_t)ks->imin, nk,
+                                                nv > 0 ? src.cols[vcols[0]].data : nullptr,
+                                                nv > 1 ? src.cols[vcols[1]].data : nullptr, vphys, nv, mm, src.n, seg,
+                                                R, (unsigned long long *)cs->p, (dev::AggState *)s0->p,
+                                                (dev::AggState *)s1->p, 0, e.stream, s.where ? &gp : nullptr);
           }
+          if (!launched) goto generic;
           auto list = Alloc(e, nslots * 4);
           dev::CompactSlots((const unsigned long long *)cs->p, nslots, (int32_t *)list->p, e.d_scratch, e.stream);
           int64_t ngroups = ReadDev<int64_t>(e, e.d_scratch);
@@ -1354,6 +1373,7 @@ static DRel Aggregate(Engine &e, const DRel &src, const BoundSelect &s) {
       }
     }
   }
+generic:
   // ---- generic path: compact [groups..., agg args...] then reduce
   std::vector<BExprPtr> exprs = s.groups;
   std::vector<int> arg_idx(na, -1);

@@ -1344,11 +1344,15 @@ __global__ __launch_bounds__(256) void group_direct_lds_kernel(const TK *__restr
                                                                const TV *__restrict__ v1, int64_t n, int64_t kmin,
                                                                int nk, int R, size_t ring_off,
                                                                unsigned long long *cstar, AggState *st0,
-                                                               AggState *st1) {
+                                                               AggState *st1, GroupPred pr) {
   extern __shared__ __attribute__((aligned(16))) unsigned char lds_raw[];
   constexpr int KB = 256 * (int)sizeof(TK), VB = 256 * (int)sizeof(TV);  // bytes per step
-  constexpr int SB = KB + NV * VB;                                         // slot bytes
-  constexpr int NLD = SB / 1024;                                           // glds per step
+  constexpr int SB0 = KB + NV * VB;                                        // slot bytes without a predicate slice
+  // NLD counts the glds of a step without the optional predicate slice: with
+  // one, the counted wait below is merely conservative (loads retire in order)
+  constexpr int NLD = SB0 / 1024;
+  const int PB = pr.src == 1 ? 256 * (pr.phys == P_I64 ? 8 : 4) : 0;
+  const int SB = SB0 + PB;
   const int nslot = nk * R;
   unsigned int *cnt = (unsigned int *)lds_raw;
   long long *sum0 = (long long *)(lds_raw + ((nslot * 4 + 15) & ~15));
@@ -1403,6 +1407,12 @@ __global__ __launch_bounds__(256) void group_direct_lds_kernel(const TK *__restr
         __builtin_amdgcn_global_load_lds((const void *)(vp + j * 1024 + lane * 16), (void *)(dst + KB + VB + j * 1024), 16,
                                          0, 2);
     }
+    if (PB) {
+      const unsigned char *pp = (const unsigned char *)pr.col + q * PB;
+      __builtin_amdgcn_global_load_lds((const void *)(pp + lane * 16), (void *)(dst + SB0), 16, 0, 2);
+      if (PB == 2048)
+        __builtin_amdgcn_global_load_lds((const void *)(pp + 1024 + lane * 16), (void *)(dst + SB0 + 1024), 16, 0, 2);
+    }
   };
   if (nsteps > 0) {
 #pragma unroll
@@ -1435,17 +1445,43 @@ __global__ __launch_bounds__(256) void group_direct_lds_kernel(const TK *__restr
         o[0] = x0.x; o[1] = x0.y; o[2] = x1.x; o[3] = x1.y;
       }
     }
+    bool ok[4] = {true, true, true, true};
+    if (pr.src) {
+      int64_t pv[4];
+      if (pr.src == 2) {
+        pv[0] = kk[0]; pv[1] = kk[1]; pv[2] = kk[2]; pv[3] = kk[3];
+      } else if (pr.src == 3) {
+        pv[0] = a[0]; pv[1] = a[1]; pv[2] = a[2]; pv[3] = a[3];
+      } else if (PB == 1024) {
+        v4i32 x = *(const v4i32 *)(src + SB0 + lane * 16);
+        pv[0] = x.x; pv[1] = x.y; pv[2] = x.z; pv[3] = x.w;
+      } else {
+        v2i64 x0 = *(const v2i64 *)(src + SB0 + lane * 32), x1 = *(const v2i64 *)(src + SB0 + lane * 32 + 16);
+        pv[0] = x0.x; pv[1] = x0.y; pv[2] = x1.x; pv[3] = x1.y;
+      }
+#pragma unroll
+      for (int e = 0; e < 4; e++) ok[e] = (uint64_t)(pv[e] - pr.lo) <= pr.span;
+    }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     int64_t q = st + DEPTH * nw;
     issue(q < nsteps ? q : st, k);
 #pragma unroll
-    for (int e = 0; e < 4; e++) row(kk[e], NV >= 1 ? a[e] : 0, NV >= 2 ? b[e] : 0);
+    for (int e = 0; e < 4; e++)
+      if (ok[e]) row(kk[e], NV >= 1 ? a[e] : 0, NV >= 2 ? b[e] : 0);
     k = k + 1 == DEPTH ? 0 : k + 1;
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   if (blockIdx.x == 0) {
-    for (int64_t i = (nsteps << 8) + t; i < n; i += blockDim.x)
-      row((int64_t)keys[i], NV >= 1 ? (int64_t)v0[i] : 0, NV >= 2 ? (int64_t)v1[i] : 0);
+    for (int64_t i = (nsteps << 8) + t; i < n; i += blockDim.x) {
+      int64_t kv = (int64_t)keys[i], av = NV >= 1 ? (int64_t)v0[i] : 0;
+      bool okr = true;
+      if (pr.src) {
+        int64_t pv = pr.src == 2 ? kv : pr.src == 3 ? av
+                   : (pr.phys == P_I64 ? ((const int64_t *)pr.col)[i] : (int64_t)((const int32_t *)pr.col)[i]);
+        okr = (uint64_t)(pv - pr.lo) <= pr.span;
+      }
+      if (okr) row(kv, av, NV >= 2 ? (int64_t)v1[i] : 0);
+    }
   }
   __syncthreads();
   for (int kq = t; kq < nk; kq += blockDim.x) {
@@ -1499,10 +1535,13 @@ size_t GroupDirectLds(int nk, int R, int nv, bool mm) {
   return b;
 }
 
-void GroupByDirectStates(const void *kcol, int kphys, int64_t kmin, int nk, const void *v0, const void *v1, int vphys,
+bool GroupByDirectStates(const void *kcol, int kphys, int64_t kmin, int nk, const void *v0, const void *v1, int vphys,
                          int nv, bool mm, int64_t nrows, int64_t seg_rows, int R, unsigned long long *cstar,
-                         AggState *st0, AggState *st1, int grid_blocks, hipStream_t s) {
-  if (nrows <= 0) return;
+                         AggState *st0, AggState *st1, int grid_blocks, hipStream_t s, const GroupPred *pred) {
+  if (nrows <= 0) return true;
+  GroupPred pr;
+  memset(&pr, 0, sizeof(pr));
+  if (pred) pr = *pred;
   // LDS-DMA variant: one flush at the end, so a block's whole row share must
   // fit the overflow bound the host derived (seg_rows) — else the segmented
   // kernel below.  MBX_GD_VARIANT="d<depth>_g<blocks per CU>" / "seg".
@@ -1511,9 +1550,9 @@ void GroupByDirectStates(const void *kcol, int kphys, int64_t kmin, int nk, cons
   // byte and stay on the segmented kernel at 4 blocks/CU (6.40 TB/s).
   {
     int depth = 2, gpc = 3;
-    bool use = nv > 0;
+    bool use = nv > 0 || pr.src != 0;  // the segmented kernel has no predicate
     const char *e = getenv("MBX_GD_VARIANT");
-    if (e && *e) use = sscanf(e, "d%d_g%d", &depth, &gpc) == 2;
+    if (e && *e) use = sscanf(e, "d%d_g%d", &depth, &gpc) == 2 || pr.src != 0;
     if (use) {
       int grid = grid_blocks > 0 ? grid_blocks : NumCUs() * gpc;
       int64_t nsteps = nrows >> 8;
@@ -1521,13 +1560,14 @@ void GroupByDirectStates(const void *kcol, int kphys, int64_t kmin, int nk, cons
       int64_t rows_per_block = ((nsteps + waves - 1) / waves) * 4 * 256 + 256;
       size_t tab = GroupDirectLds(nk, R, nv, mm);
       size_t ring_off = (tab + 15) & ~(size_t)15;
-      size_t slot = 256 * (size_t)(kphys == P_I64 ? 8 : 4) + (size_t)nv * 256 * (vphys == P_I64 ? 8 : 4);
+      size_t slot = 256 * (size_t)(kphys == P_I64 ? 8 : 4) + (size_t)nv * 256 * (vphys == P_I64 ? 8 : 4) +
+                    (pr.src == 1 ? 256 * (size_t)(pr.phys == P_I64 ? 8 : 4) : 0);
       depth = depth <= 2 ? 2 : depth <= 3 ? 3 : 4;
       size_t lds = ring_off + 4 * (size_t)depth * slot;
       if ((seg_rows <= 0 || seg_rows >= rows_per_block) && lds <= 64 * 1024) {
 #define GL(TK, TV, NV, MM, D)                                                                                       \
   hipLaunchKernelGGL((group_direct_lds_kernel<TK, TV, NV, MM, D>), dim3(grid), dim3(256), lds, s, (const TK *)kcol, \
-                     (const TV *)v0, (const TV *)v1, nrows, kmin, nk, R, ring_off, cstar, st0, st1)
+                     (const TV *)v0, (const TV *)v1, nrows, kmin, nk, R, ring_off, cstar, st0, st1, pr)
 #define GLD(TK, TV, NV, MM) \
   if (depth == 2) GL(TK, TV, NV, MM, 2); else if (depth == 3) GL(TK, TV, NV, MM, 3); else GL(TK, TV, NV, MM, 4);
 #define GLV(TK, TV)                                                                      \
@@ -1543,10 +1583,11 @@ void GroupByDirectStates(const void *kcol, int kphys, int64_t kmin, int nk, cons
 #undef GLD
 #undef GL
         CHECK_LAUNCH();
-        return;
+        return true;
       }
     }
   }
+  if (pr.src) return false;  // a predicate needs the LDS-DMA kernel
   int grid = grid_blocks > 0 ? grid_blocks : NumCUs() * 4;
   int64_t chunk = (nrows + grid - 1) / grid;
   chunk = (chunk + 3) & ~(int64_t)3;
@@ -1566,6 +1607,7 @@ void GroupByDirectStates(const void *kcol, int kphys, int64_t kmin, int nk, cons
   }
 #undef GDV
 #undef GD
+  return true;
 }
 
 // ---------------------------------------------------------------------------

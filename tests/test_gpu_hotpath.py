@@ -385,3 +385,29 @@ def test_order_by_extremes_and_varchar(conn):
     res = q(conn, "SELECT s, x FROM ox ORDER BY s DESC, x")
     got = [(None if n[0] else r[0]) for r, n in zip(res.rows, res.nulls)]
     assert got == ["prefix_longer_than_8_b", "prefix_longer_than_8_a", "prefix_longer", "b", "a", "", None]
+
+
+# ---- filter -> GROUP BY fused (range predicate inside the LDS group kernel) -------
+@pytest.mark.parametrize("variant", ["", "d3_g2"])
+def test_filter_groupby_fused_parity(conn, oracle, monkeypatch, variant):
+    monkeypatch.setenv("MBX_GD_VARIANT", variant)
+    for n in (255, 257, 100_003, 1_000_000):
+        k = oracle.synth_i64(n, 7, 0, 32, 0)
+        v = oracle.synth_i64(n, 9, 0, 2**40, -2**39)
+        x = oracle.synth_i64(n, 42, 0, 50, 1)
+        q(conn, "DROP TABLE IF EXISTS fg")
+        q(conn, f"CREATE TABLE fg AS SELECT CAST(mbx_synth(7, i, 32) AS INTEGER) AS k, "
+                f"mbx_synth(9, i, 1099511627776) - 549755813888 AS v, mbx_synth(42, i, 50) + 1 AS x, "
+                f"CAST(mbx_synth(42, i, 50) + 1 AS INTEGER) AS x4 FROM range({n}) tbl(i)")
+        cases = [("x > 24", x > 24), ("x4 BETWEEN 10 AND 20", (x >= 10) & (x <= 20)), ("k < 16", k < 16),
+                 ("v >= 0", v >= 0), ("x = 7", x == 7), ("x > 50", x > 50)]
+        for where, m in cases:
+            res = q(conn, f"SELECT k, SUM(v), COUNT(*), MIN(v), MAX(v) FROM fg WHERE {where} GROUP BY k ORDER BY k")
+            want = []
+            for kk in range(32):
+                sel = m & (k == kk)
+                c = int(sel.sum())
+                if c:
+                    vs = v[sel]
+                    want.append([str(kk), str(int(vs.astype(object).sum())), str(c), str(int(vs.min())), str(int(vs.max()))])
+            assert res.rows == want, (variant, n, where)
