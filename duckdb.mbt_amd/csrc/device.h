@@ -16,9 +16,15 @@ struct VmCols {
 
 struct VmOuts {
   void *data[VM_MAX_OUT];
-  uint32_t *valid[VM_MAX_OUT];  // 32-bit-word view of the LSB-first bitmap (zeroed), or null
-  int32_t *anynull;             // per output: set to 1 if a NULL was written
+  // 32-bit-word view of a zeroed NULL bitmap (bit = 1: row is NULL), or null.
+  // Only NULL rows touch it (rare), so the common all-valid output costs no
+  // bitmap traffic; InvertNullBits turns it into a validity bitmap when
+  // anynull says one is needed.
+  uint32_t *nullbits[VM_MAX_OUT];
+  int32_t *anynull;  // per output: set to 1 if a NULL was written
 };
+// validity[w] = ~nullbits[w] over the words covering n rows (tail bits cleared)
+void InvertNullBits(uint64_t *bits, int64_t n, hipStream_t s);
 
 // --- expression VM --------------------------------------------------------
 // Predicate pass: one bit per row into sel_bits (4 x u64 words per 256-row

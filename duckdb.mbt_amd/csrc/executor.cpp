@@ -852,9 +852,9 @@ static DRel FilterProject(Engine &e, const DRel &rel, const BExprPtr &pred, cons
     memset(&vo, 0, sizeof(vo));
     vo.anynull = (int32_t *)anynull->p;
     for (size_t k = 0; k < cnt; k++) {
-      DCol d = AllocOut(e, exprs[base + k]->type, nsel, true);
+      DCol d = AllocOut(e, exprs[base + k]->type, nsel, true);  // zeroed: the NULL bitmap until inverted
       vo.data[k] = d.data;
-      vo.valid[k] = (uint32_t *)d.validity;
+      vo.nullbits[k] = (uint32_t *)d.validity;
       outs.push_back(d);
     }
     if (nsel > 0) {
@@ -868,6 +868,7 @@ static DRel FilterProject(Engine &e, const DRel &rel, const BExprPtr &pred, cons
     for (size_t k = 0; k < cnt; k++) {
       DCol &d = outs[k];
       if (!an[k]) d.validity = nullptr;  // all valid: drop the bitmap (owner freed with the column)
+      else dev::InvertNullBits(d.validity, nsel, e.stream);
       if (ClassOf(exprs[base + k]->type) == VC_STR) {
         const DCol *src = src_cols[k] >= 0 ? &rel.cols[src_cols[k]] : nullptr;
         MaterializeStrings(e, d, src, pool, nsel);

@@ -526,9 +526,9 @@ __global__ __launch_bounds__(256) void vm_project_kernel(VmProgram P, VmCols C, 
       for (int o = 0; o < P.n_out; o++) {
         const int r = P.out_reg[o];
         store_phys(O.data[o], P.out_phys[o], out_idx, R.lo[r][t], R.hi[r][t]);
-        if (O.valid[o]) {
-          if (!R.nl[r][t]) atomicOr(&O.valid[o][out_idx >> 5], 1u << (out_idx & 31));
-          else if (O.anynull) O.anynull[o] = 1;
+        if (R.nl[r][t] && O.nullbits[o]) {
+          atomicOr(&O.nullbits[o][out_idx >> 5], 1u << (out_idx & 31));
+          if (O.anynull) O.anynull[o] = 1;
         }
       }
     }
@@ -553,6 +553,21 @@ void VmProject(const VmProgram &p, const VmCols &cols, int64_t nrows, int64_t ra
   int grid = GridFor(ntiles, 1, NumCUs() * 8);
   hipLaunchKernelGGL(vm_project_kernel, dim3(grid), dim3(256), 0, s, p, cols, nrows, range_start, range_step,
                      sel_bits, tile_offsets, outs, err);
+  CHECK_LAUNCH();
+}
+
+__global__ void invert_bits_kernel(uint64_t *bits, int64_t n) {
+  const int64_t words = (n + 63) >> 6;
+  for (int64_t w = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; w < words; w += (int64_t)gridDim.x * blockDim.x) {
+    uint64_t v = ~bits[w];
+    if (w == words - 1 && (n & 63)) v &= (1ull << (n & 63)) - 1ull;
+    bits[w] = v;
+  }
+}
+
+void InvertNullBits(uint64_t *bits, int64_t n, hipStream_t s) {
+  if (n <= 0) return;
+  hipLaunchKernelGGL(invert_bits_kernel, dim3(GridFor((n + 63) >> 6, 256, NumCUs() * 4)), dim3(256), 0, s, bits, n);
   CHECK_LAUNCH();
 }
 
