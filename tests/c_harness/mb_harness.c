@@ -1,0 +1,206 @@
+/*
+ * mb_harness.c — drives libduckdb_mb_amd.so through include/duckdb_mb.h the
+ * way MoonBit's native backend does (src/moon.pkg links the stub library;
+ * src/duckdb_native.mbt calls the symbols), with a stand-in for the MoonBit
+ * runtime: a STRONG moonbit_make_bytes_raw that tags every object it makes.
+ * The library's own allocator is weak, so every Bytes it returns must carry
+ * this runtime's tag — the property INTEGRATION.md relies on.
+ *
+ *   mb_harness cpu          host-constant queries only (mbx_allow_no_gpu)
+ *   mb_harness gpu <rows>   C2 on the device: COUNT(*) WHERE x > 24, appender,
+ *                           Arrow int64 getter; prints "count=<n>"
+ * Exit status 0 = every check passed.
+ */
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include "duckdb_mb.h"
+
+/* ---- fake MoonBit runtime: {int32 rc; uint32 meta} header + payload ---- */
+#define FAKE_RC 0x4D42 /* "MB" */
+static long g_made = 0;
+moonbit_bytes_t moonbit_make_bytes_raw(int32_t len) {
+  if (len < 0) len = 0;
+  int32_t *h = (int32_t *)calloc(1, 8 + (size_t)len + 1);
+  h[0] = FAKE_RC;
+  ((uint32_t *)h)[1] = (uint32_t)len & ((1u << 28) - 1);
+  g_made++;
+  return (moonbit_bytes_t)(h + 2);
+}
+static int32_t mb_len(moonbit_bytes_t b) { return (int32_t)(((uint32_t *)b)[-1] & ((1u << 28) - 1)); }
+static int32_t mb_rc(moonbit_bytes_t b) { return ((int32_t *)b)[-2]; }
+static void mb_free(moonbit_bytes_t b) {
+  if (b) free((int32_t *)b - 2);
+}
+static moonbit_bytes_t S(const char *s) {
+  int32_t n = (int32_t)strlen(s);
+  moonbit_bytes_t b = moonbit_make_bytes_raw(n);
+  memcpy(b, s, (size_t)n);
+  return b;
+}
+
+static int g_fail = 0;
+#define CHECK(c, ...)                                \
+  do {                                               \
+    if (!(c)) {                                      \
+      fprintf(stderr, "FAIL %s:%d: ", __FILE__, __LINE__); \
+      fprintf(stderr, __VA_ARGS__);                  \
+      fprintf(stderr, "\n");                         \
+      g_fail++;                                      \
+    }                                                \
+  } while (0)
+
+/* a returned Bytes: check it came from this runtime, copy it out, release it */
+static char *take(moonbit_bytes_t b) {
+  static char buf[4096];
+  if (!b) {
+    buf[0] = 0;
+    return buf;
+  }
+  CHECK(mb_rc(b) == FAKE_RC, "returned Bytes not allocated by the MoonBit runtime (rc=%d)", mb_rc(b));
+  int32_t n = mb_len(b);
+  if (n > (int32_t)sizeof(buf) - 1) n = sizeof(buf) - 1;
+  memcpy(buf, b, (size_t)n);
+  buf[n] = 0;
+  mb_free(b);
+  return buf;
+}
+
+static void check_cell(duckdb_mb_result *r, int col, int row, const char *want) {
+  char *got = take(duckdb_mb_result_value(r, col, row));
+  CHECK(strcmp(got, want) == 0, "cell(%d,%d) = '%s', want '%s'", col, row, got, want);
+}
+
+static duckdb_mb_connection *open_conn(int allow_no_gpu) {
+  duckdb_mb_config *cfg = duckdb_mb_config_create();
+  if (allow_no_gpu) {
+    moonbit_bytes_t k = S("mbx_allow_no_gpu"), v = S("true");
+    CHECK(duckdb_mb_config_set(cfg, k, v) == 1, "config_set mbx_allow_no_gpu");
+    mb_free(k);
+    mb_free(v);
+  }
+  moonbit_bytes_t bad_k = S("no_such_option"), bad_v = S("1");
+  CHECK(duckdb_mb_config_set(cfg, bad_k, bad_v) == 0, "unknown config key must fail");
+  CHECK(strstr(take(duckdb_mb_config_error(cfg)), "duckdb_set_config failed") != NULL, "config error text");
+  mb_free(bad_k);
+  mb_free(bad_v);
+  moonbit_bytes_t path = S(":memory:");
+  duckdb_mb_connection *c = duckdb_mb_connect_with_config(path, cfg);
+  mb_free(path);
+  duckdb_mb_config_destroy(cfg);
+  CHECK(c && !duckdb_mb_is_null_conn(c), "connect: %s", take(duckdb_mb_last_error()));
+  return c;
+}
+
+static void host_constant_checks(duckdb_mb_connection *c) {
+  moonbit_bytes_t sql = S("SELECT 1 AS a, 'x' AS b, NULL AS n, 9223372036854775807 AS big, 5.0 / 2 AS d");
+  duckdb_mb_result *r = duckdb_mb_query(c, sql);
+  mb_free(sql);
+  CHECK(r && !duckdb_mb_is_null_result(r), "query: %s", take(duckdb_mb_last_error()));
+  if (!r) return;
+  CHECK(duckdb_mb_result_column_count(r) == 5, "column_count");
+  CHECK(duckdb_mb_result_row_count(r) == 1, "row_count");
+  CHECK(strcmp(take(duckdb_mb_result_column_name(r, 1)), "b") == 0, "column_name");
+  CHECK(duckdb_mb_result_column_type(r, 0) == 4, "INTEGER type id 4 (src/duckdb_parsing.mbt:8-52)");
+  CHECK(duckdb_mb_result_column_type(r, 3) == 5, "BIGINT type id 5");
+  CHECK(duckdb_mb_result_column_type(r, 4) == 11, "DOUBLE type id 11");
+  check_cell(r, 0, 0, "1");
+  check_cell(r, 1, 0, "x");
+  CHECK(duckdb_mb_result_is_null(r, 2, 0) == 1, "is_null");
+  check_cell(r, 3, 0, "9223372036854775807");
+  check_cell(r, 4, 0, "2.5");
+  duckdb_mb_result_destroy(r);
+
+  /* errors: NULL result + message from duckdb_mb_last_error */
+  sql = S("SELEC 1");
+  r = duckdb_mb_query(c, sql);
+  mb_free(sql);
+  CHECK(r == NULL || duckdb_mb_is_null_result(r), "bad SQL must fail");
+  CHECK(strlen(take(duckdb_mb_last_error())) > 0, "last_error set on failure");
+
+  /* prepared statement with a bigint parameter (reference native test :210-227) */
+  sql = S("SELECT ? * 2");
+  duckdb_mb_statement *st = duckdb_mb_prepare(c, sql);
+  mb_free(sql);
+  CHECK(st && !duckdb_mb_is_null_statement(st), "prepare");
+  if (st) {
+    CHECK(duckdb_mb_bind_bigint(st, 1, 1000000000) == 1, "bind_bigint");
+    r = duckdb_mb_execute_prepared(st);
+    CHECK(r && !duckdb_mb_is_null_result(r), "execute_prepared");
+    if (r) {
+      check_cell(r, 0, 0, "2000000000");
+      duckdb_mb_result_destroy(r);
+    }
+    duckdb_mb_statement_destroy(st);
+  }
+}
+
+static int gpu_checks(duckdb_mb_connection *c, long rows) {
+  char q[512];
+  snprintf(q, sizeof q, "CREATE TABLE t AS SELECT mbx_synth(42, i, 50) + 1 AS x FROM range(%ld) tbl(i)", rows);
+  moonbit_bytes_t sql = S(q);
+  duckdb_mb_result *r = duckdb_mb_query(c, sql);
+  mb_free(sql);
+  CHECK(r != NULL, "CTAS: %s", take(duckdb_mb_last_error()));
+  if (r) duckdb_mb_result_destroy(r);
+  sql = S("SELECT COUNT(*) FROM t WHERE x > 24");
+  r = duckdb_mb_query(c, sql);
+  mb_free(sql);
+  CHECK(r != NULL, "C2 query: %s", take(duckdb_mb_last_error()));
+  if (r) {
+    printf("count=%s\n", take(duckdb_mb_result_value(r, 0, 0)));
+    duckdb_mb_result_destroy(r);
+  }
+  /* appender rows -> device -> Arrow int64 wire buffer [i32 count][int64 LE...] */
+  sql = S("CREATE TABLE a (v BIGINT)");
+  r = duckdb_mb_query(c, sql);
+  mb_free(sql);
+  if (r) duckdb_mb_result_destroy(r);
+  moonbit_bytes_t sch = S("main"), tab = S("a");
+  duckdb_mb_appender *ap = duckdb_mb_appender_create(c, sch, tab);
+  mb_free(sch);
+  mb_free(tab);
+  CHECK(ap != NULL, "appender_create");
+  for (int64_t i = 0; ap && i < 1000; i++) {
+    duckdb_mb_begin_row(ap);
+    duckdb_mb_append_bigint(ap, i * 2654435761LL);
+    CHECK(duckdb_mb_end_row(ap) == 1, "end_row");
+  }
+  if (ap) duckdb_mb_appender_destroy(ap); /* close => flush */
+  sql = S("SELECT v FROM a");
+  duckdb_mb_arrow_result *ar = duckdb_mb_query_arrow(c, sql);
+  mb_free(sql);
+  CHECK(ar && !duckdb_mb_is_null_arrow_result(ar), "query_arrow");
+  if (ar) {
+    moonbit_bytes_t w = duckdb_mb_arrow_get_column_int64(ar, 0);
+    CHECK(mb_rc(w) == FAKE_RC && mb_len(w) == 4 + 8 * 1000, "arrow int64 buffer size %d", mb_len(w));
+    int32_t cnt;
+    memcpy(&cnt, w, 4);
+    CHECK(cnt == 1000, "arrow count %d", cnt);
+    for (int i = 0; i < 1000; i++) {
+      int64_t v;
+      memcpy(&v, w + 4 + 8 * i, 8);
+      if (v != (int64_t)i * 2654435761LL) {
+        CHECK(0, "arrow value %d = %lld", i, (long long)v);
+        break;
+      }
+    }
+    mb_free(w);
+    duckdb_mb_arrow_destroy(ar);
+  }
+  return 0;
+}
+
+int main(int argc, char **argv) {
+  const char *mode = argc > 1 ? argv[1] : "cpu";
+  int gpu = strcmp(mode, "gpu") == 0;
+  duckdb_mb_connection *c = open_conn(!gpu);
+  if (!c) return 1;
+  host_constant_checks(c);
+  if (gpu) gpu_checks(c, argc > 2 ? atol(argv[2]) : 1000000);
+  duckdb_mb_disconnect(c);
+  CHECK(g_made > 0, "no Bytes made through the runtime allocator");
+  printf("harness %s: %s (%ld runtime Bytes)\n", mode, g_fail ? "FAILED" : "ok", g_made);
+  return g_fail ? 1 : 0;
+}
