@@ -108,6 +108,26 @@ static bool IsBareValues(const Select &s) {
          s.group_by.empty() && !s.having && s.order_by.empty() && !s.limit && !s.offset && s.union_all.empty();
 }
 
+StreamSource RunStatementStream(Connection &c, const Statement &st, const std::vector<Value> &params) {
+  StreamSource src;
+  if (st.kind == Statement::SELECT) {
+    BoundSelectPtr b = BindSelect(*st.select, c.catalog, params);
+    src.dev = ExecuteSelectDevice(c, *b, &src);
+    if (src.dev) return src;
+    src.host = ExecuteSelect(c, *b);
+  } else {
+    src.host = RunParsed(c, st, params);
+  }
+  src.names.clear();
+  src.types.clear();
+  for (auto &hc : src.host->cols) {
+    src.names.push_back(hc.name);
+    src.types.push_back(hc.type);
+  }
+  src.nrows = src.host->nrows;
+  return src;
+}
+
 ResultPtr RunParsed(Connection &c, const Statement &st, const std::vector<Value> &params) {
   switch (st.kind) {
     case Statement::NOP:

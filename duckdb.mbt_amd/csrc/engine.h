@@ -107,6 +107,20 @@ struct Connection {
   ~Connection();
 };
 
+// A SELECT result left on the device; streams copy it back in batches.
+struct DeviceResult;
+typedef std::shared_ptr<DeviceResult> DeviceResultPtr;
+struct StreamSource {
+  std::vector<std::string> names;
+  std::vector<LogicalType> types;
+  int64_t nrows = 0;
+  ResultPtr host;       // host-side result (DDL, constant SELECTs)
+  DeviceResultPtr dev;  // device-resident SELECT result
+};
+StreamSource RunStatementStream(Connection &c, const Statement &st, const std::vector<Value> &params);
+// rows [start, start + n) of a device result, materialized on the host
+ResultPtr FetchDeviceRows(Connection &c, DeviceResult &d, int64_t start, int64_t n);
+
 // Runs one statement; returns a materialized result (empty for DDL).
 ResultPtr RunStatement(Connection &c, const std::string &sql, const std::vector<Value> &params, int *n_params_out);
 ResultPtr RunParsed(Connection &c, const Statement &st, const std::vector<Value> &params);
@@ -115,6 +129,7 @@ std::string Explain(Connection &c, const std::string &sql);
 // Executor entry points (executor.cpp).
 std::shared_ptr<Engine> CreateEngine(int device, bool allow_no_gpu);
 ResultPtr ExecuteSelect(Connection &c, const BoundSelect &s);
+DeviceResultPtr ExecuteSelectDevice(Connection &c, const BoundSelect &s, StreamSource *meta);
 void ExecuteInsertSelect(Connection &c, Table &t, const BoundSelect &s, const std::vector<int> &col_map);
 TablePtr CreateDeviceTable(Connection &c, const std::string &name, const std::vector<std::string> &names,
                            const std::vector<LogicalType> &types);

@@ -2034,6 +2034,40 @@ ResultPtr ExecuteSelect(Connection &c, const BoundSelect &s) {
   return res;
 }
 
+// ---- device-resident results for streams ----------------------------------
+struct DeviceResult {
+  DRel r;
+  std::vector<std::string> names;
+};
+
+// nullptr for host-constant SELECTs (the caller materializes those)
+DeviceResultPtr ExecuteSelectDevice(Connection &c, const BoundSelect &s, StreamSource *meta) {
+  if (IsHostConstantSelect(s)) return nullptr;
+  auto t0 = std::chrono::steady_clock::now();
+  Engine &e = Eng(c);
+  e.profile = c.opts.profile;
+  e.events.clear();
+  e.plan_text = c.opts.profile ? ExplainSelect(s) : "";
+  e.ev_used = 0;
+  auto d = std::make_shared<DeviceResult>();
+  d->r = RunSelectDev(e, c, s);
+  d->names.assign(s.names.begin(), s.names.begin() + VisibleCols(s));
+  HIPCHK(hipStreamSynchronize(e.stream));
+  CheckError(e);
+  meta->names = d->names;
+  meta->types.clear();
+  for (size_t i = 0; i < d->names.size(); i++) meta->types.push_back(d->r.cols[i].type);
+  meta->nrows = d->r.n;
+  double ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+  FinishProfile(c, e, ms);
+  return d;
+}
+
+ResultPtr FetchDeviceRows(Connection &c, DeviceResult &d, int64_t start, int64_t n) {
+  Engine &e = Eng(c);
+  return ToHost(e, d.r, d.names, start, n, d.names.size());
+}
+
 // ---------------------------------------------------------------------------
 // tables: creation, append, stats
 // ---------------------------------------------------------------------------

@@ -81,8 +81,17 @@ struct duckdb_mb_connection {
 struct duckdb_mb_result {
   ResultPtr r;
 };
+// A stream reads a device-resident SELECT result back in batches of
+// kStreamBatch rows (one pinned D2H each) and serves 2048-row chunks from the
+// current batch; host-side results (DDL, constant SELECTs) are served as is.
 struct duckdb_mb_stream {
-  ResultPtr r;
+  duckdb_mb_connection *conn = nullptr;
+  std::vector<std::string> names;
+  std::vector<LogicalType> types;
+  int64_t nrows = 0;
+  DeviceResultPtr dev;
+  ResultPtr r;  // host result, or the current batch of a device result
+  int64_t batch_start = 0;
   int64_t pos = 0;
 };
 struct duckdb_mb_chunk {
@@ -230,14 +239,19 @@ static bool StreamSupported(TypeId t) {
   }
 }
 
-static duckdb_mb_stream *StreamFrom(ResultPtr r) {  // ref :320-353
-  for (auto &c : r->cols)
-    if (!StreamSupported(c.type.id)) {
+static duckdb_mb_stream *StreamFrom(duckdb_mb_connection *h, StreamSource src) {  // ref :320-353
+  for (auto &t : src.types)
+    if (!StreamSupported(t.id)) {
       SetError("streaming query has unsupported column type");
       return nullptr;
     }
   auto *s = new duckdb_mb_stream();
-  s->r = r;
+  s->conn = h;
+  s->names = std::move(src.names);
+  s->types = std::move(src.types);
+  s->nrows = src.nrows;
+  s->dev = src.dev;
+  s->r = src.host;
   return s;
 }
 
@@ -247,7 +261,8 @@ duckdb_mb_stream *duckdb_mb_query_stream(duckdb_mb_connection *h, moonbit_bytes_
     return nullptr;
   }
   try {
-    return StreamFrom(RunStatement(h->conn, BytesStr(sql), {}, nullptr));
+    Statement st = ParseSQL(BytesStr(sql));
+    return StreamFrom(h, RunStatementStream(h->conn, st, {}));
   } catch (std::exception &e) {
     SetError(e.what());
     return nullptr;
@@ -257,29 +272,40 @@ duckdb_mb_stream *duckdb_mb_query_stream(duckdb_mb_connection *h, moonbit_bytes_
 void duckdb_mb_stream_destroy(duckdb_mb_stream *s) { delete s; }  // ref :426-438
 int32_t duckdb_mb_is_null_stream(duckdb_mb_stream *s) { return s == nullptr ? 1 : 0; }  // ref :440
 int32_t duckdb_mb_stream_column_count(duckdb_mb_stream *s) {  // ref :444-449
-  return s ? (int32_t)s->r->cols.size() : 0;
+  return s ? (int32_t)s->names.size() : 0;
 }
 moonbit_bytes_t duckdb_mb_stream_column_name(duckdb_mb_stream *s, int32_t col) {  // ref :451-464
-  if (!s || col < 0 || col >= (int32_t)s->r->cols.size()) return moonbit_make_bytes_raw(0);
-  return MakeBytes(s->r->cols[col].name);
+  if (!s || col < 0 || col >= (int32_t)s->names.size()) return moonbit_make_bytes_raw(0);
+  return MakeBytes(s->names[col]);
 }
 
 // DuckDB's standard vector size: result chunks carry at most 2048 rows.
 static const int64_t kVectorSize = 2048;
+// rows per device->host batch of a streamed device result (32 vectors)
+static const int64_t kStreamBatch = 32 * kVectorSize;
 
 duckdb_mb_chunk *duckdb_mb_stream_fetch_chunk(duckdb_mb_stream *s) {  // ref :466-490
   if (!s) {
     SetError("stream is null");
     return nullptr;
   }
-  if (s->pos >= s->r->nrows) {
+  if (s->pos >= s->nrows) {
     SetError(nullptr);  // end of stream: NULL chunk with an empty error
     return nullptr;
   }
+  if (s->dev && (!s->r || s->pos >= s->batch_start + s->r->nrows)) {
+    try {
+      s->r = FetchDeviceRows(s->conn->conn, *s->dev, s->pos, std::min(kStreamBatch, s->nrows - s->pos));
+      s->batch_start = s->pos;
+    } catch (std::exception &e) {
+      SetError(e.what());
+      return nullptr;
+    }
+  }
   auto *c = new duckdb_mb_chunk();
   c->r = s->r;
-  c->start = s->pos;
-  c->n = std::min(kVectorSize, s->r->nrows - s->pos);
+  c->start = s->pos - s->batch_start;
+  c->n = std::min(kVectorSize, s->nrows - s->pos);
   c->stream = s;
   s->pos += c->n;
   return c;
@@ -441,7 +467,7 @@ duckdb_mb_stream *duckdb_mb_execute_prepared_stream(duckdb_mb_statement *s) {  /
     return nullptr;
   }
   try {
-    return StreamFrom(RunParsed(s->conn->conn, s->st, s->params));
+    return StreamFrom(s->conn, RunStatementStream(s->conn->conn, s->st, s->params));
   } catch (std::exception &e) {
     SetError(e.what());
     return nullptr;

@@ -411,3 +411,37 @@ def test_filter_groupby_fused_parity(conn, oracle, monkeypatch, variant):
                     vs = v[sel]
                     want.append([str(kk), str(int(vs.astype(object).sum())), str(c), str(int(vs.min())), str(int(vs.max()))])
             assert res.rows == want, (variant, n, where)
+
+
+# ---- streams read device-resident results back in batches ------------------------
+def test_stream_device_batches(conn):
+    n = 150_001  # > 2 device->host batches of 65 536 rows, ragged last chunk
+    q(conn, f"CREATE TABLE st AS SELECT i AS a, CASE WHEN i % 5 = 0 THEN NULL ELSE i * 3 END AS b, "
+            f"CASE WHEN i % 2 = 0 THEN 'even' ELSE 'odd' END AS s FROM range({n}) tbl(i)")
+    s = conn.query_stream("SELECT a, b, s FROM st WHERE a % 3 <> 1").value
+    assert s.columns() == ["a", "b", "s"]
+    rows, nulls, chunks = [], [], 0
+    while True:
+        r = s.next().value
+        if r is None:
+            break
+        chunks += 1
+        assert len(r.rows) <= 2048
+        rows.extend(r.rows)
+        nulls.extend(r.nulls)
+    s.close()
+    want = [i for i in range(n) if i % 3 != 1]
+    assert len(rows) == len(want) and chunks == (len(want) + 2047) // 2048
+    for (a, b, st), nl, i in zip(rows, nulls, want):
+        assert int(a) == i
+        assert nl[1] == (i % 5 == 0)
+        if i % 5:
+            assert int(b) == 3 * i
+        assert st == ("even" if i % 2 == 0 else "odd")
+    # the connection keeps working between and after partial reads
+    s2 = conn.query_stream("SELECT a FROM st").value
+    first = s2.next().value
+    assert one(conn, "SELECT COUNT(*) FROM st")[0] == str(n)
+    second = s2.next().value
+    assert int(first.rows[0][0]) == 0 and int(second.rows[0][0]) == 2048
+    s2.close()
