@@ -120,6 +120,11 @@ struct StreamSource {
 StreamSource RunStatementStream(Connection &c, const Statement &st, const std::vector<Value> &params);
 // rows [start, start + n) of a device result, materialized on the host
 ResultPtr FetchDeviceRows(Connection &c, DeviceResult &d, int64_t start, int64_t n);
+// Copies column `col` of a device result straight into host memory `dst`
+// (its physical layout, n rows) when it has physical type `phys` and no
+// NULLs; false otherwise (the caller materializes the result instead).
+bool CopyDeviceColumn(Connection &c, DeviceResult &d, int col, int phys, void *dst);
+bool DeviceColumnPlain(const DeviceResult &d, int col, int phys);  // the precondition of CopyDeviceColumn
 
 // Runs one statement; returns a materialized result (empty for DDL).
 ResultPtr RunStatement(Connection &c, const std::string &sql, const std::vector<Value> &params, int *n_params_out);

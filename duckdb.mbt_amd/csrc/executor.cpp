@@ -2068,6 +2068,22 @@ ResultPtr FetchDeviceRows(Connection &c, DeviceResult &d, int64_t start, int64_t
   return ToHost(e, d.r, d.names, start, n, d.names.size());
 }
 
+bool DeviceColumnPlain(const DeviceResult &d, int col, int phys) {
+  if (col < 0 || col >= (int)d.r.cols.size()) return false;
+  const DCol &dc = d.r.cols[col];
+  return dc.phys == phys && !dc.validity && dc.phys != P_STR && dc.data;
+}
+
+bool CopyDeviceColumn(Connection &c, DeviceResult &d, int col, int phys, void *dst) {
+  if (!DeviceColumnPlain(d, col, phys)) return false;
+  const DCol &dc = d.r.cols[col];
+  Engine &e = Eng(c);
+  size_t bytes = (size_t)d.r.n * PhysSize(dc.phys);
+  if (bytes) HIPCHK(hipMemcpyAsync(dst, dc.data, bytes, hipMemcpyDeviceToHost, e.stream));
+  HIPCHK(hipStreamSynchronize(e.stream));
+  return true;
+}
+
 // ---------------------------------------------------------------------------
 // tables: creation, append, stats
 // ---------------------------------------------------------------------------

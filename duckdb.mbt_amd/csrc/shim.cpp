@@ -121,8 +121,16 @@ struct duckdb_mb_appender {
   std::vector<const uint8_t *> raw_valid;
   std::vector<int64_t> raw_count;
 };
+// The query's result stays on the device: fixed-width getters of columns
+// without NULLs DMA straight into the returned Bytes; the others materialize
+// the result on the host once (lazily) and convert per cell like the
+// reference's duckdb_value_* calls.
 struct duckdb_mb_arrow_result {
-  ResultPtr r;
+  duckdb_mb_connection *conn = nullptr;
+  DeviceResultPtr dev;
+  std::vector<std::string> names;
+  std::vector<LogicalType> types;
+  ResultPtr r;  // host copy (lazy for device results)
   char error[256];
   int32_t column_count = 0, row_count = 0;
 };
@@ -729,12 +737,17 @@ duckdb_mb_arrow_result *duckdb_mb_query_arrow(duckdb_mb_connection *h, moonbit_b
     return nullptr;
   }
   try {
-    ResultPtr r = RunStatement(h->conn, BytesStr(sql), {}, nullptr);
+    Statement st = ParseSQL(BytesStr(sql));
+    StreamSource src = RunStatementStream(h->conn, st, {});
     auto *a = new duckdb_mb_arrow_result();
-    a->r = r;
+    a->conn = h;
+    a->dev = src.dev;
+    a->r = src.host;
+    a->names = std::move(src.names);
+    a->types = std::move(src.types);
     a->error[0] = '\0';
-    a->column_count = (int32_t)r->cols.size();
-    a->row_count = (int32_t)r->nrows;
+    a->column_count = (int32_t)a->names.size();
+    a->row_count = (int32_t)src.nrows;
     return a;
   } catch (std::exception &e) {
     SetError(e.what());
@@ -749,16 +762,16 @@ moonbit_bytes_t duckdb_mb_arrow_schema(duckdb_mb_arrow_result *a) {  // ref :228
   if (!a || a->column_count <= 0) return MakeBytes("[]", 2);
   std::string j = "[";
   for (int32_t i = 0; i < a->column_count; i++) {
-    const HostColumn &c = a->r->cols[i];
+    const LogicalType &ty = a->types[i];
     const char *tid = "string";
-    switch (c.type.id) {
+    switch (ty.id) {
       case T_BOOLEAN: tid = "bool"; break;
       case T_TINYINT: case T_SMALLINT: case T_INTEGER: tid = "int32"; break;
       case T_BIGINT: tid = "int64"; break;
       case T_FLOAT: case T_DOUBLE: tid = "double"; break;
       default: tid = "string"; break;
     }
-    j += std::string(i ? "," : "") + "{\"name\":\"" + c.name + "\",\"nullable\":true,\"type_id\":\"" + tid + "\"}";
+    j += std::string(i ? "," : "") + "{\"name\":\"" + a->names[i] + "\",\"nullable\":true,\"type_id\":\"" + tid + "\"}";
   }
   j += "]";
   return MakeBytes(j);
@@ -788,6 +801,50 @@ static uint8_t CellBool(const HostColumn &c, int64_t row) {
 static bool ArrowOk(duckdb_mb_arrow_result *a, int32_t col) {
   return a && col >= 0 && col < a->column_count && a->row_count > 0;
 }
+// device result, column of exactly this type, no NULLs: DMA into dst
+static bool ArrowDirectOk(duckdb_mb_arrow_result *a, int32_t col, TypeId t, Phys ph) {
+  return a->dev && !a->r && a->types[col].id == t && DeviceColumnPlain(*a->dev, col, ph);
+}
+static bool ArrowDirect(duckdb_mb_arrow_result *a, int32_t col, TypeId t, Phys ph, void *dst) {
+  return ArrowDirectOk(a, col, t, ph) && CopyDeviceColumn(a->conn->conn, *a->dev, col, ph, dst);
+}
+// [i32 count][values] straight from the device column, or nullptr
+static moonbit_bytes_t ArrowDirectBuffer(duckdb_mb_arrow_result *a, int32_t col, TypeId t, Phys ph, int width) {
+  if (!ArrowOk(a, col) || 4 + (int64_t)a->row_count * width > INT32_MAX || !ArrowDirectOk(a, col, t, ph))
+    return nullptr;
+  moonbit_bytes_t out = moonbit_make_bytes_raw(4 + a->row_count * width);
+  memcpy(out, &a->row_count, 4);
+  try {
+    CopyDeviceColumn(a->conn->conn, *a->dev, col, ph, out + 4);
+  } catch (std::exception &e) {
+    SetError(e.what());
+    memset(out + 4, 0, (size_t)a->row_count * width);
+  }
+  return out;
+}
+static const MaterializedResult &ArrowHost(duckdb_mb_arrow_result *a) {
+  if (a->r) return *a->r;
+  try {
+    a->r = FetchDeviceRows(a->conn->conn, *a->dev, 0, a->row_count);
+  } catch (std::exception &e) {
+    // a failed read-back must not cross the C ABI: serve all-NULL columns
+    SetError(e.what());
+    auto r = std::make_shared<MaterializedResult>();
+    r->nrows = a->row_count;
+    for (size_t i = 0; i < a->types.size(); i++) {
+      HostColumn hc;
+      hc.name = a->names[i];
+      hc.type = a->types[i];
+      hc.phys = PhysOf(a->types[i]);
+      hc.data.assign((size_t)a->row_count * 16, 0);
+      hc.valid.assign((size_t)a->row_count, 0);
+      if (hc.phys == P_STR) hc.offsets.assign((size_t)a->row_count + 1, 0);
+      r->cols.push_back(std::move(hc));
+    }
+    a->r = r;
+  }
+  return *a->r;
+}
 
 static moonbit_bytes_t ArrowFixed(duckdb_mb_arrow_result *a, int32_t col, int width, bool nullable) {
   if (!ArrowOk(a, col)) return MakeBytes("", 0);
@@ -802,7 +859,7 @@ static moonbit_bytes_t ArrowFixed(duckdb_mb_arrow_result *a, int32_t col, int wi
   memcpy(out, &cnt, 4);
   uint8_t *vals = out + 4;
   uint8_t *valid = out + 4 + n * width;
-  const HostColumn &c = a->r->cols[col];
+  const HostColumn &c = ArrowHost(a).cols[col];
   for (int64_t i = 0; i < n; i++) {
     bool null = c.IsNull(i);
     if (nullable) valid[i] = null ? 0 : 1;
@@ -831,7 +888,7 @@ static moonbit_bytes_t ArrowF64(duckdb_mb_arrow_result *a, int32_t col, bool nul
   moonbit_bytes_t out = moonbit_make_bytes_raw((int32_t)total);
   int32_t cnt = (int32_t)n;
   memcpy(out, &cnt, 4);
-  const HostColumn &c = a->r->cols[col];
+  const HostColumn &c = ArrowHost(a).cols[col];
   for (int64_t i = 0; i < n; i++) {
     bool null = c.IsNull(i);
     double x = null ? 0.0 : CellF64(c, i);
@@ -844,7 +901,7 @@ static moonbit_bytes_t ArrowF64(duckdb_mb_arrow_result *a, int32_t col, bool nul
 static moonbit_bytes_t ArrowStr(duckdb_mb_arrow_result *a, int32_t col, bool nullable) {
   if (!ArrowOk(a, col)) return MakeBytes("", 0);
   int64_t n = a->row_count;
-  const HostColumn &c = a->r->cols[col];
+  const HostColumn &c = ArrowHost(a).cols[col];
   std::string data;
   for (int64_t i = 0; i < n; i++) {
     if (!c.IsNull(i)) data += FormatValue(c.Get(i));
@@ -861,15 +918,19 @@ static moonbit_bytes_t ArrowStr(duckdb_mb_arrow_result *a, int32_t col, bool nul
   return out;
 }
 
-moonbit_bytes_t duckdb_mb_arrow_get_column_int32(duckdb_mb_arrow_result *a, int32_t col) { return ArrowFixed(a, col, 4, false); }  // ref :2359
+moonbit_bytes_t duckdb_mb_arrow_get_column_int32(duckdb_mb_arrow_result *a, int32_t col) {  // ref :2359
+  if (moonbit_bytes_t d = ArrowDirectBuffer(a, col, T_INTEGER, P_I32, 4)) return d;
+  return ArrowFixed(a, col, 4, false);
+}
 moonbit_bytes_t duckdb_mb_arrow_get_column_int64(duckdb_mb_arrow_result *a, int32_t col) {  // ref :2392
   if (!ArrowOk(a, col)) return MakeBytes("", 0);
   int64_t n = a->row_count;
   if (4 + n * 8 > INT32_MAX) return MakeBytes("", 0);
+  if (moonbit_bytes_t d = ArrowDirectBuffer(a, col, T_BIGINT, P_I64, 8)) return d;
   moonbit_bytes_t out = moonbit_make_bytes_raw((int32_t)(4 + n * 8));
   int32_t cnt = (int32_t)n;
   memcpy(out, &cnt, 4);
-  const HostColumn &c = a->r->cols[col];
+  const HostColumn &c = ArrowHost(a).cols[col];
   if (c.phys == P_I64 && c.type.id == T_BIGINT) {
     // fast path: the D2H'd column already is the wire layout
     memcpy(out + 4, c.data.data(), (size_t)n * 8);
@@ -883,7 +944,10 @@ moonbit_bytes_t duckdb_mb_arrow_get_column_int64(duckdb_mb_arrow_result *a, int3
   }
   return out;
 }
-moonbit_bytes_t duckdb_mb_arrow_get_column_double(duckdb_mb_arrow_result *a, int32_t col) { return ArrowF64(a, col, false); }  // ref :2424
+moonbit_bytes_t duckdb_mb_arrow_get_column_double(duckdb_mb_arrow_result *a, int32_t col) {  // ref :2424
+  if (moonbit_bytes_t d = ArrowDirectBuffer(a, col, T_DOUBLE, P_F64, 8)) return d;
+  return ArrowF64(a, col, false);
+}
 moonbit_bytes_t duckdb_mb_arrow_get_column_string(duckdb_mb_arrow_result *a, int32_t col) { return ArrowStr(a, col, false); }  // ref :2456
 moonbit_bytes_t duckdb_mb_arrow_get_column_bool(duckdb_mb_arrow_result *a, int32_t col) { return ArrowFixed(a, col, 1, false); }  // ref :2516
 moonbit_bytes_t duckdb_mb_arrow_get_column_int32_nullable(duckdb_mb_arrow_result *a, int32_t col) { return ArrowFixed(a, col, 4, true); }  // ref :2572
@@ -894,7 +958,7 @@ moonbit_bytes_t duckdb_mb_arrow_get_column_int64_nullable(duckdb_mb_arrow_result
   moonbit_bytes_t out = moonbit_make_bytes_raw((int32_t)(4 + n * 9));
   int32_t cnt = (int32_t)n;
   memcpy(out, &cnt, 4);
-  const HostColumn &c = a->r->cols[col];
+  const HostColumn &c = ArrowHost(a).cols[col];
   for (int64_t i = 0; i < n; i++) {
     bool null = c.IsNull(i);
     int64_t x = null ? 0 : CellI64(c, i);
