@@ -217,11 +217,22 @@ __device__ __forceinline__ double f64_unorder(uint64_t k) {
 // ---------------------------------------------------------------------------
 // expression VM (tile interpreter)
 // ---------------------------------------------------------------------------
+// VM register planes [reg][row] in dynamic LDS sized to the program's
+// register count (P.n_regs), not VM_MAX_REGS: short programs leave room for
+// more resident workgroups, i.e. more row loads in flight per CU.
 struct VmLds {
-  int64_t lo[VM_MAX_REGS][VM_TILE];
-  int64_t hi[VM_MAX_REGS][VM_TILE];
-  uint8_t nl[VM_MAX_REGS][VM_TILE];
+  int64_t *lo;
+  int64_t *hi;
+  uint8_t *nl;
 };
+__device__ __forceinline__ VmLds vm_regs(unsigned char *base, int n_regs) {
+  VmLds R;
+  R.lo = (int64_t *)base;
+  R.hi = R.lo + (size_t)n_regs * VM_TILE;
+  R.nl = (uint8_t *)(R.hi + (size_t)n_regs * VM_TILE);
+  return R;
+}
+static size_t VmLdsBytes(int n_regs) { return (size_t)(n_regs < 1 ? 1 : n_regs) * VM_TILE * 17; }
 
 __device__ __forceinline__ bool cmp_res(int c, int k) {
   // c = -1/0/1 comparison, k = cmp kind
@@ -236,7 +247,7 @@ __device__ __forceinline__ bool cmp_res(int c, int k) {
 }
 
 __device__ void vm_exec(const VmProgram &P, const VmCols &C, int64_t row, bool active, int64_t rs, int64_t rstep,
-                        VmLds &R, int t, int32_t *err) {
+                        const VmLds &R, int t, int32_t *err) {
   for (int k = 0; k < P.n_ins; k++) {
     const VmIns I = P.ins[k];
     const int d = I.dst, a = I.a, b = I.b, c = I.c;
@@ -255,52 +266,52 @@ __device__ void vm_exec(const VmProgram &P, const VmCols &C, int64_t row, bool a
       }
       case V_LOADRANGE: lo = rs + row * rstep; hi = lo >> 63; break;
       case V_CONST: lo = P.consts[a].lo; hi = P.consts[a].hi; nl = (uint8_t)P.consts[a].isnull; break;
-      case V_MOV: lo = R.lo[a][t]; hi = R.hi[a][t]; nl = R.nl[a][t]; break;
+      case V_MOV: lo = R.lo[(a) * VM_TILE + t]; hi = R.hi[(a) * VM_TILE + t]; nl = R.nl[(a) * VM_TILE + t]; break;
       case V_SELECT: {
-        bool cond = !R.nl[a][t] && R.lo[a][t] != 0;
+        bool cond = !R.nl[(a) * VM_TILE + t] && R.lo[(a) * VM_TILE + t] != 0;
         int s = cond ? b : c;
-        lo = R.lo[s][t]; hi = R.hi[s][t]; nl = R.nl[s][t];
+        lo = R.lo[(s) * VM_TILE + t]; hi = R.hi[(s) * VM_TILE + t]; nl = R.nl[(s) * VM_TILE + t];
         break;
       }
       case V_COALESCE: {
-        int s = R.nl[a][t] ? b : a;
-        lo = R.lo[s][t]; hi = R.hi[s][t]; nl = R.nl[s][t];
+        int s = R.nl[(a) * VM_TILE + t] ? b : a;
+        lo = R.lo[(s) * VM_TILE + t]; hi = R.hi[(s) * VM_TILE + t]; nl = R.nl[(s) * VM_TILE + t];
         break;
       }
       case V_AND: {
-        bool an = R.nl[a][t], bn = R.nl[b][t];
-        bool av = R.lo[a][t] != 0, bv = R.lo[b][t] != 0;
+        bool an = R.nl[(a) * VM_TILE + t], bn = R.nl[(b) * VM_TILE + t];
+        bool av = R.lo[(a) * VM_TILE + t] != 0, bv = R.lo[(b) * VM_TILE + t] != 0;
         if ((!an && !av) || (!bn && !bv)) { lo = 0; nl = 0; }
         else if (an || bn) { nl = 1; }
         else { lo = 1; }
         break;
       }
       case V_OR: {
-        bool an = R.nl[a][t], bn = R.nl[b][t];
-        bool av = R.lo[a][t] != 0, bv = R.lo[b][t] != 0;
+        bool an = R.nl[(a) * VM_TILE + t], bn = R.nl[(b) * VM_TILE + t];
+        bool av = R.lo[(a) * VM_TILE + t] != 0, bv = R.lo[(b) * VM_TILE + t] != 0;
         if ((!an && av) || (!bn && bv)) { lo = 1; nl = 0; }
         else if (an || bn) { nl = 1; }
         else { lo = 0; }
         break;
       }
-      case V_ISNULL: lo = R.nl[a][t] ? 1 : 0; break;
-      case V_ISNOTNULL: lo = R.nl[a][t] ? 0 : 1; break;
+      case V_ISNULL: lo = R.nl[(a) * VM_TILE + t] ? 1 : 0; break;
+      case V_ISNOTNULL: lo = R.nl[(a) * VM_TILE + t] ? 0 : 1; break;
       case V_DISTINCT_I: case V_DISTINCT_L: case V_DISTINCT_F: {
-        bool an = R.nl[a][t], bn = R.nl[b][t];
+        bool an = R.nl[(a) * VM_TILE + t], bn = R.nl[(b) * VM_TILE + t];
         bool same;
         if (an || bn) same = an && bn;
         else if (I.op == V_DISTINCT_F) {
-          double x = __longlong_as_double(R.lo[a][t]), y = __longlong_as_double(R.lo[b][t]);
+          double x = __longlong_as_double(R.lo[(a) * VM_TILE + t]), y = __longlong_as_double(R.lo[(b) * VM_TILE + t]);
           same = (x == y) || (x != x && y != y);
-        } else same = R.lo[a][t] == R.lo[b][t] && R.hi[a][t] == R.hi[b][t];
+        } else same = R.lo[(a) * VM_TILE + t] == R.lo[(b) * VM_TILE + t] && R.hi[(a) * VM_TILE + t] == R.hi[(b) * VM_TILE + t];
         lo = I.aux ? same : !same;
         break;
       }
       case V_SYNTH: {
-        nl = R.nl[a][t] | R.nl[b][t] | R.nl[c][t];
-        uint64_t m = (uint64_t)R.lo[c][t];
+        nl = R.nl[(a) * VM_TILE + t] | R.nl[(b) * VM_TILE + t] | R.nl[(c) * VM_TILE + t];
+        uint64_t m = (uint64_t)R.lo[(c) * VM_TILE + t];
         if (!nl && m) {
-          lo = (int64_t)(splitmix64((uint64_t)R.lo[a][t] + (uint64_t)R.lo[b][t]) % m);
+          lo = (int64_t)(splitmix64((uint64_t)R.lo[(a) * VM_TILE + t] + (uint64_t)R.lo[(b) * VM_TILE + t]) % m);
         } else {
           nl = 1;
         }
@@ -308,16 +319,16 @@ __device__ void vm_exec(const VmProgram &P, const VmCols &C, int64_t row, bool a
       }
       default: {
         // null-propagating unary/binary ops
-        nl = R.nl[a][t];
+        nl = R.nl[(a) * VM_TILE + t];
         if (I.op >= V_ADD_I && I.op != V_NOT && I.op != V_I2L && I.op != V_U2L && I.op != V_L2I && I.op != V_I2F &&
             I.op != V_L2F && I.op != V_F2I && I.op != V_F2L && I.op != V_CHECK_I && I.op != V_CHECK_L &&
             I.op != V_SCALEUP_I && I.op != V_SCALEUP_L && I.op != V_SCALEDN_I && I.op != V_SCALEDN_L &&
             I.op != V_DEC2F_I && I.op != V_DEC2F_L && I.op != V_F2DEC_I && I.op != V_F2DEC_L &&
             I.op != V_TOBOOL_I && I.op != V_TOBOOL_F && I.op != V_NEG_I && I.op != V_NEG_L && I.op != V_NEG_F &&
             I.op != V_ABS_I && I.op != V_ABS_L && I.op != V_ABS_F)
-          nl |= R.nl[b][t];
-        const int64_t xa = R.lo[a][t], xah = R.hi[a][t];
-        const int64_t xb = R.lo[b][t], xbh = R.hi[b][t];
+          nl |= R.nl[(b) * VM_TILE + t];
+        const int64_t xa = R.lo[(a) * VM_TILE + t], xah = R.hi[(a) * VM_TILE + t];
+        const int64_t xb = R.lo[(b) * VM_TILE + t], xbh = R.hi[(b) * VM_TILE + t];
         bool ok = active && !nl;
         switch (I.op) {
           case V_ADD_I: if (__builtin_add_overflow(xa, xb, &lo) && ok) raise_err(err, E_OVF_ADD); break;
@@ -467,16 +478,17 @@ __device__ void vm_exec(const VmProgram &P, const VmCols &C, int64_t row, bool a
         break;
       }
     }
-    R.lo[d][t] = lo;
-    R.hi[d][t] = hi;
-    R.nl[d][t] = nl;
+    R.lo[(d) * VM_TILE + t] = lo;
+    R.hi[(d) * VM_TILE + t] = hi;
+    R.nl[(d) * VM_TILE + t] = nl;
   }
 }
 
 __global__ __launch_bounds__(256) void vm_filter_kernel(VmProgram P, VmCols C, int64_t nrows, int64_t rs,
                                                         int64_t rstep, uint64_t *__restrict__ bits,
                                                         uint32_t *__restrict__ tile_counts, int32_t *err) {
-  __shared__ VmLds R;
+  extern __shared__ __attribute__((aligned(16))) unsigned char vm_lds[];
+  VmLds R = vm_regs(vm_lds, P.n_regs);
   __shared__ uint32_t wcnt[4];
   const int t = threadIdx.x, lane = t & 63, w = t >> 6;
   const int64_t ntiles = (nrows + VM_TILE - 1) / VM_TILE;
@@ -485,7 +497,7 @@ __global__ __launch_bounds__(256) void vm_filter_kernel(VmProgram P, VmCols C, i
     bool active = row < nrows;
     vm_exec(P, C, row, active, rs, rstep, R, t, err);
     const int pr = P.pred_reg;
-    bool sel = active && !R.nl[pr][t] && R.lo[pr][t] != 0;
+    bool sel = active && !R.nl[(pr) * VM_TILE + t] && R.lo[(pr) * VM_TILE + t] != 0;
     uint64_t m = __ballot(sel);
     if (lane == 0) {
       bits[tile * 4 + w] = m;
@@ -501,7 +513,8 @@ __global__ __launch_bounds__(256) void vm_project_kernel(VmProgram P, VmCols C, 
                                                          int64_t rstep, const uint64_t *__restrict__ bits,
                                                          const int64_t *__restrict__ tile_off, VmOuts O,
                                                          int32_t *err) {
-  __shared__ VmLds R;
+  extern __shared__ __attribute__((aligned(16))) unsigned char vm_lds[];
+  VmLds R = vm_regs(vm_lds, P.n_regs);
   const int t = threadIdx.x, lane = t & 63, w = t >> 6;
   const int64_t ntiles = (nrows + VM_TILE - 1) / VM_TILE;
   for (int64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
@@ -525,8 +538,8 @@ __global__ __launch_bounds__(256) void vm_project_kernel(VmProgram P, VmCols C, 
     if (sel) {
       for (int o = 0; o < P.n_out; o++) {
         const int r = P.out_reg[o];
-        store_phys(O.data[o], P.out_phys[o], out_idx, R.lo[r][t], R.hi[r][t]);
-        if (R.nl[r][t] && O.nullbits[o]) {
+        store_phys(O.data[o], P.out_phys[o], out_idx, R.lo[(r) * VM_TILE + t], R.hi[(r) * VM_TILE + t]);
+        if (R.nl[(r) * VM_TILE + t] && O.nullbits[o]) {
           atomicOr(&O.nullbits[o][out_idx >> 5], 1u << (out_idx & 31));
           if (O.anynull) O.anynull[o] = 1;
         }
@@ -540,7 +553,8 @@ void VmFilter(const VmProgram &p, const VmCols &cols, int64_t nrows, int64_t ran
   if (nrows <= 0) return;
   int64_t ntiles = (nrows + VM_TILE - 1) / VM_TILE;
   int grid = GridFor(ntiles, 1, NumCUs() * 8);
-  hipLaunchKernelGGL(vm_filter_kernel, dim3(grid), dim3(256), 0, s, p, cols, nrows, range_start, range_step, sel_bits,
+  hipLaunchKernelGGL(vm_filter_kernel, dim3(grid), dim3(256), VmLdsBytes(p.n_regs), s, p, cols, nrows, range_start,
+                     range_step, sel_bits,
                      tile_counts, err);
   CHECK_LAUNCH();
 }
@@ -551,7 +565,8 @@ void VmProject(const VmProgram &p, const VmCols &cols, int64_t nrows, int64_t ra
   if (nrows <= 0) return;
   int64_t ntiles = (nrows + VM_TILE - 1) / VM_TILE;
   int grid = GridFor(ntiles, 1, NumCUs() * 8);
-  hipLaunchKernelGGL(vm_project_kernel, dim3(grid), dim3(256), 0, s, p, cols, nrows, range_start, range_step,
+  hipLaunchKernelGGL(vm_project_kernel, dim3(grid), dim3(256), VmLdsBytes(p.n_regs), s, p, cols, nrows, range_start,
+                     range_step,
                      sel_bits, tile_offsets, outs, err);
   CHECK_LAUNCH();
 }
@@ -1046,9 +1061,9 @@ static FaVariant FaConfig(int mode) {
   return v;
 }
 
-static bool g_fa_pairs = true;
-static bool g_fa_mm = true, g_fa_narrow = false;  // per launch, set by FilterAggStates
-static AggPartial *g_fa_partials = nullptr;
+static thread_local bool g_fa_pairs = true;
+static thread_local bool g_fa_mm = true, g_fa_narrow = false;  // per launch, set by FilterAggStates
+static thread_local AggPartial *g_fa_partials = nullptr;
 template <typename TP, typename TA, int MODE, int U, bool NT, bool CH>
 static void LaunchFA(const void *p, const void *a, int64_t n, int64_t lo, uint64_t span, AggState *st,
                      unsigned long long *cstar, int grid, hipStream_t s) {

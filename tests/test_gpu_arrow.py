@@ -85,3 +85,33 @@ def test_arrow_wire_bytes_exact(conn, mbx):
     assert mbx._take(lib.duckdb_mb_arrow_get_column_int32(a._h, 1)) == wire.int32(B)
     # bad column index / arrow of strings as numbers -> defined empties / zeros
     assert mbx._take(lib.duckdb_mb_arrow_get_column_int64(a._h, 9)) == b""
+
+
+def test_arrow_nullable_string_double_bool(conn, mbx):
+    # duckdb_arrow_test.mbt:428-518
+    a = arrow(conn, mbx, "SELECT 'a' UNION ALL SELECT NULL UNION ALL SELECT 'c' UNION ALL SELECT NULL UNION ALL SELECT 'e'")
+    vals, valid = a.get_column_string_nullable(0)
+    assert valid == [True, False, True, False, True] and len(vals) == 5 and vals[0] == "a" and vals[2] == "c"
+    a = arrow(conn, mbx, "SELECT 1.5::DOUBLE UNION ALL SELECT NULL::DOUBLE UNION ALL SELECT 3.14::DOUBLE")
+    vals, valid = a.get_column_double_nullable(0)
+    assert valid == [True, False, True] and vals[0] == 1.5 and vals[2] == 3.14
+    a = arrow(conn, mbx, "SELECT true::BOOLEAN UNION ALL SELECT NULL::BOOLEAN UNION ALL SELECT false::BOOLEAN")
+    vals, valid = a.get_column_bool_nullable(0)
+    assert valid == [True, False, True] and vals[0] is True and vals[2] is False
+
+
+def test_arrow_device_columns_direct_and_materialized(conn, mbx):
+    # device-resident results: plain columns take the direct-DMA getters, columns with
+    # NULLs / other types the per-cell path; both must give the reference's buffers
+    q = conn.query
+    assert isinstance(q("CREATE TABLE ad AS SELECT CAST(i AS INTEGER) AS a, i * 3 AS b, CAST(i AS DOUBLE) / 4 AS d, "
+                        "CASE WHEN i % 3 = 0 THEN NULL ELSE i END AS n FROM range(5000) tbl(i)"), mbx.Ok)
+    a = arrow(conn, mbx, "SELECT a, b, d, n FROM ad")
+    assert a.get_column_int32(0) == list(range(5000))
+    assert a.get_column_int64(1) == [3 * i for i in range(5000)]
+    assert a.get_column_double(2) == [i / 4 for i in range(5000)]
+    vals, valid = a.get_column_int64_nullable(3)
+    assert valid == [i % 3 != 0 for i in range(5000)]
+    assert [v for v, ok in zip(vals, valid) if ok] == [i for i in range(5000) if i % 3]
+    # int32 getter over BIGINT truncates like the reference's (int32_t) cast (duckdb_native.c:2384-2385)
+    assert a.get_column_int32(1)[:3] == [0, 3, 6]
