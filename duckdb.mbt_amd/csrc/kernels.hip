@@ -1837,10 +1837,42 @@ __global__ __launch_bounds__(1024) void compact_slots_kernel(const unsigned long
   if (threadIdx.x == 0) *n_out = base;
 }
 
+__global__ void slot_flags_kernel(const unsigned long long *count_star, int64_t nslots, int32_t *flag) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < nslots; i += (int64_t)gridDim.x * blockDim.x)
+    flag[i] = count_star[i] > 0;
+}
+
+__global__ void slot_scatter_kernel(const int32_t *flag, const int32_t *pos, int64_t nslots, int32_t *slot_list,
+                                    int64_t *n_out) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < nslots; i += (int64_t)gridDim.x * blockDim.x) {
+    if (flag[i]) slot_list[pos[i]] = (int32_t)i;
+    if (i == nslots - 1) *n_out = (int64_t)pos[i] + flag[i];
+  }
+}
+
+// Ordered list of the non-empty slots.  One workgroup for small tables; a
+// device-wide scan (flags -> hipCUB exclusive sum -> scatter) for large ones.
 void CompactSlots(const unsigned long long *count_star, int64_t nslots, int32_t *slot_list, int64_t *n_out,
                   hipStream_t s) {
-  hipLaunchKernelGGL(compact_slots_kernel, dim3(1), dim3(1024), 0, s, count_star, nslots, slot_list, n_out);
+  if (nslots <= (1 << 16)) {
+    hipLaunchKernelGGL(compact_slots_kernel, dim3(1), dim3(1024), 0, s, count_star, nslots, slot_list, n_out);
+    CHECK_LAUNCH();
+    return;
+  }
+  int32_t *flag = (int32_t *)TempAlloc((size_t)nslots * 4);
+  int32_t *pos = (int32_t *)TempAlloc((size_t)nslots * 4);
+  const int grid = GridFor(nslots, 256 * 4, NumCUs() * 8);
+  hipLaunchKernelGGL(slot_flags_kernel, dim3(grid), dim3(256), 0, s, count_star, nslots, flag);
   CHECK_LAUNCH();
+  size_t tmp = 0;
+  (void)hipcub::DeviceScan::ExclusiveSum(nullptr, tmp, flag, pos, (int)nslots, s);
+  void *d_tmp = TempAlloc(tmp ? tmp : 16);
+  (void)hipcub::DeviceScan::ExclusiveSum(d_tmp, tmp, flag, pos, (int)nslots, s);
+  hipLaunchKernelGGL(slot_scatter_kernel, dim3(grid), dim3(256), 0, s, flag, pos, nslots, slot_list, n_out);
+  CHECK_LAUNCH();
+  TempFree(d_tmp, tmp ? tmp : 16);
+  TempFree(pos, (size_t)nslots * 4);
+  TempFree(flag, (size_t)nslots * 4);
 }
 
 // ---------------------------------------------------------------------------

@@ -445,3 +445,16 @@ def test_stream_device_batches(conn):
     second = s2.next().value
     assert int(first.rows[0][0]) == 0 and int(second.rows[0][0]) == 2048
     s2.close()
+
+
+def test_groupby_direct_wide_slot_table(conn):
+    # 100 000-slot direct-index table (> one workgroup's compaction): device-wide slot scan
+    n = 300_007
+    q(conn, f"CREATE TABLE ws AS SELECT i % 100000 AS k, i AS v FROM range({n}) tbl(i)")
+    res = q(conn, "SELECT k, COUNT(*), SUM(v) FROM ws WHERE v % 7 <> 3 GROUP BY k ORDER BY k")
+    exp = {}
+    for i in range(n):
+        if i % 7 != 3:
+            c, s = exp.get(i % 100000, (0, 0))
+            exp[i % 100000] = (c + 1, s + i)
+    assert res.rows == [[str(k), str(c), str(s)] for k, (c, s) in sorted(exp.items())]
