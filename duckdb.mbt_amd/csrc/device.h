@@ -68,6 +68,28 @@ struct AggPartial {
 // needed.  Otherwise (or for shapes the LDS kernel does not take) it zeroes
 // st/cstar itself, accumulates with atomics and returns 0.
 constexpr int kMaxAggPartials = 4096;
+
+// Fused filter-aggregate over several columns: a conjunction of range
+// predicates on up to 4 int32/int64 columns (no NULLs) and at most one
+// aggregated column (which may also carry a predicate).  Always writes
+// per-workgroup partials (returns their count, > 0).
+#define FM_MAX 4
+struct FilterMultiCol {
+  const void *data;
+  int32_t phys;     // P_I32 / P_I64
+  int32_t is_pred;  // 1: lo <= x <= lo + span
+  int64_t lo;
+  uint64_t span;
+};
+struct FilterMultiDesc {
+  int32_t ncol;
+  int32_t agg;  // index into col[] of the aggregated column, -1: COUNT only
+  int32_t mm;
+  int32_t narrow;   // set by FilterMultiPartials from maxabs and its grid
+  uint64_t maxabs;  // zone-map bound on |aggregated value|, ~0 = unknown
+  FilterMultiCol col[FM_MAX];
+};
+int FilterMultiPartials(const FilterMultiDesc &d, int64_t nrows, AggPartial *partials, hipStream_t s);
 int FilterAggStates(const void *pcol, int pphys, int64_t lo, int64_t hi, bool has_pred, const void *acol, int aphys,
                     int64_t nrows, AggState *st, unsigned long long *cstar, int grid_blocks, hipStream_t s,
                     bool need_minmax = true, uint64_t sum_maxabs = ~0ull, AggPartial *partials = nullptr);

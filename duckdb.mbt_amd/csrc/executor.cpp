@@ -937,6 +937,23 @@ static bool RangePredicate(const BExpr &p, int *col, i128 *lo, i128 *hi) {
   return true;
 }
 
+// Conjunction of range predicates over several integer columns: per column
+// lo <= col <= hi (inclusive).  false if any leaf is not such a comparison.
+static bool RangeConj(const BExpr &p, std::map<int, std::pair<i128, i128>> &ranges) {
+  if (p.kind == BExpr::FUNC && p.op == B_AND) return RangeConj(*p.ch[0], ranges) && RangeConj(*p.ch[1], ranges);
+  int col = -1;
+  i128 lo = (i128)INT64_MIN, hi = (i128)INT64_MAX;
+  if (!RangePredicate(p, &col, &lo, &hi) || col < 0) return false;
+  auto it = ranges.find(col);
+  if (it == ranges.end()) {
+    ranges[col] = {lo, hi};
+  } else {
+    it->second.first = std::max(it->second.first, lo);
+    it->second.second = std::min(it->second.second, hi);
+  }
+  return true;
+}
+
 static bool FastIntCol(const DRel &rel, int c) {
   if (rel.range && c == 0) return false;
   const DCol &d = rel.cols[c];
@@ -1167,6 +1184,93 @@ static DRel HashAggregate(Engine &e, const DRel &tmp, const BoundSelect &s, cons
   return out;
 }
 
+// F1m: no GROUP BY, a conjunction of range predicates over >= 2 int columns
+// (or one predicate column of another width than the aggregated column),
+// aggregates over one int column or COUNT(*): one LDS-DMA pass over all the
+// columns (filter_multi_lds).  The single-column shape stays on F1.
+static bool FilterMultiAggregate(Engine &e, const DRel &src, const BoundSelect &s, DRel &out) {
+  if (!s.where || src.n <= 0) return false;
+  std::map<int, std::pair<i128, i128>> ranges;
+  if (!RangeConj(*s.where, ranges)) return false;
+  int acol = -1;
+  bool need_mm = false;
+  for (auto &a : s.aggs) {
+    if (a.kind == A_COUNT_STAR) continue;
+    if (a.distinct) return false;
+    const BExpr *x = a.arg ? StripWidening(a.arg.get()) : nullptr;
+    if (!x || x->kind != BExpr::COL || !FastIntCol(src, x->col)) return false;
+    if (a.arg->type.id == T_DOUBLE || a.arg->type.id == T_FLOAT) return false;
+    if (acol >= 0 && acol != x->col) return false;
+    acol = x->col;
+    need_mm |= a.kind == A_MIN || a.kind == A_MAX;
+  }
+  for (auto &kv : ranges)
+    if (!FastIntCol(src, kv.first)) return false;
+  const bool single = ranges.size() == 1 && (acol < 0 || acol == ranges.begin()->first ||
+                                             src.cols[acol].phys == src.cols[ranges.begin()->first].phys);
+  if (single) return false;  // F1 proper
+  dev::FilterMultiDesc d;
+  memset(&d, 0, sizeof(d));
+  d.agg = -1;
+  double bytes = 0;
+  for (auto &kv : ranges) {
+    if (d.ncol == FM_MAX) return false;
+    i128 lo = std::max<i128>(kv.second.first, INT64_MIN), hi = std::min<i128>(kv.second.second, INT64_MAX);
+    dev::FilterMultiCol &c = d.col[d.ncol];
+    c.data = src.cols[kv.first].data;
+    c.phys = src.cols[kv.first].phys;
+    c.is_pred = 1;
+    if (lo > hi) return false;  // an empty range: the generic path answers it
+    c.lo = (int64_t)lo;
+    c.span = (uint64_t)(int64_t)hi - (uint64_t)(int64_t)lo;
+    if (kv.first == acol) d.agg = d.ncol;
+    bytes += (double)src.n * PhysSize(src.cols[kv.first].phys);
+    d.ncol++;
+  }
+  if (acol >= 0 && d.agg < 0) {
+    if (d.ncol == FM_MAX) return false;
+    dev::FilterMultiCol &c = d.col[d.ncol];
+    c.data = src.cols[acol].data;
+    c.phys = src.cols[acol].phys;
+    c.is_pred = 0;
+    d.agg = d.ncol++;
+    bytes += (double)src.n * PhysSize(src.cols[acol].phys);
+  }
+  d.mm = need_mm;
+  uint64_t maxabs = ~0ull;
+  if (acol >= 0 && src.cols[acol].table_col && src.cols[acol].table_col->stats_valid) {
+    const DevColumn *tc = src.cols[acol].table_col;
+    i128 m1 = tc->imin < 0 ? -tc->imin : tc->imin, m2 = tc->imax < 0 ? -tc->imax : tc->imax;
+    i128 m = m1 > m2 ? m1 : m2;
+    if (m <= (i128)INT64_MAX) maxabs = (uint64_t)m;
+  }
+  d.maxabs = maxabs;  // FilterMultiPartials decides the int64-partial (narrow) mode from it
+  const int na = (int)s.aggs.size();
+  dev::AggState *st = (dev::AggState *)e.d_small;
+  unsigned long long *cstar = (unsigned long long *)((char *)e.d_small + 1024);
+  int npartials;
+  {
+    ProfScope ps(e, "filter_multi", bytes, src.n);
+    npartials = dev::FilterMultiPartials(d, src.n, e.d_partials, e.stream);
+  }
+  out.n = 1;
+  dev::EmitDesc D;
+  memset(&D, 0, sizeof(D));
+  D.nagg = na;
+  D.cstar = cstar;
+  D.nslots = 1;
+  D.null_slot = -1;
+  D.partials = e.d_partials;
+  D.npartials = npartials;
+  for (int j = 0; j < na; j++) {
+    DCol oc = AllocOut(e, s.aggs[j].type, 1, true, false);
+    D.a[j] = EmitFor(s.aggs[j], VC_I64, s.aggs[j].kind == A_COUNT_STAR ? nullptr : st, oc);
+    out.cols.push_back(oc);
+  }
+  dev::EmitAggRelation(D, e.stream);
+  return true;
+}
+
 static DRel Aggregate(Engine &e, const DRel &src, const BoundSelect &s) {
   const int ng = (int)s.groups.size();
   const int na = (int)s.aggs.size();
@@ -1175,6 +1279,8 @@ static DRel Aggregate(Engine &e, const DRel &src, const BoundSelect &s) {
   // ---- fast path F1: no GROUP BY, range predicate on one int column, all
   //      aggregates over one int column (or COUNT(*)).
   if (ng == 0 && !src.range) {
+    DRel multi_out;
+    if (FilterMultiAggregate(e, src, s, multi_out)) return multi_out;
     int pcol = -1;
     i128 lo = (i128)INT64_MIN, hi = (i128)INT64_MAX;
     bool pred_ok = !s.where || RangePredicate(*s.where, &pcol, &lo, &hi);

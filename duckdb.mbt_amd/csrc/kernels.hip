@@ -985,6 +985,148 @@ __global__ __launch_bounds__(256) void filter_agg_lds_kernel(const T *__restrict
   }
 }
 
+// Multi-column version of the LDS-DMA filter-aggregate.  A wave step covers
+// 256 consecutive rows; each column's slice (1 KiB for int32, 2 KiB for
+// int64) lands in the wave's ring slot through global_load_lds, NLD KiB per
+// step in total (compile-time, so the counted vmcnt wait is exact); each lane
+// then owns 4 consecutive rows of every column.
+template <int NLD, int DEPTH>
+__global__ __launch_bounds__(256) void filter_multi_lds_kernel(FilterMultiDesc D, int64_t n, AggPartial *partials) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char fm_lds[];
+  constexpr int SB = NLD * 1024;
+  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  unsigned char *ring = fm_lds + (size_t)w * DEPTH * SB;
+  int off[FM_MAX];
+  {
+    int o = 0;
+#pragma unroll
+    for (int c = 0; c < FM_MAX; c++) {
+      off[c] = o;
+      if (c < D.ncol) o += D.col[c].phys == P_I64 ? 2048 : 1024;
+    }
+  }
+  const int64_t nsteps = n >> 8;
+  const int64_t nw = (int64_t)gridDim.x * 4;
+  int64_t st = (int64_t)blockIdx.x * 4 + w;
+  auto issue = [&](int64_t q, int d) {
+    unsigned char *dst = ring + d * SB;
+#pragma unroll
+    for (int c = 0; c < FM_MAX; c++) {
+      if (c >= D.ncol) break;
+      const int B = D.col[c].phys == P_I64 ? 2048 : 1024;
+      const unsigned char *src = (const unsigned char *)D.col[c].data + q * B;
+      __builtin_amdgcn_global_load_lds((const void *)(src + lane * 16), (void *)(dst + off[c]), 16, 0, 2);
+      if (B == 2048)
+        __builtin_amdgcn_global_load_lds((const void *)(src + 1024 + lane * 16), (void *)(dst + off[c] + 1024), 16, 0, 2);
+    }
+  };
+  Acc A;
+  A.cnt = 0; A.slo = 0; A.shi = 0; A.mn = INT64_MAX; A.mx = INT64_MIN;
+  const bool mm = D.mm, narrow = D.narrow;
+  if (nsteps > 0) {
+#pragma unroll
+    for (int d = 0; d < DEPTH; d++) {
+      int64_t q = st + d * nw;
+      issue(q < nsteps ? q : 0, d);
+    }
+  }
+  int k = 0;
+  for (; st < nsteps; st += nw) {
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NLD * (DEPTH - 1)) : "memory");
+    const unsigned char *src = ring + k * SB;
+    int64_t v[FM_MAX][4];
+#pragma unroll
+    for (int c = 0; c < FM_MAX; c++) {
+      if (c >= D.ncol) break;
+      if (D.col[c].phys == P_I64) {
+        v2i64 x0 = *(const v2i64 *)(src + off[c] + lane * 32), x1 = *(const v2i64 *)(src + off[c] + lane * 32 + 16);
+        v[c][0] = x0.x; v[c][1] = x0.y; v[c][2] = x1.x; v[c][3] = x1.y;
+      } else {
+        v4i32 x = *(const v4i32 *)(src + off[c] + lane * 16);
+        v[c][0] = x.x; v[c][1] = x.y; v[c][2] = x.z; v[c][3] = x.w;
+      }
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    int64_t q = st + DEPTH * nw;
+    issue(q < nsteps ? q : st, k);
+#pragma unroll
+    for (int e = 0; e < 4; e++) {
+      bool ok = true;
+#pragma unroll
+      for (int c = 0; c < FM_MAX; c++)
+        if (c < D.ncol && D.col[c].is_pred) ok = ok && (uint64_t)(v[c][e] - D.col[c].lo) <= D.col[c].span;
+      int64_t val = 0;
+#pragma unroll
+      for (int c = 0; c < FM_MAX; c++)
+        if (c == D.agg) val = v[c][e];
+      if (D.agg < 0) acc_count(A, ok);
+      else acc_row(A, ok, val, mm, narrow);
+    }
+    k = k + 1 == DEPTH ? 0 : k + 1;
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  if (blockIdx.x == 0 && w == 0) {
+    for (int64_t i = (nsteps << 8) + lane; i < n; i += 64) {
+      bool ok = true;
+      int64_t val = 0;
+      for (int c = 0; c < D.ncol; c++) {
+        int64_t x = D.col[c].phys == P_I64 ? ((const int64_t *)D.col[c].data)[i] : (int64_t)((const int32_t *)D.col[c].data)[i];
+        if (D.col[c].is_pred) ok = ok && (uint64_t)(x - D.col[c].lo) <= D.col[c].span;
+        if (c == D.agg) val = x;
+      }
+      if (D.agg < 0) acc_count(A, ok);
+      else acc_row(A, ok, val, mm, narrow);
+    }
+  }
+  if (narrow) A.shi = (int64_t)A.slo >> 63;
+  acc_wave_reduce(A);
+  __syncthreads();
+  Acc *part = (Acc *)fm_lds;
+  if (lane == 0) part[w] = A;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    Acc T0 = part[0];
+    for (int i = 1; i < 4; i++) acc_merge(T0, part[i]);
+    partials[blockIdx.x] = AggPartial{T0.cnt, T0.slo, T0.shi, T0.mn, T0.mx};
+  }
+}
+
+int FilterMultiPartials(const FilterMultiDesc &d_in, int64_t nrows, AggPartial *partials, hipStream_t s) {
+  FilterMultiDesc d = d_in;
+  int nld = 0;
+  for (int c = 0; c < d.ncol; c++) nld += d.col[c].phys == P_I64 ? 2 : 1;
+  int gpc = 2;
+  const char *e = getenv("MBX_FM_BLOCKS_PER_CU");
+  if (e && *e) gpc = atoi(e);
+  int grid = NumCUs() * (gpc > 0 ? gpc : 2);
+  int64_t need = (nrows >> 8) / 4 + 1;
+  if (grid > need) grid = (int)need;
+  if (grid > kMaxAggPartials) grid = kMaxAggPartials;
+  {
+    // a lane sees at most (ceil(steps / waves) + 1) x 4 rows, tail included
+    const int64_t waves = (int64_t)grid * 4, steps = nrows >> 8;
+    const unsigned __int128 rows_per_lane = (unsigned __int128)(((steps + waves - 1) / waves + 1) * 4);
+    d.narrow = d.maxabs <= (uint64_t)INT64_MAX &&
+               (unsigned __int128)d.maxabs * rows_per_lane < ((unsigned __int128)1 << 63);
+  }
+#define FM(L, DP)                                                                                            \
+  hipLaunchKernelGGL((filter_multi_lds_kernel<L, DP>), dim3(grid), dim3(256), (size_t)4 * DP * L * 1024, s, d, nrows, \
+                     partials)
+  switch (nld) {
+    case 1: FM(1, 6); break;
+    case 2: FM(2, 3); break;
+    case 3: FM(3, 2); break;
+    case 4: FM(4, 2); break;
+    case 5: FM(5, 2); break;
+    case 6: FM(6, 2); break;
+    case 7: FM(7, 2); break;
+    default: FM(8, 2); break;
+  }
+#undef FM
+  CHECK_LAUNCH();
+  return grid;
+}
+
 __global__ void init_agg_states_kernel(AggState *st, int64_t n) {
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
     AggState z;

@@ -458,3 +458,40 @@ def test_groupby_direct_wide_slot_table(conn):
             c, s = exp.get(i % 100000, (0, 0))
             exp[i % 100000] = (c + 1, s + i)
     assert res.rows == [[str(k), str(c), str(s)] for k, (c, s) in sorted(exp.items())]
+
+
+# ---- multi-column conjunctions fused into one LDS-DMA pass ----------------------
+def test_filter_multi_parity(mbx, oracle):
+    cfg = mbx.Config.create()
+    cfg.set("mbx_profile", "true")
+    c = mbx.connect_with_config(cfg).value
+    try:
+        for n in (1, 255, 256, 257, 70_001, 1_000_003):
+            x = oracle.synth_i64(n, 42, 0, 50, 1)
+            k = oracle.synth_i64(n, 7, 0, 32, 0)
+            v = oracle.synth_i64(n, 9, 0, 2**40, -2**39)
+            q(c, "DROP TABLE IF EXISTS fm")
+            q(c, f"CREATE TABLE fm AS SELECT mbx_synth(42, i, 50) + 1 AS x, CAST(mbx_synth(7, i, 32) AS INTEGER) AS k, "
+                 f"mbx_synth(9, i, 1099511627776) - 549755813888 AS v FROM range({n}) tbl(i)")
+            cases = [("x > 24 AND k < 16", (x > 24) & (k < 16), "v"),
+                     ("x BETWEEN 5 AND 30 AND k >= 3 AND v > 0", (x >= 5) & (x <= 30) & (k >= 3) & (v > 0), "v"),
+                     ("k = 7 AND x < 40", (k == 7) & (x < 40), "x"),
+                     ("k < 16", k < 16, "v"),            # one predicate column of another width
+                     ("x > 24 AND k < 16", (x > 24) & (k < 16), None)]
+            for where, m, col in cases:
+                if col is None:
+                    got = one(c, f"SELECT COUNT(*) FROM fm WHERE {where}")
+                    assert int(got[0]) == int(m.sum()), (n, where)
+                else:
+                    got = one(c, f"SELECT COUNT(*), SUM({col}), MIN({col}), MAX({col}) FROM fm WHERE {where}")
+                    sel = (v if col == "v" else x)[m]
+                    assert int(got[0]) == int(m.sum()), (n, where)
+                    if m.sum():
+                        assert [int(g) for g in got[1:]] == [int(sel.astype(object).sum()), int(sel.min()), int(sel.max())]
+                    else:
+                        assert got[1:] == ["", "", ""]
+                if n >= 256:
+                    names = [kk["name"] for kk in c.last_profile()["kernels"]]
+                    assert "filter_multi" in names, (where, names)
+    finally:
+        c.close()

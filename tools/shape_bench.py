@@ -25,6 +25,8 @@ shapes = {
     "c3_project": "SELECT k, SUM(v * 2), COUNT(*) FROM t GROUP BY k",
     "multi_key": "SELECT k, k2, SUM(v), COUNT(*) FROM t GROUP BY k, k2",
     "filter_sum_expr": "SELECT SUM(v + x) FROM t WHERE x > 24 AND k < 16",
+    "filter_multi": "SELECT COUNT(*), SUM(v) FROM t WHERE x > 24 AND k < 16",
+    "filter_multi3": "SELECT SUM(v), MIN(v), MAX(v) FROM t WHERE x BETWEEN 10 AND 40 AND k < 16 AND k2 = 1",
     "wide_key": "SELECT v % 1000003, COUNT(*) FROM t GROUP BY v % 1000003",
 }
 if os.environ.get("SHAPES"):
