@@ -58,8 +58,18 @@ def global_count_sum(local_count: int, local_sum, device="cpu", group=None):
     return combine_count_sum(parts)
 
 
+_count_buf = {}
+
+
 def allreduce_count(local_count: int, device="cpu", group=None) -> int:
-    t = torch.tensor([int(local_count)], dtype=torch.int64, device=device)
+    """Global COUNT(*): one int64 all-reduce (sum).  The one-element buffer is
+    reused across calls, so a step pays only the fill, the collective and the
+    read-back."""
+    key = (str(device), id(group))
+    t = _count_buf.get(key)
+    if t is None:
+        t = _count_buf[key] = torch.zeros(1, dtype=torch.int64, device=device)
+    t.fill_(int(local_count))
     dist.all_reduce(t, group=group)
     return int(t.item())
 
