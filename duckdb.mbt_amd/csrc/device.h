@@ -97,9 +97,11 @@ int FilterAggStates(const void *pcol, int pphys, int64_t lo, int64_t hi, bool ha
 // --- fused GROUP BY on a small-range integer key (config C3) -------------
 // key in [kmin, kmin + nk), no nulls; up to 2 value columns of one phys.
 size_t GroupDirectLds(int nk, int R, int nv, bool mm);
-// Optional fused range predicate of the direct GROUP BY: rows with
-// lo <= p <= hi only.  src: 0 = none, 1 = its own column `col` (int32/int64),
-// 2 = the key column, 3 = value column 0.
+// Optional fused range predicates of the direct GROUP BY (a conjunction):
+// rows with lo <= p <= lo + span for every entry.  src: 1 = its own column
+// `col` (int32/int64, loaded as an extra slice), 2 = the key column, 3 = value
+// column 0.
+#define GROUP_MAX_PRED 3
 struct GroupPred {
   int32_t src;
   int32_t phys;
@@ -107,11 +109,15 @@ struct GroupPred {
   int64_t lo;
   uint64_t span;
 };
+struct GroupPreds {
+  int32_t n;
+  GroupPred p[GROUP_MAX_PRED];
+};
 // false only when a predicate was given and the shape needs the segmented kernel
 bool GroupByDirectStates(const void *kcol, int kphys, int64_t kmin, int nk, const void *v0, const void *v1, int vphys,
                          int nv, bool mm, int64_t nrows, int64_t seg_rows, int R, unsigned long long *cstar,
                          AggState *st0, AggState *st1, int grid_blocks, hipStream_t s,
-                         const GroupPred *pred = nullptr);
+                         const GroupPreds *pred = nullptr);
 
 // --- generic aggregation over compacted columns ---------------------------
 // vclass: VC_I64 / VC_I128 / VC_F64 of the input column (phys given)

@@ -1363,10 +1363,10 @@ static DRel Aggregate(Engine &e, const DRel &src, const BoundSelect &s) {
   // ---- fast path F2: GROUP BY one small-range int key column, aggregates
   //      over <= 2 int columns of one phys, no predicate.
   //      (plus: an optional range predicate on one int column, fused)
-  int f2_pcol = -1;
-  i128 f2_lo = (i128)INT64_MIN, f2_hi = (i128)INT64_MAX;
-  bool f2_pred_ok = !s.where || (RangePredicate(*s.where, &f2_pcol, &f2_lo, &f2_hi) && f2_pcol >= 0 &&
-                                 FastIntCol(src, f2_pcol) && f2_lo <= f2_hi);
+  std::map<int, std::pair<i128, i128>> f2_ranges;
+  bool f2_pred_ok = !s.where || (RangeConj(*s.where, f2_ranges) && f2_ranges.size() <= GROUP_MAX_PRED);
+  for (auto &kv : f2_ranges)
+    if (!FastIntCol(src, kv.first) || kv.second.first > kv.second.second) f2_pred_ok = false;
   if (ng == 1 && f2_pred_ok && !src.range && s.groups[0]->kind == BExpr::COL && FastIntCol(src, s.groups[0]->col)) {
     const DCol &K = src.cols[s.groups[0]->col];
     const DevColumn *ks = K.table_col;
@@ -1423,16 +1423,17 @@ static DRel Aggregate(Engine &e, const DRel &src, const BoundSelect &s) {
           Phys vphys = nv ? src.cols[vcols[0]].phys : P_I64;
           double bytes = (double)src.n * PhysSize(K.phys);
           for (int c : vcols) bytes += (double)src.n * PhysSize(src.cols[c].phys);
-          dev::GroupPred gp;
+          dev::GroupPreds gp;
           memset(&gp, 0, sizeof(gp));
-          if (s.where) {
-            const int kcol = s.groups[0]->col;
-            gp.src = f2_pcol == kcol ? 2 : (nv > 0 && f2_pcol == vcols[0]) ? 3 : 1;
-            gp.phys = src.cols[f2_pcol].phys;
-            gp.col = src.cols[f2_pcol].data;
-            gp.lo = (int64_t)std::max<i128>(f2_lo, INT64_MIN);
-            gp.span = (uint64_t)((int64_t)std::min<i128>(f2_hi, INT64_MAX)) - (uint64_t)gp.lo;
-            if (gp.src == 1) bytes += (double)src.n * PhysSize(src.cols[f2_pcol].phys);
+          for (auto &kv : f2_ranges) {
+            const int kcol = s.groups[0]->col, pc = kv.first;
+            dev::GroupPred &g = gp.p[gp.n++];
+            g.src = pc == kcol ? 2 : (nv > 0 && pc == vcols[0]) ? 3 : 1;
+            g.phys = src.cols[pc].phys;
+            g.col = src.cols[pc].data;
+            g.lo = (int64_t)std::max<i128>(kv.second.first, INT64_MIN);
+            g.span = (uint64_t)((int64_t)std::min<i128>(kv.second.second, INT64_MAX)) - (uint64_t)g.lo;
+            if (g.src == 1) bytes += (double)src.n * PhysSize(src.cols[pc].phys);
           }
           bool launched;
           {
@@ -1441,7 +1442,7 @@ static DRel Aggregate(Engine &e, const DRel &src, const BoundSelect &s) {
                                                 nv > 0 ? src.cols[vcols[0]].data : nullptr,
                                                 nv > 1 ? src.cols[vcols[1]].data : nullptr, vphys, nv, mm, src.n, seg,
                                                 R, (unsigned long long *)cs->p, (dev::AggState *)s0->p,
-                                                (dev::AggState *)s1->p, 0, e.stream, s.where ? &gp : nullptr);
+                                                (dev::AggState *)s1->p, 0, e.stream, gp.n ? &gp : nullptr);
           }
           if (!launched) goto generic;
           auto list = Alloc(e, nslots * 4);

@@ -1516,14 +1516,21 @@ __global__ __launch_bounds__(256) void group_direct_lds_kernel(const TK *__restr
                                                                const TV *__restrict__ v1, int64_t n, int64_t kmin,
                                                                int nk, int R, size_t ring_off,
                                                                unsigned long long *cstar, AggState *st0,
-                                                               AggState *st1, GroupPred pr) {
+                                                               AggState *st1, GroupPreds pr) {
   extern __shared__ __attribute__((aligned(16))) unsigned char lds_raw[];
   constexpr int KB = 256 * (int)sizeof(TK), VB = 256 * (int)sizeof(TV);  // bytes per step
   constexpr int SB0 = KB + NV * VB;                                        // slot bytes without a predicate slice
   // NLD counts the glds of a step without the optional predicate slice: with
   // one, the counted wait below is merely conservative (loads retire in order)
   constexpr int NLD = SB0 / 1024;
-  const int PB = pr.src == 1 ? 256 * (pr.phys == P_I64 ? 8 : 4) : 0;
+  // extra slices for predicate columns of their own, after the key/value slices
+  int poff[GROUP_MAX_PRED];
+  int PB = 0;
+#pragma unroll
+  for (int j = 0; j < GROUP_MAX_PRED; j++) {
+    poff[j] = SB0 + PB;
+    if (j < pr.n && pr.p[j].src == 1) PB += 256 * (pr.p[j].phys == P_I64 ? 8 : 4);
+  }
   const int SB = SB0 + PB;
   const int nslot = nk * R;
   unsigned int *cnt = (unsigned int *)lds_raw;
@@ -1579,11 +1586,15 @@ __global__ __launch_bounds__(256) void group_direct_lds_kernel(const TK *__restr
         __builtin_amdgcn_global_load_lds((const void *)(vp + j * 1024 + lane * 16), (void *)(dst + KB + VB + j * 1024), 16,
                                          0, 2);
     }
-    if (PB) {
-      const unsigned char *pp = (const unsigned char *)pr.col + q * PB;
-      __builtin_amdgcn_global_load_lds((const void *)(pp + lane * 16), (void *)(dst + SB0), 16, 0, 2);
-      if (PB == 2048)
-        __builtin_amdgcn_global_load_lds((const void *)(pp + 1024 + lane * 16), (void *)(dst + SB0 + 1024), 16, 0, 2);
+#pragma unroll
+    for (int j = 0; j < GROUP_MAX_PRED; j++) {
+      if (j >= pr.n || pr.p[j].src != 1) continue;
+      const int B = pr.p[j].phys == P_I64 ? 2048 : 1024;
+      const unsigned char *pp = (const unsigned char *)pr.p[j].col + q * B;
+      __builtin_amdgcn_global_load_lds((const void *)(pp + lane * 16), (void *)(dst + poff[j]), 16, 0, 2);
+      if (B == 2048)
+        __builtin_amdgcn_global_load_lds((const void *)(pp + 1024 + lane * 16), (void *)(dst + poff[j] + 1024), 16, 0,
+                                         2);
     }
   };
   if (nsteps > 0) {
@@ -1618,21 +1629,24 @@ __global__ __launch_bounds__(256) void group_direct_lds_kernel(const TK *__restr
       }
     }
     bool ok[4] = {true, true, true, true};
-    if (pr.src) {
+#pragma unroll
+    for (int j = 0; j < GROUP_MAX_PRED; j++) {
+      if (j >= pr.n) break;
+      const GroupPred &g = pr.p[j];
       int64_t pv[4];
-      if (pr.src == 2) {
+      if (g.src == 2) {
         pv[0] = kk[0]; pv[1] = kk[1]; pv[2] = kk[2]; pv[3] = kk[3];
-      } else if (pr.src == 3) {
+      } else if (g.src == 3) {
         pv[0] = a[0]; pv[1] = a[1]; pv[2] = a[2]; pv[3] = a[3];
-      } else if (PB == 1024) {
-        v4i32 x = *(const v4i32 *)(src + SB0 + lane * 16);
+      } else if (g.phys != P_I64) {
+        v4i32 x = *(const v4i32 *)(src + poff[j] + lane * 16);
         pv[0] = x.x; pv[1] = x.y; pv[2] = x.z; pv[3] = x.w;
       } else {
-        v2i64 x0 = *(const v2i64 *)(src + SB0 + lane * 32), x1 = *(const v2i64 *)(src + SB0 + lane * 32 + 16);
+        v2i64 x0 = *(const v2i64 *)(src + poff[j] + lane * 32), x1 = *(const v2i64 *)(src + poff[j] + lane * 32 + 16);
         pv[0] = x0.x; pv[1] = x0.y; pv[2] = x1.x; pv[3] = x1.y;
       }
 #pragma unroll
-      for (int e = 0; e < 4; e++) ok[e] = (uint64_t)(pv[e] - pr.lo) <= pr.span;
+      for (int e = 0; e < 4; e++) ok[e] = ok[e] && (uint64_t)(pv[e] - g.lo) <= g.span;
     }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     int64_t q = st + DEPTH * nw;
@@ -1647,10 +1661,11 @@ __global__ __launch_bounds__(256) void group_direct_lds_kernel(const TK *__restr
     for (int64_t i = (nsteps << 8) + t; i < n; i += blockDim.x) {
       int64_t kv = (int64_t)keys[i], av = NV >= 1 ? (int64_t)v0[i] : 0;
       bool okr = true;
-      if (pr.src) {
-        int64_t pv = pr.src == 2 ? kv : pr.src == 3 ? av
-                   : (pr.phys == P_I64 ? ((const int64_t *)pr.col)[i] : (int64_t)((const int32_t *)pr.col)[i]);
-        okr = (uint64_t)(pv - pr.lo) <= pr.span;
+      for (int j = 0; j < pr.n; j++) {
+        const GroupPred &g = pr.p[j];
+        int64_t pv = g.src == 2 ? kv : g.src == 3 ? av
+                   : (g.phys == P_I64 ? ((const int64_t *)g.col)[i] : (int64_t)((const int32_t *)g.col)[i]);
+        okr = okr && (uint64_t)(pv - g.lo) <= g.span;
       }
       if (okr) row(kv, av, NV >= 2 ? (int64_t)v1[i] : 0);
     }
@@ -1709,9 +1724,9 @@ size_t GroupDirectLds(int nk, int R, int nv, bool mm) {
 
 bool GroupByDirectStates(const void *kcol, int kphys, int64_t kmin, int nk, const void *v0, const void *v1, int vphys,
                          int nv, bool mm, int64_t nrows, int64_t seg_rows, int R, unsigned long long *cstar,
-                         AggState *st0, AggState *st1, int grid_blocks, hipStream_t s, const GroupPred *pred) {
+                         AggState *st0, AggState *st1, int grid_blocks, hipStream_t s, const GroupPreds *pred) {
   if (nrows <= 0) return true;
-  GroupPred pr;
+  GroupPreds pr;
   memset(&pr, 0, sizeof(pr));
   if (pred) pr = *pred;
   // LDS-DMA variant: one flush at the end, so a block's whole row share must
@@ -1722,9 +1737,9 @@ bool GroupByDirectStates(const void *kcol, int kphys, int64_t kmin, int nk, cons
   // byte and stay on the segmented kernel at 4 blocks/CU (6.40 TB/s).
   {
     int depth = 2, gpc = 3;
-    bool use = nv > 0 || pr.src != 0;  // the segmented kernel has no predicate
+    bool use = nv > 0 || pr.n != 0;  // the segmented kernel has no predicate
     const char *e = getenv("MBX_GD_VARIANT");
-    if (e && *e) use = sscanf(e, "d%d_g%d", &depth, &gpc) == 2 || pr.src != 0;
+    if (e && *e) use = sscanf(e, "d%d_g%d", &depth, &gpc) == 2 || pr.n != 0;
     if (use) {
       int grid = grid_blocks > 0 ? grid_blocks : NumCUs() * gpc;
       int64_t nsteps = nrows >> 8;
@@ -1732,10 +1747,20 @@ bool GroupByDirectStates(const void *kcol, int kphys, int64_t kmin, int nk, cons
       int64_t rows_per_block = ((nsteps + waves - 1) / waves) * 4 * 256 + 256;
       size_t tab = GroupDirectLds(nk, R, nv, mm);
       size_t ring_off = (tab + 15) & ~(size_t)15;
-      size_t slot = 256 * (size_t)(kphys == P_I64 ? 8 : 4) + (size_t)nv * 256 * (vphys == P_I64 ? 8 : 4) +
-                    (pr.src == 1 ? 256 * (size_t)(pr.phys == P_I64 ? 8 : 4) : 0);
+      size_t slot = 256 * (size_t)(kphys == P_I64 ? 8 : 4) + (size_t)nv * 256 * (vphys == P_I64 ? 8 : 4);
+      for (int j = 0; j < pr.n; j++)
+        if (pr.p[j].src == 1) slot += 256 * (size_t)(pr.p[j].phys == P_I64 ? 8 : 4);
       depth = depth <= 2 ? 2 : depth <= 3 ? 3 : 4;
       size_t lds = ring_off + 4 * (size_t)depth * slot;
+      // wide slots (predicate slices): trade table replicas for ring space;
+      // seg_rows scales with R (rows per replica stay the same)
+      while (lds > 64 * 1024 && R > 1) {
+        R >>= 1;
+        if (seg_rows > 0) seg_rows >>= 1;
+        tab = GroupDirectLds(nk, R, nv, mm);
+        ring_off = (tab + 15) & ~(size_t)15;
+        lds = ring_off + 4 * (size_t)depth * slot;
+      }
       if ((seg_rows <= 0 || seg_rows >= rows_per_block) && lds <= 64 * 1024) {
 #define GL(TK, TV, NV, MM, D)                                                                                       \
   hipLaunchKernelGGL((group_direct_lds_kernel<TK, TV, NV, MM, D>), dim3(grid), dim3(256), lds, s, (const TK *)kcol, \
@@ -1759,7 +1784,7 @@ bool GroupByDirectStates(const void *kcol, int kphys, int64_t kmin, int nk, cons
       }
     }
   }
-  if (pr.src) return false;  // a predicate needs the LDS-DMA kernel
+  if (pr.n) return false;  // a predicate needs the LDS-DMA kernel
   int grid = grid_blocks > 0 ? grid_blocks : NumCUs() * 4;
   int64_t chunk = (nrows + grid - 1) / grid;
   chunk = (chunk + 3) & ~(int64_t)3;

@@ -400,7 +400,10 @@ def test_filter_groupby_fused_parity(conn, oracle, monkeypatch, variant):
                 f"mbx_synth(9, i, 1099511627776) - 549755813888 AS v, mbx_synth(42, i, 50) + 1 AS x, "
                 f"CAST(mbx_synth(42, i, 50) + 1 AS INTEGER) AS x4 FROM range({n}) tbl(i)")
         cases = [("x > 24", x > 24), ("x4 BETWEEN 10 AND 20", (x >= 10) & (x <= 20)), ("k < 16", k < 16),
-                 ("v >= 0", v >= 0), ("x = 7", x == 7), ("x > 50", x > 50)]
+                 ("v >= 0", v >= 0), ("x = 7", x == 7), ("x > 50", x > 50),
+                 ("x > 24 AND k < 16", (x > 24) & (k < 16)),
+                 ("x4 BETWEEN 10 AND 20 AND v >= 0 AND x < 45", (x >= 10) & (x <= 20) & (v >= 0)),
+                 ("x4 > 5 AND x < 40 AND k BETWEEN 3 AND 29", (x > 5) & (x < 40) & (k >= 3) & (k <= 29))]
         for where, m in cases:
             res = q(conn, f"SELECT k, SUM(v), COUNT(*), MIN(v), MAX(v) FROM fg WHERE {where} GROUP BY k ORDER BY k")
             want = []

@@ -22,6 +22,7 @@ shapes = {
     "c2_count": "SELECT COUNT(*) FROM t WHERE x > 24",
     "c3": "SELECT k, SUM(v), COUNT(*) FROM t GROUP BY k",
     "c3_where": "SELECT k, SUM(v), COUNT(*) FROM t WHERE x > 24 GROUP BY k",
+    "c3_where2": "SELECT k, SUM(v), COUNT(*) FROM t WHERE x > 24 AND k2 = 1 GROUP BY k",
     "c3_project": "SELECT k, SUM(v * 2), COUNT(*) FROM t GROUP BY k",
     "multi_key": "SELECT k, k2, SUM(v), COUNT(*) FROM t GROUP BY k, k2",
     "filter_sum_expr": "SELECT SUM(v + x) FROM t WHERE x > 24 AND k < 16",
