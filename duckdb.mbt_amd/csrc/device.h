@@ -9,20 +9,6 @@
 namespace mbx {
 namespace dev {
 
-struct VmCols {
-  VmCol c[VM_MAX_COLS];
-  int32_t n;
-};
-
-struct VmOuts {
-  void *data[VM_MAX_OUT];
-  // 32-bit-word view of a zeroed NULL bitmap (bit = 1: row is NULL), or null.
-  // Only NULL rows touch it (rare), so the common all-valid output costs no
-  // bitmap traffic; InvertNullBits turns it into a validity bitmap when
-  // anynull says one is needed.
-  uint32_t *nullbits[VM_MAX_OUT];
-  int32_t *anynull;  // per output: set to 1 if a NULL was written
-};
 // validity[w] = ~nullbits[w] over the words covering n rows (tail bits cleared)
 void InvertNullBits(uint64_t *bits, int64_t n, hipStream_t s);
 

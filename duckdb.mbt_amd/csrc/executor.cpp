@@ -19,6 +19,7 @@
 #include <thread>
 
 #include "device.h"
+#include "jit.h"
 #include "engine.h"
 #include "vm.h"
 
@@ -811,8 +812,10 @@ static DRel FilterProject(Engine &e, const DRel &rel, const BExprPtr &pred, cons
       offs = Alloc(e, std::max<int64_t>(ntiles, 1) * 8);
       {
         ProfScope ps(e, "vm_filter", 0, n);
-        dev::VmFilter(vc.P, vc.cols, n, rel.rs, rel.rstep, (uint64_t *)bits->p, (uint32_t *)counts->p, e.d_err,
-                      e.stream);
+        if (!jit::VmFilter(vc.P, vc.cols, n, rel.rs, rel.rstep, (uint64_t *)bits->p, (uint32_t *)counts->p, e.d_err,
+                           e.stream))
+          dev::VmFilter(vc.P, vc.cols, n, rel.rs, rel.rstep, (uint64_t *)bits->p, (uint32_t *)counts->p, e.d_err,
+                        e.stream);
       }
       dev::ScanTileCounts((const uint32_t *)counts->p, (int64_t *)offs->p, ntiles, e.d_scratch, e.stream);
       nsel = ReadDev<int64_t>(e, e.d_scratch);
@@ -859,7 +862,9 @@ static DRel FilterProject(Engine &e, const DRel &rel, const BExprPtr &pred, cons
     }
     if (nsel > 0) {
       ProfScope ps(e, "vm_project", 0, n);
-      dev::VmProject(vc.P, vc.cols, n, rel.rs, rel.rstep, bits ? (const uint64_t *)bits->p : nullptr,
+      if (!jit::VmProject(vc.P, vc.cols, n, rel.rs, rel.rstep, bits ? (const uint64_t *)bits->p : nullptr,
+                     offs ? (const int64_t *)offs->p : nullptr, vo, e.d_err, e.stream))
+        dev::VmProject(vc.P, vc.cols, n, rel.rs, rel.rstep, bits ? (const uint64_t *)bits->p : nullptr,
                      offs ? (const int64_t *)offs->p : nullptr, vo, e.d_err, e.stream);
     }
     int32_t an[VM_MAX_OUT];

@@ -1,0 +1,39 @@
+// jit.h — run-time specialised expression kernels.
+//
+// The tile interpreter (vm_filter_kernel / vm_project_kernel in kernels.hip)
+// reads every instruction at run time and keeps registers in LDS planes.  For
+// a program seen before, jit.cpp emits HIP source in which every instruction
+// is a vm_step(...) call with literal operands (vm_device.h), compiles it for
+// gfx950 with hipRTC on a background thread and caches the code object by the
+// program's shape (opcodes, registers, column types, outputs — not constant
+// values, which stay kernel arguments).  Until the kernel is ready, and
+// whenever compilation fails, the interpreter runs: results are identical.
+//   MBX_JIT=0      never compile (interpreter only)
+//   MBX_JIT=sync   compile on first use and wait (tests, benchmarks)
+//   default        compile asynchronously, switch over when ready
+#pragma once
+#include <hip/hip_runtime_api.h>
+#include <stdint.h>
+
+#include <string>
+
+#include "vm.h"
+
+namespace mbx {
+namespace jit {
+
+// true: launched the specialised filter (same outputs as dev::VmFilter)
+bool VmFilter(const VmProgram &p, const dev::VmCols &cols, int64_t nrows, int64_t range_start, int64_t range_step,
+              uint64_t *sel_bits, uint32_t *tile_counts, int32_t *err, hipStream_t s);
+// true: launched the specialised projection (same outputs as dev::VmProject)
+bool VmProject(const VmProgram &p, const dev::VmCols &cols, int64_t nrows, int64_t range_start, int64_t range_step,
+               const uint64_t *sel_bits, const int64_t *tile_offsets, const dev::VmOuts &outs, int32_t *err,
+               hipStream_t s);
+// The generated source for a program (exposed for tests and EXPLAIN).
+std::string Source(const VmProgram &p, const dev::VmCols &cols, bool filter);
+// Compiles source for gfx950 without loading it (no GPU needed); "" = ok,
+// else the compiler log.
+std::string CompileCheck(const std::string &src);
+
+}  // namespace jit
+}  // namespace mbx

@@ -17,6 +17,7 @@
 #include "device.h"
 #include "types.h"
 #include "vm.h"
+#include "vm_device.h"
 
 namespace mbx {
 namespace dev {
@@ -64,157 +65,6 @@ static inline int GridFor(int64_t work_items, int per_block, int max_blocks) {
 }
 
 // ---------------------------------------------------------------------------
-// small device helpers
-// ---------------------------------------------------------------------------
-__device__ __forceinline__ bool bit_valid(const uint64_t *v, int64_t row) {
-  return v == nullptr || ((v[row >> 6] >> (row & 63)) & 1ull);
-}
-
-__device__ __forceinline__ void load_phys(const void *data, int phys, int64_t row, int64_t &lo, int64_t &hi) {
-  switch (phys) {
-    case P_U8: lo = ((const uint8_t *)data)[row]; hi = 0; break;
-    case P_I8: lo = ((const int8_t *)data)[row]; hi = lo >> 63; break;
-    case P_I16: lo = ((const int16_t *)data)[row]; hi = lo >> 63; break;
-    case P_U16: lo = ((const uint16_t *)data)[row]; hi = 0; break;
-    case P_I32: lo = ((const int32_t *)data)[row]; hi = lo >> 63; break;
-    case P_U32: lo = ((const uint32_t *)data)[row]; hi = 0; break;
-    case P_I64: lo = ((const int64_t *)data)[row]; hi = lo >> 63; break;
-    case P_U64: lo = (int64_t)((const uint64_t *)data)[row]; hi = 0; break;
-    case P_I128: {
-      const int64_t *p = (const int64_t *)data + 2 * row;
-      lo = p[0];
-      hi = p[1];
-      break;
-    }
-    case P_F32: {
-      double d = ((const float *)data)[row];
-      lo = __double_as_longlong(d);
-      hi = 0;
-      break;
-    }
-    case P_F64: lo = ((const int64_t *)data)[row]; hi = 0; break;
-    default: lo = row; hi = 0; break;  // P_STR: the row index is the string code
-  }
-}
-
-__device__ __forceinline__ void store_phys(void *data, int phys, int64_t row, int64_t lo, int64_t hi) {
-  switch (phys) {
-    case P_U8: ((uint8_t *)data)[row] = (uint8_t)lo; break;
-    case P_I8: ((int8_t *)data)[row] = (int8_t)lo; break;
-    case P_I16: ((int16_t *)data)[row] = (int16_t)lo; break;
-    case P_U16: ((uint16_t *)data)[row] = (uint16_t)lo; break;
-    case P_I32: ((int32_t *)data)[row] = (int32_t)lo; break;
-    case P_U32: ((uint32_t *)data)[row] = (uint32_t)lo; break;
-    case P_I64: case P_U64: case P_F64: case P_STR: ((int64_t *)data)[row] = lo; break;
-    case P_I128: {
-      int64_t *p = (int64_t *)data + 2 * row;
-      p[0] = lo;
-      p[1] = hi;
-      break;
-    }
-    case P_F32: ((float *)data)[row] = (float)__longlong_as_double(lo); break;
-    default: break;
-  }
-}
-
-__device__ __forceinline__ i128 mk128(int64_t lo, int64_t hi) { return (i128)(((u128)(uint64_t)hi << 64) | (uint64_t)lo); }
-__device__ __forceinline__ void sp128(i128 v, int64_t &lo, int64_t &hi) {
-  lo = (int64_t)(uint64_t)(u128)v;
-  hi = (int64_t)(uint64_t)((u128)v >> 64);
-}
-
-__device__ __forceinline__ bool add_ovf128(i128 a, i128 b, i128 &r) {
-  r = (i128)((u128)a + (u128)b);
-  return ((a ^ r) & (b ^ r)) < 0;
-}
-__device__ __forceinline__ bool sub_ovf128(i128 a, i128 b, i128 &r) {
-  r = (i128)((u128)a - (u128)b);
-  return ((a ^ b) & (a ^ r)) < 0;
-}
-__device__ __forceinline__ bool mul_ovf128(i128 a, i128 b, i128 &r) {
-  bool neg = (a < 0) != (b < 0);
-  u128 ua = a < 0 ? (u128)0 - (u128)a : (u128)a;
-  u128 ub = b < 0 ? (u128)0 - (u128)b : (u128)b;
-  uint64_t ah = (uint64_t)(ua >> 64), al = (uint64_t)ua, bh = (uint64_t)(ub >> 64), bl = (uint64_t)ub;
-  if (ah && bh) return true;
-  u128 lo = (u128)al * bl;
-  u128 mid = (u128)ah * bl + (u128)al * bh;
-  if (mid >> 64) return true;
-  u128 res = lo + (mid << 64);
-  if (res < lo) return true;
-  u128 lim = neg ? ((u128)1 << 127) : (((u128)1 << 127) - 1);
-  if (res > lim) return true;
-  r = neg ? (i128)((u128)0 - res) : (i128)res;
-  return false;
-}
-__device__ __forceinline__ u128 udiv128(u128 n, u128 d) {
-  // shift-subtract division (rare path: HUGEINT / DECIMAL(>18) division)
-  if (d == 0) return 0;
-  if ((n >> 64) == 0 && (d >> 64) == 0) return (u128)((uint64_t)n / (uint64_t)d);
-  u128 q = 0, r = 0;
-  for (int i = 127; i >= 0; i--) {
-    r = (r << 1) | ((n >> i) & 1);
-    if (r >= d) {
-      r -= d;
-      q |= (u128)1 << i;
-    }
-  }
-  return q;
-}
-__device__ __forceinline__ i128 sdiv128(i128 a, i128 b) {
-  bool neg = (a < 0) != (b < 0);
-  u128 ua = a < 0 ? (u128)0 - (u128)a : (u128)a;
-  u128 ub = b < 0 ? (u128)0 - (u128)b : (u128)b;
-  u128 q = udiv128(ua, ub);
-  return neg ? (i128)((u128)0 - q) : (i128)q;
-}
-__device__ __forceinline__ i128 smod128(i128 a, i128 b) { return a - sdiv128(a, b) * b; }
-
-__device__ __forceinline__ i128 pow10_128(int k) {
-  i128 r = 1;
-  for (int i = 0; i < k; i++) r *= 10;
-  return r;
-}
-__device__ __forceinline__ int64_t pow10_64(int k) {
-  int64_t r = 1;
-  for (int i = 0; i < k; i++) r *= 10;
-  return r;
-}
-
-// int128 -> double through the magnitude (no cancellation between the
-// halves); exact rounding whenever |v| < 2^64.
-__device__ __forceinline__ double u128_to_double(u128 m) {
-  uint64_t hi = (uint64_t)(m >> 64), lo = (uint64_t)m;
-  if (hi == 0) return (double)lo;
-  return (double)hi * 18446744073709551616.0 + (double)lo;
-}
-__device__ __forceinline__ double i128_to_double(i128 v) {
-  if (v < 0) return -u128_to_double((u128)0 - (u128)v);
-  return u128_to_double((u128)v);
-}
-
-__device__ __forceinline__ uint64_t splitmix64(uint64_t z) {
-  z += 0x9E3779B97F4A7C15ull;
-  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
-  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
-  return z ^ (z >> 31);
-}
-
-__device__ __forceinline__ void raise_err(int32_t *err, int32_t code) {
-  if (err) atomicCAS(err, 0, code);
-}
-
-__device__ __forceinline__ uint64_t f64_order(double d) {
-  uint64_t u = (uint64_t)__double_as_longlong(d);
-  if (d != d) return 0xFFFFFFFFFFFFFFFFull;  // NaN sorts last
-  return (u >> 63) ? ~u : (u | 0x8000000000000000ull);
-}
-__device__ __forceinline__ double f64_unorder(uint64_t k) {
-  uint64_t u = (k >> 63) ? (k & 0x7FFFFFFFFFFFFFFFull) : ~k;
-  return __longlong_as_double((long long)u);
-}
-
-// ---------------------------------------------------------------------------
 // expression VM (tile interpreter)
 // ---------------------------------------------------------------------------
 // VM register planes [reg][row] in dynamic LDS sized to the program's
@@ -234,253 +84,22 @@ __device__ __forceinline__ VmLds vm_regs(unsigned char *base, int n_regs) {
 }
 static size_t VmLdsBytes(int n_regs) { return (size_t)(n_regs < 1 ? 1 : n_regs) * VM_TILE * 17; }
 
-__device__ __forceinline__ bool cmp_res(int c, int k) {
-  // c = -1/0/1 comparison, k = cmp kind
-  switch (k) {
-    case 0: return c == 0;
-    case 1: return c != 0;
-    case 2: return c < 0;
-    case 3: return c <= 0;
-    case 4: return c > 0;
-    default: return c >= 0;
-  }
-}
+
+// LDS-plane register file of the tile interpreter
+struct LdsRF {
+  const VmLds &R;
+  int t;
+  __device__ __forceinline__ int64_t &lo(int i) { return R.lo[i * VM_TILE + t]; }
+  __device__ __forceinline__ int64_t &hi(int i) { return R.hi[i * VM_TILE + t]; }
+  __device__ __forceinline__ uint8_t &nl(int i) { return R.nl[i * VM_TILE + t]; }
+};
 
 __device__ void vm_exec(const VmProgram &P, const VmCols &C, int64_t row, bool active, int64_t rs, int64_t rstep,
                         const VmLds &R, int t, int32_t *err) {
+  LdsRF rf{R, t};
   for (int k = 0; k < P.n_ins; k++) {
     const VmIns I = P.ins[k];
-    const int d = I.dst, a = I.a, b = I.b, c = I.c;
-    int64_t lo = 0, hi = 0;
-    uint8_t nl = 0;
-    switch (I.op) {
-      case V_LOADCOL: {
-        const VmCol &col = C.c[a];
-        if (active) {
-          nl = bit_valid(col.validity, row) ? 0 : 1;
-          load_phys(col.data, col.phys, row, lo, hi);
-        } else {
-          nl = 1;
-        }
-        break;
-      }
-      case V_LOADRANGE: lo = rs + row * rstep; hi = lo >> 63; break;
-      case V_CONST: lo = P.consts[a].lo; hi = P.consts[a].hi; nl = (uint8_t)P.consts[a].isnull; break;
-      case V_MOV: lo = R.lo[(a) * VM_TILE + t]; hi = R.hi[(a) * VM_TILE + t]; nl = R.nl[(a) * VM_TILE + t]; break;
-      case V_SELECT: {
-        bool cond = !R.nl[(a) * VM_TILE + t] && R.lo[(a) * VM_TILE + t] != 0;
-        int s = cond ? b : c;
-        lo = R.lo[(s) * VM_TILE + t]; hi = R.hi[(s) * VM_TILE + t]; nl = R.nl[(s) * VM_TILE + t];
-        break;
-      }
-      case V_COALESCE: {
-        int s = R.nl[(a) * VM_TILE + t] ? b : a;
-        lo = R.lo[(s) * VM_TILE + t]; hi = R.hi[(s) * VM_TILE + t]; nl = R.nl[(s) * VM_TILE + t];
-        break;
-      }
-      case V_AND: {
-        bool an = R.nl[(a) * VM_TILE + t], bn = R.nl[(b) * VM_TILE + t];
-        bool av = R.lo[(a) * VM_TILE + t] != 0, bv = R.lo[(b) * VM_TILE + t] != 0;
-        if ((!an && !av) || (!bn && !bv)) { lo = 0; nl = 0; }
-        else if (an || bn) { nl = 1; }
-        else { lo = 1; }
-        break;
-      }
-      case V_OR: {
-        bool an = R.nl[(a) * VM_TILE + t], bn = R.nl[(b) * VM_TILE + t];
-        bool av = R.lo[(a) * VM_TILE + t] != 0, bv = R.lo[(b) * VM_TILE + t] != 0;
-        if ((!an && av) || (!bn && bv)) { lo = 1; nl = 0; }
-        else if (an || bn) { nl = 1; }
-        else { lo = 0; }
-        break;
-      }
-      case V_ISNULL: lo = R.nl[(a) * VM_TILE + t] ? 1 : 0; break;
-      case V_ISNOTNULL: lo = R.nl[(a) * VM_TILE + t] ? 0 : 1; break;
-      case V_DISTINCT_I: case V_DISTINCT_L: case V_DISTINCT_F: {
-        bool an = R.nl[(a) * VM_TILE + t], bn = R.nl[(b) * VM_TILE + t];
-        bool same;
-        if (an || bn) same = an && bn;
-        else if (I.op == V_DISTINCT_F) {
-          double x = __longlong_as_double(R.lo[(a) * VM_TILE + t]), y = __longlong_as_double(R.lo[(b) * VM_TILE + t]);
-          same = (x == y) || (x != x && y != y);
-        } else same = R.lo[(a) * VM_TILE + t] == R.lo[(b) * VM_TILE + t] && R.hi[(a) * VM_TILE + t] == R.hi[(b) * VM_TILE + t];
-        lo = I.aux ? same : !same;
-        break;
-      }
-      case V_SYNTH: {
-        nl = R.nl[(a) * VM_TILE + t] | R.nl[(b) * VM_TILE + t] | R.nl[(c) * VM_TILE + t];
-        uint64_t m = (uint64_t)R.lo[(c) * VM_TILE + t];
-        if (!nl && m) {
-          lo = (int64_t)(splitmix64((uint64_t)R.lo[(a) * VM_TILE + t] + (uint64_t)R.lo[(b) * VM_TILE + t]) % m);
-        } else {
-          nl = 1;
-        }
-        break;
-      }
-      default: {
-        // null-propagating unary/binary ops
-        nl = R.nl[(a) * VM_TILE + t];
-        if (I.op >= V_ADD_I && I.op != V_NOT && I.op != V_I2L && I.op != V_U2L && I.op != V_L2I && I.op != V_I2F &&
-            I.op != V_L2F && I.op != V_F2I && I.op != V_F2L && I.op != V_CHECK_I && I.op != V_CHECK_L &&
-            I.op != V_SCALEUP_I && I.op != V_SCALEUP_L && I.op != V_SCALEDN_I && I.op != V_SCALEDN_L &&
-            I.op != V_DEC2F_I && I.op != V_DEC2F_L && I.op != V_F2DEC_I && I.op != V_F2DEC_L &&
-            I.op != V_TOBOOL_I && I.op != V_TOBOOL_F && I.op != V_NEG_I && I.op != V_NEG_L && I.op != V_NEG_F &&
-            I.op != V_ABS_I && I.op != V_ABS_L && I.op != V_ABS_F)
-          nl |= R.nl[(b) * VM_TILE + t];
-        const int64_t xa = R.lo[(a) * VM_TILE + t], xah = R.hi[(a) * VM_TILE + t];
-        const int64_t xb = R.lo[(b) * VM_TILE + t], xbh = R.hi[(b) * VM_TILE + t];
-        bool ok = active && !nl;
-        switch (I.op) {
-          case V_ADD_I: if (__builtin_add_overflow(xa, xb, &lo) && ok) raise_err(err, E_OVF_ADD); break;
-          case V_SUB_I: if (__builtin_sub_overflow(xa, xb, &lo) && ok) raise_err(err, E_OVF_SUB); break;
-          case V_MUL_I: if (__builtin_mul_overflow(xa, xb, &lo) && ok) raise_err(err, E_OVF_MUL); break;
-          case V_DIV_I:
-            if (xb == 0) nl = 1;
-            else if (xa == INT64_MIN && xb == -1) { if (ok) raise_err(err, E_OVF_MUL); }
-            else lo = xa / xb;
-            break;
-          case V_MOD_I:
-            if (xb == 0) nl = 1;
-            else if (xb == -1) lo = 0;
-            else lo = xa % xb;
-            break;
-          case V_NEG_I: if (__builtin_sub_overflow((int64_t)0, xa, &lo) && ok) raise_err(err, E_OVF_NEG); break;
-          case V_ABS_I:
-            if (xa == INT64_MIN && ok) raise_err(err, E_OVF_NEG);
-            lo = xa < 0 ? -xa : xa;
-            break;
-          case V_ADD_L: case V_SUB_L: case V_MUL_L: {
-            i128 r, x = mk128(xa, xah), y = mk128(xb, xbh);
-            bool o = I.op == V_ADD_L ? add_ovf128(x, y, r) : I.op == V_SUB_L ? sub_ovf128(x, y, r) : mul_ovf128(x, y, r);
-            if (o && ok) raise_err(err, I.op == V_ADD_L ? E_OVF_ADD : I.op == V_SUB_L ? E_OVF_SUB : E_OVF_MUL);
-            sp128(r, lo, hi);
-            break;
-          }
-          case V_DIV_L: case V_MOD_L: {
-            i128 x = mk128(xa, xah), y = mk128(xb, xbh);
-            if (y == 0) { nl = 1; break; }
-            i128 r = I.op == V_DIV_L ? sdiv128(x, y) : smod128(x, y);
-            sp128(r, lo, hi);
-            break;
-          }
-          case V_NEG_L: {
-            i128 r;
-            if (sub_ovf128((i128)0, mk128(xa, xah), r) && ok) raise_err(err, E_OVF_NEG);
-            sp128(r, lo, hi);
-            break;
-          }
-          case V_ABS_L: {
-            i128 x = mk128(xa, xah);
-            sp128(x < 0 ? -x : x, lo, hi);
-            break;
-          }
-          case V_ADD_F: case V_SUB_F: case V_MUL_F: case V_DIV_F: case V_MOD_F: case V_IDIV_F: {
-            double x = __longlong_as_double(xa), y = __longlong_as_double(xb), r = 0;
-            switch (I.op) {
-              case V_ADD_F: r = x + y; break;
-              case V_SUB_F: r = x - y; break;
-              case V_MUL_F: r = x * y; break;
-              case V_DIV_F: if (y == 0) nl = 1; else r = x / y; break;
-              case V_MOD_F: if (y == 0) nl = 1; else r = fmod(x, y); break;
-              default: if (y == 0) nl = 1; else r = trunc(x / y); break;
-            }
-            if (I.aux == 1) r = (double)(float)r;  // FLOAT result
-            lo = __double_as_longlong(r);
-            break;
-          }
-          case V_NEG_F: lo = __double_as_longlong(-__longlong_as_double(xa)); break;
-          case V_ABS_F: lo = __double_as_longlong(fabs(__longlong_as_double(xa))); break;
-          case V_CMP_I: lo = cmp_res(xa < xb ? -1 : xa > xb ? 1 : 0, I.aux); break;
-          case V_CMP_L: {
-            i128 x = mk128(xa, xah), y = mk128(xb, xbh);
-            lo = cmp_res(x < y ? -1 : x > y ? 1 : 0, I.aux);
-            break;
-          }
-          case V_CMP_F: {
-            double x = __longlong_as_double(xa), y = __longlong_as_double(xb);
-            bool nx = x != x, ny = y != y;
-            int cc = (nx || ny) ? (nx == ny ? 0 : (nx ? 1 : -1)) : (x < y ? -1 : x > y ? 1 : 0);
-            lo = cmp_res(cc, I.aux);
-            break;
-          }
-          case V_NOT: lo = xa == 0; break;
-          case V_TOBOOL_I: lo = (xa != 0 || xah != 0); break;
-          case V_TOBOOL_F: lo = __longlong_as_double(xa) != 0.0; break;
-          case V_I2L: lo = xa; hi = xa >> 63; break;
-          case V_U2L: lo = xa; hi = 0; break;
-          case V_L2I: {
-            i128 x = mk128(xa, xah);
-            i128 mn = b == 255 ? (i128)INT64_MIN : mk128(P.consts[b].lo, P.consts[b].hi);
-            i128 mx = c == 255 ? (i128)INT64_MAX : mk128(P.consts[c].lo, P.consts[c].hi);
-            if ((x < mn || x > mx) && ok) raise_err(err, E_CAST_RANGE);
-            lo = xa;
-            break;
-          }
-          case V_CHECK_I: {
-            if ((xa < P.consts[b].lo || xa > P.consts[c].lo) && ok) raise_err(err, E_CAST_RANGE);
-            lo = xa;
-            break;
-          }
-          case V_CHECK_L: {
-            i128 x = mk128(xa, xah);
-            if ((x < mk128(P.consts[b].lo, P.consts[b].hi) || x > mk128(P.consts[c].lo, P.consts[c].hi)) && ok)
-              raise_err(err, E_CAST_RANGE);
-            lo = xa;
-            hi = xah;
-            break;
-          }
-          case V_I2F: lo = __double_as_longlong((double)xa); break;
-          case V_L2F: lo = __double_as_longlong(i128_to_double(mk128(xa, xah))); break;
-          case V_F2I: case V_F2L: {
-            double x = rint(__longlong_as_double(xa));
-            bool bad = !(x >= -1.7014118346046923e38 && x < 1.7014118346046923e38);
-            i128 v = bad ? 0 : (i128)x;
-            i128 mn = mk128(P.consts[b].lo, P.consts[b].hi), mx = mk128(P.consts[c].lo, P.consts[c].hi);
-            if ((bad || v < mn || v > mx) && ok) raise_err(err, E_CAST_RANGE);
-            sp128(v, lo, hi);
-            break;
-          }
-          case V_SCALEUP_I: if (__builtin_mul_overflow(xa, pow10_64(I.aux), &lo) && ok) raise_err(err, E_DEC_OVF); break;
-          case V_SCALEUP_L: {
-            i128 r;
-            if (mul_ovf128(mk128(xa, xah), pow10_128(I.aux), r) && ok) raise_err(err, E_DEC_OVF);
-            sp128(r, lo, hi);
-            break;
-          }
-          case V_SCALEDN_I: {
-            int64_t p = pow10_64(I.aux), q = xa / p, r = xa % p;
-            int64_t ar = r < 0 ? -r : r;
-            if (2 * ar >= p) q += xa < 0 ? -1 : 1;
-            lo = q;
-            break;
-          }
-          case V_SCALEDN_L: {
-            i128 x = mk128(xa, xah), p = pow10_128(I.aux);
-            i128 q = sdiv128(x, p), r = x - q * p;
-            i128 ar = r < 0 ? -r : r;
-            if (2 * ar >= p) q += x < 0 ? -1 : 1;
-            sp128(q, lo, hi);
-            break;
-          }
-          case V_DEC2F_I: lo = __double_as_longlong((double)xa / (double)pow10_64(I.aux)); break;
-          case V_DEC2F_L: lo = __double_as_longlong(i128_to_double(mk128(xa, xah)) / (double)pow10_128(I.aux)); break;
-          case V_F2DEC_I: case V_F2DEC_L: {
-            double x = rint(__longlong_as_double(xa) * (double)pow10_128(I.aux));
-            bool bad = !(x >= -1.7014118346046923e38 && x < 1.7014118346046923e38);
-            i128 v = bad ? 0 : (i128)x;
-            i128 mn = mk128(P.consts[b].lo, P.consts[b].hi), mx = mk128(P.consts[c].lo, P.consts[c].hi);
-            if ((bad || v < mn || v > mx) && ok) raise_err(err, E_CAST_RANGE);
-            sp128(v, lo, hi);
-            break;
-          }
-          default: break;
-        }
-        break;
-      }
-    }
-    R.lo[(d) * VM_TILE + t] = lo;
-    R.hi[(d) * VM_TILE + t] = hi;
-    R.nl[(d) * VM_TILE + t] = nl;
+    vm_step(P, C, I.op, I.dst, I.a, I.b, I.c, I.aux, row, active, rs, rstep, rf, err);
   }
 }
 

@@ -22,6 +22,7 @@
 
 #include "../../include/duckdb_mb.h"
 #include "engine.h"
+#include "jit.h"
 
 using namespace mbx;
 
@@ -997,6 +998,66 @@ char *duckdb_mbx_explain(duckdb_mb_connection *h, const char *sql, int64_t len) 
   }
 }
 void duckdb_mbx_free(void *p) { free(p); }
+
+// Compiles (hipRTC, gfx950, no GPU needed) the specialised filter and
+// projection kernels of a small fixed program covering loads, constants,
+// integer / 128-bit / double arithmetic, comparisons and three-valued logic.
+// Returns NULL when both compile, else the compiler log (free with
+// duckdb_mbx_free).  MBX_JIT_DUMP=1 prints the generated sources.
+char *duckdb_mbx_jit_selftest(void) {
+  VmProgram p;
+  memset(&p, 0, sizeof(p));
+  dev::VmCols cols;
+  memset(&cols, 0, sizeof(cols));
+  cols.n = 2;
+  cols.c[0].phys = P_I64;
+  cols.c[1].phys = P_I32;
+  auto ins = [&](int op, int d, int a, int b = 0, int c = 0, int aux = 0) {
+    VmIns &I = p.ins[p.n_ins++];
+    I.op = (uint8_t)op;
+    I.dst = (uint8_t)d;
+    I.a = (uint8_t)a;
+    I.b = (uint8_t)b;
+    I.c = (uint8_t)c;
+    I.aux = (uint16_t)aux;
+  };
+  p.n_const = 2;
+  p.consts[0].lo = 24;
+  p.consts[1].lo = 16;
+  ins(V_LOADCOL, 0, 0);
+  ins(V_CONST, 1, 0);
+  ins(V_CMP_I, 2, 0, 1, 0, 4);  // x > 24
+  ins(V_LOADCOL, 3, 1);
+  ins(V_CONST, 4, 1);
+  ins(V_CMP_I, 5, 3, 4, 0, 2);  // k < 16
+  ins(V_AND, 2, 2, 5);
+  ins(V_ADD_I, 6, 0, 3);       // x + k
+  ins(V_I2L, 7, 6);
+  ins(V_MUL_L, 7, 7, 7);
+  ins(V_I2F, 8, 6);
+  ins(V_DIV_F, 8, 8, 8);
+  ins(V_SELECT, 9, 2, 6, 0);
+  p.n_regs = 10;
+  p.pred_reg = 2;
+  p.n_out = 3;
+  p.out_reg[0] = 9;
+  p.out_phys[0] = P_I64;
+  p.out_reg[1] = 7;
+  p.out_phys[1] = P_I128;
+  p.out_reg[2] = 8;
+  p.out_phys[2] = P_F64;
+  std::string log;
+  for (bool filter : {true, false}) {
+    std::string src = jit::Source(p, cols, filter);
+    if (getenv("MBX_JIT_DUMP")) fprintf(stderr, "%s\n", src.c_str());
+    std::string r = jit::CompileCheck(src);
+    if (!r.empty()) log += std::string(filter ? "[filter] " : "[project] ") + r;
+  }
+  if (log.empty()) return nullptr;
+  char *out = (char *)malloc(log.size() + 1);
+  memcpy(out, log.c_str(), log.size() + 1);
+  return out;
+}
 
 int32_t duckdb_mbx_hbm_calibrate(duckdb_mb_connection *h, int64_t bytes, int32_t iters, double *out3) {
   if (!h || !out3) return 0;

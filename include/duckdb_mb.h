@@ -184,6 +184,10 @@ const char *duckdb_mbx_version(void);
  * with duckdb_mb_last_error() set. */
 char *duckdb_mbx_explain(duckdb_mb_connection *handle, const char *sql, int64_t sql_len);
 void duckdb_mbx_free(void *p);
+/* Run-time compiled expression kernels (hipRTC, gfx950): compiles the kernels
+ * of a fixed sample program without a GPU; NULL = ok, else the compiler log
+ * (free with duckdb_mbx_free). */
+char *duckdb_mbx_jit_selftest(void);
 
 /* Columnar bulk ingest (MI355X-native form of the unbound
  * duckdb_mb_append_data_chunk, reference duckdb_native.c:2109-2132):

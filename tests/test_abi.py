@@ -135,3 +135,16 @@ def test_config_keys(mbx):
     assert isinstance(c.set("threads", "abc"), mbx.Err)
     r = mbx.lib.duckdb_mb_connect_with_config(mbx._Arg(":memory:").p, None)
     assert r is None and mbx._str(mbx.lib.duckdb_mb_last_error()) == "config is null"
+
+
+def test_jit_kernels_compile_without_gpu(mbx):
+    # the run-time specialised expression kernels (jit.cpp) compile for gfx950
+    # through hipRTC on a host without a GPU
+    import ctypes
+    f = mbx.lib.duckdb_mbx_jit_selftest
+    f.restype = ctypes.c_void_p
+    r = f()
+    if r:
+        log = ctypes.string_at(r).decode(errors="replace")
+        mbx.lib.duckdb_mbx_free(ctypes.c_void_p(r))
+        raise AssertionError(log[:4000])
