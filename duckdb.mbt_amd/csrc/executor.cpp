@@ -1276,6 +1276,66 @@ static bool FilterMultiAggregate(Engine &e, const DRel &src, const BoundSelect &
   return true;
 }
 
+// Run-time specialised scan -> filter -> project -> aggregate (no GROUP BY):
+// one kernel evaluates the WHERE program and every aggregate argument and
+// accumulates in registers (jit::VmAggregate); nothing is materialised.  false
+// while the kernel is still compiling, or for shapes it does not take
+// (DISTINCT, VARCHAR arguments, MIN/MAX of 128-bit values).
+static bool JitAggregate(Engine &e, const DRel &src, const BoundSelect &s, DRel &out) {
+  const int na = (int)s.aggs.size();
+  if (na > VM_MAX_OUT || src.n <= 0) return false;
+  VmCompiler vc(src, nullptr);
+  try {
+    vc.P.pred_reg = 255;
+    if (s.where) vc.P.pred_reg = (uint8_t)vc.Compile(*s.where);
+    for (int j = 0; j < na; j++) {
+      const AggSpec &a = s.aggs[j];
+      if (a.distinct) return false;
+      if (a.kind == A_COUNT_STAR) {
+        vc.P.out_reg[j] = 255;
+        continue;
+      }
+      VClass c = ClassOf(a.arg->type);
+      if (c == VC_STR) return false;
+      if (c == VC_I128 && (a.kind == A_MIN || a.kind == A_MAX)) return false;
+      vc.P.out_reg[j] = (uint8_t)vc.Compile(*a.arg);
+      vc.P.out_class[j] = (uint8_t)c;
+      // statistics the kernel accumulates: bit0 sum (SUM/AVG), bit1 min/max; COUNT only counts
+      vc.P.out_phys[j] = a.kind == A_SUM || a.kind == A_AVG ? 1 : a.kind == A_MIN || a.kind == A_MAX ? 2 : 4;
+    }
+  } catch (std::exception &) {
+    return false;  // the VM path raises the same error if it applies
+  }
+  vc.P.n_out = na;
+  vc.P.n_regs = vc.high;
+  auto states = Alloc(e, (size_t)std::max(na, 1) * sizeof(dev::AggState));
+  dev::InitAggStates((dev::AggState *)states->p, std::max(na, 1), e.stream);
+  auto cs = Alloc(e, 8, true);
+  bool ok;
+  {
+    ProfScope ps(e, "jit_aggregate", 0, src.n);
+    ok = jit::VmAggregate(vc.P, vc.cols, src.n, src.rs, src.rstep, states->p, (unsigned long long *)cs->p, e.d_err,
+                          e.stream);
+  }
+  if (!ok) return false;
+  out.n = 1;
+  dev::EmitDesc D;
+  memset(&D, 0, sizeof(D));
+  D.nagg = na;
+  D.cstar = (const unsigned long long *)cs->p;
+  D.nslots = 1;
+  D.null_slot = -1;
+  for (int j = 0; j < na; j++) {
+    DCol oc = AllocOut(e, s.aggs[j].type, 1, true, false);
+    VClass ic = s.aggs[j].kind == A_COUNT_STAR ? VC_I64 : ClassOf(s.aggs[j].arg->type);
+    D.a[j] = EmitFor(s.aggs[j], ic, (dev::AggState *)states->p + j, oc);
+    out.cols.push_back(oc);
+  }
+  dev::EmitAggRelation(D, e.stream);
+  HIPCHK(hipStreamSynchronize(e.stream));  // states / count buffers released after the emit
+  return true;
+}
+
 static DRel Aggregate(Engine &e, const DRel &src, const BoundSelect &s) {
   const int ng = (int)s.groups.size();
   const int na = (int)s.aggs.size();
@@ -1494,6 +1554,10 @@ generic:
     if (s.aggs[j].kind == A_COUNT_STAR) continue;
     arg_idx[j] = (int)exprs.size();
     exprs.push_back(s.aggs[j].arg);
+  }
+  if (ng == 0 && jit::Enabled()) {
+    DRel fused;
+    if (JitAggregate(e, src, s, fused)) return fused;
   }
   DRel tmp = FilterProject(e, src, s.where, exprs);
   if (ng == 0) {

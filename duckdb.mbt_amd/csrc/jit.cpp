@@ -16,6 +16,7 @@
 #include <vector>
 
 #include "jit_src.h"  // build/jit_src.h: phys.h + vm.h + vm_device.h as one string
+#include "types.h"
 
 namespace mbx {
 namespace jit {
@@ -54,14 +55,44 @@ extern "C" __global__ __launch_bounds__(256) void mbx_jit_project(mbx::VmProgram
   VmCols Cs = C;
 )";
 
-std::string Body(const VmProgram &p) {
+// Column loads of a program for one row, hoisted ahead of all arithmetic
+// (the loads of every row a thread handles are then in flight together; the
+// values wait in L<k>l/h/n<sfx> until the V_LOADCOL that consumes them).
+std::string Preload(const VmProgram &p, const std::string &sfx, const std::string &lrow, const std::string &act) {
   std::ostringstream o;
   for (int k = 0; k < p.n_ins; k++) {
     const VmIns &I = p.ins[k];
-    o << "      vm_step(P, Cs, " << (int)I.op << ", " << (int)I.dst << ", " << (int)I.a << ", " << (int)I.b << ", "
-      << (int)I.c << ", " << (int)I.aux << ", row, active, rs, rstep, R, err);\n";
+    if (I.op != V_LOADCOL) continue;
+    o << "    int64_t L" << k << "l" << sfx << ", L" << k << "h" << sfx << ";\n"
+      << "    load_phys(Cs.c[" << (int)I.a << "].data, Cs.c[" << (int)I.a << "].phys, " << lrow << ", L" << k << "l"
+      << sfx << ", L" << k << "h" << sfx << ");\n"
+      << "    const uint8_t L" << k << "n" << sfx << " = (" << act << " && bit_valid(Cs.c[" << (int)I.a << "].validity, "
+      << lrow << ")) ? 0 : 1;\n";
   }
   return o.str();
+}
+
+std::string Body(const VmProgram &p, const std::string &sfx = "") {
+  std::ostringstream o;
+  for (int k = 0; k < p.n_ins; k++) {
+    const VmIns &I = p.ins[k];
+    if (I.op == V_LOADCOL) {
+      o << "      R.lo(" << (int)I.dst << ") = L" << k << "l" << sfx << "; R.hi(" << (int)I.dst << ") = L" << k << "h" << sfx
+        << "; R.nl(" << (int)I.dst << ") = L" << k << "n" << sfx << ";\n";
+      continue;
+    }
+    o << "      vm_step<LocalRF, true>(P, Cs, " << (int)I.op << ", " << (int)I.dst << ", " << (int)I.a << ", "
+      << (int)I.b << ", " << (int)I.c << ", " << (int)I.aux << ", lrow, active, rs, rstep, R, err);\n";
+  }
+  return o.str();
+}
+
+// column physical types and the absence of NULL bitmaps are compiled in
+void Specialise(std::ostringstream &o, const dev::VmCols &cols) {
+  for (int q = 0; q < cols.n; q++) {
+    o << "  Cs.c[" << q << "].phys = " << cols.c[q].phys << ";\n";
+    if (!cols.c[q].validity) o << "  Cs.c[" << q << "].validity = nullptr;\n";
+  }
 }
 
 struct Entry {
@@ -123,7 +154,7 @@ std::string CompileToCode(const std::string &src, std::vector<char> *code) {
   return "";
 }
 
-void Build(int device, std::string src, bool filter, std::shared_ptr<Entry> e) {
+void Build(int device, std::string src, std::string name, std::shared_ptr<Entry> e) {
   std::vector<char> code;
   std::string err = CompileToCode(src, &code);
   hipModule_t mod = nullptr;
@@ -131,7 +162,7 @@ void Build(int device, std::string src, bool filter, std::shared_ptr<Entry> e) {
   if (err.empty()) {
     hipSetDevice(device);
     if (hipModuleLoadData(&mod, code.data()) != hipSuccess ||
-        hipModuleGetFunction(&fn, mod, filter ? "mbx_jit_filter" : "mbx_jit_project") != hipSuccess) {
+        hipModuleGetFunction(&fn, mod, name.c_str()) != hipSuccess) {
       (void)hipGetLastError();
       err = "hipModuleLoadData/GetFunction failed";
     }
@@ -144,8 +175,8 @@ void Build(int device, std::string src, bool filter, std::shared_ptr<Entry> e) {
   g_cv.notify_all();
 }
 
-// The compiled kernel for this source on the current device, or nullptr.
-hipFunction_t Get(const std::string &src, bool filter) {
+// The compiled kernel `name` of this source on the current device, or nullptr.
+hipFunction_t GetNamed(const std::string &src, const std::string &name) {
   const int mode = Mode();
   if (mode == 0) return nullptr;
   int device = 0;
@@ -166,18 +197,22 @@ hipFunction_t Get(const std::string &src, bool filter) {
   }
   if (start) {
     if (mode == 2) {
-      Build(device, src, filter, e);
+      Build(device, src, name, e);
     } else {
       static bool registered = (atexit(JoinAll), true);
       (void)registered;
       std::lock_guard<std::mutex> lk(g_mu);
-      S().threads.emplace_back(Build, device, src, filter, e);
+      S().threads.emplace_back(Build, device, src, name, e);
       return nullptr;
     }
   }
   std::unique_lock<std::mutex> lk(g_mu);
   if (mode == 2) g_cv.wait(lk, [&] { return e->state != Entry::PENDING; });
   return e->state == Entry::READY ? e->fn : nullptr;
+}
+
+hipFunction_t Get(const std::string &src, bool filter) {
+  return GetNamed(src, filter ? "mbx_jit_filter" : "mbx_jit_project");
 }
 
 }  // namespace
@@ -192,12 +227,14 @@ std::string Source(const VmProgram &p, const dev::VmCols &cols, bool filter) {
        "  __device__ __forceinline__ uint8_t &nl(int i) { return n[i]; }\n};\n";
   o << (filter ? kFilterHead : kProjectHead);
   // column physical types are part of the specialisation
-  for (int q = 0; q < cols.n; q++) o << "  Cs.c[" << q << "].phys = " << cols.c[q].phys << ";\n";
+  Specialise(o, cols);
   if (filter) {
     o << "  for (int64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {\n"
          "    const int64_t row = tile * VM_TILE + t;\n"
          "    const bool active = row < nrows;\n"
-         "    LocalRF R = {};\n    {\n";
+         "    const int64_t lrow = active ? row : nrows - 1;\n";
+    o << Preload(p, "", "lrow", "active");
+    o << "    LocalRF R = {};\n    {\n";
     o << Body(p);
     o << "    }\n"
          "    const bool sel = active && !R.nl(" << (int)p.pred_reg << ") && R.lo(" << (int)p.pred_reg << ") != 0;\n"
@@ -221,7 +258,9 @@ std::string Source(const VmProgram &p, const dev::VmCols &cols, bool filter) {
          "      out_idx = tile_off[tile] + before + __popcll(lt);\n"
          "    } else {\n      sel = row < nrows;\n      out_idx = row;\n    }\n"
          "    const bool active = sel;\n"
-         "    LocalRF R = {};\n    {\n";
+         "    const int64_t lrow = row < nrows ? row : nrows - 1;\n";
+    o << Preload(p, "", "lrow", "active");
+    o << "    LocalRF R = {};\n    {\n";
     o << Body(p);
     o << "    }\n    if (sel) {\n";
     for (int q = 0; q < p.n_out; q++) {
@@ -238,6 +277,149 @@ std::string Source(const VmProgram &p, const dev::VmCols &cols, bool filter) {
 }
 
 std::string CompileCheck(const std::string &src) { return CompileToCode(src, nullptr); }
+
+bool Enabled() { return Mode() != 0; }
+
+// Source of the fused aggregate kernel (see jit.h, VmAggregate).
+static std::string AggSource(const VmProgram &p, const dev::VmCols &cols) {
+  std::ostringstream o;
+  const int nr = p.n_regs > 0 ? p.n_regs : 1;
+  o << kJitPrelude;
+  o << "\nstruct LocalRF {\n  int64_t l[" << nr << "], h[" << nr << "];\n  uint8_t n[" << nr
+    << "];\n  __device__ __forceinline__ int64_t &lo(int i) { return l[i]; }\n"
+       "  __device__ __forceinline__ int64_t &hi(int i) { return h[i]; }\n"
+       "  __device__ __forceinline__ uint8_t &nl(int i) { return n[i]; }\n};\n"
+       "struct JAggState {\n  unsigned long long count, sum_lo;\n  long long sum_hi, min_i, max_i;\n  double sum_f;\n"
+       "  unsigned long long min_f, max_f;\n};\n"
+       "__device__ __forceinline__ unsigned long long jshfl(unsigned long long v, int m) {\n"
+       "  return (unsigned long long)__shfl_xor((long long)v, m, 64);\n}\n";
+  o << "extern \"C\" __global__ __launch_bounds__(256) void mbx_jit_agg(mbx::VmProgram P, mbx::dev::VmCols C, "
+       "int64_t nrows, int64_t rs, int64_t rstep, JAggState *states, unsigned long long *cstar, int32_t *err) {\n"
+       "  using namespace mbx;\n  using namespace mbx::dev;\n  VmCols Cs = C;\n";
+  Specialise(o, cols);
+  o << "  unsigned long long cs = 0;\n";
+  for (int j = 0; j < p.n_out; j++) {
+    if (p.out_reg[j] == 255) continue;
+    if (p.out_class[j] == VC_F64)
+      o << "  unsigned long long c" << j << " = 0, fmn" << j << " = ~0ull, fmx" << j << " = 0;\n  double sf" << j
+        << " = 0;\n";
+    else
+      o << "  unsigned long long c" << j << " = 0, slo" << j << " = 0;\n  long long shi" << j << " = 0, mn" << j
+        << " = INT64_MAX, mx" << j << " = INT64_MIN;\n";
+  }
+  // JIT_U rows per thread and iteration: U independent register files, so
+  // the column loads of all U rows are in flight together
+  int U = 4;
+  if (const char *e = getenv("MBX_JIT_U")) U = atoi(e) == 1 || atoi(e) == 2 || atoi(e) == 8 ? atoi(e) : 4;
+  o << "  const int64_t S = (int64_t)gridDim.x * blockDim.x;\n"
+       "  for (int64_t base = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; base < nrows; base += " << U << " * S) {\n";
+  for (int u = 0; u < U; u++) {
+    o << "    const int64_t row" << u << " = base + " << u << " * S;\n    const bool act" << u << " = row" << u
+      << " < nrows;\n    const int64_t lrow" << u << " = act" << u << " ? row" << u << " : nrows - 1;\n    LocalRF R" << u
+      << " = {};\n";
+  }
+  for (int u = 0; u < U; u++) o << Preload(p, std::to_string(u), "lrow" + std::to_string(u), "act" + std::to_string(u));
+  for (int u = 0; u < U; u++) {
+    o << "    {\n      const int64_t lrow = lrow" << u << ";\n      const bool active = act" << u
+      << ";\n      LocalRF &R = R" << u << ";\n";
+    o << Body(p, std::to_string(u));
+    o << "    }\n";
+  }
+  o << "#pragma unroll\n    for (int u = 0; u < " << U << "; u++) {\n      LocalRF &R = ";
+  for (int u = 0; u < U - 1; u++) o << "u == " << u << " ? R" << u << " : ";
+  o << "R" << U - 1 << ";\n      const bool act = ";
+  for (int u = 0; u < U - 1; u++) o << "u == " << u << " ? act" << u << " : ";
+  o << "act" << U - 1 << ";\n";
+  if (p.pred_reg != 255)
+    o << "    const bool sel = act && !R.nl(" << (int)p.pred_reg << ") && R.lo(" << (int)p.pred_reg << ") != 0;\n";
+  else
+    o << "    const bool sel = act;\n";
+  o << "    cs += sel;\n";
+  for (int j = 0; j < p.n_out; j++) {
+    const int r = p.out_reg[j];
+    if (r == 255) continue;
+    // bit0: sum, bit1: min/max.  All statistics by default: the lean variant
+    // (only what the aggregate kind needs) measured 1.6x slower at 1e8 rows,
+    // the scheduler sinks the hoisted loads when the loop body is short
+    // (profiles/r01_jit_sweep.log); MBX_JIT_LEAN=1 selects it.
+    int need = 3;
+    if (getenv("MBX_JIT_LEAN") && p.out_phys[j]) need = p.out_phys[j];
+    o << "    if (sel && !R.nl(" << r << ")) {\n      c" << j << "++;\n";
+    if (p.out_class[j] == VC_F64) {
+      o << "      const double d = __longlong_as_double(R.lo(" << r << "));\n";
+      if (need & 1) o << "      sf" << j << " += d;\n";
+      if (need & 2)
+        o << "      const unsigned long long k = f64_order(d);\n      fmn" << j << " = k < fmn" << j << " ? k : fmn" << j
+          << ";\n      fmx" << j << " = k > fmx" << j << " ? k : fmx" << j << ";\n";
+    } else {
+      o << "      const long long v = R.lo(" << r << "), vh = R.hi(" << r << ");\n";
+      if (need & 1)
+        o << "      const unsigned long long nlo = slo" << j << " + (unsigned long long)v;\n"
+             "      shi" << j << " += vh + (nlo < slo" << j << " ? 1 : 0);\n      slo" << j << " = nlo;\n";
+      if (need & 2)
+        o << "      mn" << j << " = v < mn" << j << " ? v : mn" << j << ";\n      mx" << j << " = v > mx" << j << " ? v : mx" << j
+          << ";\n";
+    }
+    o << "    }\n";
+  }
+  o << "    }\n  }\n  const int lane = threadIdx.x & 63;\n";
+  // wave reductions, then one set of atomics per wave
+  o << "  for (int m = 32; m >= 1; m >>= 1) {\n    cs += jshfl(cs, m);\n";
+  for (int j = 0; j < p.n_out; j++) {
+    if (p.out_reg[j] == 255) continue;
+    if (p.out_class[j] == VC_F64) {
+      o << "    c" << j << " += jshfl(c" << j << ", m);\n    sf" << j << " += __shfl_xor(sf" << j << ", m, 64);\n"
+        << "    { unsigned long long x = jshfl(fmn" << j << ", m); fmn" << j << " = x < fmn" << j << " ? x : fmn" << j
+        << "; x = jshfl(fmx" << j << ", m); fmx" << j << " = x > fmx" << j << " ? x : fmx" << j << "; }\n";
+    } else {
+      // 128-bit sum: add the partner's (lo, hi) with carry
+      o << "    c" << j << " += jshfl(c" << j << ", m);\n"
+        << "    { unsigned long long ol = jshfl(slo" << j << ", m); long long oh = (long long)jshfl((unsigned long long)shi"
+        << j << ", m);\n      unsigned long long nl2 = slo" << j << " + ol; shi" << j << " += oh + (nl2 < slo" << j
+        << " ? 1 : 0); slo" << j << " = nl2;\n"
+        << "      long long a = (long long)jshfl((unsigned long long)mn" << j << ", m); mn" << j << " = a < mn" << j
+        << " ? a : mn" << j << ";\n      a = (long long)jshfl((unsigned long long)mx" << j << ", m); mx" << j << " = a > mx"
+        << j << " ? a : mx" << j << "; }\n";
+    }
+  }
+  o << "  }\n  if (lane == 0) {\n    if (cs) atomicAdd(cstar, cs);\n";
+  for (int j = 0; j < p.n_out; j++) {
+    if (p.out_reg[j] == 255) continue;
+    o << "    if (c" << j << ") {\n      JAggState *st = states + " << j << ";\n      atomicAdd(&st->count, c" << j << ");\n";
+    if (p.out_class[j] == VC_F64) {
+      o << "      atomicAdd(&st->sum_f, sf" << j << ");\n      atomicMin(&st->min_f, fmn" << j
+        << ");\n      atomicMax(&st->max_f, fmx" << j << ");\n";
+    } else {
+      o << "      const unsigned long long old = atomicAdd(&st->sum_lo, slo" << j << ");\n"
+           "      const unsigned long long carry = (old + slo" << j << ") < old ? 1ull : 0ull;\n"
+           "      atomicAdd((unsigned long long *)&st->sum_hi, (unsigned long long)shi" << j << " + carry);\n"
+           "      atomicMin(&st->min_i, mn" << j << ");\n      atomicMax(&st->max_i, mx" << j << ");\n";
+    }
+    o << "    }\n";
+  }
+  o << "  }\n}\n";
+  return o.str();
+}
+
+std::string AggSourceForTest(const VmProgram &p, const dev::VmCols &cols) { return AggSource(p, cols); }
+
+bool VmAggregate(const VmProgram &p, const dev::VmCols &cols, int64_t nrows, int64_t range_start, int64_t range_step,
+                 void *states, unsigned long long *count_star, int32_t *err, hipStream_t s) {
+  if (nrows <= 0) return false;
+  const std::string src = AggSource(p, cols);
+  hipFunction_t fn = GetNamed(src, "mbx_jit_agg");
+  if (!fn) return false;
+  VmProgram P = p;
+  dev::VmCols C = cols;
+  void *args[] = {&P, &C, &nrows, &range_start, &range_step, &states, &count_star, &err};
+  int cus = 0, d = 0;
+  (void)hipGetDevice(&d);
+  (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, d);
+  if (cus <= 0) cus = 256;
+  int64_t g = (nrows + 255) / 256;
+  if (g > (int64_t)cus * 8) g = (int64_t)cus * 8;
+  return hipModuleLaunchKernel(fn, (unsigned)g, 1, 1, 256, 1, 1, 0, s, args, nullptr) == hipSuccess;
+}
 
 static int GridFor(int64_t ntiles) {
   int cus = 0, d = 0;

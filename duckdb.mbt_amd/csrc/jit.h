@@ -29,11 +29,22 @@ bool VmFilter(const VmProgram &p, const dev::VmCols &cols, int64_t nrows, int64_
 bool VmProject(const VmProgram &p, const dev::VmCols &cols, int64_t nrows, int64_t range_start, int64_t range_step,
                const uint64_t *sel_bits, const int64_t *tile_offsets, const dev::VmOuts &outs, int32_t *err,
                hipStream_t s);
+// Fused scan -> filter -> project -> aggregate without GROUP BY: evaluates
+// the predicate register p.pred_reg (255 = none) and, per aggregate j <
+// p.n_out, the argument register p.out_reg[j] (255 = COUNT(*)) of class
+// p.out_class[j] (VC_I64 / VC_I128 sums / VC_F64), and merges every wave's
+// accumulators into states[j] (dev::AggState layout, pre-initialised) and the
+// selected-row count into *count_star.  true: launched.
+bool VmAggregate(const VmProgram &p, const dev::VmCols &cols, int64_t nrows, int64_t range_start, int64_t range_step,
+                 void *states, unsigned long long *count_star, int32_t *err, hipStream_t s);
+bool Enabled();
+
 // The generated source for a program (exposed for tests and EXPLAIN).
 std::string Source(const VmProgram &p, const dev::VmCols &cols, bool filter);
 // Compiles source for gfx950 without loading it (no GPU needed); "" = ok,
 // else the compiler log.
 std::string CompileCheck(const std::string &src);
+std::string AggSourceForTest(const VmProgram &p, const dev::VmCols &cols);
 
 }  // namespace jit
 }  // namespace mbx

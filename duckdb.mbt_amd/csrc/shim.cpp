@@ -1053,6 +1053,19 @@ char *duckdb_mbx_jit_selftest(void) {
     std::string r = jit::CompileCheck(src);
     if (!r.empty()) log += std::string(filter ? "[filter] " : "[project] ") + r;
   }
+  // the fused aggregate kernel: SUM(x + k) (int), SUM(double), COUNT(*) WHERE x > 24 AND k < 16
+  p.n_out = 3;
+  p.out_reg[0] = 6;
+  p.out_class[0] = VC_I64;
+  p.out_reg[1] = 8;
+  p.out_class[1] = VC_F64;
+  p.out_reg[2] = 255;
+  {
+    std::string src = jit::AggSourceForTest(p, cols);
+    if (getenv("MBX_JIT_DUMP")) fprintf(stderr, "%s\n", src.c_str());
+    std::string r = jit::CompileCheck(src);
+    if (!r.empty()) log += "[aggregate] " + r;
+  }
   if (log.empty()) return nullptr;
   char *out = (char *)malloc(log.size() + 1);
   memcpy(out, log.c_str(), log.size() + 1);

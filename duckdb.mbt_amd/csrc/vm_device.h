@@ -178,7 +178,10 @@ __device__ __forceinline__ bool cmp_res(int c, int k) {
 
 // One VM instruction for the calling thread's row.  RF is the register file:
 // lo(i) / hi(i) / nl(i) return references to register i of this row.
-template <class RF>
+// UNCOND (run-time compiled kernels): `row` is always a valid row index, so
+// column loads are issued unconditionally (no branch between a row's loads)
+// and `active` only masks validity and error reporting.
+template <class RF, bool UNCOND = false>
 __device__ __forceinline__ void vm_step(const VmProgram &P, const VmCols &C, int op, int d, int a, int b, int c,
                                         int aux, int64_t row, bool active, int64_t rs, int64_t rstep, RF &R,
                                         int32_t *err) {
@@ -187,7 +190,10 @@ __device__ __forceinline__ void vm_step(const VmProgram &P, const VmCols &C, int
     switch (op) {
       case V_LOADCOL: {
         const VmCol &col = C.c[a];
-        if (active) {
+        if (UNCOND) {
+          nl = (active && bit_valid(col.validity, row)) ? 0 : 1;
+          load_phys(col.data, col.phys, row, lo, hi);
+        } else if (active) {
           nl = bit_valid(col.validity, row) ? 0 : 1;
           load_phys(col.data, col.phys, row, lo, hi);
         } else {
