@@ -1359,6 +1359,14 @@ bool GroupByDirectStates(const void *kcol, int kphys, int64_t kmin, int nk, cons
     bool use = nv > 0 || pr.n != 0;  // the segmented kernel has no predicate
     const char *e = getenv("MBX_GD_VARIANT");
     if (e && *e) use = sscanf(e, "d%d_g%d", &depth, &gpc) == 2 || pr.n != 0;
+    // MBX_GD_R=<r>: fewer replicas (experiment; seg_rows scales with R)
+    if (const char *er = getenv("MBX_GD_R")) {
+      int r = atoi(er);
+      while (use && r > 0 && R > r) {
+        R >>= 1;
+        if (seg_rows > 0) seg_rows >>= 1;
+      }
+    }
     if (use) {
       int grid = grid_blocks > 0 ? grid_blocks : NumCUs() * gpc;
       int64_t nsteps = nrows >> 8;

@@ -21,13 +21,19 @@ c.query(f"CREATE TABLE t AS SELECT CAST(mbx_synth(7, i, 32) AS INTEGER) AS k, "
 variants = os.environ.get("SWEEP_VARIANTS", "seg,d2_g1,d3_g1,d4_g1,d2_g2,d3_g2").split(",")
 rounds = int(os.environ.get("SWEEP_ROUNDS", "7"))
 sqls = {"c3": "SELECT k, SUM(v), COUNT(*) FROM t GROUP BY k", "count": "SELECT k, COUNT(*) FROM t GROUP BY k"}
+if os.environ.get("SWEEP_SQLS"):
+    sqls = {k: v for k, v in sqls.items() if k in os.environ["SWEEP_SQLS"].split(",")}
 res = {}
 ref = {}
 for name, sql in sqls.items():
     times = {v: [] for v in variants}
     for rnd in range(rounds):
         for v in (variants if rnd % 2 == 0 else variants[::-1]):
-            os.environ["MBX_GD_VARIANT"] = v
+            os.environ["MBX_GD_VARIANT"] = v.split("+")[0]
+            if "+r" in v:
+                os.environ["MBX_GD_R"] = v.split("+r")[1]
+            else:
+                os.environ.pop("MBX_GD_R", None)
             r = c.query(sql)
             assert isinstance(r, m.Ok), r
             rows = sorted(r.value.rows)
