@@ -41,7 +41,7 @@ def _worker(rank, world, port, n, q):
     q.put((rank, gc, gs, tc, big))
 
 
-@pytest.mark.parametrize("world", [2])
+@pytest.mark.parametrize("world", [2, 4])
 def test_global_count_sum_gloo(world):
     n = 200_000
     ctx = mp.get_context("spawn")
@@ -59,7 +59,7 @@ def test_global_count_sum_gloo(world):
     c, s = Oracle().synth_filter_count(42, 0, n * world, 50, 1, 25, 2**63 - 1, 4)
     for rank, gc, gs, tc, big in out:
         assert (gc, gs, tc) == (c, s, c)
-        assert big == [[-(2**100), -(2**63)], [2**100 + 1, -(2**63) - 1]]
+        assert big == [[(2**100 + r) * (1 if r else -1), -(2**63) - r] for r in range(world)]
 
 
 def test_i128_codec():
