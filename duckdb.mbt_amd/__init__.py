@@ -26,6 +26,7 @@ module raises.
 """
 from __future__ import annotations
 
+import atexit
 import ctypes
 import math
 import os
@@ -68,6 +69,8 @@ _sig("duckdb_mbx_bytes_len", _I, _B)
 _sig("duckdb_mbx_bytes_free", None, _B)
 _sig("duckdb_mbx_free", None, _P)
 _sig("duckdb_mbx_device_count", _I)
+_sig("duckdb_mbx_jit_join", None)
+atexit.register(lib.duckdb_mbx_jit_join)  # before exit() tears hipRTC down (jit.h)
 _sig("duckdb_mbx_explain", ctypes.c_void_p, _P, ctypes.c_char_p, _L)
 _sig("duckdb_mbx_last_profile", ctypes.c_void_p, _P)
 _sig("duckdb_mbx_profile_drain", ctypes.c_void_p, _P)

@@ -11,6 +11,7 @@
 #include <memory>
 #include <mutex>
 #include <sstream>
+#include <vector>
 #include <string>
 #include <thread>
 #include <vector>
@@ -307,29 +308,80 @@ static std::string AggSource(const VmProgram &p, const dev::VmCols &cols) {
       o << "  unsigned long long c" << j << " = 0, slo" << j << " = 0;\n  long long shi" << j << " = 0, mn" << j
         << " = INT64_MAX, mx" << j << " = INT64_MIN;\n";
   }
-  // JIT_U rows per thread and iteration: U independent register files, so
-  // the column loads of all U rows are in flight together
+  // Rows per thread and iteration: NR independent register files, so the
+  // column loads of all NR rows are in flight together.  Default: U single
+  // rows strided by the grid.  MBX_JIT_PAIRS=1: U pairs of consecutive rows,
+  // an 8-byte (4-byte) column of a full pair fetched with ONE 16-byte (8-byte)
+  // load -- measured no faster (profiles/r01_jit_sweep.log), kept for sweeps.
   int U = 4;
   if (const char *e = getenv("MBX_JIT_U")) U = atoi(e) == 1 || atoi(e) == 2 || atoi(e) == 8 ? atoi(e) : 4;
+  const char *pe = getenv("MBX_JIT_PAIRS");
+  const bool pairs = pe && strcmp(pe, "1") == 0;
+  const int NR = pairs ? 2 * U : U;
+  const int64_t span = pairs ? 2 : 1;
   o << "  const int64_t S = (int64_t)gridDim.x * blockDim.x;\n"
-       "  for (int64_t base = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; base < nrows; base += " << U << " * S) {\n";
+       "  const int64_t nunits = (nrows + " << span - 1 << ") / " << span << ";\n"
+       "  for (int64_t base = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; base < nunits; base += " << U << " * S) {\n";
   for (int u = 0; u < U; u++) {
-    o << "    const int64_t row" << u << " = base + " << u << " * S;\n    const bool act" << u << " = row" << u
-      << " < nrows;\n    const int64_t lrow" << u << " = act" << u << " ? row" << u << " : nrows - 1;\n    LocalRF R" << u
-      << " = {};\n";
+    o << "    const int64_t unit" << u << " = base + " << u << " * S;\n";
+    for (int h = 0; h < span; h++) {
+      const int r = u * span + h;
+      o << "    const int64_t row" << r << " = unit" << u << " * " << span << " + " << h << ";\n    const bool act" << r
+        << " = row" << r << " < nrows;\n    const int64_t lrow" << r << " = act" << r << " ? row" << r
+        << " : nrows - 1;\n    LocalRF R" << r << " = {};\n";
+    }
   }
-  for (int u = 0; u < U; u++) o << Preload(p, std::to_string(u), "lrow" + std::to_string(u), "act" + std::to_string(u));
-  for (int u = 0; u < U; u++) {
-    o << "    {\n      const int64_t lrow = lrow" << u << ";\n      const bool active = act" << u
-      << ";\n      LocalRF &R = R" << u << ";\n";
-    o << Body(p, std::to_string(u));
+  if (pairs) {
+    for (int u = 0; u < U; u++) {
+      const std::string a = std::to_string(2 * u), b = std::to_string(2 * u + 1);
+      o << "    const bool full" << u << " = act" << b << ";\n";
+      for (int k = 0; k < p.n_ins; k++) {
+        const VmIns &I = p.ins[k];
+        if (I.op != V_LOADCOL) continue;
+        const int ph = cols.c[I.a].phys;
+        const bool nov = cols.c[I.a].validity == nullptr;
+        const std::string ca = "Cs.c[" + std::to_string((int)I.a) + "]";
+        o << "    int64_t L" << k << "l" << a << ", L" << k << "h" << a << ", L" << k << "l" << b << ", L" << k << "h" << b
+          << ";\n";
+        const char *vt = (ph == P_I64 || ph == P_F64 || ph == P_U64) ? "long long" : ph == P_I32 ? "int" : nullptr;
+        if (vt && nov) {
+          o << "    if (full" << u << ") {\n      typedef " << vt << " vv __attribute__((ext_vector_type(2)));\n"
+            << "      const vv t = ((const vv *)" << ca << ".data)[unit" << u << "];\n"
+            << "      L" << k << "l" << a << " = (long long)t.x; L" << k << "l" << b << " = (long long)t.y;\n";
+          if (ph == P_U64)
+            o << "      L" << k << "h" << a << " = 0; L" << k << "h" << b << " = 0;\n";
+          else if (ph == P_F64)
+            o << "      L" << k << "h" << a << " = 0; L" << k << "h" << b << " = 0;\n";
+          else
+            o << "      L" << k << "h" << a << " = L" << k << "l" << a << " >> 63; L" << k << "h" << b << " = L" << k << "l"
+              << b << " >> 63;\n";
+          o << "    } else {\n";
+        } else {
+          o << "    {\n";
+        }
+        o << "      load_phys(" << ca << ".data, " << ca << ".phys, lrow" << a << ", L" << k << "l" << a << ", L" << k << "h"
+          << a << ");\n      load_phys(" << ca << ".data, " << ca << ".phys, lrow" << b << ", L" << k << "l" << b << ", L"
+          << k << "h" << b << ");\n    }\n";
+        o << "    const uint8_t L" << k << "n" << a << " = (act" << a << " && bit_valid(" << ca << ".validity, lrow" << a
+          << ")) ? 0 : 1;\n    const uint8_t L" << k << "n" << b << " = (act" << b << " && bit_valid(" << ca
+          << ".validity, lrow" << b << ")) ? 0 : 1;\n";
+      }
+    }
+  } else {
+    for (int r = 0; r < NR; r++)
+      o << Preload(p, std::to_string(r), "lrow" + std::to_string(r), "act" + std::to_string(r));
+  }
+  for (int r = 0; r < NR; r++) {
+    o << "    {\n      const int64_t lrow = lrow" << r << ";\n      const bool active = act" << r
+      << ";\n      LocalRF &R = R" << r << ";\n";
+    o << Body(p, std::to_string(r));
     o << "    }\n";
   }
-  o << "#pragma unroll\n    for (int u = 0; u < " << U << "; u++) {\n      LocalRF &R = ";
-  for (int u = 0; u < U - 1; u++) o << "u == " << u << " ? R" << u << " : ";
-  o << "R" << U - 1 << ";\n      const bool act = ";
-  for (int u = 0; u < U - 1; u++) o << "u == " << u << " ? act" << u << " : ";
-  o << "act" << U - 1 << ";\n";
+  o << "#pragma unroll\n    for (int u = 0; u < " << NR << "; u++) {\n      LocalRF &R = ";
+  for (int r = 0; r < NR - 1; r++) o << "u == " << r << " ? R" << r << " : ";
+  o << "R" << NR - 1 << ";\n      const bool act = ";
+  for (int r = 0; r < NR - 1; r++) o << "u == " << r << " ? act" << r << " : ";
+  o << "act" << NR - 1 << ";\n";
   if (p.pred_reg != 255)
     o << "    const bool sel = act && !R.nl(" << (int)p.pred_reg << ") && R.lo(" << (int)p.pred_reg << ") != 0;\n";
   else
@@ -362,27 +414,72 @@ static std::string AggSource(const VmProgram &p, const dev::VmCols &cols) {
     }
     o << "    }\n";
   }
-  o << "    }\n  }\n  const int lane = threadIdx.x & 63;\n";
-  // wave reductions, then one set of atomics per wave
-  o << "  for (int m = 32; m >= 1; m >>= 1) {\n    cs += jshfl(cs, m);\n";
+  o << "    }\n  }\n";
+  // Reduce every running statistic over the wave (shuffles), then over the
+  // block's four waves (LDS), so each block issues ONE set of atomics: with
+  // 2048 blocks the per-wave variant spent a visible part of the kernel on
+  // same-address atomics.  Kinds: 0 u64 add, 1 s64 min, 2 s64 max, 3 f64 add,
+  // 4 u64 min, 5 u64 max, 6 int128 add (lo, hi in two slots).
+  struct RV { std::string lo, hi; int kind; };
+  std::vector<RV> rv = {{"cs", "", 0}};
   for (int j = 0; j < p.n_out; j++) {
     if (p.out_reg[j] == 255) continue;
+    const std::string J = std::to_string(j);
+    rv.push_back({"c" + J, "", 0});
     if (p.out_class[j] == VC_F64) {
-      o << "    c" << j << " += jshfl(c" << j << ", m);\n    sf" << j << " += __shfl_xor(sf" << j << ", m, 64);\n"
-        << "    { unsigned long long x = jshfl(fmn" << j << ", m); fmn" << j << " = x < fmn" << j << " ? x : fmn" << j
-        << "; x = jshfl(fmx" << j << ", m); fmx" << j << " = x > fmx" << j << " ? x : fmx" << j << "; }\n";
+      rv.push_back({"sf" + J, "", 3});
+      rv.push_back({"fmn" + J, "", 4});
+      rv.push_back({"fmx" + J, "", 5});
     } else {
-      // 128-bit sum: add the partner's (lo, hi) with carry
-      o << "    c" << j << " += jshfl(c" << j << ", m);\n"
-        << "    { unsigned long long ol = jshfl(slo" << j << ", m); long long oh = (long long)jshfl((unsigned long long)shi"
-        << j << ", m);\n      unsigned long long nl2 = slo" << j << " + ol; shi" << j << " += oh + (nl2 < slo" << j
-        << " ? 1 : 0); slo" << j << " = nl2;\n"
-        << "      long long a = (long long)jshfl((unsigned long long)mn" << j << ", m); mn" << j << " = a < mn" << j
-        << " ? a : mn" << j << ";\n      a = (long long)jshfl((unsigned long long)mx" << j << ", m); mx" << j << " = a > mx"
-        << j << " ? a : mx" << j << "; }\n";
+      rv.push_back({"slo" + J, "shi" + J, 6});
+      rv.push_back({"mn" + J, "", 1});
+      rv.push_back({"mx" + J, "", 2});
     }
   }
-  o << "  }\n  if (lane == 0) {\n    if (cs) atomicAdd(cstar, cs);\n";
+  // combine (x, xh) <- (x, xh) op (y, yh); y/yh are expressions of 64-bit bits
+  auto comb = [&](const RV &v, const std::string &y, const std::string &yh) {
+    const std::string &x = v.lo;
+    switch (v.kind) {
+      case 0: return "    " + x + " += " + y + ";\n";
+      case 1: return "    { const long long t = (long long)(" + y + "); " + x + " = t < " + x + " ? t : " + x + "; }\n";
+      case 2: return "    { const long long t = (long long)(" + y + "); " + x + " = t > " + x + " ? t : " + x + "; }\n";
+      case 3: return "    " + x + " += __longlong_as_double((long long)(" + y + "));\n";
+      case 4: return "    { const unsigned long long t = " + y + "; " + x + " = t < " + x + " ? t : " + x + "; }\n";
+      case 5: return "    { const unsigned long long t = " + y + "; " + x + " = t > " + x + " ? t : " + x + "; }\n";
+      default:
+        return "    { const unsigned long long t = " + y + "; const long long th = (long long)(" + yh +
+               "); const unsigned long long s2 = " + x + " + t; " + v.hi + " += th + (s2 < " + x + " ? 1 : 0); " + x +
+               " = s2; }\n";
+    }
+  };
+  auto bits = [](const RV &v, const std::string &x) {
+    return v.kind == 3 ? "(unsigned long long)__double_as_longlong(" + x + ")" : "(unsigned long long)" + x;
+  };
+  int nslot = 0;
+  for (const RV &v : rv) nslot += v.kind == 6 ? 2 : 1;
+  o << "  for (int m = 32; m >= 1; m >>= 1) {\n";
+  for (const RV &v : rv)
+    o << comb(v, "jshfl(" + bits(v, v.lo) + ", m)", v.kind == 6 ? "jshfl(" + bits(v, v.hi) + ", m)" : "");
+  o << "  }\n  __shared__ unsigned long long jred[4][" << nslot << "];\n  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;\n"
+    << "  if (lane == 0) {\n";
+  {
+    int k = 0;
+    for (const RV &v : rv) {
+      o << "    jred[wv][" << k++ << "] = " << bits(v, v.lo) << ";\n";
+      if (v.kind == 6) o << "    jred[wv][" << k++ << "] = " << bits(v, v.hi) << ";\n";
+    }
+  }
+  o << "  }\n  __syncthreads();\n  if (threadIdx.x != 0) return;\n  for (int w = 1; w < (int)(blockDim.x >> 6); w++) {\n";
+  {
+    int k = 0;
+    for (const RV &v : rv) {
+      const std::string y = "jred[w][" + std::to_string(k++) + "]";
+      const std::string yh = v.kind == 6 ? "jred[w][" + std::to_string(k++) + "]" : "";
+      o << comb(v, y, yh);
+    }
+  }
+  o << "  }\n";
+  o << "  {\n    if (cs) atomicAdd(cstar, cs);\n";
   for (int j = 0; j < p.n_out; j++) {
     if (p.out_reg[j] == 255) continue;
     o << "    if (c" << j << ") {\n      JAggState *st = states + " << j << ";\n      atomicAdd(&st->count, c" << j << ");\n";
@@ -403,6 +500,8 @@ static std::string AggSource(const VmProgram &p, const dev::VmCols &cols) {
 
 std::string AggSourceForTest(const VmProgram &p, const dev::VmCols &cols) { return AggSource(p, cols); }
 
+void JoinPending() { JoinAll(); }
+
 bool VmAggregate(const VmProgram &p, const dev::VmCols &cols, int64_t nrows, int64_t range_start, int64_t range_step,
                  void *states, unsigned long long *count_star, int32_t *err, hipStream_t s) {
   if (nrows <= 0) return false;
@@ -416,8 +515,11 @@ bool VmAggregate(const VmProgram &p, const dev::VmCols &cols, int64_t nrows, int
   (void)hipGetDevice(&d);
   (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, d);
   if (cus <= 0) cus = 256;
+  // 4 blocks per CU (profiles/r01_jit_sweep.log: 0.384 ms vs 0.408 at 8)
+  int bpc = 4;
+  if (const char *e = getenv("MBX_JIT_BPC")) bpc = atoi(e) >= 1 && atoi(e) <= 32 ? atoi(e) : 4;
   int64_t g = (nrows + 255) / 256;
-  if (g > (int64_t)cus * 8) g = (int64_t)cus * 8;
+  if (g > (int64_t)cus * bpc) g = (int64_t)cus * bpc;
   return hipModuleLaunchKernel(fn, (unsigned)g, 1, 1, 256, 1, 1, 0, s, args, nullptr) == hipSuccess;
 }
 

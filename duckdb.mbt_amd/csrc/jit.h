@@ -38,6 +38,11 @@ bool VmProject(const VmProgram &p, const dev::VmCols &cols, int64_t nrows, int64
 bool VmAggregate(const VmProgram &p, const dev::VmCols &cols, int64_t nrows, int64_t range_start, int64_t range_step,
                  void *states, unsigned long long *count_star, int32_t *err, hipStream_t s);
 bool Enabled();
+// Waits for every background compile.  Called on disconnect and from the
+// Python binding's atexit: a compile still inside hipRTC while exit() runs
+// the compiler's static destructors (registered after ours, so run first)
+// can hang the process.
+void JoinPending();
 
 // The generated source for a program (exposed for tests and EXPLAIN).
 std::string Source(const VmProgram &p, const dev::VmCols &cols, bool filter);

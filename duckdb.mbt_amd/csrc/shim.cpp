@@ -177,6 +177,7 @@ duckdb_mb_connection *duckdb_mb_connect(moonbit_bytes_t path) {  // ref duckdb_n
 }
 
 void duckdb_mb_disconnect(duckdb_mb_connection *h) {  // ref :133-140
+  jit::JoinPending();
   delete h;
 }
 
@@ -1004,6 +1005,8 @@ void duckdb_mbx_free(void *p) { free(p); }
 // integer / 128-bit / double arithmetic, comparisons and three-valued logic.
 // Returns NULL when both compile, else the compiler log (free with
 // duckdb_mbx_free).  MBX_JIT_DUMP=1 prints the generated sources.
+void duckdb_mbx_jit_join(void) { jit::JoinPending(); }
+
 char *duckdb_mbx_jit_selftest(void) {
   VmProgram p;
   memset(&p, 0, sizeof(p));

@@ -188,6 +188,10 @@ void duckdb_mbx_free(void *p);
  * of a fixed sample program without a GPU; NULL = ok, else the compiler log
  * (free with duckdb_mbx_free). */
 char *duckdb_mbx_jit_selftest(void);
+/* Waits for pending background kernel compiles (also done by
+ * duckdb_mb_disconnect).  Hosts that exit without disconnecting call it
+ * first: exit() must not tear the compiler down under a running compile. */
+void duckdb_mbx_jit_join(void);
 
 /* Columnar bulk ingest (MI355X-native form of the unbound
  * duckdb_mb_append_data_chunk, reference duckdb_native.c:2109-2132):
