@@ -179,6 +179,7 @@ struct EmitAgg {
   uint32_t *valid;   // zeroed bitmap words
 };
 #define EMIT_MAX_AGGS 16
+#define EMIT_MAX_CKEYS 4
 struct EmitDesc {
   int32_t nagg;
   EmitAgg a[EMIT_MAX_AGGS];
@@ -192,6 +193,15 @@ struct EmitDesc {
   int64_t null_slot;  // -1 if none
   void *key_out;
   uint32_t *key_valid;
+  // composite keys (instead of has_key): key q of slot sl is kmin + digit,
+  // digit = (sl / stride) % radix; NULL when nullable and digit == radix - 1
+  int32_t nkeys_c;
+  struct {
+    void *out;
+    uint32_t *valid;
+    int32_t phys, nullable;
+    int64_t kmin, radix, stride;
+  } kc[EMIT_MAX_CKEYS];
   // optional: reduce these per-workgroup partials into slot 0 first
   // (states of every aggregate and cstar[0]); emit then runs one workgroup
   const AggPartial *partials;

@@ -6,12 +6,12 @@
 
 #include <condition_variable>
 #include <cstdlib>
+#include <algorithm>
 #include <cstring>
 #include <map>
 #include <memory>
 #include <mutex>
 #include <sstream>
-#include <vector>
 #include <string>
 #include <thread>
 #include <vector>
@@ -499,6 +499,188 @@ static std::string AggSource(const VmProgram &p, const dev::VmCols &cols) {
 }
 
 std::string AggSourceForTest(const VmProgram &p, const dev::VmCols &cols) { return AggSource(p, cols); }
+
+// ---- fused GROUP BY (jit.h, VmGroupAggregate) ------------------------------
+
+// Kernel argument mirror of the generated `struct JGroup`.
+struct JGroupArg {
+  int64_t kmin[JIT_MAX_KEYS], radix[JIT_MAX_KEYS], stride[JIT_MAX_KEYS];
+  int32_t nslots, R;
+};
+
+static bool ArgSum(const VmProgram &p, int j) { return (p.out_phys[j] & 1) != 0; }
+static bool ArgMM(const VmProgram &p, int j) { return (p.out_phys[j] & 2) != 0; }
+
+size_t GroupLdsBytes(const VmProgram &p, int64_t nslots, int R) {
+  const size_t ns = (size_t)nslots * R, a4 = (ns * 4 + 7) & ~(size_t)7;
+  size_t b = a4;  // COUNT(*) per slot
+  for (int j = 0; j < p.n_out; j++) {
+    if (p.out_reg[j] == 255) continue;
+    b += a4;                              // NULL arguments per slot
+    if (ArgSum(p, j)) b += ns * 8 + a4;  // int64 sum + signed wrap count
+    if (ArgMM(p, j)) b += ns * 16;
+  }
+  return b;
+}
+
+// The kernel: U rows per thread (hoisted loads, as the aggregate kernel),
+// every selected row adds into a replica of its slot in LDS (lane % R picks
+// the replica); sums are int64 in LDS with the rare signed wrap counted apart
+// (exact int128 on merge).  One merge per block and slot at the end.
+static std::string GroupSource(const VmProgram &p, const dev::VmCols &cols, const GroupSpec &g) {
+  std::ostringstream o;
+  const int nr = p.n_regs > 0 ? p.n_regs : 1;
+  int U = 4;
+  if (const char *e = getenv("MBX_JIT_GU")) U = atoi(e) == 1 || atoi(e) == 2 || atoi(e) == 8 ? atoi(e) : 4;
+  o << kJitPrelude;
+  o << "\nstruct LocalRF {\n  int64_t l[" << nr << "], h[" << nr << "];\n  uint8_t n[" << nr
+    << "];\n  __device__ __forceinline__ int64_t &lo(int i) { return l[i]; }\n"
+       "  __device__ __forceinline__ int64_t &hi(int i) { return h[i]; }\n"
+       "  __device__ __forceinline__ uint8_t &nl(int i) { return n[i]; }\n};\n"
+       "struct JAggState {\n  unsigned long long count, sum_lo;\n  long long sum_hi, min_i, max_i;\n  double sum_f;\n"
+       "  unsigned long long min_f, max_f;\n};\n"
+       "struct JGroup {\n  int64_t kmin[" << JIT_MAX_KEYS << "], radix[" << JIT_MAX_KEYS << "], stride[" << JIT_MAX_KEYS
+    << "];\n  int32_t nslots, R;\n};\n";
+  o << "extern \"C\" __global__ __launch_bounds__(256) void mbx_jit_group(mbx::VmProgram P, mbx::dev::VmCols C, "
+       "int64_t nrows, int64_t rs, int64_t rstep, JGroup G, JAggState *states, unsigned long long *cstar, "
+       "int32_t *err) {\n"
+       "  using namespace mbx;\n  using namespace mbx::dev;\n  VmCols Cs = C;\n";
+  Specialise(o, cols);
+  // LDS slot tables (layout = GroupLdsBytes)
+  o << "  extern __shared__ __attribute__((aligned(16))) unsigned char jlds[];\n"
+       "  const int NS = G.nslots * G.R;\n  const size_t A4 = ((size_t)NS * 4 + 7) & ~(size_t)7;\n"
+       "  unsigned char *lp = jlds;\n  unsigned int *cnt = (unsigned int *)lp;\n  lp += A4;\n";
+  for (int j = 0; j < p.n_out; j++) {
+    if (p.out_reg[j] == 255) continue;
+    o << "  unsigned int *nul" << j << " = (unsigned int *)lp;\n  lp += A4;\n";
+    if (ArgSum(p, j))
+      o << "  long long *sum" << j << " = (long long *)lp;\n  lp += (size_t)NS * 8;\n  int *ovf" << j
+        << " = (int *)lp;\n  lp += A4;\n";
+    if (ArgMM(p, j))
+      o << "  long long *mn" << j << " = (long long *)lp;\n  lp += (size_t)NS * 8;\n  long long *mx" << j
+        << " = (long long *)lp;\n  lp += (size_t)NS * 8;\n";
+  }
+  o << "  for (int i = threadIdx.x; i < NS; i += blockDim.x) {\n    cnt[i] = 0;\n";
+  for (int j = 0; j < p.n_out; j++) {
+    if (p.out_reg[j] == 255) continue;
+    o << "    nul" << j << "[i] = 0;\n";
+    if (ArgSum(p, j)) o << "    sum" << j << "[i] = 0;\n    ovf" << j << "[i] = 0;\n";
+    if (ArgMM(p, j)) o << "    mn" << j << "[i] = INT64_MAX;\n    mx" << j << "[i] = INT64_MIN;\n";
+  }
+  o << "  }\n  __syncthreads();\n  const int rep = (threadIdx.x & 63) % G.R;\n";
+  o << "  const int64_t S = (int64_t)gridDim.x * blockDim.x;\n"
+       "  for (int64_t base = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; base < nrows; base += " << U << " * S) {\n";
+  for (int r = 0; r < U; r++)
+    o << "    const int64_t row" << r << " = base + " << r << " * S;\n    const bool act" << r << " = row" << r
+      << " < nrows;\n    const int64_t lrow" << r << " = act" << r << " ? row" << r << " : nrows - 1;\n    LocalRF R" << r
+      << " = {};\n";
+  for (int r = 0; r < U; r++) o << Preload(p, std::to_string(r), "lrow" + std::to_string(r), "act" + std::to_string(r));
+  for (int r = 0; r < U; r++) {
+    o << "    {\n      const int64_t lrow = lrow" << r << ";\n      const bool active = act" << r
+      << ";\n      LocalRF &R = R" << r << ";\n";
+    o << Body(p, std::to_string(r));
+    o << "    }\n";
+  }
+  for (int r = 0; r < U; r++) {
+    o << "    {\n      LocalRF &R = R" << r << ";\n      const bool sel = act" << r;
+    if (p.pred_reg != 255) o << " && !R.nl(" << (int)p.pred_reg << ") && R.lo(" << (int)p.pred_reg << ") != 0";
+    o << ";\n      if (sel) {\n        long long slot = 0;\n        bool okk = true;\n";
+    for (int i = 0; i < g.nkeys; i++) {
+      const int kr = g.key_reg[i];
+      if (g.key_nullable[i])
+        o << "        { const long long d = R.nl(" << kr << ") ? G.radix[" << i << "] - 1 : R.lo(" << kr << ") - G.kmin[" << i
+          << "];\n          okk = okk && (unsigned long long)d < (unsigned long long)(R.nl(" << kr << ") ? G.radix[" << i
+          << "] : G.radix[" << i << "] - 1);\n          slot += d * G.stride[" << i << "]; }\n";
+      else
+        o << "        { const long long d = R.lo(" << kr << ") - G.kmin[" << i << "];\n          okk = okk && !R.nl(" << kr
+          << ") && (unsigned long long)d < (unsigned long long)G.radix[" << i << "];\n          slot += d * G.stride["
+          << i << "]; }\n";
+    }
+    o << "        if (!okk) {\n          atomicCAS(err, 0, " << (int)E_KEY_RANGE << ");\n        } else {\n"
+         "          const int sl = (int)slot * G.R + rep;\n          atomicAdd(&cnt[sl], 1u);\n";
+    for (int j = 0; j < p.n_out; j++) {
+      if (p.out_reg[j] == 255) continue;
+      const int ar = p.out_reg[j];
+      o << "          if (R.nl(" << ar << ")) {\n            atomicAdd(&nul" << j << "[sl], 1u);\n          } else {\n"
+        << "            const long long v = R.lo(" << ar << ");\n";
+      if (ArgSum(p, j))
+        o << "            const long long old = (long long)atomicAdd((unsigned long long *)&sum" << j
+          << "[sl], (unsigned long long)v);\n"
+             "            const long long nw = (long long)((unsigned long long)old + (unsigned long long)v);\n"
+             "            if (((old ^ nw) & (v ^ nw)) < 0) atomicAdd(&ovf" << j << "[sl], v < 0 ? -1 : 1);\n";
+      if (ArgMM(p, j)) o << "            atomicMin(&mn" << j << "[sl], v);\n            atomicMax(&mx" << j << "[sl], v);\n";
+      o << "          }\n";
+    }
+    o << "        }\n      }\n    }\n";
+  }
+  o << "  }\n  __syncthreads();\n"
+       "  for (int q = threadIdx.x; q < G.nslots; q += blockDim.x) {\n"
+       "    unsigned long long c = 0;\n    for (int r = 0; r < G.R; r++) c += cnt[q * G.R + r];\n"
+       "    if (!c) continue;\n    atomicAdd(&cstar[q], c);\n";
+  for (int j = 0; j < p.n_out; j++) {
+    if (p.out_reg[j] == 255) continue;
+    o << "    {\n      unsigned long long nn = 0, slo = 0;\n      long long shi = 0, a = INT64_MAX, b = INT64_MIN;\n"
+         "      for (int r = 0; r < G.R; r++) {\n        const int sl = q * G.R + r;\n        nn += nul" << j << "[sl];\n";
+    if (ArgSum(p, j))
+      o << "        const long long v = sum" << j << "[sl];\n        const unsigned long long nlo = slo + (unsigned long long)v;\n"
+           "        shi += (v >> 63) + (nlo < slo ? 1 : 0) + ovf" << j << "[sl];\n        slo = nlo;\n";
+    if (ArgMM(p, j))
+      o << "        a = mn" << j << "[sl] < a ? mn" << j << "[sl] : a;\n        b = mx" << j << "[sl] > b ? mx" << j
+        << "[sl] : b;\n";
+    o << "      }\n      const unsigned long long cj = c - nn;\n      if (cj) {\n"
+         "        JAggState *st = states + (size_t)" << j << " * G.nslots + q;\n        atomicAdd(&st->count, cj);\n";
+    if (ArgSum(p, j))
+      o << "        const unsigned long long old = atomicAdd(&st->sum_lo, slo);\n"
+           "        atomicAdd((unsigned long long *)&st->sum_hi, (unsigned long long)shi + ((old + slo) < old ? 1ull : 0ull));\n";
+    if (ArgMM(p, j)) o << "        atomicMin(&st->min_i, a);\n        atomicMax(&st->max_i, b);\n";
+    o << "      }\n    }\n";
+  }
+  o << "  }\n}\n";
+  return o.str();
+}
+
+std::string GroupSourceForTest(const VmProgram &p, const dev::VmCols &cols, const GroupSpec &g) {
+  return GroupSource(p, cols, g);
+}
+
+bool VmGroupAggregate(const VmProgram &p, const dev::VmCols &cols, const GroupSpec &g, int64_t nrows,
+                      int64_t range_start, int64_t range_step, void *states, unsigned long long *count_star,
+                      int32_t *err, hipStream_t s) {
+  if (nrows <= 0 || g.nkeys < 1 || g.nkeys > JIT_MAX_KEYS || g.nslots < 1) return false;
+  for (int j = 0; j < p.n_out; j++)
+    if (p.out_reg[j] != 255 && p.out_class[j] != VC_I64) return false;
+  // replicas: as many as fit 48 KiB (3 blocks per CU), at least one in 64 KiB
+  int R = 64;
+  if (const char *e = getenv("MBX_JIT_GR")) R = atoi(e) >= 1 && atoi(e) <= 64 ? atoi(e) : 64;
+  while (R > 1 && GroupLdsBytes(p, g.nslots, R) > 48 * 1024) R >>= 1;
+  const size_t lds = GroupLdsBytes(p, g.nslots, R);
+  if (lds > 64 * 1024) return false;
+  const std::string src = GroupSource(p, cols, g);
+  hipFunction_t fn = GetNamed(src, "mbx_jit_group");
+  if (!fn) return false;
+  VmProgram P = p;
+  dev::VmCols C = cols;
+  JGroupArg G;
+  memset(&G, 0, sizeof(G));
+  for (int i = 0; i < g.nkeys; i++) {
+    G.kmin[i] = g.kmin[i];
+    G.radix[i] = g.radix[i];
+    G.stride[i] = g.stride[i];
+  }
+  G.nslots = g.nslots;
+  G.R = R;
+  void *args[] = {&P, &C, &nrows, &range_start, &range_step, &G, &states, &count_star, &err};
+  int cus = 0, d = 0;
+  (void)hipGetDevice(&d);
+  (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, d);
+  if (cus <= 0) cus = 256;
+  int bpc = (int)std::min<size_t>(4, (160 * 1024) / std::max<size_t>(lds, 1));
+  if (const char *e = getenv("MBX_JIT_GBPC")) bpc = atoi(e) >= 1 && atoi(e) <= 8 ? atoi(e) : bpc;
+  if (bpc < 1) bpc = 1;
+  int64_t gsz = (nrows + 1023) / 1024;
+  if (gsz > (int64_t)cus * bpc) gsz = (int64_t)cus * bpc;
+  return hipModuleLaunchKernel(fn, (unsigned)gsz, 1, 1, 256, 1, 1, (unsigned)lds, s, args, nullptr) == hipSuccess;
+}
 
 void JoinPending() { JoinAll(); }
 

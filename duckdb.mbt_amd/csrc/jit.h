@@ -37,6 +37,26 @@ bool VmProject(const VmProgram &p, const dev::VmCols &cols, int64_t nrows, int64
 // selected-row count into *count_star.  true: launched.
 bool VmAggregate(const VmProgram &p, const dev::VmCols &cols, int64_t nrows, int64_t range_start, int64_t range_step,
                  void *states, unsigned long long *count_star, int32_t *err, hipStream_t s);
+// Fused scan -> filter -> project -> GROUP BY over up to JIT_MAX_KEYS integer
+// keys of small known range (column statistics): each selected row goes to
+// slot sum_i digit_i * stride[i], digit_i = key_i - kmin[i], or radix[i] - 1
+// for a NULL key when key_nullable[i].  The kernel keeps per-block LDS slot
+// tables (R replicas, overflow-exact int64 sums) and merges them into
+// count_star[slot] and states[j * nslots + slot] (dev::AggState layout,
+// pre-initialised) for every aggregate j with p.out_reg[j] != 255 (class
+// VC_I64 only; p.out_phys[j] = statistics needed, as for VmAggregate).
+#define JIT_MAX_KEYS 4
+struct GroupSpec {
+  int32_t nkeys, nslots;
+  uint8_t key_reg[JIT_MAX_KEYS], key_nullable[JIT_MAX_KEYS];
+  int64_t kmin[JIT_MAX_KEYS], radix[JIT_MAX_KEYS], stride[JIT_MAX_KEYS];
+};
+// LDS bytes of one block's slot tables at R replicas.
+size_t GroupLdsBytes(const VmProgram &p, int64_t nslots, int R);
+bool VmGroupAggregate(const VmProgram &p, const dev::VmCols &cols, const GroupSpec &g, int64_t nrows,
+                      int64_t range_start, int64_t range_step, void *states, unsigned long long *count_star,
+                      int32_t *err, hipStream_t s);
+std::string GroupSourceForTest(const VmProgram &p, const dev::VmCols &cols, const GroupSpec &g);
 bool Enabled();
 // Waits for every background compile.  Called on disconnect and from the
 // Python binding's atexit: a compile still inside hipRTC while exit() runs

@@ -2014,6 +2014,21 @@ __global__ __launch_bounds__(256) void emit_agg_kernel(EmitDesc D) {
         if (base + 32 < n) D.key_valid[(base >> 5) + 1] = (uint32_t)(m >> 32);
       }
     }
+    for (int q = 0; q < D.nkeys_c; q++) {
+      const auto &K = D.kc[q];
+      bool kv = in;
+      if (in) {
+        const int64_t dg = (sl / K.stride) % K.radix;
+        kv = !(K.nullable && dg == K.radix - 1);
+        const int64_t k = kv ? K.kmin + dg : 0;
+        store_phys(K.out, K.phys, i, k, k >> 63);
+      }
+      uint64_t m = __ballot(kv);
+      if (lane == 0) {
+        K.valid[base >> 5] = (uint32_t)m;
+        if (base + 32 < n) K.valid[(base >> 5) + 1] = (uint32_t)(m >> 32);
+      }
+    }
     for (int j = 0; j < D.nagg; j++) {
       const EmitAgg &A = D.a[j];
       bool valid = in;

@@ -1069,6 +1069,25 @@ char *duckdb_mbx_jit_selftest(void) {
     std::string r = jit::CompileCheck(src);
     if (!r.empty()) log += "[aggregate] " + r;
   }
+  // the fused GROUP BY kernel: keys (x nullable-less, k), SUM(x + k) and COUNT(*)
+  {
+    VmProgram q = p;
+    q.n_out = 2;
+    q.out_reg[0] = 6;
+    q.out_class[0] = VC_I64;
+    q.out_phys[0] = 3;
+    q.out_reg[1] = 255;
+    jit::GroupSpec g;
+    memset(&g, 0, sizeof(g));
+    g.nkeys = 2;
+    g.key_reg[0] = 0;
+    g.key_reg[1] = 3;
+    g.key_nullable[1] = 1;
+    std::string src = jit::GroupSourceForTest(q, cols, g);
+    if (getenv("MBX_JIT_DUMP")) fprintf(stderr, "%s\n", src.c_str());
+    std::string r = jit::CompileCheck(src);
+    if (!r.empty()) log += "[group] " + r;
+  }
   if (log.empty()) return nullptr;
   char *out = (char *)malloc(log.size() + 1);
   memcpy(out, log.c_str(), log.size() + 1);

@@ -91,6 +91,7 @@ enum VmErr : int32_t {
   E_CAST_RANGE = 5,
   E_DEC_OVF = 6,
   E_HASH_FULL = 7,
+  E_KEY_RANGE = 8,  // a GROUP BY key outside the zone map its slot table was sized from
 };
 
 namespace dev {

@@ -388,9 +388,15 @@ def test_order_by_extremes_and_varchar(conn):
 
 
 # ---- filter -> GROUP BY fused (range predicate inside the LDS group kernel) -------
-@pytest.mark.parametrize("variant", ["", "d3_g2"])
+@pytest.mark.parametrize("variant", ["", "d3_g2", "jit"])
 def test_filter_groupby_fused_parity(conn, oracle, monkeypatch, variant):
-    monkeypatch.setenv("MBX_GD_VARIANT", variant)
+    # group_direct_lds with fused predicates (MBX_JIT=0), or the compiled
+    # fused GROUP BY that a filtered GROUP BY prefers once it is built
+    if variant == "jit":
+        monkeypatch.setenv("MBX_JIT", "sync")
+    else:
+        monkeypatch.setenv("MBX_JIT", "0")
+        monkeypatch.setenv("MBX_GD_VARIANT", variant)
     for n in (255, 257, 100_003, 1_000_000):
         k = oracle.synth_i64(n, 7, 0, 32, 0)
         v = oracle.synth_i64(n, 9, 0, 2**40, -2**39)
@@ -496,5 +502,140 @@ def test_filter_multi_parity(mbx, oracle):
                 if n >= 256:
                     names = [kk["name"] for kk in c.last_profile()["kernels"]]
                     assert "filter_multi" in names, (where, names)
+    finally:
+        c.close()
+
+
+# ---- fused run-time compiled GROUP BY (jit::VmGroupAggregate) ---------------------
+def _jit_conn(mbx, monkeypatch):
+    monkeypatch.setenv("MBX_JIT", "sync")
+    cfg = mbx.Config.create()
+    cfg.set("mbx_profile", "true")
+    return mbx.connect_with_config(cfg).value
+
+
+def _kernels(c):
+    return [kk["name"] for kk in c.last_profile()["kernels"]]
+
+
+def _groups_expect(keys, cols, mask):
+    """keys: list of per-row key tuples; cols: {name: list of per-row values
+    (None = NULL)}; returns {key: {name: (count, sum, min, max)}} over rows
+    where mask; plus COUNT(*) under name '*'."""
+    acc = {}
+    for i, kt in enumerate(keys):
+        if not mask[i]:
+            continue
+        d = acc.setdefault(kt, {"*": [0, 0, None, None]})
+        d["*"][0] += 1
+        for name, vals in cols.items():
+            v = vals[i]
+            st = d.setdefault(name, [0, 0, None, None])
+            if v is None:
+                continue
+            st[0] += 1
+            st[1] += v
+            st[2] = v if st[2] is None else min(st[2], v)
+            st[3] = v if st[3] is None else max(st[3], v)
+    return acc
+
+
+def _cell(x):
+    return "" if x is None else str(x)
+
+
+@pytest.mark.parametrize("n", [1, 257, 100_003, 1_000_003])
+def test_jit_groupby_expressions_parity(mbx, oracle, monkeypatch, n):
+    c = _jit_conn(mbx, monkeypatch)
+    try:
+        k = oracle.synth_i64(n, 7, 0, 32, 0).tolist()
+        k2 = oracle.synth_i64(n, 8, 0, 4, 0).tolist()
+        v = oracle.synth_i64(n, 9, 0, 2**40, -2**39).tolist()
+        x = oracle.synth_i64(n, 42, 0, 50, 1).tolist()
+        q(c, "DROP TABLE IF EXISTS jg")
+        q(c, f"CREATE TABLE jg AS SELECT CAST(mbx_synth(7, i, 32) AS INTEGER) AS k, "
+             f"CAST(mbx_synth(8, i, 4) AS INTEGER) AS k2, mbx_synth(9, i, 1099511627776) - 549755813888 AS v, "
+             f"mbx_synth(42, i, 50) + 1 AS x FROM range({n}) tbl(i)")
+        keys1 = [(a,) for a in k]
+        keys2 = list(zip(k, k2))
+        allrows = [True] * n
+        # c3_project: an expression argument over one key
+        exp = _groups_expect(keys1, {"v2": [2 * a for a in v]}, allrows)
+        res = q(c, "SELECT k, SUM(v * 2), COUNT(*) FROM jg GROUP BY k ORDER BY k")
+        assert res.rows == [[str(kk[0]), str(exp[kk]["v2"][1]), str(exp[kk]["*"][0])] for kk in sorted(exp)]
+        if n >= 256:
+            assert "jit_group" in _kernels(c)
+        # two keys, a WHERE over an expression, several statistics
+        tmod3 = [(abs(a) % 3) * (1 if a >= 0 else -1) for a in v]  # SQL % truncates
+        m = [(x[i] + k2[i] > 24) and (tmod3[i] != 1) for i in range(n)]
+        cols = {"vx": [v[i] + x[i] for i in range(n)], "vm": [v[i] - x[i] for i in range(n)],
+                "v3": [3 * v[i] for i in range(n)], "v": v}
+        exp = _groups_expect(keys2, cols, m)
+        res = q(c, "SELECT k, k2, COUNT(*), SUM(v + x), MIN(v - x), MAX(v * 3), COUNT(v) FROM jg "
+                   "WHERE x + k2 > 24 AND v % 3 <> 1 GROUP BY k, k2 ORDER BY k, k2")
+        want = [[str(kk[0]), str(kk[1]), str(exp[kk]["*"][0]), str(exp[kk]["vx"][1]), str(exp[kk]["vm"][2]),
+                 str(exp[kk]["v3"][3]), str(exp[kk]["v"][0])] for kk in sorted(exp)]
+        assert res.rows == want
+        if n >= 256:
+            assert "jit_group" in _kernels(c)
+        # the same query without ORDER BY comes out in key order too
+        res2 = q(c, "SELECT k, k2, COUNT(*), SUM(v + x), MIN(v - x), MAX(v * 3), COUNT(v) FROM jg "
+                    "WHERE x + k2 > 24 AND v % 3 <> 1 GROUP BY k, k2")
+        assert res2.rows == want
+    finally:
+        c.close()
+
+
+def test_jit_groupby_null_keys_and_args(mbx, monkeypatch):
+    c = _jit_conn(mbx, monkeypatch)
+    try:
+        n = 300_007
+        q(c, f"CREATE TABLE jn AS SELECT CASE WHEN i % 7 = 0 THEN NULL ELSE i % 5 END AS a, "
+             f"CASE WHEN i % 11 = 0 THEN NULL ELSE CAST(i % 3 AS INTEGER) END AS b, "
+             f"CASE WHEN i % 3 = 0 THEN NULL ELSE i * 7 - 1000000 END AS v FROM range({n}) tbl(i)")
+        keys = [(None if i % 7 == 0 else i % 5, None if i % 11 == 0 else i % 3) for i in range(n)]
+        vals = [None if i % 3 == 0 else i * 7 - 1000000 for i in range(n)]
+        exp = _groups_expect(keys, {"v": vals}, [True] * n)
+        res = q(c, "SELECT a, b, COUNT(*), COUNT(v), SUM(v + 1), MIN(v), MAX(v), AVG(v) FROM jn GROUP BY a, b "
+                   "ORDER BY a, b")
+        want = []
+        for kk in sorted(exp, key=_sort_key):
+            st = exp[kk]["v"]
+            want.append([_cell(kk[0]), _cell(kk[1]), str(exp[kk]["*"][0]), str(st[0]),
+                         _cell(st[1] + st[0] if st[0] else None), _cell(st[2]), _cell(st[3])])
+        assert [r[:7] for r in res.rows] == want
+        for r, kk in zip(res.rows, sorted(exp, key=_sort_key)):
+            st = exp[kk]["v"]
+            if st[0]:
+                assert abs(float(r[7]) - st[1] / st[0]) <= 1e-9 * max(1.0, abs(st[1] / st[0]))
+            else:
+                assert r[7] == ""
+        assert "jit_group" in _kernels(c)
+        # a NULL group is emitted last with NULL key cells
+        assert res.nulls[-1][0] is True and res.nulls[-1][1] is True
+    finally:
+        c.close()
+
+
+def test_jit_groupby_int64_wrap_is_exact(mbx, monkeypatch):
+    # values near 2^62 in few groups: the per-block int64 LDS sums wrap many
+    # times; the wrap counter keeps SUM exact (HUGEINT)
+    c = _jit_conn(mbx, monkeypatch)
+    try:
+        n = 2_000_003
+        big = 4611686018427387000
+        q(c, f"CREATE TABLE jw AS SELECT CAST(i % 3 AS INTEGER) AS k, "
+             f"CASE WHEN i % 5 = 0 THEN -{big} - i ELSE {big} + i END AS v FROM range({n}) tbl(i)")
+        exp = {}
+        for kk in range(3):
+            idx = range(kk, n, 3)
+            s = sum((-big - i) if i % 5 == 0 else (big + i) for i in idx)
+            exp[kk] = (len(idx), s)
+        res = q(c, "SELECT k, COUNT(*), SUM(v + 1) FROM jw GROUP BY k ORDER BY k")
+        assert res.rows == [[str(kk), str(exp[kk][0]), str(exp[kk][1] + exp[kk][0])] for kk in range(3)]
+        assert "jit_group" in _kernels(c)
+        # an overflowing expression raises the interpreter's error
+        r = c.query("SELECT k, SUM(v * 4) FROM jw GROUP BY k")
+        assert isinstance(r, mbx.Err) and "Overflow in multiplication" in r.error.message
     finally:
         c.close()

@@ -27,6 +27,9 @@ shapes = {
     "multi_key": "SELECT k, k2, SUM(v), COUNT(*) FROM t GROUP BY k, k2",
     "filter_sum_expr": "SELECT SUM(v + x) FROM t WHERE x > 24 AND k < 16",
     "filter_multi": "SELECT COUNT(*), SUM(v) FROM t WHERE x > 24 AND k < 16",
+    "c3_jit": "SELECT k, SUM(v * 1), COUNT(*) FROM t GROUP BY k",
+    "c3_where_jit": "SELECT k, SUM(v * 1), COUNT(*) FROM t WHERE x > 24 GROUP BY k",
+    "group_expr2": "SELECT k, k2, SUM(v + x), MIN(v), COUNT(*) FROM t WHERE x + k2 > 24 GROUP BY k, k2",
     "filter_multi3": "SELECT SUM(v), MIN(v), MAX(v) FROM t WHERE x BETWEEN 10 AND 40 AND k < 16 AND k2 = 1",
     "wide_key": "SELECT v % 1000003, COUNT(*) FROM t GROUP BY v % 1000003",
 }
