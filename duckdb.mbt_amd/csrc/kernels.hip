@@ -714,10 +714,12 @@ int FilterMultiPartials(const FilterMultiDesc &d_in, int64_t nrows, AggPartial *
   FilterMultiDesc d = d_in;
   int nld = 0;
   for (int c = 0; c < d.ncol; c++) nld += d.col[c].phys == P_I64 ? 2 : 1;
-  int gpc = 2;
+  // 3 blocks per CU: 3.39 ms vs 3.79 at 2 for 1e9 rows of (x i64, k i32,
+  // v i64), equal at 1e8 (profiles/r01_filter_multi_sweep.log)
+  int gpc = 3;
   const char *e = getenv("MBX_FM_BLOCKS_PER_CU");
   if (e && *e) gpc = atoi(e);
-  int grid = NumCUs() * (gpc > 0 ? gpc : 2);
+  int grid = NumCUs() * (gpc > 0 ? gpc : 3);
   int64_t need = (nrows >> 8) / 4 + 1;
   if (grid > need) grid = (int)need;
   if (grid > kMaxAggPartials) grid = kMaxAggPartials;
@@ -731,16 +733,22 @@ int FilterMultiPartials(const FilterMultiDesc &d_in, int64_t nrows, AggPartial *
 #define FM(L, DP)                                                                                            \
   hipLaunchKernelGGL((filter_multi_lds_kernel<L, DP>), dim3(grid), dim3(256), (size_t)4 * DP * L * 1024, s, d, nrows, \
                      partials)
+  // MBX_FM_DEPTH=<2..4>: ring depth for 3..5 loads per step (sweeps)
+  int dp = 2;
+  if (const char *ed = getenv("MBX_FM_DEPTH")) dp = atoi(ed) >= 2 && atoi(ed) <= 4 ? atoi(ed) : 2;
+#define FMD(L) \
+  if (dp == 2) FM(L, 2); else if (dp == 3) FM(L, 3); else FM(L, 4);
   switch (nld) {
     case 1: FM(1, 6); break;
     case 2: FM(2, 3); break;
-    case 3: FM(3, 2); break;
-    case 4: FM(4, 2); break;
-    case 5: FM(5, 2); break;
+    case 3: FMD(3); break;
+    case 4: FMD(4); break;
+    case 5: FMD(5); break;
     case 6: FM(6, 2); break;
     case 7: FM(7, 2); break;
     default: FM(8, 2); break;
   }
+#undef FMD
 #undef FM
   CHECK_LAUNCH();
   return grid;
