@@ -75,6 +75,7 @@ _sig("duckdb_mbx_explain", ctypes.c_void_p, _P, ctypes.c_char_p, _L)
 _sig("duckdb_mbx_last_profile", ctypes.c_void_p, _P)
 _sig("duckdb_mbx_profile_drain", ctypes.c_void_p, _P)
 _sig("duckdb_mbx_result_raw", _I, _P, _I, _I, _P, _I)
+_sig("duckdb_mbx_result_text", ctypes.c_void_p, _P, ctypes.POINTER(ctypes.c_int64))
 _sig("duckdb_mbx_append_column", _I, _P, _I, _P, _P, _L)
 _sig("duckdb_mbx_append_commit", _I, _P, _L)
 _sig("duckdb_mbx_hbm_calibrate", _I, _P, _L, _I, ctypes.POINTER(ctypes.c_double))
@@ -173,6 +174,35 @@ def _take(bp) -> bytes:
 
 def _str(bp) -> str:
     return _take(bp).decode("utf-8", errors="replace")  # @encoding/utf8.decode_lossy
+
+
+def _result_text(res):
+    """(rows, nulls) of a materialized result: the strings and NULL flags that
+    duckdb_mb_result_value / _is_null give cell by cell (the loop of
+    Connection::query, duckdb_native.mbt:477-497), fetched in ONE C call
+    (duckdb_mbx_result_text) instead of two ctypes calls per cell."""
+    n = ctypes.c_int64(0)
+    p = lib.duckdb_mbx_result_text(res, ctypes.byref(n))
+    if not p:
+        raise DuckDBError("duckdb_mbx_result_text failed")
+    try:
+        data = ctypes.string_at(p, n.value)
+    finally:
+        lib.duckdb_mbx_free(ctypes.c_void_p(p))
+    nr, nc = struct.unpack_from("<qq", data, 0)
+    ncell = nr * nc
+    head = 16 + ((ncell + 7) & ~7)
+    offs = struct.unpack_from(f"<{ncell + 1}q", data, head)
+    base = head + 8 * (ncell + 1)
+    flags = data[16:16 + ncell]
+    rows, nulls = [], []
+    for r in range(nr):
+        i0 = r * nc
+        rn = [f == 1 for f in flags[i0:i0 + nc]]
+        rv = [data[base + offs[i]:base + offs[i + 1]].decode("utf-8", errors="replace") for i in range(i0, i0 + nc)]
+        rows.append(rv)
+        nulls.append(rn)
+    return rows, nulls
 
 
 class _Arg:
@@ -456,29 +486,32 @@ class Connection:
         except Exception:
             pass
 
-    # Connection::query (duckdb_native.mbt:454-501): per-cell row-major pull
+    # Connection::query (duckdb_native.mbt:454-501): row-major strings + NULL
+    # flags of every cell.  The reference's per-cell loop (:477-497) costs two
+    # native calls per cell; over ctypes that would be ~2 us per cell, so the
+    # same strings come back in one call (_result_text).  query_percell keeps
+    # the literal per-cell form over duckdb_mb_result_is_null/_value.
     def query(self, sql: str, on_done: Callable = None):
+        return self._query(sql, on_done, _result_text)
+
+    def query_percell(self, sql: str, on_done: Callable = None):
+        return self._query(sql, on_done, _result_cells)
+
+    def _query(self, sql, on_done, pull):
         a = _Arg(sql)
         res = lib.duckdb_mb_query(self._h, a.p)
         if lib.duckdb_mb_is_null_result(res):
             out = Err(DuckDBError(_last_error("duckdb_query failed")))
         else:
             ncol = lib.duckdb_mb_result_column_count(res)
-            nrow = lib.duckdb_mb_result_row_count(res)
             columns, types = [], []
             for c in range(ncol):
                 columns.append(_str(lib.duckdb_mb_result_column_name(res, c)))
                 types.append(column_type_from_id(lib.duckdb_mb_result_column_type(res, c)))
-            rows, nulls = [], []
-            for r in range(nrow):
-                rv, rn = [], []
-                for c in range(ncol):
-                    isnull = bool(lib.duckdb_mb_result_is_null(res, c, r))
-                    rn.append(isnull)
-                    rv.append("" if isnull else _str(lib.duckdb_mb_result_value(res, c, r)))
-                rows.append(rv)
-                nulls.append(rn)
-            lib.duckdb_mb_result_destroy(res)
+            try:
+                rows, nulls = pull(res)
+            finally:
+                lib.duckdb_mb_result_destroy(res)
             out = Ok(QueryResult(columns, types, rows, nulls))
         if on_done:
             on_done(out)
@@ -587,6 +620,10 @@ class RawResult:
 
     def value(self, c, r) -> str:
         return _str(lib.duckdb_mb_result_value(self._h, c, r))
+
+    def cells(self):
+        """(rows, nulls): every cell's string and NULL flag in one call."""
+        return _result_text(self._h)
 
     def raw(self, c, r) -> bytes:
         buf = ctypes.create_string_buffer(16)
@@ -766,18 +803,27 @@ class PreparedStatement:
             on_done(Ok(None))
 
 
-def _materialize(res) -> QueryResult:
+def _result_cells(res):
+    """The reference's literal per-cell pull (duckdb_native.mbt:477-497)."""
     ncol = lib.duckdb_mb_result_column_count(res)
     nrow = lib.duckdb_mb_result_row_count(res)
-    columns = [_str(lib.duckdb_mb_result_column_name(res, c)) for c in range(ncol)]
-    types = [column_type_from_id(lib.duckdb_mb_result_column_type(res, c)) for c in range(ncol)]
     rows, nulls = [], []
     for r in range(nrow):
         rn = [bool(lib.duckdb_mb_result_is_null(res, c, r)) for c in range(ncol)]
         rv = ["" if rn[c] else _str(lib.duckdb_mb_result_value(res, c, r)) for c in range(ncol)]
         rows.append(rv)
         nulls.append(rn)
-    lib.duckdb_mb_result_destroy(res)
+    return rows, nulls
+
+
+def _materialize(res) -> QueryResult:
+    ncol = lib.duckdb_mb_result_column_count(res)
+    columns = [_str(lib.duckdb_mb_result_column_name(res, c)) for c in range(ncol)]
+    types = [column_type_from_id(lib.duckdb_mb_result_column_type(res, c)) for c in range(ncol)]
+    try:
+        rows, nulls = _result_text(res)
+    finally:
+        lib.duckdb_mb_result_destroy(res)
     return QueryResult(columns, types, rows, nulls)
 
 

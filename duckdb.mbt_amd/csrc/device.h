@@ -103,7 +103,7 @@ struct GroupPreds {
 bool GroupByDirectStates(const void *kcol, int kphys, int64_t kmin, int nk, const void *v0, const void *v1, int vphys,
                          int nv, bool mm, int64_t nrows, int64_t seg_rows, int R, unsigned long long *cstar,
                          AggState *st0, AggState *st1, int grid_blocks, hipStream_t s,
-                         const GroupPreds *pred = nullptr);
+                         const GroupPreds *pred = nullptr, uint64_t vmaxabs = ~0ull);
 
 // --- generic aggregation over compacted columns ---------------------------
 // vclass: VC_I64 / VC_I128 / VC_F64 of the input column (phys given)

@@ -1030,7 +1030,7 @@ static bool DirectReduce(Engine &e, const void *kdata, Phys kphys, int64_t kmin,
   dev::GroupByDirectStates(kdata, kphys, kmin, (int)nk, nv > 0 ? vals[0]->data : nullptr,
                            nv > 1 ? vals[1]->data : nullptr, vphys, nv, mm, n, seg, R,
                            (unsigned long long *)out.cs->p, (dev::AggState *)out.s0->p, (dev::AggState *)out.s1->p, 0,
-                           e.stream);
+                           e.stream, nullptr, maxabs < ((i128)1 << 62) ? (uint64_t)maxabs : ~0ull);
   return true;
 }
 
@@ -1622,7 +1622,8 @@ static DRel Aggregate(Engine &e, const DRel &src, const BoundSelect &s) {
                                                 nv > 0 ? src.cols[vcols[0]].data : nullptr,
                                                 nv > 1 ? src.cols[vcols[1]].data : nullptr, vphys, nv, mm, src.n, seg,
                                                 R, (unsigned long long *)cs->p, (dev::AggState *)s0->p,
-                                                (dev::AggState *)s1->p, 0, e.stream, gp.n ? &gp : nullptr);
+                                                (dev::AggState *)s1->p, 0, e.stream, gp.n ? &gp : nullptr,
+                                                maxabs < ((i128)1 << 62) ? (uint64_t)maxabs : ~0ull);
           }
           if (!launched) goto generic;
           auto list = Alloc(e, nslots * 4);

@@ -1138,12 +1138,19 @@ __global__ __launch_bounds__(256) void group_direct_kernel(const TK *__restrict_
 // 16-B/lane global_load_lds (1 KiB per instruction, no VGPR staging); each
 // lane then owns 4 consecutive rows.  Waves walk steps grid-stride.  The
 // replicated LDS tables and the rings share ONE dynamic __shared__ array.
-template <typename TK, typename TV, int NV, bool MM, int DEPTH>
+//
+// PK (packed count): the row's COUNT rides in the low PKB bits of its SUM
+// atomic — one ds_add_u64 of (v << PKB) + 1 per row instead of a ds_add_u32
+// plus a ds_add_u64, which is what bounds this kernel (LDS atomics, not HBM).
+// Every PKF wave steps the block drains the packed table into per-thread
+// register partials (slot t + 256 j), before a count can reach 2^PKB or the
+// shifted sum can leave int64; the host derives PKB/PKF from the zone maps.
+template <typename TK, typename TV, int NV, bool MM, int DEPTH, bool PK>
 __global__ __launch_bounds__(256) void group_direct_lds_kernel(const TK *__restrict__ keys, const TV *__restrict__ v0,
                                                                const TV *__restrict__ v1, int64_t n, int64_t kmin,
                                                                int nk, int R, size_t ring_off,
                                                                unsigned long long *cstar, AggState *st0,
-                                                               AggState *st1, GroupPreds pr) {
+                                                               AggState *st1, GroupPreds pr, int PKB, int PKF) {
   extern __shared__ __attribute__((aligned(16))) unsigned char lds_raw[];
   constexpr int KB = 256 * (int)sizeof(TK), VB = 256 * (int)sizeof(TV);  // bytes per step
   constexpr int SB0 = KB + NV * VB;                                        // slot bytes without a predicate slice
@@ -1182,17 +1189,48 @@ __global__ __launch_bounds__(256) void group_direct_lds_kernel(const TK *__restr
   __syncthreads();
   auto row = [&](int64_t k, int64_t a, int64_t b) {
     int sl = (int)(k - kmin) * R + rep;
-    atomicAdd(&cnt[sl], 1u);
-    if (NV >= 1) atomicAdd((unsigned long long *)&sum0[sl], (unsigned long long)a);
+    if (PK) {
+      atomicAdd((unsigned long long *)&sum0[sl], ((unsigned long long)a << PKB) + 1ull);
+    } else {
+      atomicAdd(&cnt[sl], 1u);
+      if (NV >= 1) atomicAdd((unsigned long long *)&sum0[sl], (unsigned long long)a);
+    }
     if (NV >= 2) atomicAdd((unsigned long long *)&sum1[sl], (unsigned long long)b);
     if (MM) {
       atomicMin(&mn0[sl], (long long)a); atomicMax(&mx0[sl], (long long)a);
       if (NV >= 2) { atomicMin(&mn1[sl], (long long)b); atomicMax(&mx1[sl], (long long)b); }
     }
   };
+  // PK: register partials of slots t + 256 j (nslot <= 256 * PK_J, checked by the host)
+  constexpr int PK_J = 8;
+  unsigned int rc[PK_J];
+  long long rs[PK_J];
+#pragma unroll
+  for (int j = 0; j < PK_J; j++) { rc[j] = 0; rs[j] = 0; }
+  auto pk_drain = [&]() {
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    const unsigned long long m = (1ull << PKB) - 1;
+#pragma unroll
+    for (int j = 0; j < PK_J; j++) {
+      int sl = t + 256 * j;
+      if (sl < nslot) {
+        unsigned long long p = (unsigned long long)sum0[sl];
+        unsigned long long c = p & m;
+        rc[j] += (unsigned int)c;
+        rs[j] += (long long)(p - c) >> PKB;
+        sum0[sl] = 0;
+      }
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+  };
   const int64_t nsteps = n >> 8;
   const int64_t nw = (int64_t)gridDim.x * 4;
   int64_t st = (int64_t)blockIdx.x * 4 + w;
+  // steps of the block's last wave (the fewest): in-loop drains happen only
+  // while every wave of the block still iterates, so all reach the barrier
+  const int64_t last_w = (int64_t)blockIdx.x * 4 + 3;
+  const int64_t min_steps = last_w < nsteps ? (nsteps - 1 - last_w) / nw + 1 : 0;
+  int64_t it = 0;
   // issue one step's glds into slot d: key slice, then each value slice
   auto issue = [&](int64_t q, int d) {
     unsigned char *dst = ring + d * SB;
@@ -1282,6 +1320,10 @@ __global__ __launch_bounds__(256) void group_direct_lds_kernel(const TK *__restr
     for (int e = 0; e < 4; e++)
       if (ok[e]) row(kk[e], NV >= 1 ? a[e] : 0, NV >= 2 ? b[e] : 0);
     k = k + 1 == DEPTH ? 0 : k + 1;
+    if (PK) {
+      ++it;
+      if (it % PKF == 0 && it <= min_steps) pk_drain();
+    }
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   if (blockIdx.x == 0) {
@@ -1295,6 +1337,14 @@ __global__ __launch_bounds__(256) void group_direct_lds_kernel(const TK *__restr
         okr = okr && (uint64_t)(pv - g.lo) <= g.span;
       }
       if (okr) row(kv, av, NV >= 2 ? (int64_t)v1[i] : 0);
+    }
+  }
+  if (PK) {
+    pk_drain();
+#pragma unroll
+    for (int j = 0; j < PK_J; j++) {
+      int sl = t + 256 * j;
+      if (sl < nslot) { cnt[sl] = rc[j]; sum0[sl] = rs[j]; }
     }
   }
   __syncthreads();
@@ -1349,9 +1399,30 @@ size_t GroupDirectLds(int nk, int R, int nv, bool mm) {
   return b;
 }
 
+// Packed-count parameters for group_direct_lds (PK): the largest drain period
+// (wave steps) such that between drains no replica slot's count reaches 2^PKB
+// and |sum| << PKB stays inside int64.  A slot absorbs at most 1024/R rows per
+// block step (64/R lanes x 4 rows x 4 waves), plus 256 tail rows in block 0.
+// Returns false when no period of at least 16 steps exists.
+static bool PackedCountParams(uint64_t vmaxabs, int R, int &pkb, int &pkf) {
+  if (vmaxabs >= (1ull << 50)) return false;
+  const uint64_t ma = vmaxabs ? vmaxabs : 1;
+  int64_t best = 0;
+  for (int b = 8; b <= 40; b++) {
+    uint64_t m = std::min<uint64_t>((1ull << b) - 1, ((1ull << (63 - b)) - 1) / ma);  // rows per slot per period
+    if (m <= 256) continue;
+    int64_t f = (int64_t)((m - 256) * (uint64_t)R / 1024);
+    if (f > best) { best = f; pkb = b; }
+  }
+  if (best < 16) return false;
+  pkf = (int)std::min<int64_t>(best, 1 << 20);
+  return true;
+}
+
 bool GroupByDirectStates(const void *kcol, int kphys, int64_t kmin, int nk, const void *v0, const void *v1, int vphys,
                          int nv, bool mm, int64_t nrows, int64_t seg_rows, int R, unsigned long long *cstar,
-                         AggState *st0, AggState *st1, int grid_blocks, hipStream_t s, const GroupPreds *pred) {
+                         AggState *st0, AggState *st1, int grid_blocks, hipStream_t s, const GroupPreds *pred,
+                         uint64_t vmaxabs) {
   if (nrows <= 0) return true;
   GroupPreds pr;
   memset(&pr, 0, sizeof(pr));
@@ -1360,7 +1431,8 @@ bool GroupByDirectStates(const void *kcol, int kphys, int64_t kmin, int nk, cons
   // fit the overflow bound the host derived (seg_rows) — else the segmented
   // kernel below.  MBX_GD_VARIANT="d<depth>_g<blocks per CU>" / "seg".
   // Defaults from profiles/r01_group_sweep.json: d2_g3 for C3 (6.72 TB/s vs
-  // 5.87 segmented); COUNT-only tables (nv == 0) carry 3x the LDS atomics per
+  // 5.87 segmented; one block per CU streams faster but cannot keep up with
+  // the table atomics: profiles/r01_c3_probe.log); COUNT-only tables (nv == 0) carry 3x the LDS atomics per
   // byte and stay on the segmented kernel at 4 blocks/CU (6.40 TB/s).
   {
     int depth = 2, gpc = 3;
@@ -1386,22 +1458,36 @@ bool GroupByDirectStates(const void *kcol, int kphys, int64_t kmin, int nk, cons
       for (int j = 0; j < pr.n; j++)
         if (pr.p[j].src == 1) slot += 256 * (size_t)(pr.p[j].phys == P_I64 ? 8 : 4);
       depth = depth <= 2 ? 2 : depth <= 3 ? 3 : 4;
+      const size_t lds_cap = 64 * 1024;
       size_t lds = ring_off + 4 * (size_t)depth * slot;
       // wide slots (predicate slices): trade table replicas for ring space;
       // seg_rows scales with R (rows per replica stay the same)
-      while (lds > 64 * 1024 && R > 1) {
+      while (lds > lds_cap && R > 1) {
         R >>= 1;
         if (seg_rows > 0) seg_rows >>= 1;
         tab = GroupDirectLds(nk, R, nv, mm);
         ring_off = (tab + 15) & ~(size_t)15;
         lds = ring_off + 4 * (size_t)depth * slot;
       }
-      if ((seg_rows <= 0 || seg_rows >= rows_per_block) && lds <= 64 * 1024) {
-#define GL(TK, TV, NV, MM, D)                                                                                       \
-  hipLaunchKernelGGL((group_direct_lds_kernel<TK, TV, NV, MM, D>), dim3(grid), dim3(256), lds, s, (const TK *)kcol, \
-                     (const TV *)v0, (const TV *)v1, nrows, kmin, nk, R, ring_off, cstar, st0, st1, pr)
+      // packed count (MBX_GD_PACK=0 disables): needs a value column, the
+      // register partials (nslot <= 2048) and a zone-map bound on |v|
+      int pkb = 0, pkf = 0;
+      bool pk = nv >= 1 && (int64_t)nk * R <= 2048 && PackedCountParams(vmaxabs, R, pkb, pkf);
+      if (const char *ep = getenv("MBX_GD_PACK")) pk = pk && atoi(ep) != 0;
+      // MBX_GD_PKF=<steps>: drain more often than needed (tests exercise the drains)
+      if (const char *ef = getenv("MBX_GD_PKF")) pkf = std::max(1, std::min(pkf, atoi(ef)));
+      if ((seg_rows <= 0 || seg_rows >= rows_per_block) && lds <= lds_cap) {
+#define GL(TK, TV, NV, MM, D)                                                                                      \
+  if (pk && NV >= 1)                                                                                               \
+    hipLaunchKernelGGL((group_direct_lds_kernel<TK, TV, NV, MM, D, NV >= 1>), dim3(grid), dim3(256), lds, s,       \
+                       (const TK *)kcol, (const TV *)v0, (const TV *)v1, nrows, kmin, nk, R, ring_off, cstar, st0, \
+                       st1, pr, pkb, pkf);                                                                         \
+  else                                                                                                             \
+    hipLaunchKernelGGL((group_direct_lds_kernel<TK, TV, NV, MM, D, false>), dim3(grid), dim3(256), lds, s,         \
+                       (const TK *)kcol, (const TV *)v0, (const TV *)v1, nrows, kmin, nk, R, ring_off, cstar, st0, \
+                       st1, pr, 0, 1);
 #define GLD(TK, TV, NV, MM) \
-  if (depth == 2) GL(TK, TV, NV, MM, 2); else if (depth == 3) GL(TK, TV, NV, MM, 3); else GL(TK, TV, NV, MM, 4);
+  if (depth == 2) { GL(TK, TV, NV, MM, 2) } else if (depth == 3) { GL(TK, TV, NV, MM, 3) } else { GL(TK, TV, NV, MM, 4) }
 #define GLV(TK, TV)                                                                      \
   if (nv == 0) { GLD(TK, TV, 0, false) }                                                 \
   else if (nv == 1) { if (mm) { GLD(TK, TV, 1, true) } else { GLD(TK, TV, 1, false) } } \

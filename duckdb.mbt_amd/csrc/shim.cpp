@@ -1135,6 +1135,42 @@ char *duckdb_mbx_profile_drain(duckdb_mb_connection *h) {
   return strdup(j.c_str());
 }
 
+// Every cell of a result as text in ONE call: the same strings and NULL flags
+// that duckdb_mb_result_is_null / duckdb_mb_result_value return cell by cell
+// (the per-cell loop of Connection::query, duckdb_native.mbt:477-497), for
+// hosts whose per-call FFI cost dwarfs the formatting.  Layout (little endian):
+//   i64 nrows, i64 ncols, u8 null[nrows*ncols] (row-major), zero padding to 8,
+//   i64 offsets[nrows*ncols + 1], chars.
+// Returns a malloc'd buffer (free with duckdb_mbx_free) and its size in *len.
+char *duckdb_mbx_result_text(duckdb_mb_result *r, int64_t *len) {
+  if (!r || !r->r || !len) return nullptr;
+  const MaterializedResult &m = *r->r;
+  const int64_t nr = m.nrows, nc = (int64_t)m.cols.size(), ncell = nr * nc;
+  std::string chars;
+  std::vector<int64_t> off((size_t)ncell + 1, 0);
+  std::vector<uint8_t> nul((size_t)ncell, 0);
+  for (int64_t row = 0; row < nr; row++)
+    for (int64_t col = 0; col < nc; col++) {
+      const HostColumn &c = m.cols[col];
+      const int64_t i = row * nc + col;
+      if (c.IsNull(row)) nul[i] = 1;
+      else chars += FormatValue(c.Get(row));
+      off[i + 1] = (int64_t)chars.size();
+    }
+  const size_t head = 16 + (((size_t)ncell + 7) & ~(size_t)7);
+  const size_t total = head + off.size() * 8 + chars.size();
+  char *buf = (char *)malloc(total ? total : 1);
+  if (!buf) return nullptr;
+  memset(buf, 0, head);
+  memcpy(buf, &nr, 8);
+  memcpy(buf + 8, &nc, 8);
+  if (ncell) memcpy(buf + 16, nul.data(), (size_t)ncell);
+  memcpy(buf + head, off.data(), off.size() * 8);
+  if (!chars.empty()) memcpy(buf + head + off.size() * 8, chars.data(), chars.size());
+  *len = (int64_t)total;
+  return buf;
+}
+
 int32_t duckdb_mbx_result_raw(duckdb_mb_result *r, int32_t col, int32_t row, void *out, int32_t out_len) {
   if (!r || !InRange(r->r, col, row) || !out) return 0;
   const HostColumn &c = r->r->cols[col];

@@ -217,6 +217,13 @@ int32_t duckdb_mbx_hbm_calibrate(duckdb_mb_connection *handle, int64_t bytes, in
  * materialized result as raw little-endian bytes (HUGEINT: 16 bytes). */
 int32_t duckdb_mbx_result_raw(duckdb_mb_result *result, int32_t col, int32_t row, void *out, int32_t out_len);
 
+/* Every cell of a result as text in one call — the strings and NULL flags of
+ * duckdb_mb_result_is_null/_value (ref src/duckdb_native.c:216-238) for the
+ * per-cell loop of Connection::query (src/duckdb_native.mbt:477-497).
+ * Layout: i64 nrows, i64 ncols, u8 null[nrows*ncols] row-major, zero pad to 8,
+ * i64 offsets[nrows*ncols+1], chars.  malloc'd: free with duckdb_mbx_free. */
+char *duckdb_mbx_result_text(duckdb_mb_result *result, int64_t *len);
+
 #ifdef __cplusplus
 }
 #endif

@@ -120,3 +120,17 @@ def test_prepared_parameter_binding(hostconn, mbx):
     r = st.execute()
     assert isinstance(r, mbx.Err)
     st.close()
+
+
+def test_bulk_text_pull_matches_per_cell(hostconn):
+    # query() pulls every cell in one C call (duckdb_mbx_result_text);
+    # query_percell() is the reference's literal per-cell loop
+    # (duckdb_native.mbt:477-497).  Same strings, same NULL flags.
+    for sql in ["SELECT 1 AS a, NULL AS b, 'héllo' AS c, 2.5 AS d, -9223372036854775808 AS e, '' AS f",
+                "SELECT NULL, NULL AS n2, 1e300 AS big, CAST(NULL AS VARCHAR) AS v",
+                "SELECT 42 WHERE 1 = 0",
+                "CREATE TABLE bulk_t (a INTEGER)"]:
+        a = hostconn.query(sql).value
+        b = hostconn.query_percell(sql.replace("bulk_t", "bulk_t2")).value
+        assert a.rows == b.rows and a.nulls == b.nulls, sql
+        assert a.columns == b.columns and a.column_types == b.column_types

@@ -261,12 +261,16 @@ def test_filter_agg_variants_parity(conn, oracle, monkeypatch, variant):
 
 
 # ---- every fused GROUP BY launch shape gives the same bits ------------------
-GD_VARIANTS = ["", "seg", "d2_g1", "d3_g2", "d4_g2"]
+# "+p0": separate COUNT atomics; "+f<k>": packed-count drains every k wave steps
+GD_VARIANTS = ["", "seg", "d2_g1", "d3_g2", "d4_g2", "+p0", "d2_g1+f1", "d3_g2+f2"]
 
 
 @pytest.mark.parametrize("variant", GD_VARIANTS)
 def test_group_direct_variants_parity(conn, oracle, monkeypatch, variant):
-    monkeypatch.setenv("MBX_GD_VARIANT", variant)
+    base, *opts = variant.split("+")
+    monkeypatch.setenv("MBX_GD_VARIANT", base)
+    for o in opts:
+        monkeypatch.setenv({"p": "MBX_GD_PACK", "f": "MBX_GD_PKF"}[o[0]], o[1:])
     for n in (1, 255, 256, 257, 1023, 70_001, 1_000_003):
         k = oracle.synth_i64(n, 7, 0, 40, -20)           # keys -20..19
         v = oracle.synth_i64(n, 9, 0, 2**40, -2**39)

@@ -1,0 +1,284 @@
+// c3_probe.hip — research microbenchmark (not part of the product): what
+// bounds the C3 GROUP BY kernel's read pattern?  Streams a 4-B key column and
+// an 8-B value column (1e9 rows) through a per-wave LDS-DMA ring, the shape
+// group_direct_lds uses (one 256-row step = 1 KiB key + 2 KiB value), with
+//   work 0: no compute (pure two-array stream),
+//   work 1: + the LDS table atomics (u32 count + u64 sum per row, R = 64),
+//   work 2: + the packed atomic only (u64 per row),
+// and a single-array stream of the same bytes for comparison.
+//   hipcc --offload-arch=gfx950 -O3 -o c3_probe tools/c3_probe.hip && ./c3_probe
+#include <hip/hip_runtime.h>
+#include <cstdio>
+#include <cstdlib>
+#include <vector>
+#include <algorithm>
+
+typedef int v4i32 __attribute__((ext_vector_type(4)));
+typedef long long v2i64 __attribute__((ext_vector_type(2)));
+
+#define CK(x)                                                              \
+  do {                                                                     \
+    hipError_t e_ = (x);                                                   \
+    if (e_ != hipSuccess) {                                                \
+      fprintf(stderr, "%s:%d %s\n", __FILE__, __LINE__, hipGetErrorString(e_)); \
+      exit(1);                                                             \
+    }                                                                      \
+  } while (0)
+
+template <int DEPTH, int WORK>
+__global__ __launch_bounds__(256) void two_stream(const int *__restrict__ keys, const long long *__restrict__ vals,
+                                                  long long nsteps, unsigned long long *out) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
+  constexpr int SB = 3072, R = 64, NK = 32;
+  unsigned int *cnt = (unsigned int *)lds;                      // NK*R*4 = 8 KiB
+  unsigned long long *sum = (unsigned long long *)(lds + 8192);  // NK*R*8 = 16 KiB
+  const int t = threadIdx.x, w = t >> 6, lane = t & 63;
+  unsigned char *ring = lds + 24576 + w * DEPTH * SB;
+  for (int i = t; i < NK * R; i += 256) { cnt[i] = 0; sum[i] = 0; }
+  __syncthreads();
+  const long long nw = (long long)gridDim.x * 4;
+  long long st = (long long)blockIdx.x * 4 + w;
+  auto issue = [&](long long q, int d) {
+    unsigned char *dst = ring + d * SB;
+    const unsigned char *kp = (const unsigned char *)keys + q * 1024;
+    const unsigned char *vp = (const unsigned char *)vals + q * 2048;
+    __builtin_amdgcn_global_load_lds((const void *)(kp + lane * 16), (void *)dst, 16, 0, 2);
+    __builtin_amdgcn_global_load_lds((const void *)(vp + lane * 16), (void *)(dst + 1024), 16, 0, 2);
+    __builtin_amdgcn_global_load_lds((const void *)(vp + 1024 + lane * 16), (void *)(dst + 2048), 16, 0, 2);
+  };
+#pragma unroll
+  for (int d = 0; d < DEPTH; d++) {
+    long long q = st + d * nw;
+    issue(q < nsteps ? q : 0, d);
+  }
+  long long acc = 0;
+  int k = 0;
+  for (; st < nsteps; st += nw) {
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(3 * (DEPTH - 1)) : "memory");
+    const unsigned char *src = ring + k * SB;
+    v4i32 kv = *(const v4i32 *)(src + lane * 16);
+    v2i64 a0 = *(const v2i64 *)(src + 1024 + lane * 32), a1 = *(const v2i64 *)(src + 1024 + lane * 32 + 16);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    long long q = st + DEPTH * nw;
+    issue(q < nsteps ? q : st, k);
+    int kk[4] = {kv.x & 31, kv.y & 31, kv.z & 31, kv.w & 31};
+    long long a[4] = {a0.x, a0.y, a1.x, a1.y};
+    if (WORK == 0) {
+      acc += kk[0] + kk[1] + kk[2] + kk[3] + a[0] + a[1] + a[2] + a[3];
+    } else {
+#pragma unroll
+      for (int e = 0; e < 4; e++) {
+        int sl = kk[e] * R + lane;
+        if (WORK == 1) {
+          atomicAdd(&cnt[sl], 1u);
+          atomicAdd(&sum[sl], (unsigned long long)a[e]);
+        } else {
+          atomicAdd(&sum[sl], ((unsigned long long)a[e] << 12) + 1ull);
+        }
+      }
+    }
+    k = k + 1 == DEPTH ? 0 : k + 1;
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (WORK) acc += cnt[t] + sum[t];
+  if (acc == 0x5a5a5a5a5a5aLL) atomicAdd(out, 1ull);
+}
+
+// the same bytes as ONE array: 3 KiB contiguous per step
+template <int DEPTH>
+__global__ __launch_bounds__(256) void one_stream(const unsigned char *__restrict__ in, long long nsteps,
+                                                  unsigned long long *out) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
+  constexpr int SB = 3072;
+  const int t = threadIdx.x, w = t >> 6, lane = t & 63;
+  unsigned char *ring = lds + w * DEPTH * SB;
+  const long long nw = (long long)gridDim.x * 4;
+  long long st = (long long)blockIdx.x * 4 + w;
+  auto issue = [&](long long q, int d) {
+    unsigned char *dst = ring + d * SB;
+    const unsigned char *p = in + q * 3072;
+#pragma unroll
+    for (int j = 0; j < 3; j++)
+      __builtin_amdgcn_global_load_lds((const void *)(p + j * 1024 + lane * 16), (void *)(dst + j * 1024), 16, 0, 2);
+  };
+#pragma unroll
+  for (int d = 0; d < DEPTH; d++) {
+    long long q = st + d * nw;
+    issue(q < nsteps ? q : 0, d);
+  }
+  long long acc = 0;
+  int k = 0;
+  for (; st < nsteps; st += nw) {
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(3 * (DEPTH - 1)) : "memory");
+    const unsigned char *src = ring + k * SB;
+    v4i32 x = *(const v4i32 *)(src + lane * 16);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    long long q = st + DEPTH * nw;
+    issue(q < nsteps ? q : st, k);
+    acc += x.x + x.y;
+    k = k + 1 == DEPTH ? 0 : k + 1;
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  if (acc == 0x5a5a5a5a5a5aLL) atomicAdd(out, 1ull);
+}
+
+// software-pipelined form: the next slot's ds_reads are issued BEFORE this
+// step's table atomics, so the counted lgkmcnt wait before the refill waits
+// for the reads only (LDS ops retire in order), never for the atomics.
+template <int DEPTH, bool PACKED>
+__global__ __launch_bounds__(256) void two_stream_pipe(const int *__restrict__ keys, const long long *__restrict__ vals,
+                                                       long long nsteps, unsigned long long *out) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
+  constexpr int SB = 3072, R = 64, NK = 32;
+  constexpr int NAT = PACKED ? 4 : 8;
+  unsigned int *cnt = (unsigned int *)lds;
+  unsigned long long *sum = (unsigned long long *)(lds + 8192);
+  const int t = threadIdx.x, w = t >> 6, lane = t & 63;
+  unsigned char *ring = lds + 24576 + w * DEPTH * SB;
+  for (int i = t; i < NK * R; i += 256) { cnt[i] = 0; sum[i] = 0; }
+  __syncthreads();
+  const long long nw = (long long)gridDim.x * 4;
+  long long st = (long long)blockIdx.x * 4 + w;
+  auto issue = [&](long long q, int d) {
+    unsigned char *dst = ring + d * SB;
+    const unsigned char *kp = (const unsigned char *)keys + q * 1024;
+    const unsigned char *vp = (const unsigned char *)vals + q * 2048;
+    __builtin_amdgcn_global_load_lds((const void *)(kp + lane * 16), (void *)dst, 16, 0, 2);
+    __builtin_amdgcn_global_load_lds((const void *)(vp + lane * 16), (void *)(dst + 1024), 16, 0, 2);
+    __builtin_amdgcn_global_load_lds((const void *)(vp + 1024 + lane * 16), (void *)(dst + 2048), 16, 0, 2);
+  };
+  if (st >= nsteps) return;
+#pragma unroll
+  for (int d = 0; d < DEPTH; d++) {
+    long long q = st + d * nw;
+    issue(q < nsteps ? q : 0, d);
+  }
+  v4i32 kv;
+  v2i64 a0, a1;
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(3 * (DEPTH - 1)) : "memory");
+  kv = *(const v4i32 *)(ring + lane * 16);
+  a0 = *(const v2i64 *)(ring + 1024 + lane * 32);
+  a1 = *(const v2i64 *)(ring + 1024 + lane * 32 + 16);
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  issue(st + DEPTH * nw < nsteps ? st + DEPTH * nw : st, 0);
+  int k = 0;
+  for (;;) {
+    const long long nx = st + nw;
+    const int k1 = k + 1 == DEPTH ? 0 : k + 1;
+    v4i32 nkv;
+    v2i64 na0, na1;
+    if (nx < nsteps) {
+      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(3 * (DEPTH - 1)) : "memory");
+      const unsigned char *src = ring + k1 * SB;
+      nkv = *(const v4i32 *)(src + lane * 16);
+      na0 = *(const v2i64 *)(src + 1024 + lane * 32);
+      na1 = *(const v2i64 *)(src + 1024 + lane * 32 + 16);
+    }
+    int kk[4] = {kv.x & 31, kv.y & 31, kv.z & 31, kv.w & 31};
+    long long a[4] = {a0.x, a0.y, a1.x, a1.y};
+#pragma unroll
+    for (int e = 0; e < 4; e++) {
+      int sl = kk[e] * R + lane;
+      if (PACKED) {
+        atomicAdd(&sum[sl], ((unsigned long long)a[e] << 12) + 1ull);
+      } else {
+        atomicAdd(&cnt[sl], 1u);
+        atomicAdd(&sum[sl], (unsigned long long)a[e]);
+      }
+    }
+    if (nx >= nsteps) break;
+    asm volatile("s_waitcnt lgkmcnt(%0)" ::"n"(NAT) : "memory");
+    const long long q = nx + DEPTH * nw;
+    issue(q < nsteps ? q : nx, k1);
+    kv = nkv; a0 = na0; a1 = na1;
+    st = nx;
+    k = k1;
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  long long acc = cnt[t] + sum[t];
+  if (acc == 0x5a5a5a5a5a5aLL) atomicAdd(out, 1ull);
+}
+
+__global__ void fill_keys(int *k, long long n) {
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long long)gridDim.x * blockDim.x) {
+    unsigned long long z = (unsigned long long)i + 0x9e3779b97f4a7c15ull;
+    z = (z ^ (z >> 30)) * 0xbf58476d1ce4e5b9ull;
+    z = (z ^ (z >> 27)) * 0x94d049bb133111ebull;
+    k[i] = (int)((z ^ (z >> 31)) & 31);
+  }
+}
+
+template <typename F>
+static float TimeIt(F f, int iters) {
+  hipEvent_t a, b;
+  CK(hipEventCreate(&a));
+  CK(hipEventCreate(&b));
+  f();
+  CK(hipDeviceSynchronize());
+  std::vector<float> ts;
+  for (int i = 0; i < iters; i++) {
+    CK(hipEventRecord(a));
+    f();
+    CK(hipEventRecord(b));
+    CK(hipEventSynchronize(b));
+    float ms;
+    CK(hipEventElapsedTime(&ms, a, b));
+    ts.push_back(ms);
+  }
+  std::sort(ts.begin(), ts.end());
+  return ts[ts.size() / 2];
+}
+
+int main(int argc, char **argv) {
+  const long long n = argc > 1 ? atoll(argv[1]) : 1000000000LL;
+  const long long nsteps = n / 256;
+  int *k;
+  long long *v;
+  unsigned char *one;
+  unsigned long long *out;
+  CK(hipMalloc(&k, nsteps * 1024));
+  CK(hipMalloc(&v, nsteps * 2048));
+  CK(hipMalloc(&one, nsteps * 3072));
+  CK(hipMalloc(&out, 8));
+  hipLaunchKernelGGL(fill_keys, dim3(4096), dim3(256), 0, 0, k, nsteps * 256);
+  CK(hipMemset(v, 2, nsteps * 2048));
+  CK(hipMemset(one, 3, nsteps * 3072));
+  int cus = 0;
+  CK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, 0));
+  const double bytes = (double)nsteps * 3072;
+  auto report = [&](const char *name, int d, int g, float ms) {
+    printf("%-12s d%d g%d  %.4f ms  %.0f GB/s\n", name, d, g, ms, bytes / ms / 1e6);
+    fflush(stdout);
+  };
+#define RUN2(D, W, G)                                                                                         \
+  {                                                                                                           \
+    size_t lds = 24576 + 4 * (D) * 3072;                                                                      \
+    CK(hipFuncSetAttribute((const void *)two_stream<D, W>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds)); \
+    float ms = TimeIt([&] { hipLaunchKernelGGL((two_stream<D, W>), dim3(cus * (G)), dim3(256), lds, 0, k, v, nsteps, out); }, 15); \
+    report(W == 0 ? "two/none" : W == 1 ? "two/atom2" : "two/packed", D, G, ms);                              \
+  }
+#define RUN1(D, G)                                                                                            \
+  {                                                                                                           \
+    size_t lds = 4 * (D) * 3072;                                                                              \
+    CK(hipFuncSetAttribute((const void *)one_stream<D>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds)); \
+    float ms = TimeIt([&] { hipLaunchKernelGGL((one_stream<D>), dim3(cus * (G)), dim3(256), lds, 0, one, nsteps, out); }, 15); \
+    report("one/none", D, G, ms);                                                                             \
+  }
+#define RUNP(D, P, G)                                                                                         \
+  {                                                                                                           \
+    size_t lds = 24576 + 4 * (D) * 3072;                                                                      \
+    CK(hipFuncSetAttribute((const void *)two_stream_pipe<D, P>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds)); \
+    float ms = TimeIt([&] { hipLaunchKernelGGL((two_stream_pipe<D, P>), dim3(cus * (G)), dim3(256), lds, 0, k, v, nsteps, out); }, 15); \
+    report(P ? "pipe/packed" : "pipe/atom2", D, G, ms);                                                      \
+  }
+  RUNP(3, false, 1) RUNP(4, false, 1) RUNP(6, false, 1) RUNP(3, true, 1) RUNP(4, true, 1) RUNP(6, true, 1)
+  RUNP(3, false, 2) RUNP(3, true, 2) RUNP(2, false, 3) RUNP(2, true, 3)
+  RUN2(2, 0, 1) RUN2(2, 1, 3) RUN2(2, 2, 3)
+  RUN1(2, 1) RUN1(2, 2) RUN1(2, 3) RUN1(4, 1) RUN1(4, 2) RUN1(6, 1)
+  RUN2(2, 0, 1) RUN2(2, 0, 2) RUN2(2, 0, 3) RUN2(4, 0, 1) RUN2(4, 0, 2) RUN2(6, 0, 1)
+  RUN2(2, 1, 2) RUN2(2, 1, 3) RUN2(4, 1, 1) RUN2(4, 1, 2) RUN2(6, 1, 1)
+  RUN2(2, 2, 2) RUN2(2, 2, 3) RUN2(4, 2, 1) RUN2(4, 2, 2) RUN2(6, 2, 1)
+  return 0;
+}

@@ -1,7 +1,8 @@
 #!/usr/bin/env python3
 """A/B sweep of the fused GROUP BY (group_direct) launch variants on the C3
 table in ONE process: interleaved rounds, median/min kernel time.  GPU only.
-Variants: MBX_GD_VARIANT = "d<depth>_g<blocks per CU>" (LDS-DMA) or "seg"."""
+Variants: MBX_GD_VARIANT = "d<depth>_g<blocks per CU>" (LDS-DMA) or "seg",
+with options "+r<replicas>" and "+p0" (separate COUNT atomics instead of packed)."""
 import json
 import os
 import statistics
@@ -30,10 +31,13 @@ for name, sql in sqls.items():
     for rnd in range(rounds):
         for v in (variants if rnd % 2 == 0 else variants[::-1]):
             os.environ["MBX_GD_VARIANT"] = v.split("+")[0]
-            if "+r" in v:
-                os.environ["MBX_GD_R"] = v.split("+r")[1]
-            else:
-                os.environ.pop("MBX_GD_R", None)
+            os.environ.pop("MBX_GD_R", None)
+            os.environ.pop("MBX_GD_PACK", None)
+            for opt in v.split("+")[1:]:
+                if opt.startswith("r"):
+                    os.environ["MBX_GD_R"] = opt[1:]
+                elif opt.startswith("p"):
+                    os.environ["MBX_GD_PACK"] = opt[1:]  # p0: unpacked count atomics
             r = c.query(sql)
             assert isinstance(r, m.Ok), r
             rows = sorted(r.value.rows)
