@@ -247,8 +247,8 @@ def main():
             },
             "parity": parity,
         }
-        if not args.no_cpu and args.config in ("c2", "c5"):
-            result["cpu_baseline"] = cpu_baseline(args.cpu_seconds)
+        if not args.no_cpu and args.config in ("c2", "c3", "c5"):
+            result["cpu_baseline"] = cpu_baseline(args.cpu_seconds, args.config)
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()
@@ -298,19 +298,29 @@ def bench_c4(mbx, conn, n, args):
     conn.close()
 
 
-def cpu_baseline(seconds):
-    """The oracle's multi-threaded C scan (oracle/oracle.c orc_filter_agg_i64)
-    over a materialised sample of the same column, on this host's cores."""
+def cpu_baseline(seconds, config="c2"):
+    """The oracle's multi-threaded C scan over a materialised sample of the same
+    column(s), on this host's cores: orc_filter_agg_i64 (C2/C5: COUNT/SUM/MIN/MAX
+    WHERE x > 24) or orc_groupby_sum_i32_i64 (C3: per-key COUNT and int128 SUM).
+    Data generation is outside the timed loop."""
     sys.path.insert(0, HERE)
     from oracle import Oracle
     orc = Oracle()
     threads = min(16, len(os.sched_getaffinity(0)))
     sample = 100_000_000
-    x = orc.synth_i64(sample, 42, 0, 50, 1)
+    if config == "c3":
+        k = orc.synth_i32(sample, 7, 0, 32, 0)
+        v = orc.synth_i64(sample, 9, 0, 1 << 40, -(1 << 39))
+        run = lambda: orc.groupby_sum(k, v, 0, 32, threads)  # noqa: E731
+        what = "GROUP BY k: COUNT(*), SUM(v) (int128), 32 keys"
+    else:
+        x = orc.synth_i64(sample, 42, 0, 50, 1)
+        run = lambda: orc.filter_agg_i64(x, 25, 2**63 - 1, threads)  # noqa: E731
+        what = "COUNT/SUM/MIN/MAX with x > 24"
     scanned = 0
     t0 = time.perf_counter()
     while True:
-        orc.filter_agg_i64(x, 25, 2**63 - 1, threads)
+        run()
         scanned += sample
         if time.perf_counter() - t0 >= seconds:
             break
@@ -325,8 +335,8 @@ def cpu_baseline(seconds):
     except Exception:
         pass
     return {"value": scanned / dt, "unit": "rows/s", "cores": threads, "kind": "port",
-            "sample": f"{sample} rows (first 1e8 of the same column) scanned {scanned // sample}x in {dt:.1f}s, "
-                      f"COUNT/SUM/MIN/MAX with x > 24, pthreads={threads}, cpu={model or platform.processor()}"}
+            "sample": f"{sample} rows (first 1e8 of the same columns) scanned {scanned // sample}x in {dt:.1f}s, "
+                      f"{what}, pthreads={threads}, cpu={model or platform.processor()}"}
 
 
 if __name__ == "__main__":

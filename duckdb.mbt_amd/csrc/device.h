@@ -251,6 +251,27 @@ struct HostCopyDesc {
   int32_t *err_dst;
 };
 void HostCopy(const HostCopyDesc &d, hipStream_t s);
+
+// Filter -> compaction in two streaming passes (order preserving), for a
+// conjunction of range predicates over NULL-free int32/int64 columns and
+// NULL-free 4- or 8-byte output columns.  A "step" is 256 consecutive rows.
+//  1. FilterBits: predicate columns through an LDS-DMA ring; per step four
+//     ballot words (bit L of word e <-> row 256 s + 4 L + e, the lane layout
+//     of both passes) and the step's selected-row count.
+//  2. ScanTileCounts -> each step's first output position (exclusive scan).
+//  3. CompactColumns: output columns through an LDS-DMA ring; each selected
+//     row goes to offset[step] + its rank inside the step.
+#define FC_MAX_OUT 8
+struct CompactDesc {
+  int32_t nout;
+  const void *src[FC_MAX_OUT];
+  void *dst[FC_MAX_OUT];
+  int32_t ow[FC_MAX_OUT];  // 4 or 8 bytes
+};
+void FilterBits(const FilterMultiDesc &d, int64_t nrows, unsigned long long *bits, uint32_t *step_counts,
+                hipStream_t s);
+void CompactColumns(const CompactDesc &d, int64_t nrows, const unsigned long long *bits, const int64_t *step_offsets,
+                    hipStream_t s);
 void RebaseOffsets(const int64_t *src, int64_t *dst, int64_t n, int64_t delta, hipStream_t s);
 
 }  // namespace dev

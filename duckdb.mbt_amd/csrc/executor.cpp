@@ -781,10 +781,17 @@ static void MaterializeStrings(Engine &e, DCol &out, const DCol *src, const StrP
   out.data = nullptr;
 }
 
+static bool TryFilterCompact(Engine &e, const DRel &rel, const BExpr &pred, const std::vector<BExprPtr> &exprs,
+                             DRel &out);
+
 // Evaluates `pred` (may be null) and `exprs` over `rel`; returns the
 // projected relation of the selected rows.
 static DRel FilterProject(Engine &e, const DRel &rel, const BExprPtr &pred, const std::vector<BExprPtr> &exprs) {
   const int64_t n = rel.n;
+  {
+    DRel fused;
+    if (pred && pred->kind != BExpr::CONST && TryFilterCompact(e, rel, *pred, exprs, fused)) return fused;
+  }
   // pure column passthrough, no predicate, no virtual range column
   bool passthrough = !pred;
   for (auto &x : exprs)
@@ -964,6 +971,91 @@ static bool FastIntCol(const DRel &rel, int c) {
   if (rel.range && c == 0) return false;
   const DCol &d = rel.cols[c];
   return d.validity == nullptr && (d.phys == P_I32 || d.phys == P_I64) && d.data != nullptr;
+}
+
+// WHERE <range conjunction over NULL-free int columns> with plain NULL-free
+// 4/8-byte output columns: two streaming passes (dev::FilterBits, scan,
+// dev::CompactColumns) instead of vm_filter + scan + vm_project.  MBX_FC=0
+// disables it.
+static bool TryFilterCompact(Engine &e, const DRel &rel, const BExpr &pred, const std::vector<BExprPtr> &exprs,
+                             DRel &out) {
+  const char *fc = getenv("MBX_FC");
+  if ((fc && atoi(fc) == 0) || rel.range || rel.n <= 0 || exprs.empty()) return false;
+  std::map<int, std::pair<i128, i128>> ranges;
+  if (!RangeConj(pred, ranges) || ranges.empty() || ranges.size() > FM_MAX) return false;
+  dev::FilterMultiDesc F;
+  memset(&F, 0, sizeof(F));
+  F.agg = -1;
+  bool empty = false;
+  for (auto &kv : ranges) {
+    if (!FastIntCol(rel, kv.first)) return false;
+    const DCol &c = rel.cols[kv.first];
+    const bool wide = c.phys == P_I64;
+    if ((uintptr_t)c.data % 16) return false;  // 16-B LDS-DMA lanes
+    dev::FilterMultiCol &fc_ = F.col[F.ncol++];
+    fc_.data = c.data;
+    fc_.phys = c.phys;
+    fc_.is_pred = 1;
+    const i128 lo = std::max<i128>(kv.second.first, wide ? (i128)INT64_MIN : (i128)INT32_MIN);
+    const i128 hi = std::min<i128>(kv.second.second, wide ? (i128)INT64_MAX : (i128)INT32_MAX);
+    if (lo > hi) empty = true;
+    fc_.lo = (int64_t)lo;
+    fc_.span = lo > hi ? 0 : (uint64_t)(int64_t)hi - (uint64_t)(int64_t)lo;
+  }
+  for (auto &x : exprs) {
+    if (x->kind != BExpr::COL || (rel.range && x->col == 0)) return false;
+    const DCol &c = rel.cols[x->col];
+    if (c.validity || !c.data || c.phys == P_STR) return false;
+    const int w = PhysSize(c.phys);
+    if ((w != 4 && w != 8) || (uintptr_t)c.data % 16) return false;
+  }
+  out = DRel();
+  const int64_t n = rel.n;
+  if (empty) {  // nothing passes: typed empty columns
+    for (auto &x : exprs) out.cols.push_back(AllocOut(e, x->type, 0, false));
+    return true;
+  }
+  const int64_t steps = (n + 255) / 256;
+  auto bits = Alloc(e, (size_t)steps * 32);
+  auto counts = Alloc(e, (size_t)steps * 4);
+  auto offs = Alloc(e, (size_t)(steps + 2) * 8);  // compact reads offsets in 16-B aligned pairs
+  double pbytes = 0;
+  for (int j = 0; j < F.ncol; j++) pbytes += (double)n * (F.col[j].phys == P_I64 ? 8 : 4);
+  {
+    ProfScope ps(e, "filter_bits", pbytes + (double)steps * 36, n);
+    dev::FilterBits(F, n, (unsigned long long *)bits->p, (uint32_t *)counts->p, e.stream);
+  }
+  dev::ScanTileCounts((const uint32_t *)counts->p, (int64_t *)offs->p, steps, e.d_scratch, e.stream);
+  const int64_t nsel = ReadDev<int64_t>(e, e.d_scratch);
+  out.n = nsel;
+  std::vector<DCol> cols;
+  for (auto &x : exprs) cols.push_back(AllocOut(e, x->type, nsel, false));
+  if (nsel > 0) {
+    // output columns in groups of at most 8 KiB per 256-row step
+    size_t k = 0;
+    while (k < exprs.size()) {
+      dev::CompactDesc C;
+      memset(&C, 0, sizeof(C));
+      int kib = 0;
+      double bytes = (double)steps * 40;
+      for (; k < exprs.size() && C.nout < FC_MAX_OUT; k++) {
+        const DCol &c = rel.cols[exprs[k]->col];
+        const int w = PhysSize(c.phys);
+        if (kib + w / 4 > 8) break;
+        kib += w / 4;
+        C.src[C.nout] = c.data;
+        C.dst[C.nout] = cols[k].data;
+        C.ow[C.nout] = w;
+        C.nout++;
+        bytes += (double)n * w + (double)nsel * w;
+      }
+      ProfScope ps(e, "compact", bytes, n);
+      dev::CompactColumns(C, n, (const unsigned long long *)bits->p, (const int64_t *)offs->p, e.stream);
+    }
+  }
+  out.cols = cols;
+  CheckError(e);
+  return true;
 }
 
 static dev::EmitAgg EmitFor(const AggSpec &a, VClass in_class, dev::AggState *states, DCol &out) {

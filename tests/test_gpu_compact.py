@@ -1,0 +1,106 @@
+"""Filter -> compaction (dev::FilterBits + scan + dev::CompactColumns) against
+the CPU oracle's generator arrays and against the VM path (MBX_FC=0): the
+selected rows of every output column, in row order, bit for bit.  Sizes
+straddle the 256-row step and the ring's grid-stride (partial last step,
+one-row tail, many steps)."""
+import numpy as np
+import pytest
+
+from conftest import one, q
+
+pytestmark = pytest.mark.gpu
+
+SIZES = [1, 2, 255, 256, 257, 4097, 12_289, 1_000_003]
+
+
+def _col(conn, sql, kind, idx=0):
+    a = conn.query_arrow(sql).value
+    b = a._buf(kind, idx)
+    a.close()
+    n = int.from_bytes(b[:4], "little", signed=True) if len(b) >= 4 else 0
+    return np.frombuffer(b[4:4 + n * (8 if kind in ("int64", "double") else 4)],
+                         dtype=np.int64 if kind == "int64" else np.int32 if kind == "int32" else np.float64)
+
+
+def _table(conn, oracle, n):
+    q(conn, "DROP TABLE IF EXISTS fc")
+    q(conn, f"CREATE TABLE fc AS SELECT mbx_synth(42, i, 50) + 1 AS x, CAST(mbx_synth(7, i, 32) AS INTEGER) AS k, "
+            f"mbx_synth(9, i, 1099511627776) - 549755813888 AS v, "
+            f"CAST(mbx_synth(11, i, 1000) - 500 AS SMALLINT) AS s, "
+            f"CAST(mbx_synth(9, i, 1099511627776) - 549755813888 AS HUGEINT) * 1000000000000 AS h "
+            f"FROM range({n}) tbl(i)")
+    return (oracle.synth_i64(n, 42, 0, 50, 1), oracle.synth_i64(n, 7, 0, 32, 0),
+            oracle.synth_i64(n, 9, 0, 2**40, -2**39), oracle.synth_i64(n, 11, 0, 1000, -500))
+
+
+@pytest.mark.parametrize("n", SIZES)
+def test_filter_compact_parity(conn, oracle, monkeypatch, n):
+    x, k, v, s = _table(conn, oracle, n)
+    cases = [
+        ("SELECT x FROM fc WHERE x > 24", x > 24, [("int64", x)]),
+        ("SELECT k, v FROM fc WHERE x > 24 AND k < 16", (x > 24) & (k < 16), [("int32", k), ("int64", v)]),
+        ("SELECT v, x FROM fc WHERE x BETWEEN 10 AND 40 AND k >= 3 AND v > 0",
+         (x >= 10) & (x <= 40) & (k >= 3) & (v > 0), [("int64", v), ("int64", x)]),
+        ("SELECT x FROM fc WHERE x >= 1", np.ones(n, bool), [("int64", x)]),
+    ]
+    for sql, m, cols in cases:
+        for i, (kind, arr) in enumerate(cols):
+            got = _col(conn, sql, kind, i)
+            assert np.array_equal(got, arr[m].astype(got.dtype)), (n, sql, i)
+        monkeypatch.setenv("MBX_FC", "0")  # the two-pass VM path gives the same bits
+        for i, (kind, _) in enumerate(cols):
+            assert np.array_equal(_col(conn, sql, kind, i), _col(conn, sql, kind, i)), (n, sql)
+        monkeypatch.delenv("MBX_FC")
+    # nothing passes: typed empty result
+    r = q(conn, "SELECT x, k FROM fc WHERE x > 100")
+    assert r.rows == [] and r.column_types == ["BigInt", "Integer"]
+    # 2- and 16-byte outputs (SMALLINT, HUGEINT) through CTAS, checked by aggregates
+    m = (x > 24) & (k < 16)
+    q(conn, "CREATE OR REPLACE TABLE fc2 AS SELECT s, h, x FROM fc WHERE x > 24 AND k < 16")
+    got = one(conn, "SELECT COUNT(*), SUM(s), SUM(h), SUM(x) FROM fc2")
+    exp_h = int(v[m].astype(object).sum()) * 10**12
+    assert [int(g) if g else 0 for g in got] == [int(m.sum()), int(s[m].sum()), exp_h, int(x[m].sum())], n
+    if m.sum():
+        first = np.flatnonzero(m)[0]
+        assert q(conn, "SELECT s, h FROM fc2 LIMIT 1").rows[0] == [str(s[first]), str(int(v[first]) * 10**12)]
+
+
+def test_filter_compact_decimal_predicate(conn, oracle):
+    n = 100_003
+    x = oracle.synth_i64(n, 42, 0, 50, 1)
+    q(conn, "DROP TABLE IF EXISTS fcd")
+    q(conn, f"CREATE TABLE fcd AS SELECT CAST(mbx_synth(42, i, 50) + 1 AS DECIMAL(15,2)) AS q, i AS r "
+            f"FROM range({n}) tbl(i)")
+    got = _col(conn, "SELECT r FROM fcd WHERE q > 24", "int64")  # DECIMAL literal folded to raw > 2400
+    assert np.array_equal(got, np.flatnonzero(x > 24))
+    got = _col(conn, "SELECT r FROM fcd WHERE q >= 24.5 AND q < 30", "int64")
+    assert np.array_equal(got, np.flatnonzero((x >= 25) & (x < 30)))
+
+
+def test_filter_compact_runs_the_hip_passes(mbx, oracle):
+    cfg = mbx.Config.create()
+    cfg.set("mbx_profile", "true")
+    c = mbx.connect_with_config(cfg).value
+    n = 200_003
+    x, k, v, s = _table(c, oracle, n)
+    got = _col(c, "SELECT v, k FROM fc WHERE x > 24 AND k < 16", "int64")
+    names = [kk["name"] for kk in c.last_profile()["kernels"]]
+    assert "filter_bits" in names and "compact" in names, names
+    assert np.array_equal(got, v[(x > 24) & (k < 16)])
+    c.close()
+
+
+def test_filter_compact_profile_and_stream(conn, oracle):
+    n = 3_000_017
+    x, k, v, s = _table(conn, oracle, n)
+    m = x > 24
+    st = conn.query_stream("SELECT v FROM fc WHERE x > 24").value
+    got = []
+    while True:
+        r = st.next().value
+        if r is None:
+            break
+        got.extend(int(row[0]) for row in r.rows)
+    st.close()
+    assert got == v[m].tolist()
+    q(conn, "SELECT COUNT(*) FROM (SELECT v FROM fc WHERE x > 24) t")

@@ -32,6 +32,13 @@ shapes = {
     "group_expr2": "SELECT k, k2, SUM(v + x), MIN(v), COUNT(*) FROM t WHERE x + k2 > 24 GROUP BY k, k2",
     "filter_multi3": "SELECT SUM(v), MIN(v), MAX(v) FROM t WHERE x BETWEEN 10 AND 40 AND k < 16 AND k2 = 1",
     "wide_key": "SELECT v % 1000003, COUNT(*) FROM t GROUP BY v % 1000003",
+    # selection compaction kept on the device (STREAM: the result stays in HBM; no batch is fetched)
+    "sel": "STREAM SELECT x FROM t WHERE x > 24",
+    "sel2": "STREAM SELECT k, v FROM t WHERE x > 24",
+    "sel3": "STREAM SELECT v FROM t WHERE x > 24 AND k < 16",
+    "compact": "CREATE OR REPLACE TABLE tc AS SELECT x FROM t WHERE x > 24",
+    "compact2": "CREATE OR REPLACE TABLE tc AS SELECT k, v FROM t WHERE x > 24",
+    "compact_expr": "CREATE OR REPLACE TABLE tc AS SELECT v + x AS y FROM t WHERE x > 24 AND k < 16",
 }
 if os.environ.get("SHAPES"):
     shapes = {k: v for k, v in shapes.items() if k in os.environ["SHAPES"].split(",")}
@@ -41,7 +48,10 @@ for name, sql in shapes.items():
     for i in range(5):
         t0 = time.perf_counter()
         try:
-            rr = c.query_raw(sql)  # engine time: no per-cell pull of the result
+            if sql.startswith("STREAM "):
+                rr = c.query_stream(sql[7:]).value
+            else:
+                rr = c.query_raw(sql)  # engine time: no per-cell pull of the result
         except Exception as ex:  # noqa: BLE001
             out[name] = {"error": str(ex)}
             break
