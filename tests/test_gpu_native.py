@@ -206,10 +206,12 @@ def test_insert_values_and_select(conn):
 def test_bulk_text_pull_matches_per_cell_on_device(conn):
     # multi-row device results with NULLs, VARCHAR, DECIMAL, HUGEINT and DOUBLE
     conn.query("DROP TABLE IF EXISTS bt")
-    conn.query("CREATE TABLE bt AS SELECT i AS a, CASE WHEN i % 3 = 0 THEN NULL ELSE 'v' || CAST(i AS VARCHAR) END AS b, "
-               "CAST(i AS DECIMAL(15,2)) / 7 AS c, i * 0.5 AS d FROM range(3000) tbl(i)")
-    for sql in ["SELECT * FROM bt", "SELECT a % 7 AS k, SUM(a), COUNT(b), MIN(b) FROM bt GROUP BY a % 7 ORDER BY k",
-                "SELECT b FROM bt WHERE a > 2990 ORDER BY a"]:
+    r = conn.query("CREATE TABLE bt AS SELECT i AS a, CASE WHEN i % 3 = 0 THEN NULL WHEN i % 3 = 1 THEN 'one' "
+                   "ELSE 'twó' END AS b, CAST(i AS DECIMAL(15,2)) AS c, i * 0.5 AS d, "
+                   "CAST(i AS HUGEINT) * 1000000000000 AS h FROM range(3000) tbl(i)")
+    assert hasattr(r, "value"), r
+    for sql in ["SELECT * FROM bt", "SELECT a % 7 AS k, SUM(a), COUNT(b), SUM(c) FROM bt GROUP BY a % 7 ORDER BY k",
+                "SELECT b, h FROM bt WHERE a > 2990 ORDER BY a"]:
         a = conn.query(sql).value
         b = conn.query_percell(sql).value
         assert a.rows == b.rows and a.nulls == b.nulls and a.columns == b.columns, sql
