@@ -290,12 +290,29 @@ def bench_c4(mbx, conn, n, args):
     ok = all(np.array_equal(np.frombuffer(b[4:], dtype=np.int64), v[k:k + 1_000_000])
              for b, k in zip(slices, range(0, n, 1_000_000)))
     ok &= one_count(conn) == n
+    conn.close()
+    # the same round trip through the reference's row-wise Appender API
+    # (begin_row / append_bigint / end_row per row), driven natively from C
+    row_api = None
+    try:
+        import subprocess
+        import tempfile
+        lib = os.path.join(HERE, "duckdb.mbt_amd")
+        exe = os.path.join(tempfile.mkdtemp(), "mb_harness")
+        subprocess.run(["gcc", "-O2", "-std=c11", "-I", os.path.join(HERE, "include"),
+                        os.path.join(HERE, "tests", "c_harness", "mb_harness.c"), "-o", exe, "-L", lib,
+                        "-lduckdb_mb_amd", f"-Wl,-rpath,{lib}"], check=True, capture_output=True)
+        p = subprocess.run([exe, "c4", str(n)], capture_output=True, text=True, timeout=600)
+        row_api = json.loads(p.stdout.strip().splitlines()[-1]) if p.returncode == 0 else {"error": p.stderr[-400:]}
+    except Exception as ex:  # noqa: BLE001
+        row_api = {"error": str(ex)}
     res = {"metric": "C4 appender ingest + arrow read-back", "value": n / (t_in + t_out), "unit": "rows/s",
            "n_gpus": 1, "ingest_gbs": n * 8 / t_in / 1e9, "readback_gbs": n * 8 / t_out / 1e9,
            "ingest_s": t_in, "readback_s": t_out, "rows": n, "bit_exact": ok,
-           "bound": "host link (PCIe Gen5 x16, 63 GB/s spec) + host-side wire-buffer assembly"}
+           "bound": "host link (PCIe Gen5 x16, 63 GB/s spec) + host-side wire-buffer assembly",
+           "ingest_api": "columnar duckdb_mbx_append_column (extension), from Python",
+           "row_appender_native": row_api}
     print(json.dumps(res), flush=True)
-    conn.close()
 
 
 def cpu_baseline(seconds, config="c2"):

@@ -114,7 +114,6 @@ struct duckdb_mb_appender {
   duckdb_mb_connection *conn = nullptr;
   TablePtr table;
   HostBatch batch;
-  std::vector<Value> row;
   size_t col = 0;
   char error[256];
   // columnar bulk ingest
@@ -555,6 +554,19 @@ duckdb_mb_appender *duckdb_mb_appender_create(duckdb_mb_connection *h, moonbit_b
 }
 
 static bool FlushAppender(duckdb_mb_appender *a) {
+  // a partial row (destroy with a row half appended) stays out of the flush
+  for (auto &hc : a->batch.cols) {
+    const size_t n = (size_t)a->batch.nrows;
+    if (hc.phys == P_STR) {
+      if (hc.offsets.size() > n + 1) {
+        hc.offsets.resize(n + 1);
+        hc.chars.resize((size_t)hc.offsets[n]);
+      }
+    } else if (hc.data.size() > n * PhysSize(hc.phys)) {
+      hc.data.resize(n * PhysSize(hc.phys));
+    }
+    if (hc.valid.size() > n) hc.valid.resize(n);
+  }
   if (a->batch.nrows == 0) return true;
   try {
     AppendHostBatch(a->conn->conn, *a->table, a->batch);
@@ -587,6 +599,9 @@ int32_t duckdb_mb_begin_row(duckdb_mb_appender *a) {  // ref :1100-1114
   return 1;
 }
 
+// Values go straight into the batch's column buffers (a flush happens only at
+// a row boundary, so a partial row never reaches the device); the integer
+// appends into a column of their own width skip the Value round trip.
 static int32_t AppendValue(duckdb_mb_appender *a, const Value &v) {
   if (!a) return 0;
   if (a->col >= a->table->cols.size()) {
@@ -594,7 +609,7 @@ static int32_t AppendValue(duckdb_mb_appender *a, const Value &v) {
     return 0;
   }
   try {
-    a->row.push_back(CastValue(v, a->table->cols[a->col].type));
+    HostColumnPush(a->batch.cols[a->col], CastValue(v, a->table->cols[a->col].type));
   } catch (std::exception &e) {
     CopyErr(a->error, e.what());
     return 0;
@@ -603,8 +618,29 @@ static int32_t AppendValue(duckdb_mb_appender *a, const Value &v) {
   return 1;
 }
 
-int32_t duckdb_mb_append_int(duckdb_mb_appender *a, int32_t v) { return AppendValue(a, Value::Int(T_INTEGER, v)); }  // ref :1116
-int32_t duckdb_mb_append_bigint(duckdb_mb_appender *a, int64_t v) { return AppendValue(a, Value::Int(T_BIGINT, v)); }  // ref :1132
+// 1: appended; -1: not this column's exact type (or it has NULLs) -> AppendValue
+static inline int32_t AppendRaw(duckdb_mb_appender *a, const void *v, int sz, TypeId tid, Phys phys) {
+  if (a && a->col < a->batch.cols.size()) {
+    HostColumn &hc = a->batch.cols[a->col];
+    if (hc.phys == phys && hc.type.id == tid && hc.valid.empty()) {
+      const size_t at = hc.data.size();
+      hc.data.resize(at + sz);
+      memcpy(hc.data.data() + at, v, sz);
+      a->col++;
+      return 1;
+    }
+  }
+  return -1;
+}
+
+int32_t duckdb_mb_append_int(duckdb_mb_appender *a, int32_t v) {  // ref :1116
+  const int32_t r = AppendRaw(a, &v, 4, T_INTEGER, P_I32);
+  return r >= 0 ? r : AppendValue(a, Value::Int(T_INTEGER, v));
+}
+int32_t duckdb_mb_append_bigint(duckdb_mb_appender *a, int64_t v) {  // ref :1132
+  const int32_t r = AppendRaw(a, &v, 8, T_BIGINT, P_I64);
+  return r >= 0 ? r : AppendValue(a, Value::Int(T_BIGINT, v));
+}
 int32_t duckdb_mb_append_double(duckdb_mb_appender *a, double v) { return AppendValue(a, Value::Double(v)); }  // ref :1148
 int32_t duckdb_mb_append_varchar(duckdb_mb_appender *a, moonbit_bytes_t v) {  // ref :1164
   return AppendValue(a, Value::Varchar(BytesStr(v)));
@@ -616,7 +652,7 @@ int32_t duckdb_mb_append_null(duckdb_mb_appender *a) {  // ref :1205
     CopyErr(a->error, "Too many appends for chunk!");
     return 0;
   }
-  a->row.push_back(Value::Null(a->table->cols[a->col].type));
+  HostColumnPush(a->batch.cols[a->col], Value::Null(a->table->cols[a->col].type));
   a->col++;
   return 1;
 }
@@ -626,9 +662,7 @@ int32_t duckdb_mb_end_row(duckdb_mb_appender *a) {  // ref :1221-1235
     CopyErr(a->error, "Call to EndRow before all columns have been appended to!");
     return 0;
   }
-  for (size_t i = 0; i < a->row.size(); i++) HostColumnPush(a->batch.cols[i], a->row[i]);
   a->batch.nrows++;
-  a->row.clear();
   a->col = 0;
   if (a->batch.nrows >= a->conn->conn.opts.appender_flush_rows) return FlushAppender(a) ? 1 : 0;
   return 1;

@@ -9,11 +9,15 @@
  *   mb_harness cpu          host-constant queries only (mbx_allow_no_gpu)
  *   mb_harness gpu <rows>   C2 on the device: COUNT(*) WHERE x > 24, appender,
  *                           Arrow int64 getter; prints "count=<n>"
+ *   mb_harness c4 <rows>    C4 through the row-wise Appender + Arrow getter:
+ *                           one JSON line (ingest rows/s, read-back GB/s)
  * Exit status 0 = every check passed.
  */
+#define _POSIX_C_SOURCE 199309L
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
+#include <time.h>
 
 #include "duckdb_mb.h"
 
@@ -192,11 +196,80 @@ static int gpu_checks(duckdb_mb_connection *c, long rows) {
   return 0;
 }
 
+/* C4 through the reference's own row-wise Appender API, as a native MoonBit
+ * caller drives it (src/duckdb_native.mbt:955-1076): 1 begin_row + 1
+ * append_bigint + 1 end_row per row, close => flush; then the Arrow int64
+ * getter over 1e6-row slices (the MoonBit decoder cap).  Values bit-exact.
+ * Prints one JSON line. */
+
+static double now_s(void) {
+  struct timespec ts;
+  clock_gettime(CLOCK_MONOTONIC, &ts);
+  return ts.tv_sec + ts.tv_nsec * 1e-9;
+}
+static int64_t c4_value(int64_t i) { return (int64_t)(((uint64_t)i * 2654435761ull) & 0x7fffffffffffffffull); }
+
+static int c4_bench(duckdb_mb_connection *c, long rows) {
+  moonbit_bytes_t sql = S("CREATE TABLE c4 (v BIGINT)");
+  duckdb_mb_result *r = duckdb_mb_query(c, sql);
+  mb_free(sql);
+  if (r) duckdb_mb_result_destroy(r);
+  moonbit_bytes_t sch = S("main"), tab = S("c4");
+  duckdb_mb_appender *ap = duckdb_mb_appender_create(c, sch, tab);
+  mb_free(sch);
+  mb_free(tab);
+  CHECK(ap != NULL, "appender_create");
+  if (!ap) return 1;
+  double t0 = now_s();
+  int ok = 1;
+  for (int64_t i = 0; i < rows; i++) {
+    ok &= duckdb_mb_begin_row(ap);
+    ok &= duckdb_mb_append_bigint(ap, c4_value(i));
+    ok &= duckdb_mb_end_row(ap);
+  }
+  ok &= duckdb_mb_flush(ap);
+  duckdb_mb_appender_destroy(ap);
+  double t_in = now_s() - t0;
+  CHECK(ok, "row-wise appends");
+  t0 = now_s();
+  long checked = 0, bad = 0;
+  for (long k = 0; k < rows; k += 1000000) {
+    char q[160];
+    snprintf(q, sizeof q, "SELECT v FROM c4 LIMIT 1000000 OFFSET %ld", k);
+    sql = S(q);
+    duckdb_mb_arrow_result *ar = duckdb_mb_query_arrow(c, sql);
+    mb_free(sql);
+    if (!ar) { bad++; break; }
+    moonbit_bytes_t w = duckdb_mb_arrow_get_column_int64(ar, 0);
+    int32_t cnt;
+    memcpy(&cnt, w, 4);
+    for (int32_t i = 0; i < cnt; i++) {
+      int64_t v;
+      memcpy(&v, w + 4 + 8 * (size_t)i, 8);
+      bad += v != c4_value(k + i);
+    }
+    checked += cnt;
+    mb_free(w);
+    duckdb_mb_arrow_destroy(ar);
+  }
+  double t_out = now_s() - t0;
+  CHECK(checked == rows && bad == 0, "c4 read-back: %ld rows checked, %ld mismatches", checked, bad);
+  printf("{\"rows\": %ld, \"ingest_s\": %.6f, \"ingest_rows_per_s\": %.1f, \"readback_s\": %.6f, "
+         "\"readback_gbs\": %.3f, \"bit_exact\": %s}\n",
+         rows, t_in, rows / t_in, t_out, rows * 8.0 / t_out / 1e9, (checked == rows && bad == 0) ? "true" : "false");
+  return 0;
+}
+
 int main(int argc, char **argv) {
   const char *mode = argc > 1 ? argv[1] : "cpu";
-  int gpu = strcmp(mode, "gpu") == 0;
-  duckdb_mb_connection *c = open_conn(!gpu);
+  int gpu = strcmp(mode, "gpu") == 0, c4 = strcmp(mode, "c4") == 0;
+  duckdb_mb_connection *c = open_conn(!gpu && !c4);
   if (!c) return 1;
+  if (c4) {
+    c4_bench(c, argc > 2 ? atol(argv[2]) : 100000000);
+    duckdb_mb_disconnect(c);
+    return g_fail ? 1 : 0;
+  }
   host_constant_checks(c);
   if (gpu) gpu_checks(c, argc > 2 ? atol(argv[2]) : 1000000);
   duckdb_mb_disconnect(c);

@@ -4,10 +4,13 @@ reference's three read paths — Arrow int64 buffers in <= 1e6-row slices (the
 MoonBit decoders cap at 1e6, duckdb_arrow_native.mbt:474), query_stream
 chunks, and to_typed (32-bit saturation, duckdb_parsing.mbt:203-237).
 Generator: v_i = i * 2654435761 mod 2^63."""
+import json
+import os
+
 import numpy as np
 import pytest
 
-from conftest import one, q
+from conftest import ROOT, one, q
 
 pytestmark = pytest.mark.gpu
 
@@ -107,3 +110,35 @@ def test_row_appender_1e5(mbx):
     a = conn.query_arrow("SELECT v FROM r ORDER BY id").value
     assert np.array_equal(np.frombuffer(a.raw_int64_bytes(0)[4:], dtype=np.int64), v)
     conn.close()
+
+
+def test_row_appender_partial_row_and_nulls(mbx):
+    # values go straight into the batch columns: a row left half appended at
+    # close never reaches the table; NULLs after fast-path values keep their rows
+    conn = mbx.connect().value
+    q(conn, "CREATE TABLE p (a BIGINT, b INTEGER)")
+    ap = conn.create_appender("main", "p").value
+    for i in range(3):
+        ap.begin_row(); ap.append_bigint(10 * i); ap.append_int(i); ap.end_row()
+    ap.begin_row(); ap.append_null(); ap.append_int(7); ap.end_row()
+    ap.begin_row(); ap.append_bigint(99)             # partial row
+    assert isinstance(ap.flush(), mbx.Err)           # "Incomplete append to row"
+    ap.close()
+    res = q(conn, "SELECT a, b FROM p")
+    assert res.rows == [["0", "0"], ["10", "1"], ["20", "2"], ["", "7"]]
+    assert res.nulls[3] == [True, False]
+    conn.close()
+
+
+def test_c4_row_appender_native_harness(mbx, tmp_path):
+    # the reference's row-wise Appender driven from C (no Python per call)
+    import subprocess
+    exe = str(tmp_path / "mb_harness")
+    lib = os.path.join(ROOT, "duckdb.mbt_amd")
+    subprocess.run(["gcc", "-O2", "-std=c11", "-I", os.path.join(ROOT, "include"),
+                    os.path.join(ROOT, "tests", "c_harness", "mb_harness.c"), "-o", exe, "-L", lib,
+                    "-lduckdb_mb_amd", f"-Wl,-rpath,{lib}"], check=True)
+    p = subprocess.run([exe, "c4", "3000017"], capture_output=True, text=True, timeout=300)
+    assert p.returncode == 0, p.stdout + p.stderr
+    r = json.loads(p.stdout.strip().splitlines()[-1])
+    assert r["bit_exact"] and r["rows"] == 3000017
