@@ -47,7 +47,7 @@ def main():
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--rows", type=int, default=1_000_000_000)
-    ap.add_argument("--config", default="c2", choices=["c2", "c3", "c4", "c5"])
+    ap.add_argument("--config", default="c2", choices=["c1", "c2", "c3", "c4", "c5"])
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
@@ -87,6 +87,9 @@ def main():
 
     n = args.rows
     start = rank * n
+    if args.config == "c1":
+        conn.close()
+        return bench_c1()
     if args.config == "c4":
         return bench_c4(mbx, conn, min(n, 100_000_000), args)
     if args.config in ("c2", "c5"):
@@ -293,25 +296,46 @@ def bench_c4(mbx, conn, n, args):
     conn.close()
     # the same round trip through the reference's row-wise Appender API
     # (begin_row / append_bigint / end_row per row), driven natively from C
-    row_api = None
-    try:
-        import subprocess
-        import tempfile
-        lib = os.path.join(HERE, "duckdb.mbt_amd")
-        exe = os.path.join(tempfile.mkdtemp(), "mb_harness")
-        subprocess.run(["gcc", "-O2", "-std=c11", "-I", os.path.join(HERE, "include"),
-                        os.path.join(HERE, "tests", "c_harness", "mb_harness.c"), "-o", exe, "-L", lib,
-                        "-lduckdb_mb_amd", f"-Wl,-rpath,{lib}"], check=True, capture_output=True)
-        p = subprocess.run([exe, "c4", str(n)], capture_output=True, text=True, timeout=600)
-        row_api = json.loads(p.stdout.strip().splitlines()[-1]) if p.returncode == 0 else {"error": p.stderr[-400:]}
-    except Exception as ex:  # noqa: BLE001
-        row_api = {"error": str(ex)}
+    row_api = native_harness(["c4", str(n)])
     res = {"metric": "C4 appender ingest + arrow read-back", "value": n / (t_in + t_out), "unit": "rows/s",
            "n_gpus": 1, "ingest_gbs": n * 8 / t_in / 1e9, "readback_gbs": n * 8 / t_out / 1e9,
            "ingest_s": t_in, "readback_s": t_out, "rows": n, "bit_exact": ok,
            "bound": "host link (PCIe Gen5 x16, 63 GB/s spec) + host-side wire-buffer assembly",
            "ingest_api": "columnar duckdb_mbx_append_column (extension), from Python",
            "row_appender_native": row_api}
+    print(json.dumps(res), flush=True)
+
+
+def native_harness(argv):
+    """Runs tests/c_harness/mb_harness.c (gcc-built against include/duckdb_mb.h,
+    linked to the library) with `argv`; returns its JSON line or {"error": …}.
+    It drives the C-ABI the way MoonBit's native target does, so per-call FFI
+    costs are native rather than ctypes'."""
+    import subprocess
+    import tempfile
+    try:
+        lib = os.path.join(HERE, "duckdb.mbt_amd")
+        exe = os.path.join(tempfile.mkdtemp(), "mb_harness")
+        subprocess.run(["gcc", "-O2", "-std=c11", "-I", os.path.join(HERE, "include"),
+                        os.path.join(HERE, "tests", "c_harness", "mb_harness.c"), "-o", exe, "-L", lib,
+                        "-lduckdb_mb_amd", f"-Wl,-rpath,{lib}"], check=True, capture_output=True)
+        p = subprocess.run([exe] + argv, capture_output=True, text=True, timeout=600)
+        if p.returncode != 0:
+            return {"error": (p.stdout + p.stderr)[-400:]}
+        return json.loads(p.stdout.strip().splitlines()[-1])
+    except Exception as ex:  # noqa: BLE001
+        return {"error": str(ex)}
+
+
+def bench_c1():
+    """C1 (BASELINE.json configs[0]): SELECT i FROM range(1000000) WHERE i%2=0,
+    consumed natively as the MoonBit driver does (per-cell query loop, stream
+    chunk loop); exact 500 000 rows, sum 249 999 500 000."""
+    r = native_harness(["c1", "5"])
+    res = {"metric": "C1 SELECT i FROM range(1e6) WHERE i%2=0, rows/s consumed through the C-ABI",
+           "value": r.get("query_rows_per_s"), "unit": "rows/s", "n_gpus": 1, "higher_is_better": True,
+           "config": {"workload": "C1 (plumbing): per-cell Connection::query loop and query_stream chunks, native C"},
+           "native": r}
     print(json.dumps(res), flush=True)
 
 

@@ -9,6 +9,8 @@
  *   mb_harness cpu          host-constant queries only (mbx_allow_no_gpu)
  *   mb_harness gpu <rows>   C2 on the device: COUNT(*) WHERE x > 24, appender,
  *                           Arrow int64 getter; prints "count=<n>"
+ *   mb_harness c1 [reps]    C1 through the per-cell query loop and the stream
+ *                           chunk loop: one JSON line
  *   mb_harness c4 <rows>    C4 through the row-wise Appender + Arrow getter:
  *                           one JSON line (ingest rows/s, read-back GB/s)
  * Exit status 0 = every check passed.
@@ -260,11 +262,86 @@ static int c4_bench(duckdb_mb_connection *c, long rows) {
   return 0;
 }
 
+/* C1 (BASELINE configs[0]): SELECT i FROM range(1000000) WHERE i%2=0 the way
+ * the MoonBit driver consumes it — Connection::query's per-cell pull
+ * (duckdb_native.mbt:454-501: is_null + value per cell) and query_stream's
+ * chunk loop (:504-582) — checking 500 000 rows and their sum
+ * 249 999 500 000.  Prints one JSON line (best of `reps`). */
+static int c1_bench(duckdb_mb_connection *c, int reps) {
+  const char *q = "SELECT i FROM range(1000000) tbl(i) WHERE i%2=0";
+  double best_q = 1e30, best_s = 1e30;
+  long long sum_q = 0, sum_s = 0;
+  long rows_q = 0, rows_s = 0, chunks = 0;
+  for (int rep = 0; rep < reps; rep++) {
+    double t0 = now_s();
+    moonbit_bytes_t sql = S(q);
+    duckdb_mb_result *r = duckdb_mb_query(c, sql);
+    mb_free(sql);
+    CHECK(r != NULL, "c1 query: %s", take(duckdb_mb_last_error()));
+    if (!r) return 1;
+    rows_q = duckdb_mb_result_row_count(r);
+    sum_q = 0;
+    for (int32_t i = 0; i < rows_q; i++) {
+      if (duckdb_mb_result_is_null(r, 0, i)) continue;
+      moonbit_bytes_t v = duckdb_mb_result_value(r, 0, i);
+      char buf[32];
+      int32_t n = mb_len(v) < 31 ? mb_len(v) : 31;
+      memcpy(buf, v, (size_t)n);
+      buf[n] = 0;
+      sum_q += atoll(buf);
+      mb_free(v);
+    }
+    duckdb_mb_result_destroy(r);
+    double t1 = now_s();
+    if (t1 - t0 < best_q) best_q = t1 - t0;
+    sql = S(q);
+    duckdb_mb_stream *st = duckdb_mb_query_stream(c, sql);
+    mb_free(sql);
+    CHECK(st != NULL, "c1 stream: %s", take(duckdb_mb_last_error()));
+    if (!st) return 1;
+    rows_s = 0;
+    sum_s = 0;
+    chunks = 0;
+    for (;;) {
+      duckdb_mb_chunk *ch = duckdb_mb_stream_fetch_chunk(st);
+      if (!ch) break;
+      int32_t nr = duckdb_mb_chunk_row_count(ch);
+      for (int32_t i = 0; i < nr; i++) {
+        moonbit_bytes_t v = duckdb_mb_chunk_value(ch, 0, i);
+        char buf[32];
+        int32_t n = mb_len(v) < 31 ? mb_len(v) : 31;
+        memcpy(buf, v, (size_t)n);
+        buf[n] = 0;
+        sum_s += atoll(buf);
+        mb_free(v);
+      }
+      rows_s += nr;
+      chunks++;
+      duckdb_mb_chunk_destroy(ch);
+    }
+    CHECK(strlen(take(duckdb_mb_last_error())) == 0, "end of stream must leave an empty error");
+    duckdb_mb_stream_destroy(st);
+    double t2 = now_s();
+    if (t2 - t1 < best_s) best_s = t2 - t1;
+  }
+  const int ok = rows_q == 500000 && sum_q == 249999500000LL && rows_s == 500000 && sum_s == 249999500000LL;
+  CHECK(ok, "c1: query %ld rows sum %lld, stream %ld rows sum %lld", rows_q, sum_q, rows_s, sum_s);
+  printf("{\"rows\": %ld, \"query_percell_s\": %.6f, \"query_rows_per_s\": %.1f, \"stream_s\": %.6f, "
+         "\"stream_rows_per_s\": %.1f, \"stream_chunks\": %ld, \"sum\": %lld, \"exact\": %s}\n",
+         rows_q, best_q, rows_q / best_q, best_s, rows_s / best_s, chunks, sum_q, ok ? "true" : "false");
+  return 0;
+}
+
 int main(int argc, char **argv) {
   const char *mode = argc > 1 ? argv[1] : "cpu";
-  int gpu = strcmp(mode, "gpu") == 0, c4 = strcmp(mode, "c4") == 0;
-  duckdb_mb_connection *c = open_conn(!gpu && !c4);
+  int gpu = strcmp(mode, "gpu") == 0, c4 = strcmp(mode, "c4") == 0, c1 = strcmp(mode, "c1") == 0;
+  duckdb_mb_connection *c = open_conn(!gpu && !c4 && !c1);
   if (!c) return 1;
+  if (c1) {
+    c1_bench(c, argc > 2 ? atoi(argv[2]) : 5);
+    duckdb_mb_disconnect(c);
+    return g_fail ? 1 : 0;
+  }
   if (c4) {
     c4_bench(c, argc > 2 ? atol(argv[2]) : 100000000);
     duckdb_mb_disconnect(c);

@@ -36,3 +36,14 @@ def test_c_harness_gpu(mbx, oracle, tmp_path):
     assert p.returncode == 0, p.stdout + p.stderr
     c, _ = oracle.synth_filter_count(42, 0, n, 50, 1, 25, 2**63 - 1, 4)
     assert f"count={c}" in p.stdout
+
+
+@pytest.mark.gpu
+def test_c_harness_c1_native(mbx, tmp_path):
+    # C1 consumed natively: per-cell query loop and stream chunks, exact
+    import json
+    exe = _build(tmp_path)
+    p = subprocess.run([exe, "c1", "1"], capture_output=True, text=True, timeout=300)
+    assert p.returncode == 0, p.stdout + p.stderr
+    r = json.loads(p.stdout.strip().splitlines()[-1])
+    assert r["exact"] and r["rows"] == 500000 and r["sum"] == 249999500000 and r["stream_chunks"] >= 245
