@@ -28,7 +28,9 @@ def main():
             if sub in r["Kernel_Name"]:
                 vals[key][r["Counter_Name"]].append(float(r["Counter_Value"]))
     for key, counters in vals.items():
-        e = {"source": os.path.basename(path), "launches": max(len(v) for v in counters.values())}
+        # a FETCH_SIZE pass and a WRITE_SIZE pass (separate runs) merge into one entry
+        e = dict(data.get(key, {})) if len(sys.argv) > 2 else {}
+        e.update({"source": os.path.basename(path), "launches": max(len(v) for v in counters.values())})
         if "FETCH_SIZE" in counters:
             f = sum(counters["FETCH_SIZE"]) / len(counters["FETCH_SIZE"])
             e["fetch_size_kb_avg"] = f
