@@ -257,8 +257,9 @@ void HostCopy(const HostCopyDesc &d, hipStream_t s);
 // NULL-free 4- or 8-byte output columns.  A "step" is 256 consecutive rows.
 //  1. FilterBits: predicate columns through an LDS-DMA ring; per step four
 //     ballot words (bit L of word e <-> row 256 s + 4 L + e, the lane layout
-//     of both passes) and the step's selected-row count.
-//  2. ScanTileCounts -> each step's first output position (exclusive scan).
+//     of both passes).
+//  2. ScanStepBits -> each step's first output position (exclusive scan of
+//     the words' popcounts).
 //  3. CompactColumns: output columns through an LDS-DMA ring; each selected
 //     row goes to offset[step] + its rank inside the step.
 #define FC_MAX_OUT 8
@@ -268,8 +269,9 @@ struct CompactDesc {
   void *dst[FC_MAX_OUT];
   int32_t ow[FC_MAX_OUT];  // 4 or 8 bytes
 };
-void FilterBits(const FilterMultiDesc &d, int64_t nrows, unsigned long long *bits, uint32_t *step_counts,
-                hipStream_t s);
+void FilterBits(const FilterMultiDesc &d, int64_t nrows, unsigned long long *bits, hipStream_t s);
+// exclusive scan of the steps' selected-row counts (popcounts of their ballot words)
+void ScanStepBits(const unsigned long long *bits, int64_t *offsets, int64_t steps, int64_t *total, hipStream_t s);
 void CompactColumns(const CompactDesc &d, int64_t nrows, const unsigned long long *bits, const int64_t *step_offsets,
                     hipStream_t s);
 void RebaseOffsets(const int64_t *src, int64_t *dst, int64_t n, int64_t delta, hipStream_t s);

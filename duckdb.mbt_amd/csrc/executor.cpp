@@ -1017,15 +1017,14 @@ static bool TryFilterCompact(Engine &e, const DRel &rel, const BExpr &pred, cons
   }
   const int64_t steps = (n + 255) / 256;
   auto bits = Alloc(e, (size_t)steps * 32);
-  auto counts = Alloc(e, (size_t)steps * 4);
   auto offs = Alloc(e, (size_t)(steps + 2) * 8);  // compact reads offsets in 16-B aligned pairs
   double pbytes = 0;
   for (int j = 0; j < F.ncol; j++) pbytes += (double)n * (F.col[j].phys == P_I64 ? 8 : 4);
   {
-    ProfScope ps(e, "filter_bits", pbytes + (double)steps * 36, n);
-    dev::FilterBits(F, n, (unsigned long long *)bits->p, (uint32_t *)counts->p, e.stream);
+    ProfScope ps(e, "filter_bits", pbytes + (double)steps * 32, n);
+    dev::FilterBits(F, n, (unsigned long long *)bits->p, e.stream);
   }
-  dev::ScanTileCounts((const uint32_t *)counts->p, (int64_t *)offs->p, steps, e.d_scratch, e.stream);
+  dev::ScanStepBits((const unsigned long long *)bits->p, (int64_t *)offs->p, steps, e.d_scratch, e.stream);
   const int64_t nsel = ReadDev<int64_t>(e, e.d_scratch);
   out.n = nsel;
   std::vector<DCol> cols;

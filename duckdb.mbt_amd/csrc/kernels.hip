@@ -228,6 +228,34 @@ void ScanTileCounts(const uint32_t *counts, int64_t *offsets, int64_t n, int64_t
   hipLaunchKernelGGL(scan_total_kernel, dim3(1), dim3(1), 0, s, counts, offsets, n, total);
 }
 
+// selected rows of a 256-row step = popcount of its four ballot words
+struct StepPopc {
+  const unsigned long long *b;
+  __host__ __device__ int64_t operator()(int64_t i) const {
+    return (int64_t)(__popcll(b[4 * i]) + __popcll(b[4 * i + 1]) + __popcll(b[4 * i + 2]) + __popcll(b[4 * i + 3]));
+  }
+};
+
+__global__ void scan_bits_total_kernel(const unsigned long long *bits, const int64_t *offsets, int64_t n,
+                                       int64_t *total) {
+  *total = n ? offsets[n - 1] + StepPopc{bits}(n - 1) : 0;
+}
+
+void ScanStepBits(const unsigned long long *bits, int64_t *offsets, int64_t steps, int64_t *total, hipStream_t s) {
+  if (steps <= 0) {
+    (void)hipMemsetAsync(total, 0, sizeof(int64_t), s);
+    return;
+  }
+  hipcub::CountingInputIterator<int64_t> idx(0);
+  hipcub::TransformInputIterator<int64_t, StepPopc, hipcub::CountingInputIterator<int64_t>> it(idx, StepPopc{bits});
+  size_t tmp = 0;
+  (void)hipcub::DeviceScan::ExclusiveSum(nullptr, tmp, it, offsets, (int)steps, s);
+  void *d_tmp = TempAlloc(tmp);
+  (void)hipcub::DeviceScan::ExclusiveSum(d_tmp, tmp, it, offsets, (int)steps, s);
+  TempFree(d_tmp, tmp);
+  hipLaunchKernelGGL(scan_bits_total_kernel, dim3(1), dim3(1), 0, s, bits, offsets, steps, total);
+}
+
 // ---------------------------------------------------------------------------
 // fused scan -> filter -> aggregate (configs C2 and C5)
 // ---------------------------------------------------------------------------
@@ -2391,8 +2419,7 @@ void RebaseOffsets(const int64_t *src, int64_t *dst, int64_t n, int64_t delta, h
 
 // pass 1: NLD KiB of predicate slices per wave step, DEPTH steps in flight
 template <int NLD, int DEPTH>
-__global__ __launch_bounds__(256) void filter_bits_lds_kernel(FilterMultiDesc D, int64_t n, unsigned long long *bits,
-                                                              uint32_t *counts) {
+__global__ __launch_bounds__(256) void filter_bits_lds_kernel(FilterMultiDesc D, int64_t n, unsigned long long *bits) {
   extern __shared__ __attribute__((aligned(16))) unsigned char fb_lds[];
   constexpr int SB = NLD * 1024;
   const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
@@ -2421,14 +2448,13 @@ __global__ __launch_bounds__(256) void filter_bits_lds_kernel(FilterMultiDesc D,
         __builtin_amdgcn_global_load_lds((const void *)(src + 1024 + lane * 16), (void *)(dst + off[c] + 1024), 16, 0, 2);
     }
   };
-  // one step's 4 ballot words + count: lanes 0..3 store a word each, lane 4 the count
+  // one step's 4 ballot words: lanes 0..3 store a word each (32 contiguous bytes)
   auto emit = [&](int64_t step, const bool ok[4]) {
     unsigned long long b[4];
 #pragma unroll
     for (int e = 0; e < 4; e++) b[e] = __ballot(ok[e]);
     const unsigned long long mine = lane == 0 ? b[0] : lane == 1 ? b[1] : lane == 2 ? b[2] : b[3];
     if (lane < 4) __builtin_nontemporal_store(mine, bits + step * 4 + lane);
-    if (lane == 4) counts[step] = (uint32_t)(__popcll(b[0]) + __popcll(b[1]) + __popcll(b[2]) + __popcll(b[3]));
   };
   if (nsteps > 0) {
 #pragma unroll
@@ -2485,8 +2511,7 @@ __global__ __launch_bounds__(256) void filter_bits_lds_kernel(FilterMultiDesc D,
   }
 }
 
-void FilterBits(const FilterMultiDesc &d, int64_t nrows, unsigned long long *bits, uint32_t *step_counts,
-                hipStream_t s) {
+void FilterBits(const FilterMultiDesc &d, int64_t nrows, unsigned long long *bits, hipStream_t s) {
   if (nrows <= 0) return;
   int nld = 0;
   for (int c = 0; c < d.ncol; c++) nld += d.col[c].phys == P_I64 ? 2 : 1;
@@ -2499,7 +2524,7 @@ void FilterBits(const FilterMultiDesc &d, int64_t nrows, unsigned long long *bit
   if (const char *e = getenv("MBX_FB_DEPTH")) dp = atoi(e);
 #define FB(L, DP)                                                                                          \
   hipLaunchKernelGGL((filter_bits_lds_kernel<L, DP>), dim3(grid), dim3(256), (size_t)4 * DP * L * 1024, s, d, \
-                     nrows, bits, step_counts)
+                     nrows, bits)
 #define FBD(L, DEF) \
   if ((dp ? dp : DEF) <= 2) FB(L, 2); else if ((dp ? dp : DEF) <= 3) FB(L, 3); else if ((dp ? dp : DEF) <= 4) FB(L, 4); else FB(L, 6);
   switch (nld) {
