@@ -133,30 +133,44 @@ def main():
     gcount = gsum = ggroups = None
 
     def combine(out):
-        # the one exchange of the path: global aggregate over all shards
-        nonlocal gcount, gsum, ggroups
+        # the one exchange of the path: the global aggregate over all shards.
+        # C2/C5 start it asynchronously (RCCL's stream) so that it overlaps the
+        # next step's query on the engine stream; every step's global answer is
+        # collected inside the timed region (finish_combines).
         if world == 1:
-            return
+            return None
         if args.config == "c2":
-            gcount = mbx_dist.allreduce_count(int(out[0]), device=coll_dev)  # RCCL over xGMI: global COUNT(*)
-        elif args.config == "c5":
-            gcount, gsum = mbx_dist.global_count_sum(int(out[0]), int(out[1]) if out[1] else None, device=coll_dev)
-        elif args.config == "c3":
-            ggroups = mbx_dist.global_group_count_sum(out, device=coll_dev)  # 32 x (key, count, int128 sum)
+            return mbx_dist.allreduce_count_async(int(out[0]), device=coll_dev)  # RCCL over xGMI: COUNT(*)
+        if args.config == "c5":
+            return mbx_dist.global_count_sum_async(int(out[0]), int(out[1]) if out[1] else None, device=coll_dev)
+        return mbx_dist.global_group_count_sum(out, device=coll_dev)  # C3: 32 x (key, count, int128 sum)
+
+    def finish_combines(pending):
+        nonlocal gcount, gsum, ggroups
+        for p in pending:
+            if p is None:
+                continue
+            r = p.result() if hasattr(p, "result") else p
+            if args.config == "c2":
+                gcount = r
+            elif args.config == "c5":
+                gcount, gsum = r
+            else:
+                ggroups = r
 
     # warmup includes the collective, so communicator setup is never timed
-    for _ in range(args.warmup):
-        out = step()
-        combine(out)
+    finish_combines([combine(step()) for _ in range(args.warmup)])
 
     conn.profile_drain()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     t_start = time.perf_counter()
+    pending = []
     for _ in range(args.steps):
         out = step()
-        combine(out)
+        pending.append(combine(out))
+    finish_combines(pending)
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()

@@ -113,3 +113,42 @@ def global_group_count_sum(groups: Sequence[Tuple[Optional[int], int, Optional[i
             acc[key] = (cc + c, ss)
     keys = sorted(k for k in acc if k is not None) + ([None] if None in acc else [])
     return [(k, acc[k][0], acc[k][1]) for k in keys]
+
+
+# ---- asynchronous combines: the collective of step i runs on RCCL's stream
+# while the engine stream executes step i+1's query; .result() waits.
+class PendingCombine:
+    def __init__(self, work, finish):
+        self._work, self._finish = work, finish
+
+    def result(self):
+        if self._work is not None:
+            self._work.wait()
+        return self._finish()
+
+
+def allreduce_count_async(local_count: int, device="cpu", group=None) -> PendingCombine:
+    """Global COUNT(*) as an asynchronous int64 all-reduce (sum)."""
+    t = torch.full((1,), int(local_count), dtype=torch.int64, device=device)
+    w = dist.all_reduce(t, group=group, async_op=True)
+    return PendingCombine(w, lambda: int(t.item()))
+
+
+def global_count_sum_async(local_count: int, local_sum, device="cpu", group=None) -> PendingCombine:
+    """Global COUNT(*) / exact int128 SUM as an asynchronous all-gather."""
+    world = dist.get_world_size(group)
+    flat = []
+    for v in (local_count, 0 if local_sum is None else local_sum):
+        flat.extend(encode_i128(int(v)))
+    t = torch.tensor(flat, dtype=torch.int64, device=device)
+    outs = [torch.empty_like(t) for _ in range(world)]
+    w = dist.all_gather(outs, t, group=group, async_op=True)
+
+    def finish():
+        parts = []
+        for o in outs:
+            o = o.cpu().tolist()
+            parts.append([decode_i128(o[0], o[1]), decode_i128(o[2], o[3])])
+        return combine_count_sum(parts)
+
+    return PendingCombine(w, finish)

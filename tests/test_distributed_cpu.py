@@ -35,10 +35,13 @@ def _worker(rank, world, port, n, q):
     c, s = o.synth_filter_count(42, start, n, 50, 1, 25, 2**63 - 1, 2)
     gc, gs = d.global_count_sum(c, s)
     tc = d.allreduce_count(c)
+    # the async forms the bench overlaps with the next step's query: several in flight
+    pend = [(d.allreduce_count_async(c + k), d.global_count_sum_async(c, s + k)) for k in range(3)]
+    asy = [(a.result(), b.result()) for a, b in pend]
     # huge partials: carries across the 64-bit boundary must survive
     big = d.allgather_i128([(2**100 + rank) * (1 if rank else -1), -(2**63) - rank])
     dist.destroy_process_group()
-    q.put((rank, gc, gs, tc, big))
+    q.put((rank, gc, gs, tc, big, asy))
 
 
 @pytest.mark.parametrize("world", [2, 4])
@@ -57,8 +60,9 @@ def test_global_count_sum_gloo(world):
     sys.path.insert(0, ROOT)
     from oracle import Oracle
     c, s = Oracle().synth_filter_count(42, 0, n * world, 50, 1, 25, 2**63 - 1, 4)
-    for rank, gc, gs, tc, big in out:
+    for rank, gc, gs, tc, big, asy in out:
         assert (gc, gs, tc) == (c, s, c)
+        assert asy == [(c + world * k, (c, s + world * k)) for k in range(3)]
         assert big == [[(2**100 + r) * (1 if r else -1), -(2**63) - r] for r in range(world)]
 
 
