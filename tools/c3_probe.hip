@@ -201,6 +201,93 @@ __global__ __launch_bounds__(256) void two_stream_pipe(const int *__restrict__ k
   if (acc == 0x5a5a5a5a5a5aLL) atomicAdd(out, 1ull);
 }
 
+// loader/consumer split: 4 loader waves stream (the fast 4-wave shape) into
+// per-loader rings; NC consumer waves (NC/4 per loader, alternating steps) do
+// the table atomics.  LDS flags: full[w][d] = step+1 once landed, done[w][d] =
+// step+1 once consumed.  Every spin is bounded (a broken handshake ends, wrong,
+// instead of hanging).
+template <int DEPTH, int NC>
+__global__ __launch_bounds__(256 + 64 * NC) void two_stream_lc(const int *__restrict__ keys,
+                                                               const long long *__restrict__ vals, long long nsteps,
+                                                               unsigned long long *out) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
+  constexpr int SB = 3072, R = 64, NK = 32, CPL = NC / 4;
+  unsigned int *cnt = (unsigned int *)lds;
+  unsigned long long *sum = (unsigned long long *)(lds + 8192);
+  volatile int *full = (volatile int *)(lds + 24576);        // [4][DEPTH]
+  volatile int *done = (volatile int *)(lds + 24576 + 256);  // [4][DEPTH]
+  unsigned char *rings = lds + 24576 + 512;
+  const int t = threadIdx.x, wave = t >> 6, lane = t & 63;
+  for (int i = t; i < NK * R; i += blockDim.x) { cnt[i] = 0; sum[i] = 0; }
+  if (t < 4 * DEPTH) { full[t] = 0; done[t] = 0; }
+  __syncthreads();
+  const long long nw = (long long)gridDim.x * 4;
+  int bad = 0;
+  if (wave < 4) {  // loader
+    const int w = wave;
+    unsigned char *ring = rings + w * DEPTH * SB;
+    auto issue = [&](long long q, int d) {
+      unsigned char *dst = ring + d * SB;
+      const unsigned char *kp = (const unsigned char *)keys + q * 1024;
+      const unsigned char *vp = (const unsigned char *)vals + q * 2048;
+      __builtin_amdgcn_global_load_lds((const void *)(kp + lane * 16), (void *)dst, 16, 0, 2);
+      __builtin_amdgcn_global_load_lds((const void *)(vp + lane * 16), (void *)(dst + 1024), 16, 0, 2);
+      __builtin_amdgcn_global_load_lds((const void *)(vp + 1024 + lane * 16), (void *)(dst + 2048), 16, 0, 2);
+    };
+    long long nmine = 0;
+    for (long long st = (long long)blockIdx.x * 4 + w; st < nsteps; st += nw) nmine++;
+    for (long long j = 0; j < nmine + DEPTH - 1; j++) {
+      if (j < nmine) {
+        const int d = (int)(j % DEPTH);
+        if (j >= DEPTH) {  // the slot's previous step must be consumed
+          int sp = 0;
+          while (done[w * DEPTH + d] < (int)(j - DEPTH + 1)) {
+            __builtin_amdgcn_s_sleep(1);
+            if (++sp > (1 << 22)) { bad = 1; break; }
+          }
+        }
+        issue((long long)blockIdx.x * 4 + w + j * nw, d);
+      }
+      // publish the oldest in-flight step once it has landed
+      const long long pj = j - (DEPTH - 1);
+      if (pj >= 0) {
+        if (j < nmine) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(3 * (DEPTH - 1)) : "memory");
+        else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        if (lane == 0) full[w * DEPTH + (int)(pj % DEPTH)] = (int)(pj + 1);
+      }
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  } else {  // consumer
+    const int c = wave - 4, w = c % 4, phase = c / 4;
+    const unsigned char *ring = rings + w * DEPTH * SB;
+    long long nmine = 0;
+    for (long long st = (long long)blockIdx.x * 4 + w; st < nsteps; st += nw) nmine++;
+    for (long long j = phase; j < nmine; j += CPL) {
+      const int d = (int)(j % DEPTH);
+      int sp = 0;
+      while (full[w * DEPTH + d] < (int)(j + 1)) {
+        __builtin_amdgcn_s_sleep(1);
+        if (++sp > (1 << 22)) { bad = 1; break; }
+      }
+      const unsigned char *src = ring + d * SB;
+      v4i32 kv = *(const v4i32 *)(src + lane * 16);
+      v2i64 a0 = *(const v2i64 *)(src + 1024 + lane * 32), a1 = *(const v2i64 *)(src + 1024 + lane * 32 + 16);
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      if (lane == 0) done[w * DEPTH + d] = (int)(j + 1);
+      int kk[4] = {kv.x & 31, kv.y & 31, kv.z & 31, kv.w & 31};
+      long long a[4] = {a0.x, a0.y, a1.x, a1.y};
+#pragma unroll
+      for (int e = 0; e < 4; e++) {
+        int sl = kk[e] * R + lane;
+        atomicAdd(&sum[sl], ((unsigned long long)a[e] << 12) + 1ull);
+      }
+    }
+  }
+  __syncthreads();
+  long long acc = cnt[t % 2048] + sum[t % 2048] + bad;
+  if (acc == 0x5a5a5a5a5a5aLL || bad) atomicAdd(out, 1ull);
+}
+
 __global__ void fill_keys(int *k, long long n) {
   for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long long)gridDim.x * blockDim.x) {
     unsigned long long z = (unsigned long long)i + 0x9e3779b97f4a7c15ull;
@@ -272,6 +359,22 @@ int main(int argc, char **argv) {
     CK(hipFuncSetAttribute((const void *)two_stream_pipe<D, P>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds)); \
     float ms = TimeIt([&] { hipLaunchKernelGGL((two_stream_pipe<D, P>), dim3(cus * (G)), dim3(256), lds, 0, k, v, nsteps, out); }, 15); \
     report(P ? "pipe/packed" : "pipe/atom2", D, G, ms);                                                      \
+  }
+#define RUNLC(D, NC)                                                                                          \
+  {                                                                                                           \
+    size_t lds = 24576 + 512 + 4 * (D) * 3072;                                                                \
+    CK(hipFuncSetAttribute((const void *)two_stream_lc<D, NC>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds)); \
+    CK(hipMemset(out, 0, 8));                                                                                 \
+    float ms = TimeIt([&] { hipLaunchKernelGGL((two_stream_lc<D, NC>), dim3(cus), dim3(256 + 64 * (NC)), lds, 0, k, v, nsteps, out); }, 15); \
+    unsigned long long flag = 0;                                                                              \
+    CK(hipMemcpy(&flag, out, 8, hipMemcpyDeviceToHost));                                                      \
+    printf("lc NC=%d ", NC);                                                                                  \
+    report(flag ? "lc/BAD" : "lc/packed", D, 1, ms);                                                          \
+  }
+  if (argc > 2 && argv[2][0] == 'l') {
+    RUNLC(4, 4) RUNLC(6, 4) RUNLC(4, 8) RUNLC(6, 8) RUNLC(8, 8) RUNLC(6, 12)
+    RUN2(2, 0, 1) RUN2(2, 2, 3)
+    return 0;
   }
   RUNP(3, false, 1) RUNP(4, false, 1) RUNP(6, false, 1) RUNP(3, true, 1) RUNP(4, true, 1) RUNP(6, true, 1)
   RUNP(3, false, 2) RUNP(3, true, 2) RUNP(2, false, 3) RUNP(2, true, 3)
