@@ -643,3 +643,37 @@ def test_jit_groupby_int64_wrap_is_exact(mbx, monkeypatch):
         assert isinstance(r, mbx.Err) and "Overflow in multiplication" in r.error.message
     finally:
         c.close()
+
+
+# ---- beyond 2^31 rows: 64-bit row indexing through every hot-path kernel ------
+BIG_N = 2**31 + 4097
+
+
+def test_c2_c5_beyond_int32_rows(mbx, oracle):
+    import os as _os
+    th = min(16, len(_os.sched_getaffinity(0)))
+    c = mbx.connect().value
+    q(c, f"CREATE TABLE big AS SELECT mbx_synth(42, i, 50) + 1 AS x FROM range({BIG_N}) tbl(i)")
+    cnt, s = oracle.synth_filter_count(42, 0, BIG_N, 50, 1, 25, 2**63 - 1, th)
+    assert one(c, "SELECT COUNT(*) FROM big WHERE x > 24") == [str(cnt)]
+    assert one(c, "SELECT COUNT(*), SUM(x) FROM big WHERE x > 24") == [str(cnt), str(s)]
+    assert one(c, "SELECT COUNT(*) FROM big") == [str(BIG_N)]
+    # compaction with output positions past 2^31, checked by aggregates and the tail rows
+    q(c, "CREATE TABLE bigsel AS SELECT x FROM big WHERE x > 24")
+    assert one(c, "SELECT COUNT(*), SUM(x), MIN(x), MAX(x) FROM bigsel") == [str(cnt), str(s), "25", "50"]
+    tail = oracle.synth_i64(4097, 42, BIG_N - 4097, 50, 1)
+    exp_tail = tail[tail > 24][-5:].tolist()
+    got = q(c, f"SELECT x FROM bigsel LIMIT 5 OFFSET {cnt - 5}").rows
+    assert [int(r[0]) for r in got] == exp_tail
+    c.close()
+
+
+def test_c3_beyond_int32_rows(mbx, oracle):
+    import os as _os
+    th = min(16, len(_os.sched_getaffinity(0)))
+    c = mbx.connect().value
+    q(c, SYNTH_C3.replace("TABLE g", "TABLE gbig").format(n=BIG_N))
+    oc, osum = oracle.synth_groupby(7, 9, 0, BIG_N, 32, 1 << 40, -(1 << 39), th)
+    got = q(c, "SELECT k, SUM(v), COUNT(*) FROM gbig GROUP BY k ORDER BY k").rows
+    assert [(int(r[0]), int(r[1]), int(r[2])) for r in got] == [(k, osum[k], oc[k]) for k in range(32)]
+    c.close()
