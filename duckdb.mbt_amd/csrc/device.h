@@ -254,7 +254,7 @@ void HostCopy(const HostCopyDesc &d, hipStream_t s);
 
 // Filter -> compaction in two streaming passes (order preserving), for a
 // conjunction of range predicates over NULL-free int32/int64 columns and
-// NULL-free 4- or 8-byte output columns.  A "step" is 256 consecutive rows.
+// NULL-free 1/2/4/8/16-byte output columns.  A "step" is 256 consecutive rows.
 //  1. FilterBits: predicate columns through an LDS-DMA ring; per step four
 //     ballot words (bit L of word e <-> row 256 s + 4 L + e, the lane layout
 //     of both passes).
@@ -267,7 +267,7 @@ struct CompactDesc {
   int32_t nout;
   const void *src[FC_MAX_OUT];
   void *dst[FC_MAX_OUT];
-  int32_t ow[FC_MAX_OUT];  // 4 or 8 bytes
+  int32_t ow[FC_MAX_OUT];  // 1, 2, 4, 8 or 16 bytes (4/8 only: the register kernel; else the generic one)
 };
 void FilterBits(const FilterMultiDesc &d, int64_t nrows, unsigned long long *bits, hipStream_t s);
 // exclusive scan of the steps' selected-row counts (popcounts of their ballot words)

@@ -1007,7 +1007,7 @@ static bool TryFilterCompact(Engine &e, const DRel &rel, const BExpr &pred, cons
     const DCol &c = rel.cols[x->col];
     if (c.validity || !c.data || c.phys == P_STR) return false;
     const int w = PhysSize(c.phys);
-    if ((w != 4 && w != 8) || (uintptr_t)c.data % 16) return false;
+    if ((w != 1 && w != 2 && w != 4 && w != 8 && w != 16) || (uintptr_t)c.data % 16) return false;
   }
   out = DRel();
   const int64_t n = rel.n;
@@ -1030,7 +1030,7 @@ static bool TryFilterCompact(Engine &e, const DRel &rel, const BExpr &pred, cons
   std::vector<DCol> cols;
   for (auto &x : exprs) cols.push_back(AllocOut(e, x->type, nsel, false));
   if (nsel > 0) {
-    // output columns in groups of at most 8 KiB per 256-row step
+    // output columns in groups of at most 8 LDS-DMA instructions (8 KiB) per 256-row step
     size_t k = 0;
     while (k < exprs.size()) {
       dev::CompactDesc C;
@@ -1040,8 +1040,9 @@ static bool TryFilterCompact(Engine &e, const DRel &rel, const BExpr &pred, cons
       for (; k < exprs.size() && C.nout < FC_MAX_OUT; k++) {
         const DCol &c = rel.cols[exprs[k]->col];
         const int w = PhysSize(c.phys);
-        if (kib + w / 4 > 8) break;
-        kib += w / 4;
+        const int cost = (256 * w + 1023) / 1024;
+        if (kib + cost > 8) break;
+        kib += cost;
         C.src[C.nout] = c.data;
         C.dst[C.nout] = cols[k].data;
         C.ow[C.nout] = w;

@@ -2659,9 +2659,166 @@ __global__ __launch_bounds__(256) void compact_lds_kernel(CompactDesc D, int64_t
   }
 }
 
+// copies row `row` of a w-byte column to position `pos` of another
+__device__ __forceinline__ void fc_copy_row(const void *src, void *dst, int w, int64_t row, int64_t pos) {
+  switch (w) {
+    case 1: ((uint8_t *)dst)[pos] = ((const uint8_t *)src)[row]; break;
+    case 2: ((uint16_t *)dst)[pos] = ((const uint16_t *)src)[row]; break;
+    case 4: ((uint32_t *)dst)[pos] = ((const uint32_t *)src)[row]; break;
+    case 8: ((uint64_t *)dst)[pos] = ((const uint64_t *)src)[row]; break;
+    default: ((v4i32 *)dst)[pos] = ((const v4i32 *)src)[row]; break;
+  }
+}
+
+// pass 2 for any mix of 1/2/4/8/16-byte outputs: every column's slice of a
+// step (256 x w bytes, 1-4 LDS-DMA instructions; 1- and 2-byte slices use 16
+// and 32 lanes) lands in the ring; each column's selected rows are copied
+// slot -> per-wave staging area (LDS to LDS, at their rank) and stored out with
+// consecutive lanes on consecutive rows; the slot is refilled after the last
+// column.  NI = LDS-DMA instructions per step (compile time: the counted wait).
+template <int NI, int DEPTH>
+__global__ __launch_bounds__(256) void compact_any_lds_kernel(CompactDesc D, int64_t n, const unsigned long long *bits,
+                                                              const int64_t *offs, int slot_bytes) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char ca_lds[];
+  const int SB = slot_bytes;  // Σ 256 w + 64 (metadata), a multiple of 16
+  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  unsigned char *ring = ca_lds + (size_t)w * DEPTH * SB;
+  unsigned char *stage = ca_lds + (size_t)4 * DEPTH * SB + (size_t)w * 4096;  // 256 rows x 16 B per wave
+  int off[FC_MAX_OUT];
+  int meta_off = 0;
+  {
+    int o = 0;
+#pragma unroll
+    for (int c = 0; c < FC_MAX_OUT; c++) {
+      off[c] = o;
+      if (c < D.nout) o += D.ow[c] * 256;
+    }
+    meta_off = o;
+  }
+  const uint64_t lt = (1ull << lane) - 1;
+  const int64_t nsteps = n >> 8;
+  const int64_t nw = (int64_t)gridDim.x * 4;
+  int64_t st = (int64_t)blockIdx.x * 4 + w;
+  auto issue = [&](int64_t q, int d) {
+    unsigned char *dst = ring + d * SB;
+#pragma unroll
+    for (int c = 0; c < FC_MAX_OUT; c++) {
+      if (c >= D.nout) break;
+      const int B = D.ow[c] * 256;
+      const unsigned char *src = (const unsigned char *)D.src[c] + q * B;
+      for (int j = 0; j < B; j += 1024)
+        if (j + lane * 16 < B)
+          __builtin_amdgcn_global_load_lds((const void *)(src + j + lane * 16), (void *)(dst + off[c] + j), 16, 0, 2);
+    }
+    const unsigned char *msrc = lane < 2 ? (const unsigned char *)(bits + q * 4) + lane * 16
+                                         : (const unsigned char *)(offs + (q & ~(int64_t)1));
+    if (lane < 3) __builtin_amdgcn_global_load_lds((const void *)msrc, (void *)(dst + meta_off), 16, 0, 0);
+  };
+  if (nsteps > 0) {
+#pragma unroll
+    for (int d = 0; d < DEPTH; d++) {
+      int64_t q = st + d * nw;
+      issue(q < nsteps ? q : 0, d);
+    }
+  }
+  int k = 0;
+  for (; st < nsteps; st += nw) {
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NI * (DEPTH - 1)) : "memory");
+    const unsigned char *src = ring + k * SB;
+    const unsigned long long *meta = (const unsigned long long *)(src + meta_off);
+    const unsigned long long b0 = meta[0], b1 = meta[1], b2 = meta[2], b3 = meta[3];
+    const int64_t o0 = (int64_t)meta[4 + (st & 1)];
+    const unsigned m = (unsigned)((b0 >> lane) & 1) | (unsigned)((b1 >> lane) & 1) << 1 |
+                       (unsigned)((b2 >> lane) & 1) << 2 | (unsigned)((b3 >> lane) & 1) << 3;
+    const int r0 = __popcll(b0 & lt) + __popcll(b1 & lt) + __popcll(b2 & lt) + __popcll(b3 & lt);
+    const int cnt = __popcll(b0) + __popcll(b1) + __popcll(b2) + __popcll(b3);
+#pragma unroll 1
+    for (int c = 0; c < D.nout; c++) {
+      const int ow = D.ow[c];
+      const unsigned char *cs = src + off[c];
+      int r = r0;
+#pragma unroll
+      for (int e = 0; e < 4; e++) {
+        if (!((m >> e) & 1u)) continue;
+        const int row = 4 * lane + e;
+        switch (ow) {
+          case 1: stage[r] = cs[row]; break;
+          case 2: ((uint16_t *)stage)[r] = ((const uint16_t *)cs)[row]; break;
+          case 4: ((uint32_t *)stage)[r] = ((const uint32_t *)cs)[row]; break;
+          case 8: ((uint64_t *)stage)[r] = ((const uint64_t *)cs)[row]; break;
+          default: ((v4i32 *)stage)[r] = ((const v4i32 *)cs)[row]; break;
+        }
+        r++;
+      }
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      unsigned char *dst = (unsigned char *)D.dst[c];
+      switch (ow) {
+        case 1: for (int i = lane; i < cnt; i += 64) dst[o0 + i] = stage[i]; break;
+        case 2: for (int i = lane; i < cnt; i += 64) ((uint16_t *)dst)[o0 + i] = ((const uint16_t *)stage)[i]; break;
+        case 4: for (int i = lane; i < cnt; i += 64) ((uint32_t *)dst)[o0 + i] = ((const uint32_t *)stage)[i]; break;
+        case 8: for (int i = lane; i < cnt; i += 64) ((uint64_t *)dst)[o0 + i] = ((const uint64_t *)stage)[i]; break;
+        default: for (int i = lane; i < cnt; i += 64) ((v4i32 *)dst)[o0 + i] = ((const v4i32 *)stage)[i]; break;
+      }
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // staging reads done before the next column
+    }
+    int64_t q = st + DEPTH * nw;
+    issue(q < nsteps ? q : st, k);
+    k = k + 1 == DEPTH ? 0 : k + 1;
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  if (blockIdx.x == 0 && w == 0 && (n & 255)) {  // the partial last step
+    const unsigned long long b0 = bits[nsteps * 4], b1 = bits[nsteps * 4 + 1], b2 = bits[nsteps * 4 + 2],
+                             b3 = bits[nsteps * 4 + 3];
+    const unsigned m = (unsigned)((b0 >> lane) & 1) | (unsigned)((b1 >> lane) & 1) << 1 |
+                       (unsigned)((b2 >> lane) & 1) << 2 | (unsigned)((b3 >> lane) & 1) << 3;
+    int64_t pos = offs[nsteps] + __popcll(b0 & lt) + __popcll(b1 & lt) + __popcll(b2 & lt) + __popcll(b3 & lt);
+    for (int e = 0; e < 4; e++) {
+      const int64_t i = (nsteps << 8) + 4 * lane + e;
+      if (!((m >> e) & 1u)) continue;
+      for (int c = 0; c < D.nout; c++) fc_copy_row(D.src[c], D.dst[c], D.ow[c], i, pos);
+      pos++;
+    }
+  }
+}
+
+static void CompactAny(const CompactDesc &d, int64_t nrows, const unsigned long long *bits, const int64_t *step_offsets,
+                       int grid, hipStream_t s) {
+  int ni = 1, sb = 64;
+  for (int c = 0; c < d.nout; c++) {
+    ni += (d.ow[c] * 256 + 1023) / 1024;
+    sb += d.ow[c] * 256;
+  }
+  const size_t lds = (size_t)4 * 2 * sb + 4 * 4096;
+#define CA(N)                                                                                               \
+  hipLaunchKernelGGL((compact_any_lds_kernel<N, 2>), dim3(grid), dim3(256), lds, s, d, nrows, bits, step_offsets, sb)
+  switch (ni) {
+    case 2: CA(2); break;
+    case 3: CA(3); break;
+    case 4: CA(4); break;
+    case 5: CA(5); break;
+    case 6: CA(6); break;
+    case 7: CA(7); break;
+    case 8: CA(8); break;
+    default: CA(9); break;
+  }
+#undef CA
+  CHECK_LAUNCH();
+}
+
 void CompactColumns(const CompactDesc &d, int64_t nrows, const unsigned long long *bits, const int64_t *step_offsets,
                     hipStream_t s) {
   if (nrows <= 0 || d.nout <= 0) return;
+  bool any = false;
+  for (int c = 0; c < d.nout; c++) any |= d.ow[c] != 4 && d.ow[c] != 8;
+  if (any) {
+    int gpc = 3;
+    if (const char *e = getenv("MBX_CP_BLOCKS_PER_CU")) gpc = atoi(e) > 0 ? atoi(e) : 3;
+    int grid = NumCUs() * gpc;
+    const int64_t need = (nrows >> 8) / 4 + 1;
+    if (grid > need) grid = (int)need;
+    CompactAny(d, nrows, bits, step_offsets, grid, s);
+    return;
+  }
   int nld = 0;
   for (int c = 0; c < d.nout; c++) nld += d.ow[c] / 4;
   if (nld > 8) throw std::runtime_error("CompactColumns: more than 8 KiB of outputs per step");

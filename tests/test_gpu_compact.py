@@ -90,6 +90,33 @@ def test_filter_compact_runs_the_hip_passes(mbx, oracle):
     c.close()
 
 
+def test_filter_compact_any_width_outputs(mbx, oracle):
+    # 1-, 2- and 16-byte outputs (BOOLEAN, SMALLINT, HUGEINT) take the generic
+    # compaction kernel; values and order exact
+    cfg = mbx.Config.create()
+    cfg.set("mbx_profile", "true")
+    c = mbx.connect_with_config(cfg).value
+    for n in (1, 300, 70_001):
+        q(c, "DROP TABLE IF EXISTS fw")
+        q(c, f"CREATE TABLE fw AS SELECT mbx_synth(42, i, 50) + 1 AS x, (mbx_synth(13, i, 2) = 1) AS b, "
+             f"CAST(mbx_synth(11, i, 1000) - 500 AS SMALLINT) AS s, "
+             f"CAST(mbx_synth(9, i, 1099511627776) - 549755813888 AS HUGEINT) * 1000000000000 AS h, "
+             f"CAST(mbx_synth(7, i, 32) AS TINYINT) AS t FROM range({n}) tbl(i)")
+        x = oracle.synth_i64(n, 42, 0, 50, 1)
+        b = oracle.synth_i64(n, 13, 0, 2, 0) == 1
+        s_ = oracle.synth_i64(n, 11, 0, 1000, -500)
+        v = oracle.synth_i64(n, 9, 0, 2**40, -2**39)
+        t = oracle.synth_i64(n, 7, 0, 32, 0)
+        m = x > 24
+        got = q(c, "SELECT b, s, h, t, x FROM fw WHERE x > 24").rows
+        if m.any():
+            assert "compact" in [k["name"] for k in c.last_profile()["kernels"]]
+        exp = [["true" if b[i] else "false", str(s_[i]), str(int(v[i]) * 10**12), str(t[i]), str(x[i])]
+               for i in np.flatnonzero(m)]
+        assert got == exp, n
+    c.close()
+
+
 def test_filter_compact_profile_and_stream(conn, oracle):
     n = 3_000_017
     x, k, v, s = _table(conn, oracle, n)
