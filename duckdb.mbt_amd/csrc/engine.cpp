@@ -91,6 +91,26 @@ void HostColumnPush(HostColumn &c, const Value &v) {
   }
 }
 
+void ValueToRaw(const Value &v, Phys phys, uint8_t *p) {
+  switch (phys) {
+    case P_U8: case P_I8: { int8_t x = (int8_t)v.i; memcpy(p, &x, 1); break; }
+    case P_I16: case P_U16: { int16_t x = (int16_t)v.i; memcpy(p, &x, 2); break; }
+    case P_I32: case P_U32: { int32_t x = (int32_t)v.i; memcpy(p, &x, 4); break; }
+    case P_I64: case P_U64: { int64_t x = (int64_t)v.i; memcpy(p, &x, 8); break; }
+    case P_I128: {
+      uint64_t lo = (uint64_t)(u128)v.i;
+      int64_t hi = (int64_t)(uint64_t)((u128)v.i >> 64);
+      memcpy(p, &lo, 8);
+      memcpy(p + 8, &hi, 8);
+      break;
+    }
+    case P_F32: { float x = (float)v.d; memcpy(p, &x, 4); break; }
+    case P_F64: memcpy(p, &v.d, 8); break;
+    case P_INTERVAL: memcpy(p, &v.iv, 16); break;
+    default: break;
+  }
+}
+
 static ResultPtr CountResult(int64_t n) {
   auto r = std::make_shared<MaterializedResult>();
   HostColumn hc;

@@ -147,8 +147,19 @@ struct HostBatch {
   int64_t nrows = 0;
 };
 void AppendHostBatch(Connection &c, Table &t, const HostBatch &b);
+// pinned host memory for appender staging (hipHostMalloc / hipHostFree)
+void *HostPinnedAlloc(size_t bytes);
+void HostPinnedFree(void *p);
+// raw little-endian bytes of a (non-NULL) value already cast to the column type
+void ValueToRaw(const Value &v, Phys phys, uint8_t *dst);
+// Appends n rows given as host columns in their physical layout (valid[c]:
+// per-row bytes or NULL).  sync=false leaves the DMA and the zone-map
+// reduction in flight on the connection's stream (the appender's pinned
+// double buffer); the next device statement settles them first.
 void AppendRawColumns(Connection &c, Table &t, const std::vector<const void *> &vals,
-                      const std::vector<const uint8_t *> &valid, int64_t n);
+                      const std::vector<const uint8_t *> &valid, int64_t n, bool sync = true);
+// waits for in-flight appends and folds their zone-map statistics
+void SettleAppends(Connection &c);
 void HostColumnPush(HostColumn &col, const Value &v);  // v already of col.type (or NULL)
 void HbmCalibrateConn(Connection &c, int64_t bytes, int iters, double out[3]);
 

@@ -136,6 +136,17 @@ struct Engine {
   static constexpr size_t kStageBytes = (size_t)16 << 20;
   uint8_t *h_stage[kStageSlots] = {nullptr, nullptr, nullptr, nullptr};
   hipEvent_t stage_ev[kStageSlots] = {nullptr, nullptr, nullptr, nullptr};
+  // zone-map statistics of appends still in flight (appender's pinned double
+  // buffer): the stats reduction's 3 values land in a pinned slot and are
+  // folded into the column by SettlePending before the next device statement
+  struct PendingStat {
+    DevColumn *col;
+    long long *h;  // pinned: min, max, non-null count
+    int64_t n;
+    bool first_rows;
+  };
+  std::vector<PendingStat> pending_stats;
+  std::vector<long long *> stat_slots;  // free pinned 3-value slots
   bool profile = false;
   std::vector<ProfEvent> events;
   std::vector<std::pair<hipEvent_t, hipEvent_t>> ev_pool;  // reused across queries
@@ -165,6 +176,8 @@ struct Engine {
       if (d_partials) hipFree(d_partials);
       if (h_pinned) hipHostFree(h_pinned);
       if (h_mapped) hipHostFree(h_mapped);
+      for (auto &ps : pending_stats) stat_slots.push_back(ps.h);
+      for (auto *h : stat_slots) hipHostFree(h);
       for (int i = 0; i < kStageSlots; i++) {
         if (h_stage[i]) hipHostFree(h_stage[i]);
         if (stage_ev[i]) hipEventDestroy(stage_ev[i]);
@@ -219,12 +232,36 @@ std::shared_ptr<Engine> CreateEngine(int device, bool allow_no_gpu) {
   return e;
 }
 
+// folds the zone-map statistics of in-flight appends into their columns
+// (after the stream has drained: their DMAs and reductions are done)
+static void SettlePending(Engine &e) {
+  if (e.pending_stats.empty()) return;
+  HIPCHK(hipStreamSynchronize(e.stream));
+  for (auto &ps : e.pending_stats) {
+    DevColumn &c = *ps.col;
+    const long long *h = ps.h;
+    c.null_count += ps.n - h[2];
+    if (h[2] > 0) {
+      if (ps.first_rows || !c.stats_valid) {
+        c.imin = h[0];
+        c.imax = h[1];
+      } else {
+        c.imin = std::min<i128>(c.imin, h[0]);
+        c.imax = std::max<i128>(c.imax, h[1]);
+      }
+    }
+    e.stat_slots.push_back(ps.h);
+  }
+  e.pending_stats.clear();
+}
+
 static Engine &Eng(Connection &c) {
   Engine &e = *c.engine;
   if (!e.has_gpu)
     ThrowError("IO", "this statement reads table rows and needs the MI355X device, but no GPU is available");
   hipSetDevice(e.device);
   dev::SetTempAllocator(&TempAllocCb, &TempFreeCb, e.pool.get());
+  SettlePending(e);  // a statement never sees a column before its appended stats
   return e;
 }
 
@@ -2541,7 +2578,7 @@ static void EnsureValidity(Engine &e, DevColumn &c, int64_t nrows_old) {
   (void)nrows_old;
 }
 
-static void UpdateStats(Engine &e, DevColumn &c, int64_t off, int64_t n, bool first_rows) {
+static void UpdateStats(Engine &e, DevColumn &c, int64_t off, int64_t n, bool first_rows, bool async = false) {
   if (n <= 0) return;
   if (c.phys == P_STR || c.phys == P_F32 || c.phys == P_F64 || c.phys == P_I128 || c.phys == P_U64 ||
       c.phys == P_INTERVAL) {
@@ -2559,6 +2596,18 @@ static void UpdateStats(Engine &e, DevColumn &c, int64_t off, int64_t n, bool fi
     return;
   }
   dev::ColumnStats((const char *)c.data + off * sz, c.phys, v, n, o3, e.stream);
+  if (async) {
+    long long *slot = nullptr;
+    if (!e.stat_slots.empty()) {
+      slot = e.stat_slots.back();
+      e.stat_slots.pop_back();
+    } else {
+      HIPCHK(hipHostMalloc((void **)&slot, 3 * sizeof(long long), hipHostMallocDefault));
+    }
+    HIPCHK(hipMemcpyAsync(slot, o3, 3 * sizeof(long long), hipMemcpyDeviceToHost, e.stream));
+    e.pending_stats.push_back({&c, slot, n, first_rows});
+    return;
+  }
   long long h[3];
   HIPCHK(hipMemcpyAsync(h, o3, sizeof(h), hipMemcpyDeviceToHost, e.stream));
   HIPCHK(hipStreamSynchronize(e.stream));
@@ -2749,7 +2798,7 @@ static void StageH2D(Engine &e, void *dst, const void *src, size_t bytes) {
 // its physical layout and is DMA'd straight to its place at the table's end
 // (no intermediate device relation, no D2D append copy).
 void AppendRawColumns(Connection &c, Table &t, const std::vector<const void *> &vals,
-                      const std::vector<const uint8_t *> &valid, int64_t n) {
+                      const std::vector<const uint8_t *> &valid, int64_t n, bool sync) {
   Engine &e = Eng(c);
   const int64_t old = t.nrows;
   if (n <= 0) return;
@@ -2774,11 +2823,25 @@ void AppendRawColumns(Connection &c, Table &t, const std::vector<const void *> &
     } else if (col.validity) {
       dev::BitmapAppend(col.validity, old, nullptr, n, e.stream);
     }
-    UpdateStats(e, col, old, n, old == 0);
+    UpdateStats(e, col, old, n, old == 0, !sync);
   }
+  t.nrows = old + n;
+  if (!sync) return;  // DMA + stats in flight; SettlePending folds them
   HIPCHK(hipStreamSynchronize(e.stream));
   CheckError(e);
-  t.nrows = old + n;
+}
+
+void SettleAppends(Connection &c) {
+  if (c.engine && c.engine->has_gpu) SettlePending(*c.engine);
+}
+
+void *HostPinnedAlloc(size_t bytes) {
+  void *p = nullptr;
+  HIPCHK(hipHostMalloc(&p, bytes ? bytes : 16, hipHostMallocPortable));  // any device of the process
+  return p;
+}
+void HostPinnedFree(void *p) {
+  if (p) (void)hipHostFree(p);
 }
 
 void AppendHostBatch(Connection &c, Table &t, const HostBatch &b) {

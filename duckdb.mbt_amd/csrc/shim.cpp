@@ -113,13 +113,26 @@ struct duckdb_mb_statement {
 struct duckdb_mb_appender {
   duckdb_mb_connection *conn = nullptr;
   TablePtr table;
-  HostBatch batch;
+  HostBatch batch;  // VARCHAR tables: rows staged in host vectors
   size_t col = 0;
   char error[256];
+  // Fixed-width tables stage rows in two pinned buffers per column: while one
+  // fills, the other's DMA into the device column (and its zone-map
+  // reduction) is in flight on the connection's stream.
+  bool pinned = false;
+  std::vector<char *> pbuf[2];
+  std::vector<int> pw;                        // bytes per value, per column
+  std::vector<std::vector<uint8_t>> pvalid;   // per column: empty (all valid) or a byte per row
+  int pcur = 0;
+  int64_t prow = 0, pcap = 0;
   // columnar bulk ingest
   std::vector<const void *> raw_vals;
   std::vector<const uint8_t *> raw_valid;
   std::vector<int64_t> raw_count;
+  ~duckdb_mb_appender() {
+    for (int b = 0; b < 2; b++)
+      for (char *p : pbuf[b]) HostPinnedFree(p);
+  }
 };
 // The query's result stays on the device: fixed-width getters of columns
 // without NULLs DMA straight into the returned Bytes; the others materialize
@@ -543,17 +556,75 @@ duckdb_mb_appender *duckdb_mb_appender_create(duckdb_mb_connection *h, moonbit_b
   a->conn = h;
   a->table = t;
   a->error[0] = '\0';
+  a->pinned = !t->cols.empty();
   for (auto &c : t->cols) {
     HostColumn hc;
     hc.type = c.type;
     hc.phys = c.phys;
     if (hc.phys == P_STR) hc.offsets.push_back(0);
     a->batch.cols.push_back(hc);
+    if (c.phys == P_STR) a->pinned = false;
+    a->pw.push_back(c.phys == P_STR ? 0 : PhysSize(c.phys));
   }
+  a->pvalid.resize(t->cols.size());
   return a;
 }
 
+// the current pinned buffer's complete rows -> the device (async unless
+// sync); then the other buffer, whose DMA the append path has settled
+static bool FlushPinned(duckdb_mb_appender *a, bool sync) {
+  if (a->prow > 0) {
+    std::vector<const void *> vals;
+    std::vector<const uint8_t *> valid;
+    for (size_t c = 0; c < a->pw.size(); c++) {
+      vals.push_back(a->pbuf[a->pcur][c]);
+      valid.push_back(a->pvalid[c].empty() ? nullptr : a->pvalid[c].data());
+    }
+    try {
+      AppendRawColumns(a->conn->conn, *a->table, vals, valid, a->prow, sync);
+    } catch (std::exception &e) {
+      CopyErr(a->error, e.what());
+      return false;
+    }
+    a->pcur ^= 1;
+    a->prow = 0;
+    for (auto &v : a->pvalid) v.clear();
+  }
+  if (sync) {
+    try {
+      SettleAppends(a->conn->conn);
+    } catch (std::exception &e) {
+      CopyErr(a->error, e.what());
+      return false;
+    }
+  }
+  return true;
+}
+
+// pinned slot of the current row for column `c` (allocated on first use)
+static uint8_t *PinnedSlot(duckdb_mb_appender *a, size_t c) {
+  if (a->pcap == 0) {
+    int64_t row_bytes = 0;
+    for (int w : a->pw) row_bytes += w;
+    // the flush size, capped at 32 MB of pinned staging per buffer
+    a->pcap = std::max<int64_t>(1, std::min<int64_t>(a->conn->conn.opts.appender_flush_rows,
+                                                     std::max<int64_t>(1024, ((int64_t)32 << 20) / row_bytes)));
+    for (int b = 0; b < 2; b++)
+      for (int w : a->pw) a->pbuf[b].push_back((char *)HostPinnedAlloc((size_t)a->pcap * w));
+  }
+  return (uint8_t *)a->pbuf[a->pcur][c] + (size_t)a->prow * a->pw[c];
+}
+
+static void PinnedValid(duckdb_mb_appender *a, size_t c, bool valid) {
+  auto &v = a->pvalid[c];
+  if (valid && v.empty()) return;
+  if (v.empty()) v.assign((size_t)a->prow, 1);
+  v.resize((size_t)a->prow);  // drop a stale byte of an abandoned partial row
+  v.push_back(valid ? 1 : 0);
+}
+
 static bool FlushAppender(duckdb_mb_appender *a) {
+  if (a->pinned) return FlushPinned(a, true);
   // a partial row (destroy with a row half appended) stays out of the flush
   for (auto &hc : a->batch.cols) {
     const size_t n = (size_t)a->batch.nrows;
@@ -609,7 +680,18 @@ static int32_t AppendValue(duckdb_mb_appender *a, const Value &v) {
     return 0;
   }
   try {
-    HostColumnPush(a->batch.cols[a->col], CastValue(v, a->table->cols[a->col].type));
+    Value cv = CastValue(v, a->table->cols[a->col].type);
+    if (a->pinned) {
+      if (cv.is_null) {
+        memset(PinnedSlot(a, a->col), 0, a->pw[a->col]);
+        PinnedValid(a, a->col, false);
+      } else {
+        ValueToRaw(cv, a->batch.cols[a->col].phys, PinnedSlot(a, a->col));
+        PinnedValid(a, a->col, true);
+      }
+    } else {
+      HostColumnPush(a->batch.cols[a->col], cv);
+    }
   } catch (std::exception &e) {
     CopyErr(a->error, e.what());
     return 0;
@@ -622,6 +704,12 @@ static int32_t AppendValue(duckdb_mb_appender *a, const Value &v) {
 static inline int32_t AppendRaw(duckdb_mb_appender *a, const void *v, int sz, TypeId tid, Phys phys) {
   if (a && a->col < a->batch.cols.size()) {
     HostColumn &hc = a->batch.cols[a->col];
+    if (a->pinned && hc.phys == phys && hc.type.id == tid) {
+      memcpy(PinnedSlot(a, a->col), v, sz);
+      PinnedValid(a, a->col, true);
+      a->col++;
+      return 1;
+    }
     if (hc.phys == phys && hc.type.id == tid && hc.valid.empty()) {
       const size_t at = hc.data.size();
       hc.data.resize(at + sz);
@@ -652,7 +740,12 @@ int32_t duckdb_mb_append_null(duckdb_mb_appender *a) {  // ref :1205
     CopyErr(a->error, "Too many appends for chunk!");
     return 0;
   }
-  HostColumnPush(a->batch.cols[a->col], Value::Null(a->table->cols[a->col].type));
+  if (a->pinned) {
+    memset(PinnedSlot(a, a->col), 0, a->pw[a->col]);
+    PinnedValid(a, a->col, false);
+  } else {
+    HostColumnPush(a->batch.cols[a->col], Value::Null(a->table->cols[a->col].type));
+  }
   a->col++;
   return 1;
 }
@@ -662,8 +755,12 @@ int32_t duckdb_mb_end_row(duckdb_mb_appender *a) {  // ref :1221-1235
     CopyErr(a->error, "Call to EndRow before all columns have been appended to!");
     return 0;
   }
-  a->batch.nrows++;
   a->col = 0;
+  if (a->pinned) {
+    if (++a->prow >= a->pcap) return FlushPinned(a, false) ? 1 : 0;
+    return 1;
+  }
+  a->batch.nrows++;
   if (a->batch.nrows >= a->conn->conn.opts.appender_flush_rows) return FlushAppender(a) ? 1 : 0;
   return 1;
 }
