@@ -49,6 +49,61 @@ Value HostColumn::Get(int64_t row) const {
   return v;
 }
 
+int HostColumn::FormatInto(int64_t row, char *out) const {
+  const uint8_t *p = data.data();
+  i128 x;
+  switch (phys) {
+    case P_U8: x = p[row]; break;
+    case P_I8: x = ((const int8_t *)p)[row]; break;
+    case P_I16: x = ((const int16_t *)p)[row]; break;
+    case P_U16: x = ((const uint16_t *)p)[row]; break;
+    case P_I32: x = ((const int32_t *)p)[row]; break;
+    case P_U32: x = ((const uint32_t *)p)[row]; break;
+    case P_I64: x = ((const int64_t *)p)[row]; break;
+    case P_U64: x = (i128)((const uint64_t *)p)[row]; break;
+    case P_I128: {
+      uint64_t lo;
+      int64_t hi;
+      memcpy(&lo, p + 16 * row, 8);
+      memcpy(&hi, p + 16 * row + 8, 8);
+      x = (i128)(((u128)(uint64_t)hi << 64) | lo);
+      break;
+    }
+    default: return -1;
+  }
+  switch (type.id) {
+    case T_BOOLEAN:
+      if (x) { memcpy(out, "true", 4); return 4; }
+      memcpy(out, "false", 5);
+      return 5;
+    case T_TINYINT: case T_SMALLINT: case T_INTEGER: case T_BIGINT: case T_UTINYINT:
+    case T_USMALLINT: case T_UINTEGER: case T_UBIGINT: case T_HUGEINT:
+      return FormatI128Into(x, out);
+    case T_DECIMAL: {  // same spelling as FormatDecimal: [-]int.frac, frac zero-padded to scale
+      const int scale = type.scale;
+      if (scale == 0) return FormatI128Into(x, out);
+      const bool neg = x < 0;
+      char dig[48];
+      int n = FormatI128Into(neg ? (i128)(~(u128)x + 1) : x, dig);
+      int o = 0;
+      if (neg) out[o++] = '-';
+      if (n <= scale) {
+        out[o++] = '0';
+        out[o++] = '.';
+        for (int i = n; i < scale; i++) out[o++] = '0';
+        memcpy(out + o, dig, (size_t)n);
+        return o + n;
+      }
+      memcpy(out + o, dig, (size_t)(n - scale));
+      o += n - scale;
+      out[o++] = '.';
+      memcpy(out + o, dig + n - scale, (size_t)scale);
+      return o + scale;
+    }
+    default: return -1;
+  }
+}
+
 void HostColumnPush(HostColumn &c, const Value &v) {
   bool null = v.is_null;
   if (null || !c.valid.empty()) {

@@ -61,6 +61,9 @@ struct HostColumn {
   std::vector<int64_t> offsets;      // P_STR
   std::string chars;                 // P_STR
   Value Get(int64_t row) const;
+  // Text of a non-NULL integer/BOOLEAN/DECIMAL cell written into out (>= 48
+  // bytes), spelled as FormatValue(Get(row)); -1 for the other types.
+  int FormatInto(int64_t row, char *out) const;
   bool IsNull(int64_t row) const { return !valid.empty() && !valid[row]; }
 };
 

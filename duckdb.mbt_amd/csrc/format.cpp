@@ -10,6 +10,7 @@
 #include <charconv>
 #include <cmath>
 #include <cstdio>
+#include <cstring>
 
 #include "types.h"
 
@@ -43,19 +44,53 @@ bool ParseI128(const std::string &s, i128 *out) {
   return true;
 }
 
-std::string FormatI128(i128 x) {
-  if (x == 0) return "0";
-  char buf[64];
-  int p = 63;
-  buf[p] = 0;
-  bool neg = x < 0;
-  u128 u = neg ? (u128)(~(u128)x + 1) : (u128)x;
-  while (u) {
-    buf[--p] = (char)('0' + (int)(u % 10));
-    u /= 10;
+// Integer text without per-digit 128-bit division: two digits per step in
+// 64-bit arithmetic, and a 128-bit value is split into 19-digit limbs first.
+static const char kDigitPairs[] =
+    "00010203040506070809101112131415161718192021222324252627282930313233343536373839"
+    "40414243444546474849505152535455565758596061626364656667686970717273747576777879"
+    "8081828384858687888990919293949596979899";
+
+static inline int U64Back(uint64_t u, char *end) {  // digits of u ending at end; returns count
+  char *p = end;
+  while (u >= 100) {
+    const unsigned r = (unsigned)(u % 100);
+    u /= 100;
+    p -= 2;
+    memcpy(p, kDigitPairs + 2 * r, 2);
   }
-  if (neg) buf[--p] = '-';
-  return std::string(buf + p);
+  if (u >= 10) {
+    p -= 2;
+    memcpy(p, kDigitPairs + 2 * u, 2);
+  } else {
+    *--p = (char)('0' + u);
+  }
+  return (int)(end - p);
+}
+
+int FormatI128Into(i128 x, char *out) {
+  char buf[48];
+  char *end = buf + sizeof(buf), *p = end;
+  const bool neg = x < 0;
+  u128 u = neg ? (u128)(~(u128)x + 1) : (u128)x;
+  const uint64_t kP19 = 10000000000000000000ull;
+  while (u >> 64) {
+    const uint64_t r = (uint64_t)(u % kP19);
+    u /= kP19;
+    int n = U64Back(r, p);
+    p -= n;
+    for (; n < 19; n++) *--p = '0';
+  }
+  p -= U64Back((uint64_t)u, p);
+  if (neg) *--p = '-';
+  const int len = (int)(end - p);
+  memcpy(out, p, (size_t)len);
+  return len;
+}
+
+std::string FormatI128(i128 x) {
+  char buf[48];
+  return std::string(buf, (size_t)FormatI128Into(x, buf));
 }
 
 std::string FormatDecimal(i128 x, int scale) {

@@ -244,6 +244,9 @@ moonbit_bytes_t duckdb_mb_result_value(duckdb_mb_result *r, int32_t col, int32_t
   if (!r || !InRange(r->r, col, row)) return moonbit_make_bytes_raw(0);
   const HostColumn &c = r->r->cols[col];
   if (c.IsNull(row)) return moonbit_make_bytes_raw(0);
+  char buf[48];
+  const int n = c.FormatInto(row, buf);
+  if (n >= 0) return MakeBytes(buf, (size_t)n);
   return MakeBytes(FormatValue(c.Get(row)));
 }
 int32_t duckdb_mb_is_null_result(duckdb_mb_result *r) { return r == nullptr ? 1 : 0; }  // ref :252
@@ -347,6 +350,9 @@ moonbit_bytes_t duckdb_mb_chunk_value(duckdb_mb_chunk *c, int32_t col, int32_t r
   if (!c || col < 0 || col >= (int32_t)c->r->cols.size() || row < 0 || row >= c->n) return moonbit_make_bytes_raw(0);
   const HostColumn &hc = c->r->cols[col];
   if (hc.IsNull(c->start + row)) return moonbit_make_bytes_raw(0);
+  char buf[48];
+  const int n = hc.FormatInto(c->start + row, buf);
+  if (n >= 0) return MakeBytes(buf, (size_t)n);
   return MakeBytes(FormatValue(hc.Get(c->start + row)));
 }
 
@@ -1284,8 +1290,14 @@ char *duckdb_mbx_result_text(duckdb_mb_result *r, int64_t *len) {
     for (int64_t col = 0; col < nc; col++) {
       const HostColumn &c = m.cols[col];
       const int64_t i = row * nc + col;
-      if (c.IsNull(row)) nul[i] = 1;
-      else chars += FormatValue(c.Get(row));
+      if (c.IsNull(row)) {
+        nul[i] = 1;
+      } else {
+        char buf[48];
+        const int n = c.FormatInto(row, buf);
+        if (n >= 0) chars.append(buf, (size_t)n);
+        else chars += FormatValue(c.Get(row));
+      }
       off[i + 1] = (int64_t)chars.size();
     }
   const size_t head = 16 + (((size_t)ncell + 7) & ~(size_t)7);

@@ -137,6 +137,8 @@ struct Value {
 // DuckDB-compatible text rendering (what duckdb_value_varchar returns).
 std::string FormatValue(const Value &v);
 std::string FormatI128(i128 x);
+// Writes the decimal text of x into out (>= 41 bytes); returns its length.
+int FormatI128Into(i128 x, char *out);
 std::string FormatDecimal(i128 x, int scale);
 std::string FormatDouble(double x);
 std::string FormatFloat(float x);

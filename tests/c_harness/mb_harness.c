@@ -269,7 +269,7 @@ static int c4_bench(duckdb_mb_connection *c, long rows) {
  * 249 999 500 000.  Prints one JSON line (best of `reps`). */
 static int c1_bench(duckdb_mb_connection *c, int reps) {
   const char *q = "SELECT i FROM range(1000000) tbl(i) WHERE i%2=0";
-  double best_q = 1e30, best_s = 1e30;
+  double best_q = 1e30, best_s = 1e30, best_exec = 1e30, best_first = 1e30;
   long long sum_q = 0, sum_s = 0;
   long rows_q = 0, rows_s = 0, chunks = 0;
   for (int rep = 0; rep < reps; rep++) {
@@ -279,6 +279,8 @@ static int c1_bench(duckdb_mb_connection *c, int reps) {
     mb_free(sql);
     CHECK(r != NULL, "c1 query: %s", take(duckdb_mb_last_error()));
     if (!r) return 1;
+    const double te = now_s() - t0;
+    if (te < best_exec) best_exec = te;
     rows_q = duckdb_mb_result_row_count(r);
     sum_q = 0;
     for (int32_t i = 0; i < rows_q; i++) {
@@ -305,6 +307,7 @@ static int c1_bench(duckdb_mb_connection *c, int reps) {
     for (;;) {
       duckdb_mb_chunk *ch = duckdb_mb_stream_fetch_chunk(st);
       if (!ch) break;
+      if (chunks == 0 && now_s() - t1 < best_first) best_first = now_s() - t1;
       int32_t nr = duckdb_mb_chunk_row_count(ch);
       for (int32_t i = 0; i < nr; i++) {
         moonbit_bytes_t v = duckdb_mb_chunk_value(ch, 0, i);
@@ -326,9 +329,11 @@ static int c1_bench(duckdb_mb_connection *c, int reps) {
   }
   const int ok = rows_q == 500000 && sum_q == 249999500000LL && rows_s == 500000 && sum_s == 249999500000LL;
   CHECK(ok, "c1: query %ld rows sum %lld, stream %ld rows sum %lld", rows_q, sum_q, rows_s, sum_s);
-  printf("{\"rows\": %ld, \"query_percell_s\": %.6f, \"query_rows_per_s\": %.1f, \"stream_s\": %.6f, "
-         "\"stream_rows_per_s\": %.1f, \"stream_chunks\": %ld, \"sum\": %lld, \"exact\": %s}\n",
-         rows_q, best_q, rows_q / best_q, best_s, rows_s / best_s, chunks, sum_q, ok ? "true" : "false");
+  printf("{\"rows\": %ld, \"query_percell_s\": %.6f, \"query_rows_per_s\": %.1f, \"query_exec_s\": %.6f, "
+         "\"stream_s\": %.6f, \"stream_rows_per_s\": %.1f, \"stream_first_chunk_s\": %.6f, \"stream_chunks\": %ld, "
+         "\"sum\": %lld, \"exact\": %s}\n",
+         rows_q, best_q, rows_q / best_q, best_exec, best_s, rows_s / best_s, best_first, chunks, sum_q,
+         ok ? "true" : "false");
   return 0;
 }
 

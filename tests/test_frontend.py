@@ -134,3 +134,40 @@ def test_bulk_text_pull_matches_per_cell(hostconn):
         b = hostconn.query_percell(sql.replace("bulk_t", "bulk_t2")).value
         assert a.rows == b.rows and a.nulls == b.nulls, sql
         assert a.columns == b.columns and a.column_types == b.column_types
+
+
+def _dec_text(raw, scale):
+    # DuckDB's DECIMAL spelling: [-]int.frac with frac zero-padded to the scale
+    if scale == 0:
+        return str(raw)
+    a = abs(raw)
+    return ("-" if raw < 0 else "") + f"{a // 10 ** scale}.{a % 10 ** scale:0{scale}d}"
+
+
+def test_integer_cell_text_random(hostconn):
+    """The per-cell and bulk text paths format integer, HUGEINT and DECIMAL
+    cells with a 64-bit two-digit formatter (HostColumn::FormatInto); check it
+    against Python's exact text over random magnitudes and the extremes."""
+    import random
+    rng = random.Random(5)
+    ints = [0, 1, -1, 9, 10, 99, 100, -100, 2 ** 63 - 1, -2 ** 63, 10 ** 18, -10 ** 18]
+    ints += [rng.randrange(-2 ** 63, 2 ** 63) >> rng.randrange(0, 63) for _ in range(60)]
+    huge = [2 ** 127 - 1, -2 ** 127 + 1, 10 ** 19 - 1, 10 ** 19, -10 ** 19, 10 ** 38 - 1, 2 ** 64, -(2 ** 64) - 1]
+    huge += [rng.randrange(-2 ** 127, 2 ** 127) >> rng.randrange(0, 127) for _ in range(60)]
+    cols = [f"({v})::BIGINT" for v in ints] + [f"({v})::HUGEINT" for v in huge]
+    want = [str(v) for v in ints] + [str(v) for v in huge]
+    decs = []
+    for _ in range(60):
+        w = rng.choice([4, 9, 15, 18, 30, 38])
+        sc = rng.randrange(0, w + 1)
+        raw = rng.randrange(-10 ** w + 1, 10 ** w) // 10 ** rng.randrange(0, w)
+        decs.append((raw, w, sc))
+    decs += [(5, 15, 2), (-5, 15, 2), (-50, 15, 2), (0, 15, 2), (10 ** 38 - 1, 38, 38), (-(10 ** 18) + 1, 18, 18)]
+    for raw, w, sc in decs:
+        cols.append(f"CAST('{_dec_text(raw, sc)}' AS DECIMAL({w},{sc}))")
+        want.append(_dec_text(raw, sc))
+    cols += ["true", "false", "42::TINYINT", "(-7)::SMALLINT", "255::UTINYINT", "18446744073709551615::UBIGINT"]
+    want += ["true", "false", "42", "-7", "255", "18446744073709551615"]
+    sql = "SELECT " + ", ".join(cols)
+    assert q(hostconn, sql).rows == [want]
+    assert hostconn.query_percell(sql).value.rows == [want]
