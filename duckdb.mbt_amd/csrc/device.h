@@ -251,6 +251,11 @@ struct HostCopyDesc {
   int32_t *err_dst;
 };
 void HostCopy(const HostCopyDesc &d, hipStream_t s);
+// Arrow wire layout of a fixed-width (1/4/8-byte) column: vals[i] = src[i], or
+// 0 where the validity bit is clear; vbytes[i] = validity (may be nullptr;
+// valid == nullptr means no NULLs).
+void ArrowWire(const void *src, const uint64_t *valid, int64_t n, int width, void *vals, uint8_t *vbytes,
+               hipStream_t s);
 
 // Filter -> compaction in two streaming passes (order preserving), for a
 // conjunction of range predicates over NULL-free int32/int64 columns and

@@ -123,11 +123,10 @@ struct StreamSource {
 StreamSource RunStatementStream(Connection &c, const Statement &st, const std::vector<Value> &params);
 // rows [start, start + n) of a device result, materialized on the host
 ResultPtr FetchDeviceRows(Connection &c, DeviceResult &d, int64_t start, int64_t n);
-// Copies column `col` of a device result straight into host memory `dst`
-// (its physical layout, n rows) when it has physical type `phys` and no
-// NULLs; false otherwise (the caller materializes the result instead).
-bool CopyDeviceColumn(Connection &c, DeviceResult &d, int col, int phys, void *dst);
-bool DeviceColumnPlain(const DeviceResult &d, int col, int phys);  // the precondition of CopyDeviceColumn
+// Arrow wire form of a 1/4/8-byte device column, NULLs allowed: values with
+// NULL slots zeroed into vals, validity bytes into vbytes (if not nullptr).
+bool CopyDeviceColumnWire(Connection &c, DeviceResult &d, int col, int phys, void *vals, uint8_t *vbytes);
+bool DeviceColumnWireOk(const DeviceResult &d, int col, int phys);  // its precondition
 
 // Runs one statement; returns a materialized result (empty for DDL).
 ResultPtr RunStatement(Connection &c, const std::string &sql, const std::vector<Value> &params, int *n_params_out);

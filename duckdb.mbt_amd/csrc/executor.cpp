@@ -2489,19 +2489,36 @@ ResultPtr FetchDeviceRows(Connection &c, DeviceResult &d, int64_t start, int64_t
   return ToHost(e, d.r, d.names, start, n, d.names.size());
 }
 
-bool DeviceColumnPlain(const DeviceResult &d, int col, int phys) {
+bool DeviceColumnWireOk(const DeviceResult &d, int col, int phys) {
   if (col < 0 || col >= (int)d.r.cols.size()) return false;
   const DCol &dc = d.r.cols[col];
-  return dc.phys == phys && !dc.validity && dc.phys != P_STR && dc.data;
+  const int w = PhysSize(dc.phys);
+  return dc.phys == phys && dc.data && (w == 1 || w == 4 || w == 8) && dc.phys != P_STR;
 }
 
-bool CopyDeviceColumn(Connection &c, DeviceResult &d, int col, int phys, void *dst) {
-  if (!DeviceColumnPlain(d, col, phys)) return false;
+// The Arrow wire form of one device column (values with NULLs zeroed, then
+// validity bytes when vbytes != nullptr), built by one kernel in a device
+// staging buffer and copied out with one DMA per part.
+bool CopyDeviceColumnWire(Connection &c, DeviceResult &d, int col, int phys, void *vals, uint8_t *vbytes) {
+  if (!DeviceColumnWireOk(d, col, phys)) return false;
   const DCol &dc = d.r.cols[col];
   Engine &e = Eng(c);
-  size_t bytes = (size_t)d.r.n * PhysSize(dc.phys);
-  if (bytes) HIPCHK(hipMemcpyAsync(dst, dc.data, bytes, hipMemcpyDeviceToHost, e.stream));
+  const int64_t n = d.r.n;
+  const int w = PhysSize(dc.phys);
+  if (n <= 0) return true;
+  if (!dc.validity) {  // nothing to zero: the column is already the wire layout
+    HIPCHK(hipMemcpyAsync(vals, dc.data, (size_t)n * w, hipMemcpyDeviceToHost, e.stream));
+    HIPCHK(hipStreamSynchronize(e.stream));
+    if (vbytes) memset(vbytes, 1, (size_t)n);
+    return true;
+  }
+  auto buf = Alloc(e, (size_t)n * (w + 1) + 16);
+  uint8_t *dv = (uint8_t *)buf->p, *db = dv + (size_t)n * w;
+  dev::ArrowWire(dc.data, dc.validity, n, w, dv, vbytes ? db : nullptr, e.stream);
+  HIPCHK(hipMemcpyAsync(vals, dv, (size_t)n * w, hipMemcpyDeviceToHost, e.stream));
+  if (vbytes) HIPCHK(hipMemcpyAsync(vbytes, db, (size_t)n, hipMemcpyDeviceToHost, e.stream));
   HIPCHK(hipStreamSynchronize(e.stream));
+  CheckError(e);
   return true;
 }
 

@@ -2396,6 +2396,33 @@ void HostCopy(const HostCopyDesc &d, hipStream_t s) {
   CHECK_LAUNCH();
 }
 
+// Arrow wire layout of one fixed-width column (reference duckdb_native.c
+// :2572-2797, the *_nullable getters): values with NULL slots zeroed, then one
+// validity byte per row (1 = valid).  Rows are independent; each thread does
+// one row per grid-stride step, so loads and stores are coalesced.
+template <typename T>
+__global__ void arrow_wire_kernel(const T *__restrict__ src, const uint64_t *__restrict__ valid, int64_t n,
+                                  T *__restrict__ vals, uint8_t *__restrict__ vbytes) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    const bool ok = valid == nullptr || ((valid[i >> 6] >> (i & 63)) & 1);
+    vals[i] = ok ? src[i] : (T)0;
+    if (vbytes) vbytes[i] = ok ? 1 : 0;
+  }
+}
+
+void ArrowWire(const void *src, const uint64_t *valid, int64_t n, int width, void *vals, uint8_t *vbytes,
+               hipStream_t s) {
+  if (n <= 0) return;
+  const dim3 g(GridFor(n, 256 * 4, 4096)), b(256);
+  switch (width) {
+    case 1: hipLaunchKernelGGL(arrow_wire_kernel<uint8_t>, g, b, 0, s, (const uint8_t *)src, valid, n, (uint8_t *)vals, vbytes); break;
+    case 4: hipLaunchKernelGGL(arrow_wire_kernel<uint32_t>, g, b, 0, s, (const uint32_t *)src, valid, n, (uint32_t *)vals, vbytes); break;
+    case 8: hipLaunchKernelGGL(arrow_wire_kernel<uint64_t>, g, b, 0, s, (const uint64_t *)src, valid, n, (uint64_t *)vals, vbytes); break;
+    default: return;
+  }
+  CHECK_LAUNCH();
+}
+
 __global__ void rebase_kernel(const int64_t *src, int64_t *dst, int64_t n, int64_t delta) {
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
     dst[i] = src[i] + delta;

@@ -940,26 +940,41 @@ static uint8_t CellBool(const HostColumn &c, int64_t row) {
 static bool ArrowOk(duckdb_mb_arrow_result *a, int32_t col) {
   return a && col >= 0 && col < a->column_count && a->row_count > 0;
 }
-// device result, column of exactly this type, no NULLs: DMA into dst
-static bool ArrowDirectOk(duckdb_mb_arrow_result *a, int32_t col, TypeId t, Phys ph) {
-  return a->dev && !a->r && a->types[col].id == t && DeviceColumnPlain(*a->dev, col, ph);
-}
-static bool ArrowDirect(duckdb_mb_arrow_result *a, int32_t col, TypeId t, Phys ph, void *dst) {
-  return ArrowDirectOk(a, col, t, ph) && CopyDeviceColumn(a->conn->conn, *a->dev, col, ph, dst);
-}
-// [i32 count][values] straight from the device column, or nullptr
-static moonbit_bytes_t ArrowDirectBuffer(duckdb_mb_arrow_result *a, int32_t col, TypeId t, Phys ph, int width) {
-  if (!ArrowOk(a, col) || 4 + (int64_t)a->row_count * width > INT32_MAX || !ArrowDirectOk(a, col, t, ph))
+// [i32 count][values][validity bytes if nullable] straight from a device
+// column of exactly this type (NULL slots zeroed on the device), or nullptr
+static moonbit_bytes_t ArrowDirectBuffer(duckdb_mb_arrow_result *a, int32_t col, TypeId t, Phys ph, int width,
+                                         bool nullable = false) {
+  if (!ArrowOk(a, col) || !a->dev || a->r || a->types[col].id != t || !DeviceColumnWireOk(*a->dev, col, ph))
     return nullptr;
-  moonbit_bytes_t out = moonbit_make_bytes_raw(4 + a->row_count * width);
+  const int64_t n = a->row_count;
+  const int64_t total = 4 + n * width + (nullable ? n : 0);
+  if (total > INT32_MAX) return nullptr;
+  moonbit_bytes_t out = moonbit_make_bytes_raw((int32_t)total);
   memcpy(out, &a->row_count, 4);
+  uint8_t *vb = nullable ? out + 4 + n * width : nullptr;
   try {
-    CopyDeviceColumn(a->conn->conn, *a->dev, col, ph, out + 4);
+    CopyDeviceColumnWire(a->conn->conn, *a->dev, col, ph, out + 4, vb);
   } catch (std::exception &e) {
     SetError(e.what());
-    memset(out + 4, 0, (size_t)a->row_count * width);
+    memset(out + 4, 0, (size_t)(total - 4));
   }
   return out;
+}
+// the same layout from a host column of exactly this type
+static bool ArrowHostExact(const HostColumn &c, int64_t n, TypeId t, Phys ph, int width, bool nullable,
+                           uint8_t *vals) {
+  if (c.type.id != t || c.phys != ph || (int64_t)c.data.size() < n * width) return false;
+  memcpy(vals, c.data.data(), (size_t)(n * width));
+  uint8_t *vb = vals + n * width;
+  if (c.valid.empty()) {
+    if (nullable) memset(vb, 1, (size_t)n);
+    return true;
+  }
+  for (int64_t i = 0; i < n; i++) {
+    if (!c.valid[i]) memset(vals + i * width, 0, (size_t)width);
+    if (nullable) vb[i] = c.valid[i];
+  }
+  return true;
 }
 static const MaterializedResult &ArrowHost(duckdb_mb_arrow_result *a) {
   if (a->r) return *a->r;
@@ -999,6 +1014,8 @@ static moonbit_bytes_t ArrowFixed(duckdb_mb_arrow_result *a, int32_t col, int wi
   uint8_t *vals = out + 4;
   uint8_t *valid = out + 4 + n * width;
   const HostColumn &c = ArrowHost(a).cols[col];
+  if (width == 4 && ArrowHostExact(c, n, T_INTEGER, P_I32, 4, nullable, vals)) return out;
+  if (width == 1 && ArrowHostExact(c, n, T_BOOLEAN, P_U8, 1, nullable, vals)) return out;
   for (int64_t i = 0; i < n; i++) {
     bool null = c.IsNull(i);
     if (nullable) valid[i] = null ? 0 : 1;
@@ -1028,6 +1045,7 @@ static moonbit_bytes_t ArrowF64(duckdb_mb_arrow_result *a, int32_t col, bool nul
   int32_t cnt = (int32_t)n;
   memcpy(out, &cnt, 4);
   const HostColumn &c = ArrowHost(a).cols[col];
+  if (ArrowHostExact(c, n, T_DOUBLE, P_F64, 8, nullable, out + 4)) return out;
   for (int64_t i = 0; i < n; i++) {
     bool null = c.IsNull(i);
     double x = null ? 0.0 : CellF64(c, i);
@@ -1043,7 +1061,12 @@ static moonbit_bytes_t ArrowStr(duckdb_mb_arrow_result *a, int32_t col, bool nul
   const HostColumn &c = ArrowHost(a).cols[col];
   std::string data;
   for (int64_t i = 0; i < n; i++) {
-    if (!c.IsNull(i)) data += FormatValue(c.Get(i));
+    if (!c.IsNull(i)) {
+      char buf[48];
+      const int k = c.FormatInto(i, buf);
+      if (k >= 0) data.append(buf, (size_t)k);
+      else data += FormatValue(c.Get(i));
+    }
     data.push_back('\0');
   }
   int64_t total = 8 + (int64_t)data.size() + (nullable ? n : 0);
@@ -1070,12 +1093,7 @@ moonbit_bytes_t duckdb_mb_arrow_get_column_int64(duckdb_mb_arrow_result *a, int3
   int32_t cnt = (int32_t)n;
   memcpy(out, &cnt, 4);
   const HostColumn &c = ArrowHost(a).cols[col];
-  if (c.phys == P_I64 && c.type.id == T_BIGINT) {
-    // fast path: the D2H'd column already is the wire layout
-    memcpy(out + 4, c.data.data(), (size_t)n * 8);
-    for (int64_t i = 0; i < n; i++)
-      if (c.IsNull(i)) memset(out + 4 + 8 * i, 0, 8);
-  } else {
+  if (!ArrowHostExact(c, n, T_BIGINT, P_I64, 8, false, out + 4)) {
     for (int64_t i = 0; i < n; i++) {
       int64_t x = c.IsNull(i) ? 0 : CellI64(c, i);
       memcpy(out + 4 + 8 * i, &x, 8);
@@ -1088,16 +1106,24 @@ moonbit_bytes_t duckdb_mb_arrow_get_column_double(duckdb_mb_arrow_result *a, int
   return ArrowF64(a, col, false);
 }
 moonbit_bytes_t duckdb_mb_arrow_get_column_string(duckdb_mb_arrow_result *a, int32_t col) { return ArrowStr(a, col, false); }  // ref :2456
-moonbit_bytes_t duckdb_mb_arrow_get_column_bool(duckdb_mb_arrow_result *a, int32_t col) { return ArrowFixed(a, col, 1, false); }  // ref :2516
-moonbit_bytes_t duckdb_mb_arrow_get_column_int32_nullable(duckdb_mb_arrow_result *a, int32_t col) { return ArrowFixed(a, col, 4, true); }  // ref :2572
+moonbit_bytes_t duckdb_mb_arrow_get_column_bool(duckdb_mb_arrow_result *a, int32_t col) {  // ref :2516
+  if (moonbit_bytes_t d = ArrowDirectBuffer(a, col, T_BOOLEAN, P_U8, 1)) return d;
+  return ArrowFixed(a, col, 1, false);
+}
+moonbit_bytes_t duckdb_mb_arrow_get_column_int32_nullable(duckdb_mb_arrow_result *a, int32_t col) {  // ref :2572
+  if (moonbit_bytes_t d = ArrowDirectBuffer(a, col, T_INTEGER, P_I32, 4, true)) return d;
+  return ArrowFixed(a, col, 4, true);
+}
 moonbit_bytes_t duckdb_mb_arrow_get_column_int64_nullable(duckdb_mb_arrow_result *a, int32_t col) {  // ref :2611
   if (!ArrowOk(a, col)) return MakeBytes("", 0);
   int64_t n = a->row_count;
   if (4 + n * 9 > INT32_MAX) return MakeBytes("", 0);
+  if (moonbit_bytes_t d = ArrowDirectBuffer(a, col, T_BIGINT, P_I64, 8, true)) return d;
   moonbit_bytes_t out = moonbit_make_bytes_raw((int32_t)(4 + n * 9));
   int32_t cnt = (int32_t)n;
   memcpy(out, &cnt, 4);
   const HostColumn &c = ArrowHost(a).cols[col];
+  if (ArrowHostExact(c, n, T_BIGINT, P_I64, 8, true, out + 4)) return out;
   for (int64_t i = 0; i < n; i++) {
     bool null = c.IsNull(i);
     int64_t x = null ? 0 : CellI64(c, i);
@@ -1106,9 +1132,15 @@ moonbit_bytes_t duckdb_mb_arrow_get_column_int64_nullable(duckdb_mb_arrow_result
   }
   return out;
 }
-moonbit_bytes_t duckdb_mb_arrow_get_column_double_nullable(duckdb_mb_arrow_result *a, int32_t col) { return ArrowF64(a, col, true); }  // ref :2649
+moonbit_bytes_t duckdb_mb_arrow_get_column_double_nullable(duckdb_mb_arrow_result *a, int32_t col) {  // ref :2649
+  if (moonbit_bytes_t d = ArrowDirectBuffer(a, col, T_DOUBLE, P_F64, 8, true)) return d;
+  return ArrowF64(a, col, true);
+}
 moonbit_bytes_t duckdb_mb_arrow_get_column_string_nullable(duckdb_mb_arrow_result *a, int32_t col) { return ArrowStr(a, col, true); }  // ref :2687
-moonbit_bytes_t duckdb_mb_arrow_get_column_bool_nullable(duckdb_mb_arrow_result *a, int32_t col) { return ArrowFixed(a, col, 1, true); }  // ref :2761
+moonbit_bytes_t duckdb_mb_arrow_get_column_bool_nullable(duckdb_mb_arrow_result *a, int32_t col) {  // ref :2761
+  if (moonbit_bytes_t d = ArrowDirectBuffer(a, col, T_BOOLEAN, P_U8, 1, true)) return d;
+  return ArrowFixed(a, col, 1, true);
+}
 
 void duckdb_mb_arrow_destroy(duckdb_mb_arrow_result *a) { delete a; }  // ref :2548
 int32_t duckdb_mb_is_null_arrow_result(duckdb_mb_arrow_result *a) { return a == nullptr ? 1 : 0; }  // ref :2556

@@ -115,3 +115,32 @@ def test_arrow_device_columns_direct_and_materialized(conn, mbx):
     assert [v for v, ok in zip(vals, valid) if ok] == [i for i in range(5000) if i % 3]
     # int32 getter over BIGINT truncates like the reference's (int32_t) cast (duckdb_native.c:2384-2385)
     assert a.get_column_int32(1)[:3] == [0, 3, 6]
+
+
+def test_arrow_nullable_device_wire_vs_host(conn, mbx):
+    # nullable device columns of every fixed-width getter type: the device wire
+    # kernel (values with NULLs zeroed + validity bytes, one DMA each) and the
+    # host path (after the result was materialised by a string getter) must give
+    # the same bytes, and both the oracle's (duckdb_native.c:2572-2797)
+    n = 5003
+    assert isinstance(conn.query(
+        f"CREATE TABLE anw AS SELECT CASE WHEN i % 3 = 0 THEN NULL ELSE CAST(i - 2500 AS INTEGER) END AS a, "
+        f"CASE WHEN i % 5 = 1 THEN NULL ELSE i * 1000000007 - 3 END AS b, "
+        f"CASE WHEN i % 7 = 2 THEN NULL ELSE CAST(i AS DOUBLE) / 8 END AS d, "
+        f"CASE WHEN i % 4 = 3 THEN NULL ELSE i % 2 = 0 END AS t FROM range({n}) tbl(i)"), mbx.Ok)
+    A = [None if i % 3 == 0 else i - 2500 for i in range(n)]
+    B = [None if i % 5 == 1 else i * 1000000007 - 3 for i in range(n)]
+    D = [None if i % 7 == 2 else i / 8 for i in range(n)]
+    T = [None if i % 4 == 3 else i % 2 == 0 for i in range(n)]
+    want = {"int32": wire.int32, "int64": wire.int64, "double": wire.double, "bool": wire.boolean}
+    cols = {"int32": (0, A), "int64": (1, B), "double": (2, D), "bool": (3, T)}
+    sql = "SELECT a, b, d, t FROM anw"
+    for host_first in (False, True):
+        a = arrow(conn, mbx, sql)
+        if host_first:
+            assert a.get_column_string(0)[:2] == ["", "-2499"]  # materialises on the host
+        for k, (c, vals) in cols.items():
+            for nullable in (True, False):
+                suf = "_nullable" if nullable else ""
+                got = mbx._take(getattr(mbx.lib, f"duckdb_mb_arrow_get_column_{k}{suf}")(a._h, c))
+                assert got == want[k](vals, nullable), (k, nullable, host_first)
