@@ -66,6 +66,7 @@ struct FilterMultiCol {
   int32_t is_pred;  // 1: lo <= x <= lo + span
   int64_t lo;
   uint64_t span;
+  const uint64_t *valid;  // FilterBits only: validity words (NULL fails the predicate); nullptr = no NULLs
 };
 struct FilterMultiDesc {
   int32_t ncol;
@@ -277,6 +278,12 @@ struct CompactDesc {
 void FilterBits(const FilterMultiDesc &d, int64_t nrows, unsigned long long *bits, hipStream_t s);
 // exclusive scan of the steps' selected-row counts (popcounts of their ballot words)
 void ScanStepBits(const unsigned long long *bits, int64_t *offsets, int64_t steps, int64_t *total, hipStream_t s);
+// Validity of the compacted rows: bit offset[step] + rank of every selected
+// row of valid_in (64-bit words, bit r = row r) into valid_out, which must be
+// zeroed (a step's first and last output words are OR'd, shared with its
+// neighbours).
+void CompactValidity(const unsigned long long *bits, const int64_t *step_offsets, int64_t nrows,
+                     const uint64_t *valid_in, uint64_t *valid_out, hipStream_t s);
 void CompactColumns(const CompactDesc &d, int64_t nrows, const unsigned long long *bits, const int64_t *step_offsets,
                     hipStream_t s);
 void RebaseOffsets(const int64_t *src, int64_t *dst, int64_t n, int64_t delta, hipStream_t s);

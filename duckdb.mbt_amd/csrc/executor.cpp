@@ -1010,10 +1010,10 @@ static bool FastIntCol(const DRel &rel, int c) {
   return d.validity == nullptr && (d.phys == P_I32 || d.phys == P_I64) && d.data != nullptr;
 }
 
-// WHERE <range conjunction over NULL-free int columns> with plain NULL-free
-// 4/8-byte output columns: two streaming passes (dev::FilterBits, scan,
-// dev::CompactColumns) instead of vm_filter + scan + vm_project.  MBX_FC=0
-// disables it.
+// WHERE <range conjunction over int columns> with plain 1/2/4/8/16-byte output
+// columns: two streaming passes (dev::FilterBits, scan, dev::CompactColumns,
+// plus dev::CompactValidity per nullable output) instead of vm_filter + scan +
+// vm_project.  A NULL in a predicate column fails the row.  MBX_FC=0 disables it.
 static bool TryFilterCompact(Engine &e, const DRel &rel, const BExpr &pred, const std::vector<BExprPtr> &exprs,
                              DRel &out) {
   const char *fc = getenv("MBX_FC");
@@ -1024,13 +1024,16 @@ static bool TryFilterCompact(Engine &e, const DRel &rel, const BExpr &pred, cons
   memset(&F, 0, sizeof(F));
   F.agg = -1;
   bool empty = false;
+  int ninstr = 0;  // LDS-DMA instructions per 256-row step of FilterBits
   for (auto &kv : ranges) {
-    if (!FastIntCol(rel, kv.first)) return false;
     const DCol &c = rel.cols[kv.first];
+    if (!c.data || (c.phys != P_I32 && c.phys != P_I64)) return false;
     const bool wide = c.phys == P_I64;
-    if ((uintptr_t)c.data % 16) return false;  // 16-B LDS-DMA lanes
+    if ((uintptr_t)c.data % 16 || (uintptr_t)c.validity % 16) return false;  // 16-B LDS-DMA lanes
+    ninstr += (wide ? 2 : 1) + (c.validity ? 1 : 0);
     dev::FilterMultiCol &fc_ = F.col[F.ncol++];
     fc_.data = c.data;
+    fc_.valid = c.validity;
     fc_.phys = c.phys;
     fc_.is_pred = 1;
     const i128 lo = std::max<i128>(kv.second.first, wide ? (i128)INT64_MIN : (i128)INT32_MIN);
@@ -1039,24 +1042,25 @@ static bool TryFilterCompact(Engine &e, const DRel &rel, const BExpr &pred, cons
     fc_.lo = (int64_t)lo;
     fc_.span = lo > hi ? 0 : (uint64_t)(int64_t)hi - (uint64_t)(int64_t)lo;
   }
+  if (ninstr > 8) return false;
   for (auto &x : exprs) {
     if (x->kind != BExpr::COL || (rel.range && x->col == 0)) return false;
     const DCol &c = rel.cols[x->col];
-    if (c.validity || !c.data || c.phys == P_STR) return false;
+    if (!c.data || c.phys == P_STR) return false;
     const int w = PhysSize(c.phys);
     if ((w != 1 && w != 2 && w != 4 && w != 8 && w != 16) || (uintptr_t)c.data % 16) return false;
   }
   out = DRel();
   const int64_t n = rel.n;
   if (empty) {  // nothing passes: typed empty columns
-    for (auto &x : exprs) out.cols.push_back(AllocOut(e, x->type, 0, false));
+    for (auto &x : exprs) out.cols.push_back(AllocOut(e, x->type, 0, rel.cols[x->col].validity != nullptr));
     return true;
   }
   const int64_t steps = (n + 255) / 256;
   auto bits = Alloc(e, (size_t)steps * 32);
   auto offs = Alloc(e, (size_t)(steps + 2) * 8);  // compact reads offsets in 16-B aligned pairs
   double pbytes = 0;
-  for (int j = 0; j < F.ncol; j++) pbytes += (double)n * (F.col[j].phys == P_I64 ? 8 : 4);
+  for (int j = 0; j < F.ncol; j++) pbytes += (double)n * (F.col[j].phys == P_I64 ? 8 : 4) + (F.col[j].valid ? n / 8.0 : 0);
   {
     ProfScope ps(e, "filter_bits", pbytes + (double)steps * 32, n);
     dev::FilterBits(F, n, (unsigned long long *)bits->p, e.stream);
@@ -1065,7 +1069,7 @@ static bool TryFilterCompact(Engine &e, const DRel &rel, const BExpr &pred, cons
   const int64_t nsel = ReadDev<int64_t>(e, e.d_scratch);
   out.n = nsel;
   std::vector<DCol> cols;
-  for (auto &x : exprs) cols.push_back(AllocOut(e, x->type, nsel, false));
+  for (auto &x : exprs) cols.push_back(AllocOut(e, x->type, nsel, rel.cols[x->col].validity != nullptr));
   if (nsel > 0) {
     // output columns in groups of at most 8 LDS-DMA instructions (8 KiB) per 256-row step
     size_t k = 0;
@@ -1088,6 +1092,13 @@ static bool TryFilterCompact(Engine &e, const DRel &rel, const BExpr &pred, cons
       }
       ProfScope ps(e, "compact", bytes, n);
       dev::CompactColumns(C, n, (const unsigned long long *)bits->p, (const int64_t *)offs->p, e.stream);
+    }
+    for (size_t j = 0; j < exprs.size(); j++) {
+      const DCol &c = rel.cols[exprs[j]->col];
+      if (!c.validity) continue;
+      ProfScope ps(e, "compact_validity", (double)steps * 40 + n / 8.0 + nsel / 8.0, n);
+      dev::CompactValidity((const unsigned long long *)bits->p, (const int64_t *)offs->p, n, c.validity,
+                           cols[j].validity, e.stream);
     }
   }
   out.cols = cols;

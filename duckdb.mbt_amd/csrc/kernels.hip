@@ -2444,20 +2444,27 @@ void RebaseOffsets(const int64_t *src, int64_t *dst, int64_t n, int64_t delta, h
 // Both passes here stream with no inter-workgroup waits.
 // ---------------------------------------------------------------------------
 
-// pass 1: NLD KiB of predicate slices per wave step, DEPTH steps in flight
-template <int NLD, int DEPTH>
-__global__ __launch_bounds__(256) void filter_bits_lds_kernel(FilterMultiDesc D, int64_t n, unsigned long long *bits) {
+// pass 1: NI LDS-DMA instructions per wave step (1 per KiB of predicate
+// slices, 1 per nullable column for its 4 validity words), DEPTH steps in flight
+template <int NI, int DEPTH>
+__global__ __launch_bounds__(256) void filter_bits_lds_kernel(FilterMultiDesc D, int64_t n, unsigned long long *bits,
+                                                              int slot_bytes) {
   extern __shared__ __attribute__((aligned(16))) unsigned char fb_lds[];
-  constexpr int SB = NLD * 1024;
+  const int SB = slot_bytes;
   const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
   unsigned char *ring = fb_lds + (size_t)w * DEPTH * SB;
-  int off[FM_MAX];
+  int off[FM_MAX], voff[FM_MAX];
   {
     int o = 0;
 #pragma unroll
     for (int c = 0; c < FM_MAX; c++) {
       off[c] = o;
       if (c < D.ncol) o += D.col[c].phys == P_I64 ? 2048 : 1024;
+    }
+#pragma unroll
+    for (int c = 0; c < FM_MAX; c++) {
+      voff[c] = o;
+      if (c < D.ncol && D.col[c].valid) o += 32;
     }
   }
   const int64_t nsteps = n >> 8;
@@ -2473,6 +2480,10 @@ __global__ __launch_bounds__(256) void filter_bits_lds_kernel(FilterMultiDesc D,
       __builtin_amdgcn_global_load_lds((const void *)(src + lane * 16), (void *)(dst + off[c]), 16, 0, 2);
       if (B == 2048)
         __builtin_amdgcn_global_load_lds((const void *)(src + 1024 + lane * 16), (void *)(dst + off[c] + 1024), 16, 0, 2);
+      // the step's 4 validity words: lanes 0-1, 16 B each (exec-masked, still one vmcnt)
+      if (D.col[c].valid && lane < 2)
+        __builtin_amdgcn_global_load_lds((const void *)(D.col[c].valid + q * 4 + lane * 2), (void *)(dst + voff[c]), 16,
+                                         0, 0);
     }
   };
   // one step's 4 ballot words: lanes 0..3 store a word each (32 contiguous bytes)
@@ -2492,9 +2503,10 @@ __global__ __launch_bounds__(256) void filter_bits_lds_kernel(FilterMultiDesc D,
   }
   int k = 0;
   for (; st < nsteps; st += nw) {
-    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NLD * (DEPTH - 1)) : "memory");
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NI * (DEPTH - 1)) : "memory");
     const unsigned char *src = ring + k * SB;
     int64_t v[FM_MAX][4];
+    unsigned vm = 0xFu;  // rows 4 lane + e whose predicate columns are all non-NULL
 #pragma unroll
     for (int c = 0; c < FM_MAX; c++) {
       if (c >= D.ncol) break;
@@ -2505,6 +2517,8 @@ __global__ __launch_bounds__(256) void filter_bits_lds_kernel(FilterMultiDesc D,
         v4i32 x = *(const v4i32 *)(src + off[c] + lane * 16);
         v[c][0] = x.x; v[c][1] = x.y; v[c][2] = x.z; v[c][3] = x.w;
       }
+      if (D.col[c].valid)
+        vm &= (unsigned)(*(const uint64_t *)(src + voff[c] + (lane >> 4) * 8) >> (4 * (lane & 15))) & 0xFu;
     }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     int64_t q = st + DEPTH * nw;
@@ -2512,7 +2526,7 @@ __global__ __launch_bounds__(256) void filter_bits_lds_kernel(FilterMultiDesc D,
     bool ok[4];
 #pragma unroll
     for (int e = 0; e < 4; e++) {
-      ok[e] = true;
+      ok[e] = (vm >> e) & 1u;
 #pragma unroll
       for (int c = 0; c < FM_MAX; c++)
         if (c < D.ncol) ok[e] = ok[e] && (uint64_t)(v[c][e] - D.col[c].lo) <= D.col[c].span;
@@ -2531,7 +2545,8 @@ __global__ __launch_bounds__(256) void filter_bits_lds_kernel(FilterMultiDesc D,
       for (int c = 0; c < D.ncol && ok[e]; c++) {
         const int64_t x = D.col[c].phys == P_I64 ? ((const int64_t *)D.col[c].data)[i]
                                                  : (int64_t)((const int32_t *)D.col[c].data)[i];
-        ok[e] = (uint64_t)(x - D.col[c].lo) <= D.col[c].span;
+        ok[e] = (uint64_t)(x - D.col[c].lo) <= D.col[c].span &&
+                (!D.col[c].valid || ((D.col[c].valid[i >> 6] >> (i & 63)) & 1));
       }
     }
     emit(nsteps, ok);
@@ -2540,8 +2555,16 @@ __global__ __launch_bounds__(256) void filter_bits_lds_kernel(FilterMultiDesc D,
 
 void FilterBits(const FilterMultiDesc &d, int64_t nrows, unsigned long long *bits, hipStream_t s) {
   if (nrows <= 0) return;
-  int nld = 0;
-  for (int c = 0; c < d.ncol; c++) nld += d.col[c].phys == P_I64 ? 2 : 1;
+  int ni = 0, slot = 0;
+  for (int c = 0; c < d.ncol; c++) {
+    ni += d.col[c].phys == P_I64 ? 2 : 1;
+    slot += d.col[c].phys == P_I64 ? 2048 : 1024;
+    if (d.col[c].valid) {
+      ni++;
+      slot += 32;
+    }
+  }
+  slot = (slot + 15) & ~15;
   int gpc = 3;
   if (const char *e = getenv("MBX_FB_BLOCKS_PER_CU")) gpc = atoi(e) > 0 ? atoi(e) : 3;
   int grid = NumCUs() * gpc;
@@ -2549,12 +2572,12 @@ void FilterBits(const FilterMultiDesc &d, int64_t nrows, unsigned long long *bit
   if (grid > need) grid = (int)need;
   int dp = 0;  // MBX_FB_DEPTH: ring depth override (sweeps)
   if (const char *e = getenv("MBX_FB_DEPTH")) dp = atoi(e);
-#define FB(L, DP)                                                                                          \
-  hipLaunchKernelGGL((filter_bits_lds_kernel<L, DP>), dim3(grid), dim3(256), (size_t)4 * DP * L * 1024, s, d, \
-                     nrows, bits)
+#define FB(L, DP)                                                                                           \
+  hipLaunchKernelGGL((filter_bits_lds_kernel<L, DP>), dim3(grid), dim3(256), (size_t)4 * DP * slot, s, d, \
+                     nrows, bits, slot)
 #define FBD(L, DEF) \
   if ((dp ? dp : DEF) <= 2) FB(L, 2); else if ((dp ? dp : DEF) <= 3) FB(L, 3); else if ((dp ? dp : DEF) <= 4) FB(L, 4); else FB(L, 6);
-  switch (nld) {
+  switch (ni) {  // the executor keeps ni <= 8
     case 1: FBD(1, 6); break;
     case 2: FBD(2, 3); break;
     case 3: FBD(3, 2); break;
@@ -2566,6 +2589,114 @@ void FilterBits(const FilterMultiDesc &d, int64_t nrows, unsigned long long *bit
   }
 #undef FBD
 #undef FB
+  CHECK_LAUNCH();
+}
+
+// Validity of the compacted rows.  A wave owns a chunk of CV_CHUNK consecutive
+// 256-row steps and prefetches the chunk's ballot words, validity words and
+// step offsets with one load each per lane.  Per step, each lane writes the
+// validity bytes of its selected rows (rows 4 lane + e) at their rank into the
+// wave's 256-byte LDS staging row; four ballots over the staged bytes give the
+// step's 256-bit run of output validity (run word q = ballot of bytes 64 q + lane).
+// The run lands at bit offset[step] of the output through a carry word kept
+// across the chunk's steps, so output words are written once with plain
+// stores; only a chunk's first word (when a previous chunk may share it) and
+// its final carry are ORed atomically: device-scope atomics leave the XCD's L2
+// and are slow, so they are kept to about two per chunk.
+#define CV_CHUNK 32
+__device__ __forceinline__ uint64_t readlane64(uint64_t x, int l) {
+  const uint32_t lo = __builtin_amdgcn_readlane((int)(uint32_t)x, l);
+  const uint32_t hi = __builtin_amdgcn_readlane((int)(uint32_t)(x >> 32), l);
+  return (uint64_t)hi << 32 | lo;
+}
+
+__global__ __launch_bounds__(256) void compact_validity_kernel(const unsigned long long *bits, const int64_t *offs,
+                                                               int64_t n, const uint64_t *vin, uint64_t *vout) {
+  __shared__ __attribute__((aligned(16))) uint8_t stage_lds[4][256];
+  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  uint8_t *stage = stage_lds[w];
+  const uint64_t lt = (1ull << lane) - 1;
+  const int64_t steps = (n + 255) >> 8, nwords = (n + 63) >> 6;
+  const int64_t nchunks = (steps + CV_CHUNK - 1) / CV_CHUNK;
+  for (int64_t ch = (int64_t)blockIdx.x * 4 + w; ch < nchunks; ch += (int64_t)gridDim.x * 4) {
+    const int64_t s0 = ch * CV_CHUNK;
+    // the chunk's 4 x 32 ballot words and validity words: 2 of each per lane
+    const int64_t bw = 4 * s0 + 2 * lane;
+    const bool in0 = bw < 4 * steps, in1 = bw + 1 < 4 * steps;
+    const uint64_t pb0 = in0 ? bits[bw] : 0, pb1 = in1 ? bits[bw + 1] : 0;
+    const uint64_t pv0 = bw < nwords ? vin[bw] : 0, pv1 = bw + 1 < nwords ? vin[bw + 1] : 0;
+    const int64_t po = lane < CV_CHUNK && s0 + lane < steps ? offs[s0 + lane] : 0;
+    int64_t carry_idx = -1, first_word = -1;
+    uint64_t carry_val = 0;
+    bool first_shared = false;
+    auto put = [&](int64_t W, uint64_t val) {  // one complete (or final) output word
+      if (W == first_word && first_shared) {
+        if (val) atomicOr((unsigned long long *)&vout[W], (unsigned long long)val);
+      } else {
+        vout[W] = val;
+      }
+    };
+    for (int j = 0; j < CV_CHUNK && s0 + j < steps; j++) {
+      const uint64_t b0 = readlane64(pb0, 2 * j), b1 = readlane64(pb1, 2 * j);
+      const uint64_t b2 = readlane64(pb0, 2 * j + 1), b3 = readlane64(pb1, 2 * j + 1);
+      const int cnt = __popcll(b0) + __popcll(b1) + __popcll(b2) + __popcll(b3);
+      if (cnt == 0) continue;  // wave-uniform
+      const int64_t o = readlane64((uint64_t)po, j);
+      // this lane's validity word: chunk word 4 j + (lane >> 4), held by lane (4 j + (lane >> 4)) / 2
+      const int src = (4 * j + (lane >> 4)) >> 1;
+      const uint64_t v0 = __shfl(pv0, src), v1 = __shfl(pv1, src);
+      const uint64_t vword = ((lane >> 4) & 1) ? v1 : v0;
+      const unsigned m = (unsigned)((b0 >> lane) & 1) | (unsigned)((b1 >> lane) & 1) << 1 |
+                         (unsigned)((b2 >> lane) & 1) << 2 | (unsigned)((b3 >> lane) & 1) << 3;
+      const int r0 = __popcll(b0 & lt) + __popcll(b1 & lt) + __popcll(b2 & lt) + __popcll(b3 & lt);
+      const unsigned vb = (unsigned)(vword >> (4 * (lane & 15))) & 0xFu;
+      int r = r0;
+#pragma unroll
+      for (int e = 0; e < 4; e++)
+        if ((m >> e) & 1u) stage[r++] = (uint8_t)((vb >> e) & 1u);
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      uint64_t R[4];  // run word q, bit i = staged byte 64 q + i
+#pragma unroll
+      for (int qw = 0; qw < 4; qw++) R[qw] = __ballot(64 * qw + lane < cnt && stage[64 * qw + lane]);
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // staging reads done before the next step's writes
+      const int64_t w0 = o >> 6, w1 = (o + cnt - 1) >> 6;
+      if (first_word < 0) {
+        first_word = w0;
+        first_shared = (o & 63) != 0;
+      }
+      if (carry_idx >= 0 && carry_idx != w0) {  // the carry word is complete
+        if (lane == 0) put(carry_idx, carry_val);
+        carry_idx = -1;
+      }
+      const int64_t W = w0 + lane;
+      uint64_t val = 0;
+      if (lane <= 4 && W <= w1) {
+        const int64_t sh = 64 * W - o;  // run bit at output bit 64 W; in [-63, 256)
+        if (sh < 0) {
+          val = R[0] << (-sh);
+        } else {
+          const int qw = (int)(sh >> 6), rb = (int)(sh & 63);
+          const uint64_t a0 = qw == 0 ? R[0] : qw == 1 ? R[1] : qw == 2 ? R[2] : R[3];
+          const uint64_t a1 = qw == 0 ? R[1] : qw == 1 ? R[2] : qw == 2 ? R[3] : 0;
+          val = rb ? (a0 >> rb) | (a1 << (64 - rb)) : a0;
+        }
+        if (W == carry_idx) val |= carry_val;
+        if (W < w1) put(W, val);
+      }
+      carry_val = readlane64(val, (int)(w1 - w0));
+      carry_idx = w1;
+    }
+    if (carry_idx >= 0 && lane == 0 && carry_val)  // the next chunk may share it
+      atomicOr((unsigned long long *)&vout[carry_idx], (unsigned long long)carry_val);
+  }
+}
+
+void CompactValidity(const unsigned long long *bits, const int64_t *step_offsets, int64_t nrows,
+                     const uint64_t *valid_in, uint64_t *valid_out, hipStream_t s) {
+  if (nrows <= 0) return;
+  const int64_t chunks = ((nrows + 255) >> 8) / CV_CHUNK + 1;
+  hipLaunchKernelGGL(compact_validity_kernel, dim3(GridFor(chunks, 4, NumCUs() * 8)), dim3(256), 0, s, bits,
+                     step_offsets, nrows, valid_in, valid_out);
   CHECK_LAUNCH();
 }
 

@@ -131,3 +131,55 @@ def test_filter_compact_profile_and_stream(conn, oracle):
     st.close()
     assert got == v[m].tolist()
     q(conn, "SELECT COUNT(*) FROM (SELECT v FROM fc WHERE x > 24) t")
+
+
+def _ncol(conn, sql, kind, idx=0):
+    # nullable wire buffer -> (values with NULLs zeroed, validity)
+    a = conn.query_arrow(sql).value
+    b = a._buf(kind, idx, nullable=True)
+    a.close()
+    n = int.from_bytes(b[:4], "little", signed=True) if len(b) >= 4 else 0
+    w = 8 if kind == "int64" else 4
+    vals = np.frombuffer(b[4:4 + n * w], dtype=np.int64 if w == 8 else np.int32)
+    return vals, np.frombuffer(b[4 + n * w:4 + n * (w + 1)], dtype=np.uint8).astype(bool)
+
+
+@pytest.mark.parametrize("n", [1, 63, 64, 255, 257, 4097, 70_001, 1_000_003])
+def test_filter_compact_nullable(mbx, oracle, monkeypatch, n):
+    """NULLs in predicate columns (a NULL fails the row) and in output columns
+    (validity bits compacted by compact_validity) on the two-pass path: values
+    and validity exact vs numpy and vs the VM path (MBX_FC=0)."""
+    cfg = mbx.Config.create()
+    cfg.set("mbx_profile", "true")
+    c = mbx.connect_with_config(cfg).value
+    q(c, f"CREATE TABLE fn AS SELECT mbx_synth(42, i, 50) + 1 AS x, "
+         f"CASE WHEN mbx_synth(13, i, 10) = 0 THEN NULL ELSE mbx_synth(42, i, 50) + 1 END AS xn, "
+         f"CASE WHEN mbx_synth(17, i, 3) = 0 THEN NULL ELSE CAST(mbx_synth(7, i, 32) AS INTEGER) END AS kn, "
+         f"CASE WHEN mbx_synth(19, i, 7) = 0 THEN NULL ELSE mbx_synth(9, i, 1099511627776) - 549755813888 END AS vn "
+         f"FROM range({n}) tbl(i)")
+    x = oracle.synth_i64(n, 42, 0, 50, 1)
+    xv = oracle.synth_i64(n, 13, 0, 10, 0) != 0
+    k = oracle.synth_i64(n, 7, 0, 32, 0)
+    kv = oracle.synth_i64(n, 17, 0, 3, 0) != 0
+    v = oracle.synth_i64(n, 9, 0, 2**40, -2**39)
+    vv = oracle.synth_i64(n, 19, 0, 7, 0) != 0
+    cases = [
+        ("SELECT vn FROM fn WHERE xn > 24", xv & (x > 24), [("int64", v, vv)]),
+        ("SELECT vn, kn FROM fn WHERE x > 24", x > 24, [("int64", v, vv), ("int32", k, kv)]),
+        ("SELECT kn, x FROM fn WHERE xn > 24 AND kn < 16", xv & (x > 24) & kv & (k < 16),
+         [("int32", k, kv), ("int64", x, np.ones(n, bool))]),
+    ]
+    for sql, m, cols in cases:
+        for i, (kind, arr, valid) in enumerate(cols):
+            got, ok = _ncol(c, sql, kind, i)
+            names = [kk["name"] for kk in c.last_profile()["kernels"]]
+            assert "filter_bits" in names, (sql, names)
+            if i == 0 and not valid.all() and m.any():
+                assert "compact_validity" in names, (sql, names)
+            assert np.array_equal(ok, valid[m]), (n, sql, i)
+            assert np.array_equal(got, np.where(valid[m], arr[m], 0).astype(got.dtype)), (n, sql, i)
+            monkeypatch.setenv("MBX_FC", "0")
+            got2, ok2 = _ncol(c, sql, kind, i)
+            monkeypatch.delenv("MBX_FC")
+            assert np.array_equal(ok2, ok) and np.array_equal(got2, got), (n, sql, i)
+    c.close()

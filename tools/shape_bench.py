@@ -16,8 +16,12 @@ n = int(sys.argv[1]) if len(sys.argv) > 1 else 100_000_000
 cfg = m.Config.create()
 cfg.set("mbx_profile", "true")
 c = m.connect_with_config(cfg).value
+# NULLABLE=1 adds NULL-able twins of x and v (10 % / 14 % NULLs) for the seln_* shapes
+extra = (", CASE WHEN mbx_synth(13, i, 10) = 0 THEN NULL ELSE mbx_synth(42, i, 50) + 1 END AS xn, "
+         "CASE WHEN mbx_synth(19, i, 7) = 0 THEN NULL ELSE mbx_synth(9, i, 1099511627776) - 549755813888 END AS vn"
+         if os.environ.get("NULLABLE") else "")
 c.query(f"CREATE TABLE t AS SELECT CAST(mbx_synth(7, i, 32) AS INTEGER) AS k, CAST(mbx_synth(8, i, 4) AS INTEGER) AS k2, "
-        f"mbx_synth(9, i, 1099511627776) - 549755813888 AS v, mbx_synth(42, i, 50) + 1 AS x FROM range({n}) tbl(i)")
+        f"mbx_synth(9, i, 1099511627776) - 549755813888 AS v, mbx_synth(42, i, 50) + 1 AS x{extra} FROM range({n}) tbl(i)")
 shapes = {
     "c2_count": "SELECT COUNT(*) FROM t WHERE x > 24",
     "c3": "SELECT k, SUM(v), COUNT(*) FROM t GROUP BY k",
@@ -39,6 +43,10 @@ shapes = {
     "compact": "CREATE OR REPLACE TABLE tc AS SELECT x FROM t WHERE x > 24",
     "compact2": "CREATE OR REPLACE TABLE tc AS SELECT k, v FROM t WHERE x > 24",
     "compact_expr": "CREATE OR REPLACE TABLE tc AS SELECT v + x AS y FROM t WHERE x > 24 AND k < 16",
+    # NULLABLE=1: a NULL-able predicate column, NULL-able outputs
+    "seln_pred": "STREAM SELECT v FROM t WHERE xn > 24",
+    "seln_out": "STREAM SELECT vn FROM t WHERE x > 24",
+    "seln_both": "STREAM SELECT vn FROM t WHERE xn > 24 AND k < 16",
 }
 if os.environ.get("SHAPES"):
     shapes = {k: v for k, v in shapes.items() if k in os.environ["SHAPES"].split(",")}
