@@ -1334,27 +1334,52 @@ static DRel HashAggregate(Engine &e, const DRel &tmp, const BoundSelect &s, cons
 // (or one predicate column of another width than the aggregated column),
 // aggregates over one int column or COUNT(*): one LDS-DMA pass over all the
 // columns (filter_multi_lds).  The single-column shape stays on F1.
+// NULL-able columns take this kernel too (their validity words ride the ring):
+// a NULL fails a predicate; a NULL-able aggregated column that carries no
+// predicate is admitted only without COUNT(*), so that "every NULL-able column
+// valid" is exactly the set of rows each aggregate sees.
+static bool FmIntCol(const DRel &rel, int c) {
+  if (rel.range && c == 0) return false;
+  const DCol &d = rel.cols[c];
+  return d.data && (d.phys == P_I32 || d.phys == P_I64) && (uintptr_t)d.data % 16 == 0 &&
+         (uintptr_t)d.validity % 16 == 0;
+}
+
 static bool FilterMultiAggregate(Engine &e, const DRel &src, const BoundSelect &s, DRel &out) {
   if (!s.where || src.n <= 0) return false;
   std::map<int, std::pair<i128, i128>> ranges;
   if (!RangeConj(*s.where, ranges)) return false;
   int acol = -1;
-  bool need_mm = false;
+  bool need_mm = false, count_star = false;
   for (auto &a : s.aggs) {
-    if (a.kind == A_COUNT_STAR) continue;
+    if (a.kind == A_COUNT_STAR) {
+      count_star = true;
+      continue;
+    }
     if (a.distinct) return false;
     const BExpr *x = a.arg ? StripWidening(a.arg.get()) : nullptr;
-    if (!x || x->kind != BExpr::COL || !FastIntCol(src, x->col)) return false;
+    if (!x || x->kind != BExpr::COL || !FmIntCol(src, x->col)) return false;
     if (a.arg->type.id == T_DOUBLE || a.arg->type.id == T_FLOAT) return false;
     if (acol >= 0 && acol != x->col) return false;
     acol = x->col;
     need_mm |= a.kind == A_MIN || a.kind == A_MAX;
   }
-  for (auto &kv : ranges)
-    if (!FastIntCol(src, kv.first)) return false;
+  bool nullable = false;
+  int ninstr = 0;
+  for (auto &kv : ranges) {
+    if (!FmIntCol(src, kv.first)) return false;
+    nullable |= src.cols[kv.first].validity != nullptr;
+    ninstr += (src.cols[kv.first].phys == P_I64 ? 2 : 1) + (src.cols[kv.first].validity ? 1 : 0);
+  }
+  if (acol >= 0 && !ranges.count(acol)) {
+    if (src.cols[acol].validity && count_star) return false;
+    nullable |= src.cols[acol].validity != nullptr;
+    ninstr += (src.cols[acol].phys == P_I64 ? 2 : 1) + (src.cols[acol].validity ? 1 : 0);
+  }
+  if (ninstr > 8) return false;
   const bool single = ranges.size() == 1 && (acol < 0 || acol == ranges.begin()->first ||
                                              src.cols[acol].phys == src.cols[ranges.begin()->first].phys);
-  if (single) return false;  // F1 proper
+  if (single && !nullable) return false;  // F1 proper
   dev::FilterMultiDesc d;
   memset(&d, 0, sizeof(d));
   d.agg = -1;
@@ -1365,12 +1390,13 @@ static bool FilterMultiAggregate(Engine &e, const DRel &src, const BoundSelect &
     dev::FilterMultiCol &c = d.col[d.ncol];
     c.data = src.cols[kv.first].data;
     c.phys = src.cols[kv.first].phys;
+    c.valid = src.cols[kv.first].validity;
     c.is_pred = 1;
     if (lo > hi) return false;  // an empty range: the generic path answers it
     c.lo = (int64_t)lo;
     c.span = (uint64_t)(int64_t)hi - (uint64_t)(int64_t)lo;
     if (kv.first == acol) d.agg = d.ncol;
-    bytes += (double)src.n * PhysSize(src.cols[kv.first].phys);
+    bytes += (double)src.n * PhysSize(src.cols[kv.first].phys) + (c.valid ? src.n / 8.0 : 0);
     d.ncol++;
   }
   if (acol >= 0 && d.agg < 0) {
@@ -1378,9 +1404,10 @@ static bool FilterMultiAggregate(Engine &e, const DRel &src, const BoundSelect &
     dev::FilterMultiCol &c = d.col[d.ncol];
     c.data = src.cols[acol].data;
     c.phys = src.cols[acol].phys;
+    c.valid = src.cols[acol].validity;
     c.is_pred = 0;
     d.agg = d.ncol++;
-    bytes += (double)src.n * PhysSize(src.cols[acol].phys);
+    bytes += (double)src.n * PhysSize(src.cols[acol].phys) + (c.valid ? src.n / 8.0 : 0);
   }
   d.mm = need_mm;
   uint64_t maxabs = ~0ull;

@@ -634,22 +634,31 @@ __global__ __launch_bounds__(256) void filter_agg_lds_kernel(const T *__restrict
 
 // Multi-column version of the LDS-DMA filter-aggregate.  A wave step covers
 // 256 consecutive rows; each column's slice (1 KiB for int32, 2 KiB for
-// int64) lands in the wave's ring slot through global_load_lds, NLD KiB per
-// step in total (compile-time, so the counted vmcnt wait is exact); each lane
-// then owns 4 consecutive rows of every column.
-template <int NLD, int DEPTH>
-__global__ __launch_bounds__(256) void filter_multi_lds_kernel(FilterMultiDesc D, int64_t n, AggPartial *partials) {
+// int64) lands in the wave's ring slot through global_load_lds; each lane
+// then owns 4 consecutive rows of every column.  A NULL-able column adds its
+// step's 4 validity words (one exec-masked LDS-DMA instruction); a row counts
+// only where every such column is non-NULL (the host admits a NULL-able
+// aggregated column only where that is the SQL answer).  NI = LDS-DMA
+// instructions per step (compile time: the counted vmcnt wait).
+template <int NI, int DEPTH>
+__global__ __launch_bounds__(256) void filter_multi_lds_kernel(FilterMultiDesc D, int64_t n, AggPartial *partials,
+                                                               int slot_bytes) {
   extern __shared__ __attribute__((aligned(16))) unsigned char fm_lds[];
-  constexpr int SB = NLD * 1024;
+  const int SB = slot_bytes;
   const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
   unsigned char *ring = fm_lds + (size_t)w * DEPTH * SB;
-  int off[FM_MAX];
+  int off[FM_MAX], voff[FM_MAX];
   {
     int o = 0;
 #pragma unroll
     for (int c = 0; c < FM_MAX; c++) {
       off[c] = o;
       if (c < D.ncol) o += D.col[c].phys == P_I64 ? 2048 : 1024;
+    }
+#pragma unroll
+    for (int c = 0; c < FM_MAX; c++) {
+      voff[c] = o;
+      if (c < D.ncol && D.col[c].valid) o += 32;
     }
   }
   const int64_t nsteps = n >> 8;
@@ -665,6 +674,9 @@ __global__ __launch_bounds__(256) void filter_multi_lds_kernel(FilterMultiDesc D
       __builtin_amdgcn_global_load_lds((const void *)(src + lane * 16), (void *)(dst + off[c]), 16, 0, 2);
       if (B == 2048)
         __builtin_amdgcn_global_load_lds((const void *)(src + 1024 + lane * 16), (void *)(dst + off[c] + 1024), 16, 0, 2);
+      if (D.col[c].valid && lane < 2)
+        __builtin_amdgcn_global_load_lds((const void *)(D.col[c].valid + q * 4 + lane * 2), (void *)(dst + voff[c]), 16,
+                                         0, 0);
     }
   };
   Acc A;
@@ -679,9 +691,10 @@ __global__ __launch_bounds__(256) void filter_multi_lds_kernel(FilterMultiDesc D
   }
   int k = 0;
   for (; st < nsteps; st += nw) {
-    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NLD * (DEPTH - 1)) : "memory");
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NI * (DEPTH - 1)) : "memory");
     const unsigned char *src = ring + k * SB;
     int64_t v[FM_MAX][4];
+    unsigned vm = 0xFu;  // rows 4 lane + e where every NULL-able column is valid
 #pragma unroll
     for (int c = 0; c < FM_MAX; c++) {
       if (c >= D.ncol) break;
@@ -692,13 +705,15 @@ __global__ __launch_bounds__(256) void filter_multi_lds_kernel(FilterMultiDesc D
         v4i32 x = *(const v4i32 *)(src + off[c] + lane * 16);
         v[c][0] = x.x; v[c][1] = x.y; v[c][2] = x.z; v[c][3] = x.w;
       }
+      if (D.col[c].valid)
+        vm &= (unsigned)(*(const uint64_t *)(src + voff[c] + (lane >> 4) * 8) >> (4 * (lane & 15))) & 0xFu;
     }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     int64_t q = st + DEPTH * nw;
     issue(q < nsteps ? q : st, k);
 #pragma unroll
     for (int e = 0; e < 4; e++) {
-      bool ok = true;
+      bool ok = (vm >> e) & 1u;
 #pragma unroll
       for (int c = 0; c < FM_MAX; c++)
         if (c < D.ncol && D.col[c].is_pred) ok = ok && (uint64_t)(v[c][e] - D.col[c].lo) <= D.col[c].span;
@@ -719,6 +734,7 @@ __global__ __launch_bounds__(256) void filter_multi_lds_kernel(FilterMultiDesc D
       for (int c = 0; c < D.ncol; c++) {
         int64_t x = D.col[c].phys == P_I64 ? ((const int64_t *)D.col[c].data)[i] : (int64_t)((const int32_t *)D.col[c].data)[i];
         if (D.col[c].is_pred) ok = ok && (uint64_t)(x - D.col[c].lo) <= D.col[c].span;
+        if (D.col[c].valid) ok = ok && ((D.col[c].valid[i >> 6] >> (i & 63)) & 1);
         if (c == D.agg) val = x;
       }
       if (D.agg < 0) acc_count(A, ok);
@@ -740,8 +756,16 @@ __global__ __launch_bounds__(256) void filter_multi_lds_kernel(FilterMultiDesc D
 
 int FilterMultiPartials(const FilterMultiDesc &d_in, int64_t nrows, AggPartial *partials, hipStream_t s) {
   FilterMultiDesc d = d_in;
-  int nld = 0;
-  for (int c = 0; c < d.ncol; c++) nld += d.col[c].phys == P_I64 ? 2 : 1;
+  int nld = 0, slot = 0;  // nld: LDS-DMA instructions per step (the executor keeps it <= 8)
+  for (int c = 0; c < d.ncol; c++) {
+    nld += d.col[c].phys == P_I64 ? 2 : 1;
+    slot += d.col[c].phys == P_I64 ? 2048 : 1024;
+    if (d.col[c].valid) {
+      nld++;
+      slot += 32;
+    }
+  }
+  slot = (slot + 15) & ~15;
   // 3 blocks per CU: 3.39 ms vs 3.79 at 2 for 1e9 rows of (x i64, k i32,
   // v i64), equal at 1e8 (profiles/r01_filter_multi_sweep.log)
   int gpc = 3;
@@ -759,8 +783,8 @@ int FilterMultiPartials(const FilterMultiDesc &d_in, int64_t nrows, AggPartial *
                (unsigned __int128)d.maxabs * rows_per_lane < ((unsigned __int128)1 << 63);
   }
 #define FM(L, DP)                                                                                            \
-  hipLaunchKernelGGL((filter_multi_lds_kernel<L, DP>), dim3(grid), dim3(256), (size_t)4 * DP * L * 1024, s, d, nrows, \
-                     partials)
+  hipLaunchKernelGGL((filter_multi_lds_kernel<L, DP>), dim3(grid), dim3(256), (size_t)4 * DP * slot, s, d, nrows, \
+                     partials, slot)
   // MBX_FM_DEPTH=<2..4>: ring depth for 3..5 loads per step (sweeps)
   int dp = 2;
   if (const char *ed = getenv("MBX_FM_DEPTH")) dp = atoi(ed) >= 2 && atoi(ed) <= 4 ? atoi(ed) : 2;

@@ -47,12 +47,23 @@ shapes = {
     "seln_pred": "STREAM SELECT v FROM t WHERE xn > 24",
     "seln_out": "STREAM SELECT vn FROM t WHERE x > 24",
     "seln_both": "STREAM SELECT vn FROM t WHERE xn > 24 AND k < 16",
+    "c2n": "SELECT COUNT(*) FROM t WHERE xn > 24",
+    "c5n": "SELECT COUNT(*), SUM(xn) FROM t WHERE xn > 24",
+    "c5n_sumv": "SELECT COUNT(vn), SUM(vn) FROM t WHERE x > 24",
+    "c3n": "SELECT k, SUM(vn), COUNT(*) FROM t GROUP BY k",
+    "c3n_where": "SELECT k, SUM(v), COUNT(*) FROM t WHERE xn > 24 GROUP BY k",
 }
 if os.environ.get("SHAPES"):
     shapes = {k: v for k, v in shapes.items() if k in os.environ["SHAPES"].split(",")}
 out = {}
 for name, sql in shapes.items():
     walls, kern = [], []
+    if os.environ.get("JIT_WAIT"):  # let a run-time compiled kernel finish building first
+        try:
+            (c.query_stream(sql[7:]).value if sql.startswith("STREAM ") else c.query_raw(sql)).close()
+        except Exception:  # noqa: BLE001
+            pass
+        time.sleep(float(os.environ["JIT_WAIT"]))
     for i in range(5):
         t0 = time.perf_counter()
         try:
