@@ -14,7 +14,7 @@ and the global COUNT is combined with an RCCL all-reduce inside the timed
 step.  Scaling is weak (fixed rows per GPU); value = total rows / max time.
 
 Usage: python bench.py [--gpus N] [--steps K] [--warmup W] [--rows R]
-                       [--config c2|c3] [--no-cpu] [--profile-steps]
+                       [--config c1|c2|c2d|c3|c4|c5] [--no-cpu] [--profile-steps]
 """
 import argparse
 import json
@@ -47,7 +47,7 @@ def main():
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--rows", type=int, default=1_000_000_000)
-    ap.add_argument("--config", default="c2", choices=["c1", "c2", "c3", "c4", "c5"])
+    ap.add_argument("--config", default="c2", choices=["c1", "c2", "c2d", "c3", "c4", "c5"])
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
@@ -92,8 +92,10 @@ def main():
         return bench_c1()
     if args.config == "c4":
         return bench_c4(mbx, conn, min(n, 100_000_000), args)
-    if args.config in ("c2", "c5"):
-        setup = (f"CREATE TABLE t AS SELECT mbx_synth(42, i, 50) + 1 AS x "
+    c2like = args.config in ("c2", "c2d")  # c2d: C2 over DECIMAL(15,2) (raw = 100 x; x > 24 is raw > 2400)
+    if args.config in ("c2", "c2d", "c5"):
+        xexpr = "CAST(mbx_synth(42, i, 50) + 1 AS DECIMAL(15,2))" if args.config == "c2d" else "mbx_synth(42, i, 50) + 1"
+        setup = (f"CREATE TABLE t AS SELECT {xexpr} AS x "
                  f"FROM range({start}, {start + n}) tbl(i)")
         sql = "SELECT COUNT(*) FROM t WHERE x > 24"
         if args.config == "c5":
@@ -102,6 +104,8 @@ def main():
         bytes_per_row = 8
         workload = ("C2: SELECT COUNT(*) FROM t WHERE x > 24 over a device-resident 1e9-row INT64 column per GPU"
                     if args.config == "c2" else
+                    "C2 DECIMAL(15,2) variant: SELECT COUNT(*) FROM t WHERE x > 24 (raw int64 > 2400) per GPU"
+                    if args.config == "c2d" else
                     "C5: SELECT COUNT(*), SUM(x) FROM t WHERE x > 24, rows sharded per GPU")
     else:
         setup = (f"CREATE TABLE t AS SELECT CAST(mbx_synth(7, i, 32) AS INTEGER) AS k, "
@@ -139,7 +143,7 @@ def main():
         # collected inside the timed region (finish_combines).
         if world == 1:
             return None
-        if args.config == "c2":
+        if c2like:
             return mbx_dist.allreduce_count_async(int(out[0]), device=coll_dev)  # RCCL over xGMI: COUNT(*)
         if args.config == "c5":
             return mbx_dist.global_count_sum_async(int(out[0]), int(out[1]) if out[1] else None, device=coll_dev)
@@ -151,7 +155,7 @@ def main():
             if p is None:
                 continue
             r = p.result() if hasattr(p, "result") else p
-            if args.config == "c2":
+            if c2like:
                 gcount = r
             elif args.config == "c5":
                 gcount, gsum = r
@@ -184,7 +188,7 @@ def main():
 
     # parity: the GPU answer for this shard against the CPU oracle (full size)
     parity = None
-    if args.config in ("c2", "c5"):
+    if args.config in ("c2", "c2d", "c5"):
         sys.path.insert(0, HERE)
         from oracle import Oracle  # test infrastructure: checker only
         orc = Oracle()
@@ -246,7 +250,8 @@ def main():
             "dtype": "int64",
             "data": ("synthetic: k = splitmix64(7 + i) mod 32 (INT32), v = splitmix64(9 + i) mod 2^40 - 2^39 (INT64), "
                      "generated on device (no dataset)" if args.config == "c3" else
-                     "synthetic: x = splitmix64(42 + i) mod 50 + 1 generated on device (no dataset)"),
+                     "synthetic: x = splitmix64(42 + i) mod 50 + 1 generated on device (no dataset)"
+                     + (", stored as DECIMAL(15,2) (int64 raw = 100 x)" if args.config == "c2d" else "")),
             "config": {"workload": workload, "rows_per_gpu": n, "sql": sql,
                        "parallelism": f"row-range shards x{world}" + ((" + RCCL all-reduce/all-gather" if args.dist_backend == "nccl"
                                                                           else " + gloo collectives (rehearsal)") if world > 1 else "")},
@@ -264,8 +269,8 @@ def main():
             },
             "parity": parity,
         }
-        if not args.no_cpu and args.config in ("c2", "c3", "c5"):
-            result["cpu_baseline"] = cpu_baseline(args.cpu_seconds, args.config)
+        if not args.no_cpu and args.config in ("c2", "c2d", "c3", "c5"):
+            result["cpu_baseline"] = cpu_baseline(args.cpu_seconds, "c2" if args.config == "c2d" else args.config)
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()
