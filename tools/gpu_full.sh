@@ -10,3 +10,5 @@ timeout -k 10 300 python bench.py --config c4 > gpurun_out/bench_c4.json 2> gpur
 cd /tmp && export TMPDIR=/tmp
 timeout -k 10 200 rocprofv3 --kernel-trace --stats -d /root/repo/gpurun_out/prof/c2 -o c2 -- python3 /root/repo/bench.py --steps 10 --no-cpu > /root/repo/gpurun_out/prof_c2.log 2>&1 || exit 17
 timeout -k 10 200 rocprofv3 --kernel-trace --stats -d /root/repo/gpurun_out/prof/c3 -o c3 -- python3 /root/repo/bench.py --config c3 --steps 10 --no-cpu > /root/repo/gpurun_out/prof_c3.log 2>&1 || exit 18
+# the NULL-able shapes (filter_multi with validity, compact_validity), kernel trace
+NULLABLE=1 SHAPES=c2n,c5n,seln_out timeout -k 10 200 rocprofv3 --kernel-trace --stats -d /root/repo/gpurun_out/prof/nullable -o nullable -- python3 /root/repo/tools/shape_bench.py 1000000000 > /root/repo/gpurun_out/prof_nullable.log 2>&1 || exit 19
