@@ -546,7 +546,9 @@ __device__ __forceinline__ void acc_row(Acc &A, bool ok, int64_t v, bool mm, boo
   }
 }
 
-template <typename T, int MODE, int DEPTH, bool MM, bool NARROW>
+// MM: 0 no MIN/MAX, 1 int64 MIN/MAX, 2 int32 MIN/MAX (the zone map bounds |value|
+// below 2^31: one v_min_i32 / v_max_i32 per row instead of 64-bit compare pairs)
+template <typename T, int MODE, int DEPTH, int MM, bool NARROW>
 __global__ __launch_bounds__(256) void filter_agg_lds_kernel(const T *__restrict__ p, const T *__restrict__ a, int64_t n,
                                                              int64_t lo, uint64_t span, AggState *st,
                                                              unsigned long long *cstar, AggPartial *partials) {
@@ -562,6 +564,14 @@ __global__ __launch_bounds__(256) void filter_agg_lds_kernel(const T *__restrict
   const v2i64 *P = (const v2i64 *)p, *A2 = (const v2i64 *)a;
   Acc A;
   A.cnt = 0; A.slo = 0; A.shi = 0; A.mn = INT64_MAX; A.mx = INT64_MIN;
+  int32_t mn32 = INT32_MAX, mx32 = INT32_MIN;
+  auto row = [&](bool ok, int64_t v) {
+    acc_row(A, ok, v, MM == 1, NARROW);
+    if (MM == 2) {
+      mn32 = min(mn32, ok ? (int32_t)v : INT32_MAX);
+      mx32 = max(mx32, ok ? (int32_t)v : INT32_MIN);
+    }
+  };
 #pragma unroll
   for (int d = 0; d < DEPTH; d++) {
     int64_t q = pc + d * nw;
@@ -590,8 +600,8 @@ __global__ __launch_bounds__(256) void filter_agg_lds_kernel(const T *__restrict
         acc_count(A, ok0);
         acc_count(A, ok1);
       } else {
-        acc_row(A, ok0, MODE == 1 ? y.x : x.x, MM, NARROW);
-        acc_row(A, ok1, MODE == 1 ? y.y : x.y, MM, NARROW);
+        row(ok0, MODE == 1 ? y.x : x.x);
+        row(ok1, MODE == 1 ? y.y : x.y);
       }
     } else {
       const int *xi = (const int *)&x, *yi = (const int *)&y;
@@ -599,7 +609,7 @@ __global__ __launch_bounds__(256) void filter_agg_lds_kernel(const T *__restrict
       for (int e = 0; e < 4; e++) {
         bool ok = (uint64_t)((int64_t)xi[e] - lo) <= span;
         if (MODE == 2) acc_count(A, ok);
-        else acc_row(A, ok, (int64_t)(MODE == 1 ? yi[e] : xi[e]), MM, NARROW);
+        else row(ok, (int64_t)(MODE == 1 ? yi[e] : xi[e]));
       }
     }
     k = k + 1 == DEPTH ? 0 : k + 1;
@@ -610,8 +620,12 @@ __global__ __launch_bounds__(256) void filter_agg_lds_kernel(const T *__restrict
       int64_t xv = p[i];
       bool ok = (uint64_t)(xv - lo) <= span;
       if (MODE == 2) acc_count(A, ok);
-      else acc_row(A, ok, MODE == 1 ? (int64_t)a[i] : xv, MM, NARROW);
+      else row(ok, MODE == 1 ? (int64_t)a[i] : xv);
     }
+  }
+  if (MM == 2) {  // no selected row leaves INT32_MAX / INT32_MIN: the emit reads a count of 0 as NULL
+    A.mn = mn32;
+    A.mx = mx32;
   }
   if (NARROW) A.shi = (int64_t)A.slo >> 63;
   // block reduction through the same LDS array
@@ -883,7 +897,7 @@ static FaVariant FaConfig(int mode) {
 }
 
 static thread_local bool g_fa_pairs = true;
-static thread_local bool g_fa_mm = true, g_fa_narrow = false;  // per launch, set by FilterAggStates
+static thread_local bool g_fa_mm = true, g_fa_narrow = false, g_fa_mm32 = false;  // per launch, set by FilterAggStates
 static thread_local AggPartial *g_fa_partials = nullptr;
 template <typename TP, typename TA, int MODE, int U, bool NT, bool CH>
 static void LaunchFA(const void *p, const void *a, int64_t n, int64_t lo, uint64_t span, AggState *st,
@@ -903,9 +917,9 @@ static void LaunchFALds(const void *p, const void *a, int64_t n, int64_t lo, uin
 #define FAL(MM, NW)                                                                                                   \
   hipLaunchKernelGGL((filter_agg_lds_kernel<T, MODE, DEPTH, MM, NW>), dim3(grid), dim3(256), 0, s, (const T *)p,   \
                      (const T *)a, n, lo, span, st, cstar, g_fa_partials)
-  if (MODE == 2) FAL(false, false);
-  else if (g_fa_mm) { if (g_fa_narrow) FAL(true, true); else FAL(true, false); }
-  else { if (g_fa_narrow) FAL(false, true); else FAL(false, false); }
+  if (MODE == 2) FAL(0, false);
+  else if (g_fa_mm) { if (g_fa_mm32) FAL(2, true); else if (g_fa_narrow) FAL(1, true); else FAL(1, false); }
+  else { if (g_fa_narrow) FAL(0, true); else FAL(0, false); }
 #undef FAL
   CHECK_LAUNCH();
 }
@@ -980,6 +994,9 @@ int FilterAggStates(const void *pcol, int pphys, int64_t lo, int64_t hi, bool ha
     (void)asz;
     g_fa_narrow = sum_maxabs <= (uint64_t)INT64_MAX &&
                   (unsigned __int128)sum_maxabs * (unsigned __int128)rows_per_lane < ((unsigned __int128)1 << 63);
+    // MIN/MAX in int32 when the zone map bounds |value| below 2^31 (MBX_FA_MM32=0 disables)
+    const char *e32 = getenv("MBX_FA_MM32");
+    g_fa_mm32 = g_fa_narrow && sum_maxabs < ((uint64_t)1 << 31) && !(e32 && e32[0] == '0');
   }
   if (pphys == P_I64) {
     if (mode == 0) LaunchFilterAgg<int64_t, int64_t, 0>(v, pcol, acol, nrows, lo, span, st, cstar, grid, s);

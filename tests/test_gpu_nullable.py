@@ -61,3 +61,37 @@ def test_filter_aggregate_nullable(mbx, oracle, n):
     got = [_num(cell) for cell in q(c, "SELECT COUNT(*), COUNT(vn), SUM(vn) FROM tn WHERE x > 24").rows[0]]
     assert got == [int(m.sum()), int((m & vv).sum()), int(v[m & vv].astype(object).sum()) if (m & vv).any() else None]
     c.close()
+
+
+@pytest.mark.parametrize("n", [1, 1000, 100_003, 3_000_017])
+def test_filter_aggregate_minmax_int32_mode(conn, oracle, n):
+    """MIN/MAX of the fused filter-aggregate run in int32 when the zone map
+    bounds |value| below 2^31 (filter_agg_lds MM = 2): values at the int32
+    edges, empty selections and a column just past the bound (int64 mode)."""
+    v = oracle.synth_i64(n, 9, 0, 2**40, -2**39)
+    x = oracle.synth_i64(n, 42, 0, 50, 1)
+    for name, bound in (("edge", 2**31 - 1), ("past", 2**31)):
+        # values spread over [-bound, bound] with both ends present
+        vals = (v % (2 * bound + 1)) - bound
+        vals[0] = bound
+        if n > 1:
+            vals[1] = -bound
+        q(conn, f"DROP TABLE IF EXISTS mm")
+        q(conn, f"CREATE TABLE mm AS SELECT mbx_synth(42, i, 50) + 1 AS x, "
+                f"(mbx_synth(9, i, 1099511627776) - 549755813888) % {2 * bound + 1} AS r FROM range({n}) tbl(i)")
+        # the same values as numpy (truncated modulo, as in SQL), then shifted
+        r = np.fmod(v, 2 * bound + 1)
+        for sql, m in ((f"SELECT COUNT(*), SUM(r), MIN(r), MAX(r) FROM mm WHERE r > {-bound // 3}", r > -bound // 3),
+                       ("SELECT COUNT(*), MIN(r), MAX(r) FROM mm WHERE r > 99999999999", r > 99999999999),
+                       ("SELECT MIN(r), MAX(r) FROM mm", np.ones(n, bool))):
+            got = [_num(c) for c in q(conn, sql).rows[0]]
+            sel = r[m]
+            mn = int(sel.min()) if m.any() else None
+            mx = int(sel.max()) if m.any() else None
+            if sql.startswith("SELECT COUNT(*), SUM"):
+                want = [int(m.sum()), int(sel.astype(object).sum()) if m.any() else None, mn, mx]
+            elif sql.startswith("SELECT COUNT(*), MIN"):
+                want = [int(m.sum()), mn, mx]
+            else:
+                want = [mn, mx]
+            assert got == want, (n, name, sql)
