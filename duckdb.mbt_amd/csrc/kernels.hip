@@ -2633,7 +2633,7 @@ void FilterBits(const FilterMultiDesc &d, int64_t nrows, unsigned long long *bit
   CHECK_LAUNCH();
 }
 
-// Validity of the compacted rows.  A wave owns a chunk of CV_CHUNK consecutive
+// Validity of the compacted rows.  A wave owns a chunk of CV_CHUNK (8) consecutive
 // 256-row steps and prefetches the chunk's ballot words, validity words and
 // step offsets with one load each per lane.  Per step, each lane writes the
 // validity bytes of its selected rows (rows 4 lane + e) at their rank into the
@@ -2644,7 +2644,7 @@ void FilterBits(const FilterMultiDesc &d, int64_t nrows, unsigned long long *bit
 // stores; only a chunk's first word (when a previous chunk may share it) and
 // its final carry are ORed atomically: device-scope atomics leave the XCD's L2
 // and are slow, so they are kept to about two per chunk.
-#define CV_CHUNK 32
+#define CV_CHUNK 8
 __device__ __forceinline__ uint64_t readlane64(uint64_t x, int l) {
   const uint32_t lo = __builtin_amdgcn_readlane((int)(uint32_t)x, l);
   const uint32_t hi = __builtin_amdgcn_readlane((int)(uint32_t)(x >> 32), l);
@@ -2736,7 +2736,7 @@ void CompactValidity(const unsigned long long *bits, const int64_t *step_offsets
                      const uint64_t *valid_in, uint64_t *valid_out, hipStream_t s) {
   if (nrows <= 0) return;
   const int64_t chunks = ((nrows + 255) >> 8) / CV_CHUNK + 1;
-  hipLaunchKernelGGL(compact_validity_kernel, dim3(GridFor(chunks, 4, NumCUs() * 8)), dim3(256), 0, s, bits,
+  hipLaunchKernelGGL(compact_validity_kernel, dim3(GridFor(chunks, 4, NumCUs() * 32)), dim3(256), 0, s, bits,
                      step_offsets, nrows, valid_in, valid_out);
   CHECK_LAUNCH();
 }
