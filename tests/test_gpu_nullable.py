@@ -76,7 +76,7 @@ def test_filter_aggregate_minmax_int32_mode(conn, oracle, n):
         vals[0] = bound
         if n > 1:
             vals[1] = -bound
-        q(conn, f"DROP TABLE IF EXISTS mm")
+        q(conn, "DROP TABLE IF EXISTS mm")
         q(conn, f"CREATE TABLE mm AS SELECT mbx_synth(42, i, 50) + 1 AS x, "
                 f"(mbx_synth(9, i, 1099511627776) - 549755813888) % {2 * bound + 1} AS r FROM range({n}) tbl(i)")
         # the same values as numpy (truncated modulo, as in SQL), then shifted
