@@ -73,6 +73,7 @@ struct FilterMultiDesc {
   int32_t agg;  // index into col[] of the aggregated column, -1: COUNT only
   int32_t mm;
   int32_t narrow;   // set by FilterMultiPartials from maxabs and its grid
+  int32_t mm32;     // set by FilterMultiPartials: MIN/MAX in int32 (|value| < 2^31 by the zone map)
   uint64_t maxabs;  // zone-map bound on |aggregated value|, ~0 = unknown
   FilterMultiCol col[FM_MAX];
 };

@@ -695,7 +695,15 @@ __global__ __launch_bounds__(256) void filter_multi_lds_kernel(FilterMultiDesc D
   };
   Acc A;
   A.cnt = 0; A.slo = 0; A.shi = 0; A.mn = INT64_MAX; A.mx = INT64_MIN;
-  const bool mm = D.mm, narrow = D.narrow;
+  const bool mm32 = D.mm && D.mm32, mm = D.mm && !mm32, narrow = D.narrow;
+  int32_t mn32 = INT32_MAX, mx32 = INT32_MIN;
+  auto row = [&](bool ok, int64_t val) {
+    acc_row(A, ok, val, mm, narrow);
+    if (mm32) {
+      mn32 = min(mn32, ok ? (int32_t)val : INT32_MAX);
+      mx32 = max(mx32, ok ? (int32_t)val : INT32_MIN);
+    }
+  };
   if (nsteps > 0) {
 #pragma unroll
     for (int d = 0; d < DEPTH; d++) {
@@ -736,7 +744,7 @@ __global__ __launch_bounds__(256) void filter_multi_lds_kernel(FilterMultiDesc D
       for (int c = 0; c < FM_MAX; c++)
         if (c == D.agg) val = v[c][e];
       if (D.agg < 0) acc_count(A, ok);
-      else acc_row(A, ok, val, mm, narrow);
+      else row(ok, val);
     }
     k = k + 1 == DEPTH ? 0 : k + 1;
   }
@@ -752,8 +760,12 @@ __global__ __launch_bounds__(256) void filter_multi_lds_kernel(FilterMultiDesc D
         if (c == D.agg) val = x;
       }
       if (D.agg < 0) acc_count(A, ok);
-      else acc_row(A, ok, val, mm, narrow);
+      else row(ok, val);
     }
+  }
+  if (mm32) {  // a count of 0 makes the emit write NULL whatever these hold
+    A.mn = mn32;
+    A.mx = mx32;
   }
   if (narrow) A.shi = (int64_t)A.slo >> 63;
   acc_wave_reduce(A);
@@ -795,6 +807,8 @@ int FilterMultiPartials(const FilterMultiDesc &d_in, int64_t nrows, AggPartial *
     const unsigned __int128 rows_per_lane = (unsigned __int128)(((steps + waves - 1) / waves + 1) * 4);
     d.narrow = d.maxabs <= (uint64_t)INT64_MAX &&
                (unsigned __int128)d.maxabs * rows_per_lane < ((unsigned __int128)1 << 63);
+    const char *e32 = getenv("MBX_FA_MM32");
+    d.mm32 = d.mm && d.narrow && d.maxabs < ((uint64_t)1 << 31) && !(e32 && e32[0] == '0');
   }
 #define FM(L, DP)                                                                                            \
   hipLaunchKernelGGL((filter_multi_lds_kernel<L, DP>), dim3(grid), dim3(256), (size_t)4 * DP * slot, s, d, nrows, \
