@@ -46,13 +46,25 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--rows", type=int, default=1_000_000_000)
+    ap.add_argument("--rows", type=int, default=None,
+                    help="rows per GPU (default 1e9; 1.25e9 for c5 = 1e10 over 8 GPUs)")
     ap.add_argument("--config", default="c2", choices=["c1", "c2", "c2d", "c3", "c4", "c5"])
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
+    ap.add_argument("--dry-run", action="store_true",
+                    help="launcher/rendezvous plumbing only (CPU, gloo): every rank joins, all-reduces its "
+                         "rank id and rank 0 prints the JSON skeleton; no GPU is touched")
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                     help="nccl (= RCCL over xGMI) for real runs; gloo only to rehearse N>1 on fewer GPUs")
     args = ap.parse_args()
+    if args.rows is None:
+        args.rows = 1_250_000_000 if args.config == "c5" else 1_000_000_000
+
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        # `bench.py --gpus N` started bare: become the launcher of N ranks.
+        # Nothing above has touched the GPU (no torch import yet), and the
+        # ranks run as child processes (no exec), one per GPU.
+        raise SystemExit(launch_ranks(args.gpus, sys.argv[1:]))
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -60,6 +72,9 @@ def main():
 
     import torch
     import torch.distributed as dist
+
+    if args.dry_run:
+        return dry_run(args, world, rank)
 
     ndev = torch.cuda.device_count()
     device = local_rank % max(ndev, 1)  # == local_rank on a full node; folds ranks when rehearsing
@@ -192,7 +207,7 @@ def main():
         sys.path.insert(0, HERE)
         from oracle import Oracle  # test infrastructure: checker only
         orc = Oracle()
-        threads = min(16, len(os.sched_getaffinity(0)))
+        threads = host_share(world)
         oc, osum = orc.synth_filter_count(42, start, n, 50, 1, 25, 2**63 - 1, threads)
         parity = {"gpu_count": int(out[0]), "oracle_count": oc, "match": int(out[0]) == oc}
         if args.config == "c5":
@@ -211,7 +226,7 @@ def main():
         sys.path.insert(0, HERE)
         from oracle import Oracle  # test infrastructure: checker only
         orc = Oracle()
-        threads = min(16, len(os.sched_getaffinity(0)))
+        threads = host_share(world)
         oc, osum = orc.synth_groupby(7, 9, start, n, 32, 1 << 40, -(1 << 39), threads)
         exp = [(k, oc[k], osum[k]) for k in range(32) if oc[k]]
         got = sorted(out, key=lambda g: (g[0] is None, g[0]))
@@ -269,7 +284,7 @@ def main():
             },
             "parity": parity,
         }
-        if not args.no_cpu and args.config in ("c2", "c2d", "c3", "c5"):
+        if not args.no_cpu and world == 1 and args.config in ("c2", "c2d", "c3", "c5"):
             result["cpu_baseline"] = cpu_baseline(args.cpu_seconds, "c2" if args.config == "c2d" else args.config)
     if world > 1:
         dist.barrier()
@@ -277,6 +292,54 @@ def main():
     conn.close()
     if rank == 0:
         print(json.dumps(result), flush=True)
+
+
+def dry_run(args, world, rank):
+    import torch
+    import torch.distributed as dist
+    t = torch.tensor([rank + 1], dtype=torch.int64)
+    if world > 1:
+        dist.init_process_group("gloo")
+        dist.all_reduce(t)
+        dist.destroy_process_group()
+    if rank == 0:
+        print(json.dumps({"metric": METRIC, "value": None, "unit": "rows/s", "n_gpus": world,
+                          "dry_run": True, "rank_id_sum": int(t.item()),
+                          "config": {"workload": args.config, "rows_per_gpu": args.rows,
+                                     "parallelism": f"row-range shards x{world}"}}), flush=True)
+
+
+def free_port():
+    import socket
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launcher_cmd(nproc, argv, port):
+    """The torch.distributed.run command line that starts `nproc` ranks of this
+    script with the same arguments (one process per GPU, rendezvous on
+    127.0.0.1)."""
+    return [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={nproc}",
+            "--master-addr=127.0.0.1", f"--master-port={port}", os.path.abspath(__file__)] + list(argv)
+
+
+def launch_ranks(nproc, argv):
+    """Runs N ranks as a child launcher and forwards rank 0's JSON line to
+    stdout; returns the launcher's exit status."""
+    import subprocess
+    cmd = launcher_cmd(nproc, argv, free_port())
+    log("[launcher] " + " ".join(cmd))
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    p = subprocess.Popen(cmd, stdout=subprocess.PIPE, text=True, env=env)
+    for line in p.stdout:
+        t = line.strip()
+        if t.startswith("{") and t.endswith("}"):
+            print(t, flush=True)
+        else:
+            log(line.rstrip("\n"))
+    return p.wait()
 
 
 def one_count(conn):
@@ -358,16 +421,67 @@ def bench_c1():
     print(json.dumps(res), flush=True)
 
 
+def host_share(world):
+    """Oracle threads for the parity check: this host's cores split between
+    the ranks that run it at the same time."""
+    return max(1, len(os.sched_getaffinity(0)) // max(1, world))
+
+
+def l3_bytes():
+    """Total L3 of this host (sum over instances), from sysfs; 0 if unknown."""
+    seen, total = set(), 0
+    base = "/sys/devices/system/cpu"
+    try:
+        for cpu in os.listdir(base):
+            p = os.path.join(base, cpu, "cache", "index3")
+            if not cpu.startswith("cpu") or not os.path.isdir(p):
+                continue
+            ids = open(os.path.join(p, "shared_cpu_list")).read().strip()
+            if ids in seen:
+                continue
+            seen.add(ids)
+            sz = open(os.path.join(p, "size")).read().strip()
+            mult = {"K": 1 << 10, "M": 1 << 20, "G": 1 << 30}.get(sz[-1], 1)
+            total += int(sz.rstrip("KMG")) * mult
+    except OSError:
+        pass
+    return total
+
+
+def cpu_model():
+    import platform
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return platform.processor()
+
+
+def cgroup_cpus():
+    """The cgroup CPU quota in cores (None when unlimited or unknown)."""
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()
+        return None if q == "max" else int(q) / int(per)
+    except (OSError, ValueError):
+        return None
+
+
 def cpu_baseline(seconds, config="c2"):
     """The oracle's multi-threaded C scan over a materialised sample of the same
-    column(s), on this host's cores: orc_filter_agg_i64 (C2/C5: COUNT/SUM/MIN/MAX
-    WHERE x > 24) or orc_groupby_sum_i32_i64 (C3: per-key COUNT and int128 SUM).
-    Data generation is outside the timed loop."""
+    column(s), on ALL of this host's cores (one pthread per CPU in this
+    process's affinity mask, no cap): orc_filter_agg_i64 (C2/C5: COUNT/SUM/
+    MIN/MAX WHERE x > 24) or orc_groupby_sum_i32_i64 (C3: per-key COUNT and
+    int128 SUM).  The sample is >= 4x the host's total L3, so it streams from
+    DRAM as the full column would; generation is outside the timed loop."""
     sys.path.insert(0, HERE)
     from oracle import Oracle
     orc = Oracle()
-    threads = min(16, len(os.sched_getaffinity(0)))
-    sample = 100_000_000
+    threads = len(os.sched_getaffinity(0))
+    l3 = l3_bytes()
+    bpr = 12 if config == "c3" else 8
+    sample = max(250_000_000, -(-4 * l3 // bpr))
     if config == "c3":
         k = orc.synth_i32(sample, 7, 0, 32, 0)
         v = orc.synth_i64(sample, 9, 0, 1 << 40, -(1 << 39))
@@ -377,6 +491,7 @@ def cpu_baseline(seconds, config="c2"):
         x = orc.synth_i64(sample, 42, 0, 50, 1)
         run = lambda: orc.filter_agg_i64(x, 25, 2**63 - 1, threads)  # noqa: E731
         what = "COUNT/SUM/MIN/MAX with x > 24"
+    run()  # first touch / thread start-up outside the timed loop
     scanned = 0
     t0 = time.perf_counter()
     while True:
@@ -385,18 +500,13 @@ def cpu_baseline(seconds, config="c2"):
         if time.perf_counter() - t0 >= seconds:
             break
     dt = time.perf_counter() - t0
-    import platform
-    model = ""
-    try:
-        for line in open("/proc/cpuinfo"):
-            if line.startswith("model name"):
-                model = line.split(":", 1)[1].strip()
-                break
-    except Exception:
-        pass
+    quota = cgroup_cpus()
     return {"value": scanned / dt, "unit": "rows/s", "cores": threads, "kind": "port",
-            "sample": f"{sample} rows (first 1e8 of the same columns) scanned {scanned // sample}x in {dt:.1f}s, "
-                      f"{what}, pthreads={threads}, cpu={model or platform.processor()}"}
+            "nproc": os.cpu_count(), "cpu": cpu_model(), "l3_bytes": l3, "cgroup_cpu_quota": quota,
+            "gbs": scanned * bpr / dt / 1e9,
+            "sample": f"{sample} rows ({sample * bpr / 1e9:.2f} GB, >= 4x L3 = {4 * l3 / 1e9:.2f} GB) of the same "
+                      f"columns scanned {scanned // sample}x in {dt:.1f}s, {what}, pthreads={threads} "
+                      f"(= sched_getaffinity), cgroup quota={quota}"}
 
 
 if __name__ == "__main__":

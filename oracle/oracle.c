@@ -22,6 +22,7 @@
 #include <string.h>
 
 typedef __int128 i128;
+#define MAXT 1024 /* threads per call: one per host CPU on the largest boxes */
 
 uint64_t orc_splitmix64(uint64_t z) {
   z += 0x9E3779B97F4A7C15ull;
@@ -53,14 +54,17 @@ static void *fa_run(void *p) {
   uint64_t c = 0;
   i128 s = 0;
   int64_t mn = INT64_MAX, mx = INT64_MIN;
+  /* branch-free: the predicate becomes an all-ones/zero mask (a ~50 %
+     selective branch would mispredict on every other row) */
+  const int64_t lo = j->lo, hi = j->hi;
   for (int64_t i = 0; i < j->n; i++) {
     int64_t v = j->x[i];
-    if (v >= j->lo && v <= j->hi) {
-      c++;
-      s += v;
-      if (v < mn) mn = v;
-      if (v > mx) mx = v;
-    }
+    int64_t m = -(int64_t)((v >= lo) & (v <= hi));
+    c += (uint64_t)(m & 1);
+    s += (i128)(v & m);
+    int64_t vmn = (v & m) | (INT64_MAX & ~m), vmx = (v & m) | (INT64_MIN & ~m);
+    mn = vmn < mn ? vmn : mn;
+    mx = vmx > mx ? vmx : mx;
   }
   j->count = c;
   j->sum = s;
@@ -73,9 +77,9 @@ static void *fa_run(void *p) {
 void orc_filter_agg_i64(const int64_t *x, int64_t n, int64_t lo, int64_t hi, int threads, uint64_t *count,
                         void *sum16, int64_t *mn, int64_t *mx) {
   if (threads < 1) threads = 1;
-  if (threads > 256) threads = 256;
-  fa_job jobs[256];
-  pthread_t th[256];
+  if (threads > MAXT) threads = MAXT;
+  fa_job jobs[MAXT];
+  pthread_t th[MAXT];
   int64_t chunk = (n + threads - 1) / threads;
   for (int t = 0; t < threads; t++) {
     int64_t b = t * chunk, e = b + chunk < n ? b + chunk : n;
@@ -129,9 +133,9 @@ static void *sf_run(void *p) {
 void orc_synth_filter_count(uint64_t seed, int64_t start, int64_t n, uint64_t m, int64_t add, int64_t lo, int64_t hi,
                             int threads, uint64_t *count, void *sum16) {
   if (threads < 1) threads = 1;
-  if (threads > 256) threads = 256;
-  sf_job jobs[256];
-  pthread_t th[256];
+  if (threads > MAXT) threads = MAXT;
+  sf_job jobs[MAXT];
+  pthread_t th[MAXT];
   int64_t chunk = (n + threads - 1) / threads;
   for (int t = 0; t < threads; t++) {
     int64_t b = t * chunk, e = b + chunk < n ? b + chunk : n;
@@ -169,10 +173,50 @@ typedef struct {
 
 static void *gb_run(void *p) {
   gb_job *j = (gb_job *)p;
-  for (int64_t i = 0; i < j->n; i++) {
-    int s = j->k[i] - j->kmin;
-    j->cnt[s]++;
-    j->sum[s] += j->v[i];
+  if (j->nk > 64) {
+    for (int64_t i = 0; i < j->n; i++) {
+      int s = j->k[i] - j->kmin;
+      j->cnt[s]++;
+      j->sum[s] += j->v[i];
+    }
+    return NULL;
+  }
+  /* small key domain: thread-local counters in registers/stack, int64 partial
+     sums flushed into the int128 totals every 2^20 rows (|v| < 2^43 cannot
+     overflow an int64 partial in 2^20 additions for the C3 domain; larger
+     |v| takes the exact int128 path below) */
+  uint64_t cnt[64] = {0};
+  int64_t part[64] = {0};
+  i128 tot[64] = {0};
+  int ok = 1;
+  for (int64_t b = 0; b < j->n; b += 1 << 20) {
+    int64_t e = b + (1 << 20) < j->n ? b + (1 << 20) : j->n;
+    for (int64_t i = b; i < e && ok; i++) {
+      int64_t v = j->v[i];
+      if (v >= (1ll << 43) || v <= -(1ll << 43)) ok = 0;
+    }
+    if (!ok) break;
+    for (int64_t i = b; i < e; i++) {
+      int s = j->k[i] - j->kmin;
+      cnt[s]++;
+      part[s] += j->v[i];
+    }
+    for (int s = 0; s < j->nk; s++) {
+      tot[s] += part[s];
+      part[s] = 0;
+    }
+  }
+  if (!ok) {
+    for (int64_t i = 0; i < j->n; i++) {
+      int s = j->k[i] - j->kmin;
+      j->cnt[s]++;
+      j->sum[s] += j->v[i];
+    }
+    return NULL;
+  }
+  for (int s = 0; s < j->nk; s++) {
+    j->cnt[s] = cnt[s];
+    j->sum[s] = tot[s];
   }
   return NULL;
 }
@@ -181,9 +225,9 @@ static void *gb_run(void *p) {
 void orc_groupby_sum_i32_i64(const int32_t *k, const int64_t *v, int64_t n, int32_t kmin, int nk, int threads,
                              uint64_t *counts, void *sums16) {
   if (threads < 1) threads = 1;
-  if (threads > 256) threads = 256;
-  gb_job jobs[256];
-  pthread_t th[256];
+  if (threads > MAXT) threads = MAXT;
+  gb_job jobs[MAXT];
+  pthread_t th[MAXT];
   int64_t chunk = (n + threads - 1) / threads;
   for (int t = 0; t < threads; t++) {
     int64_t b = t * chunk, e = b + chunk < n ? b + chunk : n;
@@ -246,9 +290,9 @@ static void *sg_run(void *p) {
 void orc_synth_groupby(uint64_t seed_k, uint64_t seed_v, int64_t start, int64_t n, int nk, uint64_t vm, int64_t vadd,
                        int threads, uint64_t *counts, void *sums16) {
   if (threads < 1) threads = 1;
-  if (threads > 256) threads = 256;
-  sg_job jobs[256];
-  pthread_t th[256];
+  if (threads > MAXT) threads = MAXT;
+  sg_job jobs[MAXT];
+  pthread_t th[MAXT];
   int64_t chunk = (n + threads - 1) / threads;
   for (int t = 0; t < threads; t++) {
     int64_t b = t * chunk, e = b + chunk < n ? b + chunk : n;
