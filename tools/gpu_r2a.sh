@@ -5,3 +5,4 @@ timeout -k 10 120 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_ou
 timeout -k 10 200 python bench.py > gpurun_out/r2a/bench_c2.json 2> gpurun_out/r2a/bench_c2.err || exit 13
 timeout -k 10 200 python bench.py --config c3 > gpurun_out/r2a/bench_c3.json 2> gpurun_out/r2a/bench_c3.err || exit 14
 nproc > gpurun_out/r2a/host.txt; python -c "import os; print(len(os.sched_getaffinity(0)))" >> gpurun_out/r2a/host.txt; lscpu >> gpurun_out/r2a/host.txt; cat /sys/fs/cgroup/cpu.max >> gpurun_out/r2a/host.txt 2>&1 || true
+timeout -k 10 300 python bench.py --gpus 2 --config c5 --dist-backend gloo --rows 500000000 --steps 10 > gpurun_out/r2a/bench_c5_n2_gloo.json 2> gpurun_out/r2a/bench_c5_n2_gloo.err || exit 15
