@@ -275,6 +275,13 @@ struct CompactDesc {
   const void *src[FC_MAX_OUT];
   void *dst[FC_MAX_OUT];
   int32_t ow[FC_MAX_OUT];  // 1, 2, 4, 8 or 16 bytes (4/8 only: the register kernel; else the generic one)
+  // CompactRecompute only: the range predicates, each over one of the output
+  // columns (pred_out[j]; 4/8-byte integer, sign-extended), evaluated again
+  // from the slices pass 2 loads anyway
+  int32_t npred;
+  int32_t pred_out[FM_MAX];
+  int64_t pred_lo[FM_MAX];
+  uint64_t pred_span[FM_MAX];
 };
 void FilterBits(const FilterMultiDesc &d, int64_t nrows, unsigned long long *bits, hipStream_t s);
 // exclusive scan of the steps' selected-row counts (popcounts of their ballot words)
@@ -288,6 +295,48 @@ void CompactValidity(const unsigned long long *bits, const int64_t *step_offsets
 void CompactColumns(const CompactDesc &d, int64_t nrows, const unsigned long long *bits, const int64_t *step_offsets,
                     hipStream_t s);
 void RebaseOffsets(const int64_t *src, int64_t *dst, int64_t n, int64_t delta, hipStream_t s);
+
+// Count-first compaction, for a conjunction of range predicates whose columns
+// are all among the (NULL-free, 4/8-byte) outputs, e.g. SELECT x FROM t WHERE
+// x > 24.  A chunk is FC_CHUNK consecutive 256-row steps, owned by one wave in
+// both passes (so a wave's stores of a chunk form one contiguous run).
+//  1. FilterCountChunks: predicate columns through an LDS-DMA ring; one
+//     uint32 count per K1 steps (no per-row bits; K1 = FC_CHUNK by default,
+//     one count per chunk), the partial last step's count in counts[CountEntries].
+//  2. ScanTileCounts over CountEntries + 1 entries -> offsets and the total.
+//  3. CompactRecompute: output columns through an LDS-DMA ring; the predicates
+//     are evaluated again on the loaded slices (no bits to read), each selected
+//     row goes to offsets[chunk] + its rank in the chunk.
+#define FC_CHUNK 8
+int64_t CountChunks(int64_t nrows);   // pass-2 chunks of full steps
+int64_t CountEntries(int64_t nrows);  // pass-1 count entries (the count array has one more)
+void FilterCountChunks(const FilterMultiDesc &d, int64_t nrows, uint32_t *counts, hipStream_t s);
+void CompactRecompute(const CompactDesc &d, int64_t nrows, const int64_t *chunk_offsets, hipStream_t s);
+
+// One-pass filter -> compaction (select_kernels.hip): every loaded column (the
+// union of the predicate and output columns, 4 or 8 bytes, no NULLs) is read
+// from HBM once; tiles are claimed by an atomic ticket and ordered by a
+// decoupled look-back over per-tile status words.  Outputs must have room for
+// every row (the selected count is not known up front); the count lands in
+// *total.  status_buf: SelectStatusBytes(nrows, ni) bytes (ni = Σ w / 4).
+#define SL_MAX_COL 4
+#define SL_MAX_OUT 4
+struct SelectDesc {
+  int32_t ncol;
+  int32_t nout;
+  struct {
+    const void *data;
+    int32_t w;        // 4 or 8
+    int32_t is_pred;  // lo <= x <= lo + span (x sign-extended for 4 B)
+    int64_t lo;
+    uint64_t span;
+  } col[SL_MAX_COL];
+  int32_t out_col[SL_MAX_OUT];  // index into col[]
+  void *dst[SL_MAX_OUT];
+  unsigned long long *dbg;  // nullptr, or 9 counters (MBX_SL_DEBUG)
+};
+size_t SelectStatusBytes(int64_t nrows, int ni);
+void SelectCompact(const SelectDesc &d, int64_t nrows, void *status_buf, int64_t *total, hipStream_t s);
 
 }  // namespace dev
 }  // namespace mbx

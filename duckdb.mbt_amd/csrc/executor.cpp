@@ -1010,6 +1010,158 @@ static bool FastIntCol(const DRel &rel, int c) {
   return d.validity == nullptr && (d.phys == P_I32 || d.phys == P_I64) && d.data != nullptr;
 }
 
+// One-pass form of the compaction below (dev::SelectCompact): NULL-free 4/8-byte
+// columns, at most SL_MAX_COL distinct loaded columns (predicates ∪ outputs)
+// and SL_MAX_OUT outputs.  Each loaded column is read from HBM once; outputs
+// are allocated for every row (the count is known only afterwards), so the
+// form is used while that upper bound stays under MBX_SL_MAX_GB (default 64).
+// Opt-in (MBX_SL=1): its decoupled look-back measured 2-9x slower than the
+// two-pass forms on this chip (profiles/r02_select_onepass.log).
+static bool TrySelectOnePass(Engine &e, const DRel &rel, const dev::FilterMultiDesc &F,
+                             const std::vector<BExprPtr> &exprs, DRel &out) {
+  const char *env = getenv("MBX_SL");
+  if (!env || atoi(env) == 0) return false;  // opt-in: measured slower than the two-pass forms
+  if ((int)exprs.size() > SL_MAX_OUT) return false;
+  dev::SelectDesc S;
+  memset(&S, 0, sizeof(S));
+  std::vector<const void *> loaded;
+  auto slot_of = [&](const void *data, int w) -> int {
+    for (int i = 0; i < S.ncol; i++)
+      if (S.col[i].data == data) return S.col[i].w == w ? i : -2;
+    if (S.ncol >= SL_MAX_COL) return -1;
+    S.col[S.ncol].data = data;
+    S.col[S.ncol].w = w;
+    return S.ncol++;
+  };
+  for (int j = 0; j < F.ncol; j++) {
+    if (F.col[j].valid) return false;
+    const int i = slot_of(F.col[j].data, F.col[j].phys == P_I64 ? 8 : 4);
+    if (i < 0) return false;
+    S.col[i].is_pred = 1;
+    S.col[i].lo = F.col[j].lo;
+    S.col[i].span = F.col[j].span;
+  }
+  double out_bytes = 0;
+  for (auto &x : exprs) {
+    const DCol &c = rel.cols[x->col];
+    if (c.validity) return false;
+    const int w = PhysSize(c.phys);
+    if (w != 4 && w != 8) return false;
+    const int i = slot_of(c.data, w);
+    if (i < 0) return false;
+    S.out_col[S.nout++] = i;
+    out_bytes += (double)rel.n * w;
+  }
+  int ni = 0;
+  for (int i = 0; i < S.ncol; i++) ni += S.col[i].w / 4;
+  if (ni > 8) return false;
+  double cap_gb = 64;
+  if (const char *c = getenv("MBX_SL_MAX_GB")) cap_gb = atof(c);
+  if (out_bytes > cap_gb * 1e9) return false;
+  const int64_t n = rel.n;
+  std::vector<DCol> cols;
+  for (int k = 0; k < (int)exprs.size(); k++) {
+    cols.push_back(AllocOut(e, exprs[k]->type, n, false));
+    S.dst[k] = cols[k].data;
+  }
+  auto status = Alloc(e, dev::SelectStatusBytes(n, ni));
+  double bytes = 0;
+  for (int i = 0; i < S.ncol; i++) bytes += (double)n * S.col[i].w;
+  DevBufPtr dbgbuf;
+  if (getenv("MBX_SL_DEBUG")) {
+    dbgbuf = Alloc(e, 128, true);
+    S.dbg = (unsigned long long *)dbgbuf->p;
+  }
+  {
+    ProfScope ps(e, "select", bytes, n);  // algorithmic: inputs once (+ the selected rows' outputs, added below)
+    dev::SelectCompact(S, n, status->p, e.d_scratch, e.stream);
+  }
+  if (dbgbuf) {
+    unsigned long long h[9];
+    HIPCHK(hipMemcpyAsync(h, dbgbuf->p, sizeof(h), hipMemcpyDeviceToHost, e.stream));
+    HIPCHK(hipStreamSynchronize(e.stream));
+    fprintf(stderr, "[select] dma_wait %llu b1b2 %llu lookback %llu ticket %llu compact %llu windows %llu spins %llu "
+            "tiles %llu total %llu (cycles summed over workgroups)\n", h[0], h[1], h[2], h[3], h[4], h[5], h[6], h[7], h[8]);
+  }
+  const int64_t nsel = ReadDev<int64_t>(e, e.d_scratch);
+  if (e.profile && !e.events.empty() && e.events.back().name == "select") {
+    double ob = 0;
+    for (int k = 0; k < S.nout; k++) ob += (double)nsel * S.col[S.out_col[k]].w;
+    e.events.back().bytes += ob;
+  }
+  out = DRel();
+  out.n = nsel;
+  out.cols = cols;
+  CheckError(e);
+  return true;
+}
+
+// Count-first two-pass compaction (dev::FilterCountChunks, scan,
+// dev::CompactRecompute) when every predicate column is also an output and all
+// columns are NULL-free 4/8-byte ones (SELECT x FROM t WHERE x > 24): pass 1
+// writes one count per 2048-row chunk instead of per-row ballot bits, and pass 2
+// evaluates the predicates again on the slices it loads anyway, each wave
+// storing its chunk as one contiguous run.  MBX_CC=0 keeps the bits form.
+static bool TryCountFirst(Engine &e, const DRel &rel, const dev::FilterMultiDesc &F,
+                          const std::vector<BExprPtr> &exprs, DRel &out) {
+  const char *env = getenv("MBX_CC");
+  if (env && atoi(env) == 0) return false;
+  if ((int)exprs.size() > FC_MAX_OUT) return false;
+  dev::CompactDesc C;
+  memset(&C, 0, sizeof(C));
+  int nld = 0;
+  for (auto &x : exprs) {
+    const DCol &c = rel.cols[x->col];
+    const int w = PhysSize(c.phys);
+    if (c.validity || (w != 4 && w != 8)) return false;
+    C.src[C.nout] = c.data;
+    C.ow[C.nout] = w;
+    C.nout++;
+    nld += w / 4;
+  }
+  if (nld > 8) return false;
+  for (int j = 0; j < F.ncol; j++) {
+    if (F.col[j].valid) return false;
+    const int w = F.col[j].phys == P_I64 ? 8 : 4;
+    int k = -1;
+    for (int i = 0; i < C.nout && k < 0; i++)
+      if (C.src[i] == F.col[j].data && C.ow[i] == w) k = i;
+    if (k < 0) return false;
+    C.pred_out[C.npred] = k;
+    C.pred_lo[C.npred] = F.col[j].lo;
+    C.pred_span[C.npred] = F.col[j].span;
+    C.npred++;
+  }
+  const int64_t n = rel.n;
+  const int64_t chunks = dev::CountEntries(n);
+  auto counts = Alloc(e, (size_t)(chunks + 1) * 4);
+  auto offs = Alloc(e, (size_t)(chunks + 1) * 8);
+  double pbytes = 0;
+  for (int j = 0; j < F.ncol; j++) pbytes += (double)n * (F.col[j].phys == P_I64 ? 8 : 4);
+  {
+    ProfScope ps(e, "filter_count", pbytes + (double)(chunks + 1) * 4, n);
+    dev::FilterCountChunks(F, n, (uint32_t *)counts->p, e.stream);
+  }
+  dev::ScanTileCounts((const uint32_t *)counts->p, (int64_t *)offs->p, chunks + 1, e.d_scratch, e.stream);
+  const int64_t nsel = ReadDev<int64_t>(e, e.d_scratch);
+  out = DRel();
+  out.n = nsel;
+  std::vector<DCol> cols;
+  for (int k = 0; k < (int)exprs.size(); k++) {
+    cols.push_back(AllocOut(e, exprs[k]->type, nsel, false));
+    C.dst[k] = cols[k].data;
+  }
+  if (nsel > 0) {
+    double bytes = (double)(chunks + 1) * 8;
+    for (int k = 0; k < C.nout; k++) bytes += (double)n * C.ow[k] + (double)nsel * C.ow[k];
+    ProfScope ps(e, "compact", bytes, n);
+    dev::CompactRecompute(C, n, (const int64_t *)offs->p, e.stream);
+  }
+  out.cols = cols;
+  CheckError(e);
+  return true;
+}
+
 // WHERE <range conjunction over int columns> with plain 1/2/4/8/16-byte output
 // columns: two streaming passes (dev::FilterBits, scan, dev::CompactColumns,
 // plus dev::CompactValidity per nullable output) instead of vm_filter + scan +
@@ -1056,6 +1208,8 @@ static bool TryFilterCompact(Engine &e, const DRel &rel, const BExpr &pred, cons
     for (auto &x : exprs) out.cols.push_back(AllocOut(e, x->type, 0, rel.cols[x->col].validity != nullptr));
     return true;
   }
+  if (TrySelectOnePass(e, rel, F, exprs, out)) return true;
+  if (TryCountFirst(e, rel, F, exprs, out)) return true;
   const int64_t steps = (n + 255) / 256;
   auto bits = Alloc(e, (size_t)steps * 32);
   auto offs = Alloc(e, (size_t)(steps + 2) * 8);  // compact reads offsets in 16-B aligned pairs

@@ -1,0 +1,683 @@
+// select_kernels.hip — one-pass, order-preserving filter -> compaction
+// (SELECT <cols> FROM t WHERE <range conjunction>) for gfx950.
+//
+// Why one pass: the two-pass form (kernels.hip: filter_bits_lds -> scan ->
+// compact_lds) reads every predicate column twice when the predicate column
+// is also an output (SELECT x FROM t WHERE x > 24: 16 GB read + 4.2 GB
+// written per 1e9 rows).  Here each needed column is read from HBM once:
+//
+//  * A tile is 4 waves x S steps x 256 rows.  Workgroups claim tiles with an
+//    atomic ticket (claim order == output order), and every wave pulls its S
+//    steps of every loaded column into its own LDS region by LDS-DMA
+//    (global_load_lds_dwordx4), NBUF tiles in flight per workgroup.
+//  * When a tile has landed, each wave evaluates the predicates (each lane
+//    owns rows 4 lane + e of a step) into ballot words; the tile's count is
+//    published at once as an aggregate (flag AGG) in a per-tile status word.
+//  * Wave 0 then resolves the tile's exclusive prefix by a decoupled
+//    look-back over the predecessors' status words, 64 at a time (one lane
+//    per predecessor, a ballot finds the nearest inclusive prefix), and
+//    publishes the inclusive prefix (flag INC).  Meanwhile the next tiles'
+//    DMA keeps streaming, and the tile itself stays in LDS: nothing is
+//    re-read.
+//  * Each wave then compacts its steps out of LDS: selected values go to a
+//    per-wave staging row at their rank (popcounts of the ballot words below
+//    the lane), and consecutive lanes store consecutive output rows.
+//
+// Progress: a tile is claimed only by a running workgroup, and a workgroup
+// finishes its claimed tiles in claim order, so the lowest unfinished tile
+// always has all its predecessors published or being published by running
+// workgroups: no residency assumption, no deadlock with other kernels sharing
+// the GPU.  Status words are 8-byte agent-scope atomics on both sides.
+//
+// The final partial step (n % 256 rows) follows the last tile: the workgroup
+// that resolved the last tile's inclusive prefix handles it with guarded
+// loads and writes the selected-row total.
+#include <hip/hip_runtime.h>
+#include <stdexcept>
+#include <stdint.h>
+
+#include "device.h"
+#include "types.h"
+
+namespace mbx {
+namespace dev {
+
+namespace {
+
+typedef long long sl_v2i64 __attribute__((ext_vector_type(2)));
+typedef int sl_v4i32 __attribute__((ext_vector_type(4)));
+
+constexpr unsigned long long SL_AGG = 1ull << 62, SL_INC = 2ull << 62, SL_VAL = (1ull << 62) - 1;
+
+__device__ __forceinline__ int64_t sl_wave_sum(int64_t v) {
+#pragma unroll
+  for (int m = 32; m >= 1; m >>= 1) v += __shfl_xor(v, m, 64);
+  return v;
+}
+
+// 4 consecutive values (rows 4 lane .. 4 lane + 3 of a step) of a 4- or
+// 8-byte column slice held in LDS, widened to int64 (sign-extended for 4 B).
+__device__ __forceinline__ void sl_read4(const unsigned char *slice, int w, int lane, int64_t v[4]) {
+  if (w == 8) {
+    const sl_v2i64 a = *(const sl_v2i64 *)(slice + lane * 32), b = *(const sl_v2i64 *)(slice + lane * 32 + 16);
+    v[0] = a.x; v[1] = a.y; v[2] = b.x; v[3] = b.y;
+  } else {
+    const sl_v4i32 a = *(const sl_v4i32 *)(slice + lane * 16);
+    v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w;
+  }
+}
+
+// a value every lane holds alike (read from LDS), moved to an SGPR so that the
+// branches on it stay scalar
+__device__ __forceinline__ int64_t sl_uni(int64_t x) {
+  const uint32_t lo = __builtin_amdgcn_readfirstlane((int)(uint32_t)x);
+  const uint32_t hi = __builtin_amdgcn_readfirstlane((int)(uint32_t)((uint64_t)x >> 32));
+  return (int64_t)((uint64_t)hi << 32 | lo);
+}
+
+}  // namespace
+
+// NI: LDS-DMA instructions (KiB) per 256-row step over all loaded columns;
+// S: steps per wave per tile; NBUF: tiles in flight per workgroup.
+template <int NI, int S, int NBUF>
+__global__ __launch_bounds__(256) void select_lds_kernel(SelectDesc D, int64_t n, int64_t ntiles,
+                                                         unsigned long long *status, unsigned int *ticket,
+                                                         int64_t *total) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char sl_lds[];
+  __shared__ int64_t s_tick[NBUF];
+  __shared__ int64_t s_excl[2];
+  __shared__ uint32_t s_wcnt[2][4];
+  constexpr int SB = NI * 1024;  // one step of every loaded column
+  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  unsigned char *ring = sl_lds + (size_t)w * NBUF * S * SB;
+  unsigned char *stage = sl_lds + (size_t)4 * NBUF * S * SB + (size_t)w * 2048;  // 256 rows x 8 B
+  const int64_t nsteps = n >> 8;
+  const uint64_t lt = (1ull << lane) - 1;
+  int off[SL_MAX_COL];
+  {
+    int o = 0;
+#pragma unroll
+    for (int c = 0; c < SL_MAX_COL; c++) {
+      off[c] = o;
+      if (c < D.ncol) o += D.col[c].w * 256;
+    }
+  }
+  // this wave's S steps of tile T into buffer b (a dummy re-load of step 0
+  // for steps past the end, so every tile is exactly S * NI loads per wave)
+  auto issue = [&](int64_t T, int b) {
+#pragma unroll
+    for (int s = 0; s < S; s++) {
+      int64_t q = (T * 4 + w) * S + s;
+      if (T >= ntiles || q >= nsteps) q = 0;
+      unsigned char *dst = ring + (size_t)(b * S + s) * SB;
+#pragma unroll
+      for (int c = 0; c < SL_MAX_COL; c++) {
+        if (c >= D.ncol) break;
+        const int B = D.col[c].w * 256;
+        const unsigned char *src = (const unsigned char *)D.col[c].data + q * B;
+        __builtin_amdgcn_global_load_lds((const void *)(src + lane * 16), (void *)(dst + off[c]), 16, 0, 2);
+        if (B == 2048)
+          __builtin_amdgcn_global_load_lds((const void *)(src + 1024 + lane * 16), (void *)(dst + off[c] + 1024), 16, 0,
+                                           2);
+      }
+    }
+  };
+
+  if (threadIdx.x == 0)
+    for (int i = 0; i < NBUF; i++) s_tick[i] = (int64_t)atomicAdd(ticket, 1u);
+  __syncthreads();
+#pragma unroll
+  for (int i = 0; i < NBUF - 1; i++) issue(sl_uni(s_tick[i]), i);
+
+  int64_t last_incl = -1;  // wave 0: inclusive prefix of the last tile, if this workgroup resolved it
+  // MBX_SL_DEBUG: wave 0's cycle split (D.dbg: dma wait, barrier 1 -> 2,
+  // look-back loop, ticket, compaction, windows, spins, tiles, total)
+  unsigned long long dg[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
+  const bool dbg = D.dbg != nullptr && w == 0;
+  unsigned long long t_start = dbg ? clock64() : 0, t0 = 0;
+  for (int j = 0;; j++) {
+    const int b = j % NBUF, par = j & 1;
+    const int64_t T = sl_uni(s_tick[b]);
+    if (T >= ntiles) break;  // workgroup-uniform
+    {
+      const int nb = (j + NBUF - 1) % NBUF;
+      issue(sl_uni(s_tick[nb]), nb);
+    }
+    if (dbg) t0 = clock64();
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"((NBUF - 1) * S * NI) : "memory");
+    if (dbg) dg[0] += clock64() - t0;
+    // --- count: ballots of this wave's S steps
+    unsigned long long bal[S][4];
+    int cnt[S];
+    int cw = 0;
+#pragma unroll
+    for (int s = 0; s < S; s++) {
+      const unsigned char *slot = ring + (size_t)(b * S + s) * SB;
+      const bool live = (T * 4 + w) * S + s < nsteps;
+      bool ok[4] = {live, live, live, live};
+#pragma unroll
+      for (int c = 0; c < SL_MAX_COL; c++) {
+        if (c >= D.ncol) break;
+        if (!D.col[c].is_pred) continue;
+        int64_t v[4];
+        sl_read4(slot + off[c], D.col[c].w, lane, v);
+#pragma unroll
+        for (int e = 0; e < 4; e++) ok[e] = ok[e] && (uint64_t)(v[e] - D.col[c].lo) <= D.col[c].span;
+      }
+      int cs = 0;
+#pragma unroll
+      for (int e = 0; e < 4; e++) {
+        bal[s][e] = __ballot(ok[e]);
+        cs += __popcll(bal[s][e]);
+      }
+      cnt[s] = cs;
+      cw += cs;
+    }
+    if (lane == 0) s_wcnt[par][w] = (uint32_t)cw;
+    __syncthreads();
+    if (dbg) t0 = clock64();
+    // --- wave 0: publish the aggregate, look back, publish the inclusive prefix
+    if (w == 0) {
+      const int64_t A = sl_uni((int64_t)s_wcnt[par][0] + s_wcnt[par][1] + s_wcnt[par][2] + s_wcnt[par][3]);
+      if (lane == 0) __hip_atomic_store(&status[T], SL_AGG | (unsigned long long)A, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      int64_t excl = 0;
+      int64_t base = T - 1;
+      const unsigned long long tl = dbg ? clock64() : 0;
+      while (base >= 0) {
+        if (dbg) dg[5]++;
+        const int64_t idx = base - lane;
+        const unsigned long long v =
+            idx >= 0 ? __hip_atomic_load(&status[idx], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : SL_INC;
+        const unsigned long long incl = __ballot((v >> 62) == 2);
+        const unsigned long long none = __ballot((v >> 62) == 0);
+        // lanes up to and including the nearest inclusive prefix
+        const unsigned long long upto = incl ? (((incl & (~incl + 1)) << 1) - 1) : ~0ull;
+        if (none & upto) {  // a predecessor has not published yet
+          if (dbg) dg[6]++;
+          __builtin_amdgcn_s_sleep(1);
+          continue;
+        }
+        excl += sl_wave_sum(((upto >> lane) & 1) ? (int64_t)(v & SL_VAL) : 0);
+        if (incl) break;
+        base -= 64;
+      }
+      if (dbg) dg[2] += clock64() - tl;
+      const unsigned long long tt = dbg ? clock64() : 0;
+      if (lane == 0) {
+        __hip_atomic_store(&status[T], SL_INC | (unsigned long long)(excl + A), __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+        s_excl[par] = excl;
+        s_tick[b] = (int64_t)atomicAdd(ticket, 1u);  // the tile this buffer takes next
+      }
+      if (T == ntiles - 1) last_incl = excl + A;
+      if (dbg) { __builtin_amdgcn_s_waitcnt(0); dg[3] += clock64() - tt; }
+    }
+    __syncthreads();
+    if (dbg) { dg[1] += clock64() - t0; dg[7]++; t0 = clock64(); }
+    // --- compaction of this wave's steps straight out of LDS
+    int64_t o = s_excl[par];
+    for (int q = 0; q < w; q++) o += s_wcnt[par][q];
+    o = sl_uni(o);
+#pragma unroll
+    for (int s = 0; s < S; s++) {
+      if (cnt[s] == 0) continue;  // wave-uniform
+      const unsigned char *slot = ring + (size_t)(b * S + s) * SB;
+      const unsigned m = (unsigned)((bal[s][0] >> lane) & 1) | (unsigned)((bal[s][1] >> lane) & 1) << 1 |
+                         (unsigned)((bal[s][2] >> lane) & 1) << 2 | (unsigned)((bal[s][3] >> lane) & 1) << 3;
+      const int r0 = __popcll(bal[s][0] & lt) + __popcll(bal[s][1] & lt) + __popcll(bal[s][2] & lt) +
+                     __popcll(bal[s][3] & lt);
+#pragma unroll
+      for (int k = 0; k < SL_MAX_OUT; k++) {
+        if (k >= D.nout) break;
+        const int c = D.out_col[k];
+        int64_t v[4];
+        sl_read4(slot + off[c], D.col[c].w, lane, v);
+        int r = r0;
+        if (D.col[c].w == 8) {
+#pragma unroll
+          for (int e = 0; e < 4; e++)
+            if ((m >> e) & 1u) ((int64_t *)stage)[r++] = v[e];
+          asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+          int64_t *dst = (int64_t *)D.dst[k] + o;
+          for (int i = lane; i < cnt[s]; i += 64) dst[i] = ((const int64_t *)stage)[i];
+        } else {
+#pragma unroll
+          for (int e = 0; e < 4; e++)
+            if ((m >> e) & 1u) ((int32_t *)stage)[r++] = (int32_t)v[e];
+          asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+          int32_t *dst = (int32_t *)D.dst[k] + o;
+          for (int i = lane; i < cnt[s]; i += 64) dst[i] = ((const int32_t *)stage)[i];
+        }
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // staging reads done before it is rewritten
+      }
+      o += cnt[s];
+    }
+    if (dbg) dg[4] += clock64() - t0;
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  if (dbg && lane == 0) {
+    dg[8] = clock64() - t_start;
+    for (int i = 0; i < 9; i++) atomicAdd(&D.dbg[i], dg[i]);
+  }
+  // --- the partial last step and the total, by the resolver of the last tile
+  // (or block 0 when there is no full tile)
+  if (w == 0 && (last_incl >= 0 || (ntiles == 0 && blockIdx.x == 0))) {
+    const int64_t prefix = last_incl >= 0 ? last_incl : 0;
+    int64_t tcnt = 0;
+    if (n & 255) {
+      bool ok[4];
+      int64_t i0 = (nsteps << 8) + 4 * lane;
+#pragma unroll
+      for (int e = 0; e < 4; e++) {
+        const int64_t i = i0 + e;
+        ok[e] = i < n;
+        for (int c = 0; c < D.ncol && ok[e]; c++) {
+          if (!D.col[c].is_pred) continue;
+          const int64_t x = D.col[c].w == 8 ? ((const int64_t *)D.col[c].data)[i]
+                                            : (int64_t)((const int32_t *)D.col[c].data)[i];
+          ok[e] = (uint64_t)(x - D.col[c].lo) <= D.col[c].span;
+        }
+      }
+      unsigned long long bb[4];
+      for (int e = 0; e < 4; e++) bb[e] = __ballot(ok[e]);
+      int64_t pos = prefix + __popcll(bb[0] & lt) + __popcll(bb[1] & lt) + __popcll(bb[2] & lt) + __popcll(bb[3] & lt);
+      for (int e = 0; e < 4; e++) {
+        if (!ok[e]) continue;
+        for (int k = 0; k < D.nout; k++) {
+          const int c = D.out_col[k];
+          if (D.col[c].w == 8) ((int64_t *)D.dst[k])[pos] = ((const int64_t *)D.col[c].data)[i0 + e];
+          else ((int32_t *)D.dst[k])[pos] = ((const int32_t *)D.col[c].data)[i0 + e];
+        }
+        pos++;
+      }
+      tcnt = __popcll(bb[0]) + __popcll(bb[1]) + __popcll(bb[2]) + __popcll(bb[3]);
+    }
+    if (lane == 0) *total = prefix + tcnt;
+  }
+}
+
+int SelectSteps(int ni) { return ni <= 2 ? 4 : ni <= 4 ? 2 : 1; }
+
+size_t SelectStatusBytes(int64_t nrows, int ni) {
+  const int64_t tile_steps = 4 * (int64_t)SelectSteps(ni);
+  const int64_t ntiles = ((nrows >> 8) + tile_steps - 1) / tile_steps;
+  return (size_t)(ntiles + 2) * 8;  // status words + the ticket
+}
+
+void SelectCompact(const SelectDesc &d, int64_t nrows, void *status_buf, int64_t *total, hipStream_t s) {
+  int ni = 0;
+  for (int c = 0; c < d.ncol; c++) {
+    if (d.col[c].w != 4 && d.col[c].w != 8) throw std::runtime_error("SelectCompact: columns must be 4 or 8 bytes");
+    ni += d.col[c].w / 4;
+  }
+  if (ni < 1 || ni > 8 || d.nout < 1 || d.nout > SL_MAX_OUT)
+    throw std::runtime_error("SelectCompact: unsupported shape");
+  const int S = SelectSteps(ni);
+  const int64_t tile_steps = 4 * (int64_t)S;
+  const int64_t ntiles = ((nrows >> 8) + tile_steps - 1) / tile_steps;
+  unsigned long long *status = (unsigned long long *)status_buf;
+  unsigned int *ticket = (unsigned int *)(status + ntiles + 1);
+  (void)hipMemsetAsync(status, 0, (size_t)(ntiles + 2) * 8, s);
+  int nbuf = 3;
+  if (const char *e = getenv("MBX_SL_NBUF")) nbuf = atoi(e) == 2 ? 2 : atoi(e) >= 4 ? 4 : 3;
+  int gpc = 1;
+  if (const char *e = getenv("MBX_SL_BLOCKS_PER_CU")) gpc = atoi(e) > 0 ? atoi(e) : 1;
+  int64_t grid = (int64_t)NumCUs() * gpc;
+  if (grid > ntiles) grid = ntiles > 0 ? ntiles : 1;
+  const size_t lds = (size_t)4 * nbuf * S * ni * 1024 + 4 * 2048;
+#define SL(NI_, S_, NB_)                                                                                       \
+  do {                                                                                                         \
+    static bool attr = false;                                                                                  \
+    if (!attr) {                                                                                               \
+      (void)hipFuncSetAttribute((const void *)select_lds_kernel<NI_, S_, NB_>,                                 \
+                                hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024 - 256);                 \
+      attr = true;                                                                                             \
+    }                                                                                                          \
+    hipLaunchKernelGGL((select_lds_kernel<NI_, S_, NB_>), dim3((unsigned)grid), dim3(256), lds, s, d, nrows,  \
+                       ntiles, status, ticket, total);                                                         \
+  } while (0)
+#define SLN(NI_, S_)                   \
+  if (nbuf == 2) SL(NI_, S_, 2);       \
+  else if (nbuf == 4) SL(NI_, S_, 4);  \
+  else SL(NI_, S_, 3)
+  switch (ni) {
+    case 1: SLN(1, 4); break;
+    case 2: SLN(2, 4); break;
+    case 3: SLN(3, 2); break;
+    case 4: SLN(4, 2); break;
+    case 5: SLN(5, 1); break;
+    case 6: SLN(6, 1); break;
+    case 7: SLN(7, 1); break;
+    default: SLN(8, 1); break;
+  }
+#undef SLN
+#undef SL
+  (void)hipGetLastError();
+}
+
+
+// ---------------------------------------------------------------------------
+// Count-first compaction (see device.h): chunk-owned steps in both passes.
+// ---------------------------------------------------------------------------
+int64_t CountChunks(int64_t nrows) { return ((nrows >> 8) + FC_CHUNK - 1) / FC_CHUNK; }
+
+// Pass 1 counts every K1 steps (K1 divides FC_CHUNK; MBX_FK_CHUNK, default
+// FC_CHUNK: 1.29 ms at 1e9 INT64 rows vs 1.36 for K1 = 1, which walks the steps
+// grid-stride like the fused filter-aggregate); pass 2 reads the offset of
+// chunk c at entry c * FC_CHUNK / K1 of the scanned counts.
+static int FkChunk() {
+  const char *e = getenv("MBX_FK_CHUNK");
+  const int v = e ? atoi(e) : FC_CHUNK;
+  return (v == 1 || v == 2 || v == 4) ? v : FC_CHUNK;
+}
+int64_t CountEntries(int64_t nrows) {  // pass-1 count entries over the full steps (+1 for the partial step)
+  const int64_t steps = nrows >> 8;
+  return ((steps + FC_CHUNK - 1) / FC_CHUNK) * (FC_CHUNK / FkChunk());
+}
+
+namespace {
+// sequence position p of wave wv -> its step (chunk wv + (p / K) NW, step p % K
+// of that chunk), or -1 past the wave's last chunk / past the last full step
+template <int K>
+__device__ __forceinline__ int64_t cc_step(int64_t p, int64_t wv, int64_t nw, int64_t nchunks, int64_t nsteps) {
+  const int64_t c = wv + (p / K) * nw;
+  const int64_t st = c * K + p % K;
+  return c < nchunks && st < nsteps ? st : -1;
+}
+}  // namespace
+
+// pass 1: NI LDS-DMA instructions (KiB of predicate slices) per step, one
+// count per K1 steps
+template <int NI, int DEPTH, int K1>
+__global__ __launch_bounds__(256) void filter_count_lds_kernel(FilterMultiDesc D, int64_t n, uint32_t *counts,
+                                                               int slot_bytes) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char fk_lds[];
+  const int SB = slot_bytes;
+  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  unsigned char *ring = fk_lds + (size_t)w * DEPTH * SB;
+  int off[FM_MAX];
+  {
+    int o = 0;
+#pragma unroll
+    for (int c = 0; c < FM_MAX; c++) {
+      off[c] = o;
+      if (c < D.ncol) o += D.col[c].phys == P_I64 ? 2048 : 1024;
+    }
+  }
+  const int64_t nsteps = n >> 8;
+  const int64_t nchunks = ((nsteps + FC_CHUNK - 1) / FC_CHUNK) * (FC_CHUNK / K1);  // count entries
+  const int64_t nw = (int64_t)gridDim.x * 4, wv = (int64_t)blockIdx.x * 4 + w;
+  auto issue = [&](int64_t p, int d) {
+    int64_t q = cc_step<K1>(p, wv, nw, nchunks, nsteps);
+    if (q < 0) q = 0;
+    unsigned char *dst = ring + d * SB;
+#pragma unroll
+    for (int c = 0; c < FM_MAX; c++) {
+      if (c >= D.ncol) break;
+      const int B = D.col[c].phys == P_I64 ? 2048 : 1024;
+      const unsigned char *src = (const unsigned char *)D.col[c].data + q * B;
+      __builtin_amdgcn_global_load_lds((const void *)(src + lane * 16), (void *)(dst + off[c]), 16, 0, 2);
+      if (B == 2048)
+        __builtin_amdgcn_global_load_lds((const void *)(src + 1024 + lane * 16), (void *)(dst + off[c] + 1024), 16, 0, 2);
+    }
+  };
+  if (wv < nchunks) {
+#pragma unroll
+    for (int d = 0; d < DEPTH; d++) issue(d, d);
+    int k = 0;
+    uint32_t acc = 0;
+    for (int64_t p = 0;; p++) {
+      const int64_t c = wv + (p / K1) * nw;
+      if (c >= nchunks) break;
+      const int64_t st = c * K1 + p % K1;
+      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NI * (DEPTH - 1)) : "memory");
+      const unsigned char *src = ring + k * SB;
+      bool ok[4] = {st < nsteps, st < nsteps, st < nsteps, st < nsteps};
+#pragma unroll
+      for (int c2 = 0; c2 < FM_MAX; c2++) {
+        if (c2 >= D.ncol) break;
+        int64_t v[4];
+        sl_read4(src + off[c2], D.col[c2].phys == P_I64 ? 8 : 4, lane, v);
+#pragma unroll
+        for (int e = 0; e < 4; e++) ok[e] = ok[e] && (uint64_t)(v[e] - D.col[c2].lo) <= D.col[c2].span;
+      }
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      issue(p + DEPTH, k);
+#pragma unroll
+      for (int e = 0; e < 4; e++) acc += (uint32_t)__popcll(__ballot(ok[e]));
+      if (p % K1 == K1 - 1) {
+        if (lane == 0) counts[c] = acc;
+        acc = 0;
+      }
+      k = k + 1 == DEPTH ? 0 : k + 1;
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
+  // the partial last step's count after the chunks (always written)
+  if (blockIdx.x == 0 && w == 0) {
+    bool ok[4];
+#pragma unroll
+    for (int e = 0; e < 4; e++) {
+      const int64_t i = (nsteps << 8) + 4 * lane + e;
+      ok[e] = i < n;
+      for (int c = 0; c < D.ncol && ok[e]; c++) {
+        const int64_t x = D.col[c].phys == P_I64 ? ((const int64_t *)D.col[c].data)[i]
+                                                 : (int64_t)((const int32_t *)D.col[c].data)[i];
+        ok[e] = (uint64_t)(x - D.col[c].lo) <= D.col[c].span;
+      }
+    }
+    uint32_t t = 0;
+#pragma unroll
+    for (int e = 0; e < 4; e++) t += (uint32_t)__popcll(__ballot(ok[e]));
+    if (lane == 0) counts[nchunks] = t;
+  }
+}
+
+void FilterCountChunks(const FilterMultiDesc &d, int64_t nrows, uint32_t *counts, hipStream_t s) {
+  int ni = 0;
+  for (int c = 0; c < d.ncol; c++) {
+    if (d.col[c].valid) throw std::runtime_error("FilterCountChunks: NULL-able predicate column");
+    ni += d.col[c].phys == P_I64 ? 2 : 1;
+  }
+  const int slot = ni * 1024;
+  int gpc = 3;
+  if (const char *e = getenv("MBX_FK_BLOCKS_PER_CU")) gpc = atoi(e) > 0 ? atoi(e) : 3;
+  const int64_t chunks = CountEntries(nrows);
+  int64_t grid = (int64_t)NumCUs() * gpc;
+  if (grid > chunks / 4 + 1) grid = chunks / 4 + 1;
+  int dp = 0;
+  if (const char *e = getenv("MBX_FK_DEPTH")) dp = atoi(e);
+  const int k1 = FkChunk();
+#define FK1(L, DP, K)                                                                                         \
+  hipLaunchKernelGGL((filter_count_lds_kernel<L, DP, K>), dim3((unsigned)grid), dim3(256), (size_t)4 * DP * slot, s, \
+                     d, nrows, counts, slot)
+#define FK(L, DP) \
+  if (k1 == 8) FK1(L, DP, 8); else if (k1 == 4) FK1(L, DP, 4); else if (k1 == 2) FK1(L, DP, 2); else FK1(L, DP, 1)
+#define FKD(L, DEF) \
+  if ((dp ? dp : DEF) <= 2) FK(L, 2); else if ((dp ? dp : DEF) <= 3) FK(L, 3); else if ((dp ? dp : DEF) <= 4) FK(L, 4); else FK(L, 6);
+  switch (ni) {
+    case 1: FKD(1, 6); break;
+    case 2: FKD(2, 6); break;
+    case 3: FKD(3, 3); break;
+    case 4: FKD(4, 3); break;
+    case 5: FK(5, 2); break;
+    case 6: FK(6, 2); break;
+    case 7: FK(7, 2); break;
+    default: FK(8, 2); break;
+  }
+#undef FKD
+#undef FK
+#undef FK1
+  (void)hipGetLastError();
+}
+
+// pass 2: NLD KiB of output slices per step; predicates re-evaluated on them
+template <int NLD, int DEPTH>
+__global__ __launch_bounds__(256) void compact_recomp_lds_kernel(CompactDesc D, int64_t n,
+                                                                 const int64_t *__restrict__ offs, int stride) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char cr_lds[];
+  constexpr int SB = NLD * 1024;
+  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  unsigned char *ring = cr_lds + (size_t)w * DEPTH * SB;
+  unsigned char *stage = cr_lds + (size_t)4 * DEPTH * SB + (size_t)w * 2048;
+  int off[FC_MAX_OUT];
+  {
+    int o = 0;
+#pragma unroll
+    for (int c = 0; c < FC_MAX_OUT; c++) {
+      off[c] = o;
+      if (c < D.nout) o += D.ow[c] * 256;
+    }
+  }
+  const uint64_t lt = (1ull << lane) - 1;
+  const int64_t nsteps = n >> 8, nchunks = (nsteps + FC_CHUNK - 1) / FC_CHUNK;
+  const int64_t nw = (int64_t)gridDim.x * 4, wv = (int64_t)blockIdx.x * 4 + w;
+  auto issue = [&](int64_t p, int d) {
+    int64_t q = cc_step<FC_CHUNK>(p, wv, nw, nchunks, nsteps);
+    if (q < 0) q = 0;
+    unsigned char *dst = ring + d * SB;
+#pragma unroll
+    for (int c = 0; c < FC_MAX_OUT; c++) {
+      if (c >= D.nout) break;
+      const int B = D.ow[c] * 256;
+      const unsigned char *src = (const unsigned char *)D.src[c] + q * B;
+      __builtin_amdgcn_global_load_lds((const void *)(src + lane * 16), (void *)(dst + off[c]), 16, 0, 2);
+      if (B == 2048)
+        __builtin_amdgcn_global_load_lds((const void *)(src + 1024 + lane * 16), (void *)(dst + off[c] + 1024), 16, 0, 2);
+    }
+  };
+  if (wv < nchunks) {
+#pragma unroll
+    for (int d = 0; d < DEPTH; d++) issue(d, d);
+    int k = 0;
+    int64_t run = 0;
+    for (int64_t p = 0;; p++) {
+      const int64_t c = wv + (p / FC_CHUNK) * nw;
+      if (c >= nchunks) break;
+      const int64_t st = c * FC_CHUNK + p % FC_CHUNK;
+      if (p % FC_CHUNK == 0) run = offs[c * stride];
+      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NLD * (DEPTH - 1)) : "memory");
+      const unsigned char *src = ring + k * SB;
+      int64_t v[FC_MAX_OUT][4];
+#pragma unroll
+      for (int c2 = 0; c2 < FC_MAX_OUT; c2++) {
+        if (c2 >= D.nout) break;
+        sl_read4(src + off[c2], D.ow[c2], lane, v[c2]);
+      }
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      issue(p + DEPTH, k);
+      k = k + 1 == DEPTH ? 0 : k + 1;
+      if (st >= nsteps) continue;  // wave-uniform: past the last full step
+      bool ok[4] = {true, true, true, true};
+#pragma unroll
+      for (int j = 0; j < FM_MAX; j++) {
+        if (j >= D.npred) break;
+        int64_t pv[4];
+#pragma unroll
+        for (int e = 0; e < 4; e++) {
+          // the predicate's column among the outputs (a uniform index)
+          int64_t x = v[0][e];
+#pragma unroll
+          for (int c2 = 1; c2 < FC_MAX_OUT; c2++)
+            if (c2 == D.pred_out[j]) x = v[c2][e];
+          pv[e] = x;
+        }
+#pragma unroll
+        for (int e = 0; e < 4; e++) ok[e] = ok[e] && (uint64_t)(pv[e] - D.pred_lo[j]) <= D.pred_span[j];
+      }
+      const unsigned long long b0 = __ballot(ok[0]), b1 = __ballot(ok[1]), b2 = __ballot(ok[2]), b3 = __ballot(ok[3]);
+      const int cnt = __popcll(b0) + __popcll(b1) + __popcll(b2) + __popcll(b3);
+      if (cnt == 0) continue;
+      const unsigned m = (unsigned)ok[0] | (unsigned)ok[1] << 1 | (unsigned)ok[2] << 2 | (unsigned)ok[3] << 3;
+      const int r0 = __popcll(b0 & lt) + __popcll(b1 & lt) + __popcll(b2 & lt) + __popcll(b3 & lt);
+#pragma unroll
+      for (int c2 = 0; c2 < FC_MAX_OUT; c2++) {
+        if (c2 >= D.nout) break;
+        int r = r0;
+        if (D.ow[c2] == 8) {
+#pragma unroll
+          for (int e = 0; e < 4; e++)
+            if ((m >> e) & 1u) ((int64_t *)stage)[r++] = v[c2][e];
+          asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+          int64_t *dst = (int64_t *)D.dst[c2] + run;
+          for (int i = lane; i < cnt; i += 64) dst[i] = ((const int64_t *)stage)[i];
+        } else {
+#pragma unroll
+          for (int e = 0; e < 4; e++)
+            if ((m >> e) & 1u) ((int32_t *)stage)[r++] = (int32_t)v[c2][e];
+          asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+          int32_t *dst = (int32_t *)D.dst[c2] + run;
+          for (int i = lane; i < cnt; i += 64) dst[i] = ((const int32_t *)stage)[i];
+        }
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      }
+      run += cnt;
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
+  // the partial last step: block 0, wave 0, guarded loads, after every chunk
+  if (blockIdx.x == 0 && w == 0 && (n & 255)) {
+    bool ok[4];
+    const int64_t i0 = (nsteps << 8) + 4 * lane;
+#pragma unroll
+    for (int e = 0; e < 4; e++) {
+      const int64_t i = i0 + e;
+      ok[e] = i < n;
+      for (int j = 0; j < D.npred && ok[e]; j++) {
+        const int c = D.pred_out[j];
+        const int64_t x = D.ow[c] == 8 ? ((const int64_t *)D.src[c])[i] : (int64_t)((const int32_t *)D.src[c])[i];
+        ok[e] = (uint64_t)(x - D.pred_lo[j]) <= D.pred_span[j];
+      }
+    }
+    unsigned long long bb[4];
+#pragma unroll
+    for (int e = 0; e < 4; e++) bb[e] = __ballot(ok[e]);
+    int64_t pos = offs[nchunks * stride] + __popcll(bb[0] & lt) + __popcll(bb[1] & lt) + __popcll(bb[2] & lt) +
+                  __popcll(bb[3] & lt);
+    for (int e = 0; e < 4; e++) {
+      if (!ok[e]) continue;
+      for (int c = 0; c < D.nout; c++) {
+        if (D.ow[c] == 8) ((int64_t *)D.dst[c])[pos] = ((const int64_t *)D.src[c])[i0 + e];
+        else ((int32_t *)D.dst[c])[pos] = ((const int32_t *)D.src[c])[i0 + e];
+      }
+      pos++;
+    }
+  }
+}
+
+void CompactRecompute(const CompactDesc &d, int64_t nrows, const int64_t *chunk_offsets, hipStream_t s) {
+  int nld = 0;
+  for (int c = 0; c < d.nout; c++) {
+    if (d.ow[c] != 4 && d.ow[c] != 8) throw std::runtime_error("CompactRecompute: outputs must be 4 or 8 bytes");
+    nld += d.ow[c] / 4;
+  }
+  if (nld < 1 || nld > 8 || d.npred < 1 || d.npred > FM_MAX) throw std::runtime_error("CompactRecompute: shape");
+  int gpc = 3;
+  if (const char *e = getenv("MBX_CR_BLOCKS_PER_CU")) gpc = atoi(e) > 0 ? atoi(e) : 3;
+  const int64_t chunks = CountChunks(nrows);
+  int64_t grid = (int64_t)NumCUs() * gpc;
+  if (grid > chunks / 4 + 1) grid = chunks / 4 + 1;
+  int dp = 0;
+  if (const char *e = getenv("MBX_CR_DEPTH")) dp = atoi(e);
+#define CR(L, DP)                                                                                               \
+  hipLaunchKernelGGL((compact_recomp_lds_kernel<L, DP>), dim3((unsigned)grid), dim3(256),                      \
+                     (size_t)4 * DP * L * 1024 + 4 * 2048, s, d, nrows, chunk_offsets, FC_CHUNK / FkChunk())
+#define CRD(L, DEF) \
+  if ((dp ? dp : DEF) <= 2) CR(L, 2); else if ((dp ? dp : DEF) <= 3) CR(L, 3); else if ((dp ? dp : DEF) <= 4) CR(L, 4); else CR(L, 6);
+  switch (nld) {
+    case 1: CRD(1, 6); break;
+    case 2: CRD(2, 3); break;
+    case 3: CRD(3, 2); break;
+    case 4: CRD(4, 2); break;
+    case 5: CR(5, 2); break;
+    case 6: CR(6, 2); break;
+    case 7: CR(7, 2); break;
+    default: CR(8, 2); break;
+  }
+#undef CRD
+#undef CR
+  (void)hipGetLastError();
+}
+
+}  // namespace dev
+}  // namespace mbx

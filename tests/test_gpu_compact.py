@@ -1,8 +1,12 @@
-"""Filter -> compaction (dev::FilterBits + scan + dev::CompactColumns) against
-the CPU oracle's generator arrays and against the VM path (MBX_FC=0): the
-selected rows of every output column, in row order, bit for bit.  Sizes
-straddle the 256-row step and the ring's grid-stride (partial last step,
-one-row tail, many steps)."""
+"""Filter -> compaction against the CPU oracle's generator arrays: the
+count-first two-pass form (dev::FilterCountChunks + scan +
+dev::CompactRecompute, when every predicate column is an output), the
+ballot-bits two-pass form (dev::FilterBits + scan + dev::CompactColumns;
+MBX_CC=0), the one-pass look-back kernel (dev::SelectCompact; MBX_SL=1) and
+the VM path (MBX_FC=0) must all give the selected rows of every output
+column, in row order, bit for bit.  Sizes straddle the 256-row step,
+the one-pass tile (16 steps) and the ring's grid-stride (partial last step,
+one-row tail, many tiles per workgroup)."""
 import numpy as np
 import pytest
 
@@ -10,7 +14,7 @@ from conftest import one, q
 
 pytestmark = pytest.mark.gpu
 
-SIZES = [1, 2, 255, 256, 257, 4097, 12_289, 1_000_003]
+SIZES = [1, 2, 255, 256, 257, 4095, 4096, 4097, 12_289, 1_000_003, 30_000_017]
 
 
 def _col(conn, sql, kind, idx=0):
@@ -47,10 +51,13 @@ def test_filter_compact_parity(conn, oracle, monkeypatch, n):
         for i, (kind, arr) in enumerate(cols):
             got = _col(conn, sql, kind, i)
             assert np.array_equal(got, arr[m].astype(got.dtype)), (n, sql, i)
-        monkeypatch.setenv("MBX_FC", "0")  # the two-pass VM path gives the same bits
-        for i, (kind, _) in enumerate(cols):
-            assert np.array_equal(_col(conn, sql, kind, i), _col(conn, sql, kind, i)), (n, sql)
-        monkeypatch.delenv("MBX_FC")
+        # the bits form, the one-pass form, then the VM path: the same rows
+        for env, val in (("MBX_CC", "0"), ("MBX_SL", "1"), ("MBX_FC", "0")):
+            monkeypatch.setenv(env, val)
+            for i, (kind, arr) in enumerate(cols):
+                got = _col(conn, sql, kind, i)
+                assert np.array_equal(got, arr[m].astype(got.dtype)), (n, sql, i, env)
+            monkeypatch.delenv(env)
     # nothing passes: typed empty result
     r = q(conn, "SELECT x, k FROM fc WHERE x > 100")
     assert r.rows == [] and r.column_types == ["BigInt", "Integer"]
@@ -77,16 +84,57 @@ def test_filter_compact_decimal_predicate(conn, oracle):
     assert np.array_equal(got, np.flatnonzero((x >= 25) & (x < 30)))
 
 
-def test_filter_compact_runs_the_hip_passes(mbx, oracle):
+def test_filter_compact_runs_the_hip_passes(mbx, oracle, monkeypatch):
     cfg = mbx.Config.create()
     cfg.set("mbx_profile", "true")
     c = mbx.connect_with_config(cfg).value
     n = 200_003
     x, k, v, s = _table(c, oracle, n)
+    # a predicate column (x) that is not an output: ballot bits between the passes
     got = _col(c, "SELECT v, k FROM fc WHERE x > 24 AND k < 16", "int64")
     names = [kk["name"] for kk in c.last_profile()["kernels"]]
     assert "filter_bits" in names and "compact" in names, names
     assert np.array_equal(got, v[(x > 24) & (k < 16)])
+    # every predicate column is an output: per-chunk counts, predicates re-evaluated in pass 2
+    got = _col(c, "SELECT k, x FROM fc WHERE x > 24 AND k < 16", "int32")
+    names = [kk["name"] for kk in c.last_profile()["kernels"]]
+    assert "filter_count" in names and "compact" in names and "filter_bits" not in names, names
+    assert np.array_equal(got, k[(x > 24) & (k < 16)])
+    monkeypatch.setenv("MBX_SL", "1")
+    got = _col(c, "SELECT v, k FROM fc WHERE x > 24 AND k < 16", "int64")
+    names = [kk["name"] for kk in c.last_profile()["kernels"]]
+    assert "select" in names and "filter_bits" not in names, names  # one pass (opt-in)
+    assert np.array_equal(got, v[(x > 24) & (k < 16)])
+    c.close()
+
+
+@pytest.mark.parametrize("nbuf,gpc", [(2, 1), (3, 1), (4, 1), (2, 2), (3, 4)])
+def test_select_one_pass_launch_shapes(mbx, oracle, monkeypatch, nbuf, gpc):
+    """Every ring depth / workgroups-per-CU shape of the one-pass kernel over
+    many tiles per workgroup (ticket reuse, look-back windows longer than 64
+    tiles) and the 1..4-column loaded sets (NI 1..8): exact rows in order."""
+    monkeypatch.setenv("MBX_SL", "1")
+    monkeypatch.setenv("MBX_SL_NBUF", str(nbuf))
+    monkeypatch.setenv("MBX_SL_BLOCKS_PER_CU", str(gpc))
+    cfg = mbx.Config.create()
+    cfg.set("mbx_profile", "true")
+    c = mbx.connect_with_config(cfg).value
+    n = 20_000_077
+    x, k, v, s = _table(c, oracle, n)
+    cases = [
+        ("SELECT k FROM fc WHERE k < 5", k < 5, [("int32", k)]),
+        ("SELECT x FROM fc WHERE x > 24", x > 24, [("int64", x)]),
+        ("SELECT x, k FROM fc WHERE x > 24 AND k <= 16", (x > 24) & (k <= 16), [("int64", x), ("int32", k)]),
+        ("SELECT v, x, k FROM fc WHERE v > 0 AND x < 30", (v > 0) & (x < 30),
+         [("int64", v), ("int64", x), ("int32", k)]),
+        ("SELECT k, v FROM fc WHERE x BETWEEN 10 AND 40 AND k >= 3 AND v > 0",
+         (x >= 10) & (x <= 40) & (k >= 3) & (v > 0), [("int32", k), ("int64", v)]),
+    ]
+    for sql, m, cols in cases:
+        for i, (kind, arr) in enumerate(cols):
+            got = _col(c, sql, kind, i)
+            assert "select" in [kk["name"] for kk in c.last_profile()["kernels"]], sql
+            assert np.array_equal(got, arr[m].astype(got.dtype)), (sql, i)
     c.close()
 
 
@@ -173,7 +221,8 @@ def test_filter_compact_nullable(mbx, oracle, monkeypatch, n):
         for i, (kind, arr, valid) in enumerate(cols):
             got, ok = _ncol(c, sql, kind, i)
             names = [kk["name"] for kk in c.last_profile()["kernels"]]
-            assert "filter_bits" in names, (sql, names)
+            # NULL-free loaded columns (tiny n) take the one-pass kernel
+            assert "filter_bits" in names or "select" in names, (sql, names)
             if i == 0 and not valid.all() and m.any():
                 assert "compact_validity" in names, (sql, names)
             assert np.array_equal(ok, valid[m]), (n, sql, i)
