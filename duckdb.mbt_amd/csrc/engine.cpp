@@ -308,6 +308,7 @@ ResultPtr RunParsed(Connection &c, const Statement &st, const std::vector<Value>
         ThrowError("Catalog", "Table with name " + st.table + " does not exist!");
       }
       c.catalog.tables.erase(key);
+      for (auto &sc : c.shards) sc->catalog.tables.erase(key);  // the parts of a sharded table
       return std::make_shared<MaterializedResult>();
     }
   }

@@ -41,6 +41,12 @@ struct Table {
   std::vector<DevColumn> cols;
   int64_t nrows = 0;
   int device = 0;
+  // Sharded table (a connection opened with "gpu_devices"): part i holds a
+  // contiguous run of rows on shard i's device; the table's row order is part
+  // 0's rows, then part 1's, ...  `cols` then carries only names and types, and
+  // nrows is the sum over the parts.
+  std::vector<std::shared_ptr<Table>> parts;
+  bool sharded() const { return !parts.empty(); }
   ~Table();
 };
 typedef std::shared_ptr<Table> TablePtr;
@@ -96,6 +102,13 @@ struct Options {
   int threads = 0;            // "threads" (accepted; CPU-side only)
   bool allow_no_gpu = false;  // "mbx_allow_no_gpu": host-constant queries only (tests)
   int64_t appender_flush_rows = 1 << 20;  // "mbx_appender_flush_rows"
+  // "gpu_devices": a comma-separated device list (or "all"); two or more
+  // entries shard every table across them (a device may repeat: two shards on
+  // one GPU, for tests)
+  std::vector<int> devices;
+  // "mbx_shard_rows": appends fill part i of a sharded table up to this many
+  // rows before moving on to part i + 1 (0: appends go to the last part)
+  int64_t shard_rows = 0;
   std::map<std::string, std::string> raw;
 };
 
@@ -107,8 +120,16 @@ struct Connection {
   std::shared_ptr<Engine> engine;
   QueryProfile last_profile;
   std::vector<QueryProfile::Kernel> profile_history;  // drained by duckdb_mbx_profile_drain
+  // gpu_devices: one shard connection (own device, stream, pool and catalog of
+  // the table parts) per entry; this connection's engine (on the first device)
+  // combines their results
+  std::vector<std::unique_ptr<Connection>> shards;
+  bool sharded() const { return !shards.empty(); }
   ~Connection();
 };
+// Opens the shard connections of c (opts.devices) and enables peer access
+// between their devices.
+void OpenShards(Connection &c);
 
 // A SELECT result left on the device; streams copy it back in batches.
 struct DeviceResult;
@@ -138,6 +159,8 @@ std::shared_ptr<Engine> CreateEngine(int device, bool allow_no_gpu);
 ResultPtr ExecuteSelect(Connection &c, const BoundSelect &s);
 DeviceResultPtr ExecuteSelectDevice(Connection &c, const BoundSelect &s, StreamSource *meta);
 void ExecuteInsertSelect(Connection &c, Table &t, const BoundSelect &s, const std::vector<int> &col_map);
+// A table of c: on a sharded connection its parts are created on every shard
+// (and registered in the shards' catalogs under the same name).
 TablePtr CreateDeviceTable(Connection &c, const std::string &name, const std::vector<std::string> &names,
                            const std::vector<LogicalType> &types);
 void DropDeviceTable(Table &t);

@@ -15,6 +15,7 @@
 #include <cstring>
 #include <functional>
 #include <map>
+#include <mutex>
 #include <sstream>
 #include <thread>
 
@@ -149,6 +150,9 @@ struct Engine {
   std::vector<long long *> stat_slots;  // free pinned 3-value slots
   bool profile = false;
   std::vector<ProfEvent> events;
+  // kernels timed on shard engines during this query (gpu_devices)
+  std::mutex shard_mu;
+  std::vector<QueryProfile::Kernel> shard_kernels;
   std::vector<std::pair<hipEvent_t, hipEvent_t>> ev_pool;  // reused across queries
   size_t ev_used = 0;
   std::string plan_text;
@@ -2462,7 +2466,10 @@ static DRel SourceRel(Engine &e, Connection &c, const BoundSource &src) {
   return r;
 }
 
+static DRel ShardedBranch(Engine &e, Connection &c, const BoundSelect &s);
+
 static DRel RunBranch(Engine &e, Connection &c, const BoundSelect &s) {
+  if (s.src.kind == BoundSource::TABLE && s.src.table && s.src.table->sharded()) return ShardedBranch(e, c, s);
   if (IsHostConstantSelect(s) && s.union_all.empty()) {
     ResultPtr hr = HostConstantSelect(s);
     DRel r;
@@ -2610,7 +2617,10 @@ static void FinishProfile(Connection &c, Engine &e, double total_ms) {
   p.kernels.clear();
   p.total_ms = total_ms;
   p.plan = e.plan_text;
-  if (!e.profile) return;
+  if (!e.profile) {
+    e.shard_kernels.clear();
+    return;
+  }
   hipStreamSynchronize(e.stream);
   for (auto &ev : e.events) {
     float ms = 0;
@@ -2623,6 +2633,11 @@ static void FinishProfile(Connection &c, Engine &e, double total_ms) {
     p.kernels.push_back(k);
     if (c.profile_history.size() < 100000) c.profile_history.push_back(k);
   }
+  for (auto &k : e.shard_kernels) {
+    p.kernels.push_back(k);
+    if (c.profile_history.size() < 100000) c.profile_history.push_back(k);
+  }
+  e.shard_kernels.clear();
   e.events.clear();
   e.ev_used = 0;
 }
@@ -2729,6 +2744,26 @@ Table::~Table() {
 
 TablePtr CreateDeviceTable(Connection &c, const std::string &name, const std::vector<std::string> &names,
                            const std::vector<LogicalType> &types) {
+  if (c.sharded()) {
+    auto t = std::make_shared<Table>();
+    t->name = name;
+    t->col_names = names;
+    t->device = c.engine->device;
+    for (auto &ty : types) {
+      DevColumn dc;
+      dc.type = ty;
+      dc.phys = PhysOf(ty);
+      t->cols.push_back(dc);
+    }
+    std::string key = name;
+    for (auto &ch : key) ch = (char)tolower((unsigned char)ch);
+    for (auto &sc : c.shards) {
+      TablePtr p = CreateDeviceTable(*sc, name, names, types);
+      sc->catalog.tables[key] = p;
+      t->parts.push_back(p);
+    }
+    return t;
+  }
   auto t = std::make_shared<Table>();
   t->name = name;
   t->col_names = names;
@@ -2886,7 +2921,11 @@ static void AppendDRel(Engine &e, Table &t, const DRel &r, const std::vector<int
   t.nrows = old + n;
 }
 
+static void AppendCast(Engine &e, Table &t, DRel r, const std::vector<int> &col_map);
+static void ShardedInsertSelect(Connection &c, Table &t, const BoundSelect &s, const std::vector<int> &col_map);
+
 void ExecuteInsertSelect(Connection &c, Table &t, const BoundSelect &s, const std::vector<int> &col_map) {
+  if (t.sharded()) return ShardedInsertSelect(c, t, s, col_map);
   Engine &e = Eng(c);
   e.profile = false;
   DRel r;
@@ -2901,6 +2940,12 @@ void ExecuteInsertSelect(Connection &c, Table &t, const BoundSelect &s, const st
   } else {
     r = RunSelectDev(e, c, s);
   }
+  AppendCast(e, t, r, col_map);
+}
+
+// r's columns (col_map[table column] = column of r, or -1) cast to the table
+// types on the device where they differ, then appended
+static void AppendCast(Engine &e, Table &t, DRel r, const std::vector<int> &col_map) {
   // cast columns to the table types on device when they differ
   std::vector<BExprPtr> casts;
   bool need = false;
@@ -2937,6 +2982,467 @@ void ExecuteInsertSelect(Connection &c, Table &t, const BoundSelect &s, const st
     AppendDRel(e, t, r, col_map);
   }
   CheckError(e);
+}
+
+
+// ---------------------------------------------------------------------------
+// sharded tables (gpu_devices): every table is split into contiguous row runs,
+// one per shard connection (own device, stream, pool).  A query over a sharded
+// table runs its scan -> filter -> (partial) aggregate on every shard at once,
+// each on its own host thread, and this connection's engine combines:
+//   * aggregates: each shard computes decomposable partials per group
+//     (COUNT, SUM as int128/DECIMAL(38)/DOUBLE, MIN, MAX; AVG as SUM + COUNT),
+//     copied back in one small D2H each and merged exactly on the host, then
+//     HAVING / outputs / ORDER BY / LIMIT run on the combining device;
+//   * row results: each shard's rows are copied device to device (xGMI peer
+//     DMA between different devices) and concatenated in part order.
+// The cross-process form of the same combine (one process per GPU) is the
+// RCCL all-reduce / all-gather in distributed.py.
+// ---------------------------------------------------------------------------
+static void ForShards(Connection &c, const std::function<void(int)> &f) {
+  const int n = (int)c.shards.size();
+  std::vector<std::exception_ptr> errs(n);
+  std::vector<std::thread> th;
+  th.reserve(n);
+  for (int i = 0; i < n; i++)
+    th.emplace_back([&, i] {
+      try {
+        f(i);
+      } catch (...) {
+        errs[i] = std::current_exception();
+      }
+    });
+  for (auto &t : th) t.join();
+  for (auto &x : errs)
+    if (x) std::rethrow_exception(x);
+}
+
+static Engine &ShardEngine(Connection &top, Connection &sc) {
+  Engine &se = Eng(sc);
+  se.profile = top.opts.profile;
+  se.events.clear();
+  se.ev_used = 0;
+  return se;
+}
+
+// a shard's work is done: wait for it, raise its device errors, and hand its
+// kernel timings to the combining engine's profile
+static void ShardCollect(Engine &top, Engine &se) {
+  HIPCHK(hipStreamSynchronize(se.stream));
+  CheckError(se);
+  if (!se.profile) return;
+  std::vector<QueryProfile::Kernel> ks;
+  for (auto &ev : se.events) {
+    float ms = 0;
+    hipEventElapsedTime(&ms, ev.a, ev.b);
+    QueryProfile::Kernel k;
+    k.name = ev.name;
+    k.ms = ms;
+    k.bytes = ev.bytes;
+    k.rows = ev.rows;
+    ks.push_back(k);
+  }
+  se.events.clear();
+  se.ev_used = 0;
+  std::lock_guard<std::mutex> g(top.shard_mu);
+  top.shard_kernels.insert(top.shard_kernels.end(), ks.begin(), ks.end());
+}
+
+// r (on src's device, src's stream idle) as buffers of dst's device
+static DRel MoveRel(Engine &dst, Engine &src, const DRel &r) {
+  if (dst.device == src.device) return r;  // same device: readers copy from it directly
+  DRel out;
+  out.n = r.n;
+  const int64_t n = r.n;
+  for (auto &c : r.cols) {
+    DCol d;
+    d.type = c.type;
+    d.phys = c.phys;
+    auto peer = [&](const void *sp, size_t bytes) -> void * {
+      auto b = Alloc(dst, std::max<size_t>(bytes, 16));
+      if (bytes) HIPCHK(hipMemcpyPeerAsync(b->p, dst.device, sp, src.device, bytes, dst.stream));
+      d.owners.push_back(b);
+      return b->p;
+    };
+    if (c.phys == P_STR) {
+      d.offsets = (int64_t *)peer(c.offsets, (size_t)(n + 1) * 8);
+      d.chars = (char *)peer(c.chars, (size_t)c.chars_len);
+      d.chars_len = c.chars_len;
+    } else if (c.data) {
+      d.data = peer(c.data, (size_t)n * PhysSize(c.phys));
+    }
+    if (c.validity) d.validity = (uint64_t *)peer(c.validity, (size_t)Words64(n) * 8);
+    out.cols.push_back(d);
+  }
+  HIPCHK(hipStreamSynchronize(dst.stream));
+  return out;
+}
+
+// every row of a sharded table on e's device, in part order (the fallback for
+// shapes the partial aggregation does not decompose)
+static DRel GatherShards(Engine &e, Connection &c, const Table &t) {
+  std::vector<DRel> parts(t.parts.size());
+  for (size_t i = 0; i < t.parts.size(); i++) {
+    const Table &p = *t.parts[i];
+    DRel r;
+    r.n = p.nrows;
+    for (auto &col : p.cols) r.cols.push_back(ColFromTable(col));
+    Engine &se = Eng(*c.shards[i]);
+    HIPCHK(hipStreamSynchronize(se.stream));
+    parts[i] = MoveRel(e, se, r);
+  }
+  Eng(c);  // back on the combining device
+  return ConcatRels(e, parts);
+}
+
+static LogicalType SumTypeOf(const LogicalType &at) {
+  if (at.id == T_DECIMAL) return LogicalType::Decimal(38, at.scale);
+  if (at.id == T_FLOAT || at.id == T_DOUBLE) return LogicalType(T_DOUBLE);
+  return LogicalType(T_HUGEINT);
+}
+
+// the per-shard partial select of an aggregate branch: the same source,
+// WHERE and groups; aggregates decomposed; outputs = the whole aggregate
+// relation.  false when an aggregate does not decompose (COUNT(DISTINCT)).
+static bool PartialSelect(const BoundSelect &s, BoundSelect &p, std::vector<int> &first) {
+  p = s;
+  p.having.reset();
+  p.order.clear();
+  p.limit = -1;
+  p.offset = 0;
+  p.union_all.clear();
+  p.distinct = false;
+  p.aggs.clear();
+  p.outputs.clear();
+  p.names.clear();
+  const int ng = (int)s.groups.size();
+  for (auto &a : s.aggs) {
+    if (a.distinct) return false;
+    first.push_back(ng + (int)p.aggs.size());
+    if (a.kind == A_AVG) {
+      AggSpec sum = a, cnt = a;
+      sum.kind = A_SUM;
+      sum.type = SumTypeOf(a.arg->type);
+      cnt.kind = A_COUNT;
+      cnt.type = LogicalType(T_BIGINT);
+      p.aggs.push_back(sum);
+      p.aggs.push_back(cnt);
+    } else {
+      p.aggs.push_back(a);
+    }
+  }
+  for (int j = 0; j < ng + (int)p.aggs.size(); j++) {
+    auto col = std::make_shared<BExpr>();
+    col->kind = BExpr::COL;
+    col->col = j;
+    col->type = j < ng ? s.groups[j]->type : p.aggs[j - ng].type;
+    p.outputs.push_back(col);
+    p.names.push_back("__p" + std::to_string(j));
+  }
+  return true;
+}
+
+// int128 -> double exactly as the emit kernel's AVG does (through the magnitude)
+static double I128ToDoubleLikeDevice(i128 v) {
+  const bool neg = v < 0;
+  const u128 m = neg ? (u128)0 - (u128)v : (u128)v;
+  const uint64_t hi = (uint64_t)(m >> 64), lo = (uint64_t)m;
+  const double d = hi == 0 ? (double)lo : (double)hi * 18446744073709551616.0 + (double)lo;
+  return neg ? -d : d;
+}
+
+static int CompareValues(const Value &a, const Value &b) {  // non-NULL values of one type
+  switch (ClassOf(a.type)) {
+    case VC_F64: return a.d < b.d ? -1 : a.d > b.d ? 1 : 0;
+    case VC_STR: return a.s < b.s ? -1 : a.s > b.s ? 1 : 0;
+    default: return a.i < b.i ? -1 : a.i > b.i ? 1 : 0;
+  }
+}
+
+static void KeyBytes(const Value &v, std::string &out) {
+  out.push_back(v.is_null ? '\0' : '\1');
+  if (v.is_null) return;
+  switch (ClassOf(v.type)) {
+    case VC_F64: out.append((const char *)&v.d, 8); break;
+    case VC_STR: {
+      const uint64_t n = v.s.size();
+      out.append((const char *)&n, 8);
+      out += v.s;
+      break;
+    }
+    default: out.append((const char *)&v.i, 16); break;
+  }
+  if (v.type.id == T_INTERVAL) out.append((const char *)&v.iv, sizeof(v.iv));
+}
+
+static DRel ShardedAggregate(Engine &e, Connection &c, const BoundSelect &s, const BoundSelect &p,
+                             const std::vector<int> &first) {
+  const Table &t = *s.src.table;
+  const int nsh = (int)t.parts.size(), ng = (int)s.groups.size();
+  std::vector<ResultPtr> partial(nsh);
+  ForShards(c, [&](int i) {
+    Connection &sc = *c.shards[i];
+    Engine &se = ShardEngine(c, sc);
+    BoundSelect pi = p;
+    pi.src.table = t.parts[i];
+    DRel r = RunBranch(se, sc, pi);
+    partial[i] = ToHost(se, r, pi.names, 0, -1, pi.names.size());
+    ShardCollect(e, se);
+  });
+  Eng(c);
+  // merge by group key, exactly (int128 sums)
+  struct Acc {
+    int64_t cnt = 0;
+    bool has = false;
+    i128 si = 0;
+    double sd = 0;
+    Value mv;
+  };
+  std::map<std::string, size_t> index;
+  std::vector<std::vector<Value>> keys;
+  std::vector<std::vector<Acc>> accs;
+  std::string kb;
+  for (int i = 0; i < nsh; i++) {
+    const MaterializedResult &m = *partial[i];
+    for (int64_t row = 0; row < m.nrows; row++) {
+      kb.clear();
+      std::vector<Value> kv;
+      for (int g = 0; g < ng; g++) {
+        kv.push_back(m.cols[g].Get(row));
+        KeyBytes(kv.back(), kb);
+      }
+      auto it = index.find(kb);
+      size_t gi;
+      if (it == index.end()) {
+        gi = keys.size();
+        index.emplace(kb, gi);
+        keys.push_back(kv);
+        accs.emplace_back(s.aggs.size());
+      } else {
+        gi = it->second;
+      }
+      for (size_t q = 0; q < s.aggs.size(); q++) {
+        const AggSpec &a = s.aggs[q];
+        Acc &A = accs[gi][q];
+        const Value v = m.cols[first[q]].Get(row);
+        switch (a.kind) {
+          case A_COUNT_STAR:
+          case A_COUNT: A.cnt += (int64_t)v.i; break;
+          case A_SUM:
+            if (v.is_null) break;
+            A.has = true;
+            if (ClassOf(a.type) == VC_F64) A.sd += v.d;
+            else A.si += v.i;
+            break;
+          case A_MIN:
+          case A_MAX:
+            if (v.is_null) break;
+            if (!A.has || (a.kind == A_MIN ? CompareValues(v, A.mv) < 0 : CompareValues(v, A.mv) > 0)) A.mv = v;
+            A.has = true;
+            break;
+          case A_AVG: {
+            const Value n = m.cols[first[q] + 1].Get(row);
+            if (v.is_null) break;
+            A.has = true;
+            A.cnt += (int64_t)n.i;
+            if (ClassOf(SumTypeOf(a.arg->type)) == VC_F64) A.sd += v.d;
+            else A.si += v.i;
+            break;
+          }
+        }
+      }
+    }
+  }
+  // groups in key order (NULL keys last), as the direct-index paths emit them
+  std::vector<size_t> order(keys.size());
+  for (size_t i = 0; i < order.size(); i++) order[i] = i;
+  std::sort(order.begin(), order.end(), [&](size_t x, size_t y) {
+    for (int g = 0; g < ng; g++) {
+      const Value &a = keys[x][g], &b = keys[y][g];
+      if (a.is_null != b.is_null) return b.is_null;
+      if (a.is_null) continue;
+      const int r = CompareValues(a, b);
+      if (r) return r < 0;
+    }
+    return false;
+  });
+  std::vector<LogicalType> types;
+  for (auto &g : s.groups) types.push_back(g->type);
+  for (auto &a : s.aggs) types.push_back(a.type);
+  std::vector<std::vector<Value>> rows;
+  for (size_t oi : order) {
+    std::vector<Value> row = keys[oi];
+    for (size_t q = 0; q < s.aggs.size(); q++) {
+      const AggSpec &a = s.aggs[q];
+      const Acc &A = accs[oi][q];
+      Value v = Value::Null(a.type);
+      switch (a.kind) {
+        case A_COUNT_STAR:
+        case A_COUNT: v = Value::Int(T_BIGINT, A.cnt); break;
+        case A_SUM:
+          if (!A.has) break;
+          v.is_null = false;
+          if (ClassOf(a.type) == VC_F64) v.d = A.sd;
+          else v.i = A.si;
+          break;
+        case A_MIN:
+        case A_MAX:
+          if (A.has) v = A.mv;
+          break;
+        case A_AVG: {
+          if (!A.has || A.cnt == 0) break;
+          if (ClassOf(SumTypeOf(a.arg->type)) == VC_F64) {
+            v = Value::Double(A.sd / (double)A.cnt);
+          } else {
+            double div = (double)A.cnt;
+            const int scale = a.arg->type.id == T_DECIMAL ? a.arg->type.scale : 0;
+            for (int k = 0; k < scale; k++) div *= 10.0;
+            v = Value::Double(I128ToDoubleLikeDevice(A.si) / div);
+          }
+          break;
+        }
+      }
+      row.push_back(v);
+    }
+    rows.push_back(std::move(row));
+  }
+  if (ng == 0 && rows.empty()) {  // a global aggregate always has one row
+    std::vector<Value> row;
+    for (auto &a : s.aggs)
+      row.push_back(a.kind == A_COUNT_STAR || a.kind == A_COUNT ? Value::Int(T_BIGINT, 0) : Value::Null(a.type));
+    rows.push_back(row);
+  }
+  return UploadRows(e, rows, types);
+}
+
+static DRel ShardedBranch(Engine &e, Connection &c, const BoundSelect &s) {
+  const Table &t = *s.src.table;
+  if ((int)t.parts.size() != (int)c.shards.size())
+    ThrowError("Internal", "sharded table \"" + t.name + "\" does not match the connection's shards");
+  if (s.is_agg) {
+    BoundSelect p;
+    std::vector<int> first;
+    if (PartialSelect(s, p, first)) {
+      DRel agg = ShardedAggregate(e, c, s, p, first);
+      return FilterProject(e, agg, s.having, s.outputs);
+    }
+    DRel src = GatherShards(e, c, t);
+    DRel agg = Aggregate(e, src, s);
+    return FilterProject(e, agg, s.having, s.outputs);
+  }
+  // row results: filter/project on every shard, concatenated in part order
+  const int nsh = (int)t.parts.size();
+  std::vector<DRel> parts(nsh);
+  ForShards(c, [&](int i) {
+    Connection &sc = *c.shards[i];
+    Engine &se = ShardEngine(c, sc);
+    BoundSelect si = s;
+    si.src.table = t.parts[i];
+    si.union_all.clear();
+    si.order.clear();
+    si.limit = -1;
+    si.offset = 0;
+    parts[i] = RunBranch(se, sc, si);
+    ShardCollect(e, se);
+  });
+  Eng(c);
+  for (int i = 0; i < nsh; i++) parts[i] = MoveRel(e, *c.shards[i]->engine, parts[i]);
+  return ConcatRels(e, parts);
+}
+
+// the part that takes appended rows: the last non-empty part while it has room
+// (mbx_shard_rows; 0 = unbounded), else the next one -- row order stays part order
+static int TargetPart(const Connection &c, const Table &t) {
+  const int n = (int)t.parts.size();
+  int last = 0;
+  for (int i = 0; i < n; i++)
+    if (t.parts[i]->nrows > 0) last = i;
+  if (c.opts.shard_rows > 0 && t.parts[last]->nrows >= c.opts.shard_rows && last + 1 < n) return last + 1;
+  return last;
+}
+
+static void SyncRows(Table &t) {
+  int64_t n = 0;
+  for (auto &p : t.parts) n += p->nrows;
+  t.nrows = n;
+}
+
+static void ShardedInsertSelect(Connection &c, Table &t, const BoundSelect &s, const std::vector<int> &col_map) {
+  const int nsh = (int)t.parts.size();
+  bool empty = true;
+  for (auto &p : t.parts) empty = empty && p->nrows == 0;
+  const bool plain = !s.is_agg && s.union_all.empty() && s.order.empty() && s.limit < 0 && s.offset == 0 &&
+                     !s.distinct;
+  if (empty && plain && s.src.kind == BoundSource::RANGE) {
+    // generated rows: contiguous sub-ranges, one per part, built on every shard at once
+    const int64_t n = s.src.RangeCount();
+    ForShards(c, [&](int i) {
+      const int64_t lo = (int64_t)((__int128)n * i / nsh), hi = (int64_t)((__int128)n * (i + 1) / nsh);
+      BoundSelect si = s;
+      si.src.range_start = s.src.range_start + lo * s.src.range_step;
+      si.src.range_stop = s.src.range_start + hi * s.src.range_step;
+      si.src.range_inclusive = false;
+      ExecuteInsertSelect(*c.shards[i], *t.parts[i], si, col_map);
+    });
+    SyncRows(t);
+    return;
+  }
+  if (empty && plain && s.src.kind == BoundSource::TABLE && s.src.table && s.src.table->sharded() &&
+      (int)s.src.table->parts.size() == nsh) {
+    // a sharded source: every part from the same shard's part of the source
+    ForShards(c, [&](int i) {
+      BoundSelect si = s;
+      si.src.table = s.src.table->parts[i];
+      ExecuteInsertSelect(*c.shards[i], *t.parts[i], si, col_map);
+    });
+    SyncRows(t);
+    return;
+  }
+  // anything else: evaluated on the combining device, appended to the target part
+  Engine &e = Eng(c);
+  e.profile = false;
+  DRel r;
+  if (IsHostConstantSelect(s)) {
+    ResultPtr hr = HostConstantSelect(s);
+    r.n = hr->nrows;
+    for (auto &hc : hr->cols) {
+      DCol d;
+      UploadHostColumn(e, hc, hr->nrows, d);
+      r.cols.push_back(d);
+    }
+  } else {
+    r = RunSelectDev(e, c, s);
+  }
+  HIPCHK(hipStreamSynchronize(e.stream));
+  CheckError(e);
+  const int k = TargetPart(c, t);
+  Engine &se = Eng(*c.shards[k]);
+  se.profile = false;
+  AppendCast(se, *t.parts[k], MoveRel(se, e, r), col_map);
+  HIPCHK(hipStreamSynchronize(se.stream));
+  SyncRows(t);
+}
+
+void OpenShards(Connection &c) {
+  if (c.opts.devices.size() < 2) return;
+  for (int d : c.opts.devices) {
+    auto sc = std::make_unique<Connection>();
+    sc->opts = c.opts;
+    sc->opts.devices.clear();
+    sc->opts.device = d;
+    sc->engine = CreateEngine(d, false);
+    sc->catalog.device = d;
+    c.shards.push_back(std::move(sc));
+  }
+  for (int a : c.opts.devices)
+    for (int b : c.opts.devices) {
+      if (a == b) continue;
+      int can = 0;
+      hipSetDevice(a);
+      if (hipDeviceCanAccessPeer(&can, a, b) == hipSuccess && can) (void)hipDeviceEnablePeerAccess(b, 0);
+    }
+  (void)hipGetLastError();  // "already enabled" is not an error here
+  hipSetDevice(c.engine->device);
 }
 
 void HbmCalibrateConn(Connection &c, int64_t bytes, int iters, double out[3]) {
@@ -3008,6 +3514,25 @@ static void StageH2D(Engine &e, void *dst, const void *src, size_t bytes) {
 // (no intermediate device relation, no D2D append copy).
 void AppendRawColumns(Connection &c, Table &t, const std::vector<const void *> &vals,
                       const std::vector<const uint8_t *> &valid, int64_t n, bool sync) {
+  if (t.sharded()) {  // into the target part(s), split where a part fills up
+    int64_t off = 0;
+    while (off < n) {
+      const int k = TargetPart(c, t);
+      int64_t m = n - off;
+      if (c.opts.shard_rows > 0 && k + 1 < (int)t.parts.size())
+        m = std::min<int64_t>(m, std::max<int64_t>(1, c.opts.shard_rows - t.parts[k]->nrows));
+      std::vector<const void *> v2;
+      std::vector<const uint8_t *> b2;
+      for (size_t tc = 0; tc < t.cols.size(); tc++) {
+        v2.push_back((const char *)vals[tc] + (size_t)off * PhysSize(t.cols[tc].phys));
+        b2.push_back(valid[tc] ? valid[tc] + off : nullptr);
+      }
+      AppendRawColumns(*c.shards[k], *t.parts[k], v2, b2, m, sync);
+      off += m;
+      SyncRows(t);
+    }
+    return;
+  }
   Engine &e = Eng(c);
   const int64_t old = t.nrows;
   if (n <= 0) return;
@@ -3042,6 +3567,7 @@ void AppendRawColumns(Connection &c, Table &t, const std::vector<const void *> &
 
 void SettleAppends(Connection &c) {
   if (c.engine && c.engine->has_gpu) SettlePending(*c.engine);
+  for (auto &sc : c.shards) SettleAppends(*sc);
 }
 
 void *HostPinnedAlloc(size_t bytes) {
@@ -3054,6 +3580,12 @@ void HostPinnedFree(void *p) {
 }
 
 void AppendHostBatch(Connection &c, Table &t, const HostBatch &b) {
+  if (t.sharded()) {
+    const int k = TargetPart(c, t);
+    AppendHostBatch(*c.shards[k], *t.parts[k], b);
+    SyncRows(t);
+    return;
+  }
   Engine &e = Eng(c);
   DRel r;
   r.n = b.nrows;

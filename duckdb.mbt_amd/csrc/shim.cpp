@@ -173,8 +173,10 @@ static duckdb_mb_connection *OpenConn(moonbit_bytes_t path, const Options &opts)
   try {
     auto *h = new duckdb_mb_connection();
     h->conn.opts = opts;
-    h->conn.engine = CreateEngine(opts.device, opts.allow_no_gpu);
-    h->conn.catalog.device = opts.device;
+    if (opts.devices.size() >= 2) h->conn.opts.device = opts.devices[0];  // the combining device
+    h->conn.engine = CreateEngine(h->conn.opts.device, opts.allow_no_gpu);
+    h->conn.catalog.device = h->conn.opts.device;
+    if (opts.devices.size() >= 2) OpenShards(h->conn);
     (void)path;  // ":memory:" and file paths both open a volatile device-resident database
     return h;
   } catch (std::exception &e) {
@@ -386,6 +388,33 @@ int32_t duckdb_mb_config_set(duckdb_mb_config *c, moonbit_bytes_t key, moonbit_b
   if (kl == "gpu_device") {
     ok = IsInt(v, &x) && x >= 0;
     if (ok) c->opts.device = (int)x;
+  } else if (kl == "gpu_devices") {  // shard every table across these devices
+    std::vector<int> devs;
+    std::string vl = v;
+    for (auto &ch : vl) ch = (char)tolower((unsigned char)ch);
+    if (vl == "all") {
+      for (int d = 0; d < DeviceCount(); d++) devs.push_back(d);
+      ok = !devs.empty();
+    } else {
+      size_t at = 0;
+      while (ok && at <= v.size()) {
+        size_t comma = v.find(',', at);
+        if (comma == std::string::npos) comma = v.size();
+        std::string item = v.substr(at, comma - at);
+        while (!item.empty() && item.front() == ' ') item.erase(item.begin());
+        while (!item.empty() && item.back() == ' ') item.pop_back();
+        ok = IsInt(item, &x) && x >= 0 && devs.size() < 64;
+        if (ok) devs.push_back((int)x);
+        at = comma + 1;
+      }
+    }
+    if (ok) {
+      c->opts.devices = devs.size() >= 2 ? devs : std::vector<int>();
+      c->opts.device = devs[0];
+    }
+  } else if (kl == "mbx_shard_rows") {
+    ok = IsInt(v, &x) && x >= 0;
+    if (ok) c->opts.shard_rows = x;
   } else if (kl == "mbx_profile") {
     c->opts.profile = v == "true" || v == "1";
   } else if (kl == "mbx_allow_no_gpu") {

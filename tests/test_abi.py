@@ -133,6 +133,13 @@ def test_config_keys(mbx):
     bad = c.set("no_such_option", "x")
     assert isinstance(bad, mbx.Err) and bad.error.message == "duckdb_set_config failed"
     assert isinstance(c.set("threads", "abc"), mbx.Err)
+    # in-library sharding: a device list (a device may repeat), rows per part
+    assert isinstance(c.set("gpu_devices", "0,1,2,3,4,5,6,7"), mbx.Ok)
+    assert isinstance(c.set("gpu_devices", " 0, 0 "), mbx.Ok)
+    for bad_list in ("", "0,", "a,b", "0,-1", "1;2"):
+        assert isinstance(c.set("gpu_devices", bad_list), mbx.Err), bad_list
+    assert isinstance(c.set("mbx_shard_rows", "1000000"), mbx.Ok)
+    assert isinstance(c.set("mbx_shard_rows", "-1"), mbx.Err)
     r = mbx.lib.duckdb_mb_connect_with_config(mbx._Arg(":memory:").p, None)
     assert r is None and mbx._str(mbx.lib.duckdb_mb_last_error()) == "config is null"
 

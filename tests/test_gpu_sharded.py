@@ -1,0 +1,154 @@
+"""Tables sharded inside the library ("gpu_devices"): every table
+is split into contiguous row runs, one per shard, and a query over it runs on
+every shard at once and is combined by the connection's first device.  On the
+1-GPU test box the shards share device 0 ("0,0", "0,0,0"), which exercises the
+same split / per-shard kernels / combine code as distinct devices.
+
+Aggregates (C2, C5, C3 shapes) are checked against the CPU oracle; row
+results, hash GROUP BY, AVG and appender ingest against an unsharded
+connection holding the same rows."""
+import numpy as np
+import pytest
+
+from conftest import one, q
+
+pytestmark = pytest.mark.gpu
+
+
+def _conn(mbx, devices, profile=False, shard_rows=None):
+    cfg = mbx.Config.create()
+    assert isinstance(cfg.set("gpu_devices", devices), mbx.Ok)
+    if profile:
+        cfg.set("mbx_profile", "true")
+    if shard_rows is not None:
+        assert isinstance(cfg.set("mbx_shard_rows", str(shard_rows)), mbx.Ok)
+    r = mbx.connect_with_config(cfg)
+    assert isinstance(r, mbx.Ok), r.error.message
+    return r.value
+
+
+@pytest.mark.parametrize("devices", ["0,0", "0,0,0"])
+def test_sharded_c2_c5_aggregates(mbx, oracle, devices):
+    n = 50_000_017
+    c = _conn(mbx, devices, profile=True)
+    q(c, f"CREATE TABLE t AS SELECT mbx_synth(42, i, 50) + 1 AS x FROM range({n}) tbl(i)")
+    assert one(c, "SELECT COUNT(*) FROM t") == [str(n)]
+    cnt, s = oracle.synth_filter_count(42, 0, n, 50, 1, 25, 2**63 - 1, 8)
+    assert one(c, "SELECT COUNT(*) FROM t WHERE x > 24") == [str(cnt)]                 # C2
+    kinds = [k["name"] for k in c.last_profile()["kernels"]]
+    assert kinds.count("filter_agg") == devices.count(",") + 1, kinds                  # one per shard
+    got = one(c, "SELECT COUNT(*), SUM(x), MIN(x), MAX(x) FROM t WHERE x > 24")         # C5
+    assert got == [str(cnt), str(s), "25", "50"]
+    x = oracle.synth_i64(n, 42, 0, 50, 1)
+    avg = float(one(c, "SELECT AVG(x) FROM t")[0])
+    assert abs(avg - x.mean()) <= 1e-9 * abs(x.mean())
+    assert one(c, "SELECT COUNT(*), SUM(x) FROM t WHERE x > 100") == ["0", ""]  # NULL cells read as ""
+    c.close()
+
+
+def test_sharded_c3_group_by(mbx, oracle):
+    n = 40_000_003
+    c = _conn(mbx, "0,0,0")
+    q(c, f"CREATE TABLE g AS SELECT CAST(mbx_synth(7, i, 32) AS INTEGER) AS k, "
+         f"mbx_synth(9, i, 1099511627776) - 549755813888 AS v FROM range({n}) tbl(i)")
+    oc, osum = oracle.synth_groupby(7, 9, 0, n, 32, 1 << 40, -(1 << 39), 8)
+    rows = q(c, "SELECT k, SUM(v), COUNT(*) FROM g GROUP BY k").rows
+    assert rows == [[str(k), str(osum[k]), str(oc[k])] for k in range(32) if oc[k]]
+    # HAVING / ORDER BY / LIMIT over the combined groups
+    top = q(c, "SELECT k, COUNT(*) AS n FROM g GROUP BY k HAVING COUNT(*) > 0 ORDER BY n DESC, k LIMIT 3").rows
+    exp = sorted(((int(oc[k]), k) for k in range(32)), key=lambda t: (-t[0], t[1]))[:3]
+    assert top == [[str(k), str(cn)] for cn, k in exp]
+    c.close()
+
+
+def test_sharded_rows_and_hash_groups_match_unsharded(mbx):
+    n = 1_000_003
+    sql_t = (f"CREATE TABLE h AS SELECT mbx_synth(42, i, 50) + 1 AS x, "
+             f"CASE WHEN mbx_synth(5, i, 9) = 0 THEN NULL WHEN mbx_synth(3, i, 3) = 0 THEN 'apple' "
+             f"WHEN mbx_synth(3, i, 3) = 1 THEN 'kiwi' ELSE 'fig' END AS s, "
+             f"CAST(mbx_synth(11, i, 100000) - 50000 AS DECIMAL(12,2)) AS d, mbx_synth(13, i, 1000) / 7 AS f, "
+             f"i AS r FROM range({n}) tbl(i)")
+    shard = _conn(mbx, "0,0")
+    plain = mbx.connect().value
+    for c in (shard, plain):
+        q(c, sql_t)
+    queries = [
+        "SELECT r, x FROM h WHERE x > 24 AND r % 3 = 0",
+        "SELECT r FROM h WHERE x BETWEEN 10 AND 12 ORDER BY r DESC LIMIT 1000 OFFSET 5",
+        "SELECT s, COUNT(*), SUM(x), MIN(r), MAX(r) FROM h GROUP BY s ORDER BY s NULLS LAST",
+        "SELECT x % 7 AS m, s, COUNT(*) FROM h WHERE r > 100 GROUP BY m, s ORDER BY m, s",
+        "SELECT COUNT(DISTINCT x) FROM h",
+        "SELECT COUNT(s), COUNT(*), MIN(x) FROM h WHERE s IS NOT NULL",
+        "SELECT x, COUNT(*) FROM h GROUP BY x HAVING SUM(r) > 10000000000 ORDER BY x",
+        "SELECT AVG(d), SUM(d), MIN(d), MAX(d) FROM h WHERE x < 30",
+    ]
+    for sql in queries:
+        a, b = q(shard, sql), q(plain, sql)
+        assert a.column_types == b.column_types, sql
+        assert a.rows == b.rows, sql
+    # DOUBLE sums: summation order differs between shards (stated tolerance 1e-9 relative)
+    a, b = q(shard, "SELECT SUM(f), AVG(f), MIN(f), MAX(f) FROM h").rows[0], q(plain, "SELECT SUM(f), AVG(f), MIN(f), MAX(f) FROM h").rows[0]
+    for u, w in zip(a, b):
+        assert abs(float(u) - float(w)) <= 1e-9 * abs(float(w)), (a, b)
+    # stream read-back of a sharded SELECT: same rows in the same order
+    st = shard.query_stream("SELECT r FROM h WHERE x > 40").value
+    got = []
+    while True:
+        r = st.next().value
+        if r is None:
+            break
+        got.extend(int(row[0]) for row in r.rows)
+    st.close()
+    assert got == [int(r[0]) for r in q(plain, "SELECT r FROM h WHERE x > 40").rows]
+    # CTAS from a sharded table stays sharded part by part; DROP removes every part
+    q(shard, "CREATE TABLE h2 AS SELECT r, x FROM h WHERE x > 24")
+    q(plain, "CREATE TABLE h2 AS SELECT r, x FROM h WHERE x > 24")
+    assert one(shard, "SELECT COUNT(*), SUM(r) FROM h2") == one(plain, "SELECT COUNT(*), SUM(r) FROM h2")
+    q(shard, "DROP TABLE h2")
+    assert isinstance(shard.query("SELECT COUNT(*) FROM h2"), mbx.Err)
+    shard.close()
+    plain.close()
+
+
+def test_sharded_appender_fills_parts_in_order(mbx):
+    # mbx_shard_rows = 300 000: 1 000 000 appended rows land 300k / 300k / 400k
+    # over three parts; the table reads back in append order
+    c = _conn(mbx, "0,0,0", shard_rows=300_000)
+    q(c, "CREATE TABLE a (v BIGINT, w INTEGER)")
+    n = 1_000_000
+    v = (np.arange(n, dtype=np.int64) * 2654435761) & (2**62 - 1)
+    w = (np.arange(n) % 1000).astype(np.int32)
+    ap = c.create_appender("main", "a").value
+    for s0 in range(0, n, 250_000):
+        ap.append_column(0, v[s0:s0 + 250_000])
+        ap.append_column(1, w[s0:s0 + 250_000])
+        assert isinstance(ap.commit(250_000), mbx.Ok)
+    ap.close()
+    # the row-wise appender and INSERT go to the last part
+    ap = c.create_appender("main", "a").value
+    for i in range(5):
+        ap.begin_row()
+        ap.append_bigint(-i)
+        ap.append_int(i)
+        ap.end_row()
+    ap.close()
+    q(c, "INSERT INTO a VALUES (7, 7), (NULL, 8)")
+    got = c.query_arrow("SELECT v FROM a LIMIT 1000000").value
+    assert np.array_equal(np.frombuffer(got.raw_int64_bytes(0)[4:], dtype=np.int64), v)
+    got.close()
+    assert q(c, "SELECT v, w FROM a OFFSET 1000000").rows == \
+        [[str(-i), str(i)] for i in range(5)] + [["7", "7"], ["", "8"]]
+    assert one(c, "SELECT COUNT(*), COUNT(v), SUM(w) FROM a") == \
+        [str(n + 7), str(n + 6), str(int(w.astype(np.int64).sum()) + 10 + 15)]
+    c.close()
+
+
+def test_sharded_empty_and_tiny_tables(mbx):
+    c = _conn(mbx, "0,0,0")
+    q(c, "CREATE TABLE e (x BIGINT)")
+    assert one(c, "SELECT COUNT(*), SUM(x), MIN(x) FROM e") == ["0", "", ""]
+    assert q(c, "SELECT x, COUNT(*) FROM e GROUP BY x").rows == []
+    q(c, "CREATE TABLE t1 AS SELECT i AS x FROM range(2) tbl(i)")  # fewer rows than shards
+    assert q(c, "SELECT x FROM t1").rows == [["0"], ["1"]]
+    assert one(c, "SELECT SUM(x), AVG(x) FROM t1") == ["1", "0.5"]
+    c.close()
