@@ -79,6 +79,7 @@ _sig("duckdb_mbx_result_text", ctypes.c_void_p, _P, ctypes.POINTER(ctypes.c_int6
 _sig("duckdb_mbx_append_column", _I, _P, _I, _P, _P, _L)
 _sig("duckdb_mbx_append_commit", _I, _P, _L)
 _sig("duckdb_mbx_hbm_calibrate", _I, _P, _L, _I, ctypes.POINTER(ctypes.c_double))
+_sig("duckdb_mbx_statement_plan_stats", _I, _P, ctypes.POINTER(ctypes.c_int64))
 
 for _n in ["duckdb_mb_connect"]:
     _sig(_n, _P, _B)
@@ -776,6 +777,12 @@ class PreparedStatement:
 
     def clear_bindings(self):
         return self._r(lib.duckdb_mb_clear_bindings(self._h), "clear_bindings")
+
+    def plan_stats(self) -> dict:
+        """Bound-plan cache counters (extension): binds and plan reuses."""
+        out = (ctypes.c_int64 * 2)()
+        lib.duckdb_mbx_statement_plan_stats(self._h, out)
+        return {"binds": out[0], "reuses": out[1]}
 
     def execute(self, on_done: Callable = None):
         res = lib.duckdb_mb_execute_prepared(self._h)

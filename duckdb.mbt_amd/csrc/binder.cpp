@@ -11,6 +11,7 @@
 #include <cstdlib>
 #include <functional>
 #include <limits>
+#include <set>
 
 #include "engine.h"
 #include "plan.h"
@@ -729,6 +730,9 @@ struct ScopeCol {
   LogicalType type;
 };
 
+// BindSelectCapture: the constant node of every parameter reference, in bind order
+static thread_local std::vector<std::pair<BExprPtr, int>> *g_param_nodes = nullptr;
+
 struct BindCtx {
   std::vector<ScopeCol> scope;
   const std::vector<Value> *params = nullptr;
@@ -1024,6 +1028,7 @@ BExprPtr BindExprInner(const Expr &e, BindCtx &ctx) {
       Value v = (*ctx.params)[e.param_index - 1];
       auto c = MkConst(v);
       if (v.is_null) c->type = LogicalType(T_SQLNULL);
+      if (g_param_nodes) g_param_nodes->push_back({c, e.param_index - 1});
       return c;
     }
     case Expr::COLREF: {
@@ -1435,6 +1440,53 @@ std::string ExplainSelect(const BoundSelect &s, int ind) {
 TablePtr Catalog::Find(const std::string &name) const {
   auto it = tables.find(Lower(name));
   return it == tables.end() ? nullptr : it->second;
+}
+
+}  // namespace mbx
+
+namespace mbx {
+
+static void CollectExprNodes(const BExpr *e, std::set<const BExpr *> &out) {
+  if (!e || !out.insert(e).second) return;
+  for (auto &c : e->ch) CollectExprNodes(c.get(), out);
+}
+
+static void CollectPlanNodes(const BoundSelect &s, std::set<const BExpr *> &out) {
+  CollectExprNodes(s.where.get(), out);
+  CollectExprNodes(s.having.get(), out);
+  for (auto &g : s.groups) CollectExprNodes(g.get(), out);
+  for (auto &a : s.aggs) CollectExprNodes(a.arg.get(), out);
+  for (auto &o : s.outputs) CollectExprNodes(o.get(), out);
+  for (auto &o : s.order) CollectExprNodes(o.expr.get(), out);
+  if (s.src.sub) CollectPlanNodes(*s.src.sub, out);
+  for (auto &u : s.union_all) CollectPlanNodes(*u, out);
+}
+
+BoundSelectPtr BindSelectCapture(const Select &sel, Catalog &cat, const std::vector<Value> &params, bool *patchable,
+                                 std::vector<std::pair<BExprPtr, int>> *nodes) {
+  nodes->clear();
+  g_param_nodes = nodes;
+  BoundSelectPtr b;
+  try {
+    b = BindSelect(sel, cat, params);
+  } catch (...) {
+    g_param_nodes = nullptr;
+    throw;
+  }
+  g_param_nodes = nullptr;
+  // patchable when every parameter the statement has was bound into a node that
+  // is still in the plan (not folded away, not a LIMIT/VALUES/range argument)
+  std::set<const BExpr *> live;
+  CollectPlanNodes(*b, live);
+  std::vector<bool> seen(params.size(), false);
+  bool ok = true;
+  for (auto &pn : *nodes) {
+    if (!live.count(pn.first.get())) ok = false;
+    if (pn.second >= 0 && pn.second < (int)seen.size()) seen[pn.second] = true;
+  }
+  for (bool x : seen) ok = ok && x;
+  *patchable = ok;
+  return b;
 }
 
 }  // namespace mbx

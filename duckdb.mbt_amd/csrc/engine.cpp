@@ -187,14 +187,25 @@ StreamSource RunStatementStream(Connection &c, const Statement &st, const std::v
   StreamSource src;
   if (st.kind == Statement::SELECT) {
     BoundSelectPtr b = BindSelect(*st.select, c.catalog, params);
-    src.dev = ExecuteSelectDevice(c, *b, &src);
-    if (src.dev) return src;
-    src.host = ExecuteSelect(c, *b);
+    return RunBoundStream(c, *b);
   } else {
     src.host = RunParsed(c, st, params);
   }
   src.names.clear();
   src.types.clear();
+  for (auto &hc : src.host->cols) {
+    src.names.push_back(hc.name);
+    src.types.push_back(hc.type);
+  }
+  src.nrows = src.host->nrows;
+  return src;
+}
+
+StreamSource RunBoundStream(Connection &c, const BoundSelect &b) {
+  StreamSource src;
+  src.dev = ExecuteSelectDevice(c, b, &src);
+  if (src.dev) return src;
+  src.host = ExecuteSelect(c, b);
   for (auto &hc : src.host->cols) {
     src.names.push_back(hc.name);
     src.types.push_back(hc.type);
@@ -228,6 +239,7 @@ ResultPtr RunParsed(Connection &c, const Statement &st, const std::vector<Value>
           types.push_back(cd.type);
         }
         c.catalog.tables[key] = CreateDeviceTable(c, st.table, names, types);
+        c.catalog.version++;
         return std::make_shared<MaterializedResult>();
       }
       BoundSelectPtr b = BindSelect(*st.select, c.catalog, params);
@@ -247,6 +259,7 @@ ResultPtr RunParsed(Connection &c, const Statement &st, const std::vector<Value>
       for (size_t i = 0; i < types.size(); i++) map.push_back((int)i);
       ExecuteInsertSelect(c, *t, *b, map);
       c.catalog.tables[key] = t;
+      c.catalog.version++;
       return CountResult(t->nrows);
     }
     case Statement::INSERT: {
@@ -308,6 +321,7 @@ ResultPtr RunParsed(Connection &c, const Statement &st, const std::vector<Value>
         ThrowError("Catalog", "Table with name " + st.table + " does not exist!");
       }
       c.catalog.tables.erase(key);
+      c.catalog.version++;
       for (auto &sc : c.shards) sc->catalog.tables.erase(key);  // the parts of a sharded table
       return std::make_shared<MaterializedResult>();
     }

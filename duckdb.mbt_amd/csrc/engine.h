@@ -54,6 +54,7 @@ typedef std::shared_ptr<Table> TablePtr;
 struct Catalog {
   std::map<std::string, TablePtr> tables;  // lower-cased name
   int device = 0;
+  uint64_t version = 0;  // bumped by CREATE / DROP (a bound plan names TablePtrs)
   TablePtr Find(const std::string &name) const;
 };
 
@@ -142,6 +143,7 @@ struct StreamSource {
   DeviceResultPtr dev;  // device-resident SELECT result
 };
 StreamSource RunStatementStream(Connection &c, const Statement &st, const std::vector<Value> &params);
+StreamSource RunBoundStream(Connection &c, const BoundSelect &b);  // a bound SELECT as a stream source
 // rows [start, start + n) of a device result, materialized on the host
 ResultPtr FetchDeviceRows(Connection &c, DeviceResult &d, int64_t start, int64_t n);
 // Arrow wire form of a 1/4/8-byte device column, NULLs allowed: values with

@@ -85,6 +85,12 @@ struct Catalog;
 // Binds a parsed SELECT against the catalog.  `params` are the prepared
 // statement bindings (1-based index -> value); missing ones raise.
 BoundSelectPtr BindSelect(const Select &sel, Catalog &cat, const std::vector<Value> &params);
+// BindSelect that also returns the constant node each parameter was bound into
+// (node, 0-based parameter index); *patchable is true when every parameter
+// lives in such a node of the plan, so a re-execution with new values of the
+// same types may overwrite those nodes' values instead of binding again.
+BoundSelectPtr BindSelectCapture(const Select &sel, Catalog &cat, const std::vector<Value> &params, bool *patchable,
+                                 std::vector<std::pair<BExprPtr, int>> *nodes);
 
 // Host scalar evaluation for constant folding (no column references).
 Value EvalConst(const BExpr &e);

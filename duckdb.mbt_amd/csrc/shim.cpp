@@ -109,6 +109,15 @@ struct duckdb_mb_statement {
   Statement st;
   std::vector<Value> params;
   char error[256];
+  // bound-plan cache (SELECT): the plan of the last execute and the constant
+  // node of each parameter; re-executed with new values of the same types (and
+  // an unchanged catalog) by overwriting those nodes instead of binding again
+  BoundSelectPtr plan;
+  std::vector<std::pair<BExprPtr, int>> plan_params;
+  std::vector<LogicalType> plan_types;
+  std::vector<bool> plan_nulls;
+  uint64_t plan_version = 0;
+  uint64_t binds = 0, reuses = 0;  // statistics (duckdb_mbx_statement_plan_stats)
 };
 struct duckdb_mb_appender {
   duckdb_mb_connection *conn = nullptr;
@@ -502,13 +511,49 @@ int32_t duckdb_mb_clear_bindings(duckdb_mb_statement *s) {  // ref :983-989
   return 1;
 }
 
+// The bound plan of a SELECT statement for its current parameters: the cached
+// one with the parameter nodes overwritten when the parameter types and the
+// catalog are unchanged (MBX_PLAN_CACHE=0 disables), else a fresh bind.
+static BoundSelectPtr PlanFor(duckdb_mb_statement *s) {
+  Connection &c = s->conn->conn;
+  const char *pc = getenv("MBX_PLAN_CACHE");
+  const bool off = pc && atoi(pc) == 0;
+  bool same = !off && s->plan && s->plan_version == c.catalog.version && s->plan_types.size() == s->params.size();
+  for (size_t i = 0; same && i < s->params.size(); i++)
+    same = s->params[i].type == s->plan_types[i] && s->params[i].is_null == s->plan_nulls[i] &&
+           s->params[i].type.id != T_INVALID;
+  if (same) {
+    for (auto &pn : s->plan_params) pn.first->cval = CastValue(s->params[pn.second], pn.first->type);
+    s->reuses++;
+    return s->plan;
+  }
+  bool patchable = false;
+  std::vector<std::pair<BExprPtr, int>> nodes;
+  BoundSelectPtr b = BindSelectCapture(*s->st.select, c.catalog, s->params, &patchable, &nodes);
+  s->binds++;
+  s->plan.reset();
+  if (patchable && !off) {
+    s->plan = b;
+    s->plan_params = nodes;
+    s->plan_version = c.catalog.version;
+    s->plan_types.clear();
+    s->plan_nulls.clear();
+    for (auto &v : s->params) {
+      s->plan_types.push_back(v.type);
+      s->plan_nulls.push_back(v.is_null);
+    }
+  }
+  return b;
+}
+
 duckdb_mb_result *duckdb_mb_execute_prepared(duckdb_mb_statement *s) {  // ref :991-1016
   if (!s) {
     SetError("statement is null");
     return nullptr;
   }
   try {
-    ResultPtr r = RunParsed(s->conn->conn, s->st, s->params);
+    ResultPtr r = s->st.kind == Statement::SELECT ? ExecuteSelect(s->conn->conn, *PlanFor(s))
+                                                   : RunParsed(s->conn->conn, s->st, s->params);
     auto *res = new duckdb_mb_result();
     res->r = r;
     return res;
@@ -524,6 +569,7 @@ duckdb_mb_stream *duckdb_mb_execute_prepared_stream(duckdb_mb_statement *s) {  /
     return nullptr;
   }
   try {
+    if (s->st.kind == Statement::SELECT) return StreamFrom(s->conn, RunBoundStream(s->conn->conn, *PlanFor(s)));
     return StreamFrom(s->conn, RunStatementStream(s->conn->conn, s->st, s->params));
   } catch (std::exception &e) {
     SetError(e.what());
@@ -532,6 +578,13 @@ duckdb_mb_stream *duckdb_mb_execute_prepared_stream(duckdb_mb_statement *s) {  /
 }
 
 int32_t duckdb_mb_is_null_statement(duckdb_mb_statement *s) { return s == nullptr ? 1 : 0; }  // ref :1018
+
+int32_t duckdb_mbx_statement_plan_stats(duckdb_mb_statement *s, int64_t *out2) {
+  if (!s || !out2) return 0;
+  out2[0] = (int64_t)s->binds;
+  out2[1] = (int64_t)s->reuses;
+  return 1;
+}
 
 int32_t duckdb_mb_bind_date(duckdb_mb_statement *s, int32_t i, int32_t days) {  // ref :1261
   return Bind(s, i, Value::Int(T_DATE, days));

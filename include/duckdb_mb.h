@@ -213,6 +213,11 @@ char *duckdb_mbx_profile_drain(duckdb_mb_connection *handle);
  * read over `bytes`-sized buffers -> out3[0..2].  Returns 1 on success. */
 int32_t duckdb_mbx_hbm_calibrate(duckdb_mb_connection *handle, int64_t bytes, int32_t iters, double *out3);
 
+/* Bound-plan cache of a prepared SELECT: out2[0] = times the statement was
+ * bound, out2[1] = executions that reused the bound plan with only the
+ * parameter constants overwritten.  Returns 1 on success. */
+int32_t duckdb_mbx_statement_plan_stats(duckdb_mb_statement *statement, int64_t *out2);
+
 /* Partial aggregate export for multi-GPU combine: the i-th cell of the last
  * materialized result as raw little-endian bytes (HUGEINT: 16 bytes). */
 int32_t duckdb_mbx_result_raw(duckdb_mb_result *result, int32_t col, int32_t row, void *out, int32_t out_len);

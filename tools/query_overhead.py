@@ -29,6 +29,22 @@ for prof in ("false", "true"):
             rr.close()
             ts.append(time.perf_counter() - t0)
         out[f"profile={prof} {sql}"] = {"median_us": statistics.median(ts[50:]) * 1e6, "min_us": min(ts) * 1e6}
+    if prof == "false":
+        # prepared re-execution: bound-plan cache on / off (MBX_PLAN_CACHE=0)
+        st = c.prepare("SELECT COUNT(*) FROM t WHERE x > ?").value
+        for cache in ("1", "0"):
+            os.environ["MBX_PLAN_CACHE"] = cache
+            ts = []
+            for i in range(300):
+                st.bind_bigint(1, 24 + (i & 1))
+                t0 = time.perf_counter()
+                rr = m.lib.duckdb_mb_execute_prepared(st._h)
+                m.lib.duckdb_mb_result_destroy(rr)
+                ts.append(time.perf_counter() - t0)
+            out[f"prepared execute, plan cache={cache}"] = {"median_us": statistics.median(ts[50:]) * 1e6,
+                                                            "min_us": min(ts) * 1e6, "stats": st.plan_stats()}
+        os.environ.pop("MBX_PLAN_CACHE")
+        st.close()
     if prof == "true":
         c.profile_drain()
         c.query_raw("SELECT COUNT(*) FROM t WHERE x > 24").close()
