@@ -379,12 +379,14 @@ def bench_c4(mbx, conn, n, args):
     # the same round trip through the reference's row-wise Appender API
     # (begin_row / append_bigint / end_row per row), driven natively from C
     row_api = native_harness(["c4", str(n)])
+    # and through 2048-row data chunks (duckdb_mb_append_data_chunk, ref duckdb_native.c:2109-2132)
+    chunk_api = native_harness(["c4chunk", str(n)])
     res = {"metric": "C4 appender ingest + arrow read-back", "value": n / (t_in + t_out), "unit": "rows/s",
            "n_gpus": 1, "ingest_gbs": n * 8 / t_in / 1e9, "readback_gbs": n * 8 / t_out / 1e9,
            "ingest_s": t_in, "readback_s": t_out, "rows": n, "bit_exact": ok,
            "bound": "host link (PCIe Gen5 x16, 63 GB/s spec) + host-side wire-buffer assembly",
            "ingest_api": "columnar duckdb_mbx_append_column (extension), from Python",
-           "row_appender_native": row_api}
+           "row_appender_native": row_api, "chunk_appender_native": chunk_api}
     print(json.dumps(res), flush=True)
 
 

@@ -924,6 +924,195 @@ int32_t duckdb_mbx_append_column(duckdb_mb_appender *a, int32_t col, const void 
   return 1;
 }
 
+// ---- DataChunk / Vector / LogicalType (ref duckdb_native.c:1926-2132) ---------
+// A logical type handle points at an MbxLogicalType; a vector handle at an
+// MbxVector (host arrays of kVectorSize rows: values, and a validity mask of
+// 64-bit words, bit = 1 -> valid, all set by create/reset so a caller may clear
+// bits directly); a data chunk at an MbxChunk.
+namespace {
+struct MbxLogicalType {
+  LogicalType t;
+};
+struct MbxVector {
+  LogicalType t;
+  Phys phys = P_I64;
+  int w = 8;
+  std::vector<uint64_t> data;  // kVectorSize * w bytes, 8-byte aligned
+  std::vector<uint64_t> valid;
+};
+struct MbxChunk {
+  std::vector<MbxVector> vecs;
+  idx_t size = 0;
+};
+constexpr idx_t kChunkRows = 2048;  // DuckDB's STANDARD_VECTOR_SIZE
+
+duckdb_mb_logical_type *NewMbType(const LogicalType &t) {
+  auto *lt = new MbxLogicalType{t};
+  auto *mb = (duckdb_mb_logical_type *)malloc(sizeof(duckdb_mb_logical_type));
+  mb->type = (duckdb_logical_type)lt;
+  return mb;
+}
+}  // namespace
+
+duckdb_mb_logical_type *duckdb_mb_create_logical_type(duckdb_type type_id) {  // ref :1944-1956
+  switch (type_id) {
+    case T_BOOLEAN: case T_TINYINT: case T_SMALLINT: case T_INTEGER: case T_BIGINT: case T_UTINYINT:
+    case T_USMALLINT: case T_UINTEGER: case T_UBIGINT: case T_FLOAT: case T_DOUBLE: case T_HUGEINT:
+    case T_VARCHAR: case T_DATE: case T_TIMESTAMP: case T_TIME:
+      return NewMbType(LogicalType((TypeId)type_id));
+    case T_DECIMAL:
+      return NewMbType(LogicalType::Decimal(18, 3));  // duckdb_create_logical_type(DECIMAL): DECIMAL(18,3)
+    default:
+      SetError("Not implemented Error: logical type id " + std::to_string(type_id) + " is not supported");
+      return nullptr;
+  }
+}
+duckdb_mb_logical_type *duckdb_mb_create_list_type(duckdb_mb_logical_type *) {  // ref :1958-1973
+  SetError("Not implemented Error: LIST types are not supported by the MI355X backend");
+  return nullptr;
+}
+duckdb_mb_logical_type *duckdb_mb_create_struct_type(duckdb_logical_type *, const char **, idx_t) {  // ref :1975-1990
+  SetError("Not implemented Error: STRUCT types are not supported by the MI355X backend");
+  return nullptr;
+}
+duckdb_mb_logical_type *duckdb_mb_create_map_type(duckdb_logical_type *, duckdb_logical_type *) {  // ref :1992-2009
+  SetError("Not implemented Error: MAP types are not supported by the MI355X backend");
+  return nullptr;
+}
+void duckdb_mb_destroy_logical_type(duckdb_mb_logical_type *mb) {  // ref :2011-2019
+  if (!mb) return;
+  delete (MbxLogicalType *)mb->type;
+  free(mb);
+}
+int32_t duckdb_mb_is_null_logical_type(duckdb_mb_logical_type *mb) { return mb == nullptr ? 1 : 0; }  // ref :2021
+
+duckdb_mb_data_chunk *duckdb_mb_create_data_chunk(duckdb_logical_type *types, idx_t column_count) {  // ref :2029-2043
+  if (!types && column_count) return nullptr;
+  auto *ch = new MbxChunk();
+  for (idx_t i = 0; i < column_count; i++) {
+    if (!types[i]) {
+      delete ch;
+      return nullptr;
+    }
+    MbxVector v;
+    v.t = ((MbxLogicalType *)types[i])->t;
+    v.phys = PhysOf(v.t);
+    v.w = v.phys == P_STR ? 16 : PhysSize(v.phys);  // VARCHAR: a duckdb_string_t-sized slot per row
+    v.data.assign((kChunkRows * v.w + 7) / 8, 0);
+    v.valid.assign(kChunkRows / 64, ~0ull);
+    ch->vecs.push_back(std::move(v));
+  }
+  auto *mb = (duckdb_mb_data_chunk *)malloc(sizeof(duckdb_mb_data_chunk));
+  mb->chunk = (duckdb_data_chunk)ch;
+  return mb;
+}
+void duckdb_mb_destroy_data_chunk(duckdb_mb_data_chunk *mb) {  // ref :2045-2053
+  if (!mb) return;
+  delete (MbxChunk *)mb->chunk;
+  free(mb);
+}
+duckdb_vector duckdb_mb_data_chunk_get_vector(duckdb_mb_data_chunk *mb, idx_t col) {  // ref :2055-2061
+  if (!mb || !mb->chunk) return nullptr;
+  MbxChunk &ch = *(MbxChunk *)mb->chunk;
+  if (col >= ch.vecs.size()) return nullptr;
+  return (duckdb_vector)&ch.vecs[col];
+}
+void duckdb_mb_data_chunk_set_size(duckdb_mb_data_chunk *mb, idx_t size) {  // ref :2063-2068
+  if (!mb || !mb->chunk) return;
+  ((MbxChunk *)mb->chunk)->size = std::min<idx_t>(size, kChunkRows);
+}
+void duckdb_mb_data_chunk_reset(duckdb_mb_data_chunk *mb) {  // ref :2070-2075
+  if (!mb || !mb->chunk) return;
+  MbxChunk &ch = *(MbxChunk *)mb->chunk;
+  ch.size = 0;
+  for (auto &v : ch.vecs) std::fill(v.valid.begin(), v.valid.end(), ~0ull);
+}
+int32_t duckdb_mb_is_null_data_chunk(duckdb_mb_data_chunk *mb) { return mb == nullptr ? 1 : 0; }  // ref :2077
+void *duckdb_mb_vector_get_data(duckdb_vector v) { return v ? ((MbxVector *)v)->data.data() : nullptr; }  // ref :2085
+uint64_t *duckdb_mb_vector_get_validity(duckdb_vector v) {  // ref :2089
+  return v ? ((MbxVector *)v)->valid.data() : nullptr;
+}
+duckdb_vector duckdb_mb_list_vector_get_child(duckdb_vector) {  // ref :2093
+  SetError("Not implemented Error: LIST vectors are not supported by the MI355X backend");
+  return nullptr;
+}
+duckdb_state duckdb_mb_list_vector_set_size(duckdb_vector, idx_t) { return DuckDBError; }  // ref :2097
+duckdb_state duckdb_mb_list_vector_reserve(duckdb_vector, idx_t) { return DuckDBError; }   // ref :2101
+
+int32_t duckdb_mb_append_data_chunk(duckdb_mb_appender *a, duckdb_mb_data_chunk *mb) {  // ref :2109-2132
+  if (!a) return 0;
+  if (!mb || !mb->chunk) {
+    CopyErr(a->error, "data_chunk is null");
+    return 0;
+  }
+  MbxChunk &ch = *(MbxChunk *)mb->chunk;
+  const size_t nc = a->table->cols.size();
+  if (ch.vecs.size() != nc) {
+    CopyErr(a->error, "Invalid Input Error: Appender: the data chunk has " + std::to_string(ch.vecs.size()) +
+                          " columns but the table has " + std::to_string(nc));
+    return 0;
+  }
+  if (a->col != 0) {
+    CopyErr(a->error, "Failed to append data chunk: Incomplete append to row!");
+    return 0;
+  }
+  for (size_t c = 0; c < nc; c++)
+    if (ch.vecs[c].phys == P_STR) {
+      CopyErr(a->error, "Not implemented Error: VARCHAR vectors in append_data_chunk");
+      return 0;
+    }
+  const int64_t n = (int64_t)ch.size;
+  auto row_valid = [&](size_t c, int64_t r) { return (ch.vecs[c].valid[r >> 6] >> (r & 63)) & 1; };
+  try {
+    bool exact = a->pinned;
+    for (size_t c = 0; exact && c < nc; c++) exact = ch.vecs[c].t == a->table->cols[c].type;
+    if (exact) {  // whole-vector copies into the pinned double buffer
+      int64_t off = 0;
+      while (off < n) {
+        PinnedSlot(a, 0);  // allocates the buffers on first use
+        const int64_t m = std::min<int64_t>(n - off, a->pcap - a->prow);
+        for (size_t c = 0; c < nc; c++) {
+          const int w = a->pw[c];
+          memcpy((char *)a->pbuf[a->pcur][c] + (size_t)a->prow * w, (const char *)ch.vecs[c].data.data() + (size_t)off * w,
+                 (size_t)m * w);
+          bool all = true;
+          for (int64_t r = off; r < off + m && all; r++) all = row_valid(c, r);
+          auto &pv = a->pvalid[c];
+          if (!all || !pv.empty()) {
+            if (pv.empty()) pv.assign((size_t)a->prow, 1);
+            pv.resize((size_t)a->prow);
+            for (int64_t r = off; r < off + m; r++) pv.push_back((uint8_t)row_valid(c, r));
+          }
+        }
+        a->prow += m;
+        off += m;
+        if (a->prow >= a->pcap && !FlushPinned(a, false)) return 0;
+      }
+      return 1;
+    }
+    // other types: value by value through the appender's casts
+    for (int64_t r = 0; r < n; r++) {
+      for (size_t c = 0; c < nc; c++) {
+        const MbxVector &v = ch.vecs[c];
+        Value x = Value::Null(v.t);
+        if (row_valid(c, r)) {
+          HostColumn hc;
+          hc.type = v.t;
+          hc.phys = v.phys;
+          hc.data.assign((const uint8_t *)v.data.data() + (size_t)r * v.w, (const uint8_t *)v.data.data() + (size_t)(r + 1) * v.w);
+          x = hc.Get(0);
+        }
+        if (!AppendValue(a, x)) return 0;
+      }
+      if (!duckdb_mb_end_row(a)) return 0;
+    }
+    return 1;
+  } catch (std::exception &e) {
+    CopyErr(a->error, e.what());
+    return 0;
+  }
+}
+
 int32_t duckdb_mbx_append_commit(duckdb_mb_appender *a, int64_t count) {
   if (!a) return 0;
   size_t nc = a->table->cols.size();

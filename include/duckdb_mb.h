@@ -213,6 +213,47 @@ char *duckdb_mbx_profile_drain(duckdb_mb_connection *handle);
  * read over `bytes`-sized buffers -> out3[0..2].  Returns 1 on success. */
 int32_t duckdb_mbx_hbm_calibrate(duckdb_mb_connection *handle, int64_t bytes, int32_t iters, double *out3);
 
+/* ---- DataChunk / Vector / LogicalType (ref src/duckdb_native.c:1926-2132) ----
+ * The reference wraps libduckdb's data-chunk API; these handles keep its C
+ * signatures (duckdb.h handle and enum types declared below) over host-side
+ * vectors of DuckDB's vector size (2048 rows).  duckdb_mb_append_data_chunk
+ * copies a chunk's fixed-width vectors into the appender's pinned double
+ * buffer (whole-vector copies; the buffer's async H2D DMA as for the row-wise
+ * appender).  LIST/STRUCT/MAP types and list vectors are out of scope
+ * (NULL / DuckDBError with "Not implemented"). */
+#ifndef DUCKDB_API_HANDLES_DECLARED
+#define DUCKDB_API_HANDLES_DECLARED
+typedef uint64_t idx_t;
+typedef enum duckdb_state { DuckDBSuccess = 0, DuckDBError = 1 } duckdb_state;
+typedef int32_t duckdb_type; /* DUCKDB_TYPE_* ids: BOOLEAN 1 ... BIGINT 5 ... DOUBLE 11 ... HUGEINT 16, DECIMAL 19 */
+typedef struct _duckdb_logical_type { void *internal_ptr; } * duckdb_logical_type;
+typedef struct _duckdb_vector { void *internal_ptr; } * duckdb_vector;
+typedef struct _duckdb_data_chunk { void *internal_ptr; } * duckdb_data_chunk;
+#endif
+typedef struct duckdb_mb_logical_type { duckdb_logical_type type; } duckdb_mb_logical_type; /* ref :1928-1930 */
+typedef struct duckdb_mb_data_chunk { duckdb_data_chunk chunk; } duckdb_mb_data_chunk;     /* ref :1932-1934 */
+
+duckdb_mb_logical_type *duckdb_mb_create_logical_type(duckdb_type type_id);            /* ref :1944-1956 */
+duckdb_mb_logical_type *duckdb_mb_create_list_type(duckdb_mb_logical_type *child_type); /* ref :1958-1973 */
+duckdb_mb_logical_type *duckdb_mb_create_struct_type(duckdb_logical_type *member_types, const char **member_names,
+                                                     idx_t member_count);               /* ref :1975-1990 */
+duckdb_mb_logical_type *duckdb_mb_create_map_type(duckdb_logical_type *key_type,
+                                                  duckdb_logical_type *value_type);     /* ref :1992-2009 */
+void duckdb_mb_destroy_logical_type(duckdb_mb_logical_type *mb_type);                   /* ref :2011-2019 */
+int32_t duckdb_mb_is_null_logical_type(duckdb_mb_logical_type *mb_type);               /* ref :2021-2023 */
+duckdb_mb_data_chunk *duckdb_mb_create_data_chunk(duckdb_logical_type *types, idx_t column_count); /* ref :2029-2043 */
+void duckdb_mb_destroy_data_chunk(duckdb_mb_data_chunk *mb_chunk);                      /* ref :2045-2053 */
+duckdb_vector duckdb_mb_data_chunk_get_vector(duckdb_mb_data_chunk *mb_chunk, idx_t col_idx); /* ref :2055-2061 */
+void duckdb_mb_data_chunk_set_size(duckdb_mb_data_chunk *mb_chunk, idx_t size);        /* ref :2063-2068 */
+void duckdb_mb_data_chunk_reset(duckdb_mb_data_chunk *mb_chunk);                        /* ref :2070-2075 */
+int32_t duckdb_mb_is_null_data_chunk(duckdb_mb_data_chunk *mb_chunk);                   /* ref :2077-2079 */
+void *duckdb_mb_vector_get_data(duckdb_vector vector);                                  /* ref :2085-2087 */
+uint64_t *duckdb_mb_vector_get_validity(duckdb_vector vector);                          /* ref :2089-2091 */
+duckdb_vector duckdb_mb_list_vector_get_child(duckdb_vector vector);                    /* ref :2093-2095 */
+duckdb_state duckdb_mb_list_vector_set_size(duckdb_vector vector, idx_t size);          /* ref :2097-2099 */
+duckdb_state duckdb_mb_list_vector_reserve(duckdb_vector vector, idx_t capacity);       /* ref :2101-2103 */
+int32_t duckdb_mb_append_data_chunk(duckdb_mb_appender *mb_append, duckdb_mb_data_chunk *mb_chunk); /* ref :2109-2132 */
+
 /* Bound-plan cache of a prepared SELECT: out2[0] = times the statement was
  * bound, out2[1] = executions that reused the bound plan with only the
  * parameter constants overwritten.  Returns 1 on success. */

@@ -13,6 +13,8 @@
  *                           chunk loop: one JSON line
  *   mb_harness c4 <rows>    C4 through the row-wise Appender + Arrow getter:
  *                           one JSON line (ingest rows/s, read-back GB/s)
+ *   mb_harness c4chunk <rows>  the same with the ingest through 2048-row data
+ *                           chunks (duckdb_mb_append_data_chunk)
  * Exit status 0 = every check passed.
  */
 #define _POSIX_C_SOURCE 199309L
@@ -142,6 +144,90 @@ static void host_constant_checks(duckdb_mb_connection *c) {
   }
 }
 
+/* DataChunk / Vector / LogicalType handles without a device (ref :1944-2103) */
+static void chunk_api_checks(void) {
+  duckdb_mb_logical_type *bt = duckdb_mb_create_logical_type(5), *it = duckdb_mb_create_logical_type(4);
+  CHECK(bt && it && !duckdb_mb_is_null_logical_type(bt), "create_logical_type");
+  CHECK(duckdb_mb_is_null_logical_type(duckdb_mb_create_list_type(bt)), "LIST types are out of scope");
+  CHECK(strstr(take(duckdb_mb_last_error()), "Not implemented") != NULL, "LIST error text");
+  duckdb_logical_type types[2] = {bt->type, it->type};
+  duckdb_mb_data_chunk *ch = duckdb_mb_create_data_chunk(types, 2);
+  CHECK(ch && !duckdb_mb_is_null_data_chunk(ch), "create_data_chunk");
+  duckdb_vector v0 = duckdb_mb_data_chunk_get_vector(ch, 0), v1 = duckdb_mb_data_chunk_get_vector(ch, 1);
+  CHECK(v0 && v1 && duckdb_mb_data_chunk_get_vector(ch, 2) == NULL, "get_vector");
+  uint64_t *val = duckdb_mb_vector_get_validity(v1);
+  CHECK(val && val[0] == ~0ull && val[31] == ~0ull, "validity starts all-valid");
+  val[0] &= ~1ull;
+  duckdb_mb_data_chunk_reset(ch);
+  CHECK(val[0] == ~0ull, "reset restores validity");
+  CHECK(duckdb_mb_vector_get_data(v0) != NULL && duckdb_mb_list_vector_set_size(v0, 1) == DuckDBError, "vector data");
+  duckdb_mb_destroy_data_chunk(ch);
+  duckdb_mb_destroy_logical_type(bt);
+  duckdb_mb_destroy_logical_type(it);
+  CHECK(duckdb_mb_append_data_chunk(NULL, NULL) == 0, "append_data_chunk(NULL)");
+}
+
+/* two chunks into (v BIGINT, w INTEGER) with NULLs in both columns, then a
+ * DECIMAL(18,3) chunk into a DECIMAL(15,2) column (converted value by value) */
+static void chunk_append_checks(duckdb_mb_connection *c) {
+  moonbit_bytes_t sql = S("CREATE TABLE dc (v BIGINT, w INTEGER, d DECIMAL(15,2))");
+  duckdb_mb_result *r = duckdb_mb_query(c, sql);
+  mb_free(sql);
+  if (r) duckdb_mb_result_destroy(r);
+  moonbit_bytes_t sch = S("main"), tab = S("dc");
+  duckdb_mb_appender *ap = duckdb_mb_appender_create(c, sch, tab);
+  mb_free(sch);
+  mb_free(tab);
+  CHECK(ap != NULL, "appender_create dc");
+  if (!ap) return;
+  duckdb_mb_logical_type *bt = duckdb_mb_create_logical_type(5), *it = duckdb_mb_create_logical_type(4),
+                         *dt = duckdb_mb_create_logical_type(19);
+  duckdb_logical_type types[3] = {bt->type, it->type, dt->type};
+  duckdb_mb_data_chunk *ch = duckdb_mb_create_data_chunk(types, 3);
+  for (int k = 0; k < 2; k++) {
+    int64_t *v = duckdb_mb_vector_get_data(duckdb_mb_data_chunk_get_vector(ch, 0));
+    int32_t *w = duckdb_mb_vector_get_data(duckdb_mb_data_chunk_get_vector(ch, 1));
+    int64_t *d = duckdb_mb_vector_get_data(duckdb_mb_data_chunk_get_vector(ch, 2));
+    uint64_t *vv = duckdb_mb_vector_get_validity(duckdb_mb_data_chunk_get_vector(ch, 0));
+    uint64_t *wv = duckdb_mb_vector_get_validity(duckdb_mb_data_chunk_get_vector(ch, 1));
+    for (int i = 0; i < 2048; i++) {
+      v[i] = (int64_t)(k * 2048 + i) * 3;
+      w[i] = k * 2048 + i;
+      d[i] = 12345;  /* 12.345 at scale 3 -> 12.35 at scale 2 */
+      if (i % 7 == 0) vv[i >> 6] &= ~(1ull << (i & 63));
+      if (i % 11 == 0) wv[i >> 6] &= ~(1ull << (i & 63));
+    }
+    duckdb_mb_data_chunk_set_size(ch, 2048);
+    CHECK(duckdb_mb_append_data_chunk(ap, ch) == 1, "append_data_chunk: %s", take(duckdb_mb_appender_error(ap)));
+    duckdb_mb_data_chunk_reset(ch);
+  }
+  duckdb_mb_destroy_data_chunk(ch);
+  duckdb_mb_destroy_logical_type(bt);
+  duckdb_mb_destroy_logical_type(it);
+  duckdb_mb_destroy_logical_type(dt);
+  duckdb_mb_appender_destroy(ap); /* close => flush */
+  sql = S("SELECT COUNT(*), COUNT(v), SUM(v), COUNT(w), SUM(w), MIN(d), MAX(d) FROM dc");
+  r = duckdb_mb_query(c, sql);
+  mb_free(sql);
+  CHECK(r != NULL, "dc query: %s", take(duckdb_mb_last_error()));
+  if (!r) return;
+  long long cv = 0, sv = 0, cw = 0, sw = 0;
+  for (int k = 0; k < 2; k++)
+    for (int i = 0; i < 2048; i++) {
+      if (i % 7) { cv++; sv += (long long)(k * 2048 + i) * 3; }
+      if (i % 11) { cw++; sw += k * 2048 + i; }
+    }
+  char want[64];
+  check_cell(r, 0, 0, "4096");
+  snprintf(want, sizeof want, "%lld", cv); check_cell(r, 1, 0, want);
+  snprintf(want, sizeof want, "%lld", sv); check_cell(r, 2, 0, want);
+  snprintf(want, sizeof want, "%lld", cw); check_cell(r, 3, 0, want);
+  snprintf(want, sizeof want, "%lld", sw); check_cell(r, 4, 0, want);
+  check_cell(r, 5, 0, "12.35");
+  check_cell(r, 6, 0, "12.35");
+  duckdb_mb_result_destroy(r);
+}
+
 static int gpu_checks(duckdb_mb_connection *c, long rows) {
   char q[512];
   snprintf(q, sizeof q, "CREATE TABLE t AS SELECT mbx_synth(42, i, 50) + 1 AS x FROM range(%ld) tbl(i)", rows);
@@ -195,6 +281,7 @@ static int gpu_checks(duckdb_mb_connection *c, long rows) {
     mb_free(w);
     duckdb_mb_arrow_destroy(ar);
   }
+  chunk_append_checks(c);
   return 0;
 }
 
@@ -211,7 +298,31 @@ static double now_s(void) {
 }
 static int64_t c4_value(int64_t i) { return (int64_t)(((uint64_t)i * 2654435761ull) & 0x7fffffffffffffffull); }
 
-static int c4_bench(duckdb_mb_connection *c, long rows) {
+/* the chunked form of C4's ingest (ref duckdb_native.c:2029-2132): BIGINT
+ * vectors of 2048 rows filled in place, appended with duckdb_mb_append_data_chunk */
+static int c4_ingest_chunks(duckdb_mb_appender *ap, long rows) {
+  duckdb_mb_logical_type *bt = duckdb_mb_create_logical_type(5 /* DUCKDB_TYPE_BIGINT */);
+  CHECK(!duckdb_mb_is_null_logical_type(bt), "create_logical_type");
+  if (!bt) return 0;
+  duckdb_logical_type types[1] = {bt->type};
+  duckdb_mb_data_chunk *ch = duckdb_mb_create_data_chunk(types, 1);
+  CHECK(!duckdb_mb_is_null_data_chunk(ch), "create_data_chunk");
+  int ok = ch != NULL;
+  for (long base = 0; ok && base < rows; base += 2048) {
+    const long m = rows - base < 2048 ? rows - base : 2048;
+    duckdb_vector v = duckdb_mb_data_chunk_get_vector(ch, 0);
+    int64_t *d = (int64_t *)duckdb_mb_vector_get_data(v);
+    for (long i = 0; i < m; i++) d[i] = c4_value(base + i);
+    duckdb_mb_data_chunk_set_size(ch, (idx_t)m);
+    ok &= duckdb_mb_append_data_chunk(ap, ch);
+    duckdb_mb_data_chunk_reset(ch);
+  }
+  duckdb_mb_destroy_data_chunk(ch);
+  duckdb_mb_destroy_logical_type(bt);
+  return ok;
+}
+
+static int c4_bench(duckdb_mb_connection *c, long rows, int chunks) {
   moonbit_bytes_t sql = S("CREATE TABLE c4 (v BIGINT)");
   duckdb_mb_result *r = duckdb_mb_query(c, sql);
   mb_free(sql);
@@ -224,10 +335,14 @@ static int c4_bench(duckdb_mb_connection *c, long rows) {
   if (!ap) return 1;
   double t0 = now_s();
   int ok = 1;
-  for (int64_t i = 0; i < rows; i++) {
-    ok &= duckdb_mb_begin_row(ap);
-    ok &= duckdb_mb_append_bigint(ap, c4_value(i));
-    ok &= duckdb_mb_end_row(ap);
+  if (chunks) {
+    ok &= c4_ingest_chunks(ap, rows);
+  } else {
+    for (int64_t i = 0; i < rows; i++) {
+      ok &= duckdb_mb_begin_row(ap);
+      ok &= duckdb_mb_append_bigint(ap, c4_value(i));
+      ok &= duckdb_mb_end_row(ap);
+    }
   }
   ok &= duckdb_mb_flush(ap);
   duckdb_mb_appender_destroy(ap);
@@ -256,9 +371,10 @@ static int c4_bench(duckdb_mb_connection *c, long rows) {
   }
   double t_out = now_s() - t0;
   CHECK(checked == rows && bad == 0, "c4 read-back: %ld rows checked, %ld mismatches", checked, bad);
-  printf("{\"rows\": %ld, \"ingest_s\": %.6f, \"ingest_rows_per_s\": %.1f, \"readback_s\": %.6f, "
-         "\"readback_gbs\": %.3f, \"bit_exact\": %s}\n",
-         rows, t_in, rows / t_in, t_out, rows * 8.0 / t_out / 1e9, (checked == rows && bad == 0) ? "true" : "false");
+  printf("{\"rows\": %ld, \"ingest_api\": \"%s\", \"ingest_s\": %.6f, \"ingest_rows_per_s\": %.1f, "
+         "\"ingest_gbs\": %.3f, \"readback_s\": %.6f, \"readback_gbs\": %.3f, \"bit_exact\": %s}\n",
+         rows, chunks ? "append_data_chunk" : "begin_row/append_bigint/end_row", t_in, rows / t_in,
+         rows * 8.0 / t_in / 1e9, t_out, rows * 8.0 / t_out / 1e9, (checked == rows && bad == 0) ? "true" : "false");
   return 0;
 }
 
@@ -340,6 +456,8 @@ static int c1_bench(duckdb_mb_connection *c, int reps) {
 int main(int argc, char **argv) {
   const char *mode = argc > 1 ? argv[1] : "cpu";
   int gpu = strcmp(mode, "gpu") == 0, c4 = strcmp(mode, "c4") == 0, c1 = strcmp(mode, "c1") == 0;
+  const int c4chunk = strcmp(mode, "c4chunk") == 0;
+  c4 |= c4chunk;
   duckdb_mb_connection *c = open_conn(!gpu && !c4 && !c1);
   if (!c) return 1;
   if (c1) {
@@ -348,11 +466,12 @@ int main(int argc, char **argv) {
     return g_fail ? 1 : 0;
   }
   if (c4) {
-    c4_bench(c, argc > 2 ? atol(argv[2]) : 100000000);
+    c4_bench(c, argc > 2 ? atol(argv[2]) : 100000000, c4chunk);
     duckdb_mb_disconnect(c);
     return g_fail ? 1 : 0;
   }
   host_constant_checks(c);
+  chunk_api_checks();
   if (gpu) gpu_checks(c, argc > 2 ? atol(argv[2]) : 1000000);
   duckdb_mb_disconnect(c);
   CHECK(g_made > 0, "no Bytes made through the runtime allocator");

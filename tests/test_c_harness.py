@@ -47,3 +47,15 @@ def test_c_harness_c1_native(mbx, tmp_path):
     assert p.returncode == 0, p.stdout + p.stderr
     r = json.loads(p.stdout.strip().splitlines()[-1])
     assert r["exact"] and r["rows"] == 500000 and r["sum"] == 249999500000 and r["stream_chunks"] >= 245
+
+
+@pytest.mark.gpu
+def test_c_harness_c4_data_chunks(mbx, tmp_path):
+    # f3: 1e8 INT64 rows ingested through duckdb_mb_append_data_chunk (2048-row
+    # vectors, ref src/duckdb_native.c:2029-2132), read back bit-exact
+    import json
+    exe = _build(tmp_path)
+    p = subprocess.run([exe, "c4chunk", "100000000"], capture_output=True, text=True, timeout=600)
+    assert p.returncode == 0, p.stdout + p.stderr
+    r = json.loads(p.stdout.strip().splitlines()[-1])
+    assert r["bit_exact"] and r["rows"] == 100_000_000 and r["ingest_api"] == "append_data_chunk"
