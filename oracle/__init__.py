@@ -14,7 +14,10 @@ Contents
 Parity status: pinned by the reference's own golden vectors — the 35 SQL
 fixtures (tests/golden/fixtures.json, extracted from
 src/duckdb_fixture_cases.mbt by tests/golden/make_fixtures.py), the native and
-arrow test assertions (tests/golden/native_cases.json), and closed forms for
+arrow test assertions (tests/golden/native_cases.json, extracted from
+src/duckdb_test.mbt and src/duckdb_arrow_test.mbt by
+tests/golden/make_native_cases.py and replayed by
+tests/test_gpu_native_cases.py), and closed forms for
 large N (e.g. COUNT(range(N) WHERE i%2=0) = ceil(N/2)).  libduckdb itself is
 absent from /root/reference and from this image, so it cannot be executed.
 """

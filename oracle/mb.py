@@ -26,3 +26,14 @@ def column_type_from_id(i: int) -> str:
              "Bit", "TimeTz", "TimestampTz", "UHugeInt", "Array", "Any", "Bignum", "SqlNull", "StringLiteral",
              "IntegerLiteral", "TimeNs"]
     return names[i] if 0 <= i < len(names) else f"Unknown({i})"
+
+
+def date_from_ymd(year: int, month: int, day: int) -> int:
+    """duckdb_native.mbt:1188-1203 — days since 1970-01-01 (proleptic Gregorian)."""
+    import datetime
+    return (datetime.date(year, month, day) - datetime.date(1970, 1, 1)).days
+
+
+def timestamp_from_ymd_hms(year: int, month: int, day: int, hour: int, minute: int, second: int) -> int:
+    """duckdb_native.mbt:1250-1266 — microseconds since 1970-01-01 00:00:00."""
+    return (date_from_ymd(year, month, day) * 86400 + hour * 3600 + minute * 60 + second) * 1_000_000
