@@ -992,7 +992,25 @@ BExprPtr BindExprInner(const Expr &e, BindCtx &ctx);
 
 // In aggregate mode, any sub-expression equal to a GROUP BY expression
 // becomes a reference to that group column.
+// expression nesting bound of the binder's recursion (DuckDB's
+// max_expression_depth default): a deep left-leaning chain such as
+// 1 + 1 + ... parses iteratively but binds recursively
+static thread_local int g_bind_depth = 0;
+struct BindDepth {
+  BindDepth() {
+    if (++g_bind_depth > 1000) {
+      g_bind_depth = 0;  // the binder unwinds through the throw
+      ThrowError("Binder", "Max expression depth limit of 1000 exceeded. Use \"SET max_expression_depth TO x\" to "
+                           "increase the maximum expression depth.");
+    }
+  }
+  ~BindDepth() {
+    if (g_bind_depth > 0) g_bind_depth--;
+  }
+};
+
 BExprPtr BindExpr(const Expr &e, BindCtx &ctx) {
+  BindDepth depth_guard;
   if (ctx.agg_mode && !ctx.in_agg_arg && !ContainsAgg(e) && e.kind != Expr::CONST && e.kind != Expr::PARAM) {
     BindCtx sub = ctx;
     sub.agg_mode = false;

@@ -483,7 +483,21 @@ class Parser {
     return e;
   }
 
+  // recursion guard (nested parentheses, NOT NOT ..., - - ...): DuckDB's
+  // max_expression_depth default
+  static constexpr int kMaxDepth = 1000;
+  int depth_ = 0;
+  struct DepthGuard {
+    int &d;
+    explicit DepthGuard(int &x) : d(x) {
+      if (++d > kMaxDepth)
+        ThrowError("Parser", "Max expression depth limit of " + std::to_string(kMaxDepth) + " exceeded");
+    }
+    ~DepthGuard() { d--; }
+  };
+
   ExprPtr ParseExpr() {
+    DepthGuard g(depth_);
     size_t st = Cur().pos;
     ExprPtr e = ParseOr();
     size_t en = Cur().pos;
@@ -505,6 +519,7 @@ class Parser {
     return l;
   }
   ExprPtr ParseNot() {
+    DepthGuard g(depth_);
     if (AcceptKw("not")) {
       auto e = Mk(Expr::UNARY);
       e->op = "NOT";
@@ -598,6 +613,7 @@ class Parser {
     return l;
   }
   ExprPtr ParseUnary() {
+    DepthGuard g(depth_);
     if (IsOp("-") || IsOp("+")) {
       std::string op = t_[p_++].s;
       ExprPtr a = ParseUnary();

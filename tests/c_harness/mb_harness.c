@@ -15,6 +15,8 @@
  *                           one JSON line (ingest rows/s, read-back GB/s)
  *   mb_harness c4chunk <rows>  the same with the ingest through 2048-row data
  *                           chunks (duckdb_mb_append_data_chunk)
+ *   mb_harness sqlfile <f>  every line of f as a query, a prepared statement
+ *                           and every result cell (sanitizer runs, no GPU)
  * Exit status 0 = every check passed.
  */
 #define _POSIX_C_SOURCE 199309L
@@ -453,8 +455,60 @@ static int c1_bench(duckdb_mb_connection *c, int reps) {
   return 0;
 }
 
+/* every line of a file is one statement: run it, read every cell of a result
+ * (errors are expected for statements that need a device); used to drive the
+ * parser / binder / formatter under AddressSanitizer + UBSan */
+static int sql_file(duckdb_mb_connection *c, const char *path) {
+  FILE *f = fopen(path, "r");
+  CHECK(f != NULL, "open %s", path);
+  if (!f) return 1;
+  static char line[1 << 16];
+  long ok = 0, failed = 0;
+  while (fgets(line, sizeof line, f)) {
+    size_t n = strlen(line);
+    while (n && (line[n - 1] == '\n' || line[n - 1] == '\r')) line[--n] = 0;
+    if (!n) continue;
+    moonbit_bytes_t sql = S(line);
+    duckdb_mb_result *r = duckdb_mb_query(c, sql);
+    if (r) {
+      const int32_t nc = duckdb_mb_result_column_count(r), nr = duckdb_mb_result_row_count(r);
+      for (int32_t j = 0; j < nc; j++) {
+        (void)take(duckdb_mb_result_column_name(r, j));
+        (void)duckdb_mb_result_column_type(r, j);
+        for (int32_t i = 0; i < nr; i++) {
+          (void)duckdb_mb_result_is_null(r, j, i);
+          (void)take(duckdb_mb_result_value(r, j, i));
+        }
+      }
+      duckdb_mb_result_destroy(r);
+      ok++;
+    } else {
+      (void)take(duckdb_mb_last_error());
+      failed++;
+    }
+    /* the same text as a prepared statement and a stream */
+    duckdb_mb_statement *st = duckdb_mb_prepare(c, sql);
+    if (st) {
+      duckdb_mb_result *pr = duckdb_mb_execute_prepared(st);
+      if (pr) duckdb_mb_result_destroy(pr);
+      duckdb_mb_statement_destroy(st);
+    }
+    mb_free(sql);
+  }
+  fclose(f);
+  printf("sqlfile: %ld ok, %ld failed\n", ok, failed);
+  return 0;
+}
+
 int main(int argc, char **argv) {
   const char *mode = argc > 1 ? argv[1] : "cpu";
+  if (strcmp(mode, "sqlfile") == 0) {
+    duckdb_mb_connection *c = open_conn(1);
+    if (!c) return 1;
+    sql_file(c, argc > 2 ? argv[2] : "/dev/null");
+    duckdb_mb_disconnect(c);
+    return g_fail ? 1 : 0;
+  }
   int gpu = strcmp(mode, "gpu") == 0, c4 = strcmp(mode, "c4") == 0, c1 = strcmp(mode, "c1") == 0;
   const int c4chunk = strcmp(mode, "c4chunk") == 0;
   c4 |= c4chunk;
