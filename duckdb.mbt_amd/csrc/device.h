@@ -296,6 +296,20 @@ void CompactColumns(const CompactDesc &d, int64_t nrows, const unsigned long lon
                     hipStream_t s);
 void RebaseOffsets(const int64_t *src, int64_t *dst, int64_t n, int64_t delta, hipStream_t s);
 
+// Values as text in the string wire layout (text_kernels.hip): lengths (text +
+// NUL) of every row, then, at each row's exclusive-scan offset, its text and a
+// NUL; vbytes (optional) gets the validity byte of every row.
+enum TextKind { TEXT_INT = 0, TEXT_BOOL = 1, TEXT_DECIMAL = 2 };
+struct TextCol {
+  const void *data;
+  const uint64_t *valid;
+  int32_t phys;   // P_U8 .. P_I128
+  int32_t kind;   // TextKind
+  int32_t scale;  // TEXT_DECIMAL
+};
+void TextLengths(const TextCol &c, int64_t n, uint32_t *lens, hipStream_t s);
+void TextWrite(const TextCol &c, int64_t n, const int64_t *offsets, char *chars, uint8_t *vbytes, hipStream_t s);
+
 // Count-first compaction, for a conjunction of range predicates whose columns
 // are all among the (NULL-free, 4/8-byte) outputs, e.g. SELECT x FROM t WHERE
 // x > 24.  A chunk is FC_CHUNK consecutive 256-row steps, owned by one wave in

@@ -2,6 +2,7 @@
 // duckdb_mb_* C-ABI (the objects the reference keeps inside libduckdb).
 #pragma once
 
+#include <functional>
 #include <map>
 #include <memory>
 #include <mutex>
@@ -150,6 +151,12 @@ ResultPtr FetchDeviceRows(Connection &c, DeviceResult &d, int64_t start, int64_t
 // NULL slots zeroed into vals, validity bytes into vbytes (if not nullptr).
 bool CopyDeviceColumnWire(Connection &c, DeviceResult &d, int col, int phys, void *vals, uint8_t *vbytes);
 bool DeviceColumnWireOk(const DeviceResult &d, int col, int phys);  // its precondition
+// String wire form ([text \0]..., NULL = "") of an integer / BOOLEAN / DECIMAL /
+// HUGEINT device column, formatted on the device: dst(chars) returns where the
+// chars (then, when vbytes, n validity bytes) go, or nullptr to give up.
+bool DeviceColumnTextOk(const DeviceResult &d, int col);
+bool CopyDeviceColumnText(Connection &c, DeviceResult &d, int col, const std::function<uint8_t *(int64_t)> &dst,
+                          bool vbytes);
 
 // Runs one statement; returns a materialized result (empty for DDL).
 ResultPtr RunStatement(Connection &c, const std::string &sql, const std::vector<Value> &params, int *n_params_out);

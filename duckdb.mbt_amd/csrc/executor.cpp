@@ -2729,6 +2729,68 @@ bool CopyDeviceColumnWire(Connection &c, DeviceResult &d, int col, int phys, voi
   return true;
 }
 
+bool DeviceColumnTextOk(const DeviceResult &d, int col) {
+  if (col < 0 || col >= (int)d.r.cols.size()) return false;
+  const DCol &dc = d.r.cols[col];
+  if (!dc.data || dc.phys > P_I128) return false;
+  switch (dc.type.id) {
+    case T_BOOLEAN: case T_TINYINT: case T_SMALLINT: case T_INTEGER: case T_BIGINT: case T_UTINYINT:
+    case T_USMALLINT: case T_UINTEGER: case T_UBIGINT: case T_HUGEINT: case T_DECIMAL:
+      return true;
+    default:
+      return false;
+  }
+}
+
+bool CopyDeviceColumnText(Connection &c, DeviceResult &d, int col, const std::function<uint8_t *(int64_t)> &dst,
+                          bool vbytes) {
+  if (!DeviceColumnTextOk(d, col)) return false;
+  const DCol &dc = d.r.cols[col];
+  Engine &e = Eng(c);
+  const int64_t n = d.r.n;
+  dev::TextCol tc;
+  tc.data = dc.data;
+  tc.valid = dc.validity;
+  tc.phys = dc.phys;
+  tc.kind = dc.type.id == T_BOOLEAN ? dev::TEXT_BOOL : dc.type.id == T_DECIMAL ? dev::TEXT_DECIMAL : dev::TEXT_INT;
+  tc.scale = dc.type.id == T_DECIMAL ? dc.type.scale : 0;
+  auto lens = Alloc(e, (size_t)std::max<int64_t>(n, 1) * 4);
+  auto offs = Alloc(e, (size_t)(n + 1) * 8);
+  {
+    ProfScope ps(e, "text_lengths", (double)n * PhysSize(dc.phys), n);
+    dev::TextLengths(tc, n, (uint32_t *)lens->p, e.stream);
+  }
+  dev::ScanTileCounts((const uint32_t *)lens->p, (int64_t *)offs->p, n, e.d_scratch, e.stream);
+  const int64_t chars = ReadDev<int64_t>(e, e.d_scratch);
+  uint8_t *host = dst(chars);
+  if (!host) return false;
+  const size_t out_bytes = (size_t)chars + (vbytes ? (size_t)n : 0);
+  auto buf = Alloc(e, std::max<size_t>(out_bytes, 16));
+  {
+    ProfScope ps(e, "text_write", (double)n * PhysSize(dc.phys) + (double)out_bytes, n);
+    dev::TextWrite(tc, n, (const int64_t *)offs->p, (char *)buf->p, vbytes ? (uint8_t *)buf->p + chars : nullptr,
+                   e.stream);
+  }
+  if (out_bytes) HIPCHK(hipMemcpyAsync(host, buf->p, out_bytes, hipMemcpyDeviceToHost, e.stream));
+  HIPCHK(hipStreamSynchronize(e.stream));
+  CheckError(e);
+  if (e.profile) {  // a getter runs after its query's profile was taken: its kernels go to the drain history
+    for (auto &ev : e.events) {
+      float ms = 0;
+      hipEventElapsedTime(&ms, ev.a, ev.b);
+      QueryProfile::Kernel k;
+      k.name = ev.name;
+      k.ms = ms;
+      k.bytes = ev.bytes;
+      k.rows = ev.rows;
+      if (c.profile_history.size() < 100000) c.profile_history.push_back(k);
+    }
+    e.events.clear();
+    e.ev_used = 0;
+  }
+  return true;
+}
+
 // ---------------------------------------------------------------------------
 // tables: creation, append, stats
 // ---------------------------------------------------------------------------

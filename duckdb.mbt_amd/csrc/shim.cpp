@@ -1329,6 +1329,29 @@ static moonbit_bytes_t ArrowF64(duckdb_mb_arrow_result *a, int32_t col, bool nul
 static moonbit_bytes_t ArrowStr(duckdb_mb_arrow_result *a, int32_t col, bool nullable) {
   if (!ArrowOk(a, col)) return MakeBytes("", 0);
   int64_t n = a->row_count;
+  if (a->dev && !a->r && n > 0 && DeviceColumnTextOk(*a->dev, col)) {
+    // integer / BOOLEAN / DECIMAL / HUGEINT: formatted on the device, one DMA into the Bytes
+    moonbit_bytes_t out = nullptr;
+    int64_t total = 0;
+    try {
+      const bool ok = CopyDeviceColumnText(a->conn->conn, *a->dev, col, [&](int64_t chars) -> uint8_t * {
+        total = 8 + chars + (nullable ? n : 0);
+        if (total > INT32_MAX) return nullptr;
+        out = moonbit_make_bytes_raw((int32_t)total);
+        const int32_t h[2] = {(int32_t)n, (int32_t)chars};
+        memcpy(out, h, 8);
+        return out + 8;
+      }, nullable);
+      if (ok) return out;
+      if (!out) return MakeBytes("", 0);  // over the reference's int32 buffer size
+    } catch (std::exception &e) {
+      SetError(e.what());
+      if (out) {
+        memset(out + 8, 0, (size_t)(total - 8));
+        return out;
+      }
+    }
+  }
   const HostColumn &c = ArrowHost(a).cols[col];
   std::string data;
   for (int64_t i = 0; i < n; i++) {

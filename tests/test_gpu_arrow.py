@@ -144,3 +144,57 @@ def test_arrow_nullable_device_wire_vs_host(conn, mbx):
                 suf = "_nullable" if nullable else ""
                 got = mbx._take(getattr(mbx.lib, f"duckdb_mb_arrow_get_column_{k}{suf}")(a._h, c))
                 assert got == want[k](vals, nullable), (k, nullable, host_first)
+
+
+@pytest.mark.parametrize("n", [1, 255, 1_000_000])
+def test_arrow_string_getter_formats_on_device(mbx, oracle, n):
+    """The string getters of integer / BOOLEAN / DECIMAL / HUGEINT device
+    columns (DECIMAL and HUGEINT map to "string" in the reference,
+    duckdb_native.c:2336-2338) are formatted by the text kernels: the wire
+    buffer is byte-exact vs oracle/wire.py over oracle/fmt.py's spellings, NULLs
+    included, and the kernels are the ones that ran."""
+    from oracle import fmt
+    cfg = mbx.Config.create()
+    cfg.set("mbx_profile", "true")
+    c = mbx.connect_with_config(cfg).value
+    for q in (f"CREATE TABLE ts1 AS SELECT CASE WHEN mbx_synth(5, i, 7) = 0 THEN NULL ELSE "
+              f"CAST(mbx_synth(11, i, 200000) - 100000 AS DECIMAL(15,2)) END AS d FROM range({n}) tbl(i)",
+              f"CREATE TABLE ts2 AS SELECT CAST(mbx_synth(9, i, 1099511627776) - 549755813888 AS HUGEINT) * "
+              f"100000000000000000000 AS h FROM range({n}) tbl(i)",
+              f"CREATE TABLE ts3 AS SELECT mbx_synth(42, i, 50) - 25 AS b, CAST(mbx_synth(7, i, 32) - 16 AS INTEGER) AS k "
+              f"FROM range({n}) tbl(i)",
+              f"CREATE TABLE ts4 AS SELECT (mbx_synth(13, i, 2) = 1) AS f, CAST(mbx_synth(3, i, 9) AS DECIMAL(4,3)) AS s "
+              f"FROM range({n}) tbl(i)"):
+        r = c.query(q)
+        assert isinstance(r, mbx.Ok), r.error.message
+    d_valid = oracle.synth_i64(n, 5, 0, 7, 0) != 0
+    d = oracle.synth_i64(n, 11, 0, 200000, -100000)
+    h = oracle.synth_i64(n, 9, 0, 2**40, -2**39)
+    b = oracle.synth_i64(n, 42, 0, 50, -25)
+    k = oracle.synth_i64(n, 7, 0, 32, -16)
+    f = oracle.synth_i64(n, 13, 0, 2, 0) == 1
+    s3 = oracle.synth_i64(n, 3, 0, 9, 0)
+    exp = {
+        0: [fmt.decimal(int(x) * 100, 2) if v else None for x, v in zip(d, d_valid)],
+        1: [str(int(x) * 10**20) for x in h],
+        2: [str(int(x)) for x in b],
+        3: [str(int(x)) for x in k],
+        4: [fmt.boolean(bool(x)) for x in f],
+        5: [fmt.decimal(int(x) * 1000, 3) for x in s3],
+    }
+    where = {0: ("ts1", "d"), 1: ("ts2", "h"), 2: ("ts3", "b"), 3: ("ts3", "k"), 4: ("ts4", "f"), 5: ("ts4", "s")}
+    for col, vals in exp.items():
+        a = c.query_arrow(f"SELECT {where[col][1]} FROM {where[col][0]}").value
+        for nullable in (False, True):
+            got = mbx._take((mbx.lib.duckdb_mb_arrow_get_column_string_nullable if nullable else
+                             mbx.lib.duckdb_mb_arrow_get_column_string)(a._h, 0))
+            want = wire.string(vals, nullable)
+            if got != want:  # report the first difference (a full diff of MBs is too slow)
+                i = next((j for j in range(min(len(got), len(want))) if got[j] != want[j]), min(len(got), len(want)))
+                raise AssertionError(f"n={n} col={col} nullable={nullable} len {len(got)} vs {len(want)}, first "
+                                     f"difference at byte {i}: got {got[max(0, i - 24):i + 24]!r} "
+                                     f"want {want[max(0, i - 24):i + 24]!r}")
+        a.close()
+    names = [x["name"] for x in c.profile_drain()]
+    assert "text_write" in names and "text_lengths" in names
+    c.close()
