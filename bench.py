@@ -13,8 +13,13 @@ rank holds its own 1e9-row shard (rows [r*N, (r+1)*N) of the same generator)
 and the global COUNT is combined with an RCCL all-reduce inside the timed
 step.  Scaling is weak (fixed rows per GPU); value = total rows / max time.
 
+--config sel is the materialising form of C2's scan (`SELECT x FROM t WHERE
+x > 24`): the passing rows compacted in row order into a device-resident
+result (the reference's query_arrow path, rows counted through
+duckdb_mb_arrow_row_count), checked row for row against the oracle.
+
 Usage: python bench.py [--gpus N] [--steps K] [--warmup W] [--rows R]
-                       [--config c1|c2|c2d|c3|c4|c5] [--no-cpu] [--profile-steps]
+                       [--config c1|c2|c2d|c3|c4|c5|sel] [--no-cpu] [--profile-steps]
 """
 import argparse
 import json
@@ -48,7 +53,7 @@ def main():
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--rows", type=int, default=None,
                     help="rows per GPU (default 1e9; 1.25e9 for c5 = 1e10 over 8 GPUs)")
-    ap.add_argument("--config", default="c2", choices=["c1", "c2", "c2d", "c3", "c4", "c5"])
+    ap.add_argument("--config", default="c2", choices=["c1", "c2", "c2d", "c3", "c4", "c5", "sel"])
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--dry-run", action="store_true",
@@ -108,7 +113,7 @@ def main():
     if args.config == "c4":
         return bench_c4(mbx, conn, min(n, 100_000_000), args)
     c2like = args.config in ("c2", "c2d")  # c2d: C2 over DECIMAL(15,2) (raw = 100 x; x > 24 is raw > 2400)
-    if args.config in ("c2", "c2d", "c5"):
+    if args.config in ("c2", "c2d", "c5", "sel"):
         xexpr = "CAST(mbx_synth(42, i, 50) + 1 AS DECIMAL(15,2))" if args.config == "c2d" else "mbx_synth(42, i, 50) + 1"
         setup = (f"CREATE TABLE t AS SELECT {xexpr} AS x "
                  f"FROM range({start}, {start + n}) tbl(i)")
@@ -117,8 +122,14 @@ def main():
             sql = "SELECT COUNT(*), SUM(x) FROM t WHERE x > 24"
         kernel = "filter_agg"
         bytes_per_row = 8
+        if args.config == "sel":
+            sql = "SELECT x FROM t WHERE x > 24"
+            kernel = "select_rounds"
         workload = ("C2: SELECT COUNT(*) FROM t WHERE x > 24 over a device-resident 1e9-row INT64 column per GPU"
                     if args.config == "c2" else
+                    "C2 materialised (sel): SELECT x FROM t WHERE x > 24, the passing rows compacted in row order "
+                    "into a device-resident result (query_arrow + arrow_row_count), 1e9 INT64 rows per GPU"
+                    if args.config == "sel" else
                     "C2 DECIMAL(15,2) variant: SELECT COUNT(*) FROM t WHERE x > 24 (raw int64 > 2400) per GPU"
                     if args.config == "c2d" else
                     "C5: SELECT COUNT(*), SUM(x) FROM t WHERE x > 24, rows sharded per GPU")
@@ -137,6 +148,11 @@ def main():
     log(f"[rank {rank}] setup {time.time() - t0:.2f}s: {n} rows")
 
     def step():
+        if args.config == "sel":
+            a = conn.query_arrow(sql).value  # the result stays in HBM until a getter pulls it
+            rows = a.row_count()
+            a.close()
+            return [rows]
         rr = conn.query_raw(sql)
         if args.config == "c3":
             # (k, COUNT(*), SUM(v)) per group: every result cell's string, pulled
@@ -156,7 +172,7 @@ def main():
         # C2/C5 start it asynchronously (RCCL's stream) so that it overlaps the
         # next step's query on the engine stream; every step's global answer is
         # collected inside the timed region (finish_combines).
-        if world == 1:
+        if world == 1 or args.config == "sel":
             return None
         if c2like:
             return mbx_dist.allreduce_count_async(int(out[0]), device=coll_dev)  # RCCL over xGMI: COUNT(*)
@@ -222,6 +238,34 @@ def main():
                 parity["global_sum"] = gsum
                 parity["match"] = parity["match"] and gsum == g_osum
 
+    sel_rows = None
+    if args.config == "sel":
+        # parity: the full compacted column (one more query, outside the timed
+        # loop, pulled through the int64 Arrow getter) against the oracle's
+        # order-preserving selection over the same generator
+        import numpy as np
+        sys.path.insert(0, HERE)
+        from oracle import Oracle  # test infrastructure: checker only
+        orc = Oracle()
+        threads = host_share(world)
+        x = orc.synth_i64(n, 42, start, 50, 1)
+        exp = orc.select_i64(x, 25, 2**63 - 1, threads)
+        del x
+        sel_rows = int(out[0])
+        ok = sel_rows == len(exp)
+        sl = 25_000_000  # an Arrow Bytes holds < 2^28 bytes (MoonBit header): read the result in slices
+        for k in range(0, sel_rows, sl):
+            a = conn.query_arrow(f"{sql} LIMIT {sl} OFFSET {k}").value
+            raw = a.raw_int64_bytes(0)
+            a.close()
+            cnt = int.from_bytes(raw[:4], "little", signed=True) if len(raw) >= 4 else -1
+            ok = ok and cnt == min(sl, sel_rows - k) and \
+                bool(np.array_equal(np.frombuffer(raw, dtype=np.int64, offset=4, count=cnt), exp[k:k + cnt]))
+        parity = {"gpu_rows": sel_rows, "oracle_rows": int(len(exp)), "match": bool(ok),
+                  "checked": "every output value at its position (Arrow int64 getter, 25M-row LIMIT/OFFSET "
+                             "slices) vs the oracle's select_i64 over the same generator"}
+        del exp
+
     if args.config == "c3":
         sys.path.insert(0, HERE)
         from oracle import Oracle  # test infrastructure: checker only
@@ -241,7 +285,8 @@ def main():
         total_rows = n * world * args.steps
         value = total_rows / elapsed
         avg_kernel_ms = sum(kernel_ms) / len(kernel_ms) if kernel_ms else None
-        achieved = (n * bytes_per_row / (avg_kernel_ms * 1e-3)) / 1e9 if avg_kernel_ms else None
+        alg_bytes = n * bytes_per_row + (sel_rows * 8 if sel_rows is not None else 0)  # sel: + the selected rows written
+        achieved = (alg_bytes / (avg_kernel_ms * 1e-3)) / 1e9 if avg_kernel_ms else None
         traffic = None
         pmc = os.path.join(HERE, "profiles", "pmc_traffic.json")
         if os.path.exists(pmc):
@@ -278,13 +323,13 @@ def main():
                 "unit": "GB/s",
                 "frac": (achieved / HBM_PEAK_GBS) if achieved else None,
                 "traffic": traffic,
-                "algorithmic_bytes_per_launch": n * bytes_per_row,
+                "algorithmic_bytes_per_launch": alg_bytes,
                 "kernel_ms_avg": avg_kernel_ms,
                 "timing": "hipEventRecord pairs on the engine stream around every launch in the timed loop",
             },
             "parity": parity,
         }
-        if not args.no_cpu and world == 1 and args.config in ("c2", "c2d", "c3", "c5"):
+        if not args.no_cpu and world == 1 and args.config in ("c2", "c2d", "c3", "c5", "sel"):
             result["cpu_baseline"] = cpu_baseline(args.cpu_seconds, "c2" if args.config == "c2d" else args.config)
     if world > 1:
         dist.barrier()
@@ -489,6 +534,13 @@ def cpu_baseline(seconds, config="c2"):
         v = orc.synth_i64(sample, 9, 0, 1 << 40, -(1 << 39))
         run = lambda: orc.groupby_sum(k, v, 0, 32, threads)  # noqa: E731
         what = "GROUP BY k: COUNT(*), SUM(v) (int128), 32 keys"
+    elif config == "sel":
+        import numpy as np
+        x = orc.synth_i64(sample, 42, 0, 50, 1)
+        buf = np.empty(sample, dtype=np.int64)
+        buf.fill(0)  # first touch outside the timed loop
+        run = lambda: orc.select_i64(x, 25, 2**63 - 1, threads, out=buf)  # noqa: E731
+        what = "SELECT x WHERE x > 24: count pass + order-preserving copy of the passing rows"
     else:
         x = orc.synth_i64(sample, 42, 0, 50, 1)
         run = lambda: orc.filter_agg_i64(x, 25, 2**63 - 1, threads)  # noqa: E731

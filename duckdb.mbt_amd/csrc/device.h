@@ -347,10 +347,32 @@ struct SelectDesc {
   } col[SL_MAX_COL];
   int32_t out_col[SL_MAX_OUT];  // index into col[]
   void *dst[SL_MAX_OUT];
-  unsigned long long *dbg;  // nullptr, or 9 counters (MBX_SL_DEBUG)
+  unsigned long long *dbg;     // nullptr, or 9 counters (MBX_SL_DEBUG) / 13 (MBX_SR_DEBUG)
+  unsigned long long *dbg_ts;  // MBX_SR_DEBUG=2: s_memrealtime of every (round, workgroup) publish
 };
 size_t SelectStatusBytes(int64_t nrows, int ni);
 void SelectCompact(const SelectDesc &d, int64_t nrows, void *status_buf, int64_t *total, hipStream_t s);
+
+// Round-synchronous one-pass filter -> compaction (select_kernels.hip,
+// select_rounds): the same shapes and output contract as SelectCompact, one
+// persistent workgroup per CU.  Round r's tile of workgroup g is 4 S steps; a
+// workgroup's round count is published as an 8-byte {count, epoch} granule
+// and every workgroup reads each round's G granules to place its tile.  ctl:
+// SelectRoundsCtlBytes(plan) bytes, zeroed once when allocated and reused
+// with a fresh epoch per launch (never 0, never reused).  After the launch
+// ctl[0] == epoch means a workgroup gave up (no progress for 100 ms: a
+// workgroup was never scheduled) and the outputs are garbage; otherwise
+// ctl[1] is the selected-row count.
+struct SelectRoundsPlan {
+  bool ok;
+  int nc, wm, ni, depth, S, H, stg, G, sleep, test_stall;  // wm: bit c = column c is 8 bytes; H: 256-row sub-steps per step
+  int64_t nrounds;
+  size_t lds;
+};
+SelectRoundsPlan PlanSelectRounds(const SelectDesc &d, int64_t nrows);
+size_t SelectRoundsCtlBytes(const SelectRoundsPlan &p);
+void SelectRounds(const SelectDesc &d, const SelectRoundsPlan &p, int64_t nrows, unsigned long long *ctl,
+                  uint32_t epoch, hipStream_t s);
 
 }  // namespace dev
 }  // namespace mbx

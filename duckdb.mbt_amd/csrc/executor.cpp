@@ -106,6 +106,11 @@ struct Engine {
   hipStream_t stream = nullptr;
   int32_t *d_err = nullptr;
   int64_t *d_scratch = nullptr;  // small device scratch (counts)
+  // select_rounds control block (abort word, total, {count, epoch} granules):
+  // zeroed when (re)allocated, then reused with a fresh epoch per launch
+  unsigned long long *d_rounds = nullptr;
+  size_t rounds_bytes = 0;
+  uint32_t rounds_epoch = 0;
   void *d_small = nullptr;       // 64 KB scratch for small states
   dev::AggPartial *d_partials = nullptr;  // per-workgroup partials of the fused filter-aggregate
   // pinned host staging for small results: every D2H of a query lands here
@@ -176,6 +181,7 @@ struct Engine {
       }
       if (d_err) hipFree(d_err);
       if (d_scratch) hipFree(d_scratch);
+      if (d_rounds) hipFree(d_rounds);
       if (d_small) hipFree(d_small);
       if (d_partials) hipFree(d_partials);
       if (h_pinned) hipHostFree(h_pinned);
@@ -1014,21 +1020,33 @@ static bool FastIntCol(const DRel &rel, int c) {
   return d.validity == nullptr && (d.phys == P_I32 || d.phys == P_I64) && d.data != nullptr;
 }
 
-// One-pass form of the compaction below (dev::SelectCompact): NULL-free 4/8-byte
-// columns, at most SL_MAX_COL distinct loaded columns (predicates ∪ outputs)
-// and SL_MAX_OUT outputs.  Each loaded column is read from HBM once; outputs
-// are allocated for every row (the count is known only afterwards), so the
-// form is used while that upper bound stays under MBX_SL_MAX_GB (default 64).
-// Opt-in (MBX_SL=1): its decoupled look-back measured 2-9x slower than the
-// two-pass forms on this chip (profiles/r02_select_onepass.log).
+// One-pass forms of the compaction below, for NULL-free 4/8-byte columns, at
+// most SL_MAX_COL distinct loaded columns (predicates ∪ outputs) and
+// SL_MAX_OUT outputs.  Each loaded column is read from HBM once; outputs are
+// allocated for every row (the count is known only afterwards), so the form
+// is used while that upper bound stays under MBX_SL_MAX_GB (default 64).
+//  * default (n >= MBX_SR_MIN_ROWS, default 2^22): dev::SelectRounds, the
+//    round-synchronous kernel (one persistent workgroup per CU).  Engines that
+//    share a device (gpu_devices=0,0) take turns through a per-device lock, so
+//    two persistent grids never compete for the CUs; should a workgroup never
+//    be scheduled anyway, the kernel gives up after 100 ms without progress
+//    and the two-pass form runs instead.
+//  * MBX_SL=2: dev::SelectCompact, the decoupled look-back kernel (measured
+//    2-9x slower than the two-pass forms, profiles/r02_select_onepass.log).
+//  * MBX_SL=0: never (the count-first / ballot-bits two-pass forms).
+static std::mutex g_rounds_mu[64];
+
 static bool TrySelectOnePass(Engine &e, const DRel &rel, const dev::FilterMultiDesc &F,
                              const std::vector<BExprPtr> &exprs, DRel &out) {
   const char *env = getenv("MBX_SL");
-  if (!env || atoi(env) == 0) return false;  // opt-in: measured slower than the two-pass forms
+  const int mode = env ? atoi(env) : 1;
+  if (mode == 0) return false;
+  int64_t min_rows = (int64_t)1 << 22;
+  if (const char *m = getenv("MBX_SR_MIN_ROWS")) min_rows = atoll(m);
+  if (mode == 1 && rel.n < min_rows) return false;
   if ((int)exprs.size() > SL_MAX_OUT) return false;
   dev::SelectDesc S;
   memset(&S, 0, sizeof(S));
-  std::vector<const void *> loaded;
   auto slot_of = [&](const void *data, int w) -> int {
     for (int i = 0; i < S.ncol; i++)
       if (S.col[i].data == data) return S.col[i].w == w ? i : -2;
@@ -1063,32 +1081,124 @@ static bool TrySelectOnePass(Engine &e, const DRel &rel, const dev::FilterMultiD
   if (const char *c = getenv("MBX_SL_MAX_GB")) cap_gb = atof(c);
   if (out_bytes > cap_gb * 1e9) return false;
   const int64_t n = rel.n;
+  dev::SelectRoundsPlan plan;
+  memset(&plan, 0, sizeof(plan));
+  if (mode != 2) {
+    plan = dev::PlanSelectRounds(S, n);
+    if (!plan.ok) return false;
+  }
   std::vector<DCol> cols;
   for (int k = 0; k < (int)exprs.size(); k++) {
     cols.push_back(AllocOut(e, exprs[k]->type, n, false));
     S.dst[k] = cols[k].data;
   }
-  auto status = Alloc(e, dev::SelectStatusBytes(n, ni));
   double bytes = 0;
   for (int i = 0; i < S.ncol; i++) bytes += (double)n * S.col[i].w;
-  DevBufPtr dbgbuf;
-  if (getenv("MBX_SL_DEBUG")) {
-    dbgbuf = Alloc(e, 128, true);
-    S.dbg = (unsigned long long *)dbgbuf->p;
-  }
-  {
-    ProfScope ps(e, "select", bytes, n);  // algorithmic: inputs once (+ the selected rows' outputs, added below)
-    dev::SelectCompact(S, n, status->p, e.d_scratch, e.stream);
-  }
-  if (dbgbuf) {
-    unsigned long long h[9];
-    HIPCHK(hipMemcpyAsync(h, dbgbuf->p, sizeof(h), hipMemcpyDeviceToHost, e.stream));
+  int64_t nsel = 0;
+  if (mode != 2) {
+    std::unique_lock<std::mutex> lk(g_rounds_mu[e.device & 63]);
+    const size_t need = dev::SelectRoundsCtlBytes(plan);
+    if (need > e.rounds_bytes) {
+      HIPCHK(hipStreamSynchronize(e.stream));
+      if (e.d_rounds) HIPCHK(hipFree(e.d_rounds));
+      e.d_rounds = nullptr;
+      size_t b = 1 << 20;
+      while (b < need) b <<= 1;
+      HIPCHK(hipMalloc((void **)&e.d_rounds, b));
+      HIPCHK(hipMemsetAsync(e.d_rounds, 0, b, e.stream));
+      e.rounds_bytes = b;
+      e.rounds_epoch = 0;
+    }
+    if (++e.rounds_epoch == 0) {  // 2^32 launches: start over from a zeroed block
+      HIPCHK(hipMemsetAsync(e.d_rounds, 0, e.rounds_bytes, e.stream));
+      e.rounds_epoch = 1;
+    }
+    const uint32_t epoch = e.rounds_epoch;
+    DevBufPtr dbgbuf, tsbuf;
+    if (getenv("MBX_SR_DEBUG")) {
+      dbgbuf = Alloc(e, 256, true);
+      HIPCHK(hipMemsetAsync(dbgbuf->p, 0, 256, e.stream));
+      S.dbg = (unsigned long long *)dbgbuf->p;
+      if (atoi(getenv("MBX_SR_DEBUG")) == 2) {
+        tsbuf = Alloc(e, (size_t)plan.nrounds * plan.G * 8, true);
+        S.dbg_ts = (unsigned long long *)tsbuf->p;
+      }
+    }
+    {
+      ProfScope ps(e, "select_rounds", bytes, n);  // algorithmic: inputs once (+ the selected rows' outputs, added below)
+      dev::SelectRounds(S, plan, n, e.d_rounds, epoch, e.stream);
+    }
+    if (dbgbuf) {
+      unsigned long long h[13];
+      HIPCHK(hipMemcpyAsync(h, dbgbuf->p, sizeof(h), hipMemcpyDeviceToHost, e.stream));
+      HIPCHK(hipStreamSynchronize(e.stream));
+      const double L = (double)plan.G * 4, C = (double)plan.G;
+      fprintf(stderr, "[select_rounds] G %d rounds %lld S %d stg %d depth %d | per loader: cycles %.0f dma_wait %.0f "
+              "staging_wait %.0f meta_wait %.0f | per storer: cycles %.0f base_wait %.0f | per coordinator: cycles %.0f "
+              "polls %.1f no_progress %.1f poll_load_cycles %.0f (%.0f per poll) rounds %.1f max/poll %llu "
+              "publish->resolve %.0f cycles/round\n",
+              plan.G, (long long)plan.nrounds, plan.S, plan.stg, plan.depth, h[0] / L, h[1] / L, h[2] / L, h[3] / L,
+              h[4] / L, h[5] / L, h[6] / C, h[7] / C, h[8] / C, h[9] / C, h[7] ? (double)h[9] / h[7] : 0.0, h[10] / C,
+              h[11], h[10] ? (double)h[12] / h[10] : 0.0);
+      if (tsbuf) {  // publish-time spread per round (10 ns ticks): how far the last workgroup trails
+        std::vector<unsigned long long> ts((size_t)plan.nrounds * plan.G);
+        HIPCHK(hipMemcpy(ts.data(), tsbuf->p, ts.size() * 8, hipMemcpyDeviceToHost));
+        std::vector<double> spread, late_med;
+        std::vector<double> wg_late(plan.G, 0.0);
+        for (int64_t r = 0; r < plan.nrounds; r++) {
+          std::vector<unsigned long long> v(ts.begin() + r * plan.G, ts.begin() + (r + 1) * plan.G);
+          std::vector<unsigned long long> srt = v;
+          std::sort(srt.begin(), srt.end());
+          spread.push_back((double)(srt.back() - srt.front()));
+          late_med.push_back((double)(srt.back() - srt[srt.size() / 2]));
+          for (int gg = 0; gg < plan.G; gg++) wg_late[gg] += (double)(v[gg] - srt[srt.size() / 2]);
+        }
+        auto mean = [](const std::vector<double> &x) { double a = 0; for (double y : x) a += y; return x.empty() ? 0 : a / x.size(); };
+        std::sort(spread.begin(), spread.end());
+        int worst = 0;
+        for (int gg = 1; gg < plan.G; gg++) if (wg_late[gg] > wg_late[worst]) worst = gg;
+        std::vector<double> wl = wg_late;
+        std::sort(wl.begin(), wl.end());
+        fprintf(stderr, "[select_rounds] publish spread per round (us): mean %.2f median %.2f p90 %.2f max %.2f | "
+                "last - median mean %.2f | round period %.2f us | per-WG mean lateness vs median (us): min %.2f "
+                "median %.2f max %.2f (wg %d)\n",
+                mean(spread) / 100, spread[spread.size() / 2] / 100, spread[spread.size() * 9 / 10] / 100,
+                spread.back() / 100, mean(late_med) / 100,
+                plan.nrounds > 1 ? (double)(ts[(plan.nrounds - 1) * plan.G] - ts[0]) / 100 / (plan.nrounds - 1) : 0.0,
+                wl.front() / plan.nrounds / 100, wl[wl.size() / 2] / plan.nrounds / 100, wl.back() / plan.nrounds / 100,
+                worst);
+      }
+    }
+    unsigned long long h[2];
+    HIPCHK(hipMemcpyAsync(h, e.d_rounds, sizeof(h), hipMemcpyDeviceToHost, e.stream));
     HIPCHK(hipStreamSynchronize(e.stream));
-    fprintf(stderr, "[select] dma_wait %llu b1b2 %llu lookback %llu ticket %llu compact %llu windows %llu spins %llu "
-            "tiles %llu total %llu (cycles summed over workgroups)\n", h[0], h[1], h[2], h[3], h[4], h[5], h[6], h[7], h[8]);
+    lk.unlock();
+    if (h[0] == (unsigned long long)epoch) {  // a workgroup was never scheduled: two-pass form instead
+      if (e.profile && !e.events.empty() && e.events.back().name == "select_rounds") e.events.back().name = "select_rounds_abort";
+      return false;
+    }
+    nsel = (int64_t)h[1];
+  } else {
+    auto status = Alloc(e, dev::SelectStatusBytes(n, ni));
+    DevBufPtr dbgbuf;
+    if (getenv("MBX_SL_DEBUG")) {
+      dbgbuf = Alloc(e, 128, true);
+      S.dbg = (unsigned long long *)dbgbuf->p;
+    }
+    {
+      ProfScope ps(e, "select", bytes, n);
+      dev::SelectCompact(S, n, status->p, e.d_scratch, e.stream);
+    }
+    if (dbgbuf) {
+      unsigned long long h[9];
+      HIPCHK(hipMemcpyAsync(h, dbgbuf->p, sizeof(h), hipMemcpyDeviceToHost, e.stream));
+      HIPCHK(hipStreamSynchronize(e.stream));
+      fprintf(stderr, "[select] dma_wait %llu b1b2 %llu lookback %llu ticket %llu compact %llu windows %llu spins %llu "
+              "tiles %llu total %llu (cycles summed over workgroups)\n", h[0], h[1], h[2], h[3], h[4], h[5], h[6], h[7], h[8]);
+    }
+    nsel = ReadDev<int64_t>(e, e.d_scratch);
   }
-  const int64_t nsel = ReadDev<int64_t>(e, e.d_scratch);
-  if (e.profile && !e.events.empty() && e.events.back().name == "select") {
+  if (e.profile && !e.events.empty() && (e.events.back().name == "select" || e.events.back().name == "select_rounds")) {
     double ob = 0;
     for (int k = 0; k < S.nout; k++) ob += (double)nsel * S.col[S.out_col[k]].w;
     e.events.back().bytes += ob;

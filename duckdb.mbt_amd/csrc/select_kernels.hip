@@ -35,6 +35,8 @@
 #include <hip/hip_runtime.h>
 #include <stdexcept>
 #include <stdint.h>
+#include <stdlib.h>
+#include <string.h>
 
 #include "device.h"
 #include "types.h"
@@ -355,6 +357,612 @@ void SelectCompact(const SelectDesc &d, int64_t nrows, void *status_buf, int64_t
   (void)hipGetLastError();
 }
 
+
+// ---------------------------------------------------------------------------
+// Round-synchronous one-pass compaction (select_rounds; see device.h).
+//
+// One persistent workgroup per CU (G of them), 9 waves with fixed roles:
+//  * waves 0-3, loaders: stream their steps of every loaded column through an
+//    LDS-DMA ring (as filter_agg_lds does), evaluate the predicates and write
+//    each selected value straight into the wave's staging ring in LDS (its
+//    rank from the ballots).  Tile t = r G + g of round r is 4 S consecutive
+//    steps (loader w owns steps [4 S t + w S, 4 S t + (w + 1) S)).  At the end
+//    of a round the last loader to arrive (an LDS atomic) publishes the
+//    workgroup's round count as one 8-byte {count, epoch} granule with an sc1
+//    store: data and flag in one word, no ordering needed.
+//  * wave 8, coordinator: polls the G granules of the oldest unresolved
+//    rounds (sc1 loads, SR_PW rounds per poll); once a round is complete it
+//    knows the round's total and the workgroup's exclusive prefix, so the
+//    tile's output position is running + prefix.  It hands that to the
+//    storers through LDS.  No look-back chains: every coordinator reads every
+//    round's G counts once (2 KB), and nothing waits on a ticket.
+//  * waves 4-7, storers: storer s moves loader s's staged values of the round
+//    to base + Σ counts of loaders < s with contiguous 8/4-byte stores, then
+//    frees the staging rows.  Stores never share a vmcnt queue with the DMA.
+// Loaders run ahead of the storers by as many rounds as the staging rings
+// and the SR_MR meta slots allow, which hides the poll latency.
+// Progress: the workgroup at the lowest round only waits for rounds every
+// other workgroup has already published, provided all G workgroups are
+// resident (G = #CUs, LDS padded past half a CU, so one per CU).  Should a
+// workgroup never be scheduled, a coordinator that sees no progress for
+// SR_TIMEOUT gives up: it writes the launch's epoch into the abort word, every
+// wave leaves its loop (loaders drain their DMA first), and the host falls
+// back to the two-pass form.
+// ---------------------------------------------------------------------------
+namespace {
+constexpr int SR_MR = 32;                    // rounds in flight inside a workgroup (meta slots)
+constexpr int SR_PW = 2;                     // rounds polled per coordinator poll
+constexpr long long SR_TIMEOUT = 10000000;   // s_memrealtime ticks (100 MHz): 100 ms without progress
+struct SrShared {
+  unsigned long long arr[SR_MR];  // (count << 16) + arrivals of the round's loaders
+  uint32_t cnt[SR_MR][4];         // each loader's count of the round
+  long long base[SR_MR];          // output row of the workgroup's tile of the round
+  uint32_t btag[SR_MR];           // round + 1 once base is set
+  uint32_t tail[4];               // staging rows freed, per loader (monotonic)
+  uint32_t sdone[4];              // rounds finished, per storer
+  uint32_t abort_;
+  unsigned long long pubt[SR_MR];  // MBX_SR_DEBUG: clock64 when the round's granule was published
+};
+// Control words in LDS are read and written with inline-asm ds_* ops: the
+// compiler puts an s_waitcnt vmcnt(0) in front of every atomic or volatile LDS
+// access once LDS-DMA is in flight (it cannot prove they do not alias the DMA
+// targets), which would drain a loader's whole ring at every check.  Each op
+// waits for itself (lgkmcnt(0)), so program order is LDS order.
+__device__ __forceinline__ uint32_t lds_addr(const void *p) {
+  return (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) void *)p;
+}
+// (reads return the value as a wave-uniform scalar: every control word is
+// uniform, and a VGPR result would make the branches on it divergent)
+__device__ __forceinline__ uint32_t lds_ld(const uint32_t *p) {
+  uint32_t v;
+  asm volatile("ds_read_b32 %0, %1\n\ts_waitcnt lgkmcnt(0)" : "=v"(v) : "v"(lds_addr(p)) : "memory");
+  return __builtin_amdgcn_readfirstlane(v);
+}
+__device__ __forceinline__ long long lds_ld(const long long *p) {
+  long long v;
+  asm volatile("ds_read_b64 %0, %1\n\ts_waitcnt lgkmcnt(0)" : "=v"(v) : "v"(lds_addr(p)) : "memory");
+  return sl_uni(v);
+}
+__device__ __forceinline__ void lds_st(uint32_t *p, uint32_t v) {
+  asm volatile("ds_write_b32 %0, %1\n\ts_waitcnt lgkmcnt(0)" ::"v"(lds_addr(p)), "v"(v) : "memory");
+}
+__device__ __forceinline__ void lds_st(long long *p, long long v) {
+  asm volatile("ds_write_b64 %0, %1\n\ts_waitcnt lgkmcnt(0)" ::"v"(lds_addr(p)), "v"(v) : "memory");
+}
+__device__ __forceinline__ void lds_st(unsigned long long *p, unsigned long long v) {
+  asm volatile("ds_write_b64 %0, %1\n\ts_waitcnt lgkmcnt(0)" ::"v"(lds_addr(p)), "v"(v) : "memory");
+}
+__device__ __forceinline__ unsigned long long lds_add_rtn(unsigned long long *p, unsigned long long v) {
+  unsigned long long old;
+  asm volatile("ds_add_rtn_u64 %0, %1, %2\n\ts_waitcnt lgkmcnt(0)" : "=v"(old) : "v"(lds_addr(p)), "v"(v) : "memory");
+  return old;
+}
+}  // namespace
+
+// NC loaded columns; bit c of WM: column c is 8 bytes wide (else 4).
+template <int NC, int WM>
+struct SrCols {
+  static constexpr int w(int c) { return (WM >> c) & 1 ? 8 : 4; }
+  static constexpr int off(int c) { return c == 0 ? 0 : off(c - 1) + w(c - 1) * 256; }
+  static constexpr int ni() { return off(NC) / 1024; }
+};
+
+// Staging: every loaded column that feeds an output (bit c of D's staged mask)
+// has an array of stg + 64 entries per loader (the 64 extra are each lane's
+// dump slot for unselected rows, so the writes need no exec masking).
+// A step is H x 256 consecutive rows (sub-step h = rows 256 h .. 256 h + 255
+// of it); a loader handles its H sub-steps in one pass, so their dependency
+// chains interleave (one loader wave per SIMD cannot hide its own latencies).
+template <int NC, int WM, int DEPTH, int H>
+__global__ __launch_bounds__(576) void select_rounds_kernel(SelectDesc D, int64_t n, int64_t nrounds, int S, int stg,
+                                                            unsigned long long *ctl, uint32_t epoch, int sleep_,
+                                                            int test_stall) {
+  typedef SrCols<NC, WM> L;
+  extern __shared__ __attribute__((aligned(16))) unsigned char sr_lds[];
+  __shared__ SrShared sm;
+  constexpr int SB1 = L::off(NC);  // one 256-row sub-step of every loaded column
+  constexpr int SB = H * SB1;       // a ring slot: one step
+  constexpr int NI = H * L::ni();   // LDS-DMA instructions per step
+  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int G = gridDim.x, g = blockIdx.x;
+  const int64_t nsteps = n / (256 * H);
+  unsigned long long *gran = ctl + 8;  // ctl[0]: abort word, ctl[1]: total, granules from ctl[8]
+  {
+    uint32_t *z = (uint32_t *)&sm;
+    for (int i = threadIdx.x; i < (int)(sizeof(SrShared) / 4); i += blockDim.x) z[i] = 0;
+  }
+  __syncthreads();  // the only barrier: the roles diverge below
+  // staged columns: the byte offset of column c's array in a loader's staging area
+  int soff[NC];
+  uint32_t smask = 0;
+  int rowb = 0;
+  for (int o = 0; o < D.nout; o++) smask |= 1u << D.out_col[o];
+#pragma unroll
+  for (int c = 0; c < NC; c++) {
+    soff[c] = rowb * (stg + 64);
+    if ((smask >> c) & 1) rowb += L::w(c);
+  }
+  unsigned char *stage0 = sr_lds + (size_t)4 * DEPTH * SB;
+  const uint32_t mask = (uint32_t)stg - 1;
+  const uint64_t lt = (1ull << lane) - 1;
+
+  if (w < 4) {
+    // ------------------------------------------------------------ loader
+    if (nrounds == 0) return;
+    unsigned char *ring = sr_lds + (size_t)w * DEPTH * SB;
+    unsigned char *mystage = stage0 + (size_t)w * (stg + 64) * rowb;
+    const int64_t qstride = (int64_t)G * 4 * S;  // steps between a wave's tiles of consecutive rounds
+    const unsigned char *colp[NC];
+    int64_t lo[NC];
+    uint64_t span[NC];
+    uint32_t pmask = 0;
+#pragma unroll
+    for (int c = 0; c < NC; c++) {
+      colp[c] = (const unsigned char *)D.col[c].data + lane * 16;
+      lo[c] = D.col[c].lo;
+      span[c] = D.col[c].span;
+      pmask |= (D.col[c].is_pred ? 1u : 0u) << c;
+    }
+    int64_t iq = ((int64_t)g * 4 + w) * S, ir = 0;  // the next step to issue: round ir, step iq
+    int is = 0;
+    auto issue = [&](int slot) {  // dead steps re-load step 0: a fixed count per slot
+      const int64_t q = ir < nrounds && iq + is < nsteps ? iq + is : 0;
+      if (++is == S) {
+        is = 0;
+        ir++;
+        iq += qstride;
+      }
+#pragma unroll
+      for (int h = 0; h < H; h++) {
+        unsigned char *dst = ring + slot * SB + h * SB1;
+#pragma unroll
+        for (int c = 0; c < NC; c++) {
+          const unsigned char *src = colp[c] + (q * H + h) * (L::w(c) * 256);
+          __builtin_amdgcn_global_load_lds((const void *)src, (void *)(dst + L::off(c)), 16, 0, 2);
+          if (L::w(c) == 8)
+            __builtin_amdgcn_global_load_lds((const void *)(src + 1024), (void *)(dst + L::off(c) + 1024), 16, 0, 2);
+        }
+      }
+    };
+#pragma unroll
+    for (int d = 0; d < DEPTH; d++) issue(d);
+    int k = 0;
+    uint32_t head = 0, tail_seen = 0;
+    bool quit = false;
+    // MBX_SR_DEBUG (D.dbg): cycles in total, waiting on the DMA, on staging room, on meta slots
+    const bool dbg = D.dbg != nullptr;
+    unsigned long long t_all = dbg ? clock64() : 0, d_dma = 0, d_stg = 0, d_meta = 0, t0 = 0;
+    int64_t qb = ((int64_t)g * 4 + w) * S;  // this round's first step
+    for (int64_t r = 0; r < nrounds && !quit; r++, qb += qstride) {
+      const int slot = (int)(r % SR_MR);
+      if (r >= SR_MR) {  // meta slot reuse: every storer is done with round r - SR_MR
+        const uint32_t need = (uint32_t)(r - SR_MR + 1);
+        if (dbg) t0 = clock64();
+        while (true) {
+          uint32_t m = lds_ld(&sm.sdone[0]);
+          m = min(m, lds_ld(&sm.sdone[1]));
+          m = min(m, lds_ld(&sm.sdone[2]));
+          m = min(m, lds_ld(&sm.sdone[3]));
+          if (__builtin_amdgcn_readfirstlane(m) >= need) break;
+          if (lds_ld(&sm.abort_)) { quit = true; break; }
+          __builtin_amdgcn_s_sleep(1);
+        }
+        if (dbg) d_meta += clock64() - t0;
+        if (quit) break;
+      }
+      const int64_t live_steps = nsteps - qb;  // steps s < live_steps hold data
+      uint32_t rc = 0;
+      for (int s = 0; s < S; s++) {
+        if (dbg) t0 = clock64();
+        asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NI * (DEPTH - 1)) : "memory");
+        if (dbg) d_dma += clock64() - t0;
+        const unsigned char *src = ring + k * SB;
+        int64_t v[H][NC][4];
+#pragma unroll
+        for (int h = 0; h < H; h++)
+#pragma unroll
+          for (int c = 0; c < NC; c++) sl_read4(src + h * SB1 + L::off(c), L::w(c), lane, v[h][c]);
+        // ok[h][e]: row 256 h + 4 lane + e passes (kept as lane masks: each ballot is the compare's own mask)
+        const bool live = s < live_steps;
+        bool ok[H][4];
+#pragma unroll
+        for (int h = 0; h < H; h++)
+#pragma unroll
+          for (int e = 0; e < 4; e++) ok[h][e] = live;
+#pragma unroll
+        for (int c = 0; c < NC; c++) {
+          if (NC > 1 && !((pmask >> c) & 1)) continue;  // a lone column is the predicate column
+#pragma unroll
+          for (int h = 0; h < H; h++)
+#pragma unroll
+            for (int e = 0; e < 4; e++) ok[h][e] = ok[h][e] & ((uint64_t)(v[h][c][e] - lo[c]) <= span[c]);
+        }
+        unsigned long long b[H][4];
+        uint32_t hc[H];  // selected rows per sub-step
+        uint32_t cnt = 0;
+#pragma unroll
+        for (int h = 0; h < H; h++) {
+          hc[h] = 0;
+#pragma unroll
+          for (int e = 0; e < 4; e++) {
+            b[h][e] = __ballot(ok[h][e]);
+            hc[h] += (uint32_t)__popcll(b[h][e]);
+          }
+          cnt += hc[h];
+        }
+        if (cnt) {
+          if (head + 256u * H - tail_seen > (uint32_t)stg) {  // staging full: wait for the storer
+            if (dbg) t0 = clock64();
+            while (true) {
+              tail_seen = lds_ld(&sm.tail[w]);
+              if (head + 256u * H - tail_seen <= (uint32_t)stg) break;
+              if (lds_ld(&sm.abort_)) { quit = true; break; }
+              __builtin_amdgcn_s_sleep(1);
+            }
+            if (dbg) d_stg += clock64() - t0;
+            if (quit) break;
+          }
+          uint32_t hb = head;
+#pragma unroll
+          for (int h = 0; h < H; h++) {
+            // rank of row (h, lane, e): earlier sub-steps, selected rows of lower lanes (mbcnt),
+            // then this lane's earlier rows
+            uint32_t rk = hb;
+#pragma unroll
+            for (int e = 0; e < 4; e++)
+              rk = __builtin_amdgcn_mbcnt_hi((uint32_t)(b[h][e] >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)b[h][e], rk));
+            uint32_t idx[4];
+#pragma unroll
+            for (int e = 0; e < 4; e++) {
+              idx[e] = ok[h][e] ? (rk & mask) : (uint32_t)stg + lane;
+              rk += ok[h][e];
+            }
+#pragma unroll
+            for (int c = 0; c < NC; c++) {
+              if (!((smask >> c) & 1)) continue;
+              unsigned char *st = mystage + soff[c];
+#pragma unroll
+              for (int e = 0; e < 4; e++) {
+                if (L::w(c) == 8) ((int64_t *)st)[idx[e]] = v[h][c][e];
+                else ((int32_t *)st)[idx[e]] = (int32_t)v[h][c][e];
+              }
+            }
+            hb += hc[h];
+          }
+          head = __builtin_amdgcn_readfirstlane(head + cnt);  // wave-uniform: keeps the room check scalar
+          rc += cnt;
+        }
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // slot read (and staging written) before the DMA reuses it
+        issue(k);
+        k = k + 1 == DEPTH ? 0 : k + 1;
+      }
+      if (quit) break;
+      if (lane == 0) {
+        lds_st(&sm.cnt[slot][w], rc);
+        const unsigned long long old =
+            (unsigned long long)sl_uni((int64_t)lds_add_rtn(&sm.arr[slot], ((unsigned long long)rc << 16) + 1));
+        if ((old & 0xffff) == 3 && g != test_stall) {  // the last loader of the round publishes the workgroup's count
+          lds_st(&sm.arr[slot], 0ull);
+          const unsigned long long tot = (old >> 16) + rc;
+          __hip_atomic_store(&gran[r * G + g], ((unsigned long long)epoch << 32) | tot, __ATOMIC_RELAXED,
+                             __HIP_MEMORY_SCOPE_AGENT);
+          if (dbg) {
+            lds_st(&sm.pubt[slot], (unsigned long long)clock64());
+            if (D.dbg_ts) D.dbg_ts[r * G + g] = __builtin_amdgcn_s_memrealtime();  // MBX_SR_DEBUG=2: publish times
+          }
+        }
+      }
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // no LDS-DMA may land after the workgroup ends
+    if (dbg && lane == 0) {
+      atomicAdd(&D.dbg[0], clock64() - t_all);
+      atomicAdd(&D.dbg[1], d_dma);
+      atomicAdd(&D.dbg[2], d_stg);
+      atomicAdd(&D.dbg[3], d_meta);
+    }
+    return;
+  }
+  if (w < 8) {
+    // ------------------------------------------------------------ storer
+    const int sw = w - 4;
+    const unsigned char *mystage = stage0 + (size_t)sw * (stg + 64) * rowb;
+    uint32_t tail = 0;
+    const bool dbg = D.dbg != nullptr;
+    unsigned long long t_all = dbg ? clock64() : 0, d_wait = 0, t0 = 0;
+    for (int64_t r = 0; r < nrounds; r++) {
+      const int slot = (int)(r % SR_MR);
+      bool quit = false;
+      if (dbg) t0 = clock64();
+      while (__builtin_amdgcn_readfirstlane(lds_ld(&sm.btag[slot])) != (uint32_t)(r + 1)) {
+        if (lds_ld(&sm.abort_)) { quit = true; break; }
+        __builtin_amdgcn_s_sleep(1);
+      }
+      if (dbg) d_wait += clock64() - t0;
+      if (quit) break;
+      int64_t pos = sl_uni(lds_ld(&sm.base[slot]));
+      for (int q = 0; q < sw; q++) pos += lds_ld(&sm.cnt[slot][q]);
+      pos = sl_uni(pos);
+      const uint32_t c = __builtin_amdgcn_readfirstlane(lds_ld(&sm.cnt[slot][sw]));
+      for (int o = 0; o < D.nout; o++) {
+        const int oc = D.out_col[o];
+        int so = 0;
+#pragma unroll
+        for (int c = 0; c < NC; c++)
+          if (c == oc) so = soff[c];
+        if (D.col[oc].w == 8) {
+          const int64_t *st = (const int64_t *)(mystage + so);
+          int64_t *dst = (int64_t *)D.dst[o] + pos;
+          for (uint32_t i = lane; i < c; i += 64) dst[i] = st[(tail + i) & mask];
+        } else {
+          const int32_t *st = (const int32_t *)(mystage + so);
+          int32_t *dst = (int32_t *)D.dst[o] + pos;
+          for (uint32_t i = lane; i < c; i += 64) dst[i] = st[(tail + i) & mask];
+        }
+      }
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // staging read before it is freed
+      tail += c;
+      if (lane == 0) {
+        lds_st(&sm.tail[sw], tail);
+        lds_st(&sm.sdone[sw], (uint32_t)(r + 1));
+      }
+    }
+    if (dbg && lane == 0) {
+      atomicAdd(&D.dbg[4], clock64() - t_all);
+      atomicAdd(&D.dbg[5], d_wait);
+    }
+    return;
+  }
+  // -------------------------------------------------------------- coordinator
+  int64_t running = 0, r0 = 0;
+  long long last = (long long)__builtin_amdgcn_s_memrealtime();
+  bool aborted = false;
+  // MBX_SR_DEBUG: total cycles, polls, polls without progress, cycles in poll loads,
+  // rounds resolved, most rounds in one poll, publish -> resolve cycles
+  const bool dbg = D.dbg != nullptr;
+  unsigned long long t_all = dbg ? clock64() : 0, c_polls = 0, c_fail = 0, c_load = 0, c_res = 0, c_max = 0, c_lag = 0,
+                     t0 = 0;
+  while (r0 < nrounds) {
+    if (__hip_atomic_load(&ctl[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == (unsigned long long)epoch) {
+      aborted = true;  // another workgroup gave up
+      break;
+    }
+    const int pw = (int)(nrounds - r0 < SR_PW ? nrounds - r0 : SR_PW);
+    if (dbg) t0 = clock64();
+    unsigned long long x[SR_PW][4];
+#pragma unroll
+    for (int i = 0; i < SR_PW; i++)
+#pragma unroll
+      for (int j = 0; j < 4; j++) {
+        const int idx = 4 * lane + j;
+        x[i][j] = (i < pw && idx < G)
+                      ? __hip_atomic_load(&gran[(r0 + i) * G + idx], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                      : ((unsigned long long)epoch << 32);
+      }
+    if (dbg) {
+      unsigned long long acc = 0;
+#pragma unroll
+      for (int i = 0; i < SR_PW; i++)
+#pragma unroll
+        for (int j = 0; j < 4; j++) acc ^= x[i][j];
+      if (__ballot(acc == 0x5a5a5a5a5a5aull)) c_polls += 0;  // uses the loads: the clock below waits for them
+      c_load += clock64() - t0;
+      c_polls++;
+    }
+    int prog = 0;
+#pragma unroll
+    for (int i = 0; i < SR_PW; i++) {
+      if (i >= pw) break;
+      bool mine = true;
+      int64_t sa = 0, sb = 0;
+#pragma unroll
+      for (int j = 0; j < 4; j++) {
+        mine = mine && (uint32_t)(x[i][j] >> 32) == epoch;
+        const int64_t c = (int64_t)(uint32_t)x[i][j];
+        sa += c;
+        if (4 * lane + j < g) sb += c;
+      }
+      if (__ballot(!mine)) break;  // the round is not complete yet
+      sa = sl_wave_sum(sa);
+      sb = sl_wave_sum(sb);
+      if (lane == 0) {
+        const int slot = (int)((r0 + i) % SR_MR);
+        lds_st(&sm.base[slot], (long long)(running + sb));
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        lds_st(&sm.btag[slot], (uint32_t)(r0 + i + 1));
+      }
+      if (dbg) c_lag += clock64() - (unsigned long long)lds_ld((const long long *)&sm.pubt[(r0 + i) % SR_MR]);
+      running += sa;
+      prog++;
+    }
+    r0 += prog;
+    if (dbg) {
+      c_res += prog;
+      c_max = c_max > (unsigned long long)prog ? c_max : (unsigned long long)prog;
+      c_fail += prog == 0;
+    }
+    const long long now = (long long)__builtin_amdgcn_s_memrealtime();
+    if (prog) {
+      last = now;
+    } else {
+      if (now - last > SR_TIMEOUT) {
+        if (lane == 0)
+          __hip_atomic_store(&ctl[0], (unsigned long long)epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        aborted = true;
+        break;
+      }
+      for (int i = 0; i < sleep_; i++) __builtin_amdgcn_s_sleep(8);
+    }
+  }
+  if (dbg && lane == 0) {
+    atomicAdd(&D.dbg[6], clock64() - t_all);
+    atomicAdd(&D.dbg[7], c_polls);
+    atomicAdd(&D.dbg[8], c_fail);
+    atomicAdd(&D.dbg[9], c_load);
+    atomicAdd(&D.dbg[10], c_res);
+    atomicMax(&D.dbg[11], c_max);
+    atomicAdd(&D.dbg[12], c_lag);
+  }
+  if (aborted) {
+    if (lane == 0) lds_st(&sm.abort_, 1u);
+    return;
+  }
+  if (g != 0) return;
+  // workgroup 0: the rows after the last full step (guarded loads, 256 per pass), and the total
+  int64_t tcnt = 0;
+  for (int64_t base = nsteps * 256 * H; base < n; base += 256) {
+    bool ok[4];
+    const int64_t i0 = base + 4 * lane;
+#pragma unroll
+    for (int e = 0; e < 4; e++) {
+      const int64_t i = i0 + e;
+      ok[e] = i < n;
+      for (int c = 0; c < D.ncol && ok[e]; c++) {
+        if (!D.col[c].is_pred) continue;
+        const int64_t xv = D.col[c].w == 8 ? ((const int64_t *)D.col[c].data)[i]
+                                           : (int64_t)((const int32_t *)D.col[c].data)[i];
+        ok[e] = (uint64_t)(xv - D.col[c].lo) <= D.col[c].span;
+      }
+    }
+    unsigned long long bb[4];
+#pragma unroll
+    for (int e = 0; e < 4; e++) bb[e] = __ballot(ok[e]);
+    int64_t pos = running + tcnt + __popcll(bb[0] & lt) + __popcll(bb[1] & lt) + __popcll(bb[2] & lt) +
+                  __popcll(bb[3] & lt);
+    for (int e = 0; e < 4; e++) {
+      if (!ok[e]) continue;
+      for (int o = 0; o < D.nout; o++) {
+        const int c = D.out_col[o];
+        if (D.col[c].w == 8) ((int64_t *)D.dst[o])[pos] = ((const int64_t *)D.col[c].data)[i0 + e];
+        else ((int32_t *)D.dst[o])[pos] = ((const int32_t *)D.col[c].data)[i0 + e];
+      }
+      pos++;
+    }
+    tcnt += __popcll(bb[0]) + __popcll(bb[1]) + __popcll(bb[2]) + __popcll(bb[3]);
+  }
+  if (lane == 0) ctl[1] = (unsigned long long)(running + tcnt);
+}
+
+SelectRoundsPlan PlanSelectRounds(const SelectDesc &d, int64_t nrows) {
+  SelectRoundsPlan p;
+  memset(&p, 0, sizeof(p));
+  if (d.ncol < 1 || d.ncol > SL_MAX_COL || d.nout < 1 || d.nout > SL_MAX_OUT) return p;
+  uint32_t smask = 0;
+  for (int k = 0; k < d.nout; k++) smask |= 1u << d.out_col[k];
+  int rowb = 0;  // staged bytes per row: every distinct loaded column an output reads
+  for (int c = 0; c < d.ncol; c++) {
+    if (d.col[c].w != 4 && d.col[c].w != 8) return p;
+    p.ni += d.col[c].w / 4;
+    if (d.col[c].w == 8) p.wm |= 1 << c;
+    if ((smask >> c) & 1) rowb += d.col[c].w;
+  }
+  p.nc = d.ncol;
+  // Ring and staging share the CU's LDS.  Sub-steps per step (H) and ring depth
+  // per H: H = 1 with a 3-deep ring for one- and two-slot columns sets, else 2;
+  // H = 2 with a 2-deep ring.  H is the one that leaves the larger staging ring
+  // (the staging ring is what hides the round latency; ties go to H = 2, whose
+  // two interleaved sub-steps cost the loader fewer cycles per row).
+  int want_h = 0, want_s = 0, want_stg = 4096, want_depth = 0;
+  if (const char *e = getenv("MBX_SR_H")) want_h = atoi(e) == 1 ? 1 : 2;
+  if (const char *e = getenv("MBX_SR_S")) want_s = atoi(e) > 0 ? atoi(e) : 0;
+  if (const char *e = getenv("MBX_SR_STG")) want_stg = atoi(e) >= 256 ? atoi(e) : 4096;
+  if (const char *e = getenv("MBX_SR_DEPTH")) {
+    const int v = atoi(e);
+    if (p.nc == 1 && (v == 2 || v == 3 || v == 4 || v == 6)) want_depth = v;  // single-column shapes only (sweeps)
+  }
+  int best_stg = 0;
+  for (int h = 2; h >= 1; h--) {
+    if (want_h && h != want_h) continue;
+    const int depth = want_depth ? want_depth : h == 2 ? 2 : (p.ni <= 2 ? 3 : 2);
+    const size_t ring = (size_t)4 * depth * p.ni * 1024 * h;
+    if (ring + 2048 >= (size_t)160 * 1024) continue;
+    const size_t budget = (size_t)160 * 1024 - 2048 - ring;  // static meta (1.5 KB) + margin
+    int stg = want_stg;
+    while (stg >= 256 * h && (size_t)4 * (stg + 64) * rowb > budget) stg >>= 1;
+    if (stg < 256 * h || (stg & (stg - 1))) continue;
+    if (stg > best_stg) {
+      best_stg = stg;
+      p.H = h;
+      p.depth = depth;
+      p.lds = ring + (size_t)4 * (stg + 64) * rowb;
+    }
+  }
+  if (!best_stg) return p;
+  p.stg = best_stg;
+  // a round is a quarter of the staging ring (1..4 steps)
+  p.S = want_s ? want_s : std::max(1, std::min(4, p.stg / (1024 * p.H)));
+  if (p.S * 256 * p.H > p.stg) p.S = p.stg / (256 * p.H);
+  if (p.S < 1) return p;
+  p.G = NumCUs() < 256 ? NumCUs() : 256;
+  const int64_t nsteps = nrows / (256 * p.H);
+  const int64_t ntiles = (nsteps + 4 * p.S - 1) / (4 * p.S);
+  p.nrounds = (ntiles + p.G - 1) / p.G;
+  if (p.lds < (size_t)96 * 1024) p.lds = (size_t)96 * 1024;  // one workgroup per CU
+  p.sleep = 1;
+  if (const char *e = getenv("MBX_SR_SLEEP")) p.sleep = atoi(e) >= 0 ? atoi(e) : 1;
+  // tests: workgroup MBX_SR_TEST_STALL never publishes, as if it were never
+  // scheduled, so every coordinator times out and the launch aborts
+  p.test_stall = -1;
+  if (const char *e = getenv("MBX_SR_TEST_STALL")) p.test_stall = atoi(e);
+  p.ok = true;
+  return p;
+}
+
+size_t SelectRoundsCtlBytes(const SelectRoundsPlan &p) { return (size_t)(8 + p.nrounds * p.G) * 8; }
+
+namespace {
+template <int NC, int WM, int DP, int H>
+void SrLaunchH(const SelectDesc &d, const SelectRoundsPlan &p, int64_t nrows, unsigned long long *ctl, uint32_t epoch,
+               hipStream_t s) {
+  static bool attr = false;
+  if (!attr) {
+    (void)hipFuncSetAttribute((const void *)select_rounds_kernel<NC, WM, DP, H>,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024 - 2048);
+    attr = true;
+  }
+  hipLaunchKernelGGL((select_rounds_kernel<NC, WM, DP, H>), dim3((unsigned)p.G), dim3(576), p.lds, s, d, nrows,
+                     p.nrounds, p.S, p.stg, ctl, epoch, p.sleep, p.test_stall);
+}
+template <int NC, int WM>
+void SrDepth(const SelectDesc &d, const SelectRoundsPlan &p, int64_t nrows, unsigned long long *ctl, uint32_t epoch,
+             hipStream_t s) {
+  constexpr int ni = SrCols<NC, WM>::ni();
+  if (p.H == 1 && ni <= 2) {  // 3-deep ring at H = 1
+    if constexpr (NC == 1) {
+      if (p.depth == 2) return SrLaunchH<NC, WM, 2, 1>(d, p, nrows, ctl, epoch, s);
+      if (p.depth == 4) return SrLaunchH<NC, WM, 4, 1>(d, p, nrows, ctl, epoch, s);
+      if (p.depth == 6) return SrLaunchH<NC, WM, 6, 1>(d, p, nrows, ctl, epoch, s);
+    }
+    return SrLaunchH<NC, WM, 3, 1>(d, p, nrows, ctl, epoch, s);
+  }
+  if (p.H == 1) return SrLaunchH<NC, WM, 2, 1>(d, p, nrows, ctl, epoch, s);
+  if constexpr (NC == 1) {
+    if (p.depth == 3) return SrLaunchH<NC, WM, 3, 2>(d, p, nrows, ctl, epoch, s);
+    if (p.depth == 4) return SrLaunchH<NC, WM, 4, 2>(d, p, nrows, ctl, epoch, s);
+    if (p.depth == 6) return SrLaunchH<NC, WM, 6, 2>(d, p, nrows, ctl, epoch, s);
+  }
+  SrLaunchH<NC, WM, 2, 2>(d, p, nrows, ctl, epoch, s);
+}
+template <int NC, int WM = 0>
+void SrDispatch(const SelectDesc &d, const SelectRoundsPlan &p, int64_t nrows, unsigned long long *ctl,
+                uint32_t epoch, hipStream_t s) {
+  if constexpr (WM < (1 << NC)) {
+    if (p.wm == WM) return SrDepth<NC, WM>(d, p, nrows, ctl, epoch, s);
+    SrDispatch<NC, WM + 1>(d, p, nrows, ctl, epoch, s);
+  }
+}
+}  // namespace
+
+void SelectRounds(const SelectDesc &d, const SelectRoundsPlan &p, int64_t nrows, unsigned long long *ctl,
+                  uint32_t epoch, hipStream_t s) {
+  if (!p.ok) throw std::runtime_error("SelectRounds: unsupported shape");
+  switch (p.nc) {
+    case 1: SrDispatch<1>(d, p, nrows, ctl, epoch, s); break;
+    case 2: SrDispatch<2>(d, p, nrows, ctl, epoch, s); break;
+    case 3: SrDispatch<3>(d, p, nrows, ctl, epoch, s); break;
+    default: SrDispatch<4>(d, p, nrows, ctl, epoch, s); break;
+  }
+  (void)hipGetLastError();
+}
 
 // ---------------------------------------------------------------------------
 // Count-first compaction (see device.h): chunk-owned steps in both passes.

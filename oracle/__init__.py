@@ -3,7 +3,8 @@ cpu_baseline leg of bench.py).  Nothing under duckdb.mbt_amd/ imports this.
 
 Contents
   liboracle_mbx.so (oracle.c): multi-threaded C restatement of the hot-path
-      arithmetic (synthetic generator, filter+COUNT/SUM/MIN/MAX, GROUP BY SUM).
+      arithmetic (synthetic generator, filter+COUNT/SUM/MIN/MAX, GROUP BY SUM,
+      order-preserving selection SELECT x WHERE lo <= x <= hi).
   wire.py:   byte-exact restatement of the reference shim's "arrow" buffers
              (/root/reference/src/duckdb_native.c:2285-2797).
   mb.py:     restatement of the MoonBit-side parsing (duckdb_parsing.mbt) used
@@ -48,6 +49,8 @@ def load():
     lib.orc_synth_groupby.argtypes = [u64, u64, i64, i64, ctypes.c_int, u64, i64, ctypes.c_int, vp, vp]
     lib.orc_range_mod_select.restype = i64
     lib.orc_range_mod_select.argtypes = [i64, i64, i64, i64, vp, i64]
+    lib.orc_select_i64.restype = i64
+    lib.orc_select_i64.argtypes = [vp, i64, i64, i64, ctypes.c_int, vp]
     return lib
 
 
@@ -109,4 +112,13 @@ class Oracle:
         cap = n // k + 2
         out = np.empty(cap, dtype=np.int64)
         w = self.lib.orc_range_mod_select(n, k, c, mul, out.ctypes.data, cap)
+        return out[:w]
+
+    def select_i64(self, x, lo, hi, threads=1, out=None):
+        """The passing values of x (lo <= x <= hi) in row order (out: optional
+        preallocated int64 array with room for len(x) values)."""
+        import numpy as np
+        if out is None:
+            out = np.empty(max(len(x), 1), dtype=np.int64)
+        w = self.lib.orc_select_i64(x.ctypes.data, len(x), lo, hi, threads, out.ctypes.data)
         return out[:w]

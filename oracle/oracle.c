@@ -333,3 +333,67 @@ int64_t orc_range_mod_select(int64_t n, int64_t k, int64_t c, int64_t mul, int64
     }
   return w;
 }
+
+/* ---- SELECT x WHERE lo <= x <= hi (order-preserving compaction) --------
+ * What DuckDB's filter + result materialisation produces for the selection
+ * shape (SELECT x FROM t WHERE x > 24): the passing rows in row order.  Two
+ * phases over contiguous per-thread chunks: count, then each thread copies its
+ * passing rows to its exclusive-prefix offset (branch-free store + conditional
+ * advance).  out needs room for n values; returns the count. */
+typedef struct {
+  const int64_t *x;
+  int64_t n, lo, hi, count, off;
+  int64_t *out;
+} sel_job;
+
+static void *sel_count(void *p) {
+  sel_job *j = (sel_job *)p;
+  int64_t c = 0;
+  for (int64_t i = 0; i < j->n; i++) c += (j->x[i] >= j->lo) & (j->x[i] <= j->hi);
+  j->count = c;
+  return NULL;
+}
+
+static void *sel_copy(void *p) {
+  sel_job *j = (sel_job *)p;
+  int64_t *o = j->out + j->off;
+  int64_t w = 0, junk;
+  for (int64_t i = 0; i < j->n; i++) {
+    const int64_t v = j->x[i];
+    /* unconditional store (a cmov'd address), so the ~50 % selective
+       predicate costs no mispredicted branch; past this chunk's last output
+       the store goes to a scratch word, never into the next chunk */
+    int64_t *d = w < j->count ? o + w : &junk;
+    *d = v;
+    w += (v >= j->lo) & (v <= j->hi);
+  }
+  (void)junk;
+  return NULL;
+}
+
+int64_t orc_select_i64(const int64_t *x, int64_t n, int64_t lo, int64_t hi, int threads, int64_t *out) {
+  if (threads < 1) threads = 1;
+  if (threads > MAXT) threads = MAXT;
+  static sel_job jobs[MAXT];
+  pthread_t th[MAXT];
+  int64_t chunk = (n + threads - 1) / threads;
+  for (int t = 0; t < threads; t++) {
+    int64_t b = t * chunk, e = b + chunk < n ? b + chunk : n;
+    if (b > n) b = n;
+    jobs[t].x = x + b;
+    jobs[t].n = e - b;
+    jobs[t].lo = lo;
+    jobs[t].hi = hi;
+    jobs[t].out = out;
+    pthread_create(&th[t], NULL, sel_count, &jobs[t]);
+  }
+  int64_t off = 0;
+  for (int t = 0; t < threads; t++) {
+    pthread_join(th[t], NULL);
+    jobs[t].off = off;
+    off += jobs[t].count;
+  }
+  for (int t = 0; t < threads; t++) pthread_create(&th[t], NULL, sel_copy, &jobs[t]);
+  for (int t = 0; t < threads; t++) pthread_join(th[t], NULL);
+  return off;
+}

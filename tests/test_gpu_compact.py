@@ -1,12 +1,14 @@
 """Filter -> compaction against the CPU oracle's generator arrays: the
+round-synchronous one-pass kernel (dev::SelectRounds; the default from
+MBX_SR_MIN_ROWS rows, forced at every size with MBX_SR_MIN_ROWS=0), the
 count-first two-pass form (dev::FilterCountChunks + scan +
-dev::CompactRecompute, when every predicate column is an output), the
-ballot-bits two-pass form (dev::FilterBits + scan + dev::CompactColumns;
-MBX_CC=0), the one-pass look-back kernel (dev::SelectCompact; MBX_SL=1) and
-the VM path (MBX_FC=0) must all give the selected rows of every output
-column, in row order, bit for bit.  Sizes straddle the 256-row step,
-the one-pass tile (16 steps) and the ring's grid-stride (partial last step,
-one-row tail, many tiles per workgroup)."""
+dev::CompactRecompute, when every predicate column is an output; MBX_SL=0),
+the ballot-bits two-pass form (dev::FilterBits + scan + dev::CompactColumns;
+MBX_SL=0 MBX_CC=0), the one-pass look-back kernel (dev::SelectCompact;
+MBX_SL=2) and the VM path (MBX_FC=0) must all give the selected rows of every
+output column, in row order, bit for bit.  Sizes straddle the 256-row step,
+the one-pass tiles (4 S steps per workgroup and round) and the grid-stride
+(partial last step, one-row tail, many rounds per workgroup)."""
 import numpy as np
 import pytest
 
@@ -51,13 +53,16 @@ def test_filter_compact_parity(conn, oracle, monkeypatch, n):
         for i, (kind, arr) in enumerate(cols):
             got = _col(conn, sql, kind, i)
             assert np.array_equal(got, arr[m].astype(got.dtype)), (n, sql, i)
-        # the bits form, the one-pass form, then the VM path: the same rows
-        for env, val in (("MBX_CC", "0"), ("MBX_SL", "1"), ("MBX_FC", "0")):
-            monkeypatch.setenv(env, val)
+        # every other form: the same rows
+        for envs in ({"MBX_SR_MIN_ROWS": "0"}, {"MBX_SL": "0"}, {"MBX_SL": "0", "MBX_CC": "0"}, {"MBX_SL": "2"},
+                     {"MBX_FC": "0"}):
+            for env, val in envs.items():
+                monkeypatch.setenv(env, val)
             for i, (kind, arr) in enumerate(cols):
                 got = _col(conn, sql, kind, i)
-                assert np.array_equal(got, arr[m].astype(got.dtype)), (n, sql, i, env)
-            monkeypatch.delenv(env)
+                assert np.array_equal(got, arr[m].astype(got.dtype)), (n, sql, i, envs)
+            for env in envs:
+                monkeypatch.delenv(env)
     # nothing passes: typed empty result
     r = q(conn, "SELECT x, k FROM fc WHERE x > 100")
     assert r.rows == [] and r.column_types == ["BigInt", "Integer"]
@@ -100,10 +105,17 @@ def test_filter_compact_runs_the_hip_passes(mbx, oracle, monkeypatch):
     names = [kk["name"] for kk in c.last_profile()["kernels"]]
     assert "filter_count" in names and "compact" in names and "filter_bits" not in names, names
     assert np.array_equal(got, k[(x > 24) & (k < 16)])
-    monkeypatch.setenv("MBX_SL", "1")
+    monkeypatch.setenv("MBX_SR_MIN_ROWS", "0")  # the round-synchronous one pass (default from 2^22 rows)
+    for sql, col, m in (("SELECT v, k FROM fc WHERE x > 24 AND k < 16", v, (x > 24) & (k < 16)),
+                        ("SELECT x FROM fc WHERE x > 24", x, x > 24)):
+        got = _col(c, sql, "int64")
+        names = [kk["name"] for kk in c.last_profile()["kernels"]]
+        assert "select_rounds" in names and "filter_bits" not in names and "filter_count" not in names, names
+        assert np.array_equal(got, col[m])
+    monkeypatch.setenv("MBX_SL", "2")
     got = _col(c, "SELECT v, k FROM fc WHERE x > 24 AND k < 16", "int64")
     names = [kk["name"] for kk in c.last_profile()["kernels"]]
-    assert "select" in names and "filter_bits" not in names, names  # one pass (opt-in)
+    assert "select" in names and "filter_bits" not in names, names  # one pass, look-back (opt-in)
     assert np.array_equal(got, v[(x > 24) & (k < 16)])
     c.close()
 
@@ -113,7 +125,7 @@ def test_select_one_pass_launch_shapes(mbx, oracle, monkeypatch, nbuf, gpc):
     """Every ring depth / workgroups-per-CU shape of the one-pass kernel over
     many tiles per workgroup (ticket reuse, look-back windows longer than 64
     tiles) and the 1..4-column loaded sets (NI 1..8): exact rows in order."""
-    monkeypatch.setenv("MBX_SL", "1")
+    monkeypatch.setenv("MBX_SL", "2")
     monkeypatch.setenv("MBX_SL_NBUF", str(nbuf))
     monkeypatch.setenv("MBX_SL_BLOCKS_PER_CU", str(gpc))
     cfg = mbx.Config.create()
@@ -135,6 +147,75 @@ def test_select_one_pass_launch_shapes(mbx, oracle, monkeypatch, nbuf, gpc):
             got = _col(c, sql, kind, i)
             assert "select" in [kk["name"] for kk in c.last_profile()["kernels"]], sql
             assert np.array_equal(got, arr[m].astype(got.dtype)), (sql, i)
+    c.close()
+
+
+_SHAPE_CASES = [
+    ("SELECT k FROM fc WHERE k < 5", lambda x, k, v: k < 5, ["k"]),
+    ("SELECT x FROM fc WHERE x > 24", lambda x, k, v: x > 24, ["x"]),
+    ("SELECT x, k FROM fc WHERE x > 24 AND k <= 16", lambda x, k, v: (x > 24) & (k <= 16), ["x", "k"]),
+    ("SELECT v, x, k FROM fc WHERE v > 0 AND x < 30", lambda x, k, v: (v > 0) & (x < 30), ["v", "x", "k"]),
+    ("SELECT k, v FROM fc WHERE x BETWEEN 10 AND 40 AND k >= 3 AND v > 0",
+     lambda x, k, v: (x >= 10) & (x <= 40) & (k >= 3) & (v > 0), ["k", "v"]),
+    ("SELECT x FROM fc WHERE x >= 1", lambda x, k, v: np.ones(len(x), bool), ["x"]),
+]
+
+
+@pytest.mark.parametrize("s_,depth,stg,sleep,h", [(2, 0, 0, 1, 2), (1, 2, 512, 0, 2), (1, 2, 256, 0, 1),
+                                                  (2, 3, 1024, 4, 2), (8, 6, 2048, 1, 1), (4, 4, 4096, 2, 2),
+                                                  (3, 3, 4096, 1, 1)])
+def test_select_rounds_launch_shapes(mbx, oracle, monkeypatch, s_, depth, stg, sleep, h):
+    """Every tile size (S steps per loader and round), sub-steps per step (H),
+    ring depth, staging ring (one step: the loader waits on its storer every
+    step when every row passes) and poll back-off of the round-synchronous
+    kernel, over many rounds per workgroup (meta-slot reuse) and the 1..4-column
+    loaded sets: exact rows in order."""
+    monkeypatch.setenv("MBX_SR_MIN_ROWS", "0")
+    monkeypatch.setenv("MBX_SR_H", str(h))
+    monkeypatch.setenv("MBX_SR_S", str(s_))
+    if depth:
+        monkeypatch.setenv("MBX_SR_DEPTH", str(depth))
+    if stg:
+        monkeypatch.setenv("MBX_SR_STG", str(stg))
+    monkeypatch.setenv("MBX_SR_SLEEP", str(sleep))
+    cfg = mbx.Config.create()
+    cfg.set("mbx_profile", "true")
+    c = mbx.connect_with_config(cfg).value
+    n = 20_000_077
+    x, k, v, s = _table(c, oracle, n)
+    arrs = {"x": ("int64", x), "k": ("int32", k), "v": ("int64", v)}
+    for sql, mf, names in _SHAPE_CASES:
+        m = mf(x, k, v)
+        for i, nm in enumerate(names):
+            kind, arr = arrs[nm]
+            got = _col(c, sql, kind, i)
+            if stg >= 512 or len(names) == 1:  # multi-column steps need 512 staging rows (H = 2)
+                assert "select_rounds" in [kk["name"] for kk in c.last_profile()["kernels"]], sql
+            assert np.array_equal(got, arr[m].astype(got.dtype)), (sql, i)
+    c.close()
+
+
+def test_select_rounds_abort_falls_back(mbx, oracle, monkeypatch):
+    """A workgroup that never publishes (MBX_SR_TEST_STALL: as if it were never
+    scheduled) makes every coordinator give up after 100 ms; the launch is
+    reported aborted and the query answers through the two-pass form, exact."""
+    monkeypatch.setenv("MBX_SR_MIN_ROWS", "0")
+    cfg = mbx.Config.create()
+    cfg.set("mbx_profile", "true")
+    c = mbx.connect_with_config(cfg).value
+    n = 5_000_011
+    x, k, v, s = _table(c, oracle, n)
+    for stall in ("0", "17"):
+        monkeypatch.setenv("MBX_SR_TEST_STALL", stall)
+        got = _col(c, "SELECT x FROM fc WHERE x > 24", "int64")
+        names = [kk["name"] for kk in c.last_profile()["kernels"]]
+        assert "select_rounds_abort" in names and "filter_count" in names, names
+        assert np.array_equal(got, x[x > 24])
+    monkeypatch.delenv("MBX_SR_TEST_STALL")
+    got = _col(c, "SELECT x FROM fc WHERE x > 24", "int64")  # the next launch (fresh epoch) is clean
+    names = [kk["name"] for kk in c.last_profile()["kernels"]]
+    assert "select_rounds" in names and "select_rounds_abort" not in names, names
+    assert np.array_equal(got, x[x > 24])
     c.close()
 
 

@@ -152,3 +152,28 @@ def test_sharded_empty_and_tiny_tables(mbx):
     assert q(c, "SELECT x FROM t1").rows == [["0"], ["1"]]
     assert one(c, "SELECT SUM(x), AVG(x) FROM t1") == ["1", "0.5"]
     c.close()
+
+
+@pytest.mark.parametrize("devices", ["0,0", "0,0,0"])
+def test_sharded_select_rounds(mbx, oracle, monkeypatch, devices):
+    """Row results of the one-pass compaction on every shard at once: shards
+    that share a device take turns through the per-device lock (two persistent
+    grids never compete for the CUs), rows come back in part order, exact."""
+    monkeypatch.setenv("MBX_SR_MIN_ROWS", "0")
+    n = 12_000_007
+    c = _conn(mbx, devices, profile=True)
+    q(c, f"CREATE TABLE t AS SELECT mbx_synth(42, i, 50) + 1 AS x, CAST(mbx_synth(7, i, 32) AS INTEGER) AS k "
+         f"FROM range({n}) tbl(i)")
+    x = oracle.synth_i64(n, 42, 0, 50, 1)
+    k = oracle.synth_i64(n, 7, 0, 32, 0)
+    for _ in range(3):
+        a = c.query_arrow("SELECT x, k FROM t WHERE x > 24 AND k < 16").value
+        b = a._buf("int64", 0)
+        a.close()
+        cnt = int.from_bytes(b[:4], "little", signed=True)
+        got = np.frombuffer(b[4:4 + 8 * cnt], dtype=np.int64)
+        m = (x > 24) & (k < 16)
+        assert np.array_equal(got, x[m])
+        kinds = [kk["name"] for kk in c.last_profile()["kernels"]]
+        assert kinds.count("select_rounds") == devices.count(",") + 1, kinds
+    c.close()

@@ -101,3 +101,16 @@ def test_synth_groupby_matches_materialised(oracle):
         k = oracle.synth_i32(n, 7, start, 32, 0)
         v = oracle.synth_i64(n, 9, start, 2**40, -2**39)
         assert oracle.synth_groupby(7, 9, start, n, 32, 2**40, -2**39, 3) == oracle.groupby_sum(k, v, 0, 32, 2)
+
+
+def test_select_i64_matches_numpy(oracle):
+    # the order-preserving selection oracle (bench --config sel parity and CPU
+    # baseline): equal to numpy's boolean mask over ragged sizes and thread
+    # counts, including empty, all-pass and single-row chunks
+    import numpy as np
+    for n in (0, 1, 7, 1_000, 100_003):
+        x = oracle.synth_i64(n, 42, 3, 50, 1)
+        for threads in (1, 3, 8, 64):
+            for lo, hi in ((25, 2**63 - 1), (100, 200), (-5, 200), (10, 10)):
+                got = oracle.select_i64(x, lo, hi, threads)
+                assert np.array_equal(got, x[(x >= lo) & (x <= hi)]), (n, threads, lo, hi)
