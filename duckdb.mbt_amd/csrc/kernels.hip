@@ -1228,6 +1228,27 @@ __global__ __launch_bounds__(256) void group_direct_kernel(const TK *__restrict_
 // Every PKF wave steps the block drains the packed table into per-thread
 // register partials (slot t + 256 j), before a count can reach 2^PKB or the
 // shifted sum can leave int64; the host derives PKB/PKF from the zone maps.
+// LDS atomics of the table as inline-asm ds_* ops that return nothing: the
+// compiler puts an s_waitcnt vmcnt(0) in front of every atomic LDS access
+// while LDS-DMA is in flight (it cannot prove the table and the ring do not
+// alias), which drained the whole ring at every step.  The table is read only
+// behind an explicit lgkmcnt(0) + barrier.
+__device__ __forceinline__ uint32_t gd_lds(const void *p) {
+  return (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) void *)p;
+}
+__device__ __forceinline__ void gd_add_u32(unsigned int *p, unsigned int v) {
+  asm volatile("ds_add_u32 %0, %1" ::"v"(gd_lds(p)), "v"(v) : "memory");
+}
+__device__ __forceinline__ void gd_add_u64(long long *p, unsigned long long v) {
+  asm volatile("ds_add_u64 %0, %1" ::"v"(gd_lds(p)), "v"(v) : "memory");
+}
+__device__ __forceinline__ void gd_min_i64(long long *p, long long v) {
+  asm volatile("ds_min_i64 %0, %1" ::"v"(gd_lds(p)), "v"(v) : "memory");
+}
+__device__ __forceinline__ void gd_max_i64(long long *p, long long v) {
+  asm volatile("ds_max_i64 %0, %1" ::"v"(gd_lds(p)), "v"(v) : "memory");
+}
+
 template <typename TK, typename TV, int NV, bool MM, int DEPTH, bool PK>
 __global__ __launch_bounds__(256) void group_direct_lds_kernel(const TK *__restrict__ keys, const TV *__restrict__ v0,
                                                                const TV *__restrict__ v1, int64_t n, int64_t kmin,
@@ -1273,15 +1294,15 @@ __global__ __launch_bounds__(256) void group_direct_lds_kernel(const TK *__restr
   auto row = [&](int64_t k, int64_t a, int64_t b) {
     int sl = (int)(k - kmin) * R + rep;
     if (PK) {
-      atomicAdd((unsigned long long *)&sum0[sl], ((unsigned long long)a << PKB) + 1ull);
+      gd_add_u64(&sum0[sl], ((unsigned long long)a << PKB) + 1ull);
     } else {
-      atomicAdd(&cnt[sl], 1u);
-      if (NV >= 1) atomicAdd((unsigned long long *)&sum0[sl], (unsigned long long)a);
+      gd_add_u32(&cnt[sl], 1u);
+      if (NV >= 1) gd_add_u64(&sum0[sl], (unsigned long long)a);
     }
-    if (NV >= 2) atomicAdd((unsigned long long *)&sum1[sl], (unsigned long long)b);
+    if (NV >= 2) gd_add_u64(&sum1[sl], (unsigned long long)b);
     if (MM) {
-      atomicMin(&mn0[sl], (long long)a); atomicMax(&mx0[sl], (long long)a);
-      if (NV >= 2) { atomicMin(&mn1[sl], (long long)b); atomicMax(&mx1[sl], (long long)b); }
+      gd_min_i64(&mn0[sl], (long long)a); gd_max_i64(&mx0[sl], (long long)a);
+      if (NV >= 2) { gd_min_i64(&mn1[sl], (long long)b); gd_max_i64(&mx1[sl], (long long)b); }
     }
   };
   // PK: register partials of slots t + 256 j (nslot <= 256 * PK_J, checked by the host)
@@ -1422,6 +1443,7 @@ __global__ __launch_bounds__(256) void group_direct_lds_kernel(const TK *__restr
       if (okr) row(kv, av, NV >= 2 ? (int64_t)v1[i] : 0);
     }
   }
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // this thread's table atomics (asm) have landed
   if (PK) {
     pk_drain();
 #pragma unroll
@@ -1513,13 +1535,13 @@ bool GroupByDirectStates(const void *kcol, int kphys, int64_t kmin, int nk, cons
   // LDS-DMA variant: one flush at the end, so a block's whole row share must
   // fit the overflow bound the host derived (seg_rows) — else the segmented
   // kernel below.  MBX_GD_VARIANT="d<depth>_g<blocks per CU>" / "seg".
-  // Defaults from profiles/r01_group_sweep.json: d2_g3 for C3 (6.72 TB/s vs
-  // 5.87 segmented; one block per CU streams faster but cannot keep up with
-  // the table atomics: profiles/r01_c3_probe.log); COUNT-only tables (nv == 0) carry 3x the LDS atomics per
-  // byte and stay on the segmented kernel at 4 blocks/CU (6.40 TB/s).
+  // Defaults from profiles/r02_group_sweep.log (after the table atomics stopped
+  // draining the DMA ring): d2_g1 for value aggregates (C3 1.735-1.77 ms, 2-6 %
+  // under d2_g3 on two boxes) and d2_g3 for COUNT-only tables (0.56 ms vs 0.62
+  // on the segmented kernel).
   {
-    int depth = 2, gpc = 3;
-    bool use = nv > 0 || pr.n != 0;  // the segmented kernel has no predicate
+    int depth = 2, gpc = nv > 0 ? 1 : 3;
+    bool use = true;
     const char *e = getenv("MBX_GD_VARIANT");
     if (e && *e) use = sscanf(e, "d%d_g%d", &depth, &gpc) == 2 || pr.n != 0;
     // MBX_GD_R=<r>: fewer replicas (experiment; seg_rows scales with R)
@@ -1540,8 +1562,8 @@ bool GroupByDirectStates(const void *kcol, int kphys, int64_t kmin, int nk, cons
       size_t slot = 256 * (size_t)(kphys == P_I64 ? 8 : 4) + (size_t)nv * 256 * (vphys == P_I64 ? 8 : 4);
       for (int j = 0; j < pr.n; j++)
         if (pr.p[j].src == 1) slot += 256 * (size_t)(pr.p[j].phys == P_I64 ? 8 : 4);
-      depth = depth <= 2 ? 2 : depth <= 3 ? 3 : 4;
-      const size_t lds_cap = 64 * 1024;
+      depth = depth <= 2 ? 2 : depth <= 3 ? 3 : depth <= 4 ? 4 : depth <= 6 ? 6 : 8;
+      const size_t lds_cap = gpc <= 1 ? 150 * 1024 : gpc == 2 ? 76 * 1024 : 64 * 1024;
       size_t lds = ring_off + 4 * (size_t)depth * slot;
       // wide slots (predicate slices): trade table replicas for ring space;
       // seg_rows scales with R (rows per replica stay the same)
@@ -1561,6 +1583,12 @@ bool GroupByDirectStates(const void *kcol, int kphys, int64_t kmin, int nk, cons
       if (const char *ef = getenv("MBX_GD_PKF")) pkf = std::max(1, std::min(pkf, atoi(ef)));
       if ((seg_rows <= 0 || seg_rows >= rows_per_block) && lds <= lds_cap) {
 #define GL(TK, TV, NV, MM, D)                                                                                      \
+  if (lds > 64 * 1024) { /* deep rings at one or two blocks per CU */                                             \
+    (void)hipFuncSetAttribute((const void *)group_direct_lds_kernel<TK, TV, NV, MM, D, NV >= 1>,                   \
+                              hipFuncAttributeMaxDynamicSharedMemorySize, 150 * 1024);                             \
+    (void)hipFuncSetAttribute((const void *)group_direct_lds_kernel<TK, TV, NV, MM, D, false>,                     \
+                              hipFuncAttributeMaxDynamicSharedMemorySize, 150 * 1024);                             \
+  }                                                                                                                \
   if (pk && NV >= 1)                                                                                               \
     hipLaunchKernelGGL((group_direct_lds_kernel<TK, TV, NV, MM, D, NV >= 1>), dim3(grid), dim3(256), lds, s,       \
                        (const TK *)kcol, (const TV *)v0, (const TV *)v1, nrows, kmin, nk, R, ring_off, cstar, st0, \
@@ -1569,8 +1597,10 @@ bool GroupByDirectStates(const void *kcol, int kphys, int64_t kmin, int nk, cons
     hipLaunchKernelGGL((group_direct_lds_kernel<TK, TV, NV, MM, D, false>), dim3(grid), dim3(256), lds, s,         \
                        (const TK *)kcol, (const TV *)v0, (const TV *)v1, nrows, kmin, nk, R, ring_off, cstar, st0, \
                        st1, pr, 0, 1);
-#define GLD(TK, TV, NV, MM) \
-  if (depth == 2) { GL(TK, TV, NV, MM, 2) } else if (depth == 3) { GL(TK, TV, NV, MM, 3) } else { GL(TK, TV, NV, MM, 4) }
+#define GLD(TK, TV, NV, MM)                                                                     \
+  if (depth == 2) { GL(TK, TV, NV, MM, 2) } else if (depth == 3) { GL(TK, TV, NV, MM, 3) }      \
+  else if (depth == 4) { GL(TK, TV, NV, MM, 4) } else if (depth == 6) { GL(TK, TV, NV, MM, 6) } \
+  else { GL(TK, TV, NV, MM, 8) }
 #define GLV(TK, TV)                                                                      \
   if (nv == 0) { GLD(TK, TV, 0, false) }                                                 \
   else if (nv == 1) { if (mm) { GLD(TK, TV, 1, true) } else { GLD(TK, TV, 1, false) } } \

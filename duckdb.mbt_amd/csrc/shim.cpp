@@ -10,7 +10,8 @@
 //    duckdb_native.c:22-40) — identical for the single-threaded MoonBit caller;
 //  * duckdb_mb_query_arrow does not read freed memory on error
 //    (reference use-after-free at duckdb_native.c:2258-2260);
-//  * arrow buffer sizes are computed in 64 bits and refused above INT32_MAX
+//  * arrow buffer sizes are computed in 64 bits and refused at 2^28 bytes (the
+//    MoonBit byte-object length field; see MbTooBig)
 //    (reference int32 overflow at duckdb_native.c:2404).
 #include <hip/hip_runtime_api.h>
 
@@ -60,6 +61,18 @@ extern "C" moonbit_bytes_t duckdb_mbx_bytes_new(const uint8_t *data, int32_t len
 extern "C" int32_t duckdb_mbx_bytes_len(moonbit_bytes_t b) { return MbLen(b); }
 extern "C" void duckdb_mbx_bytes_free(moonbit_bytes_t b) {
   if (b) free((MbHeader *)b - 1);
+}
+
+// A MoonBit byte object's length is the low 28 bits of its header word, so a
+// getter buffer must stay below 2^28 bytes (a longer one would read back with a
+// truncated length): refused with an error instead.
+constexpr int64_t kMbMaxBytes = (1 << 28) - 1;
+static void SetError(const std::string &msg);
+static bool MbTooBig(int64_t total) {
+  if (total <= kMbMaxBytes) return false;
+  SetError("Invalid Input Error: arrow buffer of " + std::to_string(total) +
+           " bytes exceeds the 2^28-byte limit of one MoonBit Bytes object");
+  return true;
 }
 
 static moonbit_bytes_t MakeBytes(const char *data, size_t len) {
@@ -1219,7 +1232,7 @@ static moonbit_bytes_t ArrowDirectBuffer(duckdb_mb_arrow_result *a, int32_t col,
     return nullptr;
   const int64_t n = a->row_count;
   const int64_t total = 4 + n * width + (nullable ? n : 0);
-  if (total > INT32_MAX) return nullptr;
+  if (MbTooBig(total)) return nullptr;
   moonbit_bytes_t out = moonbit_make_bytes_raw((int32_t)total);
   memcpy(out, &a->row_count, 4);
   uint8_t *vb = nullable ? out + 4 + n * width : nullptr;
@@ -1275,10 +1288,7 @@ static moonbit_bytes_t ArrowFixed(duckdb_mb_arrow_result *a, int32_t col, int wi
   if (!ArrowOk(a, col)) return MakeBytes("", 0);
   int64_t n = a->row_count;
   int64_t total = 4 + n * width + (nullable ? n : 0);
-  if (total > INT32_MAX) {
-    SetError("arrow column too large for one Bytes object");
-    return MakeBytes("", 0);
-  }
+  if (MbTooBig(total)) return MakeBytes("", 0);
   moonbit_bytes_t out = moonbit_make_bytes_raw((int32_t)total);
   int32_t cnt = (int32_t)n;
   memcpy(out, &cnt, 4);
@@ -1311,7 +1321,7 @@ static moonbit_bytes_t ArrowF64(duckdb_mb_arrow_result *a, int32_t col, bool nul
   if (!ArrowOk(a, col)) return MakeBytes("", 0);
   int64_t n = a->row_count;
   int64_t total = 4 + n * 8 + (nullable ? n : 0);
-  if (total > INT32_MAX) return MakeBytes("", 0);
+  if (MbTooBig(total)) return MakeBytes("", 0);
   moonbit_bytes_t out = moonbit_make_bytes_raw((int32_t)total);
   int32_t cnt = (int32_t)n;
   memcpy(out, &cnt, 4);
@@ -1336,7 +1346,7 @@ static moonbit_bytes_t ArrowStr(duckdb_mb_arrow_result *a, int32_t col, bool nul
     try {
       const bool ok = CopyDeviceColumnText(a->conn->conn, *a->dev, col, [&](int64_t chars) -> uint8_t * {
         total = 8 + chars + (nullable ? n : 0);
-        if (total > INT32_MAX) return nullptr;
+        if (MbTooBig(total)) return nullptr;
         out = moonbit_make_bytes_raw((int32_t)total);
         const int32_t h[2] = {(int32_t)n, (int32_t)chars};
         memcpy(out, h, 8);
@@ -1364,7 +1374,7 @@ static moonbit_bytes_t ArrowStr(duckdb_mb_arrow_result *a, int32_t col, bool nul
     data.push_back('\0');
   }
   int64_t total = 8 + (int64_t)data.size() + (nullable ? n : 0);
-  if (total > INT32_MAX) return MakeBytes("", 0);
+  if (MbTooBig(total)) return MakeBytes("", 0);
   moonbit_bytes_t out = moonbit_make_bytes_raw((int32_t)total);
   int32_t h[2] = {(int32_t)n, (int32_t)data.size()};
   memcpy(out, h, 8);
@@ -1381,7 +1391,7 @@ moonbit_bytes_t duckdb_mb_arrow_get_column_int32(duckdb_mb_arrow_result *a, int3
 moonbit_bytes_t duckdb_mb_arrow_get_column_int64(duckdb_mb_arrow_result *a, int32_t col) {  // ref :2392
   if (!ArrowOk(a, col)) return MakeBytes("", 0);
   int64_t n = a->row_count;
-  if (4 + n * 8 > INT32_MAX) return MakeBytes("", 0);
+  if (MbTooBig(4 + n * 8)) return MakeBytes("", 0);
   if (moonbit_bytes_t d = ArrowDirectBuffer(a, col, T_BIGINT, P_I64, 8)) return d;
   moonbit_bytes_t out = moonbit_make_bytes_raw((int32_t)(4 + n * 8));
   int32_t cnt = (int32_t)n;
@@ -1411,7 +1421,7 @@ moonbit_bytes_t duckdb_mb_arrow_get_column_int32_nullable(duckdb_mb_arrow_result
 moonbit_bytes_t duckdb_mb_arrow_get_column_int64_nullable(duckdb_mb_arrow_result *a, int32_t col) {  // ref :2611
   if (!ArrowOk(a, col)) return MakeBytes("", 0);
   int64_t n = a->row_count;
-  if (4 + n * 9 > INT32_MAX) return MakeBytes("", 0);
+  if (MbTooBig(4 + n * 9)) return MakeBytes("", 0);
   if (moonbit_bytes_t d = ArrowDirectBuffer(a, col, T_BIGINT, P_I64, 8, true)) return d;
   moonbit_bytes_t out = moonbit_make_bytes_raw((int32_t)(4 + n * 9));
   int32_t cnt = (int32_t)n;

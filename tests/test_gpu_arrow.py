@@ -198,3 +198,27 @@ def test_arrow_string_getter_formats_on_device(mbx, oracle, n):
     names = [x["name"] for x in c.profile_drain()]
     assert "text_write" in names and "text_lengths" in names
     c.close()
+
+
+def test_arrow_buffer_limit_is_the_moonbit_bytes_limit(mbx):
+    """A MoonBit byte object holds < 2^28 bytes (its length is 28 bits of the
+    header): the largest int64 column that fits (2^25 - 1 rows: 268 435 452
+    bytes with the count) comes back whole and exact; one more row is refused
+    with an error and an empty buffer instead of a truncated length."""
+    import numpy as np
+    c = mbx.connect().value
+    n_ok = (1 << 25) - 1
+    c.query(f"CREATE TABLE big AS SELECT i * 3 AS x FROM range({n_ok + 1}) tbl(i)")
+    a = c.query_arrow(f"SELECT x FROM big LIMIT {n_ok}").value
+    raw = a.raw_int64_bytes(0)
+    a.close()
+    assert len(raw) == 4 + 8 * n_ok
+    got = np.frombuffer(raw, dtype=np.int64, offset=4)
+    assert int.from_bytes(raw[:4], "little") == n_ok and got[0] == 0 and got[-1] == 3 * (n_ok - 1)
+    assert np.array_equal(got[::1_000_003], np.arange(0, n_ok, 1_000_003, dtype=np.int64) * 3)
+    a = c.query_arrow("SELECT x FROM big").value
+    raw = a.raw_int64_bytes(0)
+    a.close()
+    assert raw == b""
+    assert "2^28" in mbx._last_error("")
+    c.close()

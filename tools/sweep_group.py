@@ -2,7 +2,8 @@
 """A/B sweep of the fused GROUP BY (group_direct) launch variants on the C3
 table in ONE process: interleaved rounds, median/min kernel time.  GPU only.
 Variants: MBX_GD_VARIANT = "d<depth>_g<blocks per CU>" (LDS-DMA) or "seg",
-with options "+r<replicas>" and "+p0" (separate COUNT atomics instead of packed)."""
+with options "+r<replicas>", "+p0" (separate COUNT atomics instead of packed)
+and "+h2" (two 256-row sub-steps per wave step)."""
 import json
 import os
 import statistics
@@ -33,7 +34,10 @@ for name, sql in sqls.items():
             os.environ["MBX_GD_VARIANT"] = v.split("+")[0]
             os.environ.pop("MBX_GD_R", None)
             os.environ.pop("MBX_GD_PACK", None)
+            os.environ.pop("MBX_GD_H", None)
             for opt in v.split("+")[1:]:
+                if opt.startswith("h"):
+                    os.environ["MBX_GD_H"] = opt[1:]  # h2: two 256-row sub-steps per wave step
                 if opt.startswith("r"):
                     os.environ["MBX_GD_R"] = opt[1:]
                 elif opt.startswith("p"):
