@@ -342,6 +342,7 @@ struct SelectDesc {
     const void *data;
     int32_t w;        // 4 or 8
     int32_t is_pred;  // lo <= x <= lo + span (x sign-extended for 4 B)
+    int32_t narrow;   // select_rounds: an 8-byte column whose values fit int32 (zone map) is staged as int32
     int64_t lo;
     uint64_t span;
   } col[SL_MAX_COL];
@@ -365,7 +366,7 @@ void SelectCompact(const SelectDesc &d, int64_t nrows, void *status_buf, int64_t
 // ctl[1] is the selected-row count.
 struct SelectRoundsPlan {
   bool ok;
-  int nc, wm, ni, depth, S, H, stg, G, sleep, test_stall;  // wm: bit c = column c is 8 bytes; H: 256-row sub-steps per step
+  int nc, wm, ni, depth, S, H, NL, stg, G, sleep, test_stall;  // wm: bit c = column c is 8 bytes; H: 256-row sub-steps per step
   int64_t nrounds;
   size_t lds;
 };

@@ -1064,6 +1064,8 @@ static bool TrySelectOnePass(Engine &e, const DRel &rel, const dev::FilterMultiD
     S.col[i].span = F.col[j].span;
   }
   double out_bytes = 0;
+  const char *nenv = getenv("MBX_SR_NARROW");
+  const bool narrow_ok = !(nenv && atoi(nenv) == 0);
   for (auto &x : exprs) {
     const DCol &c = rel.cols[x->col];
     if (c.validity) return false;
@@ -1073,6 +1075,11 @@ static bool TrySelectOnePass(Engine &e, const DRel &rel, const dev::FilterMultiD
     if (i < 0) return false;
     S.out_col[S.nout++] = i;
     out_bytes += (double)rel.n * w;
+    // an INT64 table column whose zone map fits int32 is staged in 4 bytes
+    const DevColumn *tc = c.table_col;
+    if (narrow_ok && w == 8 && tc && tc->stats_valid && tc->null_count == 0 && tc->imin >= (i128)INT32_MIN &&
+        tc->imax <= (i128)INT32_MAX)
+      S.col[i].narrow = 1;
   }
   int ni = 0;
   for (int i = 0; i < S.ncol; i++) ni += S.col[i].w / 4;

@@ -395,10 +395,10 @@ constexpr int SR_PW = 2;                     // rounds polled per coordinator po
 constexpr long long SR_TIMEOUT = 10000000;   // s_memrealtime ticks (100 MHz): 100 ms without progress
 struct SrShared {
   unsigned long long arr[SR_MR];  // (count << 16) + arrivals of the round's loaders
-  uint32_t cnt[SR_MR][4];         // each loader's count of the round
+  uint32_t cnt[SR_MR][8];         // each loader's count of the round
   long long base[SR_MR];          // output row of the workgroup's tile of the round
   uint32_t btag[SR_MR];           // round + 1 once base is set
-  uint32_t tail[4];               // staging rows freed, per loader (monotonic)
+  uint32_t tail[8];               // staging rows freed, per loader (monotonic)
   uint32_t sdone[4];              // rounds finished, per storer
   uint32_t abort_;
   unsigned long long pubt[SR_MR];  // MBX_SR_DEBUG: clock64 when the round's granule was published
@@ -453,8 +453,10 @@ struct SrCols {
 // A step is H x 256 consecutive rows (sub-step h = rows 256 h .. 256 h + 255
 // of it); a loader handles its H sub-steps in one pass, so their dependency
 // chains interleave (one loader wave per SIMD cannot hide its own latencies).
-template <int NC, int WM, int DEPTH, int H>
-__global__ __launch_bounds__(576) void select_rounds_kernel(SelectDesc D, int64_t n, int64_t nrounds, int S, int stg,
+// NL loader waves (4 or 8: two per SIMD hide each other's latencies), 4
+// storers (storer s drains loaders s, s + 4, ...) and one coordinator.
+template <int NC, int WM, int DEPTH, int H, int NL>
+__global__ __launch_bounds__((NL + 5) * 64) void select_rounds_kernel(SelectDesc D, int64_t n, int64_t nrounds, int S, int stg,
                                                             unsigned long long *ctl, uint32_t epoch, int sleep_,
                                                             int test_stall) {
   typedef SrCols<NC, WM> L;
@@ -472,26 +474,30 @@ __global__ __launch_bounds__(576) void select_rounds_kernel(SelectDesc D, int64_
     for (int i = threadIdx.x; i < (int)(sizeof(SrShared) / 4); i += blockDim.x) z[i] = 0;
   }
   __syncthreads();  // the only barrier: the roles diverge below
-  // staged columns: the byte offset of column c's array in a loader's staging area
+  // staged columns: the byte offset of column c's array in a loader's staging
+  // area, and its staged width (4 for an 8-byte column the zone map proves
+  // fits int32: half the LDS per staged row; the storer sign-extends)
   int soff[NC];
+  bool st8[NC];
   uint32_t smask = 0;
   int rowb = 0;
   for (int o = 0; o < D.nout; o++) smask |= 1u << D.out_col[o];
 #pragma unroll
   for (int c = 0; c < NC; c++) {
     soff[c] = rowb * (stg + 64);
-    if ((smask >> c) & 1) rowb += L::w(c);
+    st8[c] = L::w(c) == 8 && !D.col[c].narrow;
+    if ((smask >> c) & 1) rowb += st8[c] ? 8 : 4;
   }
-  unsigned char *stage0 = sr_lds + (size_t)4 * DEPTH * SB;
+  unsigned char *stage0 = sr_lds + (size_t)NL * DEPTH * SB;
   const uint32_t mask = (uint32_t)stg - 1;
   const uint64_t lt = (1ull << lane) - 1;
 
-  if (w < 4) {
+  if (w < NL) {
     // ------------------------------------------------------------ loader
     if (nrounds == 0) return;
     unsigned char *ring = sr_lds + (size_t)w * DEPTH * SB;
     unsigned char *mystage = stage0 + (size_t)w * (stg + 64) * rowb;
-    const int64_t qstride = (int64_t)G * 4 * S;  // steps between a wave's tiles of consecutive rounds
+    const int64_t qstride = (int64_t)G * NL * S;  // steps between a wave's tiles of consecutive rounds
     const unsigned char *colp[NC];
     int64_t lo[NC];
     uint64_t span[NC];
@@ -503,7 +509,7 @@ __global__ __launch_bounds__(576) void select_rounds_kernel(SelectDesc D, int64_
       span[c] = D.col[c].span;
       pmask |= (D.col[c].is_pred ? 1u : 0u) << c;
     }
-    int64_t iq = ((int64_t)g * 4 + w) * S, ir = 0;  // the next step to issue: round ir, step iq
+    int64_t iq = ((int64_t)g * NL + w) * S, ir = 0;  // the next step to issue: round ir, step iq
     int is = 0;
     auto issue = [&](int slot) {  // dead steps re-load step 0: a fixed count per slot
       const int64_t q = ir < nrounds && iq + is < nsteps ? iq + is : 0;
@@ -532,7 +538,7 @@ __global__ __launch_bounds__(576) void select_rounds_kernel(SelectDesc D, int64_
     // MBX_SR_DEBUG (D.dbg): cycles in total, waiting on the DMA, on staging room, on meta slots
     const bool dbg = D.dbg != nullptr;
     unsigned long long t_all = dbg ? clock64() : 0, d_dma = 0, d_stg = 0, d_meta = 0, t0 = 0;
-    int64_t qb = ((int64_t)g * 4 + w) * S;  // this round's first step
+    int64_t qb = ((int64_t)g * NL + w) * S;  // this round's first step
     for (int64_t r = 0; r < nrounds && !quit; r++, qb += qstride) {
       const int slot = (int)(r % SR_MR);
       if (r >= SR_MR) {  // meta slot reuse: every storer is done with round r - SR_MR
@@ -621,10 +627,12 @@ __global__ __launch_bounds__(576) void select_rounds_kernel(SelectDesc D, int64_
             for (int c = 0; c < NC; c++) {
               if (!((smask >> c) & 1)) continue;
               unsigned char *st = mystage + soff[c];
+              if (st8[c]) {
 #pragma unroll
-              for (int e = 0; e < 4; e++) {
-                if (L::w(c) == 8) ((int64_t *)st)[idx[e]] = v[h][c][e];
-                else ((int32_t *)st)[idx[e]] = (int32_t)v[h][c][e];
+                for (int e = 0; e < 4; e++) ((int64_t *)st)[idx[e]] = v[h][c][e];
+              } else {
+#pragma unroll
+                for (int e = 0; e < 4; e++) ((int32_t *)st)[idx[e]] = (int32_t)v[h][c][e];
               }
             }
             hb += hc[h];
@@ -641,7 +649,7 @@ __global__ __launch_bounds__(576) void select_rounds_kernel(SelectDesc D, int64_
         lds_st(&sm.cnt[slot][w], rc);
         const unsigned long long old =
             (unsigned long long)sl_uni((int64_t)lds_add_rtn(&sm.arr[slot], ((unsigned long long)rc << 16) + 1));
-        if ((old & 0xffff) == 3 && g != test_stall) {  // the last loader of the round publishes the workgroup's count
+        if ((old & 0xffff) == NL - 1 && g != test_stall) {  // the last loader of the round publishes the workgroup's count
           lds_st(&sm.arr[slot], 0ull);
           const unsigned long long tot = (old >> 16) + rc;
           __hip_atomic_store(&gran[r * G + g], ((unsigned long long)epoch << 32) | tot, __ATOMIC_RELAXED,
@@ -662,49 +670,59 @@ __global__ __launch_bounds__(576) void select_rounds_kernel(SelectDesc D, int64_
     }
     return;
   }
-  if (w < 8) {
+  if (w < NL + 4) {
     // ------------------------------------------------------------ storer
-    const int sw = w - 4;
-    const unsigned char *mystage = stage0 + (size_t)sw * (stg + 64) * rowb;
-    uint32_t tail = 0;
+    const int sw = w - NL;
+    constexpr int PER = NL / 4;  // loaders per storer: sw, sw + 4, ...
+    uint32_t tail[PER];
+#pragma unroll
+    for (int j = 0; j < PER; j++) tail[j] = 0;
     const bool dbg = D.dbg != nullptr;
     unsigned long long t_all = dbg ? clock64() : 0, d_wait = 0, t0 = 0;
     for (int64_t r = 0; r < nrounds; r++) {
       const int slot = (int)(r % SR_MR);
       bool quit = false;
       if (dbg) t0 = clock64();
-      while (__builtin_amdgcn_readfirstlane(lds_ld(&sm.btag[slot])) != (uint32_t)(r + 1)) {
+      while (lds_ld(&sm.btag[slot]) != (uint32_t)(r + 1)) {
         if (lds_ld(&sm.abort_)) { quit = true; break; }
         __builtin_amdgcn_s_sleep(1);
       }
       if (dbg) d_wait += clock64() - t0;
       if (quit) break;
-      int64_t pos = sl_uni(lds_ld(&sm.base[slot]));
-      for (int q = 0; q < sw; q++) pos += lds_ld(&sm.cnt[slot][q]);
-      pos = sl_uni(pos);
-      const uint32_t c = __builtin_amdgcn_readfirstlane(lds_ld(&sm.cnt[slot][sw]));
-      for (int o = 0; o < D.nout; o++) {
-        const int oc = D.out_col[o];
-        int so = 0;
+      int64_t pos = lds_ld(&sm.base[slot]);
+      int q = 0;
 #pragma unroll
-        for (int c = 0; c < NC; c++)
-          if (c == oc) so = soff[c];
-        if (D.col[oc].w == 8) {
-          const int64_t *st = (const int64_t *)(mystage + so);
-          int64_t *dst = (int64_t *)D.dst[o] + pos;
-          for (uint32_t i = lane; i < c; i += 64) dst[i] = st[(tail + i) & mask];
-        } else {
-          const int32_t *st = (const int32_t *)(mystage + so);
-          int32_t *dst = (int32_t *)D.dst[o] + pos;
-          for (uint32_t i = lane; i < c; i += 64) dst[i] = st[(tail + i) & mask];
+      for (int j = 0; j < PER; j++) {
+        const int l = sw + 4 * j;
+        for (; q < l; q++) pos += lds_ld(&sm.cnt[slot][q]);
+        const uint32_t c = lds_ld(&sm.cnt[slot][l]);
+        const unsigned char *mystage = stage0 + (size_t)l * (stg + 64) * rowb;
+        for (int o = 0; o < D.nout; o++) {
+          const int oc = D.out_col[o];
+          int so = 0;
+          bool s8 = false;
+#pragma unroll
+          for (int cc = 0; cc < NC; cc++)
+            if (cc == oc) so = soff[cc], s8 = st8[cc];
+          if (s8) {
+            const int64_t *st = (const int64_t *)(mystage + so);
+            int64_t *dst = (int64_t *)D.dst[o] + pos;
+            for (uint32_t i = lane; i < c; i += 64) dst[i] = st[(tail[j] + i) & mask];
+          } else if (D.col[oc].w == 8) {  // staged narrow: sign-extend back to int64
+            const int32_t *st = (const int32_t *)(mystage + so);
+            int64_t *dst = (int64_t *)D.dst[o] + pos;
+            for (uint32_t i = lane; i < c; i += 64) dst[i] = (int64_t)st[(tail[j] + i) & mask];
+          } else {
+            const int32_t *st = (const int32_t *)(mystage + so);
+            int32_t *dst = (int32_t *)D.dst[o] + pos;
+            for (uint32_t i = lane; i < c; i += 64) dst[i] = st[(tail[j] + i) & mask];
+          }
         }
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // staging read before it is freed
+        tail[j] += c;
+        if (lane == 0) lds_st(&sm.tail[l], tail[j]);
       }
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // staging read before it is freed
-      tail += c;
-      if (lane == 0) {
-        lds_st(&sm.tail[sw], tail);
-        lds_st(&sm.sdone[sw], (uint32_t)(r + 1));
-      }
+      if (lane == 0) lds_st(&sm.sdone[sw], (uint32_t)(r + 1));
     }
     if (dbg && lane == 0) {
       atomicAdd(&D.dbg[4], clock64() - t_all);
@@ -842,7 +860,13 @@ __global__ __launch_bounds__(576) void select_rounds_kernel(SelectDesc D, int64_
   if (lane == 0) ctl[1] = (unsigned long long)(running + tcnt);
 }
 
+static SelectRoundsPlan PlanSelectRoundsNL(const SelectDesc &d, int64_t nrows, int force_nl);
 SelectRoundsPlan PlanSelectRounds(const SelectDesc &d, int64_t nrows) {
+  SelectRoundsPlan p = PlanSelectRoundsNL(d, nrows, 0);
+  if (!p.ok && p.NL == 8) p = PlanSelectRoundsNL(d, nrows, 4);  // 8 loaders leave too little staging: 4
+  return p;
+}
+static SelectRoundsPlan PlanSelectRoundsNL(const SelectDesc &d, int64_t nrows, int force_nl) {
   SelectRoundsPlan p;
   memset(&p, 0, sizeof(p));
   if (d.ncol < 1 || d.ncol > SL_MAX_COL || d.nout < 1 || d.nout > SL_MAX_OUT) return p;
@@ -853,7 +877,7 @@ SelectRoundsPlan PlanSelectRounds(const SelectDesc &d, int64_t nrows) {
     if (d.col[c].w != 4 && d.col[c].w != 8) return p;
     p.ni += d.col[c].w / 4;
     if (d.col[c].w == 8) p.wm |= 1 << c;
-    if ((smask >> c) & 1) rowb += d.col[c].w;
+    if ((smask >> c) & 1) rowb += d.col[c].w == 8 && !d.col[c].narrow ? 8 : 4;
   }
   p.nc = d.ncol;
   // Ring and staging share the CU's LDS.  Sub-steps per step (H) and ring depth
@@ -862,6 +886,14 @@ SelectRoundsPlan PlanSelectRounds(const SelectDesc &d, int64_t nrows) {
   // (the staging ring is what hides the round latency; ties go to H = 2, whose
   // two interleaved sub-steps cost the loader fewer cycles per row).
   int want_h = 0, want_s = 0, want_stg = 4096, want_depth = 0;
+  // One-column shapes staged in 4 bytes (INT32, or INT64 the zone map proves
+  // fits int32) leave LDS for 8 loader waves (two per SIMD: each hides the
+  // other's latencies) with a 3-deep ring and 2048 staged rows each
+  // (profiles/r02_select_rounds_sweep.log).  MBX_SR_NL=4|8 overrides.
+  p.NL = p.nc == 1 && rowb <= 4 ? 8 : 4;
+  if (const char *e = getenv("MBX_SR_NL")) p.NL = atoi(e) == 8 && p.nc == 1 ? 8 : 4;
+  if (force_nl) p.NL = force_nl;
+  if (p.NL == 8) want_h = 1, want_depth = 3;
   if (const char *e = getenv("MBX_SR_H")) want_h = atoi(e) == 1 ? 1 : 2;
   if (const char *e = getenv("MBX_SR_S")) want_s = atoi(e) > 0 ? atoi(e) : 0;
   if (const char *e = getenv("MBX_SR_STG")) want_stg = atoi(e) >= 256 ? atoi(e) : 4096;
@@ -873,17 +905,17 @@ SelectRoundsPlan PlanSelectRounds(const SelectDesc &d, int64_t nrows) {
   for (int h = 2; h >= 1; h--) {
     if (want_h && h != want_h) continue;
     const int depth = want_depth ? want_depth : h == 2 ? 2 : (p.ni <= 2 ? 3 : 2);
-    const size_t ring = (size_t)4 * depth * p.ni * 1024 * h;
+    const size_t ring = (size_t)p.NL * depth * p.ni * 1024 * h;
     if (ring + 2048 >= (size_t)160 * 1024) continue;
     const size_t budget = (size_t)160 * 1024 - 2048 - ring;  // static meta (1.5 KB) + margin
     int stg = want_stg;
-    while (stg >= 256 * h && (size_t)4 * (stg + 64) * rowb > budget) stg >>= 1;
+    while (stg >= 256 * h && (size_t)p.NL * (stg + 64) * rowb > budget) stg >>= 1;
     if (stg < 256 * h || (stg & (stg - 1))) continue;
     if (stg > best_stg) {
       best_stg = stg;
       p.H = h;
       p.depth = depth;
-      p.lds = ring + (size_t)4 * (stg + 64) * rowb;
+      p.lds = ring + (size_t)p.NL * (stg + 64) * rowb;
     }
   }
   if (!best_stg) return p;
@@ -894,7 +926,7 @@ SelectRoundsPlan PlanSelectRounds(const SelectDesc &d, int64_t nrows) {
   if (p.S < 1) return p;
   p.G = NumCUs() < 256 ? NumCUs() : 256;
   const int64_t nsteps = nrows / (256 * p.H);
-  const int64_t ntiles = (nsteps + 4 * p.S - 1) / (4 * p.S);
+  const int64_t ntiles = (nsteps + p.NL * p.S - 1) / (p.NL * p.S);
   p.nrounds = (ntiles + p.G - 1) / p.G;
   if (p.lds < (size_t)96 * 1024) p.lds = (size_t)96 * 1024;  // one workgroup per CU
   p.sleep = 1;
@@ -910,17 +942,25 @@ SelectRoundsPlan PlanSelectRounds(const SelectDesc &d, int64_t nrows) {
 size_t SelectRoundsCtlBytes(const SelectRoundsPlan &p) { return (size_t)(8 + p.nrounds * p.G) * 8; }
 
 namespace {
-template <int NC, int WM, int DP, int H>
-void SrLaunchH(const SelectDesc &d, const SelectRoundsPlan &p, int64_t nrows, unsigned long long *ctl, uint32_t epoch,
-               hipStream_t s) {
+template <int NC, int WM, int DP, int H, int NL>
+void SrLaunchNL(const SelectDesc &d, const SelectRoundsPlan &p, int64_t nrows, unsigned long long *ctl, uint32_t epoch,
+                hipStream_t s) {
   static bool attr = false;
   if (!attr) {
-    (void)hipFuncSetAttribute((const void *)select_rounds_kernel<NC, WM, DP, H>,
+    (void)hipFuncSetAttribute((const void *)select_rounds_kernel<NC, WM, DP, H, NL>,
                               hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024 - 2048);
     attr = true;
   }
-  hipLaunchKernelGGL((select_rounds_kernel<NC, WM, DP, H>), dim3((unsigned)p.G), dim3(576), p.lds, s, d, nrows,
-                     p.nrounds, p.S, p.stg, ctl, epoch, p.sleep, p.test_stall);
+  hipLaunchKernelGGL((select_rounds_kernel<NC, WM, DP, H, NL>), dim3((unsigned)p.G), dim3((NL + 5) * 64), p.lds, s, d,
+                     nrows, p.nrounds, p.S, p.stg, ctl, epoch, p.sleep, p.test_stall);
+}
+template <int NC, int WM, int DP, int H>
+void SrLaunchH(const SelectDesc &d, const SelectRoundsPlan &p, int64_t nrows, unsigned long long *ctl, uint32_t epoch,
+               hipStream_t s) {
+  if constexpr (NC == 1) {
+    if (p.NL == 8) return SrLaunchNL<NC, WM, DP, H, 8>(d, p, nrows, ctl, epoch, s);
+  }
+  SrLaunchNL<NC, WM, DP, H, 4>(d, p, nrows, ctl, epoch, s);
 }
 template <int NC, int WM>
 void SrDepth(const SelectDesc &d, const SelectRoundsPlan &p, int64_t nrows, unsigned long long *ctl, uint32_t epoch,
