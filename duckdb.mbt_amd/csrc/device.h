@@ -366,7 +366,7 @@ void SelectCompact(const SelectDesc &d, int64_t nrows, void *status_buf, int64_t
 // ctl[1] is the selected-row count.
 struct SelectRoundsPlan {
   bool ok;
-  int nc, wm, ni, depth, S, H, NL, stg, G, sleep, test_stall;  // wm: bit c = column c is 8 bytes; H: 256-row sub-steps per step
+  int nc, wm, ni, depth, S, H, NL, stg, G, sleep, test_stall, pw;  // wm: bit c = column c is 8 bytes; H: 256-row sub-steps per step
   int64_t nrounds;
   size_t lds;
 };

@@ -391,7 +391,7 @@ void SelectCompact(const SelectDesc &d, int64_t nrows, void *status_buf, int64_t
 // ---------------------------------------------------------------------------
 namespace {
 constexpr int SR_MR = 32;                    // rounds in flight inside a workgroup (meta slots)
-constexpr int SR_PW = 2;                     // rounds polled per coordinator poll
+constexpr int SR_PW = 4;                     // most rounds polled per coordinator poll (runtime: pwmax)
 constexpr long long SR_TIMEOUT = 10000000;   // s_memrealtime ticks (100 MHz): 100 ms without progress
 struct SrShared {
   unsigned long long arr[SR_MR];  // (count << 16) + arrivals of the round's loaders
@@ -458,7 +458,7 @@ struct SrCols {
 template <int NC, int WM, int DEPTH, int H, int NL>
 __global__ __launch_bounds__((NL + 5) * 64) void select_rounds_kernel(SelectDesc D, int64_t n, int64_t nrounds, int S, int stg,
                                                             unsigned long long *ctl, uint32_t epoch, int sleep_,
-                                                            int test_stall) {
+                                                            int test_stall, int pwmax) {
   typedef SrCols<NC, WM> L;
   extern __shared__ __attribute__((aligned(16))) unsigned char sr_lds[];
   __shared__ SrShared sm;
@@ -744,7 +744,7 @@ __global__ __launch_bounds__((NL + 5) * 64) void select_rounds_kernel(SelectDesc
       aborted = true;  // another workgroup gave up
       break;
     }
-    const int pw = (int)(nrounds - r0 < SR_PW ? nrounds - r0 : SR_PW);
+    const int pw = (int)(nrounds - r0 < pwmax ? nrounds - r0 : pwmax);
     if (dbg) t0 = clock64();
     unsigned long long x[SR_PW][4];
 #pragma unroll
@@ -931,6 +931,8 @@ static SelectRoundsPlan PlanSelectRoundsNL(const SelectDesc &d, int64_t nrows, i
   if (p.lds < (size_t)96 * 1024) p.lds = (size_t)96 * 1024;  // one workgroup per CU
   p.sleep = 1;
   if (const char *e = getenv("MBX_SR_SLEEP")) p.sleep = atoi(e) >= 0 ? atoi(e) : 1;
+  p.pw = 2;  // rounds per coordinator poll (1..4)
+  if (const char *e = getenv("MBX_SR_PW")) p.pw = std::max(1, std::min(4, atoi(e)));
   // tests: workgroup MBX_SR_TEST_STALL never publishes, as if it were never
   // scheduled, so every coordinator times out and the launch aborts
   p.test_stall = -1;
@@ -952,7 +954,7 @@ void SrLaunchNL(const SelectDesc &d, const SelectRoundsPlan &p, int64_t nrows, u
     attr = true;
   }
   hipLaunchKernelGGL((select_rounds_kernel<NC, WM, DP, H, NL>), dim3((unsigned)p.G), dim3((NL + 5) * 64), p.lds, s, d,
-                     nrows, p.nrounds, p.S, p.stg, ctl, epoch, p.sleep, p.test_stall);
+                     nrows, p.nrounds, p.S, p.stg, ctl, epoch, p.sleep, p.test_stall, p.pw);
 }
 template <int NC, int WM, int DP, int H>
 void SrLaunchH(const SelectDesc &d, const SelectRoundsPlan &p, int64_t nrows, unsigned long long *ctl, uint32_t epoch,
