@@ -1976,15 +1976,11 @@ static DRel Aggregate(Engine &e, const DRel &src, const BoundSelect &s) {
   }
   // ---- fast path F2: GROUP BY one small-range int key column, aggregates
   //      over <= 2 int columns of one phys, no predicate.
-  //      (plus: an optional range predicate on one int column, fused)
-  // A filtered GROUP BY runs faster through the fused compiled kernel once it
-  // is built (profiles/r01_query_shapes_1e9.log: c3_where 3.42 vs 3.55 ms at
-  // 1e9 rows, 0.38 vs 0.46 ms at 1e8); until then (and for the unfiltered
-  // C3 shape, where group_direct_lds wins) the LDS-DMA kernel below runs.
-  if (ng >= 1 && s.where && jit::Enabled()) {
-    DRel fused;
-    if (JitGroupAggregate(e, src, s, fused)) return fused;
-  }
+  //      (plus: up to GROUP_MAX_PRED range predicates on int columns, fused)
+  // Filtered shapes run here too: since its table atomics stopped draining
+  // the DMA ring, group_direct_lds beats the run-time compiled jit_group at
+  // 1e9 rows (c3_where 3.00 vs 3.34 ms, c3_where2 3.66 vs 4.06 ms,
+  // profiles/r02_group_where_sweep.log); jit_group takes the shapes F2 does not.
   std::map<int, std::pair<i128, i128>> f2_ranges;
   bool f2_pred_ok = !s.where || (RangeConj(*s.where, f2_ranges) && f2_ranges.size() <= GROUP_MAX_PRED);
   for (auto &kv : f2_ranges)

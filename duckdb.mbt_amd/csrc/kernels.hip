@@ -1541,6 +1541,8 @@ bool GroupByDirectStates(const void *kcol, int kphys, int64_t kmin, int nk, cons
   // on the segmented kernel).
   {
     int depth = 2, gpc = nv > 0 ? 1 : 3;
+    for (int j = 0; j < pr.n; j++)  // predicate slices of their own: a deeper ring (c3_where: d3 3.00 vs d2 3.32 ms)
+      if (pr.p[j].src == 1) depth = 3;
     bool use = true;
     const char *e = getenv("MBX_GD_VARIANT");
     if (e && *e) use = sscanf(e, "d%d_g%d", &depth, &gpc) == 2 || pr.n != 0;
