@@ -780,6 +780,199 @@ __global__ __launch_bounds__(256) void filter_multi_lds_kernel(FilterMultiDesc D
   }
 }
 
+// Compile-time layout of filter_multi_t: NC columns, bit c of WM = column c is
+// 8 bytes wide (else 4); slices at fixed offsets, then the NULL-able columns'
+// 32-B validity words (runtime: which columns, at the end of the slot).
+template <int NC, int WM>
+struct FmCols {
+  static constexpr int w(int c) { return (WM >> c) & 1 ? 8 : 4; }
+  static constexpr int off(int c) { return c == 0 ? 0 : off(c - 1) + w(c - 1) * 256; }
+  static constexpr int ni() { return off(NC) / 1024; }
+};
+template <int N>
+__device__ __forceinline__ void fm_wait() {
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+
+// filter_multi_lds with the column layout as template parameters (the
+// generic kernel above decides widths and predicate roles per column and row
+// at run time: ≈865 instructions in its loop region, exec-mask branches for
+// each short-circuit, SGPR spills).  Here every slice read has a fixed offset
+// and width, predicates combine bitwise, and only the NULL-able columns
+// (0..NC, their validity words one exec-masked LDS-DMA instruction each) stay
+// run-time: a scalar switch picks the exact counted vmcnt for their number.
+template <int NC, int WM, int DEPTH>
+__global__ __launch_bounds__(256) void filter_multi_t_kernel(FilterMultiDesc D, int64_t n, AggPartial *partials,
+                                                             int slot_bytes) {
+  typedef FmCols<NC, WM> L;
+  extern __shared__ __attribute__((aligned(16))) unsigned char fmt_lds[];
+  constexpr int NIC = L::ni();
+  const int SB = slot_bytes;
+  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  unsigned char *ring = fmt_lds + (size_t)w * DEPTH * SB;
+  int voff[NC];
+  bool hv[NC], isp[NC];
+  int64_t lo[NC];
+  uint64_t span[NC];
+  const unsigned char *colp[NC];
+  int nvw = 0;
+#pragma unroll
+  for (int c = 0; c < NC; c++) {
+    hv[c] = D.col[c].valid != nullptr;
+    voff[c] = L::off(NC) + 32 * nvw;
+    nvw += hv[c];
+    isp[c] = D.col[c].is_pred != 0;
+    lo[c] = D.col[c].lo;
+    span[c] = D.col[c].span;
+    colp[c] = (const unsigned char *)D.col[c].data + lane * 16;
+  }
+  const int agg = D.agg;
+  const int64_t nsteps = n >> 8;
+  const int64_t nw = (int64_t)gridDim.x * 4;
+  int64_t st = (int64_t)blockIdx.x * 4 + w;
+  auto issue = [&](int64_t q, int d) {
+    unsigned char *dst = ring + d * SB;
+#pragma unroll
+    for (int c = 0; c < NC; c++) {
+      const unsigned char *src = colp[c] + q * (L::w(c) * 256);
+      __builtin_amdgcn_global_load_lds((const void *)src, (void *)(dst + L::off(c)), 16, 0, 2);
+      if (L::w(c) == 8)
+        __builtin_amdgcn_global_load_lds((const void *)(src + 1024), (void *)(dst + L::off(c) + 1024), 16, 0, 2);
+    }
+#pragma unroll
+    for (int c = 0; c < NC; c++)
+      if (hv[c] && lane < 2)
+        __builtin_amdgcn_global_load_lds((const void *)(D.col[c].valid + q * 4 + lane * 2), (void *)(dst + voff[c]), 16,
+                                         0, 0);
+  };
+  Acc A;
+  A.cnt = 0; A.slo = 0; A.shi = 0; A.mn = INT64_MAX; A.mx = INT64_MIN;
+  const bool mm32 = D.mm && D.mm32, mm = D.mm && !mm32, narrow = D.narrow;
+  int32_t mn32 = INT32_MAX, mx32 = INT32_MIN;
+  if (nsteps > 0) {
+#pragma unroll
+    for (int d = 0; d < DEPTH; d++) {
+      int64_t q = st + d * nw;
+      issue(q < nsteps ? q : 0, d);
+    }
+  }
+  int k = 0;
+  for (; st < nsteps; st += nw) {
+    switch (nvw) {  // wave-uniform: the exact count of the slots issued after this one
+      case 0: fm_wait<NIC * (DEPTH - 1)>(); break;
+      case 1: fm_wait<(NIC + 1) * (DEPTH - 1)>(); break;
+      case 2: fm_wait<(NIC + 2) * (DEPTH - 1)>(); break;
+      case 3: fm_wait<(NIC + 3) * (DEPTH - 1)>(); break;
+      default: fm_wait<(NIC + 4) * (DEPTH - 1)>(); break;
+    }
+    const unsigned char *src = ring + k * SB;
+    int64_t v[NC][4];
+#pragma unroll
+    for (int c = 0; c < NC; c++) {
+      if (L::w(c) == 8) {
+        v2i64 x0 = *(const v2i64 *)(src + L::off(c) + lane * 32), x1 = *(const v2i64 *)(src + L::off(c) + lane * 32 + 16);
+        v[c][0] = x0.x; v[c][1] = x0.y; v[c][2] = x1.x; v[c][3] = x1.y;
+      } else {
+        v4i32 x = *(const v4i32 *)(src + L::off(c) + lane * 16);
+        v[c][0] = x.x; v[c][1] = x.y; v[c][2] = x.z; v[c][3] = x.w;
+      }
+    }
+    unsigned vm = 0xFu;  // rows 4 lane + e where every NULL-able column is valid
+#pragma unroll
+    for (int c = 0; c < NC; c++)
+      if (hv[c]) vm &= (unsigned)(*(const uint64_t *)(src + voff[c] + (lane >> 4) * 8) >> (4 * (lane & 15))) & 0xFu;
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    int64_t q = st + DEPTH * nw;
+    issue(q < nsteps ? q : st, k);
+#pragma unroll
+    for (int e = 0; e < 4; e++) {
+      bool ok = (vm >> e) & 1u;
+      int64_t val = 0;
+#pragma unroll
+      for (int c = 0; c < NC; c++) {
+        if (isp[c]) ok = ok & ((uint64_t)(v[c][e] - lo[c]) <= span[c]);
+        val = c == agg ? v[c][e] : val;
+      }
+      if (agg < 0) {
+        acc_count(A, ok);
+      } else {
+        acc_row(A, ok, val, mm, narrow);
+        if (mm32) {
+          mn32 = min(mn32, ok ? (int32_t)val : INT32_MAX);
+          mx32 = max(mx32, ok ? (int32_t)val : INT32_MIN);
+        }
+      }
+    }
+    k = k + 1 == DEPTH ? 0 : k + 1;
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  if (blockIdx.x == 0 && w == 0) {
+    for (int64_t i = (nsteps << 8) + lane; i < n; i += 64) {
+      bool ok = true;
+      int64_t val = 0;
+      for (int c = 0; c < D.ncol; c++) {
+        int64_t x = D.col[c].phys == P_I64 ? ((const int64_t *)D.col[c].data)[i] : (int64_t)((const int32_t *)D.col[c].data)[i];
+        if (D.col[c].is_pred) ok = ok && (uint64_t)(x - D.col[c].lo) <= D.col[c].span;
+        if (D.col[c].valid) ok = ok && ((D.col[c].valid[i >> 6] >> (i & 63)) & 1);
+        if (c == D.agg) val = x;
+      }
+      if (D.agg < 0) {
+        acc_count(A, ok);
+      } else {
+        acc_row(A, ok, val, mm, narrow);
+        if (mm32) {
+          mn32 = min(mn32, ok ? (int32_t)val : INT32_MAX);
+          mx32 = max(mx32, ok ? (int32_t)val : INT32_MIN);
+        }
+      }
+    }
+  }
+  if (mm32) {  // a count of 0 makes the emit write NULL whatever these hold
+    A.mn = mn32;
+    A.mx = mx32;
+  }
+  if (narrow) A.shi = (int64_t)A.slo >> 63;
+  acc_wave_reduce(A);
+  __syncthreads();
+  Acc *part = (Acc *)fmt_lds;
+  if (lane == 0) part[w] = A;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    Acc T0 = part[0];
+    for (int i = 1; i < 4; i++) acc_merge(T0, part[i]);
+    partials[blockIdx.x] = AggPartial{T0.cnt, T0.slo, T0.shi, T0.mn, T0.mx};
+  }
+}
+
+namespace {
+template <int NC, int WM>
+void FmtLaunch(const FilterMultiDesc &d, int64_t nrows, AggPartial *partials, int slot, int grid, int dp, hipStream_t s) {
+  constexpr int ni = FmCols<NC, WM>::ni();
+  if constexpr (ni <= 1) {
+    hipLaunchKernelGGL((filter_multi_t_kernel<NC, WM, 6>), dim3(grid), dim3(256), (size_t)4 * 6 * slot, s, d, nrows,
+                       partials, slot);
+  } else if constexpr (ni == 2) {
+    hipLaunchKernelGGL((filter_multi_t_kernel<NC, WM, 3>), dim3(grid), dim3(256), (size_t)4 * 3 * slot, s, d, nrows,
+                       partials, slot);
+  } else {
+    if (dp == 3)
+      hipLaunchKernelGGL((filter_multi_t_kernel<NC, WM, 3>), dim3(grid), dim3(256), (size_t)4 * 3 * slot, s, d, nrows,
+                         partials, slot);
+    else
+      hipLaunchKernelGGL((filter_multi_t_kernel<NC, WM, 2>), dim3(grid), dim3(256), (size_t)4 * 2 * slot, s, d, nrows,
+                         partials, slot);
+  }
+}
+template <int NC, int WM = 0>
+void FmtDispatch(const FilterMultiDesc &d, int wm, int64_t nrows, AggPartial *partials, int slot, int grid, int dp,
+                 hipStream_t s) {
+  if constexpr (WM < (1 << NC)) {
+    if (wm == WM) return FmtLaunch<NC, WM>(d, nrows, partials, slot, grid, dp, s);
+    FmtDispatch<NC, WM + 1>(d, wm, nrows, partials, slot, grid, dp, s);
+  }
+}
+}  // namespace
+
 int FilterMultiPartials(const FilterMultiDesc &d_in, int64_t nrows, AggPartial *partials, hipStream_t s) {
   FilterMultiDesc d = d_in;
   int nld = 0, slot = 0;  // nld: LDS-DMA instructions per step (the executor keeps it <= 8)
@@ -816,6 +1009,23 @@ int FilterMultiPartials(const FilterMultiDesc &d_in, int64_t nrows, AggPartial *
   // MBX_FM_DEPTH=<2..4>: ring depth for 3..5 loads per step (sweeps)
   int dp = 2;
   if (const char *ed = getenv("MBX_FM_DEPTH")) dp = atoi(ed) >= 2 && atoi(ed) <= 4 ? atoi(ed) : 2;
+  // the templated kernel (MBX_FM_VARIANT=generic keeps the one below)
+  {
+    const char *ev = getenv("MBX_FM_VARIANT");
+    if (!(ev && strcmp(ev, "generic") == 0) && d.ncol >= 1 && d.ncol <= 4 && (dp == 2 || dp == 3)) {
+      int wm = 0;
+      for (int c = 0; c < d.ncol; c++)
+        if (d.col[c].phys == P_I64) wm |= 1 << c;
+      switch (d.ncol) {
+        case 1: FmtDispatch<1>(d, wm, nrows, partials, slot, grid, dp, s); break;
+        case 2: FmtDispatch<2>(d, wm, nrows, partials, slot, grid, dp, s); break;
+        case 3: FmtDispatch<3>(d, wm, nrows, partials, slot, grid, dp, s); break;
+        default: FmtDispatch<4>(d, wm, nrows, partials, slot, grid, dp, s); break;
+      }
+      CHECK_LAUNCH();
+      return grid;
+    }
+  }
 #define FMD(L) \
   if (dp == 2) FM(L, 2); else if (dp == 3) FM(L, 3); else FM(L, 4);
   switch (nld) {

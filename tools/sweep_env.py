@@ -21,14 +21,22 @@ SQL = {
     "c3_where2": "SELECT k, SUM(v), COUNT(*) FROM t WHERE x > 24 AND k2 = 1 GROUP BY k",
     "c3": "SELECT k, SUM(v), COUNT(*) FROM t GROUP BY k",
     "c5": "SELECT COUNT(*), SUM(x) FROM t WHERE x > 24",
+    "filter_mm": "SELECT COUNT(*), SUM(x), MIN(x), MAX(x) FROM t WHERE x > 24 AND k < 16",
+    # NULLABLE=1
+    "c2n": "SELECT COUNT(*) FROM t WHERE xn > 24",
+    "c5n": "SELECT COUNT(*), SUM(xn) FROM t WHERE xn > 24",
+    "c5n_sumv": "SELECT COUNT(vn), SUM(vn) FROM t WHERE x > 24",
 }
 m = ge._load()
 n = int(sys.argv[1])
 cfg = m.Config.create()
 cfg.set("mbx_profile", "true")
 c = m.connect_with_config(cfg).value
+extra = (", CASE WHEN mbx_synth(13, i, 10) = 0 THEN NULL ELSE mbx_synth(42, i, 50) + 1 END AS xn, "
+         "CASE WHEN mbx_synth(19, i, 7) = 0 THEN NULL ELSE mbx_synth(9, i, 1099511627776) - 549755813888 END AS vn"
+         if os.environ.get("NULLABLE") else "")
 c.query(f"CREATE TABLE t AS SELECT CAST(mbx_synth(7, i, 32) AS INTEGER) AS k, CAST(mbx_synth(8, i, 4) AS INTEGER) AS k2, "
-        f"mbx_synth(9, i, 1099511627776) - 549755813888 AS v, mbx_synth(42, i, 50) + 1 AS x FROM range({n}) tbl(i)")
+        f"mbx_synth(9, i, 1099511627776) - 549755813888 AS v, mbx_synth(42, i, 50) + 1 AS x{extra} FROM range({n}) tbl(i)")
 base_env = dict(os.environ)
 for shape in sys.argv[2:]:
     ref = None
