@@ -85,6 +85,47 @@ __global__ __launch_bounds__(256) void two_stream(const int *__restrict__ keys, 
   if (acc == 0x5a5a5a5a5a5aLL) atomicAdd(out, 1ull);
 }
 
+// pure two-array stream with WAVES waves per block and cache policy AUX on the
+// LDS-DMA loads (2 = nt, 0 = default); round 2: is there a faster stream shape?
+template <int DEPTH, int WAVES, int AUX>
+__global__ __launch_bounds__(WAVES * 64) void two_stream_w(const int *__restrict__ keys, const long long *__restrict__ vals,
+                                                          long long nsteps, unsigned long long *out) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
+  constexpr int SB = 3072;
+  const int t = threadIdx.x, w = t >> 6, lane = t & 63;
+  unsigned char *ring = lds + w * DEPTH * SB;
+  const long long nw = (long long)gridDim.x * WAVES;
+  long long st = (long long)blockIdx.x * WAVES + w;
+  auto issue = [&](long long q, int d) {
+    unsigned char *dst = ring + d * SB;
+    const unsigned char *kp = (const unsigned char *)keys + q * 1024;
+    const unsigned char *vp = (const unsigned char *)vals + q * 2048;
+    __builtin_amdgcn_global_load_lds((const void *)(kp + lane * 16), (void *)dst, 16, 0, AUX);
+    __builtin_amdgcn_global_load_lds((const void *)(vp + lane * 16), (void *)(dst + 1024), 16, 0, AUX);
+    __builtin_amdgcn_global_load_lds((const void *)(vp + 1024 + lane * 16), (void *)(dst + 2048), 16, 0, AUX);
+  };
+#pragma unroll
+  for (int d = 0; d < DEPTH; d++) {
+    long long q = st + d * nw;
+    issue(q < nsteps ? q : 0, d);
+  }
+  long long acc = 0;
+  int k = 0;
+  for (; st < nsteps; st += nw) {
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(3 * (DEPTH - 1)) : "memory");
+    const unsigned char *src = ring + k * SB;
+    v4i32 kv = *(const v4i32 *)(src + lane * 16);
+    v2i64 a0 = *(const v2i64 *)(src + 1024 + lane * 32);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    long long q = st + DEPTH * nw;
+    issue(q < nsteps ? q : st, k);
+    acc += kv.x + a0.x;
+    k = k + 1 == DEPTH ? 0 : k + 1;
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  if (acc == 0x5a5a5a5a5a5aLL) atomicAdd(out, 1ull);
+}
+
 // the same bytes as ONE array: 3 KiB contiguous per step
 template <int DEPTH>
 __global__ __launch_bounds__(256) void one_stream(const unsigned char *__restrict__ in, long long nsteps,
@@ -370,6 +411,21 @@ int main(int argc, char **argv) {
     CK(hipMemcpy(&flag, out, 8, hipMemcpyDeviceToHost));                                                      \
     printf("lc NC=%d ", NC);                                                                                  \
     report(flag ? "lc/BAD" : "lc/packed", D, 1, ms);                                                          \
+  }
+#define RUNW(D, W, A, G)                                                                                      \
+  {                                                                                                           \
+    size_t lds = (W) * (D) * 3072;                                                                            \
+    CK(hipFuncSetAttribute((const void *)two_stream_w<D, W, A>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds)); \
+    float ms = TimeIt([&] { hipLaunchKernelGGL((two_stream_w<D, W, A>), dim3(cus * (G)), dim3((W) * 64), lds, 0, k, v, nsteps, out); }, 15); \
+    printf("w%d aux%d ", W, A);                                                                               \
+    report("two/none", D, G, ms);                                                                             \
+  }
+  if (argc > 2 && argv[2][0] == 'w') {  // round 2: waves per block and cache policy of the pure stream
+    RUNW(2, 4, 2, 1) RUNW(2, 4, 0, 1) RUNW(3, 4, 2, 1) RUNW(2, 8, 2, 1) RUNW(2, 8, 0, 1) RUNW(3, 8, 2, 1)
+    RUNW(4, 8, 2, 1) RUNW(2, 16, 2, 1) RUNW(2, 12, 2, 1) RUNW(2, 8, 2, 2) RUNW(2, 4, 2, 2) RUNW(2, 4, 2, 3)
+    RUNW(2, 4, 2, 1) RUNW(2, 8, 2, 1)
+    RUN1(2, 1) RUN1(6, 1)
+    return 0;
   }
   if (argc > 2 && argv[2][0] == 'l') {
     RUNLC(4, 4) RUNLC(6, 4) RUNLC(4, 8) RUNLC(6, 8) RUNLC(8, 8) RUNLC(6, 12)
