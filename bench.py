@@ -402,6 +402,14 @@ def bench_c4(mbx, conn, n, args):
     batch = 10_000_000
     i = np.arange(n, dtype=np.uint64)
     v = ((i * np.uint64(2654435761)) & np.uint64(2**63 - 1)).astype(np.int64)
+    # untimed warm-up: the process's first large pageable H2D costs ~50 ms of
+    # one-time runtime setup (tools/c4_probe.py, profiles/r02_c4_probe.log)
+    conn.query("CREATE TABLE c4w (v BIGINT)")
+    ap = conn.create_appender("main", "c4w").value
+    ap.append_column(0, v[:min(batch, n)])
+    assert isinstance(ap.commit(min(batch, n)), mbx.Ok)
+    ap.close()
+    conn.query("DROP TABLE c4w")
     conn.query("CREATE TABLE c4 (v BIGINT)")
     ap = conn.create_appender("main", "c4").value
     t0 = time.perf_counter()
@@ -410,15 +418,27 @@ def bench_c4(mbx, conn, n, args):
         assert isinstance(ap.commit(min(batch, n - s)), mbx.Ok)
     ap.close()
     t_in = time.perf_counter() - t0
-    t0 = time.perf_counter()
-    slices = []
+    # read-back in 1e6-row slices (the MoonBit decoders' cap, duckdb_arrow_native.mbt:435):
+    # query_arrow + duckdb_mb_arrow_get_column_int64 timed, the check of each
+    # returned Bytes ([i32 count][int64 LE values]) done outside the clock
+    import ctypes
+    t_q = t_g = 0.0
+    ok = True
     for k in range(0, n, 1_000_000):
+        a0 = time.perf_counter()
         a = conn.query_arrow(f"SELECT v FROM c4 LIMIT 1000000 OFFSET {k}").value
-        slices.append(a.raw_int64_bytes(0))  # [i32 count][int64 LE values]: the get_column_int64 wire buffer
+        a1 = time.perf_counter()
+        bp = mbx.lib.duckdb_mb_arrow_get_column_int64(a._h, 0)
+        a2 = time.perf_counter()
+        t_q += a1 - a0
+        t_g += a2 - a1
+        m = min(1_000_000, n - k)
+        ln = mbx.lib.duckdb_mbx_bytes_len(bp)
+        got = np.ctypeslib.as_array(ctypes.cast(bp, ctypes.POINTER(ctypes.c_uint8)), shape=(max(ln, 1),))
+        ok &= ln == 4 + 8 * m and np.array_equal(got[4:4 + 8 * m].view(np.int64), v[k:k + m])
+        mbx.lib.duckdb_mbx_bytes_free(bp)
         a.close()
-    t_out = time.perf_counter() - t0
-    ok = all(np.array_equal(np.frombuffer(b[4:], dtype=np.int64), v[k:k + 1_000_000])
-             for b, k in zip(slices, range(0, n, 1_000_000)))
+    t_out = t_q + t_g
     ok &= one_count(conn) == n
     conn.close()
     # the same round trip through the reference's row-wise Appender API
@@ -428,7 +448,8 @@ def bench_c4(mbx, conn, n, args):
     chunk_api = native_harness(["c4chunk", str(n)])
     res = {"metric": "C4 appender ingest + arrow read-back", "value": n / (t_in + t_out), "unit": "rows/s",
            "n_gpus": 1, "ingest_gbs": n * 8 / t_in / 1e9, "readback_gbs": n * 8 / t_out / 1e9,
-           "ingest_s": t_in, "readback_s": t_out, "rows": n, "bit_exact": ok,
+           "ingest_s": t_in, "readback_s": t_out, "readback_getter_gbs": n * 8 / t_g / 1e9, "readback_query_s": t_q,
+           "rows": n, "bit_exact": ok,
            "bound": "host link (PCIe Gen5 x16, 63 GB/s spec) + host-side wire-buffer assembly",
            "ingest_api": "columnar duckdb_mbx_append_column (extension), from Python",
            "row_appender_native": row_api, "chunk_appender_native": chunk_api}

@@ -22,6 +22,7 @@
 #include "device.h"
 #include "jit.h"
 #include "engine.h"
+#include "hostlink.h"
 #include "vm.h"
 
 namespace mbx {
@@ -2816,6 +2817,13 @@ bool DeviceColumnWireOk(const DeviceResult &d, int col, int phys) {
   return dc.phys == phys && dc.data && (w == 1 || w == 4 || w == 8) && dc.phys != P_STR;
 }
 
+// Device -> fresh pageable host memory (a getter's Bytes) at link rate
+// (hostlink.cpp); the source is complete (its stream was synchronised).
+static void LinkCopy(Engine &e, void *dst, const void *src, size_t n) {
+  const std::string err = LinkD2H(e.device, dst, src, n);
+  if (!err.empty()) ThrowError("IO", err);
+}
+
 // The Arrow wire form of one device column (values with NULLs zeroed, then
 // validity bytes when vbytes != nullptr), built by one kernel in a device
 // staging buffer and copied out with one DMA per part.
@@ -2827,18 +2835,18 @@ bool CopyDeviceColumnWire(Connection &c, DeviceResult &d, int col, int phys, voi
   const int w = PhysSize(dc.phys);
   if (n <= 0) return true;
   if (!dc.validity) {  // nothing to zero: the column is already the wire layout
-    HIPCHK(hipMemcpyAsync(vals, dc.data, (size_t)n * w, hipMemcpyDeviceToHost, e.stream));
     HIPCHK(hipStreamSynchronize(e.stream));
+    LinkCopy(e, vals, dc.data, (size_t)n * w);
     if (vbytes) memset(vbytes, 1, (size_t)n);
     return true;
   }
   auto buf = Alloc(e, (size_t)n * (w + 1) + 16);
   uint8_t *dv = (uint8_t *)buf->p, *db = dv + (size_t)n * w;
   dev::ArrowWire(dc.data, dc.validity, n, w, dv, vbytes ? db : nullptr, e.stream);
-  HIPCHK(hipMemcpyAsync(vals, dv, (size_t)n * w, hipMemcpyDeviceToHost, e.stream));
-  if (vbytes) HIPCHK(hipMemcpyAsync(vbytes, db, (size_t)n, hipMemcpyDeviceToHost, e.stream));
   HIPCHK(hipStreamSynchronize(e.stream));
   CheckError(e);
+  LinkCopy(e, vals, dv, (size_t)n * w);
+  if (vbytes) LinkCopy(e, vbytes, db, (size_t)n);
   return true;
 }
 
@@ -2884,9 +2892,9 @@ bool CopyDeviceColumnText(Connection &c, DeviceResult &d, int col, const std::fu
     dev::TextWrite(tc, n, (const int64_t *)offs->p, (char *)buf->p, vbytes ? (uint8_t *)buf->p + chars : nullptr,
                    e.stream);
   }
-  if (out_bytes) HIPCHK(hipMemcpyAsync(host, buf->p, out_bytes, hipMemcpyDeviceToHost, e.stream));
   HIPCHK(hipStreamSynchronize(e.stream));
   CheckError(e);
+  if (out_bytes) LinkCopy(e, host, buf->p, out_bytes);
   if (e.profile) {  // a getter runs after its query's profile was taken: its kernels go to the drain history
     for (auto &ev : e.events) {
       float ms = 0;

@@ -215,10 +215,56 @@ def test_arrow_buffer_limit_is_the_moonbit_bytes_limit(mbx):
     assert len(raw) == 4 + 8 * n_ok
     got = np.frombuffer(raw, dtype=np.int64, offset=4)
     assert int.from_bytes(raw[:4], "little") == n_ok and got[0] == 0 and got[-1] == 3 * (n_ok - 1)
-    assert np.array_equal(got[::1_000_003], np.arange(0, n_ok, 1_000_003, dtype=np.int64) * 3)
+    assert np.array_equal(got, np.arange(n_ok, dtype=np.int64) * 3)  # through the host-link pool
     a = c.query_arrow("SELECT x FROM big").value
     raw = a.raw_int64_bytes(0)
     a.close()
     assert raw == b""
     assert "2^28" in mbx._last_error("")
+    c.close()
+
+
+@pytest.mark.parametrize("link", [{}, {"MBX_LINK_THREADS": "0"}, {"MBX_LINK_THREADS": "3", "MBX_LINK_MIN": "1"},
+                                  {"MBX_LINK_HUGE": "0", "MBX_LINK_MIN": "1"}], ids=["pool", "runtime", "t3_min1", "nohuge"])
+@pytest.mark.parametrize("n", [5, 3_000_017])
+def test_arrow_host_link_copies_exact(mbx, monkeypatch, link, n):
+    """Getter buffers copied by the host-link pool (csrc/hostlink.cpp: threads
+    with pinned double buffers into huge-page-advised fresh Bytes) and by the
+    runtime's own copy are byte-exact, for ragged sizes whose last chunk is
+    partial: plain int64/int32/double columns (direct DMA), NULL-able ones
+    (wire kernel + validity bytes) and device-formatted strings."""
+    import numpy as np
+    for k, v in link.items():
+        monkeypatch.setenv(k, v)
+    c = mbx.connect().value
+    assert isinstance(c.query(
+        f"CREATE TABLE hl AS SELECT i * 7 - 11 AS b, CAST(i % 100000 AS INTEGER) AS a, CAST(i AS DOUBLE) / 4 AS d, "
+        f"CASE WHEN i % 3 = 0 THEN NULL ELSE i END AS nb FROM range({n}) tbl(i)"), mbx.Ok)
+    i = np.arange(n, dtype=np.int64)
+    a = c.query_arrow("SELECT b, a, d, nb FROM hl").value
+
+    def raw(kind, col, nullable=False):
+        return mbx._take(getattr(mbx.lib, f"duckdb_mb_arrow_get_column_{kind}{'_nullable' if nullable else ''}")(a._h, col))
+
+    def body(b, dtype, count):
+        assert int.from_bytes(b[:4], "little") == n
+        return np.frombuffer(b, dtype=dtype, offset=4, count=count)
+
+    assert np.array_equal(body(raw("int64", 0), np.int64, n), i * 7 - 11)
+    assert np.array_equal(body(raw("int32", 1), np.int32, n), (i % 100000).astype(np.int32))
+    assert np.array_equal(body(raw("double", 2), np.float64, n), i.astype(np.float64) / 4)
+    nb = raw("int64", 3, nullable=True)
+    valid = i % 3 != 0
+    assert np.array_equal(body(nb, np.int64, n), np.where(valid, i, 0))
+    assert np.array_equal(np.frombuffer(nb, dtype=np.uint8, offset=4 + 8 * n), valid.astype(np.uint8))
+    if n <= 5:
+        assert a.get_column_string(0) == [str(x * 7 - 11) for x in range(n)]
+    else:
+        s = raw("string", 0)
+        nn, chars = int.from_bytes(s[:4], "little"), int.from_bytes(s[4:8], "little")
+        assert nn == n
+        text = s[8:8 + chars].split(b"\0")[:-1]
+        assert len(text) == n and text[0] == b"-11" and text[-1] == str((n - 1) * 7 - 11).encode()
+        assert text[n // 2] == str((n // 2) * 7 - 11).encode()
+    a.close()
     c.close()

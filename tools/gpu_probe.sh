@@ -1,3 +1,4 @@
 set -o pipefail
 mkdir -p gpurun_out/probe
-timeout -k 10 120 ./tools/c3_probe 1000000000 w > gpurun_out/probe/c3_probe_w.log 2>&1 || exit 11
+export C4P_GRID=1
+timeout -k 10 300 python3 -u tools/c4_probe.py > gpurun_out/probe/c4_probe.log 2>&1 || exit 12
