@@ -801,7 +801,13 @@ __device__ __forceinline__ void fm_wait() {
 // and width, predicates combine bitwise, and only the NULL-able columns
 // (0..NC, their validity words one exec-masked LDS-DMA instruction each) stay
 // run-time: a scalar switch picks the exact counted vmcnt for their number.
-template <int NC, int WM, int DEPTH>
+// The host puts the aggregated column first and gives every column that is
+// not a predicate the always-true range [INT64_MIN, +2^64), so a row's test
+// is the same branch-free compare for every column.  MODE: 0 COUNT only,
+// 1 SUM (+COUNT) accumulated in int64 (no MIN/MAX; the grid bounds the sum),
+// 3 the same plus MIN/MAX in int32 (the zone map bounds |value| < 2^31),
+// 2 general (run-time MIN/MAX, int128 SUM, int32 MIN/MAX).
+template <int NC, int WM, int DEPTH, int MODE>
 __global__ __launch_bounds__(256) void filter_multi_t_kernel(FilterMultiDesc D, int64_t n, AggPartial *partials,
                                                              int slot_bytes) {
   typedef FmCols<NC, WM> L;
@@ -811,7 +817,7 @@ __global__ __launch_bounds__(256) void filter_multi_t_kernel(FilterMultiDesc D, 
   const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
   unsigned char *ring = fmt_lds + (size_t)w * DEPTH * SB;
   int voff[NC];
-  bool hv[NC], isp[NC];
+  bool hv[NC];
   int64_t lo[NC];
   uint64_t span[NC];
   const unsigned char *colp[NC];
@@ -821,12 +827,10 @@ __global__ __launch_bounds__(256) void filter_multi_t_kernel(FilterMultiDesc D, 
     hv[c] = D.col[c].valid != nullptr;
     voff[c] = L::off(NC) + 32 * nvw;
     nvw += hv[c];
-    isp[c] = D.col[c].is_pred != 0;
     lo[c] = D.col[c].lo;
     span[c] = D.col[c].span;
     colp[c] = (const unsigned char *)D.col[c].data + lane * 16;
   }
-  const int agg = D.agg;
   const int64_t nsteps = n >> 8;
   const int64_t nw = (int64_t)gridDim.x * 4;
   int64_t st = (int64_t)blockIdx.x * 4 + w;
@@ -887,14 +891,18 @@ __global__ __launch_bounds__(256) void filter_multi_t_kernel(FilterMultiDesc D, 
 #pragma unroll
     for (int e = 0; e < 4; e++) {
       bool ok = (vm >> e) & 1u;
-      int64_t val = 0;
 #pragma unroll
-      for (int c = 0; c < NC; c++) {
-        if (isp[c]) ok = ok & ((uint64_t)(v[c][e] - lo[c]) <= span[c]);
-        val = c == agg ? v[c][e] : val;
-      }
-      if (agg < 0) {
+      for (int c = 0; c < NC; c++) ok = ok & ((uint64_t)(v[c][e] - lo[c]) <= span[c]);
+      const int64_t val = v[0][e];
+      if constexpr (MODE == 0) {
         acc_count(A, ok);
+      } else if constexpr (MODE == 1 || MODE == 3) {
+        A.cnt += ok;
+        A.slo += (uint64_t)(ok ? val : 0);
+        if constexpr (MODE == 3) {
+          mn32 = min(mn32, ok ? (int32_t)val : INT32_MAX);
+          mx32 = max(mx32, ok ? (int32_t)val : INT32_MIN);
+        }
       } else {
         acc_row(A, ok, val, mm, narrow);
         if (mm32) {
@@ -945,30 +953,39 @@ __global__ __launch_bounds__(256) void filter_multi_t_kernel(FilterMultiDesc D, 
 }
 
 namespace {
-template <int NC, int WM>
-void FmtLaunch(const FilterMultiDesc &d, int64_t nrows, AggPartial *partials, int slot, int grid, int dp, hipStream_t s) {
+template <int NC, int WM, int MODE>
+void FmtLaunchM(const FilterMultiDesc &d, int64_t nrows, AggPartial *partials, int slot, int grid, int dp,
+                hipStream_t s) {
   constexpr int ni = FmCols<NC, WM>::ni();
   if constexpr (ni <= 1) {
-    hipLaunchKernelGGL((filter_multi_t_kernel<NC, WM, 6>), dim3(grid), dim3(256), (size_t)4 * 6 * slot, s, d, nrows,
-                       partials, slot);
+    hipLaunchKernelGGL((filter_multi_t_kernel<NC, WM, 6, MODE>), dim3(grid), dim3(256), (size_t)4 * 6 * slot, s, d,
+                       nrows, partials, slot);
   } else if constexpr (ni == 2) {
-    hipLaunchKernelGGL((filter_multi_t_kernel<NC, WM, 3>), dim3(grid), dim3(256), (size_t)4 * 3 * slot, s, d, nrows,
-                       partials, slot);
+    hipLaunchKernelGGL((filter_multi_t_kernel<NC, WM, 3, MODE>), dim3(grid), dim3(256), (size_t)4 * 3 * slot, s, d,
+                       nrows, partials, slot);
   } else {
     if (dp == 3)
-      hipLaunchKernelGGL((filter_multi_t_kernel<NC, WM, 3>), dim3(grid), dim3(256), (size_t)4 * 3 * slot, s, d, nrows,
-                         partials, slot);
+      hipLaunchKernelGGL((filter_multi_t_kernel<NC, WM, 3, MODE>), dim3(grid), dim3(256), (size_t)4 * 3 * slot, s, d,
+                         nrows, partials, slot);
     else
-      hipLaunchKernelGGL((filter_multi_t_kernel<NC, WM, 2>), dim3(grid), dim3(256), (size_t)4 * 2 * slot, s, d, nrows,
-                         partials, slot);
+      hipLaunchKernelGGL((filter_multi_t_kernel<NC, WM, 2, MODE>), dim3(grid), dim3(256), (size_t)4 * 2 * slot, s, d,
+                         nrows, partials, slot);
   }
 }
+template <int NC, int WM>
+void FmtLaunch(const FilterMultiDesc &d, int mode, int64_t nrows, AggPartial *partials, int slot, int grid, int dp,
+               hipStream_t s) {
+  if (mode == 0) FmtLaunchM<NC, WM, 0>(d, nrows, partials, slot, grid, dp, s);
+  else if (mode == 1) FmtLaunchM<NC, WM, 1>(d, nrows, partials, slot, grid, dp, s);
+  else if (mode == 3) FmtLaunchM<NC, WM, 3>(d, nrows, partials, slot, grid, dp, s);
+  else FmtLaunchM<NC, WM, 2>(d, nrows, partials, slot, grid, dp, s);
+}
 template <int NC, int WM = 0>
-void FmtDispatch(const FilterMultiDesc &d, int wm, int64_t nrows, AggPartial *partials, int slot, int grid, int dp,
-                 hipStream_t s) {
+void FmtDispatch(const FilterMultiDesc &d, int wm, int mode, int64_t nrows, AggPartial *partials, int slot, int grid,
+                 int dp, hipStream_t s) {
   if constexpr (WM < (1 << NC)) {
-    if (wm == WM) return FmtLaunch<NC, WM>(d, nrows, partials, slot, grid, dp, s);
-    FmtDispatch<NC, WM + 1>(d, wm, nrows, partials, slot, grid, dp, s);
+    if (wm == WM) return FmtLaunch<NC, WM>(d, mode, nrows, partials, slot, grid, dp, s);
+    FmtDispatch<NC, WM + 1>(d, wm, mode, nrows, partials, slot, grid, dp, s);
   }
 }
 }  // namespace
@@ -985,16 +1002,17 @@ int FilterMultiPartials(const FilterMultiDesc &d_in, int64_t nrows, AggPartial *
     }
   }
   slot = (slot + 15) & ~15;
-  // 3 blocks per CU: 3.39 ms vs 3.79 at 2 for 1e9 rows of (x i64, k i32,
-  // v i64), equal at 1e8 (profiles/r01_filter_multi_sweep.log)
-  int gpc = 3;
-  const char *e = getenv("MBX_FM_BLOCKS_PER_CU");
-  if (e && *e) gpc = atoi(e);
-  int grid = NumCUs() * (gpc > 0 ? gpc : 3);
-  int64_t need = (nrows >> 8) / 4 + 1;
-  if (grid > need) grid = (int)need;
-  if (grid > kMaxAggPartials) grid = kMaxAggPartials;
-  {
+  // MBX_FM_DEPTH=<2..4>: ring depth for 3..5 loads per step (sweeps)
+  int dp = 2;
+  if (const char *ed = getenv("MBX_FM_DEPTH")) dp = atoi(ed) >= 2 && atoi(ed) <= 4 ? atoi(ed) : 2;
+  const char *ev = getenv("MBX_FM_VARIANT");
+  const bool templ = !(ev && strcmp(ev, "generic") == 0) && d.ncol >= 1 && d.ncol <= 4 && (dp == 2 || dp == 3);
+  int grid = 0;
+  auto plan = [&](int gpc) {
+    grid = NumCUs() * gpc;
+    int64_t need = (nrows >> 8) / 4 + 1;
+    if (grid > need) grid = (int)need;
+    if (grid > kMaxAggPartials) grid = kMaxAggPartials;
     // a lane sees at most (ceil(steps / waves) + 1) x 4 rows, tail included
     const int64_t waves = (int64_t)grid * 4, steps = nrows >> 8;
     const unsigned __int128 rows_per_lane = (unsigned __int128)(((steps + waves - 1) / waves + 1) * 4);
@@ -1002,29 +1020,51 @@ int FilterMultiPartials(const FilterMultiDesc &d_in, int64_t nrows, AggPartial *
                (unsigned __int128)d.maxabs * rows_per_lane < ((unsigned __int128)1 << 63);
     const char *e32 = getenv("MBX_FA_MM32");
     d.mm32 = d.mm && d.narrow && d.maxabs < ((uint64_t)1 << 31) && !(e32 && e32[0] == '0');
+  };
+  auto mode_of = [&] { return d.agg < 0 ? 0 : (!d.mm && d.narrow) ? 1 : (d.mm32 && d.narrow) ? 3 : 2; };
+  // Workgroups per CU: the generic kernel 3 (3.39 ms vs 3.79 at 2 for 1e9
+  // rows of (x i64, k i32, v i64), profiles/r01_filter_multi_sweep.log); the
+  // templated one 1 for its compile-time modes (COUNT, narrow SUM, narrow SUM
+  // + int32 MIN/MAX) and 3 for the general mode and one-column SUMs
+  // (profiles/r02_filter_multi_modes.log).
+  const char *e = getenv("MBX_FM_BLOCKS_PER_CU");
+  const int gpc_env = e && *e ? atoi(e) : 0;
+  if (gpc_env > 0) {
+    plan(gpc_env);
+  } else if (!templ) {
+    plan(3);
+  } else {
+    plan(1);
+    const int m1 = mode_of();
+    if (m1 == 2 || (m1 == 1 && d.ncol == 1)) plan(3);
   }
 #define FM(L, DP)                                                                                            \
   hipLaunchKernelGGL((filter_multi_lds_kernel<L, DP>), dim3(grid), dim3(256), (size_t)4 * DP * slot, s, d, nrows, \
                      partials, slot)
-  // MBX_FM_DEPTH=<2..4>: ring depth for 3..5 loads per step (sweeps)
-  int dp = 2;
-  if (const char *ed = getenv("MBX_FM_DEPTH")) dp = atoi(ed) >= 2 && atoi(ed) <= 4 ? atoi(ed) : 2;
   // the templated kernel (MBX_FM_VARIANT=generic keeps the one below)
-  {
-    const char *ev = getenv("MBX_FM_VARIANT");
-    if (!(ev && strcmp(ev, "generic") == 0) && d.ncol >= 1 && d.ncol <= 4 && (dp == 2 || dp == 3)) {
-      int wm = 0;
-      for (int c = 0; c < d.ncol; c++)
-        if (d.col[c].phys == P_I64) wm |= 1 << c;
-      switch (d.ncol) {
-        case 1: FmtDispatch<1>(d, wm, nrows, partials, slot, grid, dp, s); break;
-        case 2: FmtDispatch<2>(d, wm, nrows, partials, slot, grid, dp, s); break;
-        case 3: FmtDispatch<3>(d, wm, nrows, partials, slot, grid, dp, s); break;
-        default: FmtDispatch<4>(d, wm, nrows, partials, slot, grid, dp, s); break;
-      }
-      CHECK_LAUNCH();
-      return grid;
+  if (templ) {
+    FilterMultiDesc t = d;  // aggregated column first; non-predicates always true
+    if (t.agg > 0) {
+      std::swap(t.col[0], t.col[t.agg]);
+      t.agg = 0;
     }
+    for (int c = 0; c < t.ncol; c++)
+      if (!t.col[c].is_pred) {
+        t.col[c].lo = INT64_MIN;
+        t.col[c].span = ~0ull;
+      }
+    const int mode = mode_of();
+    int wm = 0;
+    for (int c = 0; c < t.ncol; c++)
+      if (t.col[c].phys == P_I64) wm |= 1 << c;
+    switch (t.ncol) {
+      case 1: FmtDispatch<1>(t, wm, mode, nrows, partials, slot, grid, dp, s); break;
+      case 2: FmtDispatch<2>(t, wm, mode, nrows, partials, slot, grid, dp, s); break;
+      case 3: FmtDispatch<3>(t, wm, mode, nrows, partials, slot, grid, dp, s); break;
+      default: FmtDispatch<4>(t, wm, mode, nrows, partials, slot, grid, dp, s); break;
+    }
+    CHECK_LAUNCH();
+    return grid;
   }
 #define FMD(L) \
   if (dp == 2) FM(L, 2); else if (dp == 3) FM(L, 3); else FM(L, 4);

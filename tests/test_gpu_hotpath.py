@@ -487,7 +487,9 @@ def test_filter_multi_parity(mbx, oracle):
             v = oracle.synth_i64(n, 9, 0, 2**40, -2**39)
             q(c, "DROP TABLE IF EXISTS fm")
             q(c, f"CREATE TABLE fm AS SELECT mbx_synth(42, i, 50) + 1 AS x, CAST(mbx_synth(7, i, 32) AS INTEGER) AS k, "
-                 f"mbx_synth(9, i, 1099511627776) - 549755813888 AS v FROM range({n}) tbl(i)")
+                 f"mbx_synth(9, i, 1099511627776) - 549755813888 AS v, "
+                 f"(mbx_synth(9, i, 1099511627776) - 549755813888) * 4194304 AS w FROM range({n}) tbl(i)")
+            w = v.astype(object) * 4194304  # |w| < 2^61: the int64 SUM would overflow -> int128 mode
             cases = [("x > 24 AND k < 16", (x > 24) & (k < 16), "v"),
                      ("x BETWEEN 5 AND 30 AND k >= 3 AND v > 0", (x >= 5) & (x <= 30) & (k >= 3) & (v > 0), "v"),
                      ("k = 7 AND x < 40", (k == 7) & (x < 40), "x"),
@@ -508,6 +510,14 @@ def test_filter_multi_parity(mbx, oracle):
                 if n >= 256:
                     names = [kk["name"] for kk in c.last_profile()["kernels"]]
                     assert "filter_multi" in names, (where, names)
+            # SUM without MIN/MAX: int64 accumulation (narrow) and int128 (w), agg column not first
+            for col, vals in (("v", v.astype(object)), ("w", w), ("x", x.astype(object))):
+                for where, m in (("x > 24 AND k < 16", (x > 24) & (k < 16)), ("k >= 3 AND x <= 30", (k >= 3) & (x <= 30))):
+                    got = one(c, f"SELECT COUNT(*), SUM({col}) FROM fm WHERE {where}")
+                    assert int(got[0]) == int(m.sum()), (n, col, where)
+                    assert got[1] == (str(sum(vals[m])) if m.sum() else ""), (n, col, where)
+                    if n >= 256:
+                        assert "filter_multi" in [kk["name"] for kk in c.last_profile()["kernels"]]
     finally:
         c.close()
 

@@ -126,6 +126,52 @@ __global__ __launch_bounds__(WAVES * 64) void two_stream_w(const int *__restrict
   if (acc == 0x5a5a5a5a5a5aLL) atomicAdd(out, 1ull);
 }
 
+// pure three-array stream of filter_multi's shape (x int64 2 KiB + k int32 1 KiB
+// + v int64 2 KiB per 256-row step): the ceiling for that kernel
+template <int DEPTH, int WAVES>
+__global__ __launch_bounds__(WAVES * 64) void three_stream_w(const long long *__restrict__ xs, const int *__restrict__ keys,
+                                                            const long long *__restrict__ vals, long long nsteps,
+                                                            unsigned long long *out) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
+  constexpr int SB = 5120;
+  const int t = threadIdx.x, w = t >> 6, lane = t & 63;
+  unsigned char *ring = lds + w * DEPTH * SB;
+  const long long nw = (long long)gridDim.x * WAVES;
+  long long st = (long long)blockIdx.x * WAVES + w;
+  auto issue = [&](long long q, int d) {
+    unsigned char *dst = ring + d * SB;
+    const unsigned char *xp = (const unsigned char *)xs + q * 2048;
+    const unsigned char *kp = (const unsigned char *)keys + q * 1024;
+    const unsigned char *vp = (const unsigned char *)vals + q * 2048;
+    __builtin_amdgcn_global_load_lds((const void *)(xp + lane * 16), (void *)dst, 16, 0, 2);
+    __builtin_amdgcn_global_load_lds((const void *)(xp + 1024 + lane * 16), (void *)(dst + 1024), 16, 0, 2);
+    __builtin_amdgcn_global_load_lds((const void *)(kp + lane * 16), (void *)(dst + 2048), 16, 0, 2);
+    __builtin_amdgcn_global_load_lds((const void *)(vp + lane * 16), (void *)(dst + 3072), 16, 0, 2);
+    __builtin_amdgcn_global_load_lds((const void *)(vp + 1024 + lane * 16), (void *)(dst + 4096), 16, 0, 2);
+  };
+#pragma unroll
+  for (int d = 0; d < DEPTH; d++) {
+    long long q = st + d * nw;
+    issue(q < nsteps ? q : 0, d);
+  }
+  long long acc = 0;
+  int k = 0;
+  for (; st < nsteps; st += nw) {
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(5 * (DEPTH - 1)) : "memory");
+    const unsigned char *src = ring + k * SB;
+    v2i64 a0 = *(const v2i64 *)(src + lane * 32);
+    v4i32 kv = *(const v4i32 *)(src + 2048 + lane * 16);
+    v2i64 b0 = *(const v2i64 *)(src + 3072 + lane * 32);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    long long q = st + DEPTH * nw;
+    issue(q < nsteps ? q : st, k);
+    acc += a0.x + kv.x + b0.x;
+    k = k + 1 == DEPTH ? 0 : k + 1;
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  if (acc == 0x5a5a5a5a5a5aLL) atomicAdd(out, 1ull);
+}
+
 // the same bytes as ONE array: 3 KiB contiguous per step
 template <int DEPTH>
 __global__ __launch_bounds__(256) void one_stream(const unsigned char *__restrict__ in, long long nsteps,
@@ -419,6 +465,21 @@ int main(int argc, char **argv) {
     float ms = TimeIt([&] { hipLaunchKernelGGL((two_stream_w<D, W, A>), dim3(cus * (G)), dim3((W) * 64), lds, 0, k, v, nsteps, out); }, 15); \
     printf("w%d aux%d ", W, A);                                                                               \
     report("two/none", D, G, ms);                                                                             \
+  }
+#define RUN3(D, W, G)                                                                                         \
+  {                                                                                                           \
+    size_t lds = (W) * (D) * 5120;                                                                            \
+    CK(hipFuncSetAttribute((const void *)three_stream_w<D, W>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds)); \
+    float ms = TimeIt([&] { hipLaunchKernelGGL((three_stream_w<D, W>), dim3(cus * (G)), dim3((W) * 64), lds, 0, x3, k, v, nsteps, out); }, 15); \
+    printf("three w%d d%d g%d  %.4f ms  %.0f GB/s\n", W, D, G, ms, 20e9 * ((double)nsteps * 256 / 1e9) / (ms * 1e6)); \
+  }
+  if (argc > 2 && argv[2][0] == '3') {  // round 2: the filter_multi shape (x i64, k i32, v i64)
+    long long *x3;
+    CK(hipMalloc((void **)&x3, (size_t)nsteps * 2048));
+    CK(hipMemset(x3, 1, (size_t)nsteps * 2048));
+    RUN3(2, 4, 1) RUN3(3, 4, 1) RUN3(4, 4, 1) RUN3(2, 4, 2) RUN3(3, 4, 2) RUN3(2, 4, 3) RUN3(3, 4, 3)
+    RUN3(2, 8, 1) RUN3(3, 8, 1) RUN3(2, 4, 1) RUN3(2, 4, 3)
+    return 0;
   }
   if (argc > 2 && argv[2][0] == 'w') {  // round 2: waves per block and cache policy of the pure stream
     RUNW(2, 4, 2, 1) RUNW(2, 4, 0, 1) RUNW(3, 4, 2, 1) RUNW(2, 8, 2, 1) RUNW(2, 8, 0, 1) RUNW(3, 8, 2, 1)

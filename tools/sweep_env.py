@@ -22,6 +22,8 @@ SQL = {
     "c3": "SELECT k, SUM(v), COUNT(*) FROM t GROUP BY k",
     "c5": "SELECT COUNT(*), SUM(x) FROM t WHERE x > 24",
     "filter_mm": "SELECT COUNT(*), SUM(x), MIN(x), MAX(x) FROM t WHERE x > 24 AND k < 16",
+    "filter_cnt2": "SELECT COUNT(*) FROM t WHERE x > 24 AND k < 16",
+    "filter_wide": "SELECT COUNT(*), SUM(v), MIN(v), MAX(v) FROM t WHERE x > 24 AND k < 16",
     # NULLABLE=1
     "c2n": "SELECT COUNT(*) FROM t WHERE xn > 24",
     "c5n": "SELECT COUNT(*), SUM(xn) FROM t WHERE xn > 24",
