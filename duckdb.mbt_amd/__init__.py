@@ -79,6 +79,7 @@ _sig("duckdb_mbx_result_text", ctypes.c_void_p, _P, ctypes.POINTER(ctypes.c_int6
 _sig("duckdb_mbx_append_column", _I, _P, _I, _P, _P, _L)
 _sig("duckdb_mbx_append_commit", _I, _P, _L)
 _sig("duckdb_mbx_hbm_calibrate", _I, _P, _L, _I, ctypes.POINTER(ctypes.c_double))
+_sig("duckdb_mbx_hbm_calibrate_ex", _I, _P, _L, _I, ctypes.POINTER(ctypes.c_double), _I)
 _sig("duckdb_mbx_statement_plan_stats", _I, _P, ctypes.POINTER(ctypes.c_int64))
 
 for _n in ["duckdb_mb_connect"]:
@@ -572,10 +573,12 @@ class Connection:
         return json.loads(s)
 
     def hbm_calibrate(self, nbytes: int = 2 << 30, iters: int = 5) -> dict:
-        out = (ctypes.c_double * 3)()
-        if not lib.duckdb_mbx_hbm_calibrate(self._h, nbytes, iters, out):
+        """This device's measured HBM ceilings (GB/s; a copy counts read + write)."""
+        out = (ctypes.c_double * 7)()
+        if lib.duckdb_mbx_hbm_calibrate_ex(self._h, nbytes, iters, out, 7) != 7:
             raise DuckDBError(_last_error("hbm_calibrate failed"))
-        return {"copy_gbs": out[0], "read_nt_gbs": out[1], "read_gbs": out[2], "bytes": nbytes}
+        return {"copy_gbs": out[0], "read_nt_gbs": out[1], "read_gbs": out[2], "ring_read_gbs": out[3],
+                "copy_nt4_gbs": out[4], "ring_copy_gbs": out[5], "ring_copy_half_gbs": out[6], "bytes": nbytes}
 
     def profile_drain(self) -> list:
         import json

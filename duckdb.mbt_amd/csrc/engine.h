@@ -195,6 +195,6 @@ void AppendRawColumns(Connection &c, Table &t, const std::vector<const void *> &
 // waits for in-flight appends and folds their zone-map statistics
 void SettleAppends(Connection &c);
 void HostColumnPush(HostColumn &col, const Value &v);  // v already of col.type (or NULL)
-void HbmCalibrateConn(Connection &c, int64_t bytes, int iters, double out[3]);
+void HbmCalibrateConn(Connection &c, int64_t bytes, int iters, double out[7]);
 
 }  // namespace mbx

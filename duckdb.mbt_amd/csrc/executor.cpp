@@ -3628,9 +3628,9 @@ void OpenShards(Connection &c) {
   hipSetDevice(c.engine->device);
 }
 
-void HbmCalibrateConn(Connection &c, int64_t bytes, int iters, double out[3]) {
+void HbmCalibrateConn(Connection &c, int64_t bytes, int iters, double out[7]) {
   Engine &e = Eng(c);
-  bytes &= ~(int64_t)255;
+  bytes &= ~(int64_t)1023;  // whole 1 KiB ring slots
   void *a = nullptr, *b = nullptr;
   HIPCHK(hipMalloc(&a, bytes));
   HIPCHK(hipMalloc(&b, bytes));

@@ -1306,27 +1306,120 @@ __global__ __launch_bounds__(256) void read_sum_kernel(const v2i64 *__restrict__
   if (acc == 0x123456789) atomicAdd(out, 1ull);  // keeps the loads live
 }
 
-void HbmCalibrate(void *buf_a, void *buf_b, int64_t bytes, int iters, double out[3], hipStream_t s) {
+// the read shape of the hot kernels: one workgroup of 4 waves per CU, each
+// wave an LDS-DMA ring of DEPTH x 1 KiB slots (16 B per lane, non-temporal)
+template <int DEPTH>
+__global__ __launch_bounds__(256) void ring_read_kernel(const unsigned char *__restrict__ in, int64_t nsteps,
+                                                        unsigned long long *flag) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char rr_lds[];
+  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  unsigned char *ring = rr_lds + w * DEPTH * 1024;
+  const int64_t nw = (int64_t)gridDim.x * 4;
+  int64_t st = (int64_t)blockIdx.x * 4 + w;
+  auto issue = [&](int64_t q, int d) {
+    __builtin_amdgcn_global_load_lds((const void *)(in + q * 1024 + lane * 16), (void *)(ring + d * 1024), 16, 0, 2);
+  };
+#pragma unroll
+  for (int d = 0; d < DEPTH; d++) issue(st + d * nw < nsteps ? st + d * nw : 0, d);
+  long long acc = 0;
+  int k = 0;
+  for (; st < nsteps; st += nw) {
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(DEPTH - 1) : "memory");
+    v2i64 x = *(const v2i64 *)(ring + k * 1024 + lane * 16);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    const int64_t q = st + DEPTH * nw;
+    issue(q < nsteps ? q : st, k);
+    acc += x.x ^ x.y;
+    k = k + 1 == DEPTH ? 0 : k + 1;
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  if (acc == 0x123456789) atomicAdd(flag, 1ull);
+}
+
+// 16-B copy with 4 independent loads in flight per lane, non-temporal both ways
+__global__ __launch_bounds__(256) void copy_nt4_kernel(const v4i32 *__restrict__ in, v4i32 *__restrict__ out, int64_t n) {
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  for (; i + 3 * stride < n; i += 4 * stride) {
+    v4i32 a = __builtin_nontemporal_load(in + i), b = __builtin_nontemporal_load(in + i + stride);
+    v4i32 c = __builtin_nontemporal_load(in + i + 2 * stride), d = __builtin_nontemporal_load(in + i + 3 * stride);
+    __builtin_nontemporal_store(a, out + i);
+    __builtin_nontemporal_store(b, out + i + stride);
+    __builtin_nontemporal_store(c, out + i + 2 * stride);
+    __builtin_nontemporal_store(d, out + i + 3 * stride);
+  }
+  for (; i < n; i += stride) out[i] = in[i];
+}
+
+// the same ring with every slot written back out (non-temporal 16-B stores):
+// the copy shape of the materialising kernels.  Stores count in vmcnt too, so
+// the wait allows the DEPTH-1 younger loads and as many stores.
+// HALF: only lanes 0..31 store, packed (512 B per 1 KiB read): the 2:1
+// read:write mix of a compaction at ~50 % selectivity
+template <int DEPTH, bool HALF>
+__global__ __launch_bounds__(256) void ring_copy_kernel(const unsigned char *__restrict__ in, unsigned char *__restrict__ out,
+                                                        int64_t nsteps) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char rc_lds[];
+  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  unsigned char *ring = rc_lds + w * DEPTH * 1024;
+  const int64_t nw = (int64_t)gridDim.x * 4;
+  int64_t st = (int64_t)blockIdx.x * 4 + w;
+  auto issue = [&](int64_t q, int d) {
+    __builtin_amdgcn_global_load_lds((const void *)(in + q * 1024 + lane * 16), (void *)(ring + d * 1024), 16, 0, 2);
+  };
+#pragma unroll
+  for (int d = 0; d < DEPTH; d++) issue(st + d * nw < nsteps ? st + d * nw : 0, d);
+  int k = 0;
+  for (; st < nsteps; st += nw) {
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * (DEPTH - 1)) : "memory");
+    v4i32 x = *(const v4i32 *)(ring + k * 1024 + lane * 16);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    const int64_t q = st + DEPTH * nw;
+    issue(q < nsteps ? q : st, k);
+    if (!HALF) __builtin_nontemporal_store(x, (v4i32 *)(out + st * 1024 + lane * 16));
+    else if (lane < 32) __builtin_nontemporal_store(x, (v4i32 *)(out + st * 512 + lane * 16));
+    k = k + 1 == DEPTH ? 0 : k + 1;
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
+
+// out: [0] float4 copy, [1] non-temporal int64 read, [2] plain read, [3] the
+// hot kernels' LDS-DMA ring read, [4] unrolled non-temporal 16-B copy, [5] the
+// LDS-DMA ring copy, [6] the ring copy writing half of what it reads (GB/s;
+// a copy counts its read and its write)
+void HbmCalibrate(void *buf_a, void *buf_b, int64_t bytes, int iters, double out[7], hipStream_t s) {
   hipEvent_t e0, e1;
   (void)hipEventCreate(&e0);
   (void)hipEventCreate(&e1);
   unsigned long long *flag = (unsigned long long *)buf_b;
   int64_t n16 = bytes / 16;
   int grid = NumCUs() * 8;
-  for (int k = 0; k < 3; k++) {
+  const int64_t nsteps = bytes / 1024;
+  for (int k = 0; k < 7; k++) {
     float best = 1e30f;
     for (int it = 0; it < iters + 1; it++) {
       (void)hipEventRecord(e0, s);
       if (k == 0) hipLaunchKernelGGL(copy_kernel, dim3(grid), dim3(256), 0, s, (const float4 *)buf_a, (float4 *)buf_b, n16);
       else if (k == 1) hipLaunchKernelGGL(read_sum_kernel<true>, dim3(grid), dim3(256), 0, s, (const v2i64 *)buf_a, n16, flag);
-      else hipLaunchKernelGGL(read_sum_kernel<false>, dim3(grid), dim3(256), 0, s, (const v2i64 *)buf_a, n16, flag);
+      else if (k == 2) hipLaunchKernelGGL(read_sum_kernel<false>, dim3(grid), dim3(256), 0, s, (const v2i64 *)buf_a, n16, flag);
+      else if (k == 3)
+        hipLaunchKernelGGL(ring_read_kernel<6>, dim3(NumCUs()), dim3(256), 4 * 6 * 1024, s, (const unsigned char *)buf_a,
+                           nsteps, flag);
+      else if (k == 4)
+        hipLaunchKernelGGL(copy_nt4_kernel, dim3(grid), dim3(256), 0, s, (const v4i32 *)buf_a, (v4i32 *)buf_b, n16);
+      else if (k == 5)
+        hipLaunchKernelGGL((ring_copy_kernel<6, false>), dim3(NumCUs()), dim3(256), 4 * 6 * 1024, s,
+                           (const unsigned char *)buf_a, (unsigned char *)buf_b, nsteps);
+      else
+        hipLaunchKernelGGL((ring_copy_kernel<6, true>), dim3(NumCUs()), dim3(256), 4 * 6 * 1024, s,
+                           (const unsigned char *)buf_a, (unsigned char *)buf_b, nsteps);
       (void)hipEventRecord(e1, s);
       (void)hipEventSynchronize(e1);
       float ms = 0;
       (void)hipEventElapsedTime(&ms, e0, e1);
       if (it > 0 && ms < best) best = ms;  // first launch is a warm-up
     }
-    double moved = (k == 0 ? 2.0 : 1.0) * (double)bytes;
+    double moved = (k == 6 ? 1.5 : k == 0 || k >= 4 ? 2.0 : 1.0) * (double)bytes;
     out[k] = moved / (best * 1e-3) / 1e9;
   }
   (void)hipEventDestroy(e0);

@@ -1567,15 +1567,21 @@ char *duckdb_mbx_jit_selftest(void) {
   return out;
 }
 
-int32_t duckdb_mbx_hbm_calibrate(duckdb_mb_connection *h, int64_t bytes, int32_t iters, double *out3) {
-  if (!h || !out3) return 0;
+int32_t duckdb_mbx_hbm_calibrate_ex(duckdb_mb_connection *h, int64_t bytes, int32_t iters, double *out, int32_t nout) {
+  if (!h || !out || nout <= 0) return 0;
   try {
-    HbmCalibrateConn(h->conn, bytes, iters, out3);
-    return 1;
+    double all[7] = {0, 0, 0, 0, 0, 0, 0};
+    HbmCalibrateConn(h->conn, bytes, iters, all);
+    const int k = nout < 7 ? nout : 7;
+    for (int i = 0; i < k; i++) out[i] = all[i];
+    return k;
   } catch (std::exception &e) {
     SetError(e.what());
     return 0;
   }
+}
+int32_t duckdb_mbx_hbm_calibrate(duckdb_mb_connection *h, int64_t bytes, int32_t iters, double *out3) {
+  return duckdb_mbx_hbm_calibrate_ex(h, bytes, iters, out3, 3) == 3 ? 1 : 0;
 }
 
 char *duckdb_mbx_last_profile(duckdb_mb_connection *h) {

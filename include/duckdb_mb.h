@@ -212,6 +212,12 @@ char *duckdb_mbx_profile_drain(duckdb_mb_connection *handle);
  * float4 copy (read+write bytes), a non-temporal int64 read and a plain int64
  * read over `bytes`-sized buffers -> out3[0..2].  Returns 1 on success. */
 int32_t duckdb_mbx_hbm_calibrate(duckdb_mb_connection *handle, int64_t bytes, int32_t iters, double *out3);
+/* the same plus the hot kernels' shapes: out[0..6] = copy, nt read, read,
+ * LDS-DMA ring read, unrolled nt copy, LDS-DMA ring copy, ring copy writing
+ * half of what it reads (GB/s; a copy counts read + write); returns how many
+ * were written (<= nout), 0 on error */
+int32_t duckdb_mbx_hbm_calibrate_ex(duckdb_mb_connection *handle, int64_t bytes, int32_t iters, double *out,
+                                    int32_t nout);
 
 /* ---- DataChunk / Vector / LogicalType (ref src/duckdb_native.c:1926-2132) ----
  * The reference wraps libduckdb's data-chunk API; these handles keep its C

@@ -689,3 +689,20 @@ def test_c3_beyond_int32_rows(mbx, oracle):
     got = q(c, "SELECT k, SUM(v), COUNT(*) FROM gbig GROUP BY k ORDER BY k").rows
     assert [(int(r[0]), int(r[1]), int(r[2])) for r in got] == [(k, osum[k], oc[k]) for k in range(32)]
     c.close()
+
+
+def test_hbm_calibrate_reports_every_shape(mbx):
+    """duckdb_mbx_hbm_calibrate_ex: the box's measured ceilings bench.py reports
+    beside the 8 TB/s spec; every shape runs and lands in a sane
+    range, and the 3-value entry agrees on the first three slots' meaning."""
+    import ctypes
+    c = mbx.connect().value
+    cal = c.hbm_calibrate(1 << 28, 2)
+    for k in ("copy_gbs", "read_nt_gbs", "read_gbs", "ring_read_gbs", "copy_nt4_gbs", "ring_copy_gbs",
+              "ring_copy_half_gbs"):
+        assert 100.0 < cal[k] < 9000.0, (k, cal)
+    out3 = (ctypes.c_double * 3)()
+    assert mbx.lib.duckdb_mbx_hbm_calibrate(c._h, 1 << 28, 1, out3) == 1 and all(100.0 < x < 9000.0 for x in out3)
+    out2 = (ctypes.c_double * 2)()
+    assert mbx.lib.duckdb_mbx_hbm_calibrate_ex(c._h, 1 << 28, 1, out2, 2) == 2
+    c.close()
