@@ -10,3 +10,6 @@ timeout -k 10 300 python bench.py --config sel > gpurun_out/round/bench_sel.json
 cd /tmp && export TMPDIR=/tmp
 timeout -k 10 240 rocprofv3 --kernel-trace --stats -d /root/repo/gpurun_out/round/prof/c2 -o c2 -- python3 /root/repo/bench.py --steps 10 --no-cpu > /root/repo/gpurun_out/round/prof_c2.log 2>&1 || exit 16
 timeout -k 10 240 rocprofv3 --kernel-trace --stats -d /root/repo/gpurun_out/round/prof/c3 -o c3 -- python3 /root/repo/bench.py --config c3 --steps 10 --no-cpu > /root/repo/gpurun_out/round/prof_c3.log 2>&1 || exit 17
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d /root/repo/gpurun_out/round/prof/sel -o sel -- python3 /root/repo/bench.py --config sel --steps 10 --no-cpu > /root/repo/gpurun_out/round/prof_sel.log 2>&1 || exit 18
+cd /root/repo
+timeout -k 10 400 python bench.py --config c4 > gpurun_out/round/bench_c4.json 2> gpurun_out/round/bench_c4.err || exit 19
