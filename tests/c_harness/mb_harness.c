@@ -393,10 +393,43 @@ static int c4_bench(duckdb_mb_connection *c, long rows, int chunks) {
     duckdb_mb_arrow_destroy(ar);
   }
   CHECK(checked == rows && bad == 0, "c4 read-back: %ld rows checked, %ld mismatches", checked, bad);
+  /* the query_stream leg (ref duckdb_native.mbt:504-582: per-cell strings of
+   * <= 2048-row chunks) over a bounded prefix: every cell pulled and parsed as
+   * the MoonBit driver would, each value checked */
+  const long srows = rows < 10000000 ? rows : 10000000;
+  char q[160];
+  snprintf(q, sizeof q, "SELECT v FROM c4 LIMIT %ld", srows);
+  sql = S(q);
+  t0 = now_s();
+  duckdb_mb_stream *st = duckdb_mb_query_stream(c, sql);
+  mb_free(sql);
+  CHECK(st != NULL, "c4 stream: %s", take(duckdb_mb_last_error()));
+  long sgot = 0, sbad = 0;
+  while (st) {
+    duckdb_mb_chunk *ch = duckdb_mb_stream_fetch_chunk(st);
+    if (!ch) break;
+    const int32_t nr = duckdb_mb_chunk_row_count(ch);
+    for (int32_t i = 0; i < nr; i++) {
+      moonbit_bytes_t v = duckdb_mb_chunk_value(ch, 0, i);
+      char buf[32];
+      const int32_t n = mb_len(v) < 31 ? mb_len(v) : 31;
+      memcpy(buf, v, (size_t)n);
+      buf[n] = 0;
+      sbad += strtoll(buf, NULL, 10) != c4_value(sgot + i);
+      mb_free(v);
+    }
+    sgot += nr;
+    duckdb_mb_chunk_destroy(ch);
+  }
+  if (st) duckdb_mb_stream_destroy(st);
+  const double t_st = now_s() - t0;
+  CHECK(sgot == srows && sbad == 0, "c4 stream: %ld rows, %ld mismatches", sgot, sbad);
   printf("{\"rows\": %ld, \"ingest_api\": \"%s\", \"ingest_s\": %.6f, \"ingest_rows_per_s\": %.1f, "
-         "\"ingest_gbs\": %.3f, \"readback_s\": %.6f, \"readback_gbs\": %.3f, \"bit_exact\": %s}\n",
+         "\"ingest_gbs\": %.3f, \"readback_s\": %.6f, \"readback_gbs\": %.3f, \"stream_rows\": %ld, "
+         "\"stream_s\": %.6f, \"stream_rows_per_s\": %.1f, \"bit_exact\": %s}\n",
          rows, chunks ? "append_data_chunk" : "begin_row/append_bigint/end_row", t_in, rows / t_in,
-         rows * 8.0 / t_in / 1e9, t_out, rows * 8.0 / t_out / 1e9, (checked == rows && bad == 0) ? "true" : "false");
+         rows * 8.0 / t_in / 1e9, t_out, rows * 8.0 / t_out / 1e9, sgot, t_st, sgot / t_st,
+         (checked == rows && bad == 0 && sgot == srows && sbad == 0) ? "true" : "false");
   return 0;
 }
 

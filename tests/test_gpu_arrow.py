@@ -268,3 +268,38 @@ def test_arrow_host_link_copies_exact(mbx, monkeypatch, link, n):
         assert text[n // 2] == str((n // 2) * 7 - 11).encode()
     a.close()
     c.close()
+
+
+def test_arrow_host_link_concurrent_connections(mbx):
+    """Two host threads pull >= 32 MiB getter buffers at once through two
+    connections on the same device: the device's host-link pool serves one
+    copy at a time and both results stay exact (ctypes drops the GIL, so the
+    getters really overlap)."""
+    import threading
+    import numpy as np
+    n = 5_000_003  # 40 MB of int64: above the pool's 32 MiB threshold
+    conns = [mbx.connect().value for _ in range(2)]
+    for j, c in enumerate(conns):
+        assert isinstance(c.query(f"CREATE TABLE hc AS SELECT i * {j + 3} + 1 AS b FROM range({n}) tbl(i)"), mbx.Ok)
+    errs = []
+
+    def pull(j):
+        try:
+            for _ in range(3):
+                a = conns[j].query_arrow("SELECT b FROM hc").value
+                raw = mbx._take(mbx.lib.duckdb_mb_arrow_get_column_int64(a._h, 0))
+                a.close()
+                got = np.frombuffer(raw, dtype=np.int64, offset=4, count=n)
+                if not np.array_equal(got, np.arange(n, dtype=np.int64) * (j + 3) + 1):
+                    errs.append(f"connection {j}: values differ")
+        except Exception as e:  # noqa: BLE001 - reported below
+            errs.append(f"connection {j}: {e!r}")
+
+    th = [threading.Thread(target=pull, args=(j,)) for j in range(2)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join(timeout=120)
+    assert not errs, errs
+    for c in conns:
+        c.close()
