@@ -345,9 +345,11 @@ struct SelectDesc {
     int32_t narrow;   // select_rounds: an 8-byte column whose values fit int32 (zone map) is staged as int32
     int64_t lo;
     uint64_t span;
+    const uint64_t *valid;  // select_rounds: validity words (NULL fails a predicate; outputs carry it), or nullptr
   } col[SL_MAX_COL];
   int32_t out_col[SL_MAX_OUT];  // index into col[]
   void *dst[SL_MAX_OUT];
+  uint8_t *vdst[SL_MAX_OUT];  // select_rounds: one validity byte per output row of a NULL-able output, or nullptr
   unsigned long long *dbg;     // nullptr, or 9 counters (MBX_SL_DEBUG) / 13 (MBX_SR_DEBUG)
   unsigned long long *dbg_ts;  // MBX_SR_DEBUG=2: s_memrealtime of every (round, workgroup) publish
 };
@@ -367,6 +369,7 @@ void SelectCompact(const SelectDesc &d, int64_t nrows, void *status_buf, int64_t
 struct SelectRoundsPlan {
   bool ok;
   int nc, wm, ni, depth, S, H, NL, stg, G, sleep, test_stall, pw;  // wm: bit c = column c is 8 bytes; H: 256-row sub-steps per step
+  int nv;  // loaded columns with validity words (their 32 B per step ride a second ring)
   int64_t nrounds;
   size_t lds;
 };
@@ -374,6 +377,8 @@ SelectRoundsPlan PlanSelectRounds(const SelectDesc &d, int64_t nrows);
 size_t SelectRoundsCtlBytes(const SelectRoundsPlan &p);
 void SelectRounds(const SelectDesc &d, const SelectRoundsPlan &p, int64_t nrows, unsigned long long *ctl,
                   uint32_t epoch, hipStream_t s);
+// bits[i / 64] bit i % 64 = bytes[i] (0/1), for the n output rows of a NULL-able select_rounds output
+void PackValidityBytes(const uint8_t *bytes, int64_t n, uint64_t *bits, hipStream_t s);
 
 }  // namespace dev
 }  // namespace mbx

@@ -1021,9 +1021,11 @@ static bool FastIntCol(const DRel &rel, int c) {
   return d.validity == nullptr && (d.phys == P_I32 || d.phys == P_I64) && d.data != nullptr;
 }
 
-// One-pass forms of the compaction below, for NULL-free 4/8-byte columns, at
-// most SL_MAX_COL distinct loaded columns (predicates ∪ outputs) and
-// SL_MAX_OUT outputs.  Each loaded column is read from HBM once; outputs are
+// One-pass forms of the compaction below, for 4/8-byte columns, at most
+// SL_MAX_COL distinct loaded columns (predicates ∪ outputs) and SL_MAX_OUT
+// outputs.  NULL-able columns take the round-synchronous form only: a NULL
+// fails a predicate, and a NULL-able output's validity comes back as one byte
+// per output row, packed into its bitmap afterwards (dev::PackValidityBytes).  Each loaded column is read from HBM once; outputs are
 // allocated for every row (the count is known only afterwards), so the form
 // is used while that upper bound stays under MBX_SL_MAX_GB (default 64).
 //  * default (n >= MBX_SR_MIN_ROWS, default 2^22): dev::SelectRounds, the
@@ -1056,10 +1058,13 @@ static bool TrySelectOnePass(Engine &e, const DRel &rel, const dev::FilterMultiD
     S.col[S.ncol].w = w;
     return S.ncol++;
   };
+  bool any_valid = false;
   for (int j = 0; j < F.ncol; j++) {
-    if (F.col[j].valid) return false;
+    if (F.col[j].valid && (mode == 2 || (uintptr_t)F.col[j].valid % 16)) return false;
     const int i = slot_of(F.col[j].data, F.col[j].phys == P_I64 ? 8 : 4);
     if (i < 0) return false;
+    S.col[i].valid = F.col[j].valid;
+    any_valid |= F.col[j].valid != nullptr;
     S.col[i].is_pred = 1;
     S.col[i].lo = F.col[j].lo;
     S.col[i].span = F.col[j].span;
@@ -1069,18 +1074,24 @@ static bool TrySelectOnePass(Engine &e, const DRel &rel, const dev::FilterMultiD
   const bool narrow_ok = !(nenv && atoi(nenv) == 0);
   for (auto &x : exprs) {
     const DCol &c = rel.cols[x->col];
-    if (c.validity) return false;
+    if (c.validity && (mode == 2 || (uintptr_t)c.validity % 16)) return false;
     const int w = PhysSize(c.phys);
     if (w != 4 && w != 8) return false;
     const int i = slot_of(c.data, w);
     if (i < 0) return false;
+    S.col[i].valid = c.validity;
+    any_valid |= c.validity != nullptr;
     S.out_col[S.nout++] = i;
-    out_bytes += (double)rel.n * w;
-    // an INT64 table column whose zone map fits int32 is staged in 4 bytes
+    out_bytes += (double)rel.n * (w + (c.validity ? 1 : 0));
+    // an INT64 table column whose zone map fits int32 is staged in 4 bytes (the
+    // map covers the valid rows; a NULL row's staged value is never read)
     const DevColumn *tc = c.table_col;
-    if (narrow_ok && w == 8 && tc && tc->stats_valid && tc->null_count == 0 && tc->imin >= (i128)INT32_MIN &&
-        tc->imax <= (i128)INT32_MAX)
+    if (narrow_ok && w == 8 && tc && tc->stats_valid && tc->imin >= (i128)INT32_MIN && tc->imax <= (i128)INT32_MAX)
       S.col[i].narrow = 1;
+  }
+  if (any_valid) {  // MBX_SR_NULLS=0: NULL-able shapes keep the two-pass form (A/B tests)
+    const char *nv = getenv("MBX_SR_NULLS");
+    if (nv && atoi(nv) == 0) return false;
   }
   int ni = 0;
   for (int i = 0; i < S.ncol; i++) ni += S.col[i].w / 4;
@@ -1096,12 +1107,18 @@ static bool TrySelectOnePass(Engine &e, const DRel &rel, const dev::FilterMultiD
     if (!plan.ok) return false;
   }
   std::vector<DCol> cols;
+  std::vector<DevBufPtr> vbytes(exprs.size());  // NULL-able outputs: one validity byte per output row
   for (int k = 0; k < (int)exprs.size(); k++) {
-    cols.push_back(AllocOut(e, exprs[k]->type, n, false));
+    const bool nullable = rel.cols[exprs[k]->col].validity != nullptr;
+    cols.push_back(AllocOut(e, exprs[k]->type, n, nullable, false));
     S.dst[k] = cols[k].data;
+    if (nullable) {  // (released to the engine's pool when this returns: later users run after the pack on e.stream)
+      vbytes[k] = Alloc(e, (size_t)std::max<int64_t>(n, 1) + 64);
+      S.vdst[k] = (uint8_t *)vbytes[k]->p;
+    }
   }
   double bytes = 0;
-  for (int i = 0; i < S.ncol; i++) bytes += (double)n * S.col[i].w;
+  for (int i = 0; i < S.ncol; i++) bytes += (double)n * S.col[i].w + (S.col[i].valid ? n / 8.0 : 0);
   int64_t nsel = 0;
   if (mode != 2) {
     std::unique_lock<std::mutex> lk(g_rounds_mu[e.device & 63]);
@@ -1208,8 +1225,13 @@ static bool TrySelectOnePass(Engine &e, const DRel &rel, const dev::FilterMultiD
   }
   if (e.profile && !e.events.empty() && (e.events.back().name == "select" || e.events.back().name == "select_rounds")) {
     double ob = 0;
-    for (int k = 0; k < S.nout; k++) ob += (double)nsel * S.col[S.out_col[k]].w;
+    for (int k = 0; k < S.nout; k++) ob += (double)nsel * (S.col[S.out_col[k]].w + (S.vdst[k] ? 1 : 0));
     e.events.back().bytes += ob;
+  }
+  for (int k = 0; k < S.nout; k++) {
+    if (!S.vdst[k]) continue;
+    ProfScope ps(e, "pack_validity", (double)nsel + nsel / 8.0, nsel);
+    dev::PackValidityBytes(S.vdst[k], nsel, cols[k].validity, e.stream);
   }
   out = DRel();
   out.n = nsel;

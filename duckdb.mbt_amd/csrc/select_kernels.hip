@@ -432,6 +432,10 @@ __device__ __forceinline__ void lds_st(long long *p, long long v) {
 __device__ __forceinline__ void lds_st(unsigned long long *p, unsigned long long v) {
   asm volatile("ds_write_b64 %0, %1\n\ts_waitcnt lgkmcnt(0)" ::"v"(lds_addr(p)), "v"(v) : "memory");
 }
+template <int N>
+__device__ __forceinline__ void sr_wait() {
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
 __device__ __forceinline__ unsigned long long lds_add_rtn(unsigned long long *p, unsigned long long v) {
   unsigned long long old;
   asm volatile("ds_add_rtn_u64 %0, %1, %2\n\ts_waitcnt lgkmcnt(0)" : "=v"(old) : "v"(lds_addr(p)), "v"(v) : "memory");
@@ -455,10 +459,16 @@ struct SrCols {
 // chains interleave (one loader wave per SIMD cannot hide its own latencies).
 // NL loader waves (4 or 8: two per SIMD hide each other's latencies), 4
 // storers (storer s drains loaders s, s + 4, ...) and one coordinator.
-template <int NC, int WM, int DEPTH, int H, int NL>
+// VAL: some columns carry validity words (H = 1).  A step's 32 B of words per
+// NULL-able column ride a second ring (one exec-masked LDS-DMA instruction
+// each, counted exactly in the wait); a NULL fails a predicate, and a NULL-able
+// output stages one validity byte per selected row, which its storer writes to
+// D.vdst (PackValidityBytes turns those into the output's bitmap).
+template <int NC, int WM, int DEPTH, int H, int NL, bool VAL>
 __global__ __launch_bounds__((NL + 5) * 64) void select_rounds_kernel(SelectDesc D, int64_t n, int64_t nrounds, int S, int stg,
                                                             unsigned long long *ctl, uint32_t epoch, int sleep_,
                                                             int test_stall, int pwmax) {
+  static_assert(!VAL || H == 1, "validity words are laid out per 256-row step");
   typedef SrCols<NC, WM> L;
   extern __shared__ __attribute__((aligned(16))) unsigned char sr_lds[];
   __shared__ SrShared sm;
@@ -488,7 +498,21 @@ __global__ __launch_bounds__((NL + 5) * 64) void select_rounds_kernel(SelectDesc
     st8[c] = L::w(c) == 8 && !D.col[c].narrow;
     if ((smask >> c) & 1) rowb += st8[c] ? 8 : 4;
   }
-  unsigned char *stage0 = sr_lds + (size_t)NL * DEPTH * SB;
+  // NULL-able columns: slot offset of their words in the validity ring, and
+  // (staged outputs) the byte offset of their validity-byte array
+  int voff[NC], vsoff[NC];
+  bool hv[NC];
+  int nv = 0;
+#pragma unroll
+  for (int c = 0; c < NC; c++) {
+    hv[c] = VAL && D.col[c].valid != nullptr;
+    voff[c] = 32 * nv;
+    nv += hv[c];
+    vsoff[c] = rowb * (stg + 64);
+    if (hv[c] && ((smask >> c) & 1)) rowb += 1;
+  }
+  constexpr int VSB = VAL ? NC * 32 : 0;  // validity ring slot
+  unsigned char *stage0 = sr_lds + (size_t)NL * DEPTH * SB + (size_t)NL * DEPTH * VSB;
   const uint32_t mask = (uint32_t)stg - 1;
   const uint64_t lt = (1ull << lane) - 1;
 
@@ -496,6 +520,7 @@ __global__ __launch_bounds__((NL + 5) * 64) void select_rounds_kernel(SelectDesc
     // ------------------------------------------------------------ loader
     if (nrounds == 0) return;
     unsigned char *ring = sr_lds + (size_t)w * DEPTH * SB;
+    unsigned char *vring = sr_lds + (size_t)NL * DEPTH * SB + (size_t)w * DEPTH * VSB;
     unsigned char *mystage = stage0 + (size_t)w * (stg + 64) * rowb;
     const int64_t qstride = (int64_t)G * NL * S;  // steps between a wave's tiles of consecutive rounds
     const unsigned char *colp[NC];
@@ -529,6 +554,13 @@ __global__ __launch_bounds__((NL + 5) * 64) void select_rounds_kernel(SelectDesc
             __builtin_amdgcn_global_load_lds((const void *)(src + 1024), (void *)(dst + L::off(c) + 1024), 16, 0, 2);
         }
       }
+      if constexpr (VAL) {
+#pragma unroll
+        for (int c = 0; c < NC; c++)
+          if (hv[c] && lane < 2)
+            __builtin_amdgcn_global_load_lds((const void *)(D.col[c].valid + q * 4 + lane * 2),
+                                             (void *)(vring + slot * VSB + voff[c]), 16, 0, 2);
+      }
     };
 #pragma unroll
     for (int d = 0; d < DEPTH; d++) issue(d);
@@ -560,7 +592,16 @@ __global__ __launch_bounds__((NL + 5) * 64) void select_rounds_kernel(SelectDesc
       uint32_t rc = 0;
       for (int s = 0; s < S; s++) {
         if (dbg) t0 = clock64();
-        asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NI * (DEPTH - 1)) : "memory");
+        if constexpr (VAL) {
+          switch (nv) {  // wave-uniform: the exact count of the instructions issued after this slot's
+            case 1: sr_wait<(NI + 1) * (DEPTH - 1)>(); break;
+            case 2: sr_wait<(NI + 2) * (DEPTH - 1)>(); break;
+            case 3: sr_wait<(NI + 3) * (DEPTH - 1)>(); break;
+            default: sr_wait<(NI + 4) * (DEPTH - 1)>(); break;
+          }
+        } else {
+          asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NI * (DEPTH - 1)) : "memory");
+        }
         if (dbg) d_dma += clock64() - t0;
         const unsigned char *src = ring + k * SB;
         int64_t v[H][NC][4];
@@ -568,6 +609,17 @@ __global__ __launch_bounds__((NL + 5) * 64) void select_rounds_kernel(SelectDesc
         for (int h = 0; h < H; h++)
 #pragma unroll
           for (int c = 0; c < NC; c++) sl_read4(src + h * SB1 + L::off(c), L::w(c), lane, v[h][c]);
+        // validity of rows 4 lane .. 4 lane + 3 per column (bit e), all valid without words
+        uint32_t vmc[NC];
+#pragma unroll
+        for (int c = 0; c < NC; c++) {
+          vmc[c] = 0xFu;
+          if constexpr (VAL) {
+            if (hv[c])
+              vmc[c] = (uint32_t)(*(const uint64_t *)(vring + k * VSB + voff[c] + (lane >> 4) * 8) >> (4 * (lane & 15))) &
+                       0xFu;
+          }
+        }
         // ok[h][e]: row 256 h + 4 lane + e passes (kept as lane masks: each ballot is the compare's own mask)
         const bool live = s < live_steps;
         bool ok[H][4];
@@ -582,6 +634,10 @@ __global__ __launch_bounds__((NL + 5) * 64) void select_rounds_kernel(SelectDesc
           for (int h = 0; h < H; h++)
 #pragma unroll
             for (int e = 0; e < 4; e++) ok[h][e] = ok[h][e] & ((uint64_t)(v[h][c][e] - lo[c]) <= span[c]);
+          if constexpr (VAL) {  // a NULL fails the predicate (H = 1)
+#pragma unroll
+            for (int e = 0; e < 4; e++) ok[0][e] = ok[0][e] & (((vmc[c] >> e) & 1u) != 0);
+          }
         }
         unsigned long long b[H][4];
         uint32_t hc[H];  // selected rows per sub-step
@@ -633,6 +689,13 @@ __global__ __launch_bounds__((NL + 5) * 64) void select_rounds_kernel(SelectDesc
               } else {
 #pragma unroll
                 for (int e = 0; e < 4; e++) ((int32_t *)st)[idx[e]] = (int32_t)v[h][c][e];
+              }
+              if constexpr (VAL) {
+                if (hv[c]) {
+                  uint8_t *vb = mystage + vsoff[c];
+#pragma unroll
+                  for (int e = 0; e < 4; e++) vb[idx[e]] = (uint8_t)((vmc[c] >> e) & 1u);
+                }
               }
             }
             hb += hc[h];
@@ -716,6 +779,17 @@ __global__ __launch_bounds__((NL + 5) * 64) void select_rounds_kernel(SelectDesc
             const int32_t *st = (const int32_t *)(mystage + so);
             int32_t *dst = (int32_t *)D.dst[o] + pos;
             for (uint32_t i = lane; i < c; i += 64) dst[i] = st[(tail[j] + i) & mask];
+          }
+          if constexpr (VAL) {
+            if (D.vdst[o]) {
+              int vo = 0;
+#pragma unroll
+              for (int cc = 0; cc < NC; cc++)
+                if (cc == oc) vo = vsoff[cc];
+              const uint8_t *vb = mystage + vo;
+              uint8_t *vd = D.vdst[o] + pos;
+              for (uint32_t i = lane; i < c; i += 64) vd[i] = vb[(tail[j] + i) & mask];
+            }
           }
         }
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // staging read before it is freed
@@ -839,6 +913,7 @@ __global__ __launch_bounds__((NL + 5) * 64) void select_rounds_kernel(SelectDesc
         const int64_t xv = D.col[c].w == 8 ? ((const int64_t *)D.col[c].data)[i]
                                            : (int64_t)((const int32_t *)D.col[c].data)[i];
         ok[e] = (uint64_t)(xv - D.col[c].lo) <= D.col[c].span;
+        if (VAL && D.col[c].valid) ok[e] = ok[e] && ((D.col[c].valid[i >> 6] >> (i & 63)) & 1);
       }
     }
     unsigned long long bb[4];
@@ -852,6 +927,7 @@ __global__ __launch_bounds__((NL + 5) * 64) void select_rounds_kernel(SelectDesc
         const int c = D.out_col[o];
         if (D.col[c].w == 8) ((int64_t *)D.dst[o])[pos] = ((const int64_t *)D.col[c].data)[i0 + e];
         else ((int32_t *)D.dst[o])[pos] = ((const int32_t *)D.col[c].data)[i0 + e];
+        if (VAL && D.vdst[o]) D.vdst[o][pos] = (uint8_t)((D.col[c].valid[(i0 + e) >> 6] >> ((i0 + e) & 63)) & 1);
       }
       pos++;
     }
@@ -872,12 +948,16 @@ static SelectRoundsPlan PlanSelectRoundsNL(const SelectDesc &d, int64_t nrows, i
   if (d.ncol < 1 || d.ncol > SL_MAX_COL || d.nout < 1 || d.nout > SL_MAX_OUT) return p;
   uint32_t smask = 0;
   for (int k = 0; k < d.nout; k++) smask |= 1u << d.out_col[k];
-  int rowb = 0;  // staged bytes per row: every distinct loaded column an output reads
+  int rowb = 0;  // staged bytes per row: every distinct loaded column an output reads (+1 if NULL-able)
   for (int c = 0; c < d.ncol; c++) {
     if (d.col[c].w != 4 && d.col[c].w != 8) return p;
     p.ni += d.col[c].w / 4;
     if (d.col[c].w == 8) p.wm |= 1 << c;
     if ((smask >> c) & 1) rowb += d.col[c].w == 8 && !d.col[c].narrow ? 8 : 4;
+    if (d.col[c].valid) {
+      p.nv++;
+      if ((smask >> c) & 1) rowb += 1;
+    }
   }
   p.nc = d.ncol;
   // Ring and staging share the CU's LDS.  Sub-steps per step (H) and ring depth
@@ -890,22 +970,24 @@ static SelectRoundsPlan PlanSelectRoundsNL(const SelectDesc &d, int64_t nrows, i
   // fits int32) leave LDS for 8 loader waves (two per SIMD: each hides the
   // other's latencies) with a 3-deep ring and 2048 staged rows each
   // (profiles/r02_select_rounds_sweep.log).  MBX_SR_NL=4|8 overrides.
-  p.NL = p.nc == 1 && rowb <= 4 ? 8 : 4;
+  // (+1 staged byte per row for a NULL-able output's validity)
+  p.NL = p.nc == 1 && rowb <= 4 + p.nv ? 8 : 4;
   if (const char *e = getenv("MBX_SR_NL")) p.NL = atoi(e) == 8 && p.nc == 1 ? 8 : 4;
   if (force_nl) p.NL = force_nl;
   if (p.NL == 8) want_h = 1, want_depth = 3;
   if (const char *e = getenv("MBX_SR_H")) want_h = atoi(e) == 1 ? 1 : 2;
+  if (p.nv) want_h = 1;
   if (const char *e = getenv("MBX_SR_S")) want_s = atoi(e) > 0 ? atoi(e) : 0;
   if (const char *e = getenv("MBX_SR_STG")) want_stg = atoi(e) >= 256 ? atoi(e) : 4096;
   if (const char *e = getenv("MBX_SR_DEPTH")) {
     const int v = atoi(e);
-    if (p.nc == 1 && (v == 2 || v == 3 || v == 4 || v == 6)) want_depth = v;  // single-column shapes only (sweeps)
+    if (p.nc == 1 && !p.nv && (v == 2 || v == 3 || v == 4 || v == 6)) want_depth = v;  // single-column shapes only (sweeps)
   }
   int best_stg = 0;
   for (int h = 2; h >= 1; h--) {
     if (want_h && h != want_h) continue;
     const int depth = want_depth ? want_depth : h == 2 ? 2 : (p.ni <= 2 ? 3 : 2);
-    const size_t ring = (size_t)p.NL * depth * p.ni * 1024 * h;
+    const size_t ring = (size_t)p.NL * depth * p.ni * 1024 * h + (p.nv ? (size_t)p.NL * depth * p.nc * 32 : 0);
     if (ring + 2048 >= (size_t)160 * 1024) continue;
     const size_t budget = (size_t)160 * 1024 - 2048 - ring;  // static meta (1.5 KB) + margin
     int stg = want_stg;
@@ -944,17 +1026,17 @@ static SelectRoundsPlan PlanSelectRoundsNL(const SelectDesc &d, int64_t nrows, i
 size_t SelectRoundsCtlBytes(const SelectRoundsPlan &p) { return (size_t)(8 + p.nrounds * p.G) * 8; }
 
 namespace {
-template <int NC, int WM, int DP, int H, int NL>
+template <int NC, int WM, int DP, int H, int NL, bool VAL = false>
 void SrLaunchNL(const SelectDesc &d, const SelectRoundsPlan &p, int64_t nrows, unsigned long long *ctl, uint32_t epoch,
                 hipStream_t s) {
   static bool attr = false;
   if (!attr) {
-    (void)hipFuncSetAttribute((const void *)select_rounds_kernel<NC, WM, DP, H, NL>,
+    (void)hipFuncSetAttribute((const void *)select_rounds_kernel<NC, WM, DP, H, NL, VAL>,
                               hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024 - 2048);
     attr = true;
   }
-  hipLaunchKernelGGL((select_rounds_kernel<NC, WM, DP, H, NL>), dim3((unsigned)p.G), dim3((NL + 5) * 64), p.lds, s, d,
-                     nrows, p.nrounds, p.S, p.stg, ctl, epoch, p.sleep, p.test_stall, p.pw);
+  hipLaunchKernelGGL((select_rounds_kernel<NC, WM, DP, H, NL, VAL>), dim3((unsigned)p.G), dim3((NL + 5) * 64), p.lds, s,
+                     d, nrows, p.nrounds, p.S, p.stg, ctl, epoch, p.sleep, p.test_stall, p.pw);
 }
 template <int NC, int WM, int DP, int H>
 void SrLaunchH(const SelectDesc &d, const SelectRoundsPlan &p, int64_t nrows, unsigned long long *ctl, uint32_t epoch,
@@ -968,6 +1050,13 @@ template <int NC, int WM>
 void SrDepth(const SelectDesc &d, const SelectRoundsPlan &p, int64_t nrows, unsigned long long *ctl, uint32_t epoch,
              hipStream_t s) {
   constexpr int ni = SrCols<NC, WM>::ni();
+  if (p.nv) {  // NULL-able columns: H = 1, 3-deep ring for one- and two-slot sets (8 loaders: one column only)
+    if constexpr (NC == 1) {
+      if (p.NL == 8) return SrLaunchNL<NC, WM, 3, 1, 8, true>(d, p, nrows, ctl, epoch, s);
+    }
+    if (ni <= 2) return SrLaunchNL<NC, WM, 3, 1, 4, true>(d, p, nrows, ctl, epoch, s);
+    return SrLaunchNL<NC, WM, 2, 1, 4, true>(d, p, nrows, ctl, epoch, s);
+  }
   if (p.H == 1 && ni <= 2) {  // 3-deep ring at H = 1
     if constexpr (NC == 1) {
       if (p.depth == 2) return SrLaunchH<NC, WM, 2, 1>(d, p, nrows, ctl, epoch, s);
@@ -993,6 +1082,30 @@ void SrDispatch(const SelectDesc &d, const SelectRoundsPlan &p, int64_t nrows, u
   }
 }
 }  // namespace
+
+// one thread per output word: 64 validity bytes (0/1) -> 64 bits; 8 bytes at a
+// time, bit i of (y * 0x0102040810204080) >> 56 = byte i of y
+__global__ __launch_bounds__(256) void pack_validity_bytes_kernel(const uint8_t *__restrict__ b, int64_t n,
+                                                                  uint64_t *__restrict__ bits) {
+  const int64_t wd = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int64_t base = wd * 64;
+  if (base >= n) return;
+  uint64_t x = 0;
+  if (base + 64 <= n) {
+    const uint64_t *p = (const uint64_t *)(b + base);
+#pragma unroll
+    for (int j = 0; j < 8; j++) x |= ((p[j] * 0x0102040810204080ull) >> 56) << (8 * j);
+  } else {
+    for (int64_t i = base; i < n; i++) x |= (uint64_t)(b[i] & 1) << (i - base);
+  }
+  bits[wd] = x;
+}
+
+void PackValidityBytes(const uint8_t *bytes, int64_t n, uint64_t *bits, hipStream_t s) {
+  if (n <= 0) return;
+  const int64_t words = (n + 63) / 64;
+  hipLaunchKernelGGL(pack_validity_bytes_kernel, dim3((unsigned)((words + 255) / 256)), dim3(256), 0, s, bytes, n, bits);
+}
 
 void SelectRounds(const SelectDesc &d, const SelectRoundsPlan &p, int64_t nrows, unsigned long long *ctl,
                   uint32_t epoch, hipStream_t s) {

@@ -273,11 +273,19 @@ def _ncol(conn, sql, kind, idx=0):
     return vals, np.frombuffer(b[4 + n * w:4 + n * (w + 1)], dtype=np.uint8).astype(bool)
 
 
+@pytest.mark.parametrize("path", ["auto", "rounds", "twopass"])
 @pytest.mark.parametrize("n", [1, 63, 64, 255, 257, 4097, 70_001, 1_000_003])
-def test_filter_compact_nullable(mbx, oracle, monkeypatch, n):
-    """NULLs in predicate columns (a NULL fails the row) and in output columns
-    (validity bits compacted by compact_validity) on the two-pass path: values
-    and validity exact vs numpy and vs the VM path (MBX_FC=0)."""
+def test_filter_compact_nullable(mbx, oracle, monkeypatch, n, path):
+    """NULLs in predicate columns (a NULL fails the row) and in output columns:
+    the two-pass path (validity bits compacted by compact_validity) and the
+    one-pass select_rounds (validity words in a second ring, one byte per
+    output row packed by pack_validity), forced at every size with
+    MBX_SR_MIN_ROWS=0; values and validity exact vs numpy and vs the VM path
+    (MBX_FC=0)."""
+    if path != "auto":
+        monkeypatch.setenv("MBX_SR_MIN_ROWS", "0")
+    if path == "twopass":
+        monkeypatch.setenv("MBX_SR_NULLS", "0")
     cfg = mbx.Config.create()
     cfg.set("mbx_profile", "true")
     c = mbx.connect_with_config(cfg).value
@@ -304,7 +312,11 @@ def test_filter_compact_nullable(mbx, oracle, monkeypatch, n):
             names = [kk["name"] for kk in c.last_profile()["kernels"]]
             # NULL-free loaded columns (tiny n) take the one-pass kernel
             assert "filter_bits" in names or "select" in names or "select_rounds" in names, (sql, names)
-            if i == 0 and not valid.all() and m.any():
+            if path == "rounds":
+                assert "select_rounds" in names and "filter_bits" not in names, (sql, names)
+                if i == 0 and not valid.all() and m.any():
+                    assert "pack_validity" in names, (sql, names)
+            elif i == 0 and not valid.all() and m.any() and "select_rounds" not in names:
                 assert "compact_validity" in names, (sql, names)
             assert np.array_equal(ok, valid[m]), (n, sql, i)
             assert np.array_equal(got, np.where(valid[m], arr[m], 0).astype(got.dtype)), (n, sql, i)

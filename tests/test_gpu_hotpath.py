@@ -680,6 +680,37 @@ def test_c2_c5_beyond_int32_rows(mbx, oracle):
     c.close()
 
 
+def test_select_rounds_output_positions_beyond_int32(mbx, oracle):
+    """The one-pass compaction (select_rounds) with OUTPUT positions past 2^31:
+    every one of 2^31 + 4097 rows passes, so the run bases, per-round prefix and
+    storer addresses all cross the int32 range; checked by COUNT/SUM/MIN/MAX of
+    the result, its head and tail rows, and the kernel that ran."""
+    import os as _os
+    th = min(16, len(_os.sched_getaffinity(0)))
+    cfg = mbx.Config.create()
+    cfg.set("mbx_profile", "true")
+    c = mbx.connect_with_config(cfg).value
+    q(c, f"CREATE TABLE big2 AS SELECT mbx_synth(42, i, 50) + 1 AS x FROM range({BIG_N}) tbl(i)")
+    cnt, s = oracle.synth_filter_count(42, 0, BIG_N, 50, 1, 1, 2**63 - 1, th)
+    assert cnt == BIG_N
+    a = c.query_arrow("SELECT x FROM big2 WHERE x >= 1").value  # device-resident result
+    names = [k["name"] for k in c.last_profile()["kernels"]]
+    assert "select_rounds" in names, names
+    # the reference's arrow row count is an int32 (duckdb_native.c:2277): the low 32 bits
+    assert a.row_count() == BIG_N - 2**32
+    a.close()
+    q(c, "CREATE TABLE bigall AS SELECT x FROM big2 WHERE x >= 1")
+    assert one(c, "SELECT COUNT(*), SUM(x), MIN(x), MAX(x) FROM bigall") == [str(BIG_N), str(s), "1", "50"]
+    head = oracle.synth_i64(5, 42, 0, 50, 1).tolist()
+    tail = oracle.synth_i64(5, 42, BIG_N - 5, 50, 1).tolist()
+    assert [int(r[0]) for r in q(c, "SELECT x FROM bigall LIMIT 5").rows] == head
+    assert [int(r[0]) for r in q(c, f"SELECT x FROM bigall LIMIT 5 OFFSET {BIG_N - 5}").rows] == tail
+    mid = 2**31 - 2  # the rows either side of output position 2^31
+    assert ([int(r[0]) for r in q(c, f"SELECT x FROM bigall LIMIT 4 OFFSET {mid}").rows] ==
+            oracle.synth_i64(4, 42, mid, 50, 1).tolist())
+    c.close()
+
+
 def test_c3_beyond_int32_rows(mbx, oracle):
     import os as _os
     th = min(16, len(_os.sched_getaffinity(0)))
