@@ -84,7 +84,7 @@ int FilterAggStates(const void *pcol, int pphys, int64_t lo, int64_t hi, bool ha
 
 // --- fused GROUP BY on a small-range integer key (config C3) -------------
 // key in [kmin, kmin + nk), no nulls; up to 2 value columns of one phys.
-size_t GroupDirectLds(int nk, int R, int nv, bool mm);
+size_t GroupDirectLds(int nk, int R, int nv, bool mm, bool vv = false);  // vv: + valid-row counts
 // Optional fused range predicates of the direct GROUP BY (a conjunction):
 // rows with lo <= p <= lo + span for every entry.  src: 1 = its own column
 // `col` (int32/int64, loaded as an extra slice), 2 = the key column, 3 = value
@@ -105,7 +105,8 @@ struct GroupPreds {
 bool GroupByDirectStates(const void *kcol, int kphys, int64_t kmin, int nk, const void *v0, const void *v1, int vphys,
                          int nv, bool mm, int64_t nrows, int64_t seg_rows, int R, unsigned long long *cstar,
                          AggState *st0, AggState *st1, int grid_blocks, hipStream_t s,
-                         const GroupPreds *pred = nullptr, uint64_t vmaxabs = ~0ull);
+                         const GroupPreds *pred = nullptr, uint64_t vmaxabs = ~0ull,
+                         const uint64_t *v0valid = nullptr);  // v0's validity words (nv == 1): false if unsupported
 
 // --- generic aggregation over compacted columns ---------------------------
 // vclass: VC_I64 / VC_I128 / VC_F64 of the input column (phys given)

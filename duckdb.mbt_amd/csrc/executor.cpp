@@ -2014,17 +2014,30 @@ static DRel Aggregate(Engine &e, const DRel &src, const BoundSelect &s) {
     std::vector<int> vcols;
     bool ok = ks && ks->stats_valid && ks->null_count == 0 && src.n > 0;
     bool mm = false;
+    // one value column may hold NULLs (group_direct_lds VV: its validity words ride the ring)
+    auto int_col = [&](int c) {
+      const DCol &d = src.cols[c];
+      return FastIntCol(src, c) ||
+             (d.validity && (d.phys == P_I32 || d.phys == P_I64) && d.data && (uintptr_t)d.validity % 16 == 0);
+    };
     for (auto &a : s.aggs) {
       if (a.kind == A_COUNT_STAR) continue;
       if (a.distinct) ok = false;
       const BExpr *x = a.arg ? StripWidening(a.arg.get()) : nullptr;
-      if (!x || x->kind != BExpr::COL || !FastIntCol(src, x->col) || a.arg->type.id == T_DOUBLE) {
+      if (!x || x->kind != BExpr::COL || !int_col(x->col) || a.arg->type.id == T_DOUBLE) {
         ok = false;
         break;
       }
       if (a.kind == A_MIN || a.kind == A_MAX) mm = true;
       if (std::find(vcols.begin(), vcols.end(), x->col) == vcols.end()) vcols.push_back(x->col);
     }
+    const uint64_t *vvalid = nullptr;
+    for (int c : vcols)
+      if (src.cols[c].validity) {
+        const char *gn = getenv("MBX_GD_NULLS");  // MBX_GD_NULLS=0: NULL-able values keep the generic paths
+        if (vcols.size() != 1 || (gn && atoi(gn) == 0)) ok = false;
+        vvalid = src.cols[c].validity;
+      }
     if (ok && vcols.size() <= 2) {
       if (vcols.size() == 2 && src.cols[vcols[0]].phys != src.cols[vcols[1]].phys) ok = false;
       i128 range = ks->imax - ks->imin + 1;
@@ -2040,8 +2053,9 @@ static DRel Aggregate(Engine &e, const DRel &src, const BoundSelect &s) {
         int nk = (int)range;
         int nv = (int)vcols.size();
         int R = 64;
-        while (R > 1 && dev::GroupDirectLds(nk, R, nv, mm) > 48 * 1024) R >>= 1;
-        if (dev::GroupDirectLds(nk, R, nv, mm) > 64 * 1024) ok = false;
+        const bool vv = vvalid != nullptr;
+        while (R > 1 && dev::GroupDirectLds(nk, R, nv, mm, vv) > 48 * 1024) R >>= 1;
+        if (dev::GroupDirectLds(nk, R, nv, mm, vv) > 64 * 1024) ok = false;
         int64_t seg = 0;  // whole chunk
         if (maxabs > 0) {
           i128 per_rep = ((i128)1 << 62) / maxabs;  // rows one replica may absorb
@@ -2064,6 +2078,7 @@ static DRel Aggregate(Engine &e, const DRel &src, const BoundSelect &s) {
           Phys vphys = nv ? src.cols[vcols[0]].phys : P_I64;
           double bytes = (double)src.n * PhysSize(K.phys);
           for (int c : vcols) bytes += (double)src.n * PhysSize(src.cols[c].phys);
+          if (vvalid) bytes += src.n / 8.0;
           dev::GroupPreds gp;
           memset(&gp, 0, sizeof(gp));
           for (auto &kv : f2_ranges) {
@@ -2084,7 +2099,7 @@ static DRel Aggregate(Engine &e, const DRel &src, const BoundSelect &s) {
                                                 nv > 1 ? src.cols[vcols[1]].data : nullptr, vphys, nv, mm, src.n, seg,
                                                 R, (unsigned long long *)cs->p, (dev::AggState *)s0->p,
                                                 (dev::AggState *)s1->p, 0, e.stream, gp.n ? &gp : nullptr,
-                                                maxabs < ((i128)1 << 62) ? (uint64_t)maxabs : ~0ull);
+                                                maxabs < ((i128)1 << 62) ? (uint64_t)maxabs : ~0ull, vvalid);
           }
           if (!launched) goto generic;
           auto list = Alloc(e, nslots * 4);

@@ -1592,18 +1592,26 @@ __device__ __forceinline__ void gd_max_i64(long long *p, long long v) {
   asm volatile("ds_max_i64 %0, %1" ::"v"(gd_lds(p)), "v"(v) : "memory");
 }
 
-template <typename TK, typename TV, int NV, bool MM, int DEPTH, bool PK>
+// VV (NV = 1, PK): the value column has NULLs.  Its step's 32 B of validity
+// words ride the ring slot after the value slice (one exec-masked glds);
+// COUNT(*) takes its own ds_add_u32 per row, the packed count of the SUM atomic
+// counts the valid rows only (drained into vcnt), and SUM / MIN / MAX see the
+// valid rows only; a predicate on the value column fails on NULL.
+template <typename TK, typename TV, int NV, bool MM, int DEPTH, bool PK, bool VV = false>
 __global__ __launch_bounds__(256) void group_direct_lds_kernel(const TK *__restrict__ keys, const TV *__restrict__ v0,
                                                                const TV *__restrict__ v1, int64_t n, int64_t kmin,
                                                                int nk, int R, size_t ring_off,
                                                                unsigned long long *cstar, AggState *st0,
-                                                               AggState *st1, GroupPreds pr, int PKB, int PKF) {
+                                                               AggState *st1, GroupPreds pr, int PKB, int PKF,
+                                                               const uint64_t *__restrict__ vvalid) {
+  static_assert(!VV || (NV == 1 && PK), "validity: one value column, packed counts");
   extern __shared__ __attribute__((aligned(16))) unsigned char lds_raw[];
   constexpr int KB = 256 * (int)sizeof(TK), VB = 256 * (int)sizeof(TV);  // bytes per step
-  constexpr int SB0 = KB + NV * VB;                                        // slot bytes without a predicate slice
+  constexpr int SBD = KB + NV * VB;                                        // key + value slices
+  constexpr int SB0 = SBD + (VV ? 32 : 0);                                 // + validity words
   // NLD counts the glds of a step without the optional predicate slice: with
   // one, the counted wait below is merely conservative (loads retire in order)
-  constexpr int NLD = SB0 / 1024;
+  constexpr int NLD = SBD / 1024 + (VV ? 1 : 0);
   // extra slices for predicate columns of their own, after the key/value slices
   int poff[GROUP_MAX_PRED];
   int PB = 0;
@@ -1621,6 +1629,8 @@ __global__ __launch_bounds__(256) void group_direct_lds_kernel(const TK *__restr
   long long *mx0 = mn0 + nslot;
   long long *mn1 = mx0 + nslot;
   long long *mx1 = mn1 + nslot;
+  // VV: valid-row counts per slot, after the table (GroupDirectLds sizes it)
+  unsigned int *vcnt = (unsigned int *)(sum0 + (NV >= 2 ? 2 : 1) * nslot + (MM ? 2 * (NV >= 2 ? 2 : 1) * nslot : 0));
   const int t = threadIdx.x, lane = t & 63, w = t >> 6;
   const int rep = lane % R;
   unsigned char *ring = lds_raw + ring_off + (size_t)w * DEPTH * SB;
@@ -1634,8 +1644,14 @@ __global__ __launch_bounds__(256) void group_direct_lds_kernel(const TK *__restr
     }
   }
   __syncthreads();
-  auto row = [&](int64_t k, int64_t a, int64_t b) {
+  auto row = [&](int64_t k, int64_t a, int64_t b, bool valid) {
     int sl = (int)(k - kmin) * R + rep;
+    if (VV) {
+      gd_add_u32(&cnt[sl], 1u);
+      if (valid) gd_add_u64(&sum0[sl], ((unsigned long long)a << PKB) + 1ull);
+      if (MM && valid) { gd_min_i64(&mn0[sl], (long long)a); gd_max_i64(&mx0[sl], (long long)a); }
+      return;
+    }
     if (PK) {
       gd_add_u64(&sum0[sl], ((unsigned long long)a << PKB) + 1ull);
     } else {
@@ -1698,6 +1714,8 @@ __global__ __launch_bounds__(256) void group_direct_lds_kernel(const TK *__restr
         __builtin_amdgcn_global_load_lds((const void *)(vp + j * 1024 + lane * 16), (void *)(dst + KB + VB + j * 1024), 16,
                                          0, 2);
     }
+    if (VV && lane < 2)
+      __builtin_amdgcn_global_load_lds((const void *)(vvalid + q * 4 + lane * 2), (void *)(dst + SBD), 16, 0, 2);
 #pragma unroll
     for (int j = 0; j < GROUP_MAX_PRED; j++) {
       if (j >= pr.n || pr.p[j].src != 1) continue;
@@ -1741,6 +1759,8 @@ __global__ __launch_bounds__(256) void group_direct_lds_kernel(const TK *__restr
       }
     }
     bool ok[4] = {true, true, true, true};
+    unsigned vm = 0xFu;  // VV: validity of this lane's 4 rows
+    if (VV) vm = (unsigned)(*(const uint64_t *)(src + SBD + (lane >> 4) * 8) >> (4 * (lane & 15))) & 0xFu;
 #pragma unroll
     for (int j = 0; j < GROUP_MAX_PRED; j++) {
       if (j >= pr.n) break;
@@ -1759,13 +1779,17 @@ __global__ __launch_bounds__(256) void group_direct_lds_kernel(const TK *__restr
       }
 #pragma unroll
       for (int e = 0; e < 4; e++) ok[e] = ok[e] && (uint64_t)(pv[e] - g.lo) <= g.span;
+      if (VV && g.src == 3) {  // a predicate on the NULL-able value column
+#pragma unroll
+        for (int e = 0; e < 4; e++) ok[e] = ok[e] && ((vm >> e) & 1u);
+      }
     }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     int64_t q = st + DEPTH * nw;
     issue(q < nsteps ? q : st, k);
 #pragma unroll
     for (int e = 0; e < 4; e++)
-      if (ok[e]) row(kk[e], NV >= 1 ? a[e] : 0, NV >= 2 ? b[e] : 0);
+      if (ok[e]) row(kk[e], NV >= 1 ? a[e] : 0, NV >= 2 ? b[e] : 0, ((vm >> e) & 1u) != 0);
     k = k + 1 == DEPTH ? 0 : k + 1;
     if (PK) {
       ++it;
@@ -1776,14 +1800,15 @@ __global__ __launch_bounds__(256) void group_direct_lds_kernel(const TK *__restr
   if (blockIdx.x == 0) {
     for (int64_t i = (nsteps << 8) + t; i < n; i += blockDim.x) {
       int64_t kv = (int64_t)keys[i], av = NV >= 1 ? (int64_t)v0[i] : 0;
+      const bool vr = !VV || ((vvalid[i >> 6] >> (i & 63)) & 1);
       bool okr = true;
       for (int j = 0; j < pr.n; j++) {
         const GroupPred &g = pr.p[j];
         int64_t pv = g.src == 2 ? kv : g.src == 3 ? av
                    : (g.phys == P_I64 ? ((const int64_t *)g.col)[i] : (int64_t)((const int32_t *)g.col)[i]);
-        okr = okr && (uint64_t)(pv - g.lo) <= g.span;
+        okr = okr && (uint64_t)(pv - g.lo) <= g.span && (g.src != 3 || vr);
       }
-      if (okr) row(kv, av, NV >= 2 ? (int64_t)v1[i] : 0);
+      if (okr) row(kv, av, NV >= 2 ? (int64_t)v1[i] : 0, vr);
     }
   }
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // this thread's table atomics (asm) have landed
@@ -1792,17 +1817,22 @@ __global__ __launch_bounds__(256) void group_direct_lds_kernel(const TK *__restr
 #pragma unroll
     for (int j = 0; j < PK_J; j++) {
       int sl = t + 256 * j;
-      if (sl < nslot) { cnt[sl] = rc[j]; sum0[sl] = rs[j]; }
+      if (sl < nslot) {
+        if (VV) vcnt[sl] = rc[j];  // cnt[] keeps COUNT(*) from its own atomics
+        else cnt[sl] = rc[j];
+        sum0[sl] = rs[j];
+      }
     }
   }
   __syncthreads();
   for (int kq = t; kq < nk; kq += blockDim.x) {
-    unsigned long long c = 0;
+    unsigned long long c = 0, vc = 0;
     i128 s0 = 0, s1 = 0;
     long long a0 = INT64_MAX, b0 = INT64_MIN, a1 = INT64_MAX, b1 = INT64_MIN;
     for (int r = 0; r < R; r++) {
       int sl = kq * R + r;
       c += cnt[sl];
+      if (VV) vc += vcnt[sl];
       if (NV >= 1) s0 += (i128)sum0[sl];
       if (NV >= 2) s1 += (i128)sum1[sl];
       if (MM) {
@@ -1810,10 +1840,11 @@ __global__ __launch_bounds__(256) void group_direct_lds_kernel(const TK *__restr
         if (NV >= 2) { a1 = mn1[sl] < a1 ? mn1[sl] : a1; b1 = mx1[sl] > b1 ? mx1[sl] : b1; }
       }
     }
-    if (c) {
-      atomicAdd(&cstar[kq], c);
+    if (!VV) vc = c;
+    if (c) atomicAdd(&cstar[kq], c);
+    if (vc) {
       Acc A;
-      A.cnt = c;
+      A.cnt = vc;
       if (NV >= 1) {
         int64_t lo, hi;
         sp128(s0, lo, hi);
@@ -1839,11 +1870,12 @@ static void LaunchGroupDirect(const void *k, const void *v0, const void *v1, int
   CHECK_LAUNCH();
 }
 
-size_t GroupDirectLds(int nk, int R, int nv, bool mm) {
+size_t GroupDirectLds(int nk, int R, int nv, bool mm, bool vv) {
   size_t nslot = (size_t)nk * R;
   size_t b = (nslot * 4 + 15) & ~(size_t)15;
   b += nslot * 8 * (size_t)(nv >= 2 ? 2 : 1);
   if (mm) b += nslot * 8 * 2 * (size_t)(nv >= 2 ? 2 : 1);
+  if (vv) b += (nslot * 4 + 15) & ~(size_t)15;  // valid-row counts
   return b;
 }
 
@@ -1870,7 +1902,9 @@ static bool PackedCountParams(uint64_t vmaxabs, int R, int &pkb, int &pkf) {
 bool GroupByDirectStates(const void *kcol, int kphys, int64_t kmin, int nk, const void *v0, const void *v1, int vphys,
                          int nv, bool mm, int64_t nrows, int64_t seg_rows, int R, unsigned long long *cstar,
                          AggState *st0, AggState *st1, int grid_blocks, hipStream_t s, const GroupPreds *pred,
-                         uint64_t vmaxabs) {
+                         uint64_t vmaxabs, const uint64_t *v0valid) {
+  const bool vv = v0valid != nullptr;
+  if (vv && nv != 1) return false;
   if (nrows <= 0) return true;
   GroupPreds pr;
   memset(&pr, 0, sizeof(pr));
@@ -1889,6 +1923,7 @@ bool GroupByDirectStates(const void *kcol, int kphys, int64_t kmin, int nk, cons
     bool use = true;
     const char *e = getenv("MBX_GD_VARIANT");
     if (e && *e) use = sscanf(e, "d%d_g%d", &depth, &gpc) == 2 || pr.n != 0;
+    if (vv && !use) return false;  // the segmented kernel below has no validity words
     // MBX_GD_R=<r>: fewer replicas (experiment; seg_rows scales with R)
     if (const char *er = getenv("MBX_GD_R")) {
       int r = atoi(er);
@@ -1902,9 +1937,10 @@ bool GroupByDirectStates(const void *kcol, int kphys, int64_t kmin, int nk, cons
       int64_t nsteps = nrows >> 8;
       int64_t waves = (int64_t)grid * 4;
       int64_t rows_per_block = ((nsteps + waves - 1) / waves) * 4 * 256 + 256;
-      size_t tab = GroupDirectLds(nk, R, nv, mm);
+      if (vv && depth > 3) depth = 3;  // the validity form is built for 2- and 3-deep rings
+      size_t tab = GroupDirectLds(nk, R, nv, mm, vv);
       size_t ring_off = (tab + 15) & ~(size_t)15;
-      size_t slot = 256 * (size_t)(kphys == P_I64 ? 8 : 4) + (size_t)nv * 256 * (vphys == P_I64 ? 8 : 4);
+      size_t slot = 256 * (size_t)(kphys == P_I64 ? 8 : 4) + (size_t)nv * 256 * (vphys == P_I64 ? 8 : 4) + (vv ? 32 : 0);
       for (int j = 0; j < pr.n; j++)
         if (pr.p[j].src == 1) slot += 256 * (size_t)(pr.p[j].phys == P_I64 ? 8 : 4);
       depth = depth <= 2 ? 2 : depth <= 3 ? 3 : depth <= 4 ? 4 : depth <= 6 ? 6 : 8;
@@ -1915,7 +1951,7 @@ bool GroupByDirectStates(const void *kcol, int kphys, int64_t kmin, int nk, cons
       while (lds > lds_cap && R > 1) {
         R >>= 1;
         if (seg_rows > 0) seg_rows >>= 1;
-        tab = GroupDirectLds(nk, R, nv, mm);
+        tab = GroupDirectLds(nk, R, nv, mm, vv);
         ring_off = (tab + 15) & ~(size_t)15;
         lds = ring_off + 4 * (size_t)depth * slot;
       }
@@ -1926,6 +1962,29 @@ bool GroupByDirectStates(const void *kcol, int kphys, int64_t kmin, int nk, cons
       if (const char *ep = getenv("MBX_GD_PACK")) pk = pk && atoi(ep) != 0;
       // MBX_GD_PKF=<steps>: drain more often than needed (tests exercise the drains)
       if (const char *ef = getenv("MBX_GD_PKF")) pkf = std::max(1, std::min(pkf, atoi(ef)));
+      if (vv) {  // NULL-able value column: packed counts and one flush only
+        if (!pk || !((seg_rows <= 0 || seg_rows >= rows_per_block) && lds <= lds_cap)) return false;
+#define GLVV(TK, TV, MM, D)                                                                                         \
+  {                                                                                                                 \
+    (void)hipFuncSetAttribute((const void *)group_direct_lds_kernel<TK, TV, 1, MM, D, true, true>,                  \
+                              hipFuncAttributeMaxDynamicSharedMemorySize, 150 * 1024);                              \
+    hipLaunchKernelGGL((group_direct_lds_kernel<TK, TV, 1, MM, D, true, true>), dim3(grid), dim3(256), lds, s,     \
+                       (const TK *)kcol, (const TV *)v0, (const TV *)v1, nrows, kmin, nk, R, ring_off, cstar, st0,  \
+                       st1, pr, pkb, pkf, v0valid);                                                                 \
+  }
+#define GLVVD(TK, TV)                                                                                             \
+  if (mm) { if (depth == 2) GLVV(TK, TV, true, 2) else GLVV(TK, TV, true, 3) }                                      \
+  else { if (depth == 2) GLVV(TK, TV, false, 2) else GLVV(TK, TV, false, 3) }
+        if (kphys == P_I32) {
+          if (vphys == P_I64) { GLVVD(int32_t, int64_t) } else { GLVVD(int32_t, int32_t) }
+        } else {
+          if (vphys == P_I64) { GLVVD(int64_t, int64_t) } else { GLVVD(int64_t, int32_t) }
+        }
+#undef GLVVD
+#undef GLVV
+        CHECK_LAUNCH();
+        return true;
+      }
       if ((seg_rows <= 0 || seg_rows >= rows_per_block) && lds <= lds_cap) {
 #define GL(TK, TV, NV, MM, D)                                                                                      \
   if (lds > 64 * 1024) { /* deep rings at one or two blocks per CU */                                             \
@@ -1937,11 +1996,11 @@ bool GroupByDirectStates(const void *kcol, int kphys, int64_t kmin, int nk, cons
   if (pk && NV >= 1)                                                                                               \
     hipLaunchKernelGGL((group_direct_lds_kernel<TK, TV, NV, MM, D, NV >= 1>), dim3(grid), dim3(256), lds, s,       \
                        (const TK *)kcol, (const TV *)v0, (const TV *)v1, nrows, kmin, nk, R, ring_off, cstar, st0, \
-                       st1, pr, pkb, pkf);                                                                         \
+                       st1, pr, pkb, pkf, (const uint64_t *)nullptr);                                              \
   else                                                                                                             \
     hipLaunchKernelGGL((group_direct_lds_kernel<TK, TV, NV, MM, D, false>), dim3(grid), dim3(256), lds, s,         \
                        (const TK *)kcol, (const TV *)v0, (const TV *)v1, nrows, kmin, nk, R, ring_off, cstar, st0, \
-                       st1, pr, 0, 1);
+                       st1, pr, 0, 1, (const uint64_t *)nullptr);
 #define GLD(TK, TV, NV, MM)                                                                     \
   if (depth == 2) { GL(TK, TV, NV, MM, 2) } else if (depth == 3) { GL(TK, TV, NV, MM, 3) }      \
   else if (depth == 4) { GL(TK, TV, NV, MM, 4) } else if (depth == 6) { GL(TK, TV, NV, MM, 6) } \

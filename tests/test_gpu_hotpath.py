@@ -737,3 +737,48 @@ def test_hbm_calibrate_reports_every_shape(mbx):
     out2 = (ctypes.c_double * 2)()
     assert mbx.lib.duckdb_mbx_hbm_calibrate_ex(c._h, 1 << 28, 1, out2, 2) == 2
     c.close()
+
+
+@pytest.mark.parametrize("n", [1, 257, 100_003, 1_000_003])
+def test_group_direct_nullable_value(mbx, oracle, monkeypatch, n):
+    """F2's group_direct_lds with a NULL-able value column (VV: validity words
+    in the ring, COUNT(*) apart from the value's count): COUNT(*), COUNT(vn),
+    SUM, MIN, MAX, AVG per key, a key whose values are all NULL (SUM / MIN /
+    MAX / AVG NULL, COUNT(vn) 0), with and without a fused WHERE, exact vs
+    numpy and equal to the generic path (MBX_GD_NULLS=0); drains forced often."""
+    import numpy as np
+    monkeypatch.setenv("MBX_GD_PKF", "16")
+    cfg = mbx.Config.create()
+    cfg.set("mbx_profile", "true")
+    c = mbx.connect_with_config(cfg).value
+    q(c, f"CREATE TABLE gn AS SELECT CAST(mbx_synth(7, i, 32) AS INTEGER) AS k, mbx_synth(42, i, 50) + 1 AS x, "
+         f"CASE WHEN mbx_synth(19, i, 7) = 0 OR mbx_synth(7, i, 32) = 5 THEN NULL "
+         f"ELSE mbx_synth(9, i, 1099511627776) - 549755813888 END AS vn FROM range({n}) tbl(i)")
+    k = oracle.synth_i64(n, 7, 0, 32, 0)
+    x = oracle.synth_i64(n, 42, 0, 50, 1)
+    v = oracle.synth_i64(n, 9, 0, 2**40, -2**39)
+    valid = (oracle.synth_i64(n, 19, 0, 7, 0) != 0) & (k != 5)
+    for where, m in (("", np.ones(n, bool)), (" WHERE x > 24", x > 24), (" WHERE x > 24 AND k < 20", (x > 24) & (k < 20))):
+        sql = f"SELECT k, COUNT(*), COUNT(vn), SUM(vn), MIN(vn), MAX(vn), AVG(vn) FROM gn{where} GROUP BY k ORDER BY k"
+        res = q(c, sql)
+        if n >= 256:
+            assert "group_direct" in _kernels(c), (sql, _kernels(c))
+        want = []
+        for kk in sorted(set(k[m].tolist())):
+            sel = m & (k == kk)
+            vs = v[sel & valid]
+            want.append([str(kk), str(int(sel.sum())), str(len(vs)), str(int(vs.astype(object).sum())) if len(vs) else "",
+                         str(int(vs.min())) if len(vs) else "", str(int(vs.max())) if len(vs) else ""])
+        assert [r[:6] for r in res.rows] == want, (n, sql)
+        for r in res.rows:  # AVG: DOUBLE of the exact sum / count
+            if r[2] == "0":
+                assert r[6] == ""
+            else:
+                assert abs(float(r[6]) - int(r[3]) / int(r[2])) <= 1e-9 * max(1.0, abs(int(r[3]) / int(r[2])))
+        monkeypatch.setenv("MBX_GD_NULLS", "0")
+        res2 = q(c, sql)
+        monkeypatch.delenv("MBX_GD_NULLS")
+        if n >= 256:
+            assert "group_direct" not in _kernels(c)
+        assert [r[:6] for r in res2.rows] == [r[:6] for r in res.rows], (n, sql)
+    c.close()

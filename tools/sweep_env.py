@@ -28,6 +28,9 @@ SQL = {
     "c2n": "SELECT COUNT(*) FROM t WHERE xn > 24",
     "c5n": "SELECT COUNT(*), SUM(xn) FROM t WHERE xn > 24",
     "c5n_sumv": "SELECT COUNT(vn), SUM(vn) FROM t WHERE x > 24",
+    "c3n": "SELECT k, SUM(vn), COUNT(*) FROM t GROUP BY k",
+    "c3n_where": "SELECT k, SUM(vn), COUNT(*) FROM t WHERE x > 24 GROUP BY k",
+    "c3n_mm": "SELECT k, COUNT(vn), SUM(vn), MIN(vn), MAX(vn) FROM t GROUP BY k",
 }
 m = ge._load()
 n = int(sys.argv[1])
