@@ -99,6 +99,7 @@ struct GroupPred {
 };
 struct GroupPreds {
   int32_t n;
+  int32_t xcd;  // group_direct_lds: 1 = XCD-grouped step windows (blocks b, b+8, ... share an XCD)
   GroupPred p[GROUP_MAX_PRED];
 };
 // false only when a predicate was given and the shape needs the segmented kernel

@@ -1688,10 +1688,15 @@ __global__ __launch_bounds__(256) void group_direct_lds_kernel(const TK *__restr
   };
   const int64_t nsteps = n >> 8;
   const int64_t nw = (int64_t)gridDim.x * 4;
-  int64_t st = (int64_t)blockIdx.x * 4 + w;
+  // pr.xcd: blocks are dealt round-robin over the 8 XCDs, so block b's logical
+  // index (b % 8) * (grid / 8) + b / 8 gives each XCD one contiguous eighth of
+  // every grid-stride window instead of every eighth 1-KiB piece of it
+  int64_t bl = blockIdx.x;
+  if (pr.xcd && (gridDim.x & 7) == 0) bl = (int64_t)(blockIdx.x & 7) * (gridDim.x >> 3) + (blockIdx.x >> 3);
+  int64_t st = bl * 4 + w;
   // steps of the block's last wave (the fewest): in-loop drains happen only
   // while every wave of the block still iterates, so all reach the barrier
-  const int64_t last_w = (int64_t)blockIdx.x * 4 + 3;
+  const int64_t last_w = bl * 4 + 3;
   const int64_t min_steps = last_w < nsteps ? (nsteps - 1 - last_w) / nw + 1 : 0;
   int64_t it = 0;
   // issue one step's glds into slot d: key slice, then each value slice
@@ -1909,6 +1914,8 @@ bool GroupByDirectStates(const void *kcol, int kphys, int64_t kmin, int nk, cons
   GroupPreds pr;
   memset(&pr, 0, sizeof(pr));
   if (pred) pr = *pred;
+  pr.xcd = 0;
+  if (const char *ex = getenv("MBX_GD_XCD")) pr.xcd = atoi(ex) != 0;
   // LDS-DMA variant: one flush at the end, so a block's whole row share must
   // fit the overflow bound the host derived (seg_rows) — else the segmented
   // kernel below.  MBX_GD_VARIANT="d<depth>_g<blocks per CU>" / "seg".
