@@ -1567,7 +1567,9 @@ __global__ __launch_bounds__(256) void group_direct_kernel(const TK *__restrict_
 //
 // PK (packed count): the row's COUNT rides in the low PKB bits of its SUM
 // atomic — one ds_add_u64 of (v << PKB) + 1 per row instead of a ds_add_u32
-// plus a ds_add_u64, which is what bounds this kernel (LDS atomics, not HBM).
+// plus a ds_add_u64.  That bounded this kernel while the compiler drained the
+// ring before every LDS atomic; with the asm atomics below the plain form is
+// faster, and PK stays for the VV form (and MBX_GD_PACK=1).
 // Every PKF wave steps the block drains the packed table into per-thread
 // register partials (slot t + 256 j), before a count can reach 2^PKB or the
 // shifted sum can leave int64; the host derives PKB/PKF from the zone maps.
@@ -1962,11 +1964,20 @@ bool GroupByDirectStates(const void *kcol, int kphys, int64_t kmin, int nk, cons
         ring_off = (tab + 15) & ~(size_t)15;
         lds = ring_off + 4 * (size_t)depth * slot;
       }
-      // packed count (MBX_GD_PACK=0 disables): needs a value column, the
-      // register partials (nslot <= 2048) and a zone-map bound on |v|
+      // packed count: needs a value column, the register partials (nslot <=
+      // 2048) and a zone-map bound on |v|.  Since the table atomics stopped
+      // draining the DMA ring, two plain atomics per row beat one packed atomic
+      // plus the periodic drains (C3 1.744 -> 1.684 ms, with MIN/MAX 2.12 ->
+      // 1.87; profiles/r02_group_unpacked.log).  Both forms need the one flush
+      // at the end to be overflow-safe (else the segmented kernel), so packing
+      // is now kept for the VV form, which is built on packed counts, and for
+      // MBX_GD_PACK=1 (MBX_GD_PACK=0 turns it off everywhere).
       int pkb = 0, pkf = 0;
       bool pk = nv >= 1 && (int64_t)nk * R <= 2048 && PackedCountParams(vmaxabs, R, pkb, pkf);
-      if (const char *ep = getenv("MBX_GD_PACK")) pk = pk && atoi(ep) != 0;
+      const bool one_flush = seg_rows <= 0 || seg_rows >= rows_per_block;
+      if (one_flush && !vv) pk = false;
+      if (const char *ep = getenv("MBX_GD_PACK"))
+        pk = atoi(ep) != 0 && nv >= 1 && (int64_t)nk * R <= 2048 && PackedCountParams(vmaxabs, R, pkb, pkf);
       // MBX_GD_PKF=<steps>: drain more often than needed (tests exercise the drains)
       if (const char *ef = getenv("MBX_GD_PKF")) pkf = std::max(1, std::min(pkf, atoi(ef)));
       if (vv) {  // NULL-able value column: packed counts and one flush only

@@ -261,8 +261,9 @@ def test_filter_agg_variants_parity(conn, oracle, monkeypatch, variant):
 
 
 # ---- every fused GROUP BY launch shape gives the same bits ------------------
-# "+p0": separate COUNT atomics; "+f<k>": packed-count drains every k wave steps
-GD_VARIANTS = ["", "seg", "d2_g1", "d3_g2", "d4_g2", "+p0", "d2_g1+f1", "d3_g2+f2"]
+# "+p0"/"+p1": separate COUNT atomics (the default) / packed counts;
+# "+f<k>": packed-count drains every k wave steps
+GD_VARIANTS = ["", "seg", "d2_g1", "d3_g2", "d4_g2", "+p0", "+p1", "d2_g1+p1+f1", "d3_g2+p1+f2"]
 
 
 @pytest.mark.parametrize("variant", GD_VARIANTS)

@@ -20,6 +20,8 @@ SQL = {
     "c3_where": "SELECT k, SUM(v), COUNT(*) FROM t WHERE x > 24 GROUP BY k",
     "c3_where2": "SELECT k, SUM(v), COUNT(*) FROM t WHERE x > 24 AND k2 = 1 GROUP BY k",
     "c3": "SELECT k, SUM(v), COUNT(*) FROM t GROUP BY k",
+    "c3_mm": "SELECT k, SUM(v), MIN(v), MAX(v), COUNT(*) FROM t GROUP BY k",
+    "c3_two": "SELECT k, SUM(v), SUM(x), COUNT(*) FROM t GROUP BY k",
     "c5": "SELECT COUNT(*), SUM(x) FROM t WHERE x > 24",
     "filter_mm": "SELECT COUNT(*), SUM(x), MIN(x), MAX(x) FROM t WHERE x > 24 AND k < 16",
     "filter_cnt2": "SELECT COUNT(*) FROM t WHERE x > 24 AND k < 16",
