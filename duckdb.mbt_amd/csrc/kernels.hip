@@ -1569,7 +1569,7 @@ __global__ __launch_bounds__(256) void group_direct_kernel(const TK *__restrict_
 // atomic — one ds_add_u64 of (v << PKB) + 1 per row instead of a ds_add_u32
 // plus a ds_add_u64.  That bounded this kernel while the compiler drained the
 // ring before every LDS atomic; with the asm atomics below the plain form is
-// faster, and PK stays for the VV form (and MBX_GD_PACK=1).
+// faster, and PK stays behind MBX_GD_PACK=1.
 // Every PKF wave steps the block drains the packed table into per-thread
 // register partials (slot t + 256 j), before a count can reach 2^PKB or the
 // shifted sum can leave int64; the host derives PKB/PKF from the zone maps.
@@ -1594,11 +1594,12 @@ __device__ __forceinline__ void gd_max_i64(long long *p, long long v) {
   asm volatile("ds_max_i64 %0, %1" ::"v"(gd_lds(p)), "v"(v) : "memory");
 }
 
-// VV (NV = 1, PK): the value column has NULLs.  Its step's 32 B of validity
+// VV (NV = 1): the value column has NULLs.  Its step's 32 B of validity
 // words ride the ring slot after the value slice (one exec-masked glds);
-// COUNT(*) takes its own ds_add_u32 per row, the packed count of the SUM atomic
-// counts the valid rows only (drained into vcnt), and SUM / MIN / MAX see the
-// valid rows only; a predicate on the value column fails on NULL.
+// COUNT(*) takes its own ds_add_u32 per row, the valid rows are counted in
+// vcnt (a ds_add_u32 of their own, or the packed count of the SUM atomic
+// drained into vcnt under PK), and SUM / MIN / MAX see the valid rows only; a
+// predicate on the value column fails on NULL.
 template <typename TK, typename TV, int NV, bool MM, int DEPTH, bool PK, bool VV = false>
 __global__ __launch_bounds__(256) void group_direct_lds_kernel(const TK *__restrict__ keys, const TV *__restrict__ v0,
                                                                const TV *__restrict__ v1, int64_t n, int64_t kmin,
@@ -1606,7 +1607,7 @@ __global__ __launch_bounds__(256) void group_direct_lds_kernel(const TK *__restr
                                                                unsigned long long *cstar, AggState *st0,
                                                                AggState *st1, GroupPreds pr, int PKB, int PKF,
                                                                const uint64_t *__restrict__ vvalid) {
-  static_assert(!VV || (NV == 1 && PK), "validity: one value column, packed counts");
+  static_assert(!VV || NV == 1, "validity: one value column");
   extern __shared__ __attribute__((aligned(16))) unsigned char lds_raw[];
   constexpr int KB = 256 * (int)sizeof(TK), VB = 256 * (int)sizeof(TV);  // bytes per step
   constexpr int SBD = KB + NV * VB;                                        // key + value slices
@@ -1638,6 +1639,7 @@ __global__ __launch_bounds__(256) void group_direct_lds_kernel(const TK *__restr
   unsigned char *ring = lds_raw + ring_off + (size_t)w * DEPTH * SB;
   for (int i = t; i < nslot; i += blockDim.x) {
     cnt[i] = 0;
+    if (VV) vcnt[i] = 0;
     if (NV >= 1) sum0[i] = 0;
     if (NV >= 2) sum1[i] = 0;
     if (MM) {
@@ -1650,7 +1652,8 @@ __global__ __launch_bounds__(256) void group_direct_lds_kernel(const TK *__restr
     int sl = (int)(k - kmin) * R + rep;
     if (VV) {
       gd_add_u32(&cnt[sl], 1u);
-      if (valid) gd_add_u64(&sum0[sl], ((unsigned long long)a << PKB) + 1ull);
+      if (valid && PK) gd_add_u64(&sum0[sl], ((unsigned long long)a << PKB) + 1ull);
+      if (valid && !PK) { gd_add_u32(&vcnt[sl], 1u); gd_add_u64(&sum0[sl], (unsigned long long)a); }
       if (MM && valid) { gd_min_i64(&mn0[sl], (long long)a); gd_max_i64(&mx0[sl], (long long)a); }
       return;
     }
@@ -1970,26 +1973,28 @@ bool GroupByDirectStates(const void *kcol, int kphys, int64_t kmin, int nk, cons
       // plus the periodic drains (C3 1.744 -> 1.684 ms, with MIN/MAX 2.12 ->
       // 1.87; profiles/r02_group_unpacked.log).  Both forms need the one flush
       // at the end to be overflow-safe (else the segmented kernel), so packing
-      // is now kept for the VV form, which is built on packed counts, and for
-      // MBX_GD_PACK=1 (MBX_GD_PACK=0 turns it off everywhere).
+      // is now used only for MBX_GD_PACK=1 (the NULL-able value form included:
+      // c3n 2.18 ms packed, profiles/r02_group_unpacked.log).
       int pkb = 0, pkf = 0;
       bool pk = nv >= 1 && (int64_t)nk * R <= 2048 && PackedCountParams(vmaxabs, R, pkb, pkf);
       const bool one_flush = seg_rows <= 0 || seg_rows >= rows_per_block;
-      if (one_flush && !vv) pk = false;
+      if (one_flush) pk = false;
       if (const char *ep = getenv("MBX_GD_PACK"))
         pk = atoi(ep) != 0 && nv >= 1 && (int64_t)nk * R <= 2048 && PackedCountParams(vmaxabs, R, pkb, pkf);
       // MBX_GD_PKF=<steps>: drain more often than needed (tests exercise the drains)
       if (const char *ef = getenv("MBX_GD_PKF")) pkf = std::max(1, std::min(pkf, atoi(ef)));
       if (vv) {  // NULL-able value column: packed counts and one flush only
-        if (!pk || !((seg_rows <= 0 || seg_rows >= rows_per_block) && lds <= lds_cap)) return false;
-#define GLVV(TK, TV, MM, D)                                                                                         \
+        if (!one_flush || lds > lds_cap) return false;
+#define GLVV1(TK, TV, MM, D, P)                                                                                     \
   {                                                                                                                 \
-    (void)hipFuncSetAttribute((const void *)group_direct_lds_kernel<TK, TV, 1, MM, D, true, true>,                  \
+    (void)hipFuncSetAttribute((const void *)group_direct_lds_kernel<TK, TV, 1, MM, D, P, true>,                     \
                               hipFuncAttributeMaxDynamicSharedMemorySize, 150 * 1024);                              \
-    hipLaunchKernelGGL((group_direct_lds_kernel<TK, TV, 1, MM, D, true, true>), dim3(grid), dim3(256), lds, s,     \
+    hipLaunchKernelGGL((group_direct_lds_kernel<TK, TV, 1, MM, D, P, true>), dim3(grid), dim3(256), lds, s,        \
                        (const TK *)kcol, (const TV *)v0, (const TV *)v1, nrows, kmin, nk, R, ring_off, cstar, st0,  \
-                       st1, pr, pkb, pkf, v0valid);                                                                 \
+                       st1, pr, pk ? pkb : 0, pk ? pkf : 1, v0valid);                                               \
   }
+#define GLVV(TK, TV, MM, D) \
+  if (pk) GLVV1(TK, TV, MM, D, true) else GLVV1(TK, TV, MM, D, false)
 #define GLVVD(TK, TV)                                                                                             \
   if (mm) { if (depth == 2) GLVV(TK, TV, true, 2) else GLVV(TK, TV, true, 3) }                                      \
   else { if (depth == 2) GLVV(TK, TV, false, 2) else GLVV(TK, TV, false, 3) }
@@ -2000,6 +2005,7 @@ bool GroupByDirectStates(const void *kcol, int kphys, int64_t kmin, int nk, cons
         }
 #undef GLVVD
 #undef GLVV
+#undef GLVV1
         CHECK_LAUNCH();
         return true;
       }

@@ -740,14 +740,17 @@ def test_hbm_calibrate_reports_every_shape(mbx):
     c.close()
 
 
+@pytest.mark.parametrize("pack", ["0", "1"])
 @pytest.mark.parametrize("n", [1, 257, 100_003, 1_000_003])
-def test_group_direct_nullable_value(mbx, oracle, monkeypatch, n):
+def test_group_direct_nullable_value(mbx, oracle, monkeypatch, n, pack):
     """F2's group_direct_lds with a NULL-able value column (VV: validity words
     in the ring, COUNT(*) apart from the value's count): COUNT(*), COUNT(vn),
     SUM, MIN, MAX, AVG per key, a key whose values are all NULL (SUM / MIN /
     MAX / AVG NULL, COUNT(vn) 0), with and without a fused WHERE, exact vs
-    numpy and equal to the generic path (MBX_GD_NULLS=0); drains forced often."""
+    numpy and equal to the generic path (MBX_GD_NULLS=0); plain valid-row
+    counts (the default) and packed counts with drains forced often."""
     import numpy as np
+    monkeypatch.setenv("MBX_GD_PACK", pack)
     monkeypatch.setenv("MBX_GD_PKF", "16")
     cfg = mbx.Config.create()
     cfg.set("mbx_profile", "true")
