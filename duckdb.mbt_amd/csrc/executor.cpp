@@ -386,9 +386,12 @@ static void RaiseDeviceError(Engine &e, int32_t err) {
 
 template <typename T>
 static T ReadDev(Engine &e, const void *p) {
-  T v;
-  HIPCHK(hipMemcpyAsync(&v, p, sizeof(T), hipMemcpyDeviceToHost, e.stream));
+  // through the pinned arena: a pageable destination would take HIP's staged copy
+  static_assert(sizeof(T) <= 64, "small device words only");
+  HIPCHK(hipMemcpyAsync(e.h_pinned, p, sizeof(T), hipMemcpyDeviceToHost, e.stream));
   HIPCHK(hipStreamSynchronize(e.stream));
+  T v;
+  memcpy(&v, e.h_pinned, sizeof(T));
   return v;
 }
 
@@ -2071,10 +2074,12 @@ static DRel Aggregate(Engine &e, const DRel &src, const BoundSelect &s) {
         if (ok) {
           int64_t nslots = nk;
           size_t st_bytes = (size_t)nslots * sizeof(dev::AggState);
-          auto cs = Alloc(e, nslots * 8, true);
-          auto s0 = Alloc(e, st_bytes), s1 = Alloc(e, st_bytes);
-          dev::InitAggStates((dev::AggState *)s0->p, nslots, e.stream);
-          dev::InitAggStates((dev::AggState *)s1->p, nslots, e.stream);
+          // both value columns' states in one block, zeroed with the COUNT(*) slots
+          // by one launch ahead of the scan
+          auto cs = Alloc(e, nslots * 8);
+          auto sb = Alloc(e, 2 * st_bytes);
+          dev::AggState *const s0p = (dev::AggState *)sb->p, *const s1p = s0p + nslots;
+          dev::InitAggStatesCounts(s0p, 2 * nslots, (unsigned long long *)cs->p, nslots, e.stream);
           Phys vphys = nv ? src.cols[vcols[0]].phys : P_I64;
           double bytes = (double)src.n * PhysSize(K.phys);
           for (int c : vcols) bytes += (double)src.n * PhysSize(src.cols[c].phys);
@@ -2097,42 +2102,42 @@ static DRel Aggregate(Engine &e, const DRel &src, const BoundSelect &s) {
             launched = dev::GroupByDirectStates(K.data, K.phys, (int64_t)ks->imin, nk,
                                                 nv > 0 ? src.cols[vcols[0]].data : nullptr,
                                                 nv > 1 ? src.cols[vcols[1]].data : nullptr, vphys, nv, mm, src.n, seg,
-                                                R, (unsigned long long *)cs->p, (dev::AggState *)s0->p,
-                                                (dev::AggState *)s1->p, 0, e.stream, gp.n ? &gp : nullptr,
+                                                R, (unsigned long long *)cs->p, s0p,
+                                                s1p, 0, e.stream, gp.n ? &gp : nullptr,
                                                 maxabs < ((i128)1 << 62) ? (uint64_t)maxabs : ~0ull, vvalid);
           }
           if (!launched) goto generic;
           auto list = Alloc(e, nslots * 4);
           dev::CompactSlots((const unsigned long long *)cs->p, nslots, (int32_t *)list->p, e.d_scratch, e.stream);
-          int64_t ngroups = ReadDev<int64_t>(e, e.d_scratch);
+          // outputs sized for every slot (<= 1024 rows): the emit reads the group
+          // count from the device, so the query waits on the stream once, after it
           dev::EmitDesc D;
           memset(&D, 0, sizeof(D));
           D.nagg = na;
           D.cstar = (const unsigned long long *)cs->p;
           D.slot_list = (const int32_t *)list->p;
           D.n_list = e.d_scratch;
-          D.nslots = ngroups;
+          D.nslots = nslots;
           D.has_key = 1;
           D.key_phys = PhysOf(s.groups[0]->type);
           D.kmin = (int64_t)ks->imin;
           D.null_slot = -1;
-          DCol kc = AllocOut(e, s.groups[0]->type, ngroups, true, false);
+          DCol kc = AllocOut(e, s.groups[0]->type, nslots, true, false);
           D.key_out = kc.data;
           D.key_valid = (uint32_t *)kc.validity;
-          out.n = ngroups;
           out.cols.push_back(kc);
           for (int j = 0; j < na; j++) {
-            DCol oc = AllocOut(e, s.aggs[j].type, ngroups, true, false);
+            DCol oc = AllocOut(e, s.aggs[j].type, nslots, true, false);
             dev::AggState *stp = nullptr;
             if (s.aggs[j].kind != A_COUNT_STAR) {
               int c = StripWidening(s.aggs[j].arg.get())->col;
-              stp = c == vcols[0] ? (dev::AggState *)s0->p : (dev::AggState *)s1->p;
+              stp = c == vcols[0] ? s0p : s1p;
             }
             D.a[j] = EmitFor(s.aggs[j], VC_I64, stp, oc);
             out.cols.push_back(oc);
           }
           dev::EmitAggRelation(D, e.stream);
-          HIPCHK(hipStreamSynchronize(e.stream));  // state buffers released after emit
+          out.n = ReadDev<int64_t>(e, e.d_scratch);  // its synchronisation also covers the emit (state buffers)
           return out;
         }
       }
