@@ -362,9 +362,11 @@ static int64_t Words64(int64_t n) { return (n + 63) / 64; }
 static void RaiseDeviceError(Engine &e, int32_t err);
 
 static void CheckError(Engine &e) {
-  int32_t err = 0;
-  HIPCHK(hipMemcpyAsync(&err, e.d_err, sizeof(int32_t), hipMemcpyDeviceToHost, e.stream));
+  // through the pinned arena: a pageable destination would take HIP's staged copy
+  HIPCHK(hipMemcpyAsync(e.h_pinned, e.d_err, sizeof(int32_t), hipMemcpyDeviceToHost, e.stream));
   HIPCHK(hipStreamSynchronize(e.stream));
+  int32_t err;
+  memcpy(&err, e.h_pinned, sizeof(err));
   RaiseDeviceError(e, err);
 }
 
@@ -1123,6 +1125,7 @@ static bool TrySelectOnePass(Engine &e, const DRel &rel, const dev::FilterMultiD
   double bytes = 0;
   for (int i = 0; i < S.ncol; i++) bytes += (double)n * S.col[i].w + (S.col[i].valid ? n / 8.0 : 0);
   int64_t nsel = 0;
+  int32_t rounds_err = -1;  // the error word read with the round total (-1: not read)
   if (mode != 2) {
     std::unique_lock<std::mutex> lk(g_rounds_mu[e.device & 63]);
     const size_t need = dev::SelectRoundsCtlBytes(plan);
@@ -1197,9 +1200,14 @@ static bool TrySelectOnePass(Engine &e, const DRel &rel, const dev::FilterMultiD
                 worst);
       }
     }
+    // {abort word, total} and the device error word in one synchronisation
+    // (pinned arena: a pageable destination would take HIP's staged copy)
     unsigned long long h[2];
-    HIPCHK(hipMemcpyAsync(h, e.d_rounds, sizeof(h), hipMemcpyDeviceToHost, e.stream));
+    HIPCHK(hipMemcpyAsync(e.h_pinned, e.d_rounds, sizeof(h), hipMemcpyDeviceToHost, e.stream));
+    HIPCHK(hipMemcpyAsync(e.h_pinned + 16, e.d_err, sizeof(int32_t), hipMemcpyDeviceToHost, e.stream));
     HIPCHK(hipStreamSynchronize(e.stream));
+    memcpy(h, e.h_pinned, sizeof(h));
+    memcpy(&rounds_err, e.h_pinned + 16, sizeof(rounds_err));
     lk.unlock();
     if (h[0] == (unsigned long long)epoch) {  // a workgroup was never scheduled: two-pass form instead
       if (e.profile && !e.events.empty() && e.events.back().name == "select_rounds") e.events.back().name = "select_rounds_abort";
@@ -1239,7 +1247,10 @@ static bool TrySelectOnePass(Engine &e, const DRel &rel, const dev::FilterMultiD
   out = DRel();
   out.n = nsel;
   out.cols = cols;
-  CheckError(e);
+  bool packed = false;
+  for (int k = 0; k < S.nout; k++) packed |= S.vdst[k] != nullptr;
+  if (rounds_err >= 0 && !packed) RaiseDeviceError(e, rounds_err);  // nothing ran after that read
+  else CheckError(e);
   return true;
 }
 
