@@ -81,6 +81,7 @@ _sig("duckdb_mbx_append_commit", _I, _P, _L)
 _sig("duckdb_mbx_hbm_calibrate", _I, _P, _L, _I, ctypes.POINTER(ctypes.c_double))
 _sig("duckdb_mbx_hbm_calibrate_ex", _I, _P, _L, _I, ctypes.POINTER(ctypes.c_double), _I)
 _sig("duckdb_mbx_statement_plan_stats", _I, _P, ctypes.POINTER(ctypes.c_int64))
+_sig("duckdb_mbx_shard_stats", _I, _P, ctypes.POINTER(ctypes.c_int64), ctypes.POINTER(ctypes.c_double))
 
 for _n in ["duckdb_mb_connect"]:
     _sig(_n, _P, _B)
@@ -580,6 +581,15 @@ class Connection:
         return {"copy_gbs": out[0], "read_nt_gbs": out[1], "read_gbs": out[2], "ring_read_gbs": out[3],
                 "copy_nt4_gbs": out[4], "ring_copy_gbs": out[5], "ring_copy_half_gbs": out[6], "bytes": nbytes}
 
+    def shard_stats(self) -> dict:
+        """Counters of the in-library multi-device path (gpu_devices; extension)."""
+        out = (ctypes.c_int64 * 6)()
+        outd = (ctypes.c_double * 2)()
+        lib.duckdb_mbx_shard_stats(self._h, out, outd)
+        return {"shards": out[0], "peer_links": out[1], "dispatches": out[2], "peer_copies": out[3],
+                "peer_bytes": out[4], "host_results": out[5], "last_dispatch_us": outd[0],
+                "last_combine_us": outd[1]}
+
     def profile_drain(self) -> list:
         import json
         p = lib.duckdb_mbx_profile_drain(self._h)
@@ -889,13 +899,23 @@ class Appender:
         return self._r(lib.duckdb_mb_flush(self._h), "flush")
 
     def append_column(self, col: int, array, validity=None):
-        """Columnar bulk ingest (extension): `array` is a contiguous numpy array
-        in the column's physical layout."""
+        """Columnar bulk ingest (extension): `array` is a numpy array in the
+        column's physical layout.  The library keeps only the pointers until
+        commit(), so the (contiguous) arrays are held here until then."""
+        import numpy as np
+        array = np.ascontiguousarray(array)
+        if validity is not None:
+            validity = np.ascontiguousarray(validity, dtype=np.uint8)
+        if not hasattr(self, "_held"):
+            self._held = {}
+        self._held[col] = (array, validity)
         vp = validity.ctypes.data if validity is not None else None
         return self._r(lib.duckdb_mbx_append_column(self._h, col, array.ctypes.data, vp, len(array)), "append_column")
 
     def commit(self, count: int):
-        return self._r(lib.duckdb_mbx_append_commit(self._h, count), "append_commit")
+        r = self._r(lib.duckdb_mbx_append_commit(self._h, count), "append_commit")
+        self._held = {}  # the rows are on the device (or staged): the host arrays may go
+        return r
 
     def close(self, on_done: Callable = None):
         if self._h:

@@ -111,10 +111,25 @@ struct Options {
   // "mbx_shard_rows": appends fill part i of a sharded table up to this many
   // rows before moving on to part i + 1 (0: appends go to the last part)
   int64_t shard_rows = 0;
+  // "mbx_force_peer" (tests): shards on the same device still exchange row
+  // results by peer DMA (hipMemcpyPeerAsync), as distinct devices do
+  bool force_peer = false;
   std::map<std::string, std::string> raw;
 };
 
-struct Engine;  // per-connection executor state (device stream, scratch)
+struct Engine;        // per-connection executor state (device stream, scratch)
+struct ShardWorkers;  // persistent per-shard host threads (executor.cpp)
+
+// Counters of the multi-device path (duckdb_mbx_shard_stats).
+struct ShardStats {
+  int64_t dispatches = 0;    // ForShards calls (one per sharded statement step)
+  int64_t peer_links = 0;    // device pairs with peer access enabled at connect
+  int64_t peer_copies = 0;   // buffers moved between shards by peer DMA
+  int64_t peer_bytes = 0;
+  int64_t host_results = 0;  // sharded aggregates finished on the host (no re-upload)
+  double last_dispatch_us = 0;  // wall time of the last ForShards (all shards' work)
+  double last_combine_us = 0;   // host merge of the last sharded aggregate
+};
 
 struct Connection {
   Options opts;
@@ -126,6 +141,8 @@ struct Connection {
   // the table parts) per entry; this connection's engine (on the first device)
   // combines their results
   std::vector<std::unique_ptr<Connection>> shards;
+  std::shared_ptr<ShardWorkers> workers;  // declared after shards: stopped before they go
+  ShardStats shard_stats;
   bool sharded() const { return !shards.empty(); }
   ~Connection();
 };

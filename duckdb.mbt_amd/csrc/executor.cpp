@@ -10,11 +10,15 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <atomic>
 #include <chrono>
 #include <cmath>
+#include <condition_variable>
 #include <cstring>
 #include <functional>
+#include <limits>
 #include <map>
+#include <unordered_map>
 #include <mutex>
 #include <sstream>
 #include <thread>
@@ -24,6 +28,7 @@
 #include "engine.h"
 #include "hostlink.h"
 #include "vm.h"
+#include "knobs.h"
 
 namespace mbx {
 
@@ -154,6 +159,9 @@ struct Engine {
   };
   std::vector<PendingStat> pending_stats;
   std::vector<long long *> stat_slots;  // free pinned 3-value slots
+  // an async append's DMA from a pinned appender buffer is in flight: the next
+  // SettlePending waits for it, so the buffer is never refilled under the DMA
+  bool inflight_h2d = false;
   bool profile = false;
   std::vector<ProfEvent> events;
   // kernels timed on shard engines during this query (gpu_devices)
@@ -246,8 +254,9 @@ std::shared_ptr<Engine> CreateEngine(int device, bool allow_no_gpu) {
 // folds the zone-map statistics of in-flight appends into their columns
 // (after the stream has drained: their DMAs and reductions are done)
 static void SettlePending(Engine &e) {
-  if (e.pending_stats.empty()) return;
+  if (e.pending_stats.empty() && !e.inflight_h2d) return;
   HIPCHK(hipStreamSynchronize(e.stream));
+  e.inflight_h2d = false;
   for (auto &ps : e.pending_stats) {
     DevColumn &c = *ps.col;
     const long long *h = ps.h;
@@ -1029,8 +1038,8 @@ static bool FastIntCol(const DRel &rel, int c) {
 // One-pass forms of the compaction below, for 4/8-byte columns, at most
 // SL_MAX_COL distinct loaded columns (predicates ∪ outputs) and SL_MAX_OUT
 // outputs.  NULL-able columns take the round-synchronous form only: a NULL
-// fails a predicate, and a NULL-able output's validity comes back as one byte
-// per output row, packed into its bitmap afterwards (dev::PackValidityBytes).  Each loaded column is read from HBM once; outputs are
+// fails a predicate, and a NULL-able output's bitmap is written by the
+// kernel's storers (ballots per output word, boundary words ORed).  Each loaded column is read from HBM once; outputs are
 // allocated for every row (the count is known only afterwards), so the form
 // is used while that upper bound stays under MBX_SL_MAX_GB (default 64).
 //  * default (n >= MBX_SR_MIN_ROWS, default 2^22): dev::SelectRounds, the
@@ -1046,11 +1055,11 @@ static std::mutex g_rounds_mu[64];
 
 static bool TrySelectOnePass(Engine &e, const DRel &rel, const dev::FilterMultiDesc &F,
                              const std::vector<BExprPtr> &exprs, DRel &out) {
-  const char *env = getenv("MBX_SL");
+  const char *env = Knob("MBX_SL");
   const int mode = env ? atoi(env) : 1;
   if (mode == 0) return false;
   int64_t min_rows = (int64_t)1 << 22;
-  if (const char *m = getenv("MBX_SR_MIN_ROWS")) min_rows = atoll(m);
+  if (const char *m = Knob("MBX_SR_MIN_ROWS")) min_rows = atoll(m);
   if (mode == 1 && rel.n < min_rows) return false;
   if ((int)exprs.size() > SL_MAX_OUT) return false;
   dev::SelectDesc S;
@@ -1075,7 +1084,7 @@ static bool TrySelectOnePass(Engine &e, const DRel &rel, const dev::FilterMultiD
     S.col[i].span = F.col[j].span;
   }
   double out_bytes = 0;
-  const char *nenv = getenv("MBX_SR_NARROW");
+  const char *nenv = Knob("MBX_SR_NARROW");
   const bool narrow_ok = !(nenv && atoi(nenv) == 0);
   for (auto &x : exprs) {
     const DCol &c = rel.cols[x->col];
@@ -1095,14 +1104,14 @@ static bool TrySelectOnePass(Engine &e, const DRel &rel, const dev::FilterMultiD
       S.col[i].narrow = 1;
   }
   if (any_valid) {  // MBX_SR_NULLS=0: NULL-able shapes keep the two-pass form (A/B tests)
-    const char *nv = getenv("MBX_SR_NULLS");
+    const char *nv = Knob("MBX_SR_NULLS");
     if (nv && atoi(nv) == 0) return false;
   }
   int ni = 0;
   for (int i = 0; i < S.ncol; i++) ni += S.col[i].w / 4;
   if (ni > 8) return false;
   double cap_gb = 64;
-  if (const char *c = getenv("MBX_SL_MAX_GB")) cap_gb = atof(c);
+  if (const char *c = Knob("MBX_SL_MAX_GB")) cap_gb = atof(c);
   if (out_bytes > cap_gb * 1e9) return false;
   const int64_t n = rel.n;
   dev::SelectRoundsPlan plan;
@@ -1112,14 +1121,13 @@ static bool TrySelectOnePass(Engine &e, const DRel &rel, const dev::FilterMultiD
     if (!plan.ok) return false;
   }
   std::vector<DCol> cols;
-  std::vector<DevBufPtr> vbytes(exprs.size());  // NULL-able outputs: one validity byte per output row
   for (int k = 0; k < (int)exprs.size(); k++) {
     const bool nullable = rel.cols[exprs[k]->col].validity != nullptr;
     cols.push_back(AllocOut(e, exprs[k]->type, n, nullable, false));
     S.dst[k] = cols[k].data;
-    if (nullable) {  // (released to the engine's pool when this returns: later users run after the pack on e.stream)
-      vbytes[k] = Alloc(e, (size_t)std::max<int64_t>(n, 1) + 64);
-      S.vdst[k] = (uint8_t *)vbytes[k]->p;
+    if (nullable) {  // the storers write the bitmap itself: ORed boundary words need a zeroed start
+      S.vbits[k] = cols[k].validity;
+      HIPCHK(hipMemsetAsync(cols[k].validity, 0, (size_t)Words64(std::max<int64_t>(n, 1)) * 8, e.stream));
     }
   }
   double bytes = 0;
@@ -1146,18 +1154,24 @@ static bool TrySelectOnePass(Engine &e, const DRel &rel, const dev::FilterMultiD
     }
     const uint32_t epoch = e.rounds_epoch;
     DevBufPtr dbgbuf, tsbuf;
-    if (getenv("MBX_SR_DEBUG")) {
+    if (Knob("MBX_SR_DEBUG")) {
       dbgbuf = Alloc(e, 256, true);
       HIPCHK(hipMemsetAsync(dbgbuf->p, 0, 256, e.stream));
       S.dbg = (unsigned long long *)dbgbuf->p;
-      if (atoi(getenv("MBX_SR_DEBUG")) == 2) {
+      if (atoi(Knob("MBX_SR_DEBUG")) == 2) {
         tsbuf = Alloc(e, (size_t)plan.nrounds * plan.G * 8, true);
         S.dbg_ts = (unsigned long long *)tsbuf->p;
       }
     }
+    hipError_t launch;
     {
       ProfScope ps(e, "select_rounds", bytes, n);  // algorithmic: inputs once (+ the selected rows' outputs, added below)
-      dev::SelectRounds(S, plan, n, e.d_rounds, epoch, e.stream);
+      launch = dev::SelectRounds(S, plan, n, e.d_rounds, epoch, e.stream);
+    }
+    if (launch != hipSuccess) {  // nothing ran: the control block still holds the last launch's total
+      if (e.profile && !e.events.empty() && e.events.back().name == "select_rounds")
+        e.events.back().name = "select_rounds_launch_failed";
+      return false;  // the two-pass form instead
     }
     if (dbgbuf) {
       unsigned long long h[13];
@@ -1217,7 +1231,7 @@ static bool TrySelectOnePass(Engine &e, const DRel &rel, const dev::FilterMultiD
   } else {
     auto status = Alloc(e, dev::SelectStatusBytes(n, ni));
     DevBufPtr dbgbuf;
-    if (getenv("MBX_SL_DEBUG")) {
+    if (Knob("MBX_SL_DEBUG")) {
       dbgbuf = Alloc(e, 128, true);
       S.dbg = (unsigned long long *)dbgbuf->p;
     }
@@ -1236,20 +1250,13 @@ static bool TrySelectOnePass(Engine &e, const DRel &rel, const dev::FilterMultiD
   }
   if (e.profile && !e.events.empty() && (e.events.back().name == "select" || e.events.back().name == "select_rounds")) {
     double ob = 0;
-    for (int k = 0; k < S.nout; k++) ob += (double)nsel * (S.col[S.out_col[k]].w + (S.vdst[k] ? 1 : 0));
+    for (int k = 0; k < S.nout; k++) ob += (double)nsel * (S.col[S.out_col[k]].w + (S.vbits[k] ? 0.125 : 0));
     e.events.back().bytes += ob;
-  }
-  for (int k = 0; k < S.nout; k++) {
-    if (!S.vdst[k]) continue;
-    ProfScope ps(e, "pack_validity", (double)nsel + nsel / 8.0, nsel);
-    dev::PackValidityBytes(S.vdst[k], nsel, cols[k].validity, e.stream);
   }
   out = DRel();
   out.n = nsel;
   out.cols = cols;
-  bool packed = false;
-  for (int k = 0; k < S.nout; k++) packed |= S.vdst[k] != nullptr;
-  if (rounds_err >= 0 && !packed) RaiseDeviceError(e, rounds_err);  // nothing ran after that read
+  if (rounds_err >= 0) RaiseDeviceError(e, rounds_err);  // nothing ran after that read
   else CheckError(e);
   return true;
 }
@@ -1262,7 +1269,7 @@ static bool TrySelectOnePass(Engine &e, const DRel &rel, const dev::FilterMultiD
 // storing its chunk as one contiguous run.  MBX_CC=0 keeps the bits form.
 static bool TryCountFirst(Engine &e, const DRel &rel, const dev::FilterMultiDesc &F,
                           const std::vector<BExprPtr> &exprs, DRel &out) {
-  const char *env = getenv("MBX_CC");
+  const char *env = Knob("MBX_CC");
   if (env && atoi(env) == 0) return false;
   if ((int)exprs.size() > FC_MAX_OUT) return false;
   dev::CompactDesc C;
@@ -1326,7 +1333,7 @@ static bool TryCountFirst(Engine &e, const DRel &rel, const dev::FilterMultiDesc
 // vm_project.  A NULL in a predicate column fails the row.  MBX_FC=0 disables it.
 static bool TryFilterCompact(Engine &e, const DRel &rel, const BExpr &pred, const std::vector<BExprPtr> &exprs,
                              DRel &out) {
-  const char *fc = getenv("MBX_FC");
+  const char *fc = Knob("MBX_FC");
   if ((fc && atoi(fc) == 0) || rel.range || rel.n <= 0 || exprs.empty()) return false;
   std::map<int, std::pair<i128, i128>> ranges;
   if (!RangeConj(pred, ranges) || ranges.empty() || ranges.size() > FM_MAX) return false;
@@ -1922,10 +1929,86 @@ static bool JitGroupAggregate(Engine &e, const DRel &src, const BoundSelect &s, 
   return true;
 }
 
+static ResultPtr ToHost(Engine &e, const DRel &r, const std::vector<std::string> &names, int64_t offset, int64_t limit,
+                        size_t ncols);
+static void KeyBytes(const Value &v, std::string &out);
+static DRel Aggregate(Engine &e, const DRel &src, const BoundSelect &s);
+
+// COUNT(DISTINCT arg) (the binder keeps DISTINCT only on COUNT; MIN/MAX
+// DISTINCT are plain MIN/MAX).  Per distinct aggregate, two device
+// aggregations: the distinct (groups..., arg) pairs of the filtered source (a
+// GROUP BY with no aggregates of its own), then COUNT(arg) of those pairs per
+// group (a NULL arg is one pair and is not counted).  The other aggregates
+// come from one pass with COUNT(arg) in the distinct ones' places; the
+// per-group distinct counts (one row per group) are merged into that relation
+// on the host by group key (KeyBytes, as the sharded combine does) and the
+// relation is uploaded back in the main pass's group order.
+static DRel DistinctAggregate(Engine &e, const DRel &src, const BoundSelect &s) {
+  const int ng = (int)s.groups.size(), na = (int)s.aggs.size();
+  BoundSelect m = s;
+  for (auto &a : m.aggs) a.distinct = false;
+  const DRel main = Aggregate(e, src, m);
+  std::vector<std::string> names(ng + na, "");
+  const ResultPtr mh = ToHost(e, main, names, 0, -1, (size_t)(ng + na));
+  std::vector<std::vector<Value>> rows((size_t)mh->nrows);
+  std::vector<std::string> keys((size_t)mh->nrows);
+  std::map<std::string, size_t> at;
+  for (int64_t r = 0; r < mh->nrows; r++) {
+    for (int c = 0; c < ng + na; c++) rows[r].push_back(mh->cols[c].Get(r));
+    for (int c = 0; c < ng; c++) KeyBytes(rows[r][c], keys[r]);
+    at[keys[r]] = (size_t)r;
+  }
+  for (int j = 0; j < na; j++) {
+    if (!s.aggs[j].distinct) continue;
+    BoundSelect p;
+    p.where = s.where;
+    p.is_agg = true;
+    p.groups = s.groups;
+    p.groups.push_back(s.aggs[j].arg);
+    AggSpec cs;
+    cs.kind = A_COUNT_STAR;
+    cs.type = LogicalType(T_BIGINT);
+    p.aggs.push_back(cs);
+    const DRel pairs = Aggregate(e, src, p);  // [groups..., arg, COUNT(*)]
+    BoundSelect q;
+    q.is_agg = true;
+    for (int c = 0; c <= ng; c++) {
+      auto col = std::make_shared<BExpr>();
+      col->kind = BExpr::COL;
+      col->col = c;
+      col->type = c < ng ? s.groups[c]->type : s.aggs[j].arg->type;
+      if (c < ng) q.groups.push_back(col);
+      else {
+        AggSpec cnt;
+        cnt.kind = A_COUNT;
+        cnt.arg = col;
+        cnt.type = LogicalType(T_BIGINT);
+        q.aggs.push_back(cnt);
+      }
+    }
+    const DRel per = Aggregate(e, pairs, q);  // [groups..., COUNT(DISTINCT arg)]
+    std::vector<std::string> pn(ng + 1, "");
+    const ResultPtr ph = ToHost(e, per, pn, 0, -1, (size_t)(ng + 1));
+    for (auto &row : rows) row[ng + j] = Value::Int(T_BIGINT, 0);  // groups whose args are all NULL
+    for (int64_t r = 0; r < ph->nrows; r++) {
+      std::string kb;
+      for (int c = 0; c < ng; c++) KeyBytes(ph->cols[c].Get(r), kb);
+      auto it = at.find(kb);
+      if (it != at.end()) rows[it->second][ng + j] = Value::Int(T_BIGINT, (int64_t)ph->cols[ng].Get(r).i);
+    }
+  }
+  std::vector<LogicalType> types;
+  for (auto &g : s.groups) types.push_back(g->type);
+  for (auto &a : s.aggs) types.push_back(a.type);
+  return UploadRows(e, rows, types);
+}
+
 static DRel Aggregate(Engine &e, const DRel &src, const BoundSelect &s) {
   const int ng = (int)s.groups.size();
   const int na = (int)s.aggs.size();
   if (na > EMIT_MAX_AGGS) ThrowError("Not implemented", "too many aggregates in one query for the device path");
+  for (auto &a : s.aggs)
+    if (a.distinct) return DistinctAggregate(e, src, s);
   DRel out;
   // ---- fast path F1: no GROUP BY, range predicate on one int column, all
   //      aggregates over one int column (or COUNT(*)).
@@ -2048,7 +2131,7 @@ static DRel Aggregate(Engine &e, const DRel &src, const BoundSelect &s) {
     const uint64_t *vvalid = nullptr;
     for (int c : vcols)
       if (src.cols[c].validity) {
-        const char *gn = getenv("MBX_GD_NULLS");  // MBX_GD_NULLS=0: NULL-able values keep the generic paths
+        const char *gn = Knob("MBX_GD_NULLS");  // MBX_GD_NULLS=0: NULL-able values keep the generic paths
         if (vcols.size() != 1 || (gn && atoi(gn) == 0)) ok = false;
         vvalid = src.cols[c].validity;
       }
@@ -2484,7 +2567,7 @@ static ResultPtr ToHostPinned(Engine &e, const DRel &r, const std::vector<std::s
   }
   // small results: one copy kernel into the coherent mapped buffer instead of
   // one DMA per buffer; larger ones: DMA into the (growable) pinned arena
-  const bool mapped = need <= Engine::kMappedBytes && ncols * 2 <= HOSTCOPY_MAX && !getenv("MBX_NO_HOSTCOPY");
+  const bool mapped = need <= Engine::kMappedBytes && ncols * 2 <= HOSTCOPY_MAX && !Knob("MBX_NO_HOSTCOPY");
   if (!mapped && !e.EnsurePinned(need)) return nullptr;
   uint8_t *const H = mapped ? e.h_mapped : e.h_pinned;
   std::vector<size_t> data_off(ncols), valid_off(ncols, 0);
@@ -2779,6 +2862,8 @@ static ResultPtr HostConstantSelect(const BoundSelect &s) {
   return res;
 }
 
+static ResultPtr ShardedAggregateHost(Connection &c, const BoundSelect &s);
+
 static void FinishProfile(Connection &c, Engine &e, double total_ms) {
   QueryProfile &p = c.last_profile;
   p.kernels.clear();
@@ -2821,6 +2906,13 @@ ResultPtr ExecuteSelect(Connection &c, const BoundSelect &s) {
   e.events.clear();
   e.plan_text = c.opts.profile ? ExplainSelect(s) : "";
   e.ev_used = 0;
+  if (c.sharded()) {
+    if (ResultPtr hr = ShardedAggregateHost(c, s)) {
+      double ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+      FinishProfile(c, e, ms);
+      return hr;
+    }
+  }
   DRel r = RunSelectDev(e, c, s);
   std::vector<std::string> names(s.names.begin(), s.names.begin() + VisibleCols(s));
   ResultPtr res = ToHost(e, r, names, 0, -1, names.size());  // raises pending device errors
@@ -3235,22 +3327,88 @@ static void AppendCast(Engine &e, Table &t, DRel r, const std::vector<int> &col_
 // The cross-process form of the same combine (one process per GPU) is the
 // RCCL all-reduce / all-gather in distributed.py.
 // ---------------------------------------------------------------------------
-static void ForShards(Connection &c, const std::function<void(int)> &f) {
-  const int n = (int)c.shards.size();
-  std::vector<std::exception_ptr> errs(n);
+// One persistent host thread per shard 1..n-1 (shard 0 runs on the calling
+// thread).  A dispatch bumps a generation word; a worker that finished its
+// last job spins on it for up to kSpinUs (back-to-back queries re-dispatch
+// within tens of microseconds) and otherwise sleeps on the condition
+// variable.  Each worker keeps its shard's device current (HIP's current
+// device and the scratch allocator are per thread).
+struct ShardWorkers {
+  static constexpr int kSpinUs = 300;
+  const int n;
   std::vector<std::thread> th;
-  th.reserve(n);
-  for (int i = 0; i < n; i++)
-    th.emplace_back([&, i] {
+  std::mutex mu;
+  std::condition_variable cv;
+  std::atomic<uint64_t> gen{0};
+  std::atomic<int> left{0};
+  std::atomic<bool> stop{false};
+  const std::function<void(int)> *job = nullptr;
+  std::vector<std::exception_ptr> errs;
+  explicit ShardWorkers(int nshards) : n(nshards), errs(nshards) {
+    for (int i = 1; i < n; i++) th.emplace_back([this, i] { Loop(i); });
+  }
+  void Loop(int i) {
+    uint64_t seen = 0;
+    for (;;) {
+      const auto t0 = std::chrono::steady_clock::now();
+      int k = 0;
+      while (gen.load(std::memory_order_acquire) == seen && !stop.load(std::memory_order_acquire)) {
+        if ((++k & 63) == 0 &&
+            std::chrono::steady_clock::now() - t0 > std::chrono::microseconds(kSpinUs)) {
+          std::unique_lock<std::mutex> lk(mu);
+          cv.wait(lk, [&] { return gen.load(std::memory_order_acquire) != seen || stop.load(); });
+          break;
+        }
+        __builtin_ia32_pause();
+      }
+      if (stop.load(std::memory_order_acquire)) return;
+      seen = gen.load(std::memory_order_acquire);
       try {
-        f(i);
+        (*job)(i);
       } catch (...) {
         errs[i] = std::current_exception();
       }
-    });
-  for (auto &t : th) t.join();
-  for (auto &x : errs)
-    if (x) std::rethrow_exception(x);
+      left.fetch_sub(1, std::memory_order_acq_rel);
+    }
+  }
+  void Run(const std::function<void(int)> &f) {
+    for (auto &x : errs) x = nullptr;
+    job = &f;
+    left.store(n - 1, std::memory_order_release);
+    {
+      std::lock_guard<std::mutex> g(mu);
+      gen.fetch_add(1, std::memory_order_acq_rel);
+    }
+    cv.notify_all();
+    try {
+      f(0);
+    } catch (...) {
+      errs[0] = std::current_exception();
+    }
+    for (int k = 0; left.load(std::memory_order_acquire) > 0; k++) {
+      if (k < 4096) __builtin_ia32_pause();
+      else std::this_thread::yield();
+    }
+    for (auto &x : errs)
+      if (x) std::rethrow_exception(x);
+  }
+  ~ShardWorkers() {
+    {
+      std::lock_guard<std::mutex> g(mu);
+      stop.store(true, std::memory_order_release);
+    }
+    cv.notify_all();
+    for (auto &t : th) t.join();
+  }
+};
+
+static void ForShards(Connection &c, const std::function<void(int)> &f) {
+  const auto t0 = std::chrono::steady_clock::now();
+  if (!c.workers) c.workers = std::make_shared<ShardWorkers>((int)c.shards.size());
+  c.shard_stats.dispatches++;
+  c.workers->Run(f);
+  c.shard_stats.last_dispatch_us =
+      std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0).count();
 }
 
 static Engine &ShardEngine(Connection &top, Connection &sc) {
@@ -3261,11 +3419,14 @@ static Engine &ShardEngine(Connection &top, Connection &sc) {
   return se;
 }
 
-// a shard's work is done: wait for it, raise its device errors, and hand its
-// kernel timings to the combining engine's profile
-static void ShardCollect(Engine &top, Engine &se) {
-  HIPCHK(hipStreamSynchronize(se.stream));
-  CheckError(se);
+// a shard's work is done: wait for it, raise its device errors (unless the
+// shard's result copy already read its error word after a synchronisation),
+// and hand its kernel timings to the combining engine's profile
+static void ShardCollect(Engine &top, Engine &se, bool checked = false) {
+  if (!checked) {
+    HIPCHK(hipStreamSynchronize(se.stream));
+    CheckError(se);
+  }
   if (!se.profile) return;
   std::vector<QueryProfile::Kernel> ks;
   for (auto &ev : se.events) {
@@ -3284,9 +3445,13 @@ static void ShardCollect(Engine &top, Engine &se) {
   top.shard_kernels.insert(top.shard_kernels.end(), ks.begin(), ks.end());
 }
 
-// r (on src's device, src's stream idle) as buffers of dst's device
-static DRel MoveRel(Engine &dst, Engine &src, const DRel &r) {
-  if (dst.device == src.device) return r;  // same device: readers copy from it directly
+// r (on src's device, src's stream idle) as buffers of dst's device, copied by
+// peer DMA on dst's stream (xGMI between MI355X devices); the caller
+// synchronises dst's stream once for all the moves it queued.  Shards on the
+// same device share r as is, unless the connection forces the peer path
+// (mbx_force_peer, tests).
+static DRel MoveRelAsync(Connection &conn, Engine &dst, Engine &src, const DRel &r) {
+  if (dst.device == src.device && !conn.opts.force_peer) return r;
   DRel out;
   out.n = r.n;
   const int64_t n = r.n;
@@ -3296,7 +3461,11 @@ static DRel MoveRel(Engine &dst, Engine &src, const DRel &r) {
     d.phys = c.phys;
     auto peer = [&](const void *sp, size_t bytes) -> void * {
       auto b = Alloc(dst, std::max<size_t>(bytes, 16));
-      if (bytes) HIPCHK(hipMemcpyPeerAsync(b->p, dst.device, sp, src.device, bytes, dst.stream));
+      if (bytes) {
+        HIPCHK(hipMemcpyPeerAsync(b->p, dst.device, sp, src.device, bytes, dst.stream));
+        conn.shard_stats.peer_copies++;
+        conn.shard_stats.peer_bytes += (int64_t)bytes;
+      }
       d.owners.push_back(b);
       return b->p;
     };
@@ -3310,24 +3479,33 @@ static DRel MoveRel(Engine &dst, Engine &src, const DRel &r) {
     if (c.validity) d.validity = (uint64_t *)peer(c.validity, (size_t)Words64(n) * 8);
     out.cols.push_back(d);
   }
+  return out;
+}
+
+static DRel MoveRel(Connection &c, Engine &dst, Engine &src, const DRel &r) {
+  DRel out = MoveRelAsync(c, dst, src, r);
   HIPCHK(hipStreamSynchronize(dst.stream));
   return out;
 }
 
 // every row of a sharded table on e's device, in part order (the fallback for
-// shapes the partial aggregation does not decompose)
+// shapes the partial aggregation does not decompose): every shard's pending
+// work settled, then all parts' peer copies queued and waited for once
 static DRel GatherShards(Engine &e, Connection &c, const Table &t) {
   std::vector<DRel> parts(t.parts.size());
+  for (size_t i = 0; i < t.parts.size(); i++) {
+    Engine &se = Eng(*c.shards[i]);
+    HIPCHK(hipStreamSynchronize(se.stream));
+  }
+  Eng(c);  // back on the combining device
   for (size_t i = 0; i < t.parts.size(); i++) {
     const Table &p = *t.parts[i];
     DRel r;
     r.n = p.nrows;
     for (auto &col : p.cols) r.cols.push_back(ColFromTable(col));
-    Engine &se = Eng(*c.shards[i]);
-    HIPCHK(hipStreamSynchronize(se.stream));
-    parts[i] = MoveRel(e, se, r);
+    parts[i] = MoveRelAsync(c, e, *c.shards[i]->engine, r);
   }
-  Eng(c);  // back on the combining device
+  HIPCHK(hipStreamSynchronize(e.stream));
   return ConcatRels(e, parts);
 }
 
@@ -3389,7 +3567,11 @@ static double I128ToDoubleLikeDevice(i128 v) {
 
 static int CompareValues(const Value &a, const Value &b) {  // non-NULL values of one type
   switch (ClassOf(a.type)) {
-    case VC_F64: return a.d < b.d ? -1 : a.d > b.d ? 1 : 0;
+    case VC_F64: {  // NaN sorts above every number, as DuckDB orders it
+      const bool an = std::isnan(a.d), bn = std::isnan(b.d);
+      if (an || bn) return an == bn ? 0 : an ? 1 : -1;
+      return a.d < b.d ? -1 : a.d > b.d ? 1 : 0;
+    }
     case VC_STR: return a.s < b.s ? -1 : a.s > b.s ? 1 : 0;
     default: return a.i < b.i ? -1 : a.i > b.i ? 1 : 0;
   }
@@ -3399,7 +3581,13 @@ static void KeyBytes(const Value &v, std::string &out) {
   out.push_back(v.is_null ? '\0' : '\1');
   if (v.is_null) return;
   switch (ClassOf(v.type)) {
-    case VC_F64: out.append((const char *)&v.d, 8); break;
+    case VC_F64: {
+      // one group per value, as on one device: -0.0 joins 0.0, every NaN one NaN
+      double d = v.d == 0.0 ? 0.0 : v.d;
+      if (std::isnan(d)) d = std::numeric_limits<double>::quiet_NaN();
+      out.append((const char *)&d, 8);
+      break;
+    }
     case VC_STR: {
       const uint64_t n = v.s.size();
       out.append((const char *)&n, 8);
@@ -3411,21 +3599,28 @@ static void KeyBytes(const Value &v, std::string &out) {
   if (v.type.id == T_INTERVAL) out.append((const char *)&v.iv, sizeof(v.iv));
 }
 
-static DRel ShardedAggregate(Engine &e, Connection &c, const BoundSelect &s, const BoundSelect &p,
-                             const std::vector<int> &first) {
+// The aggregate relation of a sharded aggregate branch (groups in key order,
+// then one column per aggregate) as host rows: every shard computes its
+// decomposable partials (one small D2H each, on its own worker thread), and
+// the host merges them by key exactly (int128 sums).
+static void ShardedAggregateRows(Connection &c, const BoundSelect &s, const BoundSelect &p,
+                                 const std::vector<int> &first, std::vector<std::vector<Value>> &rows,
+                                 std::vector<LogicalType> &types) {
   const Table &t = *s.src.table;
   const int nsh = (int)t.parts.size(), ng = (int)s.groups.size();
   std::vector<ResultPtr> partial(nsh);
+  Engine &e = *c.engine;
   ForShards(c, [&](int i) {
     Connection &sc = *c.shards[i];
     Engine &se = ShardEngine(c, sc);
     BoundSelect pi = p;
     pi.src.table = t.parts[i];
     DRel r = RunBranch(se, sc, pi);
-    partial[i] = ToHost(se, r, pi.names, 0, -1, pi.names.size());
-    ShardCollect(e, se);
+    partial[i] = ToHost(se, r, pi.names, 0, -1, pi.names.size());  // synchronises and raises device errors
+    ShardCollect(e, se, true);
   });
   Eng(c);
+  const auto t_merge = std::chrono::steady_clock::now();
   // merge by group key, exactly (int128 sums)
   struct Acc {
     int64_t cnt = 0;
@@ -3434,18 +3629,23 @@ static DRel ShardedAggregate(Engine &e, Connection &c, const BoundSelect &s, con
     double sd = 0;
     Value mv;
   };
-  std::map<std::string, size_t> index;
+  size_t total_rows = 0;
+  for (int i = 0; i < nsh; i++) total_rows += (size_t)partial[i]->nrows;
+  std::unordered_map<std::string, size_t> index;
+  index.reserve(total_rows * 2 + 1);
   std::vector<std::vector<Value>> keys;
   std::vector<std::vector<Acc>> accs;
+  keys.reserve(total_rows);
+  accs.reserve(total_rows);
   std::string kb;
+  std::vector<Value> kv(ng);
   for (int i = 0; i < nsh; i++) {
     const MaterializedResult &m = *partial[i];
     for (int64_t row = 0; row < m.nrows; row++) {
       kb.clear();
-      std::vector<Value> kv;
       for (int g = 0; g < ng; g++) {
-        kv.push_back(m.cols[g].Get(row));
-        KeyBytes(kv.back(), kb);
+        kv[g] = m.cols[g].Get(row);
+        KeyBytes(kv[g], kb);
       }
       auto it = index.find(kb);
       size_t gi;
@@ -3502,10 +3702,10 @@ static DRel ShardedAggregate(Engine &e, Connection &c, const BoundSelect &s, con
     }
     return false;
   });
-  std::vector<LogicalType> types;
+  types.clear();
   for (auto &g : s.groups) types.push_back(g->type);
   for (auto &a : s.aggs) types.push_back(a.type);
-  std::vector<std::vector<Value>> rows;
+  rows.clear();
   for (size_t oi : order) {
     std::vector<Value> row = keys[oi];
     for (size_t q = 0; q < s.aggs.size(); q++) {
@@ -3548,7 +3748,56 @@ static DRel ShardedAggregate(Engine &e, Connection &c, const BoundSelect &s, con
       row.push_back(a.kind == A_COUNT_STAR || a.kind == A_COUNT ? Value::Int(T_BIGINT, 0) : Value::Null(a.type));
     rows.push_back(row);
   }
+  c.shard_stats.last_combine_us =
+      std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t_merge).count();
+}
+
+static DRel ShardedAggregate(Engine &e, Connection &c, const BoundSelect &s, const BoundSelect &p,
+                             const std::vector<int> &first) {
+  std::vector<std::vector<Value>> rows;
+  std::vector<LogicalType> types;
+  ShardedAggregateRows(c, s, p, first, rows, types);
   return UploadRows(e, rows, types);
+}
+
+// A top-level SELECT over a sharded table whose result is exactly its merged
+// aggregate relation, columns picked in any order (no HAVING, ORDER BY,
+// LIMIT, UNION or expressions over the aggregates): the merged rows become
+// the host result directly, without a round trip through the combining
+// device.  nullptr when the statement does not have that shape.
+static ResultPtr ShardedAggregateHost(Connection &c, const BoundSelect &s) {
+  if (!(s.src.kind == BoundSource::TABLE && s.src.table && s.src.table->sharded() && s.is_agg)) return nullptr;
+  if (s.having || !s.order.empty() || s.limit >= 0 || s.offset > 0 || !s.union_all.empty() || s.distinct)
+    return nullptr;
+  if ((int)s.src.table->parts.size() != (int)c.shards.size()) return nullptr;
+  const size_t nvis = VisibleCols(s);
+  const size_t nagg = s.groups.size() + s.aggs.size();
+  for (size_t k = 0; k < nvis; k++) {
+    const BExpr &o = *s.outputs[k];
+    if (o.kind != BExpr::COL || o.col < 0 || (size_t)o.col >= nagg) return nullptr;
+    const LogicalType &src = o.col < (int)s.groups.size() ? s.groups[o.col]->type : s.aggs[o.col - s.groups.size()].type;
+    if (!(src == o.type)) return nullptr;
+  }
+  BoundSelect p;
+  std::vector<int> first;
+  if (!PartialSelect(s, p, first)) return nullptr;
+  std::vector<std::vector<Value>> rows;
+  std::vector<LogicalType> types;
+  ShardedAggregateRows(c, s, p, first, rows, types);
+  auto res = std::make_shared<MaterializedResult>();
+  res->nrows = (int64_t)rows.size();
+  for (size_t k = 0; k < nvis; k++) {
+    const int j = s.outputs[k]->col;
+    HostColumn hc;
+    hc.name = s.names[k];
+    hc.type = types[j];
+    hc.phys = PhysOf(hc.type);
+    if (hc.phys == P_STR) hc.offsets.push_back(0);
+    for (auto &row : rows) HostColumnPush(hc, row[j]);
+    res->cols.push_back(std::move(hc));
+  }
+  c.shard_stats.host_results++;
+  return res;
 }
 
 static DRel ShardedBranch(Engine &e, Connection &c, const BoundSelect &s) {
@@ -3582,7 +3831,8 @@ static DRel ShardedBranch(Engine &e, Connection &c, const BoundSelect &s) {
     ShardCollect(e, se);
   });
   Eng(c);
-  for (int i = 0; i < nsh; i++) parts[i] = MoveRel(e, *c.shards[i]->engine, parts[i]);
+  for (int i = 0; i < nsh; i++) parts[i] = MoveRelAsync(c, e, *c.shards[i]->engine, parts[i]);
+  HIPCHK(hipStreamSynchronize(e.stream));
   return ConcatRels(e, parts);
 }
 
@@ -3654,7 +3904,7 @@ static void ShardedInsertSelect(Connection &c, Table &t, const BoundSelect &s, c
   const int k = TargetPart(c, t);
   Engine &se = Eng(*c.shards[k]);
   se.profile = false;
-  AppendCast(se, *t.parts[k], MoveRel(se, e, r), col_map);
+  AppendCast(se, *t.parts[k], MoveRel(c, se, e, r), col_map);
   HIPCHK(hipStreamSynchronize(se.stream));
   SyncRows(t);
 }
@@ -3670,15 +3920,24 @@ void OpenShards(Connection &c) {
     sc->catalog.device = d;
     c.shards.push_back(std::move(sc));
   }
-  for (int a : c.opts.devices)
-    for (int b : c.opts.devices) {
+  // peer access between every pair of distinct devices (xGMI on an MI355X
+  // node), so row results move by peer DMA without host staging
+  std::vector<int> devs = c.opts.devices;
+  std::sort(devs.begin(), devs.end());
+  devs.erase(std::unique(devs.begin(), devs.end()), devs.end());
+  for (int a : devs)
+    for (int b : devs) {
       if (a == b) continue;
       int can = 0;
       hipSetDevice(a);
-      if (hipDeviceCanAccessPeer(&can, a, b) == hipSuccess && can) (void)hipDeviceEnablePeerAccess(b, 0);
+      if (hipDeviceCanAccessPeer(&can, a, b) == hipSuccess && can) {
+        const hipError_t r = hipDeviceEnablePeerAccess(b, 0);
+        if (r == hipSuccess || r == hipErrorPeerAccessAlreadyEnabled) c.shard_stats.peer_links++;
+      }
     }
   (void)hipGetLastError();  // "already enabled" is not an error here
   hipSetDevice(c.engine->device);
+  c.workers = std::make_shared<ShardWorkers>((int)c.shards.size());
 }
 
 void HbmCalibrateConn(Connection &c, int64_t bytes, int iters, double out[7]) {
@@ -3720,7 +3979,7 @@ static void StageH2D(Engine &e, void *dst, const void *src, size_t bytes) {
   // Default: hand the pageable source to the runtime's own staged DMA — 14.5
   // GB/s on the C4 ingest vs 12.6 for this ring with 8 copy threads
   // (MI355X box, 1e8 INT64 rows).  MBX_INGEST=staged selects the ring.
-  const char *mode = getenv("MBX_INGEST");
+  const char *mode = Knob("MBX_INGEST");
   if (!mode || strcmp(mode, "staged") != 0) {
     HIPCHK(hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, e.stream));
     return;
@@ -3751,6 +4010,10 @@ static void StageH2D(Engine &e, void *dst, const void *src, size_t bytes) {
 void AppendRawColumns(Connection &c, Table &t, const std::vector<const void *> &vals,
                       const std::vector<const uint8_t *> &valid, int64_t n, bool sync) {
   if (t.sharded()) {  // into the target part(s), split where a part fills up
+    // the caller reuses the buffer of its previous flush once this returns, and
+    // that flush may have gone to another shard's stream: settle every shard
+    // (Eng of the target shard alone would wait only for its own stream)
+    SettleAppends(c);
     int64_t off = 0;
     while (off < n) {
       const int k = TargetPart(c, t);
@@ -3796,7 +4059,10 @@ void AppendRawColumns(Connection &c, Table &t, const std::vector<const void *> &
     UpdateStats(e, col, old, n, old == 0, !sync);
   }
   t.nrows = old + n;
-  if (!sync) return;  // DMA + stats in flight; SettlePending folds them
+  if (!sync) {  // DMA + stats in flight; SettlePending waits for them and folds the stats
+    e.inflight_h2d = true;
+    return;
+  }
   HIPCHK(hipStreamSynchronize(e.stream));
   CheckError(e);
 }

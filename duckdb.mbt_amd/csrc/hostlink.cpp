@@ -22,6 +22,7 @@
 // default 32 MiB), MBX_LINK_HUGE=0 skips the huge-page advice (never given
 // below 32 MiB).
 #include "hostlink.h"
+#include "knobs.h"
 
 #include <hip/hip_runtime_api.h>
 #include <sys/mman.h>
@@ -39,12 +40,12 @@ namespace mbx {
 namespace {
 
 constexpr size_t kMaxChunk = (size_t)4 << 20;
-constexpr size_t kMinChunk = (size_t)1 << 20;
+constexpr size_t kMinChunk = (size_t)256 << 10;
 constexpr size_t kHugePage = (size_t)2 << 20;
 constexpr int kFreshBytes = 32 << 20;  // glibc's largest mmap threshold
 
 int EnvInt(const char *name, int dflt) {
-  const char *v = getenv(name);
+  const char *v = Knob(name);
   return v && *v ? atoi(v) : dflt;
 }
 

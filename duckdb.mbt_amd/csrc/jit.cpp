@@ -18,6 +18,7 @@
 
 #include "jit_src.h"  // build/jit_src.h: phys.h + vm.h + vm_device.h as one string
 #include "types.h"
+#include "knobs.h"
 
 namespace mbx {
 namespace jit {
@@ -25,7 +26,7 @@ namespace jit {
 namespace {
 
 int Mode() {  // 0 off, 1 async, 2 sync
-  const char *e = getenv("MBX_JIT");
+  const char *e = Knob("MBX_JIT");
   if (!e || !*e) return 1;
   if (!strcmp(e, "0") || !strcmp(e, "off")) return 0;
   if (!strcmp(e, "sync")) return 2;
@@ -314,8 +315,8 @@ static std::string AggSource(const VmProgram &p, const dev::VmCols &cols) {
   // an 8-byte (4-byte) column of a full pair fetched with ONE 16-byte (8-byte)
   // load -- measured no faster (profiles/r01_jit_sweep.log), kept for sweeps.
   int U = 4;
-  if (const char *e = getenv("MBX_JIT_U")) U = atoi(e) == 1 || atoi(e) == 2 || atoi(e) == 8 ? atoi(e) : 4;
-  const char *pe = getenv("MBX_JIT_PAIRS");
+  if (const char *e = Knob("MBX_JIT_U")) U = atoi(e) == 1 || atoi(e) == 2 || atoi(e) == 8 ? atoi(e) : 4;
+  const char *pe = Knob("MBX_JIT_PAIRS");
   const bool pairs = pe && strcmp(pe, "1") == 0;
   const int NR = pairs ? 2 * U : U;
   const int64_t span = pairs ? 2 : 1;
@@ -395,7 +396,7 @@ static std::string AggSource(const VmProgram &p, const dev::VmCols &cols) {
     // the scheduler sinks the hoisted loads when the loop body is short
     // (profiles/r01_jit_sweep.log); MBX_JIT_LEAN=1 selects it.
     int need = 3;
-    if (getenv("MBX_JIT_LEAN") && p.out_phys[j]) need = p.out_phys[j];
+    if (Knob("MBX_JIT_LEAN") && p.out_phys[j]) need = p.out_phys[j];
     o << "    if (sel && !R.nl(" << r << ")) {\n      c" << j << "++;\n";
     if (p.out_class[j] == VC_F64) {
       o << "      const double d = __longlong_as_double(R.lo(" << r << "));\n";
@@ -531,7 +532,7 @@ static std::string GroupSource(const VmProgram &p, const dev::VmCols &cols, cons
   std::ostringstream o;
   const int nr = p.n_regs > 0 ? p.n_regs : 1;
   int U = 4;
-  if (const char *e = getenv("MBX_JIT_GU")) U = atoi(e) == 1 || atoi(e) == 2 || atoi(e) == 8 ? atoi(e) : 4;
+  if (const char *e = Knob("MBX_JIT_GU")) U = atoi(e) == 1 || atoi(e) == 2 || atoi(e) == 8 ? atoi(e) : 4;
   o << kJitPrelude;
   o << "\nstruct LocalRF {\n  int64_t l[" << nr << "], h[" << nr << "];\n  uint8_t n[" << nr
     << "];\n  __device__ __forceinline__ int64_t &lo(int i) { return l[i]; }\n"
@@ -651,7 +652,7 @@ bool VmGroupAggregate(const VmProgram &p, const dev::VmCols &cols, const GroupSp
     if (p.out_reg[j] != 255 && p.out_class[j] != VC_I64) return false;
   // replicas: as many as fit 48 KiB (3 blocks per CU), at least one in 64 KiB
   int R = 64;
-  if (const char *e = getenv("MBX_JIT_GR")) R = atoi(e) >= 1 && atoi(e) <= 64 ? atoi(e) : 64;
+  if (const char *e = Knob("MBX_JIT_GR")) R = atoi(e) >= 1 && atoi(e) <= 64 ? atoi(e) : 64;
   while (R > 1 && GroupLdsBytes(p, g.nslots, R) > 48 * 1024) R >>= 1;
   const size_t lds = GroupLdsBytes(p, g.nslots, R);
   if (lds > 64 * 1024) return false;
@@ -675,7 +676,7 @@ bool VmGroupAggregate(const VmProgram &p, const dev::VmCols &cols, const GroupSp
   (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, d);
   if (cus <= 0) cus = 256;
   int bpc = (int)std::min<size_t>(4, (160 * 1024) / std::max<size_t>(lds, 1));
-  if (const char *e = getenv("MBX_JIT_GBPC")) bpc = atoi(e) >= 1 && atoi(e) <= 8 ? atoi(e) : bpc;
+  if (const char *e = Knob("MBX_JIT_GBPC")) bpc = atoi(e) >= 1 && atoi(e) <= 8 ? atoi(e) : bpc;
   if (bpc < 1) bpc = 1;
   int64_t gsz = (nrows + 1023) / 1024;
   if (gsz > (int64_t)cus * bpc) gsz = (int64_t)cus * bpc;
@@ -699,7 +700,7 @@ bool VmAggregate(const VmProgram &p, const dev::VmCols &cols, int64_t nrows, int
   if (cus <= 0) cus = 256;
   // 4 blocks per CU (profiles/r01_jit_sweep.log: 0.384 ms vs 0.408 at 8)
   int bpc = 4;
-  if (const char *e = getenv("MBX_JIT_BPC")) bpc = atoi(e) >= 1 && atoi(e) <= 32 ? atoi(e) : 4;
+  if (const char *e = Knob("MBX_JIT_BPC")) bpc = atoi(e) >= 1 && atoi(e) <= 32 ? atoi(e) : 4;
   int64_t g = (nrows + 255) / 256;
   if (g > (int64_t)cus * bpc) g = (int64_t)cus * bpc;
   return hipModuleLaunchKernel(fn, (unsigned)g, 1, 1, 256, 1, 1, 0, s, args, nullptr) == hipSuccess;

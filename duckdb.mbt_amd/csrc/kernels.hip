@@ -11,6 +11,8 @@
 //     (one replica per lane index -> no same-address conflicts inside a wave).
 #include <hip/hip_runtime.h>
 #include <hipcub/hipcub.hpp>
+#include <algorithm>
+#include <limits>
 #include <stdexcept>
 #include <stdint.h>
 
@@ -18,6 +20,7 @@
 #include "types.h"
 #include "vm.h"
 #include "vm_device.h"
+#include "knobs.h"
 
 namespace mbx {
 namespace dev {
@@ -419,7 +422,7 @@ __global__ __launch_bounds__(256) void filter_agg_v4_kernel(const TP *__restrict
 #pragma unroll
       for (int e = 0; e < 4; e++) {
         int64_t x = pv[u][e];
-        bool ok = (uint64_t)(x - lo) <= span;
+        bool ok = (uint64_t)(x) - (uint64_t)(lo) <= span;
         if (MODE == 2) acc_count(A, ok);
         else if (MODE == 1) acc_add(A, ok, av[u][e]);
         else acc_add(A, ok, x);
@@ -431,7 +434,7 @@ __global__ __launch_bounds__(256) void filter_agg_v4_kernel(const TP *__restrict
     if (MODE == 1) Vec4<TA, NT>::load(a, g, av);
 #pragma unroll
     for (int e = 0; e < 4; e++) {
-      bool ok = (uint64_t)(pv[e] - lo) <= span;
+      bool ok = (uint64_t)(pv[e]) - (uint64_t)(lo) <= span;
       if (MODE == 2) acc_count(A, ok);
       else acc_add(A, ok, MODE == 1 ? av[e] : pv[e]);
     }
@@ -440,7 +443,7 @@ __global__ __launch_bounds__(256) void filter_agg_v4_kernel(const TP *__restrict
   int64_t tail = (ngroups << 2) + (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (tail < n) {
     int64_t x = p[tail];
-    bool ok = (uint64_t)(x - lo) <= span;
+    bool ok = (uint64_t)(x) - (uint64_t)(lo) <= span;
     if (MODE == 2) acc_count(A, ok);
     else acc_add(A, ok, MODE == 1 ? (int64_t)a[tail] : x);
   }
@@ -477,7 +480,7 @@ __global__ __launch_bounds__(256) void filter_agg_kernel(const TP *__restrict__ 
     }
 #pragma unroll
     for (int u = 0; u < UNROLL; u++) {
-      bool ok0 = (uint64_t)(p0[u] - lo) <= span, ok1 = (uint64_t)(p1[u] - lo) <= span;
+      bool ok0 = (uint64_t)(p0[u]) - (uint64_t)(lo) <= span, ok1 = (uint64_t)(p1[u]) - (uint64_t)(lo) <= span;
       if (MODE == 2) {
         acc_count(A, ok0);
         acc_count(A, ok1);
@@ -494,7 +497,7 @@ __global__ __launch_bounds__(256) void filter_agg_kernel(const TP *__restrict__ 
     int64_t x0, x1, y0 = 0, y1 = 0;
     Pair<TP, NT>::load(p, g, x0, x1);
     if (MODE == 1) Pair<TA, NT>::load(a, g, y0, y1);
-    bool ok0 = (uint64_t)(x0 - lo) <= span, ok1 = (uint64_t)(x1 - lo) <= span;
+    bool ok0 = (uint64_t)(x0) - (uint64_t)(lo) <= span, ok1 = (uint64_t)(x1) - (uint64_t)(lo) <= span;
     if (MODE == 2) {
       acc_count(A, ok0);
       acc_count(A, ok1);
@@ -506,7 +509,7 @@ __global__ __launch_bounds__(256) void filter_agg_kernel(const TP *__restrict__ 
   // odd last row: first thread of block 0
   if ((n & 1) && blockIdx.x == 0 && threadIdx.x == 0) {
     int64_t x = p[n - 1];
-    bool ok = (uint64_t)(x - lo) <= span;
+    bool ok = (uint64_t)(x) - (uint64_t)(lo) <= span;
     if (MODE == 2) acc_count(A, ok);
     else acc_add(A, ok, MODE == 1 ? (int64_t)a[n - 1] : x);
   }
@@ -595,7 +598,7 @@ __global__ __launch_bounds__(256) void filter_agg_lds_kernel(const T *__restrict
     if (NS == 2)
       __builtin_amdgcn_global_load_lds((const void *)(A2 + q * 64 + lane), (void *)(slot0 + (DEPTH + k) * 64), 16, 0, 2);
     if (sizeof(T) == 8) {
-      bool ok0 = (uint64_t)(x.x - lo) <= span, ok1 = (uint64_t)(x.y - lo) <= span;
+      bool ok0 = (uint64_t)(x.x) - (uint64_t)(lo) <= span, ok1 = (uint64_t)(x.y) - (uint64_t)(lo) <= span;
       if (MODE == 2) {
         acc_count(A, ok0);
         acc_count(A, ok1);
@@ -607,7 +610,7 @@ __global__ __launch_bounds__(256) void filter_agg_lds_kernel(const T *__restrict
       const int *xi = (const int *)&x, *yi = (const int *)&y;
 #pragma unroll
       for (int e = 0; e < 4; e++) {
-        bool ok = (uint64_t)((int64_t)xi[e] - lo) <= span;
+        bool ok = (uint64_t)((int64_t)xi[e]) - (uint64_t)(lo) <= span;
         if (MODE == 2) acc_count(A, ok);
         else row(ok, (int64_t)(MODE == 1 ? yi[e] : xi[e]));
       }
@@ -618,7 +621,7 @@ __global__ __launch_bounds__(256) void filter_agg_lds_kernel(const T *__restrict
   if (blockIdx.x == 0 && w == 0) {
     for (int64_t i = npieces * RP + lane; i < n; i += 64) {
       int64_t xv = p[i];
-      bool ok = (uint64_t)(xv - lo) <= span;
+      bool ok = (uint64_t)(xv) - (uint64_t)(lo) <= span;
       if (MODE == 2) acc_count(A, ok);
       else row(ok, MODE == 1 ? (int64_t)a[i] : xv);
     }
@@ -738,7 +741,7 @@ __global__ __launch_bounds__(256) void filter_multi_lds_kernel(FilterMultiDesc D
       bool ok = (vm >> e) & 1u;
 #pragma unroll
       for (int c = 0; c < FM_MAX; c++)
-        if (c < D.ncol && D.col[c].is_pred) ok = ok && (uint64_t)(v[c][e] - D.col[c].lo) <= D.col[c].span;
+        if (c < D.ncol && D.col[c].is_pred) ok = ok && (uint64_t)(v[c][e]) - (uint64_t)(D.col[c].lo) <= D.col[c].span;
       int64_t val = 0;
 #pragma unroll
       for (int c = 0; c < FM_MAX; c++)
@@ -755,7 +758,7 @@ __global__ __launch_bounds__(256) void filter_multi_lds_kernel(FilterMultiDesc D
       int64_t val = 0;
       for (int c = 0; c < D.ncol; c++) {
         int64_t x = D.col[c].phys == P_I64 ? ((const int64_t *)D.col[c].data)[i] : (int64_t)((const int32_t *)D.col[c].data)[i];
-        if (D.col[c].is_pred) ok = ok && (uint64_t)(x - D.col[c].lo) <= D.col[c].span;
+        if (D.col[c].is_pred) ok = ok && (uint64_t)(x) - (uint64_t)(D.col[c].lo) <= D.col[c].span;
         if (D.col[c].valid) ok = ok && ((D.col[c].valid[i >> 6] >> (i & 63)) & 1);
         if (c == D.agg) val = x;
       }
@@ -892,7 +895,7 @@ __global__ __launch_bounds__(256) void filter_multi_t_kernel(FilterMultiDesc D, 
     for (int e = 0; e < 4; e++) {
       bool ok = (vm >> e) & 1u;
 #pragma unroll
-      for (int c = 0; c < NC; c++) ok = ok & ((uint64_t)(v[c][e] - lo[c]) <= span[c]);
+      for (int c = 0; c < NC; c++) ok = ok & ((uint64_t)(v[c][e]) - (uint64_t)(lo[c]) <= span[c]);
       const int64_t val = v[0][e];
       if constexpr (MODE == 0) {
         acc_count(A, ok);
@@ -920,7 +923,7 @@ __global__ __launch_bounds__(256) void filter_multi_t_kernel(FilterMultiDesc D, 
       int64_t val = 0;
       for (int c = 0; c < D.ncol; c++) {
         int64_t x = D.col[c].phys == P_I64 ? ((const int64_t *)D.col[c].data)[i] : (int64_t)((const int32_t *)D.col[c].data)[i];
-        if (D.col[c].is_pred) ok = ok && (uint64_t)(x - D.col[c].lo) <= D.col[c].span;
+        if (D.col[c].is_pred) ok = ok && (uint64_t)(x) - (uint64_t)(D.col[c].lo) <= D.col[c].span;
         if (D.col[c].valid) ok = ok && ((D.col[c].valid[i >> 6] >> (i & 63)) & 1);
         if (c == D.agg) val = x;
       }
@@ -1004,8 +1007,8 @@ int FilterMultiPartials(const FilterMultiDesc &d_in, int64_t nrows, AggPartial *
   slot = (slot + 15) & ~15;
   // MBX_FM_DEPTH=<2..4>: ring depth for 3..5 loads per step (sweeps)
   int dp = 2;
-  if (const char *ed = getenv("MBX_FM_DEPTH")) dp = atoi(ed) >= 2 && atoi(ed) <= 4 ? atoi(ed) : 2;
-  const char *ev = getenv("MBX_FM_VARIANT");
+  if (const char *ed = Knob("MBX_FM_DEPTH")) dp = atoi(ed) >= 2 && atoi(ed) <= 4 ? atoi(ed) : 2;
+  const char *ev = Knob("MBX_FM_VARIANT");
   const bool templ = !(ev && strcmp(ev, "generic") == 0) && d.ncol >= 1 && d.ncol <= 4 && (dp == 2 || dp == 3);
   int grid = 0;
   auto plan = [&](int gpc) {
@@ -1018,7 +1021,7 @@ int FilterMultiPartials(const FilterMultiDesc &d_in, int64_t nrows, AggPartial *
     const unsigned __int128 rows_per_lane = (unsigned __int128)(((steps + waves - 1) / waves + 1) * 4);
     d.narrow = d.maxabs <= (uint64_t)INT64_MAX &&
                (unsigned __int128)d.maxabs * rows_per_lane < ((unsigned __int128)1 << 63);
-    const char *e32 = getenv("MBX_FA_MM32");
+    const char *e32 = Knob("MBX_FA_MM32");
     d.mm32 = d.mm && d.narrow && d.maxabs < ((uint64_t)1 << 31) && !(e32 && e32[0] == '0');
   };
   auto mode_of = [&] { return d.agg < 0 ? 0 : (!d.mm && d.narrow) ? 1 : (d.mm32 && d.narrow) ? 3 : 2; };
@@ -1027,7 +1030,7 @@ int FilterMultiPartials(const FilterMultiDesc &d_in, int64_t nrows, AggPartial *
   // templated one 1 for its compile-time modes (COUNT, narrow SUM, narrow SUM
   // + int32 MIN/MAX) and 3 for the general mode and one-column SUMs
   // (profiles/r02_filter_multi_modes.log).
-  const char *e = getenv("MBX_FM_BLOCKS_PER_CU");
+  const char *e = Knob("MBX_FM_BLOCKS_PER_CU");
   const int gpc_env = e && *e ? atoi(e) : 0;
   if (gpc_env > 0) {
     plan(gpc_env);
@@ -1142,7 +1145,7 @@ struct FaVariant {
 static FaVariant FaConfig(int mode) {
   FaVariant v;
   (void)mode;
-  const char *e = getenv("MBX_FA_VARIANT");
+  const char *e = Knob("MBX_FA_VARIANT");
   if (!e || !*e) return v;
   int u = 8, g = 4;
   char m1[8] = {0}, m2[8] = {0};
@@ -1232,7 +1235,7 @@ int FilterAggStates(const void *pcol, int pphys, int64_t lo, int64_t hi, bool ha
   if (!has_pred) lo = INT64_MIN;
   int mode = acol == nullptr ? 2 : (acol == pcol ? 0 : 1);
   if (mode == 2) {
-    const char *cs = getenv("MBX_FA_COUNT_AS_SUM");  // experiment: COUNT through the SUM-shaped loop
+    const char *cs = Knob("MBX_FA_COUNT_AS_SUM");  // experiment: COUNT through the SUM-shaped loop
     if (cs && cs[0] == '1') {
       mode = 0;
       acol = pcol;
@@ -1259,7 +1262,7 @@ int FilterAggStates(const void *pcol, int pphys, int64_t lo, int64_t hi, bool ha
     g_fa_narrow = sum_maxabs <= (uint64_t)INT64_MAX &&
                   (unsigned __int128)sum_maxabs * (unsigned __int128)rows_per_lane < ((unsigned __int128)1 << 63);
     // MIN/MAX in int32 when the zone map bounds |value| below 2^31 (MBX_FA_MM32=0 disables)
-    const char *e32 = getenv("MBX_FA_MM32");
+    const char *e32 = Knob("MBX_FA_MM32");
     g_fa_mm32 = g_fa_narrow && sum_maxabs < ((uint64_t)1 << 31) && !(e32 && e32[0] == '0');
   }
   if (pphys == P_I64) {
@@ -1788,7 +1791,7 @@ __global__ __launch_bounds__(256) void group_direct_lds_kernel(const TK *__restr
         pv[0] = x0.x; pv[1] = x0.y; pv[2] = x1.x; pv[3] = x1.y;
       }
 #pragma unroll
-      for (int e = 0; e < 4; e++) ok[e] = ok[e] && (uint64_t)(pv[e] - g.lo) <= g.span;
+      for (int e = 0; e < 4; e++) ok[e] = ok[e] && (uint64_t)(pv[e]) - (uint64_t)(g.lo) <= g.span;
       if (VV && g.src == 3) {  // a predicate on the NULL-able value column
 #pragma unroll
         for (int e = 0; e < 4; e++) ok[e] = ok[e] && ((vm >> e) & 1u);
@@ -1816,7 +1819,7 @@ __global__ __launch_bounds__(256) void group_direct_lds_kernel(const TK *__restr
         const GroupPred &g = pr.p[j];
         int64_t pv = g.src == 2 ? kv : g.src == 3 ? av
                    : (g.phys == P_I64 ? ((const int64_t *)g.col)[i] : (int64_t)((const int32_t *)g.col)[i]);
-        okr = okr && (uint64_t)(pv - g.lo) <= g.span && (g.src != 3 || vr);
+        okr = okr && (uint64_t)(pv) - (uint64_t)(g.lo) <= g.span && (g.src != 3 || vr);
       }
       if (okr) row(kv, av, NV >= 2 ? (int64_t)v1[i] : 0, vr);
     }
@@ -1920,7 +1923,7 @@ bool GroupByDirectStates(const void *kcol, int kphys, int64_t kmin, int nk, cons
   memset(&pr, 0, sizeof(pr));
   if (pred) pr = *pred;
   pr.xcd = 0;
-  if (const char *ex = getenv("MBX_GD_XCD")) pr.xcd = atoi(ex) != 0;
+  if (const char *ex = Knob("MBX_GD_XCD")) pr.xcd = atoi(ex) != 0;
   // LDS-DMA variant: one flush at the end, so a block's whole row share must
   // fit the overflow bound the host derived (seg_rows) — else the segmented
   // kernel below.  MBX_GD_VARIANT="d<depth>_g<blocks per CU>" / "seg".
@@ -1933,11 +1936,11 @@ bool GroupByDirectStates(const void *kcol, int kphys, int64_t kmin, int nk, cons
     for (int j = 0; j < pr.n; j++)  // predicate slices of their own: a deeper ring (c3_where: d3 3.00 vs d2 3.32 ms)
       if (pr.p[j].src == 1) depth = 3;
     bool use = true;
-    const char *e = getenv("MBX_GD_VARIANT");
+    const char *e = Knob("MBX_GD_VARIANT");
     if (e && *e) use = sscanf(e, "d%d_g%d", &depth, &gpc) == 2 || pr.n != 0;
     if (vv && !use) return false;  // the segmented kernel below has no validity words
     // MBX_GD_R=<r>: fewer replicas (experiment; seg_rows scales with R)
-    if (const char *er = getenv("MBX_GD_R")) {
+    if (const char *er = Knob("MBX_GD_R")) {
       int r = atoi(er);
       while (use && r > 0 && R > r) {
         R >>= 1;
@@ -1979,10 +1982,10 @@ bool GroupByDirectStates(const void *kcol, int kphys, int64_t kmin, int nk, cons
       bool pk = nv >= 1 && (int64_t)nk * R <= 2048 && PackedCountParams(vmaxabs, R, pkb, pkf);
       const bool one_flush = seg_rows <= 0 || seg_rows >= rows_per_block;
       if (one_flush) pk = false;
-      if (const char *ep = getenv("MBX_GD_PACK"))
+      if (const char *ep = Knob("MBX_GD_PACK"))
         pk = atoi(ep) != 0 && nv >= 1 && (int64_t)nk * R <= 2048 && PackedCountParams(vmaxabs, R, pkb, pkf);
       // MBX_GD_PKF=<steps>: drain more often than needed (tests exercise the drains)
-      if (const char *ef = getenv("MBX_GD_PKF")) pkf = std::max(1, std::min(pkf, atoi(ef)));
+      if (const char *ef = Knob("MBX_GD_PKF")) pkf = std::max(1, std::min(pkf, atoi(ef)));
       if (vv) {  // NULL-able value column: packed counts and one flush only
         if (!one_flush || lds > lds_cap) return false;
 #define GLVV1(TK, TV, MM, D, P)                                                                                     \
@@ -2170,11 +2173,150 @@ __global__ void init3_kernel(long long *o) {
   o[2] = 0;
 }
 
+// Zone map (min, max, non-NULL count) of an INT32 / INT64 column at HBM speed:
+// the LDS-DMA ring of filter_agg_lds.  A wave step covers 256 rows: the
+// step's values (1 KiB for int32, 2 KiB for int64) and, for a NULL-able
+// column, its 4 validity words (one exec-masked LDS-DMA instruction) land in
+// the wave's ring slot by global_load_lds, DEPTH steps in flight with a
+// counted vmcnt (never 0 in the loop); each lane then owns 4 consecutive rows.
+// Min / max stay in T's width.  Ring and reduction scratch share one
+// __shared__ array; one atomic set per block.  Rows past the last whole step
+// are done by wave 0 of block 0.  p is 16-B aligned; valid (if any) starts at
+// row 0 of p.
+template <typename T, bool VAL, int DEPTH>
+__global__ __launch_bounds__(256) void zone_map_lds_kernel(const T *__restrict__ p, const uint64_t *__restrict__ valid,
+                                                           int64_t n, long long *out3) {
+  constexpr int VB = 256 * (int)sizeof(T);  // value bytes per step
+  constexpr int SB = VB + (VAL ? 32 : 0);   // slot bytes
+  constexpr int NI = (sizeof(T) == 8 ? 2 : 1) + (VAL ? 1 : 0);
+  constexpr T TMAX = std::numeric_limits<T>::max();
+  constexpr T TMIN = std::numeric_limits<T>::min();
+  __shared__ __attribute__((aligned(16))) unsigned char ring[4 * DEPTH * SB];
+  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  unsigned char *slot0 = ring + w * DEPTH * SB;
+  const int64_t nsteps = n >> 8;
+  const int64_t nw = (int64_t)gridDim.x * 4;
+  int64_t st = (int64_t)blockIdx.x * 4 + w;
+  auto issue = [&](int64_t q, int d) {
+    unsigned char *dst = slot0 + d * SB;
+    const unsigned char *src = (const unsigned char *)p + q * VB;
+    __builtin_amdgcn_global_load_lds((const void *)(src + lane * 16), (void *)dst, 16, 0, 2);
+    if (sizeof(T) == 8) __builtin_amdgcn_global_load_lds((const void *)(src + 1024 + lane * 16), (void *)(dst + 1024), 16, 0, 2);
+    if (VAL && lane < 2) __builtin_amdgcn_global_load_lds((const void *)(valid + q * 4 + lane * 2), (void *)(dst + VB), 16, 0, 0);
+  };
+  T mn = TMAX, mx = TMIN;
+  uint32_t c = 0;
+  if (nsteps > 0) {
+#pragma unroll
+    for (int d = 0; d < DEPTH; d++) {
+      const int64_t q = st + d * nw;
+      issue(q < nsteps ? q : 0, d);  // keep the per-slot load count uniform (dummy step 0)
+    }
+  }
+  int k = 0;
+  for (; st < nsteps; st += nw) {
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NI * (DEPTH - 1)) : "memory");
+    const unsigned char *src = slot0 + k * SB;
+    T v[4];
+    if (sizeof(T) == 8) {
+      const v2i64 a = ((const v2i64 *)src)[2 * lane], b = ((const v2i64 *)src)[2 * lane + 1];
+      v[0] = (T)a.x; v[1] = (T)a.y; v[2] = (T)b.x; v[3] = (T)b.y;
+    } else {
+      const v4i32 a = ((const v4i32 *)src)[lane];
+      v[0] = (T)a.x; v[1] = (T)a.y; v[2] = (T)a.z; v[3] = (T)a.w;
+    }
+    uint32_t vb = 0xFu;
+    if (VAL) vb = (uint32_t)(((const uint64_t *)(src + VB))[lane >> 4] >> ((lane & 15) * 4)) & 0xFu;
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    int64_t q = st + DEPTH * nw;
+    q = q < nsteps ? q : st;  // past the end: re-read the step just consumed
+    issue(q, k);
+#pragma unroll
+    for (int e = 0; e < 4; e++) {
+      const bool ok = !VAL || ((vb >> e) & 1u);
+      mn = ok && v[e] < mn ? v[e] : mn;
+      mx = ok && v[e] > mx ? v[e] : mx;
+      c += ok ? 1u : 0u;
+    }
+    k = k + 1 == DEPTH ? 0 : k + 1;
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  if (blockIdx.x == 0 && w == 0) {
+    for (int64_t i = nsteps * 256 + lane; i < n; i += 64) {
+      if (VAL && !((valid[i >> 6] >> (i & 63)) & 1ull)) continue;
+      const T x = p[i];
+      mn = x < mn ? x : mn;
+      mx = x > mx ? x : mx;
+      c++;
+    }
+  }
+  long long lmn = (long long)mn, lmx = (long long)mx;
+  unsigned long long lc = c;
+#pragma unroll
+  for (int m = 32; m >= 1; m >>= 1) {
+    long long o = __shfl_xor(lmn, m, 64);
+    lmn = o < lmn ? o : lmn;
+    o = __shfl_xor(lmx, m, 64);
+    lmx = o > lmx ? o : lmx;
+    lc += __shfl_xor(lc, m, 64);
+  }
+  __syncthreads();  // every wave is done with its ring slots
+  long long *part = (long long *)ring;
+  if (lane == 0) {
+    part[3 * w] = lmn;
+    part[3 * w + 1] = lmx;
+    part[3 * w + 2] = (long long)lc;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    long long a = part[0], b = part[1], cc = part[2];
+    for (int i = 1; i < 4; i++) {
+      a = part[3 * i] < a ? part[3 * i] : a;
+      b = part[3 * i + 1] > b ? part[3 * i + 1] : b;
+      cc += part[3 * i + 2];
+    }
+    if (cc > 0) {
+      atomicMin(&out3[0], a);
+      atomicMax(&out3[1], b);
+      atomicAdd((unsigned long long *)&out3[2], (unsigned long long)cc);
+    }
+  }
+}
+
+template <typename T, bool VAL>
+static void LaunchZoneMap(const void *col, const uint64_t *valid, int64_t n, long long *out3, hipStream_t s) {
+  const int64_t steps = n >> 8;
+  const int grid = (int)std::max<int64_t>(1, std::min<int64_t>((int64_t)NumCUs(), (steps + 3) / 4));
+  hipLaunchKernelGGL((zone_map_lds_kernel<T, VAL, 6>), dim3(grid), dim3(256), 0, s, (const T *)col, valid, n, out3);
+}
+
 void KeyRange(const void *col, int phys, const uint64_t *valid, int64_t n, long long *out3, hipStream_t s) {
   hipLaunchKernelGGL(init3_kernel, dim3(1), dim3(1), 0, s, out3);
-  if (n > 0)
-    hipLaunchKernelGGL(key_range_kernel, dim3(GridFor(n, 256 * 16, NumCUs() * 4)), dim3(256), 0, s, col, phys, valid,
-                       n, out3);
+  if (n <= 0) {
+    CHECK_LAUNCH();
+    return;
+  }
+  const int sz = phys == P_I64 ? 8 : phys == P_I32 ? 4 : 0;
+  const uintptr_t mis = (uintptr_t)col % 16;
+  if (sz && n >= 1024 && (mis == 0 || (!valid && mis % sz == 0))) {
+    // an appended range may start mid-vector: its first rows go through the
+    // element-wise kernel, the 16-B aligned rest through the ring
+    const int64_t head = mis ? (int64_t)((16 - mis) / sz) : 0;
+    if (head)
+      hipLaunchKernelGGL(key_range_kernel, dim3(1), dim3(64), 0, s, col, phys, (const uint64_t *)nullptr, head, out3);
+    const void *body = (const char *)col + head * sz;
+    if (sz == 8) {
+      if (valid) LaunchZoneMap<int64_t, true>(body, valid, n - head, out3, s);
+      else LaunchZoneMap<int64_t, false>(body, nullptr, n - head, out3, s);
+    } else {
+      if (valid) LaunchZoneMap<int32_t, true>(body, valid, n - head, out3, s);
+      else LaunchZoneMap<int32_t, false>(body, nullptr, n - head, out3, s);
+    }
+    CHECK_LAUNCH();
+    return;
+  }
+  hipLaunchKernelGGL(key_range_kernel, dim3(GridFor(n, 256 * 16, NumCUs() * 4)), dim3(256), 0, s, col, phys, valid,
+                     n, out3);
   CHECK_LAUNCH();
 }
 
@@ -3042,7 +3184,7 @@ __global__ __launch_bounds__(256) void filter_bits_lds_kernel(FilterMultiDesc D,
       ok[e] = (vm >> e) & 1u;
 #pragma unroll
       for (int c = 0; c < FM_MAX; c++)
-        if (c < D.ncol) ok[e] = ok[e] && (uint64_t)(v[c][e] - D.col[c].lo) <= D.col[c].span;
+        if (c < D.ncol) ok[e] = ok[e] && (uint64_t)(v[c][e]) - (uint64_t)(D.col[c].lo) <= D.col[c].span;
     }
     emit(st, ok);
     k = k + 1 == DEPTH ? 0 : k + 1;
@@ -3058,7 +3200,7 @@ __global__ __launch_bounds__(256) void filter_bits_lds_kernel(FilterMultiDesc D,
       for (int c = 0; c < D.ncol && ok[e]; c++) {
         const int64_t x = D.col[c].phys == P_I64 ? ((const int64_t *)D.col[c].data)[i]
                                                  : (int64_t)((const int32_t *)D.col[c].data)[i];
-        ok[e] = (uint64_t)(x - D.col[c].lo) <= D.col[c].span &&
+        ok[e] = (uint64_t)(x) - (uint64_t)(D.col[c].lo) <= D.col[c].span &&
                 (!D.col[c].valid || ((D.col[c].valid[i >> 6] >> (i & 63)) & 1));
       }
     }
@@ -3079,12 +3221,12 @@ void FilterBits(const FilterMultiDesc &d, int64_t nrows, unsigned long long *bit
   }
   slot = (slot + 15) & ~15;
   int gpc = 3;
-  if (const char *e = getenv("MBX_FB_BLOCKS_PER_CU")) gpc = atoi(e) > 0 ? atoi(e) : 3;
+  if (const char *e = Knob("MBX_FB_BLOCKS_PER_CU")) gpc = atoi(e) > 0 ? atoi(e) : 3;
   int grid = NumCUs() * gpc;
   const int64_t need = (nrows >> 8) / 4 + 1;
   if (grid > need) grid = (int)need;
   int dp = 0;  // MBX_FB_DEPTH: ring depth override (sweeps)
-  if (const char *e = getenv("MBX_FB_DEPTH")) dp = atoi(e);
+  if (const char *e = Knob("MBX_FB_DEPTH")) dp = atoi(e);
 #define FB(L, DP)                                                                                           \
   hipLaunchKernelGGL((filter_bits_lds_kernel<L, DP>), dim3(grid), dim3(256), (size_t)4 * DP * slot, s, d, \
                      nrows, bits, slot)
@@ -3483,7 +3625,7 @@ void CompactColumns(const CompactDesc &d, int64_t nrows, const unsigned long lon
   for (int c = 0; c < d.nout; c++) any |= d.ow[c] != 4 && d.ow[c] != 8;
   if (any) {
     int gpc = 3;
-    if (const char *e = getenv("MBX_CP_BLOCKS_PER_CU")) gpc = atoi(e) > 0 ? atoi(e) : 3;
+    if (const char *e = Knob("MBX_CP_BLOCKS_PER_CU")) gpc = atoi(e) > 0 ? atoi(e) : 3;
     int grid = NumCUs() * gpc;
     const int64_t need = (nrows >> 8) / 4 + 1;
     if (grid > need) grid = (int)need;
@@ -3494,12 +3636,12 @@ void CompactColumns(const CompactDesc &d, int64_t nrows, const unsigned long lon
   for (int c = 0; c < d.nout; c++) nld += d.ow[c] / 4;
   if (nld > 8) throw std::runtime_error("CompactColumns: more than 8 KiB of outputs per step");
   int gpc = 3;
-  if (const char *e = getenv("MBX_CP_BLOCKS_PER_CU")) gpc = atoi(e) > 0 ? atoi(e) : 3;
+  if (const char *e = Knob("MBX_CP_BLOCKS_PER_CU")) gpc = atoi(e) > 0 ? atoi(e) : 3;
   int grid = NumCUs() * gpc;
   const int64_t need = (nrows >> 8) / 4 + 1;
   if (grid > need) grid = (int)need;
   int dp = 0;  // MBX_CP_DEPTH: ring depth override (sweeps)
-  if (const char *e = getenv("MBX_CP_DEPTH")) dp = atoi(e);
+  if (const char *e = Knob("MBX_CP_DEPTH")) dp = atoi(e);
 #define CP(L, DP)                                                                                              \
   hipLaunchKernelGGL((compact_lds_kernel<L, DP>), dim3(grid), dim3(256), (size_t)4 * DP * (L * 1024 + 64) + 4 * 2048, s, d, \
                      nrows, bits, step_offsets)

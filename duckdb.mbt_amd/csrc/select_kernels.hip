@@ -33,6 +33,7 @@
 // that resolved the last tile's inclusive prefix handles it with guarded
 // loads and writes the selected-row total.
 #include <hip/hip_runtime.h>
+#include <atomic>
 #include <stdexcept>
 #include <stdint.h>
 #include <stdlib.h>
@@ -40,9 +41,22 @@
 
 #include "device.h"
 #include "types.h"
+#include "knobs.h"
 
 namespace mbx {
 namespace dev {
+
+// hipFuncAttributeMaxDynamicSharedMemorySize once per (kernel, device): the
+// attribute belongs to a device, and the shard workers of one process launch
+// on several devices at once (a per-process flag would skip devices and race)
+static void EnsureMaxLds(const void *fn, std::atomic<uint64_t> &done, int bytes) {
+  int d = 0;
+  (void)hipGetDevice(&d);
+  const uint64_t bit = 1ull << (d & 63);
+  if (done.load(std::memory_order_acquire) & bit) return;
+  (void)hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, bytes);
+  done.fetch_or(bit, std::memory_order_acq_rel);
+}
 
 namespace {
 
@@ -164,7 +178,7 @@ __global__ __launch_bounds__(256) void select_lds_kernel(SelectDesc D, int64_t n
         int64_t v[4];
         sl_read4(slot + off[c], D.col[c].w, lane, v);
 #pragma unroll
-        for (int e = 0; e < 4; e++) ok[e] = ok[e] && (uint64_t)(v[e] - D.col[c].lo) <= D.col[c].span;
+        for (int e = 0; e < 4; e++) ok[e] = ok[e] && (uint64_t)(v[e]) - (uint64_t)(D.col[c].lo) <= D.col[c].span;
       }
       int cs = 0;
 #pragma unroll
@@ -277,7 +291,7 @@ __global__ __launch_bounds__(256) void select_lds_kernel(SelectDesc D, int64_t n
           if (!D.col[c].is_pred) continue;
           const int64_t x = D.col[c].w == 8 ? ((const int64_t *)D.col[c].data)[i]
                                             : (int64_t)((const int32_t *)D.col[c].data)[i];
-          ok[e] = (uint64_t)(x - D.col[c].lo) <= D.col[c].span;
+          ok[e] = (uint64_t)(x) - (uint64_t)(D.col[c].lo) <= D.col[c].span;
         }
       }
       unsigned long long bb[4];
@@ -321,20 +335,16 @@ void SelectCompact(const SelectDesc &d, int64_t nrows, void *status_buf, int64_t
   unsigned int *ticket = (unsigned int *)(status + ntiles + 1);
   (void)hipMemsetAsync(status, 0, (size_t)(ntiles + 2) * 8, s);
   int nbuf = 3;
-  if (const char *e = getenv("MBX_SL_NBUF")) nbuf = atoi(e) == 2 ? 2 : atoi(e) >= 4 ? 4 : 3;
+  if (const char *e = Knob("MBX_SL_NBUF")) nbuf = atoi(e) == 2 ? 2 : atoi(e) >= 4 ? 4 : 3;
   int gpc = 1;
-  if (const char *e = getenv("MBX_SL_BLOCKS_PER_CU")) gpc = atoi(e) > 0 ? atoi(e) : 1;
+  if (const char *e = Knob("MBX_SL_BLOCKS_PER_CU")) gpc = atoi(e) > 0 ? atoi(e) : 1;
   int64_t grid = (int64_t)NumCUs() * gpc;
   if (grid > ntiles) grid = ntiles > 0 ? ntiles : 1;
   const size_t lds = (size_t)4 * nbuf * S * ni * 1024 + 4 * 2048;
 #define SL(NI_, S_, NB_)                                                                                       \
   do {                                                                                                         \
-    static bool attr = false;                                                                                  \
-    if (!attr) {                                                                                               \
-      (void)hipFuncSetAttribute((const void *)select_lds_kernel<NI_, S_, NB_>,                                 \
-                                hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024 - 256);                 \
-      attr = true;                                                                                             \
-    }                                                                                                          \
+    static std::atomic<uint64_t> attr{0};                                                                      \
+    EnsureMaxLds((const void *)select_lds_kernel<NI_, S_, NB_>, attr, 160 * 1024 - 256);                      \
     hipLaunchKernelGGL((select_lds_kernel<NI_, S_, NB_>), dim3((unsigned)grid), dim3(256), lds, s, d, nrows,  \
                        ntiles, status, ticket, total);                                                         \
   } while (0)
@@ -462,8 +472,11 @@ struct SrCols {
 // VAL: some columns carry validity words (H = 1).  A step's 32 B of words per
 // NULL-able column ride a second ring (one exec-masked LDS-DMA instruction
 // each, counted exactly in the wait); a NULL fails a predicate, and a NULL-able
-// output stages one validity byte per selected row, which its storer writes to
-// D.vdst (PackValidityBytes turns those into the output's bitmap).
+// output stages one validity byte per selected row next to its value.  The
+// storer turns a run's bytes into the output bitmap D.vbits directly: one
+// ballot per 64 output rows aligned to the bitmap's words, interior words
+// stored, the run's partial first and last words ORed (runs of other storers
+// and workgroups share them; the caller zeroed the bitmap).
 template <int NC, int WM, int DEPTH, int H, int NL, bool VAL>
 __global__ __launch_bounds__((NL + 5) * 64) void select_rounds_kernel(SelectDesc D, int64_t n, int64_t nrounds, int S, int stg,
                                                             unsigned long long *ctl, uint32_t epoch, int sleep_,
@@ -633,7 +646,7 @@ __global__ __launch_bounds__((NL + 5) * 64) void select_rounds_kernel(SelectDesc
 #pragma unroll
           for (int h = 0; h < H; h++)
 #pragma unroll
-            for (int e = 0; e < 4; e++) ok[h][e] = ok[h][e] & ((uint64_t)(v[h][c][e] - lo[c]) <= span[c]);
+            for (int e = 0; e < 4; e++) ok[h][e] = ok[h][e] & ((uint64_t)(v[h][c][e]) - (uint64_t)(lo[c]) <= span[c]);
           if constexpr (VAL) {  // a NULL fails the predicate (H = 1)
 #pragma unroll
             for (int e = 0; e < 4; e++) ok[0][e] = ok[0][e] & (((vmc[c] >> e) & 1u) != 0);
@@ -781,14 +794,32 @@ __global__ __launch_bounds__((NL + 5) * 64) void select_rounds_kernel(SelectDesc
             for (uint32_t i = lane; i < c; i += 64) dst[i] = st[(tail[j] + i) & mask];
           }
           if constexpr (VAL) {
-            if (D.vdst[o]) {
+            if (D.vbits[o] && c) {
               int vo = 0;
 #pragma unroll
               for (int cc = 0; cc < NC; cc++)
                 if (cc == oc) vo = vsoff[cc];
               const uint8_t *vb = mystage + vo;
-              uint8_t *vd = D.vdst[o] + pos;
-              for (uint32_t i = lane; i < c; i += 64) vd[i] = vb[(tail[j] + i) & mask];
+              uint64_t *bits = D.vbits[o];
+              const int64_t end = pos + (int64_t)c, wlast = (end - 1) >> 6;
+              // one output word per lane (64 words = 4096 rows per pass): the
+              // word's staged bytes -> bits, interior words stored, the run's
+              // partial first / last word ORed
+              for (int64_t wb = pos >> 6; wb <= wlast; wb += 64) {
+                const int64_t w = wb + lane;
+                if (w <= wlast) {
+                  const int64_t r0 = w * 64 > pos ? w * 64 : pos, r1 = w * 64 + 64 < end ? w * 64 + 64 : end;
+                  uint64_t word = 0;
+                  uint32_t si = (tail[j] + (uint32_t)(r0 - pos)) & mask;
+                  for (int64_t r = r0; r < r1; r++, si = (si + 1) & mask)
+                    word |= (uint64_t)(vb[si] & 1u) << (r & 63);
+                  if (r1 - r0 < 64) {
+                    if (word) atomicOr((unsigned long long *)&bits[w], (unsigned long long)word);
+                  } else {
+                    bits[w] = word;
+                  }
+                }
+              }
             }
           }
         }
@@ -912,7 +943,7 @@ __global__ __launch_bounds__((NL + 5) * 64) void select_rounds_kernel(SelectDesc
         if (!D.col[c].is_pred) continue;
         const int64_t xv = D.col[c].w == 8 ? ((const int64_t *)D.col[c].data)[i]
                                            : (int64_t)((const int32_t *)D.col[c].data)[i];
-        ok[e] = (uint64_t)(xv - D.col[c].lo) <= D.col[c].span;
+        ok[e] = (uint64_t)(xv) - (uint64_t)(D.col[c].lo) <= D.col[c].span;
         if (VAL && D.col[c].valid) ok[e] = ok[e] && ((D.col[c].valid[i >> 6] >> (i & 63)) & 1);
       }
     }
@@ -927,7 +958,8 @@ __global__ __launch_bounds__((NL + 5) * 64) void select_rounds_kernel(SelectDesc
         const int c = D.out_col[o];
         if (D.col[c].w == 8) ((int64_t *)D.dst[o])[pos] = ((const int64_t *)D.col[c].data)[i0 + e];
         else ((int32_t *)D.dst[o])[pos] = ((const int32_t *)D.col[c].data)[i0 + e];
-        if (VAL && D.vdst[o]) D.vdst[o][pos] = (uint8_t)((D.col[c].valid[(i0 + e) >> 6] >> ((i0 + e) & 63)) & 1);
+        if (VAL && D.vbits[o] && ((D.col[c].valid[(i0 + e) >> 6] >> ((i0 + e) & 63)) & 1))
+          atomicOr((unsigned long long *)&D.vbits[o][pos >> 6], 1ull << (pos & 63));
       }
       pos++;
     }
@@ -972,14 +1004,14 @@ static SelectRoundsPlan PlanSelectRoundsNL(const SelectDesc &d, int64_t nrows, i
   // (profiles/r02_select_rounds_sweep.log).  MBX_SR_NL=4|8 overrides.
   // (+1 staged byte per row for a NULL-able output's validity)
   p.NL = p.nc == 1 && rowb <= 4 + p.nv ? 8 : 4;
-  if (const char *e = getenv("MBX_SR_NL")) p.NL = atoi(e) == 8 && p.nc == 1 ? 8 : 4;
+  if (const char *e = Knob("MBX_SR_NL")) p.NL = atoi(e) == 8 && p.nc == 1 ? 8 : 4;
   if (force_nl) p.NL = force_nl;
   if (p.NL == 8) want_h = 1, want_depth = 3;
-  if (const char *e = getenv("MBX_SR_H")) want_h = atoi(e) == 1 ? 1 : 2;
+  if (const char *e = Knob("MBX_SR_H")) want_h = atoi(e) == 1 ? 1 : 2;
   if (p.nv) want_h = 1;
-  if (const char *e = getenv("MBX_SR_S")) want_s = atoi(e) > 0 ? atoi(e) : 0;
-  if (const char *e = getenv("MBX_SR_STG")) want_stg = atoi(e) >= 256 ? atoi(e) : 4096;
-  if (const char *e = getenv("MBX_SR_DEPTH")) {
+  if (const char *e = Knob("MBX_SR_S")) want_s = atoi(e) > 0 ? atoi(e) : 0;
+  if (const char *e = Knob("MBX_SR_STG")) want_stg = atoi(e) >= 256 ? atoi(e) : 4096;
+  if (const char *e = Knob("MBX_SR_DEPTH")) {
     const int v = atoi(e);
     if (p.nc == 1 && !p.nv && (v == 2 || v == 3 || v == 4 || v == 6)) want_depth = v;  // single-column shapes only (sweeps)
   }
@@ -1012,13 +1044,13 @@ static SelectRoundsPlan PlanSelectRoundsNL(const SelectDesc &d, int64_t nrows, i
   p.nrounds = (ntiles + p.G - 1) / p.G;
   if (p.lds < (size_t)96 * 1024) p.lds = (size_t)96 * 1024;  // one workgroup per CU
   p.sleep = 1;
-  if (const char *e = getenv("MBX_SR_SLEEP")) p.sleep = atoi(e) >= 0 ? atoi(e) : 1;
+  if (const char *e = Knob("MBX_SR_SLEEP")) p.sleep = atoi(e) >= 0 ? atoi(e) : 1;
   p.pw = 2;  // rounds per coordinator poll (1..4)
-  if (const char *e = getenv("MBX_SR_PW")) p.pw = std::max(1, std::min(4, atoi(e)));
+  if (const char *e = Knob("MBX_SR_PW")) p.pw = std::max(1, std::min(4, atoi(e)));
   // tests: workgroup MBX_SR_TEST_STALL never publishes, as if it were never
   // scheduled, so every coordinator times out and the launch aborts
   p.test_stall = -1;
-  if (const char *e = getenv("MBX_SR_TEST_STALL")) p.test_stall = atoi(e);
+  if (const char *e = Knob("MBX_SR_TEST_STALL")) p.test_stall = atoi(e);
   p.ok = true;
   return p;
 }
@@ -1029,12 +1061,8 @@ namespace {
 template <int NC, int WM, int DP, int H, int NL, bool VAL = false>
 void SrLaunchNL(const SelectDesc &d, const SelectRoundsPlan &p, int64_t nrows, unsigned long long *ctl, uint32_t epoch,
                 hipStream_t s) {
-  static bool attr = false;
-  if (!attr) {
-    (void)hipFuncSetAttribute((const void *)select_rounds_kernel<NC, WM, DP, H, NL, VAL>,
-                              hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024 - 2048);
-    attr = true;
-  }
+  static std::atomic<uint64_t> attr{0};
+  EnsureMaxLds((const void *)select_rounds_kernel<NC, WM, DP, H, NL, VAL>, attr, 160 * 1024 - 2048);
   hipLaunchKernelGGL((select_rounds_kernel<NC, WM, DP, H, NL, VAL>), dim3((unsigned)p.G), dim3((NL + 5) * 64), p.lds, s,
                      d, nrows, p.nrounds, p.S, p.stg, ctl, epoch, p.sleep, p.test_stall, p.pw);
 }
@@ -1083,40 +1111,17 @@ void SrDispatch(const SelectDesc &d, const SelectRoundsPlan &p, int64_t nrows, u
 }
 }  // namespace
 
-// one thread per output word: 64 validity bytes (0/1) -> 64 bits; 8 bytes at a
-// time, bit i of (y * 0x0102040810204080) >> 56 = byte i of y
-__global__ __launch_bounds__(256) void pack_validity_bytes_kernel(const uint8_t *__restrict__ b, int64_t n,
-                                                                  uint64_t *__restrict__ bits) {
-  const int64_t wd = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  const int64_t base = wd * 64;
-  if (base >= n) return;
-  uint64_t x = 0;
-  if (base + 64 <= n) {
-    const uint64_t *p = (const uint64_t *)(b + base);
-#pragma unroll
-    for (int j = 0; j < 8; j++) x |= ((p[j] * 0x0102040810204080ull) >> 56) << (8 * j);
-  } else {
-    for (int64_t i = base; i < n; i++) x |= (uint64_t)(b[i] & 1) << (i - base);
-  }
-  bits[wd] = x;
-}
-
-void PackValidityBytes(const uint8_t *bytes, int64_t n, uint64_t *bits, hipStream_t s) {
-  if (n <= 0) return;
-  const int64_t words = (n + 63) / 64;
-  hipLaunchKernelGGL(pack_validity_bytes_kernel, dim3((unsigned)((words + 255) / 256)), dim3(256), 0, s, bytes, n, bits);
-}
-
-void SelectRounds(const SelectDesc &d, const SelectRoundsPlan &p, int64_t nrows, unsigned long long *ctl,
-                  uint32_t epoch, hipStream_t s) {
+hipError_t SelectRounds(const SelectDesc &d, const SelectRoundsPlan &p, int64_t nrows, unsigned long long *ctl,
+                        uint32_t epoch, hipStream_t s) {
   if (!p.ok) throw std::runtime_error("SelectRounds: unsupported shape");
+  (void)hipGetLastError();  // an earlier, unrelated sticky error must not be taken for this launch's
   switch (p.nc) {
     case 1: SrDispatch<1>(d, p, nrows, ctl, epoch, s); break;
     case 2: SrDispatch<2>(d, p, nrows, ctl, epoch, s); break;
     case 3: SrDispatch<3>(d, p, nrows, ctl, epoch, s); break;
     default: SrDispatch<4>(d, p, nrows, ctl, epoch, s); break;
   }
-  (void)hipGetLastError();
+  return hipGetLastError();  // the launch's own error (LDS / resource limits): the caller falls back
 }
 
 // ---------------------------------------------------------------------------
@@ -1129,7 +1134,7 @@ int64_t CountChunks(int64_t nrows) { return ((nrows >> 8) + FC_CHUNK - 1) / FC_C
 // grid-stride like the fused filter-aggregate); pass 2 reads the offset of
 // chunk c at entry c * FC_CHUNK / K1 of the scanned counts.
 static int FkChunk() {
-  const char *e = getenv("MBX_FK_CHUNK");
+  const char *e = Knob("MBX_FK_CHUNK");
   const int v = e ? atoi(e) : FC_CHUNK;
   return (v == 1 || v == 2 || v == 4) ? v : FC_CHUNK;
 }
@@ -1202,7 +1207,7 @@ __global__ __launch_bounds__(256) void filter_count_lds_kernel(FilterMultiDesc D
         int64_t v[4];
         sl_read4(src + off[c2], D.col[c2].phys == P_I64 ? 8 : 4, lane, v);
 #pragma unroll
-        for (int e = 0; e < 4; e++) ok[e] = ok[e] && (uint64_t)(v[e] - D.col[c2].lo) <= D.col[c2].span;
+        for (int e = 0; e < 4; e++) ok[e] = ok[e] && (uint64_t)(v[e]) - (uint64_t)(D.col[c2].lo) <= D.col[c2].span;
       }
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       issue(p + DEPTH, k);
@@ -1226,7 +1231,7 @@ __global__ __launch_bounds__(256) void filter_count_lds_kernel(FilterMultiDesc D
       for (int c = 0; c < D.ncol && ok[e]; c++) {
         const int64_t x = D.col[c].phys == P_I64 ? ((const int64_t *)D.col[c].data)[i]
                                                  : (int64_t)((const int32_t *)D.col[c].data)[i];
-        ok[e] = (uint64_t)(x - D.col[c].lo) <= D.col[c].span;
+        ok[e] = (uint64_t)(x) - (uint64_t)(D.col[c].lo) <= D.col[c].span;
       }
     }
     uint32_t t = 0;
@@ -1244,12 +1249,12 @@ void FilterCountChunks(const FilterMultiDesc &d, int64_t nrows, uint32_t *counts
   }
   const int slot = ni * 1024;
   int gpc = 3;
-  if (const char *e = getenv("MBX_FK_BLOCKS_PER_CU")) gpc = atoi(e) > 0 ? atoi(e) : 3;
+  if (const char *e = Knob("MBX_FK_BLOCKS_PER_CU")) gpc = atoi(e) > 0 ? atoi(e) : 3;
   const int64_t chunks = CountEntries(nrows);
   int64_t grid = (int64_t)NumCUs() * gpc;
   if (grid > chunks / 4 + 1) grid = chunks / 4 + 1;
   int dp = 0;
-  if (const char *e = getenv("MBX_FK_DEPTH")) dp = atoi(e);
+  if (const char *e = Knob("MBX_FK_DEPTH")) dp = atoi(e);
   const int k1 = FkChunk();
 #define FK1(L, DP, K)                                                                                         \
   hipLaunchKernelGGL((filter_count_lds_kernel<L, DP, K>), dim3((unsigned)grid), dim3(256), (size_t)4 * DP * slot, s, \
@@ -1346,7 +1351,7 @@ __global__ __launch_bounds__(256) void compact_recomp_lds_kernel(CompactDesc D, 
           pv[e] = x;
         }
 #pragma unroll
-        for (int e = 0; e < 4; e++) ok[e] = ok[e] && (uint64_t)(pv[e] - D.pred_lo[j]) <= D.pred_span[j];
+        for (int e = 0; e < 4; e++) ok[e] = ok[e] && (uint64_t)(pv[e]) - (uint64_t)(D.pred_lo[j]) <= D.pred_span[j];
       }
       const unsigned long long b0 = __ballot(ok[0]), b1 = __ballot(ok[1]), b2 = __ballot(ok[2]), b3 = __ballot(ok[3]);
       const int cnt = __popcll(b0) + __popcll(b1) + __popcll(b2) + __popcll(b3);
@@ -1389,7 +1394,7 @@ __global__ __launch_bounds__(256) void compact_recomp_lds_kernel(CompactDesc D, 
       for (int j = 0; j < D.npred && ok[e]; j++) {
         const int c = D.pred_out[j];
         const int64_t x = D.ow[c] == 8 ? ((const int64_t *)D.src[c])[i] : (int64_t)((const int32_t *)D.src[c])[i];
-        ok[e] = (uint64_t)(x - D.pred_lo[j]) <= D.pred_span[j];
+        ok[e] = (uint64_t)(x) - (uint64_t)(D.pred_lo[j]) <= D.pred_span[j];
       }
     }
     unsigned long long bb[4];
@@ -1416,12 +1421,12 @@ void CompactRecompute(const CompactDesc &d, int64_t nrows, const int64_t *chunk_
   }
   if (nld < 1 || nld > 8 || d.npred < 1 || d.npred > FM_MAX) throw std::runtime_error("CompactRecompute: shape");
   int gpc = 3;
-  if (const char *e = getenv("MBX_CR_BLOCKS_PER_CU")) gpc = atoi(e) > 0 ? atoi(e) : 3;
+  if (const char *e = Knob("MBX_CR_BLOCKS_PER_CU")) gpc = atoi(e) > 0 ? atoi(e) : 3;
   const int64_t chunks = CountChunks(nrows);
   int64_t grid = (int64_t)NumCUs() * gpc;
   if (grid > chunks / 4 + 1) grid = chunks / 4 + 1;
   int dp = 0;
-  if (const char *e = getenv("MBX_CR_DEPTH")) dp = atoi(e);
+  if (const char *e = Knob("MBX_CR_DEPTH")) dp = atoi(e);
 #define CR(L, DP)                                                                                               \
   hipLaunchKernelGGL((compact_recomp_lds_kernel<L, DP>), dim3((unsigned)grid), dim3(256),                      \
                      (size_t)4 * DP * L * 1024 + 4 * 2048, s, d, nrows, chunk_offsets, FC_CHUNK / FkChunk())

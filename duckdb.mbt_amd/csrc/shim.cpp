@@ -24,6 +24,7 @@
 #include "../../include/duckdb_mb.h"
 #include "engine.h"
 #include "jit.h"
+#include "knobs.h"
 
 using namespace mbx;
 
@@ -61,6 +62,12 @@ extern "C" moonbit_bytes_t duckdb_mbx_bytes_new(const uint8_t *data, int32_t len
 extern "C" int32_t duckdb_mbx_bytes_len(moonbit_bytes_t b) { return MbLen(b); }
 extern "C" void duckdb_mbx_bytes_free(moonbit_bytes_t b) {
   if (b) free((MbHeader *)b - 1);
+}
+// Drops a Bytes this library allocated and will not return (an error path):
+// the MoonBit runtime's own moonbit_decref when linked into a MoonBit program,
+// else (this weak definition, test harnesses) the matching free.
+extern "C" __attribute__((weak)) void moonbit_decref(void *obj) {
+  if (obj) free((MbHeader *)obj - 1);
 }
 
 // A MoonBit byte object's length is the low 28 bits of its header word, so a
@@ -437,6 +444,8 @@ int32_t duckdb_mb_config_set(duckdb_mb_config *c, moonbit_bytes_t key, moonbit_b
   } else if (kl == "mbx_shard_rows") {
     ok = IsInt(v, &x) && x >= 0;
     if (ok) c->opts.shard_rows = x;
+  } else if (kl == "mbx_force_peer") {
+    c->opts.force_peer = v == "true" || v == "1";
   } else if (kl == "mbx_profile") {
     c->opts.profile = v == "true" || v == "1";
   } else if (kl == "mbx_allow_no_gpu") {
@@ -529,7 +538,7 @@ int32_t duckdb_mb_clear_bindings(duckdb_mb_statement *s) {  // ref :983-989
 // catalog are unchanged (MBX_PLAN_CACHE=0 disables), else a fresh bind.
 static BoundSelectPtr PlanFor(duckdb_mb_statement *s) {
   Connection &c = s->conn->conn;
-  const char *pc = getenv("MBX_PLAN_CACHE");
+  const char *pc = Knob("MBX_PLAN_CACHE");
   const bool off = pc && atoi(pc) == 0;
   bool same = !off && s->plan && s->plan_version == c.catalog.version && s->plan_types.size() == s->params.size();
   for (size_t i = 0; same && i < s->params.size(); i++)
@@ -1353,13 +1362,13 @@ static moonbit_bytes_t ArrowStr(duckdb_mb_arrow_result *a, int32_t col, bool nul
         return out + 8;
       }, nullable);
       if (ok) return out;
-      if (!out) return MakeBytes("", 0);  // over the reference's int32 buffer size
+      if (!out) return MakeBytes("", 0);  // over the 2^28-byte limit of one MoonBit Bytes (MbTooBig set the error)
     } catch (std::exception &e) {
+      // never hand back a buffer whose header claims n strings it does not hold:
+      // drop it, keep the error, return the empty Bytes of the other failures
       SetError(e.what());
-      if (out) {
-        memset(out + 8, 0, (size_t)(total - 8));
-        return out;
-      }
+      if (out) moonbit_decref(out);
+      return MakeBytes("", 0);
     }
   }
   const HostColumn &c = ArrowHost(a).cols[col];
@@ -1525,7 +1534,7 @@ char *duckdb_mbx_jit_selftest(void) {
   std::string log;
   for (bool filter : {true, false}) {
     std::string src = jit::Source(p, cols, filter);
-    if (getenv("MBX_JIT_DUMP")) fprintf(stderr, "%s\n", src.c_str());
+    if (Knob("MBX_JIT_DUMP")) fprintf(stderr, "%s\n", src.c_str());
     std::string r = jit::CompileCheck(src);
     if (!r.empty()) log += std::string(filter ? "[filter] " : "[project] ") + r;
   }
@@ -1538,7 +1547,7 @@ char *duckdb_mbx_jit_selftest(void) {
   p.out_reg[2] = 255;
   {
     std::string src = jit::AggSourceForTest(p, cols);
-    if (getenv("MBX_JIT_DUMP")) fprintf(stderr, "%s\n", src.c_str());
+    if (Knob("MBX_JIT_DUMP")) fprintf(stderr, "%s\n", src.c_str());
     std::string r = jit::CompileCheck(src);
     if (!r.empty()) log += "[aggregate] " + r;
   }
@@ -1557,7 +1566,7 @@ char *duckdb_mbx_jit_selftest(void) {
     g.key_reg[1] = 3;
     g.key_nullable[1] = 1;
     std::string src = jit::GroupSourceForTest(q, cols, g);
-    if (getenv("MBX_JIT_DUMP")) fprintf(stderr, "%s\n", src.c_str());
+    if (Knob("MBX_JIT_DUMP")) fprintf(stderr, "%s\n", src.c_str());
     std::string r = jit::CompileCheck(src);
     if (!r.empty()) log += "[group] " + r;
   }
@@ -1654,6 +1663,29 @@ char *duckdb_mbx_result_text(duckdb_mb_result *r, int64_t *len) {
   if (!chars.empty()) memcpy(buf + head + off.size() * 8, chars.data(), chars.size());
   *len = (int64_t)total;
   return buf;
+}
+
+// Counters of the in-library multi-device path (gpu_devices): out[0] shards,
+// [1] peer-access links enabled at connect, [2] ForShards dispatches, [3] peer
+// DMA copies, [4] peer DMA bytes, [5] sharded aggregates finished on the host;
+// outd[0] the last dispatch's wall time (us), outd[1] the last host merge (us).
+// Returns the number of int64 counters written (0 for a null handle).
+int32_t duckdb_mbx_shard_stats(duckdb_mb_connection *h, int64_t *out6, double *outd2) {
+  if (!h) return 0;
+  const ShardStats &st = h->conn.shard_stats;
+  if (out6) {
+    out6[0] = (int64_t)h->conn.shards.size();
+    out6[1] = st.peer_links;
+    out6[2] = st.dispatches;
+    out6[3] = st.peer_copies;
+    out6[4] = st.peer_bytes;
+    out6[5] = st.host_results;
+  }
+  if (outd2) {
+    outd2[0] = st.last_dispatch_us;
+    outd2[1] = st.last_combine_us;
+  }
+  return 6;
 }
 
 int32_t duckdb_mbx_result_raw(duckdb_mb_result *r, int32_t col, int32_t row, void *out, int32_t out_len) {

@@ -167,9 +167,11 @@ double duckdb_mb_bytes_to_double(const char *bytes, int32_t offset);            
  * ======================================================================== */
 
 /* MoonBit byte objects for hosts that are not a MoonBit program.  Inside a
- * MoonBit executable the runtime's moonbit_make_bytes_raw is used instead
- * (ours is a weak definition). */
+ * MoonBit executable the runtime's moonbit_make_bytes_raw and moonbit_decref
+ * are used instead (ours are weak definitions); the
+ * library calls moonbit_decref only on a Bytes it built and does not return. */
 moonbit_bytes_t moonbit_make_bytes_raw(int32_t len);
+void moonbit_decref(void *obj);
 moonbit_bytes_t duckdb_mbx_bytes_new(const uint8_t *data, int32_t len);
 int32_t duckdb_mbx_bytes_len(moonbit_bytes_t bytes);
 void duckdb_mbx_bytes_free(moonbit_bytes_t bytes);
@@ -275,6 +277,13 @@ int32_t duckdb_mbx_result_raw(duckdb_mb_result *result, int32_t col, int32_t row
  * Layout: i64 nrows, i64 ncols, u8 null[nrows*ncols] row-major, zero pad to 8,
  * i64 offsets[nrows*ncols+1], chars.  malloc'd: free with duckdb_mbx_free. */
 char *duckdb_mbx_result_text(duckdb_mb_result *result, int64_t *len);
+
+/* Counters of the in-library multi-device path (Config::set "gpu_devices",
+ * the key rides ref src/duckdb_native.c:714-747): out6 = {shards, peer-access
+ * links enabled at connect, shard dispatches, peer DMA copies, peer DMA bytes,
+ * sharded aggregates finished on the host}; outd2 = {last dispatch wall us,
+ * last host merge us}.  Either pointer may be NULL.  Returns 6 (0: no handle). */
+int32_t duckdb_mbx_shard_stats(duckdb_mb_connection *connection, int64_t *out6, double *outd2);
 
 #ifdef __cplusplus
 }

@@ -38,6 +38,11 @@ moonbit_bytes_t moonbit_make_bytes_raw(int32_t len) {
   g_made++;
   return (moonbit_bytes_t)(h + 2);
 }
+/* the runtime's release of an object (the library drops a Bytes it built but
+ * will not return, e.g. after a failed device copy, through this) */
+void moonbit_decref(void *obj) {
+  if (obj) free((int32_t *)obj - 2);
+}
 static int32_t mb_len(moonbit_bytes_t b) { return (int32_t)(((uint32_t *)b)[-1] & ((1u << 28) - 1)); }
 static int32_t mb_rc(moonbit_bytes_t b) { return ((int32_t *)b)[-2]; }
 static void mb_free(moonbit_bytes_t b) {

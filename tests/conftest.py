@@ -9,6 +9,10 @@ import sys
 import pytest
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+# the tests set MBX_* tuning / fault-injection switches (monkeypatch); the
+# library reads them only with this opt-in (csrc/knobs.h).  Set before the
+# library is loaded: it is read once per process.
+os.environ["MBX_EXPERIMENTS"] = "1"
 if ROOT not in sys.path:
     sys.path.insert(0, ROOT)
 LIB = os.path.join(ROOT, "duckdb.mbt_amd", "libduckdb_mb_amd.so")

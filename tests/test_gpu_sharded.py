@@ -177,3 +177,101 @@ def test_sharded_select_rounds(mbx, oracle, monkeypatch, devices):
         kinds = [kk["name"] for kk in c.last_profile()["kernels"]]
         assert kinds.count("select_rounds") == devices.count(",") + 1, kinds
     c.close()
+
+
+def test_force_peer_rows_and_groups_vs_oracle(mbx, oracle):
+    """mbx_force_peer sends row results of shards that share the test GPU
+    through the multi-device move (hipMemcpyPeerAsync into the combining
+    engine, one synchronisation for all parts), as distinct MI355X devices
+    would; rows, the gathered COUNT(DISTINCT) path and GROUP BY are checked
+    against the oracle (not against another connection of the same engine)."""
+    n = 6_000_011
+    cfg = mbx.Config.create()
+    assert isinstance(cfg.set("gpu_devices", "0,0,0"), mbx.Ok)
+    assert isinstance(cfg.set("mbx_force_peer", "true"), mbx.Ok)
+    c = mbx.connect_with_config(cfg).value
+    q(c, f"CREATE TABLE t AS SELECT mbx_synth(42, i, 50) + 1 AS x, CAST(mbx_synth(7, i, 32) AS INTEGER) AS k, "
+         f"mbx_synth(9, i, 1099511627776) - 549755813888 AS v, i AS r FROM range({n}) tbl(i)")
+    x = oracle.synth_i64(n, 42, 0, 50, 1)
+    k = oracle.synth_i64(n, 7, 0, 32, 0)
+    st0 = c.shard_stats()
+    assert st0["shards"] == 3
+    # row result: every shard's passing rows moved by peer DMA, concatenated in part order
+    a = c.query_arrow("SELECT r, x FROM t WHERE x > 24 AND k < 16").value
+    br, bx = a._buf("int64", 0), a._buf("int64", 1)
+    a.close()
+    m = (x > 24) & (k < 16)
+    cnt = int.from_bytes(br[:4], "little", signed=True)
+    assert cnt == int(m.sum())
+    assert np.array_equal(np.frombuffer(br[4:4 + 8 * cnt], dtype=np.int64), np.nonzero(m)[0])
+    assert np.array_equal(np.frombuffer(bx[4:4 + 8 * cnt], dtype=np.int64), x[m])
+    st1 = c.shard_stats()
+    assert st1["peer_copies"] >= 3 * 2 and st1["peer_bytes"] >= cnt * 16, st1  # 2 columns from every shard
+    # a shape that does not decompose: every part gathered by peer DMA first
+    assert one(c, "SELECT COUNT(DISTINCT x) FROM t WHERE k < 3") == [str(len(np.unique(x[k < 3])))]
+    assert c.shard_stats()["peer_copies"] > st1["peer_copies"]
+    # C3 over the shards vs the oracle: finished on the host (no re-upload)
+    oc, osum = oracle.synth_groupby(7, 9, 0, n, 32, 1 << 40, -(1 << 39), 8)
+    h0 = c.shard_stats()["host_results"]
+    assert q(c, "SELECT k, SUM(v), COUNT(*) FROM t GROUP BY k").rows == \
+        [[str(g), str(osum[g]), str(oc[g])] for g in range(32) if oc[g]]
+    assert c.shard_stats()["host_results"] == h0 + 1
+    # the columns picked out of order, and HAVING (device path) agree
+    assert q(c, "SELECT COUNT(*), k FROM t GROUP BY k").rows == [[str(oc[g]), str(g)] for g in range(32) if oc[g]]
+    got = q(c, "SELECT k, COUNT(*) FROM t GROUP BY k HAVING COUNT(*) > 187500 ORDER BY k").rows
+    assert got == [[str(g), str(oc[g])] for g in range(32) if oc[g] > 187500]
+    c.close()
+
+
+def test_sharded_float_keys_merge_like_one_device(mbx):
+    """-0.0 and 0.0 (and every NaN) are one group on one device; the host merge
+    of the shards' partial groups must not split them.  With
+    mbx_shard_rows = 10, each 10-row INSERT fills the next part, so every
+    shard holds 0.0, -0.0 and NaN keys."""
+    vals = ["0.0", "-0.0", "NaN", "1.5", "-0.0", "NaN", "0.0", "2.5", "NaN", "-1.0"]
+    out = []
+    for devs in ("0,0,0", None):
+        if devs:
+            c = _conn(mbx, devs, shard_rows=10)
+        else:
+            c = mbx.connect().value
+        q(c, "CREATE TABLE f (d DOUBLE, i BIGINT)")
+        for part in range(3):
+            q(c, "INSERT INTO f VALUES " + ", ".join(f"('{v}'::DOUBLE, {10 * part + j})" for j, v in enumerate(vals)))
+        if devs:
+            assert q(c, "SELECT COUNT(*) FROM f").rows == [["30"]]
+        out.append(q(c, "SELECT d, COUNT(*), SUM(i) FROM f GROUP BY d ORDER BY d").rows)
+        out.append(q(c, "SELECT COUNT(*), SUM(i) FROM f WHERE d = 0.0").rows)
+        c.close()
+    assert out[0] == out[2] and out[1] == out[3]
+    assert len(out[2]) == 5, out[2]  # -1.0, 0.0, 1.5, 2.5, nan
+    assert [r[1] for r in out[2]] == ["3", "12", "3", "3", "9"], out[2]
+
+
+def test_sharded_rowwise_appender_across_parts(mbx):
+    """The row-wise appender's pinned double buffer flushed across part
+    boundaries (mbx_shard_rows smaller than a flush, flushes smaller than a
+    part): a buffer is refilled only after its DMA to whichever shard took it
+    has completed, so every value lands intact."""
+    cfg = mbx.Config.create()
+    assert isinstance(cfg.set("gpu_devices", "0,0,0,0"), mbx.Ok)
+    assert isinstance(cfg.set("mbx_shard_rows", "25000"), mbx.Ok)
+    assert isinstance(cfg.set("mbx_appender_flush_rows", "7001"), mbx.Ok)
+    c = mbx.connect_with_config(cfg).value
+    q(c, "CREATE TABLE a (v BIGINT, d DOUBLE)")
+    n = 90_000
+    v = (np.arange(n, dtype=np.int64) * 2654435761) & (2**62 - 1)
+    ap = c.create_appender("main", "a").value
+    for i in range(n):
+        ap.begin_row()
+        ap.append_bigint(int(v[i]))
+        ap.append_double(float(i) * 0.5)
+        ap.end_row()
+    ap.close()
+    got = c.query_arrow("SELECT v, d FROM a").value
+    bv = got._buf("int64", 0)
+    bd = got._buf("double", 1)
+    got.close()
+    assert np.array_equal(np.frombuffer(bv[4:], dtype=np.int64), v)
+    assert np.array_equal(np.frombuffer(bd[4:], dtype=np.float64), np.arange(n) * 0.5)
+    c.close()
