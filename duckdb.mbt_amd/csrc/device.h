@@ -351,9 +351,7 @@ struct SelectDesc {
   } col[SL_MAX_COL];
   int32_t out_col[SL_MAX_OUT];  // index into col[]
   void *dst[SL_MAX_OUT];
-  // select_rounds: the output validity bitmap of a NULL-able output (zeroed by the
-  // caller: storers OR the partial first/last words of their runs), or nullptr
-  uint64_t *vbits[SL_MAX_OUT];
+  uint8_t *vdst[SL_MAX_OUT];  // select_rounds: one validity byte per output row of a NULL-able output, or nullptr
   unsigned long long *dbg;     // nullptr, or 9 counters (MBX_SL_DEBUG) / 13 (MBX_SR_DEBUG)
   unsigned long long *dbg_ts;  // MBX_SR_DEBUG=2: s_memrealtime of every (round, workgroup) publish
 };
@@ -381,6 +379,8 @@ SelectRoundsPlan PlanSelectRounds(const SelectDesc &d, int64_t nrows);
 size_t SelectRoundsCtlBytes(const SelectRoundsPlan &p);
 hipError_t SelectRounds(const SelectDesc &d, const SelectRoundsPlan &p, int64_t nrows, unsigned long long *ctl,
                   uint32_t epoch, hipStream_t s);
+// bits[i / 64] bit i % 64 = bytes[i] (0/1), for the n output rows of a NULL-able select_rounds output
+void PackValidityBytes(const uint8_t *bytes, int64_t n, uint64_t *bits, hipStream_t s);
 
 }  // namespace dev
 }  // namespace mbx

@@ -1038,8 +1038,8 @@ static bool FastIntCol(const DRel &rel, int c) {
 // One-pass forms of the compaction below, for 4/8-byte columns, at most
 // SL_MAX_COL distinct loaded columns (predicates ∪ outputs) and SL_MAX_OUT
 // outputs.  NULL-able columns take the round-synchronous form only: a NULL
-// fails a predicate, and a NULL-able output's bitmap is written by the
-// kernel's storers (ballots per output word, boundary words ORed).  Each loaded column is read from HBM once; outputs are
+// fails a predicate, and a NULL-able output's validity comes back as one byte
+// per output row, packed into its bitmap afterwards (dev::PackValidityBytes).  Each loaded column is read from HBM once; outputs are
 // allocated for every row (the count is known only afterwards), so the form
 // is used while that upper bound stays under MBX_SL_MAX_GB (default 64).
 //  * default (n >= MBX_SR_MIN_ROWS, default 2^22): dev::SelectRounds, the
@@ -1121,13 +1121,14 @@ static bool TrySelectOnePass(Engine &e, const DRel &rel, const dev::FilterMultiD
     if (!plan.ok) return false;
   }
   std::vector<DCol> cols;
+  std::vector<DevBufPtr> vbytes(exprs.size());  // NULL-able outputs: one validity byte per output row
   for (int k = 0; k < (int)exprs.size(); k++) {
     const bool nullable = rel.cols[exprs[k]->col].validity != nullptr;
     cols.push_back(AllocOut(e, exprs[k]->type, n, nullable, false));
     S.dst[k] = cols[k].data;
-    if (nullable) {  // the storers write the bitmap itself: ORed boundary words need a zeroed start
-      S.vbits[k] = cols[k].validity;
-      HIPCHK(hipMemsetAsync(cols[k].validity, 0, (size_t)Words64(std::max<int64_t>(n, 1)) * 8, e.stream));
+    if (nullable) {  // (released to the engine's pool when this returns: later users run after the pack on e.stream)
+      vbytes[k] = Alloc(e, (size_t)std::max<int64_t>(n, 1) + 64);
+      S.vdst[k] = (uint8_t *)vbytes[k]->p;
     }
   }
   double bytes = 0;
@@ -1250,13 +1251,20 @@ static bool TrySelectOnePass(Engine &e, const DRel &rel, const dev::FilterMultiD
   }
   if (e.profile && !e.events.empty() && (e.events.back().name == "select" || e.events.back().name == "select_rounds")) {
     double ob = 0;
-    for (int k = 0; k < S.nout; k++) ob += (double)nsel * (S.col[S.out_col[k]].w + (S.vbits[k] ? 0.125 : 0));
+    for (int k = 0; k < S.nout; k++) ob += (double)nsel * (S.col[S.out_col[k]].w + (S.vdst[k] ? 1 : 0));
     e.events.back().bytes += ob;
+  }
+  for (int k = 0; k < S.nout; k++) {
+    if (!S.vdst[k]) continue;
+    ProfScope ps(e, "pack_validity", (double)nsel + nsel / 8.0, nsel);
+    dev::PackValidityBytes(S.vdst[k], nsel, cols[k].validity, e.stream);
   }
   out = DRel();
   out.n = nsel;
   out.cols = cols;
-  if (rounds_err >= 0) RaiseDeviceError(e, rounds_err);  // nothing ran after that read
+  bool packed = false;
+  for (int k = 0; k < S.nout; k++) packed |= S.vdst[k] != nullptr;
+  if (rounds_err >= 0 && !packed) RaiseDeviceError(e, rounds_err);  // nothing ran after that read
   else CheckError(e);
   return true;
 }

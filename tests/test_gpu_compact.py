@@ -278,8 +278,8 @@ def _ncol(conn, sql, kind, idx=0):
 def test_filter_compact_nullable(mbx, oracle, monkeypatch, n, path):
     """NULLs in predicate columns (a NULL fails the row) and in output columns:
     the two-pass path (validity bits compacted by compact_validity) and the
-    one-pass select_rounds (validity words in a second ring; the storers write
-    the output bitmap, ORing the boundary words of their runs), forced at every size with
+    one-pass select_rounds (validity words in a second ring, one byte per
+    output row packed by pack_validity), forced at every size with
     MBX_SR_MIN_ROWS=0; values and validity exact vs numpy and vs the VM path
     (MBX_FC=0)."""
     if path != "auto":
@@ -312,9 +312,10 @@ def test_filter_compact_nullable(mbx, oracle, monkeypatch, n, path):
             names = [kk["name"] for kk in c.last_profile()["kernels"]]
             # NULL-free loaded columns (tiny n) take the one-pass kernel
             assert "filter_bits" in names or "select" in names or "select_rounds" in names, (sql, names)
-            if path == "rounds":  # the bitmap comes from the storers: no second kernel
+            if path == "rounds":
                 assert "select_rounds" in names and "filter_bits" not in names, (sql, names)
-                assert "compact_validity" not in names and "pack_validity" not in names, (sql, names)
+                if i == 0 and not valid.all() and m.any():
+                    assert "pack_validity" in names, (sql, names)
             elif i == 0 and not valid.all() and m.any() and "select_rounds" not in names:
                 assert "compact_validity" in names, (sql, names)
             assert np.array_equal(ok, valid[m]), (n, sql, i)

@@ -4,9 +4,10 @@ every shard at once and is combined by the connection's first device.  On the
 1-GPU test box the shards share device 0 ("0,0", "0,0,0"), which exercises the
 same split / per-shard kernels / combine code as distinct devices.
 
-Aggregates (C2, C5, C3 shapes) are checked against the CPU oracle; row
-results, hash GROUP BY, AVG and appender ingest against an unsharded
-connection holding the same rows."""
+Everything is checked against the CPU oracle or numpy over the oracle's
+generator: aggregates (C2, C5, C3 shapes), row results, hash GROUP BY, HAVING,
+AVG over DECIMAL / DOUBLE, streams, CTAS, appender ingest; with
+mbx_force_peer the same-device shards also exchange rows by peer DMA."""
 import numpy as np
 import pytest
 
@@ -61,53 +62,92 @@ def test_sharded_c3_group_by(mbx, oracle):
     c.close()
 
 
-def test_sharded_rows_and_hash_groups_match_unsharded(mbx):
+@pytest.mark.parametrize("force_peer", [False, True])
+def test_sharded_rows_and_hash_groups_vs_numpy(mbx, oracle, force_peer):
+    """Row results, hash GROUP BY (VARCHAR / NULL keys, two keys), HAVING,
+    ORDER BY / LIMIT, AVG / SUM over DECIMAL and DOUBLE, streams and CTAS over a
+    2-shard table, each against numpy over the oracle's generator (not against
+    another connection of the same engine)."""
+    from oracle import fmt
     n = 1_000_003
     sql_t = (f"CREATE TABLE h AS SELECT mbx_synth(42, i, 50) + 1 AS x, "
              f"CASE WHEN mbx_synth(5, i, 9) = 0 THEN NULL WHEN mbx_synth(3, i, 3) = 0 THEN 'apple' "
              f"WHEN mbx_synth(3, i, 3) = 1 THEN 'kiwi' ELSE 'fig' END AS s, "
              f"CAST(mbx_synth(11, i, 100000) - 50000 AS DECIMAL(12,2)) AS d, mbx_synth(13, i, 1000) / 7 AS f, "
              f"i AS r FROM range({n}) tbl(i)")
-    shard = _conn(mbx, "0,0")
-    plain = mbx.connect().value
-    for c in (shard, plain):
-        q(c, sql_t)
-    queries = [
-        "SELECT r, x FROM h WHERE x > 24 AND r % 3 = 0",
-        "SELECT r FROM h WHERE x BETWEEN 10 AND 12 ORDER BY r DESC LIMIT 1000 OFFSET 5",
-        "SELECT s, COUNT(*), SUM(x), MIN(r), MAX(r) FROM h GROUP BY s ORDER BY s NULLS LAST",
-        "SELECT x % 7 AS m, s, COUNT(*) FROM h WHERE r > 100 GROUP BY m, s ORDER BY m, s",
-        "SELECT COUNT(DISTINCT x) FROM h",
-        "SELECT COUNT(s), COUNT(*), MIN(x) FROM h WHERE s IS NOT NULL",
-        "SELECT x, COUNT(*) FROM h GROUP BY x HAVING SUM(r) > 10000000000 ORDER BY x",
-        "SELECT AVG(d), SUM(d), MIN(d), MAX(d) FROM h WHERE x < 30",
-    ]
-    for sql in queries:
-        a, b = q(shard, sql), q(plain, sql)
-        assert a.column_types == b.column_types, sql
-        assert a.rows == b.rows, sql
+    cfg = mbx.Config.create()
+    assert isinstance(cfg.set("gpu_devices", "0,0"), mbx.Ok)
+    if force_peer:
+        assert isinstance(cfg.set("mbx_force_peer", "true"), mbx.Ok)
+    c = mbx.connect_with_config(cfg).value
+    q(c, sql_t)
+    x = oracle.synth_i64(n, 42, 0, 50, 1)
+    s5 = oracle.synth_i64(n, 5, 0, 9, 0)
+    s3 = oracle.synth_i64(n, 3, 0, 3, 0)
+    sv = np.where(s3 == 0, "apple", np.where(s3 == 1, "kiwi", "fig")).astype(object)
+    sv[s5 == 0] = None
+    snull = s5 == 0
+    draw = (oracle.synth_i64(n, 11, 0, 100000, 0) - 50000) * 100  # DECIMAL(12,2) unscaled
+    fv = oracle.synth_i64(n, 13, 0, 1000, 0) / 7.0
+    r = np.arange(n, dtype=np.int64)
+
+    def rows(sql):
+        return q(c, sql).rows
+
+    m = (x > 24) & (r % 3 == 0)
+    assert rows("SELECT r, x FROM h WHERE x > 24 AND r % 3 = 0") == [[str(a), str(b)] for a, b in zip(r[m], x[m])]
+    sel = np.sort(r[(x >= 10) & (x <= 12)])[::-1][5:1005]
+    assert rows("SELECT r FROM h WHERE x BETWEEN 10 AND 12 ORDER BY r DESC LIMIT 1000 OFFSET 5") == \
+        [[str(v)] for v in sel]
+    exp = []
+    for key in ["apple", "fig", "kiwi", None]:
+        mk = snull if key is None else (~snull) & (sv == key)
+        exp.append(["" if key is None else key, str(int(mk.sum())), str(int(x[mk].sum())), str(int(r[mk].min())),
+                    str(int(r[mk].max()))])
+    res = q(c, "SELECT s, COUNT(*), SUM(x), MIN(r), MAX(r) FROM h GROUP BY s ORDER BY s NULLS LAST")
+    assert res.rows == exp
+    assert res.column_types == ["Varchar", "BigInt", "HugeInt", "BigInt", "BigInt"]
+    exp = []
+    mr = r > 100
+    for mm in range(7):
+        for key in ["apple", "fig", "kiwi", None]:
+            mk = mr & (x % 7 == mm) & (snull if key is None else (~snull) & (sv == key))
+            if mk.any():
+                exp.append([str(mm), "" if key is None else key, str(int(mk.sum()))])
+    assert rows("SELECT x % 7 AS m, s, COUNT(*) FROM h WHERE r > 100 GROUP BY m, s ORDER BY m, s") == exp
+    assert rows("SELECT COUNT(DISTINCT x) FROM h") == [[str(len(np.unique(x)))]]
+    assert rows("SELECT COUNT(s), COUNT(*), MIN(x) FROM h WHERE s IS NOT NULL") == \
+        [[str(int((~snull).sum())), str(int((~snull).sum())), str(int(x[~snull].min()))]]
+    exp = [[str(v), str(int((x == v).sum()))] for v in range(1, 51) if int(r[x == v].sum()) > 10_000_000_000]
+    assert rows("SELECT x, COUNT(*) FROM h GROUP BY x HAVING SUM(r) > 10000000000 ORDER BY x") == exp
+    md = x < 30
+    got = rows("SELECT AVG(d), SUM(d), MIN(d), MAX(d) FROM h WHERE x < 30")[0]
+    ssum = int(draw[md].sum())
+    assert got[1:] == [fmt.decimal(ssum, 2), fmt.decimal(int(draw[md].min()), 2), fmt.decimal(int(draw[md].max()), 2)]
+    avg = float(ssum) / (float(md.sum()) * 100.0)
+    assert abs(float(got[0]) - avg) <= 1e-12 * abs(avg)
     # DOUBLE sums: summation order differs between shards (stated tolerance 1e-9 relative)
-    a, b = q(shard, "SELECT SUM(f), AVG(f), MIN(f), MAX(f) FROM h").rows[0], q(plain, "SELECT SUM(f), AVG(f), MIN(f), MAX(f) FROM h").rows[0]
-    for u, w in zip(a, b):
-        assert abs(float(u) - float(w)) <= 1e-9 * abs(float(w)), (a, b)
-    # stream read-back of a sharded SELECT: same rows in the same order
-    st = shard.query_stream("SELECT r FROM h WHERE x > 40").value
+    got = [float(v) for v in rows("SELECT SUM(f), AVG(f), MIN(f), MAX(f) FROM h")[0]]
+    for u, w in zip(got, [float(fv.sum()), float(fv.mean()), float(fv.min()), float(fv.max())]):
+        assert abs(u - w) <= 1e-9 * abs(w)
+    # stream read-back of a sharded SELECT: the rows in part (= row) order
+    st = c.query_stream("SELECT r FROM h WHERE x > 40").value
     got = []
     while True:
-        r = st.next().value
-        if r is None:
+        ch = st.next().value
+        if ch is None:
             break
-        got.extend(int(row[0]) for row in r.rows)
+        got.extend(int(row[0]) for row in ch.rows)
     st.close()
-    assert got == [int(r[0]) for r in q(plain, "SELECT r FROM h WHERE x > 40").rows]
+    assert got == r[x > 40].tolist()
     # CTAS from a sharded table stays sharded part by part; DROP removes every part
-    q(shard, "CREATE TABLE h2 AS SELECT r, x FROM h WHERE x > 24")
-    q(plain, "CREATE TABLE h2 AS SELECT r, x FROM h WHERE x > 24")
-    assert one(shard, "SELECT COUNT(*), SUM(r) FROM h2") == one(plain, "SELECT COUNT(*), SUM(r) FROM h2")
-    q(shard, "DROP TABLE h2")
-    assert isinstance(shard.query("SELECT COUNT(*) FROM h2"), mbx.Err)
-    shard.close()
-    plain.close()
+    q(c, "CREATE TABLE h2 AS SELECT r, x FROM h WHERE x > 24")
+    assert rows("SELECT COUNT(*), SUM(r) FROM h2") == [[str(int((x > 24).sum())), str(int(r[x > 24].sum()))]]
+    q(c, "DROP TABLE h2")
+    assert isinstance(c.query("SELECT COUNT(*) FROM h2"), mbx.Err)
+    if force_peer:
+        assert c.shard_stats()["peer_copies"] > 0
+    c.close()
 
 
 def test_sharded_appender_fills_parts_in_order(mbx):

@@ -1,0 +1,64 @@
+# One GPU pass on the box (gpurun): the steps named in STEPS run in this order,
+# each under its own time limit; the chain stops at the first failure.
+#   tests     the -m gpu suite (PYTEST_K narrows it)      smoke   __graft_entry__.smoke()
+#   bench     the headline line (C2 + C3/sel extras, CPU baseline)
+#   configs   bench.py --config c3 / c5 / sel / c4        shards  --shards-per-gpu 2 (c2, c5, c3)
+#   overhead  tools/shard_overhead.py                      shapes  tools/shape_bench.py (SHAPES, NULLABLE)
+#   layout    tools/c3_layout_probe.py                     rehearse  2 gloo ranks on one GPU (--ranks)
+#   prof      rocprofv3 --kernel-trace --stats of bench.py (c2 line with extras)
+#   pmc       rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes of bench.py (one counter set per run)
+#   link      tools/link8_probe (8 MB D2H variants; build it first: see its header)
+# Results go to gpurun_out/ (merged back by gpurun); copy what is judged into profiles/.
+set -o pipefail
+mkdir -p gpurun_out
+R=${GRAFT_REPO_ROOT:-$PWD}
+STEPS=${STEPS:-tests,smoke,bench}
+has() { [[ ",$STEPS," == *",$1,"* ]]; }
+if has tests; then
+  timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread ${PYTEST_K:+-k "$PYTEST_K"} > gpurun_out/gpu_tests.log 2>&1 || exit 11
+fi
+if has smoke; then
+  timeout -k 10 180 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1 || exit 12
+fi
+if has bench; then
+  timeout -k 10 300 python bench.py > gpurun_out/bench_c2.json 2> gpurun_out/bench_c2.err || exit 13
+fi
+if has configs; then
+  for c in c3 c5 sel; do
+    timeout -k 10 300 python bench.py --config $c --extra "" > gpurun_out/bench_$c.json 2> gpurun_out/bench_$c.err || exit 14
+  done
+  timeout -k 10 400 python bench.py --config c4 > gpurun_out/bench_c4.json 2> gpurun_out/bench_c4.err || exit 15
+fi
+if has shards; then
+  for c in c2 c5 c3; do
+    timeout -k 10 240 python bench.py --shards-per-gpu 2 --config $c --no-cpu > gpurun_out/bench_${c}_s2.json 2> gpurun_out/bench_${c}_s2.err || exit 16
+  done
+fi
+if has overhead; then
+  timeout -k 10 240 python tools/shard_overhead.py > gpurun_out/shard_overhead.json 2> gpurun_out/shard_overhead.err || exit 17
+fi
+if has shapes; then
+  SHAPES=${SHAPES:-seln_out,seln_pred,seln_both,sel,compact,compact2} NULLABLE=1 timeout -k 10 400 python tools/shape_bench.py ${SHAPE_ROWS:-1000000000} > gpurun_out/shapes.json 2> gpurun_out/shapes.err || exit 18
+fi
+if has layout; then
+  timeout -k 10 300 python tools/c3_layout_probe.py > gpurun_out/c3_layout.json 2> gpurun_out/c3_layout.err || exit 19
+fi
+if has rehearse; then
+  for c in c2 c5 c3; do
+    timeout -k 10 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 2951${#c} bench.py --ranks --gpus 2 --config $c --dist-backend gloo --no-cpu --steps 10 > gpurun_out/rehearse_n2_$c.json 2> gpurun_out/rehearse_n2_$c.err || exit 20
+  done
+fi
+if has prof; then
+  mkdir -p gpurun_out/prof
+  ( cd /tmp && export TMPDIR=/tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $R/gpurun_out/prof/c2 -o c2 -- python3 $R/bench.py --steps 10 --no-cpu > $R/gpurun_out/prof_c2.log 2>&1 ) || exit 21
+fi
+if has pmc; then
+  mkdir -p gpurun_out/pmc
+  for ctr in FETCH_SIZE WRITE_SIZE; do
+    ( cd /tmp && export TMPDIR=/tmp && timeout -s KILL 300 rocprofv3 --pmc $ctr --output-format csv -d $R/gpurun_out/pmc/$ctr -o $ctr -- python3 $R/bench.py --steps 5 --warmup 1 --no-cpu > $R/gpurun_out/pmc_$ctr.log 2>&1 ) || exit 22
+  done
+fi
+if has link; then
+  timeout -k 10 200 ./tools/link8_probe ${LINK_MB:-8} 200 > gpurun_out/link8_probe.log 2>&1 || exit 23
+fi
+echo ALL_OK
