@@ -82,6 +82,7 @@ _sig("duckdb_mbx_hbm_calibrate", _I, _P, _L, _I, ctypes.POINTER(ctypes.c_double)
 _sig("duckdb_mbx_hbm_calibrate_ex", _I, _P, _L, _I, ctypes.POINTER(ctypes.c_double), _I)
 _sig("duckdb_mbx_statement_plan_stats", _I, _P, ctypes.POINTER(ctypes.c_int64))
 _sig("duckdb_mbx_shard_stats", _I, _P, ctypes.POINTER(ctypes.c_int64), ctypes.POINTER(ctypes.c_double))
+_sig("duckdb_mbx_engine_stats", _I, _P, ctypes.POINTER(ctypes.c_int64))
 
 for _n in ["duckdb_mb_connect"]:
     _sig(_n, _P, _B)
@@ -589,6 +590,13 @@ class Connection:
         return {"shards": out[0], "peer_links": out[1], "dispatches": out[2], "peer_copies": out[3],
                 "peer_bytes": out[4], "host_results": out[5], "last_dispatch_us": outd[0],
                 "last_combine_us": outd[1]}
+
+    def engine_stats(self) -> dict:
+        """select_rounds outcomes (extension): launches, aborts, launch failures."""
+        out = (ctypes.c_int64 * 3)()
+        lib.duckdb_mbx_engine_stats(self._h, out)
+        return {"select_rounds_launches": out[0], "select_rounds_aborts": out[1],
+                "select_rounds_launch_failures": out[2]}
 
     def profile_drain(self) -> list:
         import json

@@ -50,6 +50,11 @@ Value HostColumn::Get(int64_t row) const {
 }
 
 int HostColumn::FormatInto(int64_t row, char *out) const {
+  if (!text_off.empty()) {  // formatted on the device with the result
+    const uint32_t b = text_off[row], n = text_off[row + 1] - b - 1;
+    memcpy(out, text.data() + b, n);
+    return (int)n;
+  }
   const uint8_t *p = data.data();
   i128 x;
   switch (phys) {

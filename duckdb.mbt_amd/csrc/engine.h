@@ -68,6 +68,11 @@ struct HostColumn {
   std::vector<uint8_t> valid;        // 1 byte per row (1 = valid)
   std::vector<int64_t> offsets;      // P_STR
   std::string chars;                 // P_STR
+  // cell text formatted on the device (large integer / BOOLEAN / DECIMAL /
+  // HUGEINT results of duckdb_mb_query and stream batches): row i's text is
+  // text[text_off[i], text_off[i + 1] - 1) (each row's text is followed by a NUL)
+  std::vector<uint32_t> text_off;
+  std::string text;
   Value Get(int64_t row) const;
   // Text of a non-NULL integer/BOOLEAN/DECIMAL cell written into out (>= 48
   // bytes), spelled as FormatValue(Get(row)); -1 for the other types.
@@ -213,5 +218,8 @@ void AppendRawColumns(Connection &c, Table &t, const std::vector<const void *> &
 void SettleAppends(Connection &c);
 void HostColumnPush(HostColumn &col, const Value &v);  // v already of col.type (or NULL)
 void HbmCalibrateConn(Connection &c, int64_t bytes, int iters, double out[7]);
+// adds this connection's (and its shards') select_rounds counters to out:
+// launches, aborts (a workgroup never scheduled: the two-pass form reran), launch failures
+void EngineCounters(const Connection &c, int64_t out[3]);
 
 }  // namespace mbx

@@ -162,6 +162,10 @@ struct Engine {
   // an async append's DMA from a pinned appender buffer is in flight: the next
   // SettlePending waits for it, so the buffer is never refilled under the DMA
   bool inflight_h2d = false;
+  // select_rounds outcomes (duckdb_mbx_engine_stats): launches, launches that
+  // gave up because a workgroup was never scheduled (the two-pass form reran
+  // the query), launches that failed to start
+  int64_t sr_launches = 0, sr_aborts = 0, sr_launch_failures = 0;
   bool profile = false;
   std::vector<ProfEvent> events;
   // kernels timed on shard engines during this query (gpu_devices)
@@ -1169,7 +1173,9 @@ static bool TrySelectOnePass(Engine &e, const DRel &rel, const dev::FilterMultiD
       ProfScope ps(e, "select_rounds", bytes, n);  // algorithmic: inputs once (+ the selected rows' outputs, added below)
       launch = dev::SelectRounds(S, plan, n, e.d_rounds, epoch, e.stream);
     }
+    e.sr_launches++;
     if (launch != hipSuccess) {  // nothing ran: the control block still holds the last launch's total
+      e.sr_launch_failures++;
       if (e.profile && !e.events.empty() && e.events.back().name == "select_rounds")
         e.events.back().name = "select_rounds_launch_failed";
       return false;  // the two-pass form instead
@@ -1225,6 +1231,7 @@ static bool TrySelectOnePass(Engine &e, const DRel &rel, const dev::FilterMultiD
     memcpy(&rounds_err, e.h_pinned + 16, sizeof(rounds_err));
     lk.unlock();
     if (h[0] == (unsigned long long)epoch) {  // a workgroup was never scheduled: two-pass form instead
+      e.sr_aborts++;
       if (e.profile && !e.events.empty() && e.events.back().name == "select_rounds") e.events.back().name = "select_rounds_abort";
       return false;
     }
@@ -1938,7 +1945,7 @@ static bool JitGroupAggregate(Engine &e, const DRel &src, const BoundSelect &s, 
 }
 
 static ResultPtr ToHost(Engine &e, const DRel &r, const std::vector<std::string> &names, int64_t offset, int64_t limit,
-                        size_t ncols);
+                        size_t ncols, bool text = false);
 static void KeyBytes(const Value &v, std::string &out);
 static DRel Aggregate(Engine &e, const DRel &src, const BoundSelect &s);
 
@@ -2563,8 +2570,34 @@ static DRel ConcatRels(Engine &e, std::vector<DRel> &parts) {
 // the stream once.  Returns nullptr when the result does not qualify.
 // Rows [start, start + n) of every column land in the pinned arena (grown on
 // demand) with ONE synchronisation; the device error word rides along.
+// Large results pulled cell by cell (duckdb_mb_query, stream batches) bring
+// their integer / BOOLEAN / DECIMAL / HUGEINT cells' text along: the text
+// kernels format the rows on the device (lengths -> scan -> write, as the
+// Arrow string getters do) and the lengths and the NUL-separated text ride the
+// same D2H as the values, so duckdb_mb_result_value / duckdb_mb_chunk_value
+// only copy bytes.  From kTextRows rows (smaller results keep host formatting).
+constexpr int64_t kTextRows = 65536;
+
+static bool TextCol(const DCol &d, int64_t start, dev::TextCol &tc) {
+  if (!d.data || d.phys > P_I128) return false;
+  switch (d.type.id) {
+    case T_BOOLEAN: case T_TINYINT: case T_SMALLINT: case T_INTEGER: case T_BIGINT: case T_UTINYINT:
+    case T_USMALLINT: case T_UINTEGER: case T_UBIGINT: case T_HUGEINT: case T_DECIMAL:
+      break;
+    default:
+      return false;
+  }
+  if (d.validity && (start & 63)) return false;  // validity words must start at the first row
+  tc.data = (const char *)d.data + (size_t)start * PhysSize(d.phys);
+  tc.valid = d.validity ? d.validity + (start >> 6) : nullptr;
+  tc.phys = d.phys;
+  tc.kind = d.type.id == T_BOOLEAN ? dev::TEXT_BOOL : d.type.id == T_DECIMAL ? dev::TEXT_DECIMAL : dev::TEXT_INT;
+  tc.scale = d.type.id == T_DECIMAL ? d.type.scale : 0;
+  return true;
+}
+
 static ResultPtr ToHostPinned(Engine &e, const DRel &r, const std::vector<std::string> &names, size_t ncols,
-                              int64_t start, int64_t n) {
+                              int64_t start, int64_t n, bool text = false) {
   size_t need = 64;
   const int64_t w0 = start >> 6, w1 = (start + n + 63) >> 6;
   for (size_t c = 0; c < ncols; c++) {
@@ -2573,9 +2606,48 @@ static ResultPtr ToHostPinned(Engine &e, const DRel &r, const std::vector<std::s
     need += ((size_t)n * PhysSize(d.phys) + 63) & ~(size_t)63;
     if (d.validity) need += ((size_t)(w1 - w0) * 8 + 63) & ~(size_t)63;
   }
+  // device text: per eligible column, lengths and an exclusive scan (the
+  // totals read back with one synchronisation), then the text itself
+  struct TextJob {
+    size_t c;
+    dev::TextCol tc;
+    DevBufPtr lens, offs, chars;
+    int64_t total = 0;
+    size_t len_off = 0, chr_off = 0;
+  };
+  std::vector<TextJob> tj;
+  if (text && n >= kTextRows && n < ((int64_t)1 << 31)) {
+    for (size_t c = 0; c < ncols && tj.size() < 64; c++) {
+      TextJob j;
+      j.c = c;
+      if (!TextCol(r.cols[c], start, j.tc)) continue;
+      j.lens = Alloc(e, (size_t)n * 4);
+      j.offs = Alloc(e, (size_t)(n + 1) * 8);
+      {
+        ProfScope ps(e, "text_lengths", (double)n * PhysSize(r.cols[c].phys), n);
+        dev::TextLengths(j.tc, n, (uint32_t *)j.lens->p, e.stream);
+      }
+      dev::ScanTileCounts((const uint32_t *)j.lens->p, (int64_t *)j.offs->p, n, e.d_scratch + 64 + tj.size(),
+                          e.stream);
+      tj.push_back(j);
+    }
+    if (!tj.empty()) {
+      HIPCHK(hipMemcpyAsync(e.h_pinned, e.d_scratch + 64, tj.size() * 8, hipMemcpyDeviceToHost, e.stream));
+      HIPCHK(hipStreamSynchronize(e.stream));
+      for (size_t k = 0; k < tj.size(); k++) memcpy(&tj[k].total, e.h_pinned + 8 * k, 8);
+      tj.erase(std::remove_if(tj.begin(), tj.end(), [](const TextJob &j) { return j.total > (int64_t)UINT32_MAX; }),
+               tj.end());  // 32-bit text offsets on the host
+      for (size_t k = 0; k < tj.size(); k++) {
+        tj[k].chars = Alloc(e, (size_t)std::max<int64_t>(tj[k].total, 16));
+        ProfScope ps(e, "text_write", (double)n * PhysSize(r.cols[tj[k].c].phys) + (double)tj[k].total, n);
+        dev::TextWrite(tj[k].tc, n, (const int64_t *)tj[k].offs->p, (char *)tj[k].chars->p, nullptr, e.stream);
+        need += (((size_t)n * 4 + 63) & ~(size_t)63) + (((size_t)tj[k].total + 63) & ~(size_t)63);
+      }
+    }
+  }
   // small results: one copy kernel into the coherent mapped buffer instead of
   // one DMA per buffer; larger ones: DMA into the (growable) pinned arena
-  const bool mapped = need <= Engine::kMappedBytes && ncols * 2 <= HOSTCOPY_MAX && !Knob("MBX_NO_HOSTCOPY");
+  const bool mapped = tj.empty() && need <= Engine::kMappedBytes && ncols * 2 <= HOSTCOPY_MAX && !Knob("MBX_NO_HOSTCOPY");
   if (!mapped && !e.EnsurePinned(need)) return nullptr;
   uint8_t *const H = mapped ? e.h_mapped : e.h_pinned;
   std::vector<size_t> data_off(ncols), valid_off(ncols, 0);
@@ -2600,6 +2672,14 @@ static ResultPtr ToHostPinned(Engine &e, const DRel &r, const std::vector<std::s
       if (n > 0) seg(d.validity + w0, at, vb);
       at += (vb + 63) & ~(size_t)63;
     }
+  }
+  for (auto &j : tj) {
+    j.len_off = at;
+    seg(j.lens->p, at, (size_t)n * 4);
+    at += ((size_t)n * 4 + 63) & ~(size_t)63;
+    j.chr_off = at;
+    if (j.total) seg(j.chars->p, at, (size_t)j.total);
+    at += ((size_t)j.total + 63) & ~(size_t)63;
   }
   if (mapped) {
     hd.err_src = e.d_err;
@@ -2626,18 +2706,30 @@ static ResultPtr ToHostPinned(Engine &e, const DRel &r, const std::vector<std::s
       hc.valid.resize(n);
       for (int64_t i = 0; i < n; i++) hc.valid[i] = (bm[(i + sh) >> 6] >> ((i + sh) & 63)) & 1;
     }
+    for (auto &j : tj) {
+      if (j.c != c) continue;
+      const uint32_t *len = (const uint32_t *)(H + j.len_off);
+      hc.text_off.resize((size_t)n + 1);
+      uint32_t o = 0;
+      for (int64_t i = 0; i < n; i++) {
+        hc.text_off[i] = o;
+        o += len[i];
+      }
+      hc.text_off[n] = o;
+      hc.text.assign((const char *)H + j.chr_off, (size_t)j.total);
+    }
     res->cols.push_back(std::move(hc));
   }
   return res;
 }
 
 static ResultPtr ToHost(Engine &e, const DRel &r, const std::vector<std::string> &names, int64_t offset, int64_t limit,
-                        size_t ncols) {
+                        size_t ncols, bool text) {
   int64_t start = std::min(std::max<int64_t>(offset, 0), r.n);
   int64_t n = r.n - start;
   if (limit >= 0) n = std::min(n, limit);
   {
-    ResultPtr p = ToHostPinned(e, r, names, ncols, start, n);
+    ResultPtr p = ToHostPinned(e, r, names, ncols, start, n, text);
     if (p) return p;
   }
   auto res = std::make_shared<MaterializedResult>();
@@ -2923,7 +3015,7 @@ ResultPtr ExecuteSelect(Connection &c, const BoundSelect &s) {
   }
   DRel r = RunSelectDev(e, c, s);
   std::vector<std::string> names(s.names.begin(), s.names.begin() + VisibleCols(s));
-  ResultPtr res = ToHost(e, r, names, 0, -1, names.size());  // raises pending device errors
+  ResultPtr res = ToHost(e, r, names, 0, -1, names.size(), true);  // raises pending device errors
   double ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
   FinishProfile(c, e, ms);
   return res;
@@ -2960,7 +3052,7 @@ DeviceResultPtr ExecuteSelectDevice(Connection &c, const BoundSelect &s, StreamS
 
 ResultPtr FetchDeviceRows(Connection &c, DeviceResult &d, int64_t start, int64_t n) {
   Engine &e = Eng(c);
-  return ToHost(e, d.r, d.names, start, n, d.names.size());
+  return ToHost(e, d.r, d.names, start, n, d.names.size(), true);
 }
 
 bool DeviceColumnWireOk(const DeviceResult &d, int col, int phys) {
@@ -3946,6 +4038,15 @@ void OpenShards(Connection &c) {
   (void)hipGetLastError();  // "already enabled" is not an error here
   hipSetDevice(c.engine->device);
   c.workers = std::make_shared<ShardWorkers>((int)c.shards.size());
+}
+
+void EngineCounters(const Connection &c, int64_t out[3]) {
+  if (c.engine) {
+    out[0] += c.engine->sr_launches;
+    out[1] += c.engine->sr_aborts;
+    out[2] += c.engine->sr_launch_failures;
+  }
+  for (auto &sc : c.shards) EngineCounters(*sc, out);
 }
 
 void HbmCalibrateConn(Connection &c, int64_t bytes, int iters, double out[7]) {

@@ -469,7 +469,7 @@ struct SrCols {
 // chains interleave (one loader wave per SIMD cannot hide its own latencies).
 // NL loader waves (4 or 8: two per SIMD hide each other's latencies), 4
 // storers (storer s drains loaders s, s + 4, ...) and one coordinator.
-// VAL: some columns carry validity words (H = 1).  A step's 32 B of words per
+// VAL: some columns carry validity words.  A sub-step's 32 B of words per
 // NULL-able column ride a second ring (one exec-masked LDS-DMA instruction
 // each, counted exactly in the wait); a NULL fails a predicate, and a NULL-able
 // output stages one validity byte per selected row, which its storer writes to
@@ -482,7 +482,6 @@ template <int NC, int WM, int DEPTH, int H, int NL, bool VAL>
 __global__ __launch_bounds__((NL + 5) * 64) void select_rounds_kernel(SelectDesc D, int64_t n, int64_t nrounds, int S, int stg,
                                                             unsigned long long *ctl, uint32_t epoch, int sleep_,
                                                             int test_stall, int pwmax) {
-  static_assert(!VAL || H == 1, "validity words are laid out per 256-row step");
   typedef SrCols<NC, WM> L;
   extern __shared__ __attribute__((aligned(16))) unsigned char sr_lds[];
   __shared__ SrShared sm;
@@ -525,7 +524,7 @@ __global__ __launch_bounds__((NL + 5) * 64) void select_rounds_kernel(SelectDesc
     vsoff[c] = rowb * (stg + 64);
     if (hv[c] && ((smask >> c) & 1)) rowb += 1;
   }
-  constexpr int VSB = VAL ? NC * 32 : 0;  // validity ring slot
+  constexpr int VSB = VAL ? H * NC * 32 : 0;  // validity ring slot: 4 words per sub-step and NULL-able column
   unsigned char *stage0 = sr_lds + (size_t)NL * DEPTH * SB + (size_t)NL * DEPTH * VSB;
   const uint32_t mask = (uint32_t)stg - 1;
   const uint64_t lt = (1ull << lane) - 1;
@@ -571,10 +570,12 @@ __global__ __launch_bounds__((NL + 5) * 64) void select_rounds_kernel(SelectDesc
       }
       if constexpr (VAL) {
 #pragma unroll
-        for (int c = 0; c < NC; c++)
-          if (hv[c] && lane < 2)
-            __builtin_amdgcn_global_load_lds((const void *)(D.col[c].valid + q * 4 + lane * 2),
-                                             (void *)(vring + slot * VSB + voff[c]), 16, 0, 2);
+        for (int h = 0; h < H; h++)
+#pragma unroll
+          for (int c = 0; c < NC; c++)
+            if (hv[c] && lane < 2)
+              __builtin_amdgcn_global_load_lds((const void *)(D.col[c].valid + (q * H + h) * 4 + lane * 2),
+                                               (void *)(vring + slot * VSB + h * NC * 32 + voff[c]), 16, 0, 2);
       }
     };
 #pragma unroll
@@ -609,10 +610,10 @@ __global__ __launch_bounds__((NL + 5) * 64) void select_rounds_kernel(SelectDesc
         if (dbg) t0 = clock64();
         if constexpr (VAL) {
           switch (nv) {  // wave-uniform: the exact count of the instructions issued after this slot's
-            case 1: sr_wait<(NI + 1) * (DEPTH - 1)>(); break;
-            case 2: sr_wait<(NI + 2) * (DEPTH - 1)>(); break;
-            case 3: sr_wait<(NI + 3) * (DEPTH - 1)>(); break;
-            default: sr_wait<(NI + 4) * (DEPTH - 1)>(); break;
+            case 1: sr_wait<(NI + H) * (DEPTH - 1)>(); break;
+            case 2: sr_wait<(NI + 2 * H) * (DEPTH - 1)>(); break;
+            case 3: sr_wait<(NI + 3 * H) * (DEPTH - 1)>(); break;
+            default: sr_wait<(NI + 4 * H) * (DEPTH - 1)>(); break;
           }
         } else {
           asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NI * (DEPTH - 1)) : "memory");
@@ -624,17 +625,20 @@ __global__ __launch_bounds__((NL + 5) * 64) void select_rounds_kernel(SelectDesc
         for (int h = 0; h < H; h++)
 #pragma unroll
           for (int c = 0; c < NC; c++) sl_read4(src + h * SB1 + L::off(c), L::w(c), lane, v[h][c]);
-        // validity of rows 4 lane .. 4 lane + 3 per column (bit e), all valid without words
-        uint32_t vmc[NC];
+        // validity of rows 256 h + 4 lane .. + 3 per column (bit e), all valid without words
+        uint32_t vmc[H][NC];
 #pragma unroll
-        for (int c = 0; c < NC; c++) {
-          vmc[c] = 0xFu;
-          if constexpr (VAL) {
-            if (hv[c])
-              vmc[c] = (uint32_t)(*(const uint64_t *)(vring + k * VSB + voff[c] + (lane >> 4) * 8) >> (4 * (lane & 15))) &
-                       0xFu;
+        for (int h = 0; h < H; h++)
+#pragma unroll
+          for (int c = 0; c < NC; c++) {
+            vmc[h][c] = 0xFu;
+            if constexpr (VAL) {
+              if (hv[c])
+                vmc[h][c] = (uint32_t)(*(const uint64_t *)(vring + k * VSB + h * NC * 32 + voff[c] + (lane >> 4) * 8) >>
+                                       (4 * (lane & 15))) &
+                            0xFu;
+            }
           }
-        }
         // ok[h][e]: row 256 h + 4 lane + e passes (kept as lane masks: each ballot is the compare's own mask)
         const bool live = s < live_steps;
         bool ok[H][4];
@@ -649,9 +653,11 @@ __global__ __launch_bounds__((NL + 5) * 64) void select_rounds_kernel(SelectDesc
           for (int h = 0; h < H; h++)
 #pragma unroll
             for (int e = 0; e < 4; e++) ok[h][e] = ok[h][e] & ((uint64_t)(v[h][c][e]) - (uint64_t)(lo[c]) <= span[c]);
-          if constexpr (VAL) {  // a NULL fails the predicate (H = 1)
+          if constexpr (VAL) {  // a NULL fails the predicate
 #pragma unroll
-            for (int e = 0; e < 4; e++) ok[0][e] = ok[0][e] & (((vmc[c] >> e) & 1u) != 0);
+            for (int h = 0; h < H; h++)
+#pragma unroll
+              for (int e = 0; e < 4; e++) ok[h][e] = ok[h][e] & (((vmc[h][c] >> e) & 1u) != 0);
           }
         }
         unsigned long long b[H][4];
@@ -709,7 +715,7 @@ __global__ __launch_bounds__((NL + 5) * 64) void select_rounds_kernel(SelectDesc
                 if (hv[c]) {  // one 0/1 byte per staged row (unselected rows: the dump slot)
                   uint8_t *vb = mystage + vsoff[c];
 #pragma unroll
-                  for (int e = 0; e < 4; e++) vb[idx[e]] = (uint8_t)((vmc[c] >> e) & 1u);
+                  for (int e = 0; e < 4; e++) vb[idx[e]] = (uint8_t)((vmc[h][c] >> e) & 1u);
                 }
               }
             }
@@ -991,7 +997,7 @@ static SelectRoundsPlan PlanSelectRoundsNL(const SelectDesc &d, int64_t nrows, i
   if (force_nl) p.NL = force_nl;
   if (p.NL == 8) want_h = 1, want_depth = 3;
   if (const char *e = Knob("MBX_SR_H")) want_h = atoi(e) == 1 ? 1 : 2;
-  if (p.nv) want_h = 1;
+  if (p.nv && p.NL == 8) want_h = 1;  // the 8-loader NULL-able form is H = 1 only
   if (const char *e = Knob("MBX_SR_S")) want_s = atoi(e) > 0 ? atoi(e) : 0;
   if (const char *e = Knob("MBX_SR_STG")) want_stg = atoi(e) >= 256 ? atoi(e) : 4096;
   if (const char *e = Knob("MBX_SR_DEPTH")) {
@@ -1002,7 +1008,7 @@ static SelectRoundsPlan PlanSelectRoundsNL(const SelectDesc &d, int64_t nrows, i
   for (int h = 2; h >= 1; h--) {
     if (want_h && h != want_h) continue;
     const int depth = want_depth ? want_depth : h == 2 ? 2 : (p.ni <= 2 ? 3 : 2);
-    const size_t ring = (size_t)p.NL * depth * p.ni * 1024 * h + (p.nv ? (size_t)p.NL * depth * p.nc * 32 : 0);
+    const size_t ring = (size_t)p.NL * depth * p.ni * 1024 * h + (p.nv ? (size_t)p.NL * depth * p.nc * 32 * h : 0);
     if (ring + 2048 >= (size_t)160 * 1024) continue;
     const size_t budget = (size_t)160 * 1024 - 2048 - ring;  // static meta (1.5 KB) + margin
     int stg = want_stg;
@@ -1061,10 +1067,11 @@ template <int NC, int WM>
 void SrDepth(const SelectDesc &d, const SelectRoundsPlan &p, int64_t nrows, unsigned long long *ctl, uint32_t epoch,
              hipStream_t s) {
   constexpr int ni = SrCols<NC, WM>::ni();
-  if (p.nv) {  // NULL-able columns: H = 1, 3-deep ring for one- and two-slot sets (8 loaders: one column only)
+  if (p.nv) {  // NULL-able columns: 8 loaders for one column only; H = 2 with a 2-deep ring, or H = 1
     if constexpr (NC == 1) {
       if (p.NL == 8) return SrLaunchNL<NC, WM, 3, 1, 8, true>(d, p, nrows, ctl, epoch, s);
     }
+    if (p.H == 2) return SrLaunchNL<NC, WM, 2, 2, 4, true>(d, p, nrows, ctl, epoch, s);
     if (ni <= 2) return SrLaunchNL<NC, WM, 3, 1, 4, true>(d, p, nrows, ctl, epoch, s);
     return SrLaunchNL<NC, WM, 2, 1, 4, true>(d, p, nrows, ctl, epoch, s);
   }

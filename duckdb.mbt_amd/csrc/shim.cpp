@@ -1688,6 +1688,16 @@ int32_t duckdb_mbx_shard_stats(duckdb_mb_connection *h, int64_t *out6, double *o
   return 6;
 }
 
+// out3 = {select_rounds launches, aborts (a persistent workgroup was never
+// scheduled within 100 ms: the query reran in the two-pass form), launch
+// failures (the two-pass form ran instead)} over the connection and its shards.
+int32_t duckdb_mbx_engine_stats(duckdb_mb_connection *h, int64_t *out3) {
+  if (!h || !out3) return 0;
+  out3[0] = out3[1] = out3[2] = 0;
+  EngineCounters(h->conn, out3);
+  return 3;
+}
+
 int32_t duckdb_mbx_result_raw(duckdb_mb_result *r, int32_t col, int32_t row, void *out, int32_t out_len) {
   if (!r || !InRange(r->r, col, row) || !out) return 0;
   const HostColumn &c = r->r->cols[col];

@@ -285,6 +285,12 @@ char *duckdb_mbx_result_text(duckdb_mb_result *result, int64_t *len);
  * last host merge us}.  Either pointer may be NULL.  Returns 6 (0: no handle). */
 int32_t duckdb_mbx_shard_stats(duckdb_mb_connection *connection, int64_t *out6, double *outd2);
 
+/* One-pass selection (select_rounds) outcomes over the connection and its
+ * shards: out3 = {launches, aborts (a persistent workgroup was never scheduled
+ * within 100 ms, so the query reran in the two-pass form), launch failures (the
+ * two-pass form ran instead)}.  Returns 3 (0: no handle). */
+int32_t duckdb_mbx_engine_stats(duckdb_mb_connection *connection, int64_t *out3);
+
 #ifdef __cplusplus
 }
 #endif

@@ -205,12 +205,16 @@ def test_select_rounds_abort_falls_back(mbx, oracle, monkeypatch):
     c = mbx.connect_with_config(cfg).value
     n = 5_000_011
     x, k, v, s = _table(c, oracle, n)
+    st0 = c.engine_stats()
     for stall in ("0", "17"):
         monkeypatch.setenv("MBX_SR_TEST_STALL", stall)
         got = _col(c, "SELECT x FROM fc WHERE x > 24", "int64")
         names = [kk["name"] for kk in c.last_profile()["kernels"]]
         assert "select_rounds_abort" in names and "filter_count" in names, names
         assert np.array_equal(got, x[x > 24])
+    st1 = c.engine_stats()  # the aborts are counted (duckdb_mbx_engine_stats)
+    assert st1["select_rounds_aborts"] - st0["select_rounds_aborts"] == 2, (st0, st1)
+    assert st1["select_rounds_launches"] - st0["select_rounds_launches"] >= 2
     monkeypatch.delenv("MBX_SR_TEST_STALL")
     got = _col(c, "SELECT x FROM fc WHERE x > 24", "int64")  # the next launch (fresh epoch) is clean
     names = [kk["name"] for kk in c.last_profile()["kernels"]]

@@ -3,6 +3,7 @@
 #   tests     the -m gpu suite (PYTEST_K narrows it)      smoke   __graft_entry__.smoke()
 #   bench     the headline line (C2 + C3/sel extras, CPU baseline)
 #   configs   bench.py --config c3 / c5 / sel / c4        shards  --shards-per-gpu 2 (c2, c5, c3)
+#   c1        bench.py --config c1 (native per-cell and stream loops)
 #   overhead  tools/shard_overhead.py                      shapes  tools/shape_bench.py (SHAPES, NULLABLE)
 #   layout    tools/c3_layout_probe.py                     rehearse  2 gloo ranks on one GPU (--ranks)
 #   prof      rocprofv3 --kernel-trace --stats of bench.py (c2 line with extras)
@@ -22,6 +23,9 @@ if has smoke; then
 fi
 if has bench; then
   timeout -k 10 300 python bench.py > gpurun_out/bench_c2.json 2> gpurun_out/bench_c2.err || exit 13
+fi
+if has c1; then
+  timeout -k 10 200 python bench.py --config c1 > gpurun_out/bench_c1.json 2> gpurun_out/bench_c1.err || exit 24
 fi
 if has configs; then
   for c in c3 c5 sel; do
