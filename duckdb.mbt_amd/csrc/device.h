@@ -352,6 +352,12 @@ struct SelectDesc {
   int32_t out_col[SL_MAX_OUT];  // index into col[]
   void *dst[SL_MAX_OUT];
   uint8_t *vdst[SL_MAX_OUT];  // select_rounds: one validity byte per output row of a NULL-able output, or nullptr
+  // select_rounds: nullptr, or the zone map of the selected rows of every
+  // output column c with bit c of zmask: zstats[3c .. 3c + 2] = {min, max,
+  // non-NULL count (NULL-able columns only)} (values sign-extended), folded in
+  // with atomics - the caller sets them to {INT64_MAX, INT64_MIN, 0} first
+  long long *zstats;
+  int32_t zmask;
   unsigned long long *dbg;     // nullptr, or 9 counters (MBX_SL_DEBUG) / 13 (MBX_SR_DEBUG)
   unsigned long long *dbg_ts;  // MBX_SR_DEBUG=2: s_memrealtime of every (round, workgroup) publish
 };

@@ -29,6 +29,10 @@ struct DevColumn {
   char *chars = nullptr;       // P_STR
   int64_t chars_len = 0, chars_cap = 0;
   int64_t capacity = 0;  // rows
+  // set when data / validity are device-pool blocks taken over from a query
+  // result (CREATE TABLE AS, INSERT ... SELECT into an empty table): they go
+  // back to that pool, not to hipFree
+  std::shared_ptr<void> data_owner, validity_owner;
   // zone-map statistics over all rows (kept by ingest; used by the planner
   // to pick overflow-free accumulators and direct-index group tables)
   bool stats_valid = false;

@@ -121,6 +121,10 @@ struct Engine {
   dev::AggPartial *d_partials = nullptr;  // per-workgroup partials of the fused filter-aggregate
   // pinned host staging for small results: every D2H of a query lands here
   // and the query pays ONE stream synchronisation
+  // set around the query of CREATE TABLE AS / INSERT ... SELECT: select_rounds
+  // then also returns its outputs' zone maps (DCol::zn), so the append needs no
+  // statistics pass
+  bool want_zone_maps = false;
   uint8_t *h_pinned = nullptr;
   size_t h_pinned_bytes = 0;
   // grows the arena (power of two, up to kPinnedMax) so a query result of
@@ -187,7 +191,8 @@ struct Engine {
     if (has_gpu) {
       hipSetDevice(device);
       if (stream) hipStreamSynchronize(stream);
-      pool.reset();  // returns cached buffers before the stream goes away
+      pool->s = nullptr;  // tables may hold pool blocks past this engine (adopted results)
+      pool.reset();       // returns cached buffers before the stream goes away
       for (auto &e : ev_pool) {
         hipEventDestroy(e.first);
         hipEventDestroy(e.second);
@@ -255,6 +260,21 @@ std::shared_ptr<Engine> CreateEngine(int device, bool allow_no_gpu) {
   return e;
 }
 
+// n appended rows, nvalid of them non-NULL with values in [mn, mx], folded
+// into the column's zone map
+static void FoldStats(DevColumn &c, int64_t n, int64_t nvalid, i128 mn, i128 mx, bool first_rows) {
+  c.null_count += n - nvalid;
+  if (nvalid > 0) {
+    if (first_rows || !c.stats_valid) {
+      c.imin = mn;
+      c.imax = mx;
+    } else {
+      c.imin = std::min<i128>(c.imin, mn);
+      c.imax = std::max<i128>(c.imax, mx);
+    }
+  }
+}
+
 // folds the zone-map statistics of in-flight appends into their columns
 // (after the stream has drained: their DMAs and reductions are done)
 static void SettlePending(Engine &e) {
@@ -262,18 +282,8 @@ static void SettlePending(Engine &e) {
   HIPCHK(hipStreamSynchronize(e.stream));
   e.inflight_h2d = false;
   for (auto &ps : e.pending_stats) {
-    DevColumn &c = *ps.col;
     const long long *h = ps.h;
-    c.null_count += ps.n - h[2];
-    if (h[2] > 0) {
-      if (ps.first_rows || !c.stats_valid) {
-        c.imin = h[0];
-        c.imax = h[1];
-      } else {
-        c.imin = std::min<i128>(c.imin, h[0]);
-        c.imax = std::max<i128>(c.imax, h[1]);
-      }
-    }
+    FoldStats(*ps.col, ps.n, h[2], h[0], h[1], ps.first_rows);
     e.stat_slots.push_back(ps.h);
   }
   e.pending_stats.clear();
@@ -348,6 +358,10 @@ struct DCol {
   std::vector<DevBufPtr> owners;
   // statistics when the column is a table column
   const DevColumn *table_col = nullptr;
+  // zone map the producing kernel computed over its zn rows (select_rounds
+  // under Engine::want_zone_maps): min / max of the non-NULL values, their count
+  int64_t zn = -1, zvalid = 0;
+  i128 zmin = 0, zmax = 0;
 };
 
 struct DRel {
@@ -1168,6 +1182,19 @@ static bool TrySelectOnePass(Engine &e, const DRel &rel, const dev::FilterMultiD
         S.dbg_ts = (unsigned long long *)tsbuf->p;
       }
     }
+    const char *zk = Knob("MBX_SR_ZONE");  // 0: the append's own zone-map pass instead (A/B)
+    if (e.want_zone_maps && !(zk && atoi(zk) == 0)) {
+      for (int k = 0; k < S.nout; k++) {
+        const Phys ph = rel.cols[exprs[k]->col].phys;
+        if (ph == P_I32 || ph == P_I64) S.zmask |= 1 << S.out_col[k];
+      }
+      if (S.zmask) {  // {INT64_MAX, INT64_MIN, 0} per column, from the pinned arena (synchronised below)
+        S.zstats = (long long *)((char *)e.d_small + 4096);
+        long long *z0 = (long long *)(e.h_pinned + 256);
+        for (int c = 0; c < SL_MAX_COL; c++) z0[3 * c] = LLONG_MAX, z0[3 * c + 1] = LLONG_MIN, z0[3 * c + 2] = 0;
+        HIPCHK(hipMemcpyAsync(S.zstats, z0, SL_MAX_COL * 3 * sizeof(long long), hipMemcpyHostToDevice, e.stream));
+      }
+    }
     hipError_t launch;
     {
       ProfScope ps(e, "select_rounds", bytes, n);  // algorithmic: inputs once (+ the selected rows' outputs, added below)
@@ -1226,9 +1253,23 @@ static bool TrySelectOnePass(Engine &e, const DRel &rel, const dev::FilterMultiD
     unsigned long long h[2];
     HIPCHK(hipMemcpyAsync(e.h_pinned, e.d_rounds, sizeof(h), hipMemcpyDeviceToHost, e.stream));
     HIPCHK(hipMemcpyAsync(e.h_pinned + 16, e.d_err, sizeof(int32_t), hipMemcpyDeviceToHost, e.stream));
+    if (S.zmask)
+      HIPCHK(hipMemcpyAsync(e.h_pinned + 64, S.zstats, SL_MAX_COL * 3 * sizeof(long long), hipMemcpyDeviceToHost,
+                            e.stream));
     HIPCHK(hipStreamSynchronize(e.stream));
     memcpy(h, e.h_pinned, sizeof(h));
     memcpy(&rounds_err, e.h_pinned + 16, sizeof(rounds_err));
+    if (S.zmask && h[0] != (unsigned long long)epoch) {
+      const long long *z = (const long long *)(e.h_pinned + 64);
+      for (int k = 0; k < S.nout; k++) {
+        const int oc = S.out_col[k];
+        if (!((S.zmask >> oc) & 1)) continue;
+        cols[k].zn = (int64_t)h[1];
+        cols[k].zmin = z[3 * oc];
+        cols[k].zmax = z[3 * oc + 1];
+        cols[k].zvalid = S.col[oc].valid ? z[3 * oc + 2] : (int64_t)h[1];  // (counted for NULL-able columns only)
+      }
+    }
     lk.unlock();
     if (h[0] == (unsigned long long)epoch) {  // a workgroup was never scheduled: two-pass form instead
       e.sr_aborts++;
@@ -3163,8 +3204,8 @@ bool CopyDeviceColumnText(Connection &c, DeviceResult &d, int col, const std::fu
 Table::~Table() {
   hipSetDevice(device);
   for (auto &c : cols) {
-    if (c.data) hipFree(c.data);
-    if (c.validity) hipFree(c.validity);
+    if (c.data && !c.data_owner) hipFree(c.data);
+    if (c.validity && !c.validity_owner) hipFree(c.validity);
     if (c.offsets) hipFree(c.offsets);
     if (c.chars) hipFree(c.chars);
   }
@@ -3227,7 +3268,8 @@ static void Grow(Engine &e, DevColumn &c, int64_t nrows_old, int64_t need) {
     HIPCHK(hipMalloc(&nd, (size_t)cap * sz));
     if (c.data && nrows_old) HIPCHK(hipMemcpyAsync(nd, c.data, (size_t)nrows_old * sz, hipMemcpyDeviceToDevice, e.stream));
     HIPCHK(hipStreamSynchronize(e.stream));
-    if (c.data) HIPCHK(hipFree(c.data));
+    if (c.data_owner) c.data_owner.reset();
+    else if (c.data) HIPCHK(hipFree(c.data));
     c.data = nd;
   }
   if (c.validity) {
@@ -3236,7 +3278,8 @@ static void Grow(Engine &e, DevColumn &c, int64_t nrows_old, int64_t need) {
     HIPCHK(hipMemsetAsync(nv, 0xFF, Words64(cap) * 8, e.stream));
     HIPCHK(hipMemcpyAsync(nv, c.validity, Words64(nrows_old) * 8, hipMemcpyDeviceToDevice, e.stream));
     HIPCHK(hipStreamSynchronize(e.stream));
-    HIPCHK(hipFree(c.validity));
+    if (c.validity_owner) c.validity_owner.reset();
+    else HIPCHK(hipFree(c.validity));
     c.validity = nv;
   }
   c.capacity = cap;
@@ -3248,6 +3291,14 @@ static void EnsureValidity(Engine &e, DevColumn &c, int64_t nrows_old) {
   HIPCHK(hipMalloc(&c.validity, Words64(cap) * 8));
   HIPCHK(hipMemsetAsync(c.validity, 0xFF, Words64(cap) * 8, e.stream));
   (void)nrows_old;
+}
+
+// the zone map the producing kernel left on d (DCol::zn), folded in instead of
+// a statistics pass over the appended rows
+static bool FoldKernelStats(DevColumn &c, const DCol &d, int64_t n, bool first_rows) {
+  if (d.zn != n || d.phys != c.phys || (c.phys != P_I32 && c.phys != P_I64)) return false;
+  FoldStats(c, n, d.zvalid, d.zmin, d.zmax, first_rows);
+  return true;
 }
 
 static void UpdateStats(Engine &e, DevColumn &c, int64_t off, int64_t n, bool first_rows, bool async = false) {
@@ -3267,7 +3318,10 @@ static void UpdateStats(Engine &e, DevColumn &c, int64_t off, int64_t n, bool fi
     c.stats_valid = false;
     return;
   }
-  dev::ColumnStats((const char *)c.data + off * sz, c.phys, v, n, o3, e.stream);
+  {
+    ProfScope ps(e, "zone_map", (double)n * sz + (v ? n / 8.0 : 0), n);
+    dev::ColumnStats((const char *)c.data + off * sz, c.phys, v, n, o3, e.stream);
+  }
   if (async) {
     long long *slot = nullptr;
     if (!e.stat_slots.empty()) {
@@ -3283,25 +3337,56 @@ static void UpdateStats(Engine &e, DevColumn &c, int64_t off, int64_t n, bool fi
   long long h[3];
   HIPCHK(hipMemcpyAsync(h, o3, sizeof(h), hipMemcpyDeviceToHost, e.stream));
   HIPCHK(hipStreamSynchronize(e.stream));
-  c.null_count += n - h[2];
-  if (h[2] > 0) {
-    if (first_rows || !c.stats_valid) {
-      c.imin = h[0];
-      c.imax = h[1];
-    } else {
-      c.imin = std::min<i128>(c.imin, h[0]);
-      c.imax = std::max<i128>(c.imax, h[1]);
-    }
+  FoldStats(c, n, h[2], h[0], h[1], first_rows);
+}
+
+// An empty fixed-width table column takes over the pool blocks of a result
+// column (values, and the bitmap when there is one) instead of allocating and
+// copying: CREATE TABLE AS / INSERT ... SELECT into a new table then costs the
+// query plus the zone-map pass.  A block is adopted at most once per append
+// (SELECT x, x) and only when it starts at the column's pointer; string
+// columns and blocks far larger than the rows still take the copy.
+static bool AdoptResultColumn(DevColumn &c, const DCol &d, int64_t n, std::vector<const void *> &taken) {
+  if (c.phys == P_STR || d.phys != c.phys || c.data || c.validity || c.capacity) return false;
+  auto owner_of = [&](const void *p) -> DevBufPtr {
+    if (!p) return nullptr;
+    for (auto &o : d.owners)
+      if (o && o->p == p && o->pool) return o;
+    return nullptr;
+  };
+  DevBufPtr db = owner_of(d.data), vb = owner_of(d.validity);
+  if (!db || (d.validity && !vb)) return false;
+  for (const void *p : taken)
+    if (p == db->p || (vb && p == vb->p)) return false;
+  int64_t cap = (int64_t)(db->bytes / PhysSize(c.phys));
+  if (vb) cap = std::min<int64_t>(cap, (int64_t)(vb->bytes / 8) * 64);
+  // (a selective filter's output block is sized for every input row: keep at
+  // most twice what the rows need, as Grow's doubling would)
+  if (cap < n || db->bytes > 2 * (size_t)n * PhysSize(c.phys) + ((size_t)2 << 20)) return false;
+  taken.push_back(db->p);
+  c.data = db->p;
+  c.data_owner = db;
+  if (vb) {
+    taken.push_back(vb->p);
+    c.validity = (uint64_t *)vb->p;
+    c.validity_owner = vb;
   }
+  c.capacity = cap;
+  return true;
 }
 
 static void AppendDRel(Engine &e, Table &t, const DRel &r, const std::vector<int> &col_map) {
   int64_t n = r.n, old = t.nrows;
   if (n <= 0) return;
+  std::vector<const void *> taken;
   for (size_t tc = 0; tc < t.cols.size(); tc++) {
     DevColumn &c = t.cols[tc];
-    Grow(e, c, old, old + n);
     int src = col_map[tc];
+    if (old == 0 && src >= 0 && AdoptResultColumn(c, r.cols[src], n, taken)) {
+      if (!FoldKernelStats(c, r.cols[src], n, true)) UpdateStats(e, c, 0, n, true);
+      continue;
+    }
+    Grow(e, c, old, old + n);
     if (src < 0) {
       // column not provided: NULLs
       EnsureValidity(e, c, old);
@@ -3335,6 +3420,7 @@ static void AppendDRel(Engine &e, Table &t, const DRel &r, const std::vector<int
       c.chars_len += d.chars_len;
     } else {
       int sz = PhysSize(c.phys);
+      ProfScope ps(e, "append_copy", 2.0 * n * sz, n);
       HIPCHK(hipMemcpyAsync((char *)c.data + old * sz, d.data, (size_t)n * sz, hipMemcpyDeviceToDevice, e.stream));
     }
     if (d.validity) {
@@ -3343,7 +3429,7 @@ static void AppendDRel(Engine &e, Table &t, const DRel &r, const std::vector<int
     } else if (c.validity) {
       dev::BitmapAppend(c.validity, old, nullptr, n, e.stream);
     }
-    UpdateStats(e, c, old, n, old == 0);
+    if (!FoldKernelStats(c, d, n, old == 0)) UpdateStats(e, c, old, n, old == 0);
   }
   HIPCHK(hipStreamSynchronize(e.stream));
   t.nrows = old + n;
@@ -3354,8 +3440,12 @@ static void ShardedInsertSelect(Connection &c, Table &t, const BoundSelect &s, c
 
 void ExecuteInsertSelect(Connection &c, Table &t, const BoundSelect &s, const std::vector<int> &col_map) {
   if (t.sharded()) return ShardedInsertSelect(c, t, s, col_map);
+  auto t0 = std::chrono::steady_clock::now();
   Engine &e = Eng(c);
-  e.profile = false;
+  e.profile = c.opts.profile;  // the statement's kernels (query, append copy, zone map) become last_profile
+  e.events.clear();
+  e.plan_text = "";
+  e.ev_used = 0;
   DRel r;
   if (IsHostConstantSelect(s)) {
     ResultPtr hr = HostConstantSelect(s);
@@ -3366,9 +3456,15 @@ void ExecuteInsertSelect(Connection &c, Table &t, const BoundSelect &s, const st
       r.cols.push_back(d);
     }
   } else {
+    struct Want {
+      Engine &e;
+      ~Want() { e.want_zone_maps = false; }
+    } want{e};
+    e.want_zone_maps = true;
     r = RunSelectDev(e, c, s);
   }
   AppendCast(e, t, r, col_map);
+  FinishProfile(c, e, std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count());
 }
 
 // r's columns (col_map[table column] = column of r, or -1) cast to the table

@@ -33,7 +33,9 @@
 // that resolved the last tile's inclusive prefix handles it with guarded
 // loads and writes the selected-row total.
 #include <hip/hip_runtime.h>
+
 #include <atomic>
+#include <climits>
 #include <stdexcept>
 #include <stdint.h>
 #include <stdlib.h>
@@ -587,6 +589,17 @@ __global__ __launch_bounds__((NL + 5) * 64) void select_rounds_kernel(SelectDesc
     const bool dbg = D.dbg != nullptr;
     unsigned long long t_all = dbg ? clock64() : 0, d_dma = 0, d_stg = 0, d_meta = 0, t0 = 0;
     int64_t qb = ((int64_t)g * NL + w) * S;  // this round's first step
+    // zone map of the selected rows of the D.zmask output columns (CREATE
+    // TABLE AS keeps it as the new column's statistics), NULL rows skipped:
+    // folded from the values already in registers (4-byte columns in 32-bit
+    // ops); the non-NULL count only for NULL-able columns (otherwise it is the
+    // selected count)
+    const uint32_t zmask = D.zstats ? (uint32_t)D.zmask & smask : 0u;
+    long long zmn[NC], zmx[NC];
+    int zmn4[NC], zmx4[NC];
+    uint32_t zcnt[NC];
+#pragma unroll
+    for (int c = 0; c < NC; c++) zmn[c] = LLONG_MAX, zmx[c] = LLONG_MIN, zmn4[c] = INT_MAX, zmx4[c] = INT_MIN, zcnt[c] = 0;
     for (int64_t r = 0; r < nrounds && !quit; r++, qb += qstride) {
       const int slot = (int)(r % SR_MR);
       if (r >= SR_MR) {  // meta slot reuse: every storer is done with round r - SR_MR
@@ -718,6 +731,22 @@ __global__ __launch_bounds__((NL + 5) * 64) void select_rounds_kernel(SelectDesc
                   for (int e = 0; e < 4; e++) vb[idx[e]] = (uint8_t)((vmc[h][c] >> e) & 1u);
                 }
               }
+              if ((zmask >> c) & 1) {
+#pragma unroll
+                for (int e = 0; e < 4; e++) {
+                  const bool z = ok[h][e] && ((vmc[h][c] >> e) & 1u);
+                  if (L::w(c) == 4) {
+                    const int x = (int)v[h][c][e];
+                    zmn4[c] = min(zmn4[c], z ? x : INT_MAX);
+                    zmx4[c] = max(zmx4[c], z ? x : INT_MIN);
+                  } else {
+                    const long long x = v[h][c][e];
+                    zmn[c] = z && x < zmn[c] ? x : zmn[c];
+                    zmx[c] = z && x > zmx[c] ? x : zmx[c];
+                  }
+                  if (hv[c]) zcnt[c] += z;
+                }
+              }
             }
             hb += hc[h];
           }
@@ -746,6 +775,26 @@ __global__ __launch_bounds__((NL + 5) * 64) void select_rounds_kernel(SelectDesc
       }
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // no LDS-DMA may land after the workgroup ends
+    if (zmask) {
+#pragma unroll
+      for (int c = 0; c < NC; c++) {
+        if (!((zmask >> c) & 1)) continue;
+        long long a = L::w(c) == 4 ? (long long)zmn4[c] : zmn[c], b = L::w(c) == 4 ? (long long)zmx4[c] : zmx[c];
+        uint32_t n = zcnt[c];
+#pragma unroll
+        for (int off = 32; off; off >>= 1) {
+          const long long a2 = __shfl_xor(a, off), b2 = __shfl_xor(b, off);
+          a = a2 < a ? a2 : a;
+          b = b2 > b ? b2 : b;
+          n += __shfl_xor(n, off);
+        }
+        if (lane == 0) {
+          atomicMin(&D.zstats[3 * c], a);
+          atomicMax(&D.zstats[3 * c + 1], b);
+          atomicAdd((unsigned long long *)&D.zstats[3 * c + 2], (unsigned long long)n);
+        }
+      }
+    }
     if (dbg && lane == 0) {
       atomicAdd(&D.dbg[0], clock64() - t_all);
       atomicAdd(&D.dbg[1], d_dma);
