@@ -29,10 +29,12 @@ struct DevColumn {
   char *chars = nullptr;       // P_STR
   int64_t chars_len = 0, chars_cap = 0;
   int64_t capacity = 0;  // rows
-  // set when data / validity are device-pool blocks taken over from a query
-  // result (CREATE TABLE AS, INSERT ... SELECT into an empty table): they go
-  // back to that pool, not to hipFree
-  std::shared_ptr<void> data_owner, validity_owner;
+  // owners of the buffers above (hipFree, or back to the device pool for the
+  // blocks CREATE TABLE AS took over from its query): a result that still
+  // reads the column without a copy (a stream, an Arrow result, a LIMIT
+  // slice) holds them too, so an append that regrows the column, or a DROP,
+  // never frees memory a live result reads
+  std::shared_ptr<void> data_owner, validity_owner, offsets_owner, chars_owner;
   // zone-map statistics over all rows (kept by ingest; used by the planner
   // to pick overflow-free accumulators and direct-index group tables)
   bool stats_valid = false;

@@ -358,6 +358,8 @@ struct DCol {
   std::vector<DevBufPtr> owners;
   // statistics when the column is a table column
   const DevColumn *table_col = nullptr;
+  // the table column's buffer owners, when the data is read in place
+  std::vector<std::shared_ptr<void>> pins;
   // zone map the producing kernel computed over its zn rows (select_rounds
   // under Engine::want_zone_maps): min / max of the non-NULL values, their count
   int64_t zn = -1, zvalid = 0;
@@ -373,6 +375,8 @@ struct DRel {
 
 static DCol ColFromTable(const DevColumn &c) {
   DCol d;
+  for (const auto *o : {&c.data_owner, &c.validity_owner, &c.offsets_owner, &c.chars_owner})
+    if (*o) d.pins.push_back(*o);
   d.type = c.type;
   d.phys = c.phys;
   d.data = c.data;
@@ -2822,7 +2826,7 @@ static ResultPtr ToHost(Engine &e, const DRel &r, const std::vector<std::string>
 // ---------------------------------------------------------------------------
 static ResultPtr HostConstantSelect(const BoundSelect &s);
 
-static DRel RunSelectDev(Engine &e, Connection &c, const BoundSelect &s);
+static DRel RunSelectDev(Engine &e, Connection &c, const BoundSelect &s, bool top = false);
 
 static DRel SourceRel(Engine &e, Connection &c, const BoundSource &src) {
   DRel r;
@@ -2887,7 +2891,9 @@ static size_t VisibleCols(const BoundSelect &s) {
   return n;
 }
 
-static DRel RunSelectDev(Engine &e, Connection &c, const BoundSelect &s) {
+// top: the statement's own result (handed to the host or kept as a device
+// result), not a subquery's or an INSERT's input
+static DRel RunSelectDev(Engine &e, Connection &c, const BoundSelect &s, bool top) {
   DRel r = RunBranch(e, c, s);
   if (!s.union_all.empty()) {
     std::vector<DRel> parts;
@@ -2900,6 +2906,22 @@ static DRel RunSelectDev(Engine &e, Connection &c, const BoundSelect &s) {
     int64_t start = std::min(s.offset, r.n);
     int64_t n = r.n - start;
     if (s.limit >= 0) n = std::min(n, s.limit);
+    // a top-level result's fixed-width columns are sliced in place (their
+    // owners / pins keep the buffers alive; only element-wise kernels and
+    // copies read a result, so the slice's 4/8-B alignment is enough); strings,
+    // the virtual range column and a bitmap that would start mid-word take the
+    // gather
+    bool slice = top && !r.range;
+    for (auto &d : r.cols) slice &= d.phys != P_STR && d.data && (!d.validity || start % 64 == 0);
+    if (slice) {
+      for (auto &d : r.cols) {
+        d.data = (char *)d.data + (size_t)start * PhysSize(d.phys);
+        if (d.validity) d.validity += start / 64;
+      }
+      r.n = n;
+      r.cols.resize(VisibleCols(s));
+      return r;
+    }
     auto perm = Alloc(e, std::max<int64_t>(n, 1) * 8);
     dev::Iota((int64_t *)perm->p, n, start, e.stream);
     r = GatherRel(e, r, (const int64_t *)perm->p, n);
@@ -3054,7 +3076,7 @@ ResultPtr ExecuteSelect(Connection &c, const BoundSelect &s) {
       return hr;
     }
   }
-  DRel r = RunSelectDev(e, c, s);
+  DRel r = RunSelectDev(e, c, s, true);
   std::vector<std::string> names(s.names.begin(), s.names.begin() + VisibleCols(s));
   ResultPtr res = ToHost(e, r, names, 0, -1, names.size(), true);  // raises pending device errors
   double ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
@@ -3078,7 +3100,7 @@ DeviceResultPtr ExecuteSelectDevice(Connection &c, const BoundSelect &s, StreamS
   e.plan_text = c.opts.profile ? ExplainSelect(s) : "";
   e.ev_used = 0;
   auto d = std::make_shared<DeviceResult>();
-  d->r = RunSelectDev(e, c, s);
+  d->r = RunSelectDev(e, c, s, true);
   d->names.assign(s.names.begin(), s.names.begin() + VisibleCols(s));
   HIPCHK(hipStreamSynchronize(e.stream));
   CheckError(e);
@@ -3201,15 +3223,7 @@ bool CopyDeviceColumnText(Connection &c, DeviceResult &d, int col, const std::fu
 // ---------------------------------------------------------------------------
 // tables: creation, append, stats
 // ---------------------------------------------------------------------------
-Table::~Table() {
-  hipSetDevice(device);
-  for (auto &c : cols) {
-    if (c.data && !c.data_owner) hipFree(c.data);
-    if (c.validity && !c.validity_owner) hipFree(c.validity);
-    if (c.offsets) hipFree(c.offsets);
-    if (c.chars) hipFree(c.chars);
-  }
-}
+Table::~Table() {}  // column buffers go with their owners (a live result may still hold them)
 
 TablePtr CreateDeviceTable(Connection &c, const std::string &name, const std::vector<std::string> &names,
                            const std::vector<LogicalType> &types) {
@@ -3251,6 +3265,19 @@ TablePtr CreateDeviceTable(Connection &c, const std::string &name, const std::ve
 
 void DropDeviceTable(Table &t) { (void)t; }
 
+// a table buffer from hipMalloc, freed when its last holder lets go (the
+// column, or a result reading it in place; possibly on another thread)
+static std::shared_ptr<void> DevOwned(Engine &e, void *p) {
+  const int dev = e.device;
+  return std::shared_ptr<void>(p, [dev](void *q) {
+    int prev = -1;
+    (void)hipGetDevice(&prev);
+    if (prev != dev) (void)hipSetDevice(dev);
+    (void)hipFree(q);
+    if (prev != dev && prev >= 0) (void)hipSetDevice(prev);
+  });
+}
+
 static void Grow(Engine &e, DevColumn &c, int64_t nrows_old, int64_t need) {
   if (need <= c.capacity && (c.phys != P_STR || c.offsets)) return;
   int64_t cap = std::max<int64_t>(need, std::max<int64_t>(1024, c.capacity * 2));
@@ -3260,7 +3287,7 @@ static void Grow(Engine &e, DevColumn &c, int64_t nrows_old, int64_t need) {
     if (c.offsets) HIPCHK(hipMemcpyAsync(no, c.offsets, (nrows_old + 1) * 8, hipMemcpyDeviceToDevice, e.stream));
     else HIPCHK(hipMemsetAsync(no, 0, 8, e.stream));
     HIPCHK(hipStreamSynchronize(e.stream));
-    if (c.offsets) HIPCHK(hipFree(c.offsets));
+    c.offsets_owner = DevOwned(e, no);
     c.offsets = no;
   } else {
     void *nd = nullptr;
@@ -3268,8 +3295,7 @@ static void Grow(Engine &e, DevColumn &c, int64_t nrows_old, int64_t need) {
     HIPCHK(hipMalloc(&nd, (size_t)cap * sz));
     if (c.data && nrows_old) HIPCHK(hipMemcpyAsync(nd, c.data, (size_t)nrows_old * sz, hipMemcpyDeviceToDevice, e.stream));
     HIPCHK(hipStreamSynchronize(e.stream));
-    if (c.data_owner) c.data_owner.reset();
-    else if (c.data) HIPCHK(hipFree(c.data));
+    c.data_owner = DevOwned(e, nd);
     c.data = nd;
   }
   if (c.validity) {
@@ -3278,8 +3304,7 @@ static void Grow(Engine &e, DevColumn &c, int64_t nrows_old, int64_t need) {
     HIPCHK(hipMemsetAsync(nv, 0xFF, Words64(cap) * 8, e.stream));
     HIPCHK(hipMemcpyAsync(nv, c.validity, Words64(nrows_old) * 8, hipMemcpyDeviceToDevice, e.stream));
     HIPCHK(hipStreamSynchronize(e.stream));
-    if (c.validity_owner) c.validity_owner.reset();
-    else HIPCHK(hipFree(c.validity));
+    c.validity_owner = DevOwned(e, nv);
     c.validity = nv;
   }
   c.capacity = cap;
@@ -3289,6 +3314,7 @@ static void EnsureValidity(Engine &e, DevColumn &c, int64_t nrows_old) {
   if (c.validity) return;
   int64_t cap = std::max<int64_t>(c.capacity, 1);
   HIPCHK(hipMalloc(&c.validity, Words64(cap) * 8));
+  c.validity_owner = DevOwned(e, c.validity);
   HIPCHK(hipMemsetAsync(c.validity, 0xFF, Words64(cap) * 8, e.stream));
   (void)nrows_old;
 }
@@ -3411,7 +3437,7 @@ static void AppendDRel(Engine &e, Table &t, const DRel &r, const std::vector<int
         HIPCHK(hipMalloc(&nc, cap));
         if (c.chars_len) HIPCHK(hipMemcpyAsync(nc, c.chars, c.chars_len, hipMemcpyDeviceToDevice, e.stream));
         HIPCHK(hipStreamSynchronize(e.stream));
-        if (c.chars) HIPCHK(hipFree(c.chars));
+        c.chars_owner = DevOwned(e, nc);
         c.chars = nc;
         c.chars_cap = cap;
       }

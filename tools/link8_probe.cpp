@@ -91,6 +91,32 @@ int main(int argc, char **argv) {
       if (b < len) memcpy(dst + b, src + b, std::min(part, len - b));
     });
   };
+  // all threads copy each chunk as soon as its DMA lands (one stream, an
+  // event per chunk): the copy-out of chunk c overlaps the DMA of c + 1..
+  std::vector<hipEvent_t> cev(64);
+  for (auto &e : cev) CK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+  auto fine = [&](Team &t, unsigned char *dst, size_t CHK) {
+    const size_t nch = (n + CHK - 1) / CHK;
+    for (size_t c = 0; c < nch; c++) {
+      CK(hipMemcpyAsync(pin + c * CHK, (char *)d + c * CHK, std::min(CHK, n - c * CHK), hipMemcpyDeviceToHost, s));
+      CK(hipEventRecord(cev[c], s));
+    }
+    std::atomic<size_t> landed{0};
+    t.Run([&](int i) {
+      for (size_t c = 0; c < nch; c++) {
+        if (i == 0) {
+          while (hipEventQuery(cev[c]) == hipErrorNotReady) __builtin_ia32_pause();
+          landed.store(c + 1, std::memory_order_release);
+        } else {
+          while (landed.load(std::memory_order_acquire) <= c) __builtin_ia32_pause();
+        }
+        const size_t len = std::min(CHK, n - c * CHK);
+        size_t part = (len / t.n + 4095) & ~(size_t)4095;
+        size_t b = (size_t)i * part;
+        if (b < len) memcpy(dst + c * CHK + b, pin + c * CHK + b, std::min(part, len - b));
+      }
+    });
+  };
   struct V {
     const char *name;
     std::function<void(unsigned char *)> f;
@@ -137,6 +163,10 @@ int main(int argc, char **argv) {
          CK(hipStreamSynchronize(s));
          par_copy(team4, dst + h, pin + h, n - h);
        }},
+      {"fine 8 chunks, 8 thr", [&](unsigned char *dst) { fine(team8, dst, n / 8); }},
+      {"fine 16 chunks, 8 thr", [&](unsigned char *dst) { fine(team8, dst, n / 16); }},
+      {"fine 32 chunks, 8 thr", [&](unsigned char *dst) { fine(team8, dst, n / 32); }},
+      {"fine 16 chunks, 4 thr", [&](unsigned char *dst) { fine(team4, dst, n / 16); }},
   };
   for (int alloc = 0; alloc < 2; alloc++) {
     for (auto &v : vs) {

@@ -39,6 +39,7 @@ shapes = {
     # selection compaction kept on the device (STREAM: the result stays in HBM; no batch is fetched)
     "sel": "STREAM SELECT x FROM t WHERE x > 24",
     "sel2": "STREAM SELECT k, v FROM t WHERE x > 24",
+    "selv": "STREAM SELECT v FROM t WHERE x > 24",
     "sel3": "STREAM SELECT v FROM t WHERE x > 24 AND k < 16",
     "compact": "CREATE OR REPLACE TABLE tc AS SELECT x FROM t WHERE x > 24",
     "compact2": "CREATE OR REPLACE TABLE tc AS SELECT k, v FROM t WHERE x > 24",
