@@ -403,6 +403,12 @@ void SelectCompact(const SelectDesc &d, int64_t nrows, void *status_buf, int64_t
 // ---------------------------------------------------------------------------
 namespace {
 constexpr int SR_MR = 32;                    // rounds in flight inside a workgroup (meta slots)
+// staged validity of a NULL-able output: one 0/1 byte per staged row (16-bit
+// entries measured no faster for SELECT vn ... WHERE x > 24, 4.06 ms either
+// way, and their larger rows halved the staging ring of three-column shapes:
+// SELECT vn ... WHERE xn > 24 AND k < 16 4.83 -> 5.45 ms)
+typedef uint8_t sr_vb_t;
+constexpr int SR_VB = sizeof(sr_vb_t);
 constexpr int SR_PW = 4;                     // most rounds polled per coordinator poll (runtime: pwmax)
 constexpr long long SR_TIMEOUT = 10000000;   // s_memrealtime ticks (100 MHz): 100 ms without progress
 struct SrShared {
@@ -524,7 +530,7 @@ __global__ __launch_bounds__((NL + 5) * 64) void select_rounds_kernel(SelectDesc
     voff[c] = 32 * nv;
     nv += hv[c];
     vsoff[c] = rowb * (stg + 64);
-    if (hv[c] && ((smask >> c) & 1)) rowb += 1;
+    if (hv[c] && ((smask >> c) & 1)) rowb += SR_VB;
   }
   constexpr int VSB = VAL ? H * NC * 32 : 0;  // validity ring slot: 4 words per sub-step and NULL-able column
   unsigned char *stage0 = sr_lds + (size_t)NL * DEPTH * SB + (size_t)NL * DEPTH * VSB;
@@ -726,9 +732,9 @@ __global__ __launch_bounds__((NL + 5) * 64) void select_rounds_kernel(SelectDesc
               }
               if constexpr (VAL) {
                 if (hv[c]) {  // one 0/1 byte per staged row (unselected rows: the dump slot)
-                  uint8_t *vb = mystage + vsoff[c];
+                  sr_vb_t *vb = (sr_vb_t *)(mystage + vsoff[c]);
 #pragma unroll
-                  for (int e = 0; e < 4; e++) vb[idx[e]] = (uint8_t)((vmc[h][c] >> e) & 1u);
+                  for (int e = 0; e < 4; e++) vb[idx[e]] = (sr_vb_t)((vmc[h][c] >> e) & 1u);
                 }
               }
               if ((zmask >> c) & 1) {
@@ -856,7 +862,7 @@ __global__ __launch_bounds__((NL + 5) * 64) void select_rounds_kernel(SelectDesc
 #pragma unroll
               for (int cc = 0; cc < NC; cc++)
                 if (cc == oc) vo = vsoff[cc];
-              const uint8_t *vb = mystage + vo;
+              const sr_vb_t *vb = (const sr_vb_t *)(mystage + vo);
               uint8_t *vd = D.vdst[o] + pos;
               for (uint32_t i = lane; i < c; i += 64) vd[i] = vb[(tail[j] + i) & mask];
             }
@@ -1018,7 +1024,8 @@ static SelectRoundsPlan PlanSelectRoundsNL(const SelectDesc &d, int64_t nrows, i
   if (d.ncol < 1 || d.ncol > SL_MAX_COL || d.nout < 1 || d.nout > SL_MAX_OUT) return p;
   uint32_t smask = 0;
   for (int k = 0; k < d.nout; k++) smask |= 1u << d.out_col[k];
-  int rowb = 0;  // staged bytes per row: every distinct loaded column an output reads (+1 if NULL-able)
+  int rowb = 0;  // staged bytes per row: every distinct loaded column an output reads (+SR_VB if NULL-able)
+  bool vout = false;
   for (int c = 0; c < d.ncol; c++) {
     if (d.col[c].w != 4 && d.col[c].w != 8) return p;
     p.ni += d.col[c].w / 4;
@@ -1026,7 +1033,7 @@ static SelectRoundsPlan PlanSelectRoundsNL(const SelectDesc &d, int64_t nrows, i
     if ((smask >> c) & 1) rowb += d.col[c].w == 8 && !d.col[c].narrow ? 8 : 4;
     if (d.col[c].valid) {
       p.nv++;
-      if ((smask >> c) & 1) rowb += 1;
+      if ((smask >> c) & 1) rowb += SR_VB, vout = true;
     }
   }
   p.nc = d.ncol;
@@ -1040,13 +1047,18 @@ static SelectRoundsPlan PlanSelectRoundsNL(const SelectDesc &d, int64_t nrows, i
   // fits int32) leave LDS for 8 loader waves (two per SIMD: each hides the
   // other's latencies) with a 3-deep ring and 2048 staged rows each
   // (profiles/r02_select_rounds_sweep.log).  MBX_SR_NL=4|8 overrides.
-  // (+1 staged byte per row for a NULL-able output's validity)
-  p.NL = p.nc == 1 && rowb <= 4 + p.nv ? 8 : 4;
-  if (const char *e = Knob("MBX_SR_NL")) p.NL = atoi(e) == 8 && p.nc == 1 ? 8 : 4;
+  // (+SR_VB staged bytes per row for a NULL-able output's validity).  Two
+  // columns without a NULL-able output take 8 loaders too, at H = 1 with a
+  // 1024-row staging ring each (SELECT v ... WHERE xn > 24: 3.83 -> 3.59 ms;
+  // SELECT v ... WHERE x > 24: 3.45 -> 3.39); with one (SELECT vn ... WHERE
+  // x > 24) the validity staging leaves too little LDS (4.07 -> 4.34 ms).
+  p.NL = (p.nc == 1 && rowb <= 4 + p.nv * SR_VB) || (p.nc == 2 && !vout) ? 8 : 4;
+  if (const char *e = Knob("MBX_SR_NL")) p.NL = atoi(e) == 8 && p.nc <= 2 ? 8 : 4;
   if (force_nl) p.NL = force_nl;
-  if (p.NL == 8) want_h = 1, want_depth = 3;
+  if (p.NL == 8) want_h = 1, want_depth = p.nc == 1 || p.ni <= 2 ? 3 : 2;  // (the depths SrDepth instantiates)
   if (const char *e = Knob("MBX_SR_H")) want_h = atoi(e) == 1 ? 1 : 2;
   if (p.nv && p.NL == 8) want_h = 1;  // the 8-loader NULL-able form is H = 1 only
+  if (p.nc == 2 && p.NL == 8 && want_h == 2) p.NL = 4, want_depth = 0;  // (two columns: 8 loaders at H = 1 only)
   if (const char *e = Knob("MBX_SR_S")) want_s = atoi(e) > 0 ? atoi(e) : 0;
   if (const char *e = Knob("MBX_SR_STG")) want_stg = atoi(e) >= 256 ? atoi(e) : 4096;
   if (const char *e = Knob("MBX_SR_DEPTH")) {
@@ -1099,6 +1111,9 @@ namespace {
 template <int NC, int WM, int DP, int H, int NL, bool VAL = false>
 void SrLaunchNL(const SelectDesc &d, const SelectRoundsPlan &p, int64_t nrows, unsigned long long *ctl, uint32_t epoch,
                 hipStream_t s) {
+  // the plan's layout must be this instance's: a mismatch (a planner rule
+  // without a matching instance) would place rows wrongly, so it never launches
+  if (p.NL != NL || p.H != H || p.depth != DP) throw std::logic_error("select_rounds: plan has no matching kernel");
   static std::atomic<uint64_t> attr{0};
   EnsureMaxLds((const void *)select_rounds_kernel<NC, WM, DP, H, NL, VAL>, attr, 160 * 1024 - 2048);
   hipLaunchKernelGGL((select_rounds_kernel<NC, WM, DP, H, NL, VAL>), dim3((unsigned)p.G), dim3((NL + 5) * 64), p.lds, s,
@@ -1107,7 +1122,7 @@ void SrLaunchNL(const SelectDesc &d, const SelectRoundsPlan &p, int64_t nrows, u
 template <int NC, int WM, int DP, int H>
 void SrLaunchH(const SelectDesc &d, const SelectRoundsPlan &p, int64_t nrows, unsigned long long *ctl, uint32_t epoch,
                hipStream_t s) {
-  if constexpr (NC == 1) {
+  if constexpr (NC == 1 || (NC == 2 && H == 1)) {
     if (p.NL == 8) return SrLaunchNL<NC, WM, DP, H, 8>(d, p, nrows, ctl, epoch, s);
   }
   SrLaunchNL<NC, WM, DP, H, 4>(d, p, nrows, ctl, epoch, s);
@@ -1119,6 +1134,9 @@ void SrDepth(const SelectDesc &d, const SelectRoundsPlan &p, int64_t nrows, unsi
   if (p.nv) {  // NULL-able columns: 8 loaders for one column only; H = 2 with a 2-deep ring, or H = 1
     if constexpr (NC == 1) {
       if (p.NL == 8) return SrLaunchNL<NC, WM, 3, 1, 8, true>(d, p, nrows, ctl, epoch, s);
+    }
+    if constexpr (NC == 2) {  // two columns: 8 loaders with H = 1 (the planner's ring depth for ni)
+      if (p.NL == 8) return SrLaunchNL<NC, WM, (ni <= 2 ? 3 : 2), 1, 8, true>(d, p, nrows, ctl, epoch, s);
     }
     if (p.H == 2) return SrLaunchNL<NC, WM, 2, 2, 4, true>(d, p, nrows, ctl, epoch, s);
     if (ni <= 2) return SrLaunchNL<NC, WM, 3, 1, 4, true>(d, p, nrows, ctl, epoch, s);
@@ -1178,11 +1196,15 @@ hipError_t SelectRounds(const SelectDesc &d, const SelectRoundsPlan &p, int64_t 
                         uint32_t epoch, hipStream_t s) {
   if (!p.ok) throw std::runtime_error("SelectRounds: unsupported shape");
   (void)hipGetLastError();  // an earlier, unrelated sticky error must not be taken for this launch's
-  switch (p.nc) {
-    case 1: SrDispatch<1>(d, p, nrows, ctl, epoch, s); break;
-    case 2: SrDispatch<2>(d, p, nrows, ctl, epoch, s); break;
-    case 3: SrDispatch<3>(d, p, nrows, ctl, epoch, s); break;
-    default: SrDispatch<4>(d, p, nrows, ctl, epoch, s); break;
+  try {
+    switch (p.nc) {
+      case 1: SrDispatch<1>(d, p, nrows, ctl, epoch, s); break;
+      case 2: SrDispatch<2>(d, p, nrows, ctl, epoch, s); break;
+      case 3: SrDispatch<3>(d, p, nrows, ctl, epoch, s); break;
+      default: SrDispatch<4>(d, p, nrows, ctl, epoch, s); break;
+    }
+  } catch (const std::logic_error &) {
+    return hipErrorInvalidConfiguration;  // nothing launched: the caller takes the two-pass form
   }
   return hipGetLastError();  // the launch's own error (LDS / resource limits): the caller falls back
 }

@@ -9,6 +9,7 @@
 #   prof      rocprofv3 --kernel-trace --stats of bench.py (c2 line with extras)
 #   pmc       rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes of bench.py (one counter set per run)
 #   link      tools/link8_probe (8 MB D2H variants; build it first: see its header)
+#   pmcshape  rocprofv3 kernel trace + FETCH_SIZE / WRITE_SIZE of tools/shape_bench.py (PMC_SHAPES)
 # Results go to gpurun_out/ (merged back by gpurun); copy what is judged into profiles/.
 set -o pipefail
 mkdir -p gpurun_out
@@ -60,6 +61,14 @@ if has pmc; then
   mkdir -p gpurun_out/pmc
   for ctr in FETCH_SIZE WRITE_SIZE; do
     ( cd /tmp && export TMPDIR=/tmp && timeout -s KILL 300 rocprofv3 --pmc $ctr --output-format csv -d $R/gpurun_out/pmc/$ctr -o $ctr -- python3 $R/bench.py --steps 5 --warmup 1 --no-cpu > $R/gpurun_out/pmc_$ctr.log 2>&1 ) || exit 22
+  done
+fi
+if has pmcshape; then  # kernel trace + FETCH_SIZE / WRITE_SIZE passes of tools/shape_bench.py (PMC_SHAPES, 1e9 rows)
+  mkdir -p gpurun_out/pmcshape
+  export SHAPES=${PMC_SHAPES:-seln_out} NULLABLE=1
+  ( cd /tmp && export TMPDIR=/tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $R/gpurun_out/pmcshape/trace -o trace -- python3 $R/tools/shape_bench.py 1000000000 > $R/gpurun_out/pmcshape_trace.log 2>&1 ) || exit 25
+  for ctr in FETCH_SIZE WRITE_SIZE; do
+    ( cd /tmp && export TMPDIR=/tmp && timeout -s KILL 300 rocprofv3 --pmc $ctr --output-format csv -d $R/gpurun_out/pmcshape/$ctr -o $ctr -- python3 $R/tools/shape_bench.py 1000000000 > $R/gpurun_out/pmcshape_$ctr.log 2>&1 ) || exit 26
   done
 fi
 if has link; then
