@@ -358,6 +358,7 @@ struct SelectDesc {
   // with atomics - the caller sets them to {INT64_MAX, INT64_MIN, 0} first
   long long *zstats;
   int32_t zmask;
+  int32_t zstore;  // 1: the storers fold the zone maps while copying, 0: the loaders
   unsigned long long *dbg;     // nullptr, or 9 counters (MBX_SL_DEBUG) / 13 (MBX_SR_DEBUG)
   unsigned long long *dbg_ts;  // MBX_SR_DEBUG=2: s_memrealtime of every (round, workgroup) publish
 };

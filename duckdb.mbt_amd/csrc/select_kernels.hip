@@ -600,7 +600,7 @@ __global__ __launch_bounds__((NL + 5) * 64) void select_rounds_kernel(SelectDesc
     // folded from the values already in registers (4-byte columns in 32-bit
     // ops); the non-NULL count only for NULL-able columns (otherwise it is the
     // selected count)
-    const uint32_t zmask = D.zstats ? (uint32_t)D.zmask & smask : 0u;
+    const uint32_t zmask = D.zstats && !D.zstore ? (uint32_t)D.zmask & smask : 0u;
     long long zmn[NC], zmx[NC];
     int zmn4[NC], zmx4[NC];
     uint32_t zcnt[NC];
@@ -818,6 +818,13 @@ __global__ __launch_bounds__((NL + 5) * 64) void select_rounds_kernel(SelectDesc
     for (int j = 0; j < PER; j++) tail[j] = 0;
     const bool dbg = D.dbg != nullptr;
     unsigned long long t_all = dbg ? clock64() : 0, d_wait = 0, t0 = 0;
+    // D.zstore: the zone map of the D.zmask columns is folded here, per
+    // output, from the values the copy loads anyway (else by the loaders)
+    const uint32_t zsmask = D.zstats && D.zstore ? (uint32_t)D.zmask & smask : 0u;
+    long long zmn[SL_MAX_OUT], zmx[SL_MAX_OUT];
+    uint32_t zcnt[SL_MAX_OUT];
+#pragma unroll
+    for (int o = 0; o < SL_MAX_OUT; o++) zmn[o] = LLONG_MAX, zmx[o] = LLONG_MIN, zcnt[o] = 0;
     for (int64_t r = 0; r < nrounds; r++) {
       const int slot = (int)(r % SR_MR);
       bool quit = false;
@@ -836,35 +843,67 @@ __global__ __launch_bounds__((NL + 5) * 64) void select_rounds_kernel(SelectDesc
         for (; q < l; q++) pos += lds_ld(&sm.cnt[slot][q]);
         const uint32_t c = lds_ld(&sm.cnt[slot][l]);
         const unsigned char *mystage = stage0 + (size_t)l * (stg + 64) * rowb;
-        for (int o = 0; o < D.nout; o++) {
+#pragma unroll
+        for (int o = 0; o < SL_MAX_OUT; o++) {
+          if (o >= D.nout) break;
           const int oc = D.out_col[o];
-          int so = 0;
+          int so = 0, vo = 0;
           bool s8 = false;
 #pragma unroll
           for (int cc = 0; cc < NC; cc++)
-            if (cc == oc) so = soff[cc], s8 = st8[cc];
-          if (s8) {
+            if (cc == oc) so = soff[cc], s8 = st8[cc], vo = vsoff[cc];
+          const sr_vb_t *vb = nullptr;
+          if constexpr (VAL) {
+            if (D.vdst[o]) vb = (const sr_vb_t *)(mystage + vo);
+          }
+          const uint32_t t0w = tail[j];
+          if ((zsmask >> oc) & 1) {  // the copy also folds the output's zone map (NULL rows skipped)
+            long long mn = zmn[o], mx = zmx[o];
+            uint32_t nv = 0;
+            if (s8) {
+              const int64_t *st = (const int64_t *)(mystage + so);
+              int64_t *dst = (int64_t *)D.dst[o] + pos;
+              for (uint32_t i = lane; i < c; i += 64) {
+                const uint32_t k = (t0w + i) & mask;
+                const long long x = st[k];
+                dst[i] = x;
+                const bool ok = VAL ? (!vb || vb[k] != 0) : true;
+                mn = ok && x < mn ? x : mn;
+                mx = ok && x > mx ? x : mx;
+                nv += ok;
+              }
+            } else {  // 4 bytes staged: an int32 column, or a narrow-staged int64 one
+              const int32_t *st = (const int32_t *)(mystage + so);
+              const bool w8 = D.col[oc].w == 8;
+              for (uint32_t i = lane; i < c; i += 64) {
+                const uint32_t k = (t0w + i) & mask;
+                const int32_t x = st[k];
+                if (w8) ((int64_t *)D.dst[o] + pos)[i] = (int64_t)x;
+                else ((int32_t *)D.dst[o] + pos)[i] = x;
+                const bool ok = VAL ? (!vb || vb[k] != 0) : true;
+                mn = ok && x < mn ? x : mn;
+                mx = ok && x > mx ? x : mx;
+                nv += ok;
+              }
+            }
+            zmn[o] = mn, zmx[o] = mx, zcnt[o] += nv;
+          } else if (s8) {
             const int64_t *st = (const int64_t *)(mystage + so);
             int64_t *dst = (int64_t *)D.dst[o] + pos;
-            for (uint32_t i = lane; i < c; i += 64) dst[i] = st[(tail[j] + i) & mask];
+            for (uint32_t i = lane; i < c; i += 64) dst[i] = st[(t0w + i) & mask];
           } else if (D.col[oc].w == 8) {  // staged narrow: sign-extend back to int64
             const int32_t *st = (const int32_t *)(mystage + so);
             int64_t *dst = (int64_t *)D.dst[o] + pos;
-            for (uint32_t i = lane; i < c; i += 64) dst[i] = (int64_t)st[(tail[j] + i) & mask];
+            for (uint32_t i = lane; i < c; i += 64) dst[i] = (int64_t)st[(t0w + i) & mask];
           } else {
             const int32_t *st = (const int32_t *)(mystage + so);
             int32_t *dst = (int32_t *)D.dst[o] + pos;
-            for (uint32_t i = lane; i < c; i += 64) dst[i] = st[(tail[j] + i) & mask];
+            for (uint32_t i = lane; i < c; i += 64) dst[i] = st[(t0w + i) & mask];
           }
           if constexpr (VAL) {
-            if (D.vdst[o]) {
-              int vo = 0;
-#pragma unroll
-              for (int cc = 0; cc < NC; cc++)
-                if (cc == oc) vo = vsoff[cc];
-              const sr_vb_t *vb = (const sr_vb_t *)(mystage + vo);
+            if (vb) {
               uint8_t *vd = D.vdst[o] + pos;
-              for (uint32_t i = lane; i < c; i += 64) vd[i] = vb[(tail[j] + i) & mask];
+              for (uint32_t i = lane; i < c; i += 64) vd[i] = vb[(t0w + i) & mask];
             }
           }
         }
@@ -873,6 +912,28 @@ __global__ __launch_bounds__((NL + 5) * 64) void select_rounds_kernel(SelectDesc
         if (lane == 0) lds_st(&sm.tail[l], tail[j]);
       }
       if (lane == 0) lds_st(&sm.sdone[sw], (uint32_t)(r + 1));
+    }
+    if (zsmask) {
+#pragma unroll
+      for (int o = 0; o < SL_MAX_OUT; o++) {
+        if (o >= D.nout) break;
+        const int oc = D.out_col[o];
+        if (!((zsmask >> oc) & 1)) continue;
+        long long a = zmn[o], b = zmx[o];
+        uint32_t n = zcnt[o];
+#pragma unroll
+        for (int off = 32; off; off >>= 1) {
+          const long long a2 = __shfl_xor(a, off), b2 = __shfl_xor(b, off);
+          a = a2 < a ? a2 : a;
+          b = b2 > b ? b2 : b;
+          n += __shfl_xor(n, off);
+        }
+        if (lane == 0) {
+          atomicMin(&D.zstats[3 * oc], a);
+          atomicMax(&D.zstats[3 * oc + 1], b);
+          atomicAdd((unsigned long long *)&D.zstats[3 * oc + 2], (unsigned long long)n);
+        }
+      }
     }
     if (dbg && lane == 0) {
       atomicAdd(&D.dbg[4], clock64() - t_all);
