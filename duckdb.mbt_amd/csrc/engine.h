@@ -102,7 +102,6 @@ struct QueryProfile {
   };
   std::vector<Kernel> kernels;
   double total_ms = 0;
-  std::string plan;
 };
 
 struct Database;

@@ -177,7 +177,6 @@ struct Engine {
   std::vector<QueryProfile::Kernel> shard_kernels;
   std::vector<std::pair<hipEvent_t, hipEvent_t>> ev_pool;  // reused across queries
   size_t ev_used = 0;
-  std::string plan_text;
   std::pair<hipEvent_t, hipEvent_t> NextEvents() {
     if (ev_used == ev_pool.size()) {
       hipEvent_t a, b;
@@ -3038,7 +3037,6 @@ static void FinishProfile(Connection &c, Engine &e, double total_ms) {
   QueryProfile &p = c.last_profile;
   p.kernels.clear();
   p.total_ms = total_ms;
-  p.plan = e.plan_text;
   if (!e.profile) {
     e.shard_kernels.clear();
     return;
@@ -3074,7 +3072,6 @@ ResultPtr ExecuteSelect(Connection &c, const BoundSelect &s) {
   Engine &e = Eng(c);
   e.profile = c.opts.profile;
   e.events.clear();
-  e.plan_text = c.opts.profile ? ExplainSelect(s) : "";
   e.ev_used = 0;
   if (c.sharded()) {
     if (ResultPtr hr = ShardedAggregateHost(c, s)) {
@@ -3104,7 +3101,6 @@ DeviceResultPtr ExecuteSelectDevice(Connection &c, const BoundSelect &s, StreamS
   Engine &e = Eng(c);
   e.profile = c.opts.profile;
   e.events.clear();
-  e.plan_text = c.opts.profile ? ExplainSelect(s) : "";
   e.ev_used = 0;
   auto d = std::make_shared<DeviceResult>();
   d->r = RunSelectDev(e, c, s, true);
@@ -3477,7 +3473,6 @@ void ExecuteInsertSelect(Connection &c, Table &t, const BoundSelect &s, const st
   Engine &e = Eng(c);
   e.profile = c.opts.profile;  // the statement's kernels (query, append copy, zone map) become last_profile
   e.events.clear();
-  e.plan_text = "";
   e.ev_used = 0;
   DRel r;
   if (IsHostConstantSelect(s)) {
