@@ -818,6 +818,9 @@ __global__ __launch_bounds__((NL + 5) * 64) void select_rounds_kernel(SelectDesc
     for (int j = 0; j < PER; j++) tail[j] = 0;
     const bool dbg = D.dbg != nullptr;
     unsigned long long t_all = dbg ? clock64() : 0, d_wait = 0, t0 = 0;
+    // Output stores are non-temporal: the rows are written once and not read
+    // back by this kernel (sel 2.055 -> 2.025 ms, SELECT k, v 4.61 -> 4.44,
+    // SELECT v 3.40 -> 3.30 at 1e9 rows).
     // D.zstore: the zone map of the D.zmask columns is folded here, per
     // output, from the values the copy loads anyway (else by the loaders)
     const uint32_t zsmask = D.zstats && D.zstore ? (uint32_t)D.zmask & smask : 0u;
@@ -866,7 +869,7 @@ __global__ __launch_bounds__((NL + 5) * 64) void select_rounds_kernel(SelectDesc
               for (uint32_t i = lane; i < c; i += 64) {
                 const uint32_t k = (t0w + i) & mask;
                 const long long x = st[k];
-                dst[i] = x;
+                __builtin_nontemporal_store((int64_t)x, dst + i);
                 const bool ok = VAL ? (!vb || vb[k] != 0) : true;
                 mn = ok && x < mn ? x : mn;
                 mx = ok && x > mx ? x : mx;
@@ -878,8 +881,8 @@ __global__ __launch_bounds__((NL + 5) * 64) void select_rounds_kernel(SelectDesc
               for (uint32_t i = lane; i < c; i += 64) {
                 const uint32_t k = (t0w + i) & mask;
                 const int32_t x = st[k];
-                if (w8) ((int64_t *)D.dst[o] + pos)[i] = (int64_t)x;
-                else ((int32_t *)D.dst[o] + pos)[i] = x;
+                if (w8) __builtin_nontemporal_store((int64_t)x, (int64_t *)D.dst[o] + pos + i);
+                else __builtin_nontemporal_store(x, (int32_t *)D.dst[o] + pos + i);
                 const bool ok = VAL ? (!vb || vb[k] != 0) : true;
                 mn = ok && x < mn ? x : mn;
                 mx = ok && x > mx ? x : mx;
@@ -890,20 +893,20 @@ __global__ __launch_bounds__((NL + 5) * 64) void select_rounds_kernel(SelectDesc
           } else if (s8) {
             const int64_t *st = (const int64_t *)(mystage + so);
             int64_t *dst = (int64_t *)D.dst[o] + pos;
-            for (uint32_t i = lane; i < c; i += 64) dst[i] = st[(t0w + i) & mask];
+            for (uint32_t i = lane; i < c; i += 64) __builtin_nontemporal_store(st[(t0w + i) & mask], dst + i);
           } else if (D.col[oc].w == 8) {  // staged narrow: sign-extend back to int64
             const int32_t *st = (const int32_t *)(mystage + so);
             int64_t *dst = (int64_t *)D.dst[o] + pos;
-            for (uint32_t i = lane; i < c; i += 64) dst[i] = (int64_t)st[(t0w + i) & mask];
+            for (uint32_t i = lane; i < c; i += 64) __builtin_nontemporal_store((int64_t)st[(t0w + i) & mask], dst + i);
           } else {
             const int32_t *st = (const int32_t *)(mystage + so);
             int32_t *dst = (int32_t *)D.dst[o] + pos;
-            for (uint32_t i = lane; i < c; i += 64) dst[i] = st[(t0w + i) & mask];
+            for (uint32_t i = lane; i < c; i += 64) __builtin_nontemporal_store(st[(t0w + i) & mask], dst + i);
           }
           if constexpr (VAL) {
             if (vb) {
               uint8_t *vd = D.vdst[o] + pos;
-              for (uint32_t i = lane; i < c; i += 64) vd[i] = vb[(t0w + i) & mask];
+              for (uint32_t i = lane; i < c; i += 64) __builtin_nontemporal_store((uint8_t)vb[(t0w + i) & mask], vd + i);
             }
           }
         }
