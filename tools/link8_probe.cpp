@@ -163,6 +163,14 @@ int main(int argc, char **argv) {
          CK(hipStreamSynchronize(s));
          par_copy(team4, dst + h, pin + h, n - h);
        }},
+      {"register + DMA + unregister", [&](unsigned char *dst) {
+         CK(hipHostRegister(dst, n, hipHostRegisterDefault));
+         void *dp = nullptr;
+         CK(hipHostGetDevicePointer(&dp, dst, 0));
+         CK(hipMemcpyAsync(dst, d, n, hipMemcpyDeviceToHost, s));
+         CK(hipStreamSynchronize(s));
+         CK(hipHostUnregister(dst));
+       }},
       {"fine 8 chunks, 8 thr", [&](unsigned char *dst) { fine(team8, dst, n / 8); }},
       {"fine 16 chunks, 8 thr", [&](unsigned char *dst) { fine(team8, dst, n / 16); }},
       {"fine 32 chunks, 8 thr", [&](unsigned char *dst) { fine(team8, dst, n / 32); }},
