@@ -1,6 +1,7 @@
 #!/usr/bin/env python3
 """C3 kernel time vs what else is resident in HBM: the C3 table alone, after
-an 8 GB C2 table, before it, and after that table is dropped.  One JSON line."""
+an 8 GB C2 table, before it, and after that table is dropped; and the C2
+kernel with its table created first or after the C3 table.  One JSON line."""
 import json
 import os
 import sys
@@ -23,15 +24,22 @@ def conn():
     return m.connect_with_config(cfg).value
 
 
-def c3_ms(c, t, k=15):
-    sql = f"SELECT k, SUM(v), COUNT(*) FROM {t} GROUP BY k"
+def kernel_ms(c, sql, name, k=15):
     for _ in range(3):
         c.query_raw(sql).close()
     c.profile_drain()
     for _ in range(k):
         c.query_raw(sql).close()
-    ks = sorted(x["ms"] for x in c.profile_drain() if x["name"] == "group_direct")
+    ks = sorted(x["ms"] for x in c.profile_drain() if x["name"] == name)
     return round(ks[len(ks) // 2], 4)
+
+
+def c3_ms(c, t, k=15):
+    return kernel_ms(c, f"SELECT k, SUM(v), COUNT(*) FROM {t} GROUP BY k", "group_direct", k)
+
+
+def c2_ms(c, t, k=15):
+    return kernel_ms(c, f"SELECT COUNT(*) FROM {t} WHERE x > 24", "filter_agg", k)
 
 
 out = {}
@@ -40,9 +48,11 @@ c.query(C3.format(n="g"))
 out["c3_alone"] = c3_ms(c, "g")
 c.query(C2.format(n="t"))
 out["c3_then_c2_resident"] = c3_ms(c, "g")
+out["c2_after_c3 (C2 kernel)"] = c2_ms(c, "t")
 c.close()
 c = conn()
 c.query(C2.format(n="t"))
+out["c2_first (C2 kernel)"] = c2_ms(c, "t")
 c.query(C3.format(n="g"))
 out["c2_then_c3"] = c3_ms(c, "g")
 c.query("DROP TABLE t")

@@ -488,6 +488,26 @@ int main(int argc, char **argv) {
     RUN1(2, 1) RUN1(6, 1)
     return 0;
   }
+  if (argc > 2 && argv[2][0] == 'o') {  // round 3: the value array's offset from the key array in one allocation
+    unsigned char *big;
+    const size_t kb = (size_t)nsteps * 1024, vb = (size_t)nsteps * 2048;
+    CK(hipMalloc((void **)&big, kb + vb + ((size_t)64 << 20)));
+    hipLaunchKernelGGL(fill_keys, dim3(4096), dim3(256), 0, 0, (int *)big, nsteps * 256);
+    const size_t deltas[] = {0, 4096, 65536, 262144, 524288, 1 << 20, 1536 << 10, (2 << 20) + 65536, 3 << 20,
+                             5 << 20, 17 << 20, 33 << 20, 0};
+    for (size_t dv : deltas) {
+      long long *vv = (long long *)(big + kb + dv);
+      CK(hipMemset(vv, 2, vb));
+      size_t lds = 24576 + 4 * 2 * 3072;
+      CK(hipFuncSetAttribute((const void *)two_stream<2, 0>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+      float ms = TimeIt([&] { hipLaunchKernelGGL((two_stream<2, 0>), dim3(cus), dim3(256), lds, 0, (int *)big, vv, nsteps, out); }, 15);
+      printf("delta %9zu  ", dv);
+      report("two/none", 2, 1, ms);
+    }
+    // separate allocations, as the engine makes them
+    RUN2(2, 0, 1)
+    return 0;
+  }
   if (argc > 2 && argv[2][0] == 'l') {
     RUNLC(4, 4) RUNLC(6, 4) RUNLC(4, 8) RUNLC(6, 8) RUNLC(8, 8) RUNLC(6, 12)
     RUN2(2, 0, 1) RUN2(2, 2, 3)
