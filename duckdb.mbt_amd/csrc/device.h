@@ -348,6 +348,12 @@ struct SelectDesc {
     int64_t lo;
     uint64_t span;
     const uint64_t *valid;  // select_rounds: validity words (NULL fails a predicate; outputs carry it), or nullptr
+    // select_rounds, a NULL-able output column: 1 = a NULL row is staged as the
+    // value `sent` (outside the zone map of the valid rows, in the staged
+    // width) instead of with a validity byte of its own; the storer writes
+    // validity = (staged != sent) and 0 under NULL
+    int32_t vsent;
+    int64_t sent;
   } col[SL_MAX_COL];
   int32_t out_col[SL_MAX_OUT];  // index into col[]
   void *dst[SL_MAX_OUT];
@@ -359,6 +365,7 @@ struct SelectDesc {
   long long *zstats;
   int32_t zmask;
   int32_t zstore;  // 1: the storers fold the zone maps while copying, 0: the loaders
+  int32_t copy1;   // select_rounds: 1 = storers copy one row per lane per pass (MBX_SR_COPY1=1, A/B), else 4
   unsigned long long *dbg;     // nullptr, or 9 counters (MBX_SL_DEBUG) / 13 (MBX_SR_DEBUG)
   unsigned long long *dbg_ts;  // MBX_SR_DEBUG=2: s_memrealtime of every (round, workgroup) publish
 };

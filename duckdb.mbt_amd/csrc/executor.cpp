@@ -1107,6 +1107,9 @@ static bool TrySelectOnePass(Engine &e, const DRel &rel, const dev::FilterMultiD
   double out_bytes = 0;
   const char *nenv = Knob("MBX_SR_NARROW");
   const bool narrow_ok = !(nenv && atoi(nenv) == 0);
+  const char *senv = Knob("MBX_SR_SENT");  // MBX_SR_SENT=0: NULL-able outputs stage validity bytes (A/B)
+  const bool sent_off = senv && atoi(senv) == 0;
+  if (const char *c1 = Knob("MBX_SR_COPY1")) S.copy1 = atoi(c1) != 0;  // storers: one row per lane per pass (A/B)
   for (auto &x : exprs) {
     const DCol &c = rel.cols[x->col];
     if (c.validity && (mode == 2 || (uintptr_t)c.validity % 16)) return false;
@@ -1123,6 +1126,16 @@ static bool TrySelectOnePass(Engine &e, const DRel &rel, const dev::FilterMultiD
     const DevColumn *tc = c.table_col;
     if (narrow_ok && w == 8 && tc && tc->stats_valid && tc->imin >= (i128)INT32_MIN && tc->imax <= (i128)INT32_MAX)
       S.col[i].narrow = 1;
+    // a NULL-able output whose zone map leaves a value of the staged width
+    // unused stages NULL rows as that value instead of staging a validity byte
+    // per row: the staging rows are as wide as without NULLs, so the shape
+    // keeps the loader count and ring of its NULL-free form
+    if (c.validity && tc && tc->stats_valid && !sent_off) {
+      const bool w4 = w == 4 || S.col[i].narrow;
+      const i128 tmax = w4 ? (i128)INT32_MAX : (i128)INT64_MAX, tmin = w4 ? (i128)INT32_MIN : (i128)INT64_MIN;
+      if (tc->imax < tmax) S.col[i].vsent = 1, S.col[i].sent = (int64_t)tmax;
+      else if (tc->imin > tmin) S.col[i].vsent = 1, S.col[i].sent = (int64_t)tmin;
+    }
   }
   if (any_valid) {  // MBX_SR_NULLS=0: NULL-able shapes keep the two-pass form (A/B tests)
     const char *nv = Knob("MBX_SR_NULLS");

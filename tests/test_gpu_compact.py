@@ -277,7 +277,7 @@ def _ncol(conn, sql, kind, idx=0):
     return vals, np.frombuffer(b[4 + n * w:4 + n * (w + 1)], dtype=np.uint8).astype(bool)
 
 
-@pytest.mark.parametrize("path", ["auto", "rounds", "twopass"])
+@pytest.mark.parametrize("path", ["auto", "rounds", "rounds_bytes", "twopass"])
 @pytest.mark.parametrize("n", [1, 63, 64, 255, 257, 4097, 70_001, 1_000_003])
 def test_filter_compact_nullable(mbx, oracle, monkeypatch, n, path):
     """NULLs in predicate columns (a NULL fails the row) and in output columns:
@@ -316,7 +316,7 @@ def test_filter_compact_nullable(mbx, oracle, monkeypatch, n, path):
             names = [kk["name"] for kk in c.last_profile()["kernels"]]
             # NULL-free loaded columns (tiny n) take the one-pass kernel
             assert "filter_bits" in names or "select" in names or "select_rounds" in names, (sql, names)
-            if path == "rounds":
+            if path.startswith("rounds"):
                 assert "select_rounds" in names and "filter_bits" not in names, (sql, names)
                 if i == 0 and not valid.all() and m.any():
                     assert "pack_validity" in names, (sql, names)
@@ -328,4 +328,50 @@ def test_filter_compact_nullable(mbx, oracle, monkeypatch, n, path):
             got2, ok2 = _ncol(c, sql, kind, i)
             monkeypatch.delenv("MBX_FC")
             assert np.array_equal(ok2, ok) and np.array_equal(got2, got), (n, sql, i)
+    c.close()
+
+
+@pytest.mark.parametrize("sent", ["1", "0"])
+def test_select_rounds_nullable_sentinel_extremes(mbx, monkeypatch, sent):
+    """NULL-able outputs whose valid values reach the ends of the staged width:
+    an INT64 column holding INT64_MIN and INT64_MAX leaves no sentinel (validity
+    bytes are staged), an INTEGER column holding INT32_MAX and a narrow-staged
+    BIGINT column holding INT32_MAX take INT32_MIN as the sentinel, and one
+    holding INT32_MIN and INT32_MAX leaves none in 4 bytes.  Values (0 under
+    NULL) and validity exact vs numpy, one-pass kernel forced (and, with
+    sent=0, validity bytes everywhere)."""
+    monkeypatch.setenv("MBX_SR_MIN_ROWS", "0")
+    monkeypatch.setenv("MBX_SR_SENT", sent)
+    n = 300_001
+    i = np.arange(n, dtype=np.int64)
+    ext = np.array([-2**63, 2**63 - 1, -2**63 + 1, 2**63 - 2, 0, -1], dtype=np.int64)
+    e64 = ext[i % 6]
+    e32 = np.array([2**31 - 1, -5, 7, 2**31 - 2], dtype=np.int64)[i % 4]
+    f32 = np.array([2**31 - 1, -2**31, 3], dtype=np.int64)[i % 3]
+    null = (i % 5) == 2
+    cfg = mbx.Config.create()
+    cfg.set("mbx_profile", "true")
+    c = mbx.connect_with_config(cfg).value
+    def case(col):
+        return f"CASE WHEN i % 5 = 2 THEN NULL ELSE {col} END"
+    e64_sql = ("CASE WHEN i % 6 = 0 THEN -9223372036854775808 WHEN i % 6 = 1 THEN 9223372036854775807 "
+               "WHEN i % 6 = 2 THEN -9223372036854775807 WHEN i % 6 = 3 THEN 9223372036854775806 "
+               "WHEN i % 6 = 4 THEN 0 ELSE -1 END")
+    e32_sql = "CASE WHEN i % 4 = 0 THEN 2147483647 WHEN i % 4 = 1 THEN -5 WHEN i % 4 = 2 THEN 7 ELSE 2147483646 END"
+    f32_sql = "CASE WHEN i % 3 = 0 THEN 2147483647 WHEN i % 3 = 1 THEN -2147483648 ELSE 3 END"
+    m = (i % 3) != 1
+    sel = i > 1000
+    for col, kind, arr, expr in [("a", "int64", e64, e64_sql + "::BIGINT"), ("b", "int32", e32, e32_sql + "::INTEGER"),
+                                 ("c", "int64", e32, e32_sql + "::BIGINT"), ("d", "int32", f32, f32_sql + "::INTEGER"),
+                                 ("e", "int64", f32, f32_sql + "::BIGINT")]:
+        # one table per column (the device VM caps the instructions of one CTAS)
+        q(c, f"CREATE OR REPLACE TABLE se AS SELECT i AS x, {case(expr)} AS {col} FROM range({n}) tbl(i)")
+        got, ok = _ncol(c, f"SELECT {col} FROM se WHERE x % 3 <> 1", kind)
+        got2, ok2 = _ncol(c, f"SELECT {col}, x FROM se WHERE x > 1000", kind)
+        names = [kk["name"] for kk in c.last_profile()["kernels"]]
+        assert "select_rounds" in names, (col, names)
+        assert np.array_equal(ok2, ~null[sel]), col
+        assert np.array_equal(got2, np.where(null[sel], 0, arr[sel]).astype(got2.dtype)), col
+        assert np.array_equal(ok, ~null[m]), col
+        assert np.array_equal(got, np.where(null[m], 0, arr[m]).astype(got.dtype)), col
     c.close()

@@ -65,7 +65,7 @@ for name, sql in shapes.items():
         except Exception:  # noqa: BLE001
             pass
         time.sleep(float(os.environ["JIT_WAIT"]))
-    for i in range(5):
+    for i in range(int(os.environ.get("REPS", "5"))):
         t0 = time.perf_counter()
         try:
             if sql.startswith("STREAM "):
@@ -80,5 +80,6 @@ for name, sql in shapes.items():
         prof = c.last_profile()
         kern.append({k["name"]: k["ms"] for k in prof["kernels"]})
     else:
-        out[name] = {"wall_ms_median": statistics.median(walls[1:]) * 1e3, "kernels_last": kern[-1]}
+        med = {k: statistics.median(d[k] for d in kern[1:] if k in d) for k in kern[-1]}
+        out[name] = {"wall_ms_median": statistics.median(walls[1:]) * 1e3, "kernels_last": kern[-1], "kernels_median": med}
     print(name, json.dumps(out[name]), flush=True)
