@@ -1109,7 +1109,7 @@ static bool TrySelectOnePass(Engine &e, const DRel &rel, const dev::FilterMultiD
   const bool narrow_ok = !(nenv && atoi(nenv) == 0);
   const char *senv = Knob("MBX_SR_SENT");  // MBX_SR_SENT=0: NULL-able outputs stage validity bytes (A/B)
   const bool sent_off = senv && atoi(senv) == 0;
-  if (const char *c1 = Knob("MBX_SR_COPY1")) S.copy1 = atoi(c1) != 0;  // storers: one row per lane per pass (A/B)
+  if (const char *c1 = Knob("MBX_SR_COPY1")) S.copy1 = atoi(c1);  // storers: 1 = one row per lane per pass, 2 = byte validity stores (A/B)
   for (auto &x : exprs) {
     const DCol &c = rel.cols[x->col];
     if (c.validity && (mode == 2 || (uintptr_t)c.validity % 16)) return false;

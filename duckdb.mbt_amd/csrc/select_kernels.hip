@@ -466,9 +466,9 @@ __device__ __forceinline__ unsigned long long lds_add_rtn(unsigned long long *p,
 // wait.
 template <typename TS, typename TD>
 __device__ __forceinline__ void sr_copy(const TS *st, uint32_t t0w, uint32_t mask, uint32_t c, int lane, TD *dst,
-                                        bool one) {
+                                        int mode) {
   uint32_t i = lane;
-  for (; !one && i + 192 < c; i += 256) {
+  for (; mode != 1 && i + 192 < c; i += 256) {
     TS x[4];
 #pragma unroll
     for (int u = 0; u < 4; u++) x[u] = st[(t0w + i + 64 * u) & mask];
@@ -484,26 +484,39 @@ __device__ __forceinline__ void sr_copy(const TS *st, uint32_t t0w, uint32_t mas
 template <typename TS, typename TD, bool Z>
 __device__ __forceinline__ void sr_copy_sent(const TS *st, uint32_t t0w, uint32_t mask, uint32_t c, int lane, TD *dst,
                                              uint8_t *vd, TS sent, long long &mn, long long &mx, uint32_t &nv,
-                                             bool one) {
-  uint32_t i = lane;
-  // 4 rows per lane per pass: the 4 staging reads share one LDS wait
-  for (; !one && i + 192 < c; i += 256) {
+                                             int mode) {
+  uint32_t b = 0;
+  // whole passes of 256 rows, 4 per lane (rows b + lane + 64 u): the 4 staging
+  // reads share one LDS wait.  The validity of the pass comes back as 4 ballots
+  // (bit l of ballot u = row b + 64 u + l), from which lane l writes the bytes
+  // of rows b + 4 l .. b + 4 l + 3 as one 4-byte store (nibble -> bytes by one
+  // multiply), so a pass stores its 256 validity bytes with one instruction
+  // instead of four (mode 2: four byte stores, MBX_SR_COPY1=2)
+  for (; mode != 1 && b + 256 <= c; b += 256) {
     TS x[4];
 #pragma unroll
-    for (int u = 0; u < 4; u++) x[u] = st[(t0w + i + 64 * u) & mask];
+    for (int u = 0; u < 4; u++) x[u] = st[(t0w + b + lane + 64 * u) & mask];
+    unsigned long long bal[4];
 #pragma unroll
     for (int u = 0; u < 4; u++) {
       const bool ok = x[u] != sent;
-      __builtin_nontemporal_store((TD)(ok ? x[u] : (TS)0), dst + i + 64 * u);
-      __builtin_nontemporal_store((uint8_t)ok, vd + i + 64 * u);
+      __builtin_nontemporal_store((TD)(ok ? x[u] : (TS)0), dst + b + lane + 64 * u);
+      if (mode == 2) __builtin_nontemporal_store((uint8_t)ok, vd + b + lane + 64 * u);
+      bal[u] = __ballot(ok);
       if constexpr (Z) {
         mn = ok && (long long)x[u] < mn ? (long long)x[u] : mn;
         mx = ok && (long long)x[u] > mx ? (long long)x[u] : mx;
         nv += ok;
       }
     }
+    if (mode != 2) {
+      const int q = lane >> 4;
+      const unsigned long long bw = q == 0 ? bal[0] : q == 1 ? bal[1] : q == 2 ? bal[2] : bal[3];
+      const uint32_t nib = (uint32_t)(bw >> ((4 * lane) & 63)) & 0xFu;
+      __builtin_nontemporal_store((nib * 0x00204081u) & 0x01010101u, (uint32_t *)(vd + b + 4 * lane));
+    }
   }
-  for (; i < c; i += 64) {
+  for (uint32_t i = b + lane; i < c; i += 64) {
     const TS x = st[(t0w + i) & mask];
     const bool ok = x != sent;
     __builtin_nontemporal_store((TD)(ok ? x : (TS)0), dst + i);
