@@ -375,3 +375,48 @@ def test_select_rounds_nullable_sentinel_extremes(mbx, monkeypatch, sent):
         assert np.array_equal(ok, ~null[m]), col
         assert np.array_equal(got, np.where(null[m], 0, arr[m]).astype(got.dtype)), col
     c.close()
+
+
+def test_nullable_selection_large_properties(mbx, oracle):
+    """The sentinel-staged NULL-able selection at 2e8 rows (select_rounds with
+    8 loaders, result adopted by CREATE TABLE AS with the storers' zone map):
+    the result's COUNT(*), COUNT(vn), SUM(vn), MIN(vn), MAX(vn) against numpy
+    over the same generators, in 5e7-row chunks; then every output value and
+    validity bit of one 1e6-row slice in the middle."""
+    n, chunk = 200_000_000, 50_000_000
+    cfg = mbx.Config.create()
+    cfg.set("mbx_profile", "true")
+    c = mbx.connect_with_config(cfg).value
+    q(c, f"CREATE TABLE fl AS SELECT mbx_synth(42, i, 50) + 1 AS x, "
+         f"CASE WHEN mbx_synth(19, i, 7) = 0 THEN NULL ELSE mbx_synth(9, i, 1099511627776) - 549755813888 END AS vn "
+         f"FROM range({n}) tbl(i)")
+    q(c, "CREATE TABLE sl AS SELECT vn FROM fl WHERE x > 24")
+    assert "select_rounds" in [k["name"] for k in c.last_profile()["kernels"]]
+    cnt = cv = s = 0
+    mn, mx = None, None
+    for a in range(0, n, chunk):
+        x = oracle.synth_i64(chunk, 42, a, 50, 1)
+        v = oracle.synth_i64(chunk, 9, a, 2**40, -2**39)
+        ok = oracle.synth_i64(chunk, 19, a, 7, 0) != 0
+        m = x > 24
+        sv = v[m & ok]
+        cnt += int(m.sum())
+        cv += int(sv.size)
+        s += int(sv.sum(dtype=np.int64))
+        mn = int(sv.min()) if mn is None else min(mn, int(sv.min()))
+        mx = int(sv.max()) if mx is None else max(mx, int(sv.max()))
+    assert one(c, "SELECT COUNT(*), COUNT(vn), SUM(vn), MIN(vn), MAX(vn) FROM sl") == [
+        str(cnt), str(cv), str(s), str(mn), str(mx)]
+    # one slice: rows [a0, a0 + 2e6) of fl hold the selected rows [off, off + len) of sl
+    a0 = 100_000_000
+    x = oracle.synth_i64(2_000_000, 42, a0, 50, 1)
+    v = oracle.synth_i64(2_000_000, 9, a0, 2**40, -2**39)
+    ok = oracle.synth_i64(2_000_000, 19, a0, 7, 0) != 0
+    off = 0  # selected rows before a0, from the generator
+    for a in range(0, a0, chunk):
+        off += int((oracle.synth_i64(chunk, 42, a, 50, 1) > 24).sum())
+    m = x > 24
+    got, gv = _ncol(c, f"SELECT vn FROM sl LIMIT {int(m.sum())} OFFSET {off}", "int64")
+    assert np.array_equal(gv, ok[m])
+    assert np.array_equal(got, np.where(ok[m], v[m], 0))
+    c.close()
