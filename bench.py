@@ -95,15 +95,74 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
 
-    if args.dry_run:
-        return dry_run(args, world, rank)
-    if args.config in ("c1", "c4"):
+    if args.config in ("c1", "c4") and not args.dry_run:
         if rank == 0:
             return run_single_device_config(args)
         return None
-    if args.ranks:
-        return run_ranks(args, world, rank, local_rank)
-    return run_inlib(args, world, rank)
+    # N > 1 under a launcher: before anything touches a GPU, every rank counts
+    # the devices it can see and a gloo all-gather of the counts decides the
+    # form -- the in-library shards when rank 0 sees all N devices, else one
+    # device per rank with an RCCL combine (no re-exec either way)
+    form, vote = ("ranks" if args.ranks else "in-library"), None
+    if world > 1:
+        import torch.distributed as dist
+        dist.init_process_group("gloo")
+        form, vote = vote_form(args, world, rank)
+        if form is None:
+            if rank == 0:
+                log(f"[bench] {vote['reason']}")
+            dist.destroy_process_group()
+            raise SystemExit(2)
+    if args.dry_run:
+        return dry_run(args, world, rank, form, vote)
+    if form == "ranks":
+        return run_ranks(args, world, rank, local_rank, vote)
+    return run_inlib(args, world, rank, vote)
+
+
+def visible_devices(world):
+    """GPUs this process can see, counted without initialising HIP:
+    MBX_BENCH_VISIBLE_GPUS (tests simulate a launch's visibility with it), else
+    torch.cuda.device_count() (it honours HIP/ROCR/CUDA_VISIBLE_DEVICES and does
+    not initialise the GPU on this image).  A CPU dry run has nothing to count:
+    it rehearses a full node (world devices)."""
+    env = os.environ.get("MBX_BENCH_VISIBLE_GPUS")
+    if env is not None:
+        return int(env)
+    import torch
+    n = torch.cuda.device_count()
+    return n if n > 0 else -world  # negative: no GPU (a CPU rehearsal)
+
+
+def choose_form(counts, world, ranks_flag, dry_run=False):
+    """The multi-GPU form from every rank's visible-device count: (form, reason);
+    form None = no usable layout (a rank sees no GPU)."""
+    c = [(-x if x < 0 and dry_run else x) for x in counts]
+    if min(c) < 1:
+        bad = [r for r, x in enumerate(c) if x < 1]
+        return None, f"rank(s) {bad} see no GPU (visible-device counts {counts}): no usable layout"
+    if ranks_flag:
+        return "ranks", "--ranks asked for one process per GPU"
+    if c[0] >= world:
+        return "in-library", (f"rank 0 sees {c[0]} >= {world} devices: one process drives devices 0..{world - 1} "
+                              f"through gpu_devices; the other ranks only join the barriers")
+    return "ranks", (f"rank 0 sees {c[0]} < {world} devices (counts {c}): one device per rank, each rank its own "
+                     f"connection and shard, global aggregate combined by RCCL")
+
+
+def vote_form(args, world, rank):
+    """gloo all-gather of every rank's visible-device count (no GPU touched) and
+    the form all ranks then take: (form, vote dict)."""
+    import torch
+    import torch.distributed as dist
+    mine = visible_devices(world)
+    t = torch.tensor([mine], dtype=torch.int64)
+    outs = [torch.zeros(1, dtype=torch.int64) for _ in range(world)]
+    dist.all_gather(outs, t)
+    counts = [int(o.item()) for o in outs]
+    form, reason = choose_form(counts, world, args.ranks, args.dry_run)
+    return form, {"visible_devices_per_rank": counts, "min": min(counts), "max": max(counts), "form": form,
+                  "reason": reason}
 
 
 def inlib_plan(args, world):
@@ -248,28 +307,31 @@ def time_steps(step, steps, warmup, barrier=None, sync=None):
     return time.perf_counter() - t0, out
 
 
-def kernel_stats(conn, kernel, nshards, steps):
+def kernel_stats(kern, kernel, nshards, steps):
     """HIP-event durations of `kernel` over the timed loop (shard engines'
-    launches included): mean per launch and, per step, the slowest shard."""
-    ks = [k["ms"] for k in conn.profile_drain() if k["name"] == kernel]
+    launches included; `kern` = the drained profile, or a connection to drain):
+    mean per launch and, per step, the slowest shard."""
+    if not isinstance(kern, list):
+        kern = kern.profile_drain()
+    ks = [k["ms"] for k in kern if k["name"] == kernel]
     if not ks:
         return None, None, []
     per_step = [max(ks[i:i + nshards]) for i in range(0, len(ks) - nshards + 1, nshards)][:steps]
     return sum(ks) / len(ks), (sum(per_step) / len(per_step) if per_step else None), ks
 
 
-def run_inlib(args, world, rank):
+def run_inlib(args, world, rank, vote=None):
     """The product's multi-GPU path: ONE process opens every device through the
     library's own `gpu_devices` key and runs the query through duckdb_mb_query;
     the library shards the table, runs every shard on its own device/stream
     from a persistent host worker, and merges the partials.  Under the
-    driver's torch.distributed launch (one process per GPU) rank 0 drives all
-    devices and the other ranks only join the barriers (gloo, CPU)."""
+    driver's torch.distributed launch (one process per GPU, gloo world group
+    set up by the vote) rank 0 drives all devices and the other ranks only
+    join the barriers."""
     plan = inlib_plan(args, world)
     dist = None
     if world > 1:
         import torch.distributed as dist
-        dist.init_process_group("gloo")
         if rank != 0:
             dist.barrier()  # rank 0's timed region starts
             dist.barrier()  # ... and ends
@@ -289,47 +351,74 @@ def run_inlib(args, world, rank):
     cfg.set("mbx_profile", "true")
     r = mbx.connect_with_config(cfg)
     if isinstance(r, mbx.Err):
-        raise SystemExit(f"connect failed: {r.error.message}")
+        fail(dist, f"connect over gpu_devices={plan['devices']} failed: {r.error.message}")
     conn = r.value
     n_total = plan["rows_total"]
     w = workload(args.config, 0, n_total)
     t0 = time.time()
     res = conn.query(w["setup"])
     if isinstance(res, mbx.Err):
-        raise SystemExit(f"setup failed: {res.error.message}")
+        fail(dist, f"setup failed: {res.error.message}")
     log(f"[rank {rank}] setup {time.time() - t0:.2f}s: {n_total} rows over {plan['nshards']} shard(s)")
     step = make_step(conn, args.config, w["sql"])
-    for _ in range(args.warmup):
-        step()
-    conn.profile_drain()
-    barrier = dist.barrier if dist else None
-    elapsed, out = time_steps(step, args.steps, 0, barrier, torch.cuda.synchronize if torch.cuda.is_available() else None)
-    avg_k, step_k, _ = kernel_stats(conn, w["kernel"], plan["nshards"], args.steps)
+    try:
+        for _ in range(args.warmup):
+            step()
+        conn.profile_drain()
+        barrier = dist.barrier if dist else None
+        sr0 = conn.engine_stats()
+        elapsed, out = time_steps(step, args.steps, 0, barrier,
+                                  torch.cuda.synchronize if torch.cuda.is_available() else None)
+        sr_out = sel_outcomes(conn, sr0)
+    except Exception as ex:  # noqa: BLE001 - a shard's error names the shard and its device
+        fail(dist, f"query failed: {ex}")
+    kern = conn.profile_drain()
+    avg_k, step_k, _ = kernel_stats(kern, w["kernel"], plan["nshards"], args.steps)
     sstats = conn.shard_stats() if plan["nshards"] > 1 else None
     if dist:
         t_all = torch.tensor([elapsed], dtype=torch.float64)
         dist.all_reduce(t_all, op=dist.ReduceOp.MAX)
         elapsed = float(t_all.item())
     threads = len(os.sched_getaffinity(0))
-    parity, _ = parity_check(conn, args.config, w["sql"], out, 0, n_total, threads)
+    shard_par = None
+    if sstats and args.config in ("c2", "c2d", "c5", "c3"):
+        parity, shard_par = sharded_parity(conn, args.config, out, n_total, plan["nshards"], threads)
+    else:
+        parity, _ = parity_check(conn, args.config, w["sql"], out, 0, n_total, threads)
     if sstats:
         parity["checked"] = (f"the global answer over all {n_total} rows ({plan['nshards']} shards, merged in the "
-                             f"library) vs the oracle over the same rows")
+                             f"library) vs the oracle over the same rows"
+                             + ("; every shard's partial vs the oracle over its own row range" if shard_par else ""))
     result = headline(args, w, plan["ngpu"], elapsed, avg_k, n_total, args.rows // plan["shards_per_gpu"],
                       plan["parallelism"], parity,
                       sel_rows=int(out[0]) if args.config == "sel" else None)
+    if vote:
+        result["config"]["form"] = vote
     if sstats:
         ms = elapsed / args.steps * 1e3
-        result["multi_device"] = {
+        md = {
             "path": "in-library (gpu_devices)", "shards": plan["nshards"], "devices": plan["devices"],
             "rows_per_shard": n_total // plan["nshards"],
             "kernel_ms_per_launch_avg": avg_k, "slowest_shard_kernel_ms_per_step": step_k,
+            "kernel_ms_per_shard": per_shard_kernel_ms(kern, w["kernel"], plan["nshards"]),
             "combine_overhead_ms_per_step": (ms - step_k) if step_k else None,
-            "last_dispatch_us": sstats["last_dispatch_us"], "last_host_merge_us": sstats["last_combine_us"],
             "peer_links": sstats["peer_links"], "host_results": sstats["host_results"],
             "note": ("shards on one device run concurrently, so per-launch times overlap"
                      if plan["shards_per_gpu"] > 1 else "one shard per device")}
+        md["split_us"] = overhead_split(conn, step, 10)
+        if shard_par is not None:
+            md["shard_parity"] = shard_par
+        if args.config in ("c2", "c2d", "c5"):
+            md["rccl_combine"] = rccl_leg(conn, step, args, w, n_total, plan)
+        result["multi_device"] = md
     calibrate_into(conn, result, args.config)
+    if args.config == "sel":
+        # every timed step must have run the one-pass kernel (per shard): a fallback fails parity loudly
+        result["select_rounds"] = sr_out
+        result["fallbacks"] = sr_out["fallbacks"]
+        if sr_out["fallbacks"] or sr_out["select_rounds_launches"] < args.steps * plan["nshards"]:
+            result["parity"]["match"] = False
+            result["parity"]["fallback_error"] = f"select_rounds outcomes in the timed loop: {sr_out}"
     extras = args.extra
     if extras == "auto":
         extras = "c3,sel" if (args.config == "c2" and plan["nshards"] == 1) else ""
@@ -344,7 +433,160 @@ def run_inlib(args, world, rank):
         dist.destroy_process_group()
     conn.close()
     print(json.dumps(result), flush=True)
+    bad = not result["parity"].get("match", True) or (shard_par and not all(p["match"] for p in shard_par))
+    if bad:
+        log("[bench] PARITY FAILURE: " + json.dumps(result["parity"]) +
+            (" shards: " + json.dumps([p for p in shard_par if not p["match"]]) if shard_par else ""))
+        raise SystemExit(3)
     return result
+
+
+def fail(dist, msg):
+    """A failure before the JSON line: the message (naming the shard and device
+    when a shard raised it) on stderr, every rank released, exit status 2."""
+    log(f"[bench] FAILED: {msg}")
+    if dist is not None:
+        try:
+            dist.destroy_process_group()
+        except Exception:  # noqa: BLE001
+            pass
+    raise SystemExit(2)
+
+
+def per_shard_kernel_ms(kern, kernel, nshards):
+    """Mean HIP-event duration of `kernel` per shard (from the profile's shard tags)."""
+    acc = {}
+    for k in kern:
+        if k["name"] == kernel and k.get("shard", -1) >= 0:
+            acc.setdefault(k["shard"], []).append(k["ms"])
+    return [{"shard": i, "device": next((k["device"] for k in kern if k.get("shard") == i), None),
+             "kernel_ms_avg": (sum(acc[i]) / len(acc[i])) if i in acc else None, "launches": len(acc.get(i, []))}
+            for i in range(nshards)]
+
+
+def overhead_split(conn, step, reps):
+    """Where a sharded step's host time goes, from `reps` untimed steps after the
+    timed loop (medians): until every worker took the job (dispatch), until its
+    launches were queued, its kernel + D2H + synchronisation, and the merge."""
+    import statistics
+    rows = []
+    for _ in range(reps):
+        t0 = time.perf_counter()
+        step()
+        wall = (time.perf_counter() - t0) * 1e6
+        st = conn.shard_stats()
+        tm = conn.shard_timings()
+        if not tm:
+            continue
+        rows.append({"wall": wall, "dispatch": max(t["wake_us"] for t in tm),
+                     "launch": max(t["launch_us"] - t["wake_us"] for t in tm),
+                     "kernel_d2h": max(t["done_us"] - t["launch_us"] for t in tm),
+                     "all_done": max(t["done_us"] for t in tm), "merge": st["last_combine_us"],
+                     "dispatch_wall": st["last_dispatch_us"], "per_shard": tm})
+    if not rows:
+        return None
+    med = {k: statistics.median(r[k] for r in rows) for k in
+           ("wall", "dispatch", "launch", "kernel_d2h", "all_done", "merge", "dispatch_wall")}
+    return {"step_wall_us": med["wall"], "dispatch_us": med["dispatch"], "launch_us": med["launch"],
+            "kernel_d2h_sync_us": med["kernel_d2h"], "all_shards_done_us": med["all_done"],
+            "host_merge_us": med["merge"], "dispatch_wall_us": med["dispatch_wall"],
+            "rest_us": med["wall"] - med["dispatch_wall"] - med["merge"],
+            "last_step_per_shard": rows[-1]["per_shard"], "reps": len(rows),
+            "definition": "medians over untimed steps after the timed loop; dispatch = until the last worker took "
+                          "the job; launch = plan + launches queued (max over shards); kernel_d2h_sync = launch "
+                          "queued -> partial on the host (max over shards); rest = parse/bind/result outside the "
+                          "sharded dispatch and merge"}
+
+
+def sharded_parity(conn, config, out, n_total, nshards, threads):
+    """Every shard's partial (duckdb_mbx_shard_partial) vs the oracle over the
+    shard's own row range (CTAS splits range(n) evenly: part i = rows
+    [n i / S, n (i + 1) / S)), and the global answer vs the sum of those
+    oracles (checker only, outside the timed loop)."""
+    sys.path.insert(0, HERE)
+    from oracle import Oracle
+    orc = Oracle()
+    shard_par, g_cnt, g_sum, g_groups = [], 0, 0, {}
+    for i in range(nshards):
+        lo, hi = n_total * i // nshards, n_total * (i + 1) // nshards
+        rr = conn.shard_partial(i)
+        if config == "c3":
+            oc, osum = orc.synth_groupby(7, 9, lo, hi - lo, 32, 1 << 40, -(1 << 39), threads)
+            exp = [(k, oc[k], osum[k]) for k in range(32) if oc[k]]
+            for k, c_, s_ in exp:
+                gc, gs = g_groups.get(k, (0, 0))
+                g_groups[k] = (gc + c_, gs + s_)
+            got = None
+            if rr is not None:
+                rows, nulls = rr.cells()
+                got = sorted((None if nl[0] else int(rw[0]), int(rw[2]), None if nl[1] else int(rw[1]))
+                             for rw, nl in zip(rows, nulls))
+            shard_par.append({"shard": i, "rows": [lo, hi], "groups": len(got or []), "match": got == exp})
+        else:
+            oc, osum = orc.synth_filter_count(42, lo, hi - lo, 50, 1, 25, 2**63 - 1, threads)
+            g_cnt += oc
+            g_sum += osum
+            got_c = int(rr.value(0, 0)) if rr is not None else None
+            ent = {"shard": i, "rows": [lo, hi], "count": got_c, "oracle_count": oc}
+            ok = got_c == oc
+            if config == "c5" and rr is not None:
+                ent["sum"] = int(rr.value(1, 0))
+                ent["oracle_sum"] = osum
+                ok = ok and ent["sum"] == osum
+            ent["match"] = ok
+            shard_par.append(ent)
+        if rr is not None:
+            rr.close()
+    if config == "c3":
+        exp = [(k, g_groups[k][0], g_groups[k][1]) for k in sorted(g_groups)]
+        got = sorted(out, key=lambda g: (g[0] is None, g[0]))
+        par = {"groups": len(got), "oracle_groups": len(exp), "match": got == exp}
+    else:
+        par = {"gpu_count": int(out[0]), "oracle_count": g_cnt, "match": int(out[0]) == g_cnt}
+        if config == "c5":
+            par.update({"gpu_sum": int(out[1]), "oracle_sum": g_sum, "match": par["match"] and int(out[1]) == g_sum})
+    return par, shard_par
+
+
+def rccl_leg(conn, step, args, w, n_total, plan):
+    """The same query with the library's RCCL combine (mbx_combine=rccl), timed
+    with the same discipline right after the host-merge headline: warmup (the
+    communicators are created on first use), K timed steps, the global answer
+    vs the headline's.  On same-device shards RCCL cannot run (one rank per
+    device) and the library falls back to the host merge: reported as such."""
+    import torch
+    try:
+        conn.set_combine(True)
+        for _ in range(max(1, args.warmup)):
+            step()
+        st0 = conn.rccl_stats()
+        conn.profile_drain()
+        elapsed, out = time_steps(step, args.steps, 0, None, torch.cuda.synchronize)
+        st1 = conn.rccl_stats()
+        conn.profile_drain()
+        conn.set_combine(False)
+        ran = st1["rccl_combines"] - st0["rccl_combines"]
+        exp = step()  # host merge again: the reference answer of the same rows
+        return {"ran_rccl_steps": ran, "fell_back_steps": st1["rccl_fallbacks"] - st0["rccl_fallbacks"],
+                "note": st1["note"], "ms_per_step": elapsed / args.steps * 1e3,
+                "value": n_total * args.steps / elapsed, "unit": "rows/s",
+                "last_collective_d2h_us": st1["last_rccl_us"],
+                "parity": {"rccl": [str(x) for x in out], "host_merge": [str(x) for x in exp],
+                           "match": [str(x) for x in out] == [str(x) for x in exp]}}
+    except Exception as ex:  # noqa: BLE001 - the RCCL leg must not lose the headline line
+        conn.set_combine(False)
+        return {"error": str(ex)}
+
+
+def sel_outcomes(conn, before):
+    """select_rounds outcomes since `before` (duckdb_mbx_engine_stats): launches,
+    aborts (a persistent workgroup never scheduled: the two-pass form reran)
+    and launch failures; fallbacks = aborts + failures."""
+    st = conn.engine_stats()
+    if before:
+        st = {k: st[k] - before.get(k, 0) for k in st}
+    st["fallbacks"] = st["select_rounds_aborts"] + st["select_rounds_launch_failures"]
+    return st
 
 
 def headline(args, w, ngpu, elapsed, avg_kernel_ms, n_rows_step, launch_rows, parallelism, parity, sel_rows=None):
@@ -412,7 +654,9 @@ def sub_bench(conn, config, plan, args):
             step()
         conn.profile_drain()
         import torch
+        before = conn.engine_stats()
         elapsed, out = time_steps(step, args.steps, 0, None, torch.cuda.synchronize)
+        outcomes = sel_outcomes(conn, before) if config == "sel" else None
         avg_k, _, _ = kernel_stats(conn, w["kernel"], plan["nshards"], args.steps)
         launch_rows = n_total // plan["nshards"]
         sel_rows = int(out[0]) if config == "sel" else None
@@ -421,11 +665,23 @@ def sub_bench(conn, config, plan, args):
         parity, _ = parity_check(conn, config, w["sql"], out, 0, n_total, len(os.sched_getaffinity(0)))
         if config == "c3":
             conn.query("DROP TABLE t3")
-        return {"workload": w["workload"], "sql": w["sql"], "steps": args.steps, "warmup": args.warmup,
-                "ms_per_step": elapsed / args.steps * 1e3, "value": n_total * args.steps / elapsed, "unit": "rows/s",
-                "kernel": w["kernel"], "kernel_ms_avg": avg_k, "algorithmic_bytes_per_launch": alg,
-                "achieved_gbs": ach, "frac": ach / HBM_PEAK_GBS if ach else None,
-                "traffic": pmc_traffic(w["kernel"], launch_rows), "parity": parity}
+        r = {"workload": w["workload"], "sql": w["sql"], "steps": args.steps, "warmup": args.warmup,
+             "ms_per_step": elapsed / args.steps * 1e3, "value": n_total * args.steps / elapsed, "unit": "rows/s",
+             "kernel": w["kernel"], "kernel_ms_avg": avg_k, "algorithmic_bytes_per_launch": alg,
+             "achieved_gbs": ach, "frac": ach / HBM_PEAK_GBS if ach else None,
+             "traffic": pmc_traffic(w["kernel"], launch_rows), "parity": parity}
+        if outcomes is not None:
+            # every timed step must have run the one-pass kernel: an abort (a persistent workgroup
+            # never scheduled, the two-pass form reran) or a launch failure is a fallback
+            r["select_rounds"] = outcomes
+            r["fallbacks"] = outcomes["fallbacks"]
+            if outcomes["fallbacks"] or outcomes["select_rounds_launches"] < args.steps:
+                r["parity"]["match"] = False
+                r["parity"]["fallback_error"] = (f"{outcomes['fallbacks']} select_rounds fallback(s) / "
+                                                 f"{outcomes['select_rounds_launches']} launches in "
+                                                 f"{args.steps} timed steps")
+                log("[bench] sel: select_rounds fell back in the timed loop: " + json.dumps(outcomes))
+        return r
     except Exception as ex:  # noqa: BLE001 - a sub-benchmark failure must not lose the headline line
         return {"error": str(ex)}
 
@@ -442,22 +698,22 @@ def run_single_device_config(args):
     return bench_c4(mbx, conn, min(args.rows, 100_000_000), args)
 
 
-def run_ranks(args, world, rank, local_rank):
+def run_ranks(args, world, rank, local_rank, vote=None):
     """One process per GPU (torch.distributed): every rank holds its own
     1e9-row shard (rows [r*N, (r+1)*N) of the same generator) in its own
     connection, and the global aggregate is combined with an RCCL collective
-    inside the timed step (distributed.py)."""
+    inside the timed step (distributed.py).  The world group is gloo (the
+    vote, barriers, timing); the combine runs on an RCCL group (backend
+    "nccl") over the ranks' devices, or on the gloo group to rehearse."""
     import torch
     import torch.distributed as dist
     ndev = torch.cuda.device_count()
-    device = local_rank % max(ndev, 1)  # == local_rank on a full node; folds ranks when rehearsing
+    device = local_rank % max(ndev, 1)  # == local_rank on a full node; 0 when each rank sees one device
     torch.cuda.set_device(device)
-    coll_dev = "cuda" if args.dist_backend == "nccl" else "cpu"
-    if world > 1:
-        if args.dist_backend == "nccl":
-            dist.init_process_group("nccl", device_id=torch.device("cuda", device))
-        else:
-            dist.init_process_group("gloo")
+    coll_dev, group = "cpu", None
+    if world > 1 and args.dist_backend == "nccl":
+        coll_dev = "cuda"
+        group = dist.new_group(backend="nccl")
     mbx = load_mbx()
     import importlib.util
     spec = importlib.util.spec_from_file_location("duckdb_mbt_amd_distributed",
@@ -470,7 +726,7 @@ def run_ranks(args, world, rank, local_rank):
     cfg.set("mbx_profile", "true")
     r = mbx.connect_with_config(cfg)
     if isinstance(r, mbx.Err):
-        raise SystemExit(f"connect failed: {r.error.message}")
+        fail(dist if world > 1 else None, f"rank {rank}: connect to device {device} failed: {r.error.message}")
     conn = r.value
     n = args.rows
     start = rank * n
@@ -479,7 +735,7 @@ def run_ranks(args, world, rank, local_rank):
     t0 = time.time()
     res = conn.query(w["setup"])
     if isinstance(res, mbx.Err):
-        raise SystemExit(f"setup failed: {res.error.message}")
+        fail(dist if world > 1 else None, f"rank {rank} (device {device}): setup failed: {res.error.message}")
     log(f"[rank {rank}] setup {time.time() - t0:.2f}s: {n} rows")
     step = make_step(conn, args.config, w["sql"])
     gcount = gsum = ggroups = None
@@ -492,10 +748,11 @@ def run_ranks(args, world, rank, local_rank):
         if world == 1 or args.config == "sel":
             return None
         if c2like:
-            return mbx_dist.allreduce_count_async(int(out[0]), device=coll_dev)  # RCCL over xGMI: COUNT(*)
+            return mbx_dist.allreduce_count_async(int(out[0]), device=coll_dev, group=group)  # COUNT(*)
         if args.config == "c5":
-            return mbx_dist.global_count_sum_async(int(out[0]), int(out[1]) if out[1] else None, device=coll_dev)
-        return mbx_dist.global_group_count_sum(out, device=coll_dev)  # C3: 32 x (key, count, int128 sum)
+            return mbx_dist.global_count_sum_async(int(out[0]), int(out[1]) if out[1] else None, device=coll_dev,
+                                                   group=group)
+        return mbx_dist.global_group_count_sum(out, device=coll_dev, group=group)  # C3: 32 x (key, count, sum)
 
     def finish_combines(pending):
         nonlocal gcount, gsum, ggroups
@@ -510,32 +767,36 @@ def run_ranks(args, world, rank, local_rank):
             else:
                 ggroups = r
 
-    # warmup includes the collective, so communicator setup is never timed
-    finish_combines([combine(step()) for _ in range(args.warmup)])
-    conn.profile_drain()
+    try:
+        # warmup includes the collective, so communicator setup is never timed
+        finish_combines([combine(step()) for _ in range(args.warmup)])
+        conn.profile_drain()
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+        t_start = time.perf_counter()
+        pending = []
+        out = None
+        for _ in range(args.steps):
+            out = step()
+            pending.append(combine(out))
+        finish_combines(pending)
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+        elapsed = time.perf_counter() - t_start
+    except Exception as ex:  # noqa: BLE001
+        fail(dist if world > 1 else None, f"rank {rank} (device {device}): {ex}")
+    kern = conn.profile_drain()
+    avg_k, _, _ = kernel_stats(kern, w["kernel"], 1, args.steps)
+    t_all = torch.tensor([elapsed], dtype=torch.float64)
     if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t_start = time.perf_counter()
-    pending = []
-    out = None
-    for _ in range(args.steps):
-        out = step()
-        pending.append(combine(out))
-    finish_combines(pending)
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    elapsed = time.perf_counter() - t_start
-    avg_k, _, _ = kernel_stats(conn, w["kernel"], 1, args.steps)
-    t_all = torch.tensor([elapsed], dtype=torch.float64, device=coll_dev)
-    if world > 1:
-        dist.all_reduce(t_all, op=dist.ReduceOp.MAX)
+        dist.all_reduce(t_all, op=dist.ReduceOp.MAX)  # (gloo world group)
     elapsed = float(t_all.item())
     parity, orc = parity_check(conn, args.config, w["sql"], out, start, n, host_share(world))
     if world > 1 and args.config in ("c2", "c2d", "c5"):
         # global answer (combined over RCCL in the timed loop) vs the sum of the shard oracles
-        g_oracle, g_osum = mbx_dist.global_count_sum(orc[0], orc[1], device=coll_dev)
+        g_oracle, g_osum = mbx_dist.global_count_sum(orc[0], orc[1], device=coll_dev, group=group)
         parity["global_count"] = gcount
         parity["global_oracle_count"] = g_oracle
         parity["match"] = parity["match"] and gcount == g_oracle
@@ -543,15 +804,30 @@ def run_ranks(args, world, rank, local_rank):
             parity["global_sum"] = gsum
             parity["match"] = parity["match"] and gsum == g_osum
     if world > 1 and args.config == "c3":
-        g_exp = mbx_dist.global_group_count_sum(orc, device=coll_dev)
+        g_exp = mbx_dist.global_group_count_sum(orc, device=coll_dev, group=group)
         parity["global_groups"] = len(ggroups)
         parity["match"] = parity["match"] and ggroups == g_exp
+    # every rank's own line items, gathered to rank 0 (gloo)
+    mine = {"rank": rank, "device": device, "kernel_ms_avg": avg_k, "elapsed_s": elapsed,
+            "shard_match": parity.get("match"), "rows": [start, start + n]}
+    per_rank = [mine]
+    if world > 1:
+        per_rank = [None] * world
+        dist.all_gather_object(per_rank, mine)
     result = None
     if rank == 0:
         par = f"row-range shards x{world}" + ((" + RCCL all-reduce/all-gather" if args.dist_backend == "nccl"
                                               else " + gloo collectives (rehearsal)") if world > 1 else "")
+        if vote:
+            par += " [one process per GPU: " + vote["reason"] + "]"
         result = headline(args, w, world, elapsed, avg_k, n * world, n, par, parity,
                           sel_rows=int(out[0]) if args.config == "sel" else None)
+        if vote:
+            result["config"]["form"] = vote
+        if world > 1:
+            result["multi_device"] = {"path": "one process per GPU (torch.distributed)", "ranks": world,
+                                      "combine": ("RCCL (nccl group)" if args.dist_backend == "nccl" else "gloo"),
+                                      "per_rank": per_rank}
         calibrate_into(conn, result, args.config)
         if not args.no_cpu and world == 1 and args.config in ("c2", "c2d", "c3", "c5", "sel"):
             result["cpu_baseline"] = cpu_baseline(args.cpu_seconds, "c2" if args.config == "c2d" else args.config)
@@ -561,30 +837,37 @@ def run_ranks(args, world, rank, local_rank):
     conn.close()
     if rank == 0:
         print(json.dumps(result), flush=True)
+        if not result["parity"].get("match", True) or not all(p["shard_match"] for p in per_rank):
+            log("[bench] PARITY FAILURE: " + json.dumps(per_rank))
+            raise SystemExit(3)
 
 
-def dry_run(args, world, rank):
+def dry_run(args, world, rank, form=None, vote=None):
     """Plumbing only (no GPU): every rank joins a gloo all-reduce of its rank id
-    and rank 0 prints the JSON skeleton of the layout it would run."""
+    (after the device vote, when there is one) and rank 0 prints the JSON
+    skeleton of the layout it would run."""
     import torch
     import torch.distributed as dist
     t = torch.tensor([rank + 1], dtype=torch.int64)
     if world > 1:
-        dist.init_process_group("gloo")
         dist.all_reduce(t)
         dist.destroy_process_group()
+    form = form or ("ranks" if args.ranks else "in-library")
     if rank == 0:
-        if args.ranks:
+        if form == "ranks":
             mode, ngpu, devices = "ranks", world, None
             par = f"row-range shards x{world}" + (" + RCCL all-reduce/all-gather" if world > 1 else "")
+            if vote:
+                par += " [one process per GPU: " + vote["reason"] + "]"
         else:
             plan = inlib_plan(args, world)
             mode, ngpu, devices, par = "in-library", plan["ngpu"], plan["devices"], plan["parallelism"]
+        cfg = {"workload": args.config, "rows_per_gpu": args.rows, "parallelism": par}
+        if vote:
+            cfg["form"] = vote
         print(json.dumps({"metric": METRIC, "value": None, "unit": "rows/s", "n_gpus": ngpu,
                           "dry_run": True, "mode": mode, "processes": world, "rank_id_sum": int(t.item()),
-                          "gpu_devices": devices,
-                          "config": {"workload": args.config, "rows_per_gpu": args.rows,
-                                     "parallelism": par}}), flush=True)
+                          "gpu_devices": devices, "config": cfg}), flush=True)
 
 
 def free_port():

@@ -83,6 +83,13 @@ _sig("duckdb_mbx_hbm_calibrate_ex", _I, _P, _L, _I, ctypes.POINTER(ctypes.c_doub
 _sig("duckdb_mbx_statement_plan_stats", _I, _P, ctypes.POINTER(ctypes.c_int64))
 _sig("duckdb_mbx_shard_stats", _I, _P, ctypes.POINTER(ctypes.c_int64), ctypes.POINTER(ctypes.c_double))
 _sig("duckdb_mbx_engine_stats", _I, _P, ctypes.POINTER(ctypes.c_int64))
+_sig("duckdb_mbx_shard_timings", _I, _P, ctypes.POINTER(ctypes.c_double), _I)
+_sig("duckdb_mbx_shard_partial", _P, _P, _I)
+_sig("duckdb_mbx_rccl_stats", _I, _P, ctypes.POINTER(ctypes.c_int64), ctypes.POINTER(ctypes.c_double))
+_sig("duckdb_mbx_rccl_note", ctypes.c_void_p, _P)
+_sig("duckdb_mbx_set_combine", _I, _P, _I)
+_sig("duckdb_mbx_combine_lanes", _I, ctypes.POINTER(ctypes.c_int64), _I, _I, ctypes.POINTER(ctypes.c_int8),
+     ctypes.POINTER(ctypes.c_int64))
 
 for _n in ["duckdb_mb_connect"]:
     _sig(_n, _P, _B)
@@ -598,6 +605,37 @@ class Connection:
         return {"select_rounds_launches": out[0], "select_rounds_aborts": out[1],
                 "select_rounds_launch_failures": out[2]}
 
+    def shard_timings(self) -> list:
+        """The last sharded dispatch, per shard (extension): device and the us
+        since the dispatch began at which the worker took the job (wake), its
+        launches were queued (launch) and its result reached the host (done)."""
+        cap = 256
+        out = (ctypes.c_double * (4 * cap))()
+        n = lib.duckdb_mbx_shard_timings(self._h, out, cap)
+        return [{"shard": i, "device": int(out[4 * i]), "wake_us": out[4 * i + 1], "launch_us": out[4 * i + 2],
+                 "done_us": out[4 * i + 3]} for i in range(min(n, cap))]
+
+    def shard_partial(self, shard: int):
+        """Shard `shard`'s partial aggregate row(s) of the last sharded aggregate
+        as a RawResult (None if there is none)."""
+        h = lib.duckdb_mbx_shard_partial(self._h, shard)
+        return RawResult(h) if h else None
+
+    def rccl_stats(self) -> dict:
+        """mbx_combine=rccl counters (extension): RCCL combines, fallbacks to the
+        host merge and why the last one fell back, the last collective's us."""
+        out = (ctypes.c_int64 * 2)()
+        us = (ctypes.c_double * 1)()
+        lib.duckdb_mbx_rccl_stats(self._h, out, us)
+        p = lib.duckdb_mbx_rccl_note(self._h)
+        note = ctypes.string_at(p).decode()
+        lib.duckdb_mbx_free(p)
+        return {"rccl_combines": out[0], "rccl_fallbacks": out[1], "last_rccl_us": us[0], "note": note}
+
+    def set_combine(self, rccl: bool) -> None:
+        """Host merge (False) or RCCL combine (True) from the next statement on."""
+        lib.duckdb_mbx_set_combine(self._h, 1 if rccl else 0)
+
     def profile_drain(self) -> list:
         import json
         p = lib.duckdb_mbx_profile_drain(self._h)
@@ -1084,3 +1122,37 @@ class ArrowResult:
             self._h = None
         if on_done:
             on_done(Ok(None))
+
+
+def combine_lanes(parts, kinds):
+    """The in-library RCCL combine's lane arithmetic run on the host
+    (duckdb_mbx_combine_lanes; the device runs the same code, combine.h).
+    parts[rank][j] = a partial value (int, up to int128) or None (NULL);
+    kinds[j] = "sum" | "min" | "max".  Returns the combined value per column
+    (None if every rank's is NULL)."""
+    nr, nc = len(parts), len(kinds)
+    lanes = (ctypes.c_int64 * (nr * (3 * nc + 1)))()
+    m64 = (1 << 64) - 1
+    for r, row in enumerate(parts):
+        for j, v in enumerate(row):
+            base = r * (3 * nc + 1) + 3 * j
+            if v is None:
+                lanes[base + 2] = 0
+                continue
+            u = v & ((1 << 128) - 1)
+            lo, hi = u & m64, u >> 64
+            lanes[base] = lo - (1 << 64) if lo >> 63 else lo
+            lanes[base + 1] = hi - (1 << 64) if hi >> 63 else hi
+            lanes[base + 2] = 1
+    kk = (ctypes.c_int8 * nc)(*[{"sum": 0, "min": 1, "max": 2}[k] for k in kinds])
+    out = (ctypes.c_int64 * (3 * nc))()
+    if lib.duckdb_mbx_combine_lanes(lanes, nr, nc, kk, out) != 1:
+        raise ValueError("combine_lanes: bad arguments")
+    res = []
+    for j in range(nc):
+        if not out[3 * j + 2] & 1:
+            res.append(None)
+            continue
+        v = ((out[3 * j + 1] & m64) << 64) | (out[3 * j] & m64)
+        res.append(v - (1 << 128) if v >> 127 else v)
+    return res

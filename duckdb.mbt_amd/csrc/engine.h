@@ -99,6 +99,7 @@ struct QueryProfile {
     double ms = 0;
     double bytes = 0;  // algorithmic bytes moved
     int64_t rows = 0;
+    int shard = -1, device = -1;  // the shard engine that ran it (gpu_devices), -1: the connection's own
   };
   std::vector<Kernel> kernels;
   double total_ms = 0;
@@ -124,10 +125,17 @@ struct Options {
   // "mbx_force_peer" (tests): shards on the same device still exchange row
   // results by peer DMA (hipMemcpyPeerAsync), as distinct devices do
   bool force_peer = false;
+  // "mbx_combine" = "host" (default) | "rccl": a sharded global aggregate over
+  // distinct devices combines its partials with RCCL collectives on the shard
+  // devices (rccl_combine.h) instead of the host merge
+  bool combine_rccl = false;
   std::map<std::string, std::string> raw;
 };
 
 struct Engine;        // per-connection executor state (device stream, scratch)
+namespace rc {
+struct Comms;  // RCCL communicators over the shard devices (rccl_combine.h)
+}
 struct ShardWorkers;  // persistent per-shard host threads (executor.cpp)
 
 // Counters of the multi-device path (duckdb_mbx_shard_stats).
@@ -139,6 +147,22 @@ struct ShardStats {
   int64_t host_results = 0;  // sharded aggregates finished on the host (no re-upload)
   double last_dispatch_us = 0;  // wall time of the last ForShards (all shards' work)
   double last_combine_us = 0;   // host merge of the last sharded aggregate
+  // the last ForShards, per shard (duckdb_mbx_shard_timings), in us from the
+  // dispatch: the worker picked the job up (wake), its plan + launches were
+  // queued (launch), its result reached the host (done: kernel + D2H + sync)
+  struct Timing {
+    int device = -1;
+    double wake_us = 0, launch_us = 0, done_us = 0;
+  };
+  std::vector<Timing> last;
+  // the per-shard partial relations of the last sharded aggregate, as they
+  // came back from each device before the merge (duckdb_mbx_shard_partial)
+  std::vector<ResultPtr> last_partials;
+  // mbx_combine=rccl: sharded global aggregates combined by RCCL collectives
+  // on the shard devices instead of the host merge
+  int64_t rccl_combines = 0, rccl_fallbacks = 0;
+  double last_rccl_us = 0;
+  std::string rccl_note;  // why the last rccl request fell back (empty: it ran)
 };
 
 struct Connection {
@@ -152,7 +176,10 @@ struct Connection {
   // combines their results
   std::vector<std::unique_ptr<Connection>> shards;
   std::shared_ptr<ShardWorkers> workers;  // declared after shards: stopped before they go
+  std::shared_ptr<rc::Comms> rccl;        // mbx_combine=rccl, opened on first use
+  bool rccl_tried = false;
   ShardStats shard_stats;
+  int64_t shard_stats_t0 = 0;  // steady-clock ns at the start of the current ForShards
   bool sharded() const { return !shards.empty(); }
   ~Connection();
 };

@@ -12,6 +12,7 @@
 #include <algorithm>
 #include <atomic>
 #include <chrono>
+#include <type_traits>
 #include <cmath>
 #include <condition_variable>
 #include <cstring>
@@ -29,6 +30,7 @@
 #include "hostlink.h"
 #include "vm.h"
 #include "knobs.h"
+#include "rccl_combine.h"
 
 namespace mbx {
 
@@ -3639,11 +3641,40 @@ struct ShardWorkers {
   }
 };
 
+// us since the current dispatch of c started (per-shard timings)
+static double SinceDispatch(const Connection &c) {
+  return (double)(std::chrono::steady_clock::now().time_since_epoch().count() - c.shard_stats_t0) * 1e-3;
+}
+// a shard's plan and launches are queued (called on its worker thread)
+static void MarkLaunched(Connection &c, int i) {
+  if (i < (int)c.shard_stats.last.size()) c.shard_stats.last[i].launch_us = SinceDispatch(c);
+}
+
+// Runs f(i) for every shard i at once (shard 0 on the calling thread).  Each
+// shard's times land in shard_stats.last; an error raised on a shard comes
+// back naming the shard and its device.
 static void ForShards(Connection &c, const std::function<void(int)> &f) {
+  static_assert(std::is_same<std::chrono::steady_clock::duration, std::chrono::nanoseconds>::value, "ns clock");
   const auto t0 = std::chrono::steady_clock::now();
+  c.shard_stats_t0 = t0.time_since_epoch().count();
   if (!c.workers) c.workers = std::make_shared<ShardWorkers>((int)c.shards.size());
   c.shard_stats.dispatches++;
-  c.workers->Run(f);
+  const int nsh = (int)c.shards.size();
+  c.shard_stats.last.assign(nsh, ShardStats::Timing());
+  const std::function<void(int)> g = [&](int i) {
+    ShardStats::Timing &T = c.shard_stats.last[i];
+    T.device = c.shards[i]->opts.device;
+    T.wake_us = SinceDispatch(c);
+    try {
+      f(i);
+    } catch (std::exception &ex) {
+      throw EngineError(std::string(ex.what()) + " (shard " + std::to_string(i) + " of " + std::to_string(nsh) +
+                        ", device " + std::to_string(T.device) + ")");
+    }
+    if (T.launch_us == 0) T.launch_us = SinceDispatch(c);
+    T.done_us = SinceDispatch(c);
+  };
+  c.workers->Run(g);
   c.shard_stats.last_dispatch_us =
       std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0).count();
 }
@@ -3659,7 +3690,7 @@ static Engine &ShardEngine(Connection &top, Connection &sc) {
 // a shard's work is done: wait for it, raise its device errors (unless the
 // shard's result copy already read its error word after a synchronisation),
 // and hand its kernel timings to the combining engine's profile
-static void ShardCollect(Engine &top, Engine &se, bool checked = false) {
+static void ShardCollect(Engine &top, Engine &se, int shard, bool checked = false) {
   if (!checked) {
     HIPCHK(hipStreamSynchronize(se.stream));
     CheckError(se);
@@ -3674,6 +3705,8 @@ static void ShardCollect(Engine &top, Engine &se, bool checked = false) {
     k.ms = ms;
     k.bytes = ev.bytes;
     k.rows = ev.rows;
+    k.shard = shard;
+    k.device = se.device;
     ks.push_back(k);
   }
   se.events.clear();
@@ -3836,13 +3869,287 @@ static void KeyBytes(const Value &v, std::string &out) {
   if (v.type.id == T_INTERVAL) out.append((const char *)&v.iv, sizeof(v.iv));
 }
 
+// One group's running merge of the shards' partials, per aggregate.
+struct ShardAcc {
+  int64_t cnt = 0;
+  bool has = false;
+  i128 si = 0;
+  double sd = 0;
+  Value mv;
+};
+
+// folds one partial row (get(col) = its column col) into the group's accumulators
+static void FoldPartial(const BoundSelect &s, const std::vector<int> &first, std::vector<ShardAcc> &accs,
+                        const std::function<Value(int)> &get) {
+  for (size_t q = 0; q < s.aggs.size(); q++) {
+    const AggSpec &a = s.aggs[q];
+    ShardAcc &A = accs[q];
+    const Value v = get(first[q]);
+    switch (a.kind) {
+      case A_COUNT_STAR:
+      case A_COUNT: A.cnt += (int64_t)v.i; break;
+      case A_SUM:
+        if (v.is_null) break;
+        A.has = true;
+        if (ClassOf(a.type) == VC_F64) A.sd += v.d;
+        else A.si += v.i;
+        break;
+      case A_MIN:
+      case A_MAX:
+        if (v.is_null) break;
+        if (!A.has || (a.kind == A_MIN ? CompareValues(v, A.mv) < 0 : CompareValues(v, A.mv) > 0)) A.mv = v;
+        A.has = true;
+        break;
+      case A_AVG: {
+        const Value n = get(first[q] + 1);
+        if (v.is_null) break;
+        A.has = true;
+        A.cnt += (int64_t)n.i;
+        if (ClassOf(SumTypeOf(a.arg->type)) == VC_F64) A.sd += v.d;
+        else A.si += v.i;
+        break;
+      }
+    }
+  }
+}
+
+// the merged group's aggregate values (AVG finished as the emit kernel does)
+static void FinishAccs(const BoundSelect &s, const std::vector<ShardAcc> &accs, std::vector<Value> &row) {
+  for (size_t q = 0; q < s.aggs.size(); q++) {
+    const AggSpec &a = s.aggs[q];
+    const ShardAcc &A = accs[q];
+    Value v = Value::Null(a.type);
+    switch (a.kind) {
+      case A_COUNT_STAR:
+      case A_COUNT: v = Value::Int(T_BIGINT, A.cnt); break;
+      case A_SUM:
+        if (!A.has) break;
+        v.is_null = false;
+        if (ClassOf(a.type) == VC_F64) v.d = A.sd;
+        else v.i = A.si;
+        break;
+      case A_MIN:
+      case A_MAX:
+        if (A.has) v = A.mv;
+        break;
+      case A_AVG: {
+        if (!A.has || A.cnt == 0) break;
+        if (ClassOf(SumTypeOf(a.arg->type)) == VC_F64) {
+          v = Value::Double(A.sd / (double)A.cnt);
+        } else {
+          double div = (double)A.cnt;
+          const int scale = a.arg->type.id == T_DECIMAL ? a.arg->type.scale : 0;
+          for (int k = 0; k < scale; k++) div *= 10.0;
+          v = Value::Double(I128ToDoubleLikeDevice(A.si) / div);
+        }
+        break;
+      }
+    }
+    row.push_back(v);
+  }
+}
+
+static Value LanesValue(const LogicalType &t, int64_t lo, int64_t hi, bool valid) {
+  if (!valid) return Value::Null(t);
+  Value v;
+  v.type = t;
+  v.is_null = false;
+  v.i = (i128)(((u128)(uint64_t)hi << 64) | (u128)(uint64_t)lo);
+  return v;
+}
+
+// mbx_combine=rccl: a sharded global aggregate whose partials are integers
+// (COUNT, SUM as HUGEINT / DECIMAL(38,s), integer MIN / MAX; AVG over
+// integers) is combined by RCCL on the shard devices: every shard packs its
+// one partial row into int64 lanes (combine.h) and takes part in one
+// collective on its own stream -- an ncclInt64 all-reduce when every partial
+// is a COUNT, else an all-gather finished by the carry-correct combine kernel
+// on device 0 -- and device 0's answer (with every rank's error word) comes
+// back in one small D2H.  false (the host merge runs instead, the reason in
+// shard_stats.rccl_note) for other shapes or without distinct devices.
+static bool ShardedAggregateRccl(Connection &c, const BoundSelect &s, const BoundSelect &p,
+                                 const std::vector<int> &first, std::vector<std::vector<Value>> &rows,
+                                 std::vector<LogicalType> &types) {
+  ShardStats &st = c.shard_stats;
+  if (!c.opts.combine_rccl) return false;
+  auto fallback = [&](const std::string &why) {
+    st.rccl_fallbacks++;
+    st.rccl_note = why;
+    return false;
+  };
+  if (!s.groups.empty()) return fallback("GROUP BY: host merge (the RCCL combine covers global aggregates)");
+  const int ncols = (int)p.aggs.size();
+  if (ncols < 1 || ncols > rc::kMaxCols) return fallback("partial row wider than the RCCL lane block");
+  rc::CombineDesc cd;
+  memset(&cd, 0, sizeof(cd));
+  bool counts_only = true;
+  for (int k = 0; k < ncols; k++) {
+    const AggSpec &a = p.aggs[k];
+    const VClass vc = ClassOf(a.type);
+    switch (a.kind) {
+      case A_COUNT_STAR:
+      case A_COUNT: cd.kind[k] = rc::K_SUM; break;
+      case A_SUM:
+        if (vc != VC_I64 && vc != VC_I128) return fallback("floating-point SUM: host merge");
+        cd.kind[k] = rc::K_SUM, counts_only = false;
+        break;
+      case A_MIN:
+      case A_MAX:
+        if ((vc != VC_I64 && vc != VC_I128) || PhysOf(a.type) == P_STR || PhysOf(a.type) == P_INTERVAL)
+          return fallback("non-integer MIN/MAX: host merge");
+        cd.kind[k] = a.kind == A_MIN ? rc::K_MIN : rc::K_MAX, counts_only = false;
+        break;
+      default: return fallback("aggregate without an integer partial: host merge");
+    }
+  }
+  if (!c.rccl_tried) {
+    c.rccl_tried = true;
+    std::string note;
+    c.rccl = rc::Open(c.opts.devices, &note);
+    if (!c.rccl) st.rccl_note = note;
+  }
+  if (!c.rccl) return fallback(st.rccl_note.empty() ? "RCCL unavailable" : st.rccl_note);
+  const Table &t = *s.src.table;
+  const int nsh = (int)t.parts.size();
+  const int P = rc::LanesPerRank(ncols, counts_only);
+  const size_t recv_lanes = counts_only ? (size_t)P : (size_t)nsh * P;
+  cd.ncols = ncols;
+  cd.nranks = nsh;
+  Engine &e = *c.engine;
+  std::vector<int64_t> host(recv_lanes + 3 * ncols);
+  double t_coll = 0;
+  ForShards(c, [&](int i) {
+    Connection &sc = *c.shards[i];
+    Engine &se = ShardEngine(c, sc);
+    BoundSelect pi = p;
+    pi.src.table = t.parts[i];
+    DRel r = RunBranch(se, sc, pi);
+    if (r.n != 1 || (int)r.cols.size() < ncols) ThrowError("Internal", "RCCL combine: partial row shape");
+    rc::PackDesc pd;
+    memset(&pd, 0, sizeof(pd));
+    for (int k = 0; k < ncols; k++) {
+      const DCol &d = r.cols[k];
+      if (d.phys == P_STR || d.phys == P_F32 || d.phys == P_F64 || d.phys == P_INTERVAL || !d.data)
+        ThrowError("Internal", "RCCL combine: partial column type");
+      pd.data[k] = d.data;
+      pd.valid[k] = d.validity;
+      pd.phys[k] = d.phys;
+    }
+    pd.ncols = ncols;
+    pd.counts_only = counts_only;
+    pd.err = se.d_err;
+    auto send = Alloc(se, (size_t)P * 8);
+    auto recv = Alloc(se, recv_lanes * 8);
+    rc::Pack(pd, (int64_t *)send->p, se.stream);
+    MarkLaunched(c, i);
+    const auto tc0 = std::chrono::steady_clock::now();
+    std::string err;
+    const bool ok = counts_only ? rc::AllReduceSum(*c.rccl, i, (const int64_t *)send->p, (int64_t *)recv->p, P,
+                                                   se.stream, &err)
+                                : rc::AllGather(*c.rccl, i, (const int64_t *)send->p, (int64_t *)recv->p, P,
+                                                se.stream, &err);
+    if (!ok) ThrowError("IO", err);
+    if (i == 0) {
+      DevBufPtr out;
+      if (!counts_only) {
+        out = Alloc(se, (size_t)3 * ncols * 8);
+        rc::Combine(cd, (const int64_t *)recv->p, (int64_t *)out->p, se.stream);
+      }
+      const size_t need = host.size() * 8;
+      if (!se.EnsurePinned(need)) ThrowError("IO", "RCCL combine: pinned staging");
+      HIPCHK(hipMemcpyAsync(se.h_pinned, recv->p, recv_lanes * 8, hipMemcpyDeviceToHost, se.stream));
+      if (out)
+        HIPCHK(hipMemcpyAsync(se.h_pinned + recv_lanes * 8, out->p, (size_t)3 * ncols * 8, hipMemcpyDeviceToHost,
+                              se.stream));
+      HIPCHK(hipStreamSynchronize(se.stream));  // every rank's part of the collective has landed
+      memcpy(host.data(), se.h_pinned, need);
+      t_coll = std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - tc0).count();
+    } else if (se.profile) {
+      HIPCHK(hipStreamSynchronize(se.stream));  // (the kernel events must have completed)
+    }
+    ShardCollect(e, se, i, true);
+  });
+  Eng(c);
+  const auto t_merge = std::chrono::steady_clock::now();
+  // every rank's device error word, raised as that shard's error
+  for (int i = 0; i < (counts_only ? 1 : nsh); i++) {
+    const int64_t err = host[(size_t)i * P + P - 1];
+    if (!err) continue;
+    if (counts_only) {  // the summed words only say some shard failed: ask each one
+      for (int k = 0; k < nsh; k++) {
+        Engine &se = Eng(*c.shards[k]);
+        try {
+          CheckError(se);
+        } catch (std::exception &ex) {
+          Eng(c);
+          throw EngineError(std::string(ex.what()) + " (shard " + std::to_string(k) + " of " + std::to_string(nsh) +
+                            ", device " + std::to_string(c.shards[k]->opts.device) + ")");
+        }
+      }
+      Eng(c);
+      ThrowError("Internal", "RCCL combine: a shard reported a device error");
+    }
+    Engine &se = Eng(*c.shards[i]);
+    HIPCHK(hipMemsetAsync(se.d_err, 0, sizeof(int32_t), se.stream));
+    HIPCHK(hipStreamSynchronize(se.stream));
+    Eng(c);
+    try {
+      RaiseDeviceError(e, (int32_t)err);
+    } catch (std::exception &ex) {
+      throw EngineError(std::string(ex.what()) + " (shard " + std::to_string(i) + " of " + std::to_string(nsh) +
+                        ", device " + std::to_string(c.shards[i]->opts.device) + ")");
+    }
+  }
+  // the combined partial row, then the aggregates finished as the host merge does
+  std::vector<Value> part(ncols);
+  for (int k = 0; k < ncols; k++) {
+    const LogicalType &pt = p.aggs[k].type;
+    if (counts_only) part[k] = Value::Int(T_BIGINT, (i128)host[k]);
+    else {
+      const int64_t *o = host.data() + recv_lanes + 3 * k;
+      part[k] = LanesValue(pt, o[0], o[1], o[2] & 1);
+    }
+  }
+  std::vector<ShardAcc> accs(s.aggs.size());
+  FoldPartial(s, first, accs, [&](int col) { return part[col]; });
+  types.clear();
+  for (auto &a : s.aggs) types.push_back(a.type);
+  rows.assign(1, std::vector<Value>());
+  FinishAccs(s, accs, rows[0]);
+  // each rank's partial row, as the host merge keeps them (all-gather only)
+  st.last_partials.clear();
+  if (!counts_only) {
+    for (int i = 0; i < nsh; i++) {
+      auto res = std::make_shared<MaterializedResult>();
+      res->nrows = 1;
+      for (int k = 0; k < ncols; k++) {
+        HostColumn hc;
+        hc.name = p.names[k];
+        hc.type = p.aggs[k].type;
+        hc.phys = PhysOf(hc.type);
+        const int64_t *x = host.data() + (size_t)i * P + 3 * k;
+        HostColumnPush(hc, LanesValue(hc.type, x[0], x[1], x[2] & 1));
+        res->cols.push_back(std::move(hc));
+      }
+      st.last_partials.push_back(res);
+    }
+  }
+  st.rccl_combines++;
+  st.rccl_note.clear();
+  st.last_rccl_us = t_coll;
+  st.last_combine_us = std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t_merge).count();
+  return true;
+}
+
 // The aggregate relation of a sharded aggregate branch (groups in key order,
 // then one column per aggregate) as host rows: every shard computes its
 // decomposable partials (one small D2H each, on its own worker thread), and
-// the host merges them by key exactly (int128 sums).
+// the host merges them by key exactly (int128 sums) -- or, with
+// mbx_combine=rccl, RCCL combines a global aggregate on the devices.
 static void ShardedAggregateRows(Connection &c, const BoundSelect &s, const BoundSelect &p,
                                  const std::vector<int> &first, std::vector<std::vector<Value>> &rows,
                                  std::vector<LogicalType> &types) {
+  if (ShardedAggregateRccl(c, s, p, first, rows, types)) return;
   const Table &t = *s.src.table;
   const int nsh = (int)t.parts.size(), ng = (int)s.groups.size();
   std::vector<ResultPtr> partial(nsh);
@@ -3853,25 +4160,20 @@ static void ShardedAggregateRows(Connection &c, const BoundSelect &s, const Boun
     BoundSelect pi = p;
     pi.src.table = t.parts[i];
     DRel r = RunBranch(se, sc, pi);
+    MarkLaunched(c, i);
     partial[i] = ToHost(se, r, pi.names, 0, -1, pi.names.size());  // synchronises and raises device errors
-    ShardCollect(e, se, true);
+    ShardCollect(e, se, i, true);
   });
   Eng(c);
+  c.shard_stats.last_partials = partial;
   const auto t_merge = std::chrono::steady_clock::now();
   // merge by group key, exactly (int128 sums)
-  struct Acc {
-    int64_t cnt = 0;
-    bool has = false;
-    i128 si = 0;
-    double sd = 0;
-    Value mv;
-  };
   size_t total_rows = 0;
   for (int i = 0; i < nsh; i++) total_rows += (size_t)partial[i]->nrows;
   std::unordered_map<std::string, size_t> index;
   index.reserve(total_rows * 2 + 1);
   std::vector<std::vector<Value>> keys;
-  std::vector<std::vector<Acc>> accs;
+  std::vector<std::vector<ShardAcc>> accs;
   keys.reserve(total_rows);
   accs.reserve(total_rows);
   std::string kb;
@@ -3894,36 +4196,7 @@ static void ShardedAggregateRows(Connection &c, const BoundSelect &s, const Boun
       } else {
         gi = it->second;
       }
-      for (size_t q = 0; q < s.aggs.size(); q++) {
-        const AggSpec &a = s.aggs[q];
-        Acc &A = accs[gi][q];
-        const Value v = m.cols[first[q]].Get(row);
-        switch (a.kind) {
-          case A_COUNT_STAR:
-          case A_COUNT: A.cnt += (int64_t)v.i; break;
-          case A_SUM:
-            if (v.is_null) break;
-            A.has = true;
-            if (ClassOf(a.type) == VC_F64) A.sd += v.d;
-            else A.si += v.i;
-            break;
-          case A_MIN:
-          case A_MAX:
-            if (v.is_null) break;
-            if (!A.has || (a.kind == A_MIN ? CompareValues(v, A.mv) < 0 : CompareValues(v, A.mv) > 0)) A.mv = v;
-            A.has = true;
-            break;
-          case A_AVG: {
-            const Value n = m.cols[first[q] + 1].Get(row);
-            if (v.is_null) break;
-            A.has = true;
-            A.cnt += (int64_t)n.i;
-            if (ClassOf(SumTypeOf(a.arg->type)) == VC_F64) A.sd += v.d;
-            else A.si += v.i;
-            break;
-          }
-        }
-      }
+      FoldPartial(s, first, accs[gi], [&](int col) { return m.cols[col].Get(row); });
     }
   }
   // groups in key order (NULL keys last), as the direct-index paths emit them
@@ -3945,38 +4218,7 @@ static void ShardedAggregateRows(Connection &c, const BoundSelect &s, const Boun
   rows.clear();
   for (size_t oi : order) {
     std::vector<Value> row = keys[oi];
-    for (size_t q = 0; q < s.aggs.size(); q++) {
-      const AggSpec &a = s.aggs[q];
-      const Acc &A = accs[oi][q];
-      Value v = Value::Null(a.type);
-      switch (a.kind) {
-        case A_COUNT_STAR:
-        case A_COUNT: v = Value::Int(T_BIGINT, A.cnt); break;
-        case A_SUM:
-          if (!A.has) break;
-          v.is_null = false;
-          if (ClassOf(a.type) == VC_F64) v.d = A.sd;
-          else v.i = A.si;
-          break;
-        case A_MIN:
-        case A_MAX:
-          if (A.has) v = A.mv;
-          break;
-        case A_AVG: {
-          if (!A.has || A.cnt == 0) break;
-          if (ClassOf(SumTypeOf(a.arg->type)) == VC_F64) {
-            v = Value::Double(A.sd / (double)A.cnt);
-          } else {
-            double div = (double)A.cnt;
-            const int scale = a.arg->type.id == T_DECIMAL ? a.arg->type.scale : 0;
-            for (int k = 0; k < scale; k++) div *= 10.0;
-            v = Value::Double(I128ToDoubleLikeDevice(A.si) / div);
-          }
-          break;
-        }
-      }
-      row.push_back(v);
-    }
+    FinishAccs(s, accs[oi], row);
     rows.push_back(std::move(row));
   }
   if (ng == 0 && rows.empty()) {  // a global aggregate always has one row
@@ -4065,7 +4307,8 @@ static DRel ShardedBranch(Engine &e, Connection &c, const BoundSelect &s) {
     si.limit = -1;
     si.offset = 0;
     parts[i] = RunBranch(se, sc, si);
-    ShardCollect(e, se);
+    MarkLaunched(c, i);
+    ShardCollect(e, se, i);
   });
   Eng(c);
   for (int i = 0; i < nsh; i++) parts[i] = MoveRelAsync(c, e, *c.shards[i]->engine, parts[i]);

@@ -1127,7 +1127,15 @@ __global__ __launch_bounds__((NL + 5) * 64) void select_rounds_kernel(SelectDesc
     return;
   }
   if (g != 0) return;
-  // workgroup 0: the rows after the last full step (guarded loads, 256 per pass), and the total
+  // workgroup 0: the rows after the last full step (guarded loads, 256 per pass), and the total.
+  // The zone map of the D.zmask outputs folds these rows too, whichever role
+  // (loaders or storers) folded the full steps: the host takes the map as the
+  // statistics of every selected row (DCol::zn = the total)
+  const uint32_t tzm = D.zstats ? (uint32_t)D.zmask & smask : 0u;
+  long long tmn[NC], tmx[NC];
+  uint32_t tnv[NC];
+#pragma unroll
+  for (int c = 0; c < NC; c++) tmn[c] = LLONG_MAX, tmx[c] = LLONG_MIN, tnv[c] = 0;
   int64_t tcnt = 0;
   for (int64_t base = nsteps * 256 * H; base < n; base += 256) {
     bool ok[4];
@@ -1159,7 +1167,44 @@ __global__ __launch_bounds__((NL + 5) * 64) void select_rounds_kernel(SelectDesc
       }
       pos++;
     }
+    if (tzm) {
+#pragma unroll
+      for (int c = 0; c < NC; c++) {
+        if (!((tzm >> c) & 1)) continue;
+        for (int e = 0; e < 4; e++) {
+          if (!ok[e]) continue;
+          const int64_t i = i0 + e;
+          const bool vz = !(VAL && D.col[c].valid) || ((D.col[c].valid[i >> 6] >> (i & 63)) & 1);
+          if (!vz) continue;
+          const long long x = D.col[c].w == 8 ? ((const int64_t *)D.col[c].data)[i]
+                                              : (long long)((const int32_t *)D.col[c].data)[i];
+          tmn[c] = x < tmn[c] ? x : tmn[c];
+          tmx[c] = x > tmx[c] ? x : tmx[c];
+          tnv[c]++;
+        }
+      }
+    }
     tcnt += __popcll(bb[0]) + __popcll(bb[1]) + __popcll(bb[2]) + __popcll(bb[3]);
+  }
+  if (tzm) {
+#pragma unroll
+    for (int c = 0; c < NC; c++) {
+      if (!((tzm >> c) & 1)) continue;
+      long long a = tmn[c], b = tmx[c];
+      uint32_t nz = tnv[c];
+#pragma unroll
+      for (int off = 32; off; off >>= 1) {
+        const long long a2 = __shfl_xor(a, off), b2 = __shfl_xor(b, off);
+        a = a2 < a ? a2 : a;
+        b = b2 > b ? b2 : b;
+        nz += __shfl_xor(nz, off);
+      }
+      if (lane == 0 && nz) {
+        atomicMin(&D.zstats[3 * c], a);
+        atomicMax(&D.zstats[3 * c + 1], b);
+        atomicAdd((unsigned long long *)&D.zstats[3 * c + 2], (unsigned long long)nz);
+      }
+    }
   }
   if (lane == 0) ctl[1] = (unsigned long long)(running + tcnt);
 }

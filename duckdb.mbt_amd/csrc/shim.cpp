@@ -22,6 +22,7 @@
 #include <string>
 
 #include "../../include/duckdb_mb.h"
+#include "combine.h"
 #include "engine.h"
 #include "jit.h"
 #include "knobs.h"
@@ -444,6 +445,9 @@ int32_t duckdb_mb_config_set(duckdb_mb_config *c, moonbit_bytes_t key, moonbit_b
   } else if (kl == "mbx_shard_rows") {
     ok = IsInt(v, &x) && x >= 0;
     if (ok) c->opts.shard_rows = x;
+  } else if (kl == "mbx_combine") {
+    ok = v == "host" || v == "rccl";
+    if (ok) c->opts.combine_rccl = v == "rccl";
   } else if (kl == "mbx_force_peer") {
     c->opts.force_peer = v == "true" || v == "1";
   } else if (kl == "mbx_profile") {
@@ -1614,8 +1618,9 @@ char *duckdb_mbx_profile_drain(duckdb_mb_connection *h) {
   for (size_t i = 0; i < h->conn.profile_history.size(); i++) {
     const auto &k = h->conn.profile_history[i];
     char buf[256];
-    snprintf(buf, sizeof(buf), "%s{\"name\":\"%s\",\"ms\":%.6f,\"bytes\":%.0f,\"rows\":%lld}", i ? "," : "",
-             k.name.c_str(), k.ms, k.bytes, (long long)k.rows);
+    snprintf(buf, sizeof(buf),
+             "%s{\"name\":\"%s\",\"ms\":%.6f,\"bytes\":%.0f,\"rows\":%lld,\"shard\":%d,\"device\":%d}",
+             i ? "," : "", k.name.c_str(), k.ms, k.bytes, (long long)k.rows, k.shard, k.device);
     j += buf;
   }
   j += "]";
@@ -1686,6 +1691,73 @@ int32_t duckdb_mbx_shard_stats(duckdb_mb_connection *h, int64_t *out6, double *o
     outd2[1] = st.last_combine_us;
   }
   return 6;
+}
+
+// The last sharded dispatch (ForShards), per shard: out[4 i .. 4 i + 3] =
+// {device, wake_us, launch_us, done_us}, times in us since the dispatch began
+// (the worker picked the job up; its plan and launches were queued; its
+// result reached the host, i.e. kernel + D2H + synchronisation).  Writes at
+// most cap shards; returns the shard count of that dispatch (0: none yet).
+int32_t duckdb_mbx_shard_timings(duckdb_mb_connection *h, double *out, int32_t cap) {
+  if (!h) return 0;
+  const auto &last = h->conn.shard_stats.last;
+  for (int32_t i = 0; out && i < cap && i < (int32_t)last.size(); i++) {
+    out[4 * i] = last[i].device;
+    out[4 * i + 1] = last[i].wake_us;
+    out[4 * i + 2] = last[i].launch_us;
+    out[4 * i + 3] = last[i].done_us;
+  }
+  return (int32_t)last.size();
+}
+
+// Shard i's partial aggregate relation of the last sharded aggregate (groups,
+// then the decomposed partials: COUNT, SUM as HUGEINT / DECIMAL(38,s) /
+// DOUBLE, MIN, MAX; AVG as SUM then COUNT), as it came back from its device
+// before the merge.  A result handle for the duckdb_mb_result_* accessors
+// (free with duckdb_mb_result_destroy); NULL if there is none.
+duckdb_mb_result *duckdb_mbx_shard_partial(duckdb_mb_connection *h, int32_t shard) {
+  if (!h || shard < 0 || shard >= (int32_t)h->conn.shard_stats.last_partials.size()) return nullptr;
+  const ResultPtr &p = h->conn.shard_stats.last_partials[shard];
+  if (!p) return nullptr;
+  auto *r = new duckdb_mb_result;
+  r->r = p;
+  return r;
+}
+
+// mbx_combine=rccl counters: out2 = {sharded aggregates RCCL combined,
+// requests that fell back to the host merge}; out_us1 = the last RCCL
+// combine's collective + D2H wall time on device 0 (us).  Either may be NULL.
+int32_t duckdb_mbx_rccl_stats(duckdb_mb_connection *h, int64_t *out2, double *out_us1) {
+  if (!h) return 0;
+  const ShardStats &st = h->conn.shard_stats;
+  if (out2) out2[0] = st.rccl_combines, out2[1] = st.rccl_fallbacks;
+  if (out_us1) out_us1[0] = st.last_rccl_us;
+  return 2;
+}
+
+// Why the last mbx_combine=rccl request fell back to the host merge ("" when
+// it ran); malloc'd, free with duckdb_mbx_free.
+char *duckdb_mbx_rccl_note(duckdb_mb_connection *h) {
+  return strdup(h ? h->conn.shard_stats.rccl_note.c_str() : "");
+}
+
+// Switches a connection's combine between the host merge (0) and RCCL (1), as
+// Config::set("mbx_combine", ...) at connect would.  Returns 1.
+int32_t duckdb_mbx_set_combine(duckdb_mb_connection *h, int32_t rccl) {
+  if (!h) return 0;
+  h->conn.opts.combine_rccl = rccl != 0;
+  return 1;
+}
+
+// The RCCL combine's lane arithmetic on the host (combine.h; CPU tests):
+// gathered = nranks x (3 ncols + 1) lanes, kinds[ncols] (0 sum, 1 min, 2 max);
+// out = 3 ncols lanes {lo, hi, non-NULL}.  Returns 1 (0: bad arguments).
+int32_t duckdb_mbx_combine_lanes(const int64_t *gathered, int32_t nranks, int32_t ncols, const int8_t *kinds,
+                                 int64_t *out) {
+  if (!gathered || !kinds || !out || nranks < 1 || ncols < 1 || ncols > rc::kMaxCols) return 0;
+  for (int j = 0; j < ncols; j++)
+    rc::CombineColumn(gathered, nranks, rc::LanesPerRank(ncols, false), j, kinds[j], out + 3 * j);
+  return 1;
 }
 
 // out3 = {select_rounds launches, aborts (a persistent workgroup was never

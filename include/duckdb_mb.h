@@ -291,6 +291,37 @@ int32_t duckdb_mbx_shard_stats(duckdb_mb_connection *connection, int64_t *out6, 
  * two-pass form ran instead)}.  Returns 3 (0: no handle). */
 int32_t duckdb_mbx_engine_stats(duckdb_mb_connection *connection, int64_t *out3);
 
+/* The last sharded dispatch, per shard i: out[4 i .. 4 i + 3] = {device,
+ * wake_us, launch_us, done_us}, us since the dispatch began (the worker took
+ * the job; its plan and launches were queued; its result reached the host:
+ * kernel + D2H + synchronisation).  At most cap shards are written; returns
+ * the dispatch's shard count (0: none yet). */
+int32_t duckdb_mbx_shard_timings(duckdb_mb_connection *connection, double *out, int32_t cap);
+
+/* Shard i's partial aggregate relation of the last sharded aggregate, as it
+ * left its device before the merge (groups, then COUNT / SUM / MIN / MAX
+ * partials; AVG as SUM then COUNT).  Read it with the duckdb_mb_result_*
+ * accessors and free it with duckdb_mb_result_destroy; NULL if none. */
+duckdb_mb_result *duckdb_mbx_shard_partial(duckdb_mb_connection *connection, int32_t shard);
+
+/* mbx_combine=rccl (Config::set key, ref src/duckdb_native.c:714-747): a
+ * sharded global aggregate over distinct devices is combined by RCCL on the
+ * shard devices (ncclInt64 all-reduce for COUNT-only rows; all-gather of int128
+ * lanes + a carry-correct combine on device 0 otherwise).  out2 = {RCCL
+ * combines, requests that fell back to the host merge}; out_us1 = the last
+ * combine's collective + D2H wall us.  Returns 2 (0: no handle). */
+int32_t duckdb_mbx_rccl_stats(duckdb_mb_connection *connection, int64_t *out2, double *out_us1);
+/* Why the last RCCL request fell back ("" if it ran); free with duckdb_mbx_free. */
+char *duckdb_mbx_rccl_note(duckdb_mb_connection *connection);
+/* 1: RCCL combine, 0: host merge, from the next statement on.  Returns 1. */
+int32_t duckdb_mbx_set_combine(duckdb_mb_connection *connection, int32_t rccl);
+/* The RCCL combine's lane arithmetic on the host (tests): gathered holds
+ * nranks x (3 ncols + 1) int64 lanes ({lo, hi, non-NULL} per column, then the
+ * rank's error word); kinds[j] = 0 sum / 1 min / 2 max; out = 3 ncols lanes.
+ * Returns 1 (0: bad arguments). */
+int32_t duckdb_mbx_combine_lanes(const int64_t *gathered, int32_t nranks, int32_t ncols, const int8_t *kinds,
+                                 int64_t *out);
+
 #ifdef __cplusplus
 }
 #endif

@@ -99,3 +99,63 @@ def test_under_launcher_does_not_respawn():
     assert p.returncode == 0, p.stderr[-2000:]
     assert "[launcher]" not in p.stderr
     assert _json_lines(p.stdout)[0]["n_gpus"] == 1
+
+
+@pytest.mark.parametrize("counts,world,ranks,form", [
+    ([8] * 8, 8, False, "in-library"),   # a full node visible to every rank
+    ([8, 1, 1, 1, 1, 1, 1, 1], 8, False, "in-library"),
+    ([1] * 8, 8, False, "ranks"),        # one device per rank (per-rank visibility)
+    ([2, 2], 4, False, "ranks"),
+    ([8] * 8, 8, True, "ranks"),         # --ranks asks for it
+    ([0, 1], 2, False, None),            # a rank without a GPU: no layout
+])
+def test_choose_form(counts, world, ranks, form):
+    import bench
+    f, reason = bench.choose_form(counts, world, ranks)
+    assert f == form, reason
+    assert reason
+
+
+def _torchrun(n, port, extra_env, *args):
+    env = dict(_bare_env(), **extra_env)
+    return subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+                           "--master-addr=127.0.0.1", f"--master-port={port}", os.path.join(ROOT, "bench.py")]
+                          + list(args), capture_output=True, text=True, timeout=180, env=env)
+
+
+@pytest.mark.parametrize("visible,form", [("2", "in-library"), ("1", "ranks")])
+def test_driver_launch_follows_device_visibility(visible, form):
+    """The driver's launch under the two visibilities an 8-GPU node can give:
+    every rank sees all devices (one process drives them in-library) or only
+    its own (one device per rank, RCCL combine); the choice, the counts and
+    the reason are in config.form and config.parallelism."""
+    p = _torchrun(2, 29573 if form == "ranks" else 29575, {"MBX_BENCH_VISIBLE_GPUS": visible},
+                  "--gpus", "2", "--dry-run")
+    assert p.returncode == 0, p.stderr[-2000:]
+    lines = _json_lines(p.stdout)
+    assert len(lines) == 1, p.stdout
+    d = lines[0]
+    assert d["mode"] == form and d["processes"] == 2 and d["rank_id_sum"] == 3
+    f = d["config"]["form"]
+    assert f["form"] == form and f["visible_devices_per_rank"] == [int(visible)] * 2
+    assert f["min"] == f["max"] == int(visible) and f["reason"]
+    if form == "ranks":
+        assert d["gpu_devices"] is None
+        assert "one process per GPU" in d["config"]["parallelism"]
+    else:
+        assert d["gpu_devices"] == [0, 1] and "in-library" in d["config"]["parallelism"]
+
+
+def test_driver_launch_without_gpus_fails_loudly():
+    p = _torchrun(2, 29577, {"MBX_BENCH_VISIBLE_GPUS": "0"}, "--gpus", "2", "--dry-run")
+    assert p.returncode != 0
+    assert "see no GPU" in p.stderr
+
+
+def test_gpus_1_is_unchanged():
+    p = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--dry-run"], capture_output=True,
+                       text=True, timeout=120, env=_bare_env())
+    assert p.returncode == 0, p.stderr[-2000:]
+    d = _json_lines(p.stdout)[0]
+    assert d["n_gpus"] == 1 and d["mode"] == "in-library" and d["gpu_devices"] == [0]
+    assert "form" not in d["config"]  # no vote without a launcher
