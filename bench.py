@@ -394,6 +394,7 @@ def run_inlib(args, world, rank, vote=None):
                       sel_rows=int(out[0]) if args.config == "sel" else None)
     if vote:
         result["config"]["form"] = vote
+    stuck = False
     if sstats:
         ms = elapsed / args.steps * 1e3
         md = {
@@ -409,7 +410,8 @@ def run_inlib(args, world, rank, vote=None):
         if shard_par is not None:
             md["shard_parity"] = shard_par
         if args.config in ("c2", "c2d", "c5"):
-            md["rccl_combine"] = rccl_leg(conn, step, args, w, n_total, plan)
+            md["rccl_combine"] = guarded(lambda: rccl_leg(conn, step, args, w, n_total, plan), RCCL_LEG_TIMEOUT_S)
+            stuck = md["rccl_combine"].get("error", "").startswith("timeout")
         result["multi_device"] = md
     calibrate_into(conn, result, args.config)
     if args.config == "sel":
@@ -431,14 +433,46 @@ def run_inlib(args, world, rank, vote=None):
     if dist:
         dist.barrier()
         dist.destroy_process_group()
-    conn.close()
+    if not stuck:
+        conn.close()
     print(json.dumps(result), flush=True)
     bad = not result["parity"].get("match", True) or (shard_par and not all(p["match"] for p in shard_par))
     if bad:
         log("[bench] PARITY FAILURE: " + json.dumps(result["parity"]) +
             (" shards: " + json.dumps([p for p in shard_par if not p["match"]]) if shard_par else ""))
+    if stuck:
+        # the RCCL leg's thread is still inside a collective: the headline line
+        # is out, so leave without joining it (interpreter teardown would wait)
+        log("[bench] RCCL combine leg did not finish; exiting without closing the connection")
+        sys.stdout.flush()
+        sys.stderr.flush()
+        os._exit(3 if bad else 0)
+    if bad:
         raise SystemExit(3)
     return result
+
+
+RCCL_LEG_TIMEOUT_S = float(os.environ.get("MBX_BENCH_RCCL_TIMEOUT_S", "120"))
+
+
+def guarded(fn, timeout_s):
+    """fn() on a daemon thread, given timeout_s seconds: its dict, an {"error"}
+    dict if it raised, or {"error": "timeout ..."} if it is still running (a
+    collective that never completes must not cost the headline line)."""
+    import threading
+    box = {}
+
+    def run():
+        try:
+            box["r"] = fn()
+        except Exception as ex:  # noqa: BLE001
+            box["r"] = {"error": str(ex)}
+    th = threading.Thread(target=run, daemon=True)
+    th.start()
+    th.join(timeout_s)
+    if th.is_alive():
+        return {"error": f"timeout: the leg did not finish within {timeout_s:.0f} s"}
+    return box["r"]
 
 
 def fail(dist, msg):

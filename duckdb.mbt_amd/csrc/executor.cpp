@@ -3573,7 +3573,12 @@ static void AppendCast(Engine &e, Table &t, DRel r, const std::vector<int> &col_
 // variable.  Each worker keeps its shard's device current (HIP's current
 // device and the scratch allocator are per thread).
 struct ShardWorkers {
-  static constexpr int kSpinUs = 300;
+  // MBX_SHARD_SPIN_US (0 = sleep at once): with 8 shards, 7 spinning workers
+  // compete with the host merge and the appender's copy threads
+  const int kSpinUs = [] {
+    const char *e = Knob("MBX_SHARD_SPIN_US");
+    return e ? atoi(e) : 300;
+  }();
   const int n;
   std::vector<std::thread> th;
   std::mutex mu;

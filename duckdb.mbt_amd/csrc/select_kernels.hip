@@ -510,6 +510,10 @@ __device__ __forceinline__ void sr_copy_sent(const TS *st, uint32_t t0w, uint32_
       }
     }
     if (mode != 2) {
+      // vd = D.vdst[o] + pos with pos any prefix count, so this dword store is
+      // generally not 4-byte aligned: it relies on the unaligned global access
+      // mode the ROCm runtime configures for gfx9 (SH_MEM_CONFIG alignment_mode
+      // UNALIGNED, ROCm's default); MBX_SR_COPY1=2 is the byte-store form
       const int q = lane >> 4;
       const unsigned long long bw = q == 0 ? bal[0] : q == 1 ? bal[1] : q == 2 ? bal[2] : bal[3];
       const uint32_t nib = (uint32_t)(bw >> ((4 * lane) & 63)) & 0xFu;

@@ -159,3 +159,17 @@ def test_gpus_1_is_unchanged():
     d = _json_lines(p.stdout)[0]
     assert d["n_gpus"] == 1 and d["mode"] == "in-library" and d["gpu_devices"] == [0]
     assert "form" not in d["config"]  # no vote without a launcher
+
+
+def test_guarded_leg_times_out_and_reports():
+    """The RCCL leg runs under a watchdog: a leg that never returns becomes an
+    {"error": "timeout ..."} entry instead of hanging the headline line."""
+    import threading
+    import bench
+    ev = threading.Event()
+    r = bench.guarded(lambda: ev.wait(30) and {"ok": 1}, 0.2)
+    assert r["error"].startswith("timeout")
+    ev.set()
+    assert bench.guarded(lambda: {"ok": 1}, 5) == {"ok": 1}
+    r = bench.guarded(lambda: 1 // 0, 5)
+    assert "division" in r["error"]

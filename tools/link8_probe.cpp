@@ -117,6 +117,36 @@ int main(int argc, char **argv) {
       }
     });
   };
+  // the same pipeline with the chunk landings signalled by the stream itself:
+  // after each chunk's DMA, hipStreamWriteValue32 stores the call's generation
+  // into a coherent pinned flag, and the copy threads spin on plain loads of
+  // their flags (no event queries).  per_thread: thread t copies chunks t,
+  // t+T, ... whole; else every thread copies its slice of every chunk.
+  unsigned *flags = nullptr;
+  CK(hipHostMalloc((void **)&flags, 64 * sizeof(unsigned), hipHostMallocCoherent));
+  memset(flags, 0, 64 * sizeof(unsigned));
+  unsigned fgen = 0;
+  auto flagged = [&](Team &t, unsigned char *dst, size_t CHK, bool per_thread) {
+    const size_t nch = (n + CHK - 1) / CHK;
+    const unsigned g = ++fgen;
+    for (size_t c = 0; c < nch; c++) {
+      CK(hipMemcpyAsync(pin + c * CHK, (char *)d + c * CHK, std::min(CHK, n - c * CHK), hipMemcpyDeviceToHost, s));
+      CK(hipStreamWriteValue32(s, flags + c, g, 0));
+    }
+    t.Run([&](int i) {
+      for (size_t c = per_thread ? i : 0; c < nch; c += per_thread ? t.n : 1) {
+        while (__atomic_load_n(flags + c, __ATOMIC_ACQUIRE) != g) __builtin_ia32_pause();
+        const size_t len = std::min(CHK, n - c * CHK);
+        if (per_thread) {
+          memcpy(dst + c * CHK, pin + c * CHK, len);
+          continue;
+        }
+        size_t part = (len / t.n + 4095) & ~(size_t)4095;
+        size_t b = (size_t)i * part;
+        if (b < len) memcpy(dst + c * CHK + b, pin + c * CHK + b, std::min(part, len - b));
+      }
+    });
+  };
   struct V {
     const char *name;
     std::function<void(unsigned char *)> f;
@@ -175,6 +205,12 @@ int main(int argc, char **argv) {
       {"fine 16 chunks, 8 thr", [&](unsigned char *dst) { fine(team8, dst, n / 16); }},
       {"fine 32 chunks, 8 thr", [&](unsigned char *dst) { fine(team8, dst, n / 32); }},
       {"fine 16 chunks, 4 thr", [&](unsigned char *dst) { fine(team4, dst, n / 16); }},
+      {"flag 8 chunks, 8 thr slices", [&](unsigned char *dst) { flagged(team8, dst, n / 8, false); }},
+      {"flag 16 chunks, 8 thr slices", [&](unsigned char *dst) { flagged(team8, dst, n / 16, false); }},
+      {"flag 8 chunks, 8 thr whole", [&](unsigned char *dst) { flagged(team8, dst, n / 8, true); }},
+      {"flag 16 chunks, 8 thr whole", [&](unsigned char *dst) { flagged(team8, dst, n / 16, true); }},
+      {"flag 32 chunks, 8 thr whole", [&](unsigned char *dst) { flagged(team8, dst, n / 32, true); }},
+      {"flag 16 chunks, 4 thr whole", [&](unsigned char *dst) { flagged(team4, dst, n / 16, true); }},
   };
   for (int alloc = 0; alloc < 2; alloc++) {
     for (auto &v : vs) {

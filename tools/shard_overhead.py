@@ -73,9 +73,37 @@ def main():
                            "last_dispatch_us": st.get("last_dispatch_us"),
                            "last_host_merge_us": st.get("last_combine_us"),
                            "host_results": st.get("host_results")}
+            if k > 1:
+                res[str(k)]["split_us"] = split(conn, sql)
             conn.close()
         out["queries"][sql] = res
     print(json.dumps(out), flush=True)
+
+
+def split(conn, sql, iters=400):
+    """Median over `iters` queries of where a sharded dispatch's time goes
+    (duckdb_mbx_shard_timings / shard_stats): the slowest worker's wake-up,
+    the last shard's launches queued, the last shard's partial on the host
+    (its D2H + synchronisation), the whole dispatch, and the host merge after
+    it; wall = the query's wall time through the C-ABI."""
+    keys = ("wake_max", "launch_max", "done_max", "done_min", "dispatch", "merge", "wall")
+    rows = {k: [] for k in keys}
+    for _ in range(iters):
+        t0 = time.perf_counter()
+        r = conn.query_raw(sql)
+        r.value(0, 0)
+        r.close()
+        wall = (time.perf_counter() - t0) * 1e6
+        tm = conn.shard_timings()
+        st = conn.shard_stats()
+        rows["wake_max"].append(max(t["wake_us"] for t in tm))
+        rows["launch_max"].append(max(t["launch_us"] for t in tm))
+        rows["done_max"].append(max(t["done_us"] for t in tm))
+        rows["done_min"].append(min(t["done_us"] for t in tm))
+        rows["dispatch"].append(st["last_dispatch_us"])
+        rows["merge"].append(st["last_combine_us"])
+        rows["wall"].append(wall)
+    return {k: round(statistics.median(v), 2) for k, v in rows.items()}
 
 
 if __name__ == "__main__":
