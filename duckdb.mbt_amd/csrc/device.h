@@ -365,6 +365,7 @@ struct SelectDesc {
   long long *zstats;
   int32_t zmask;
   int32_t zstore;  // 1: the storers fold the zone maps while copying, 0: the loaders
+  int32_t nt_off;  // select_rounds storers (MBX_SR_NT_OFF, A/B): bit 0 = plain value stores, bit 1 = plain validity stores (default: non-temporal)
   int32_t copy1;   // select_rounds storers (MBX_SR_COPY1, A/B): 0 = 4 rows per lane per pass, 1 = one, 2 = 4 with byte validity stores
   unsigned long long *dbg;     // nullptr, or 9 counters (MBX_SL_DEBUG) / 13 (MBX_SR_DEBUG)
   unsigned long long *dbg_ts;  // MBX_SR_DEBUG=2: s_memrealtime of every (round, workgroup) publish

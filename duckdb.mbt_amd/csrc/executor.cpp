@@ -1111,7 +1111,8 @@ static bool TrySelectOnePass(Engine &e, const DRel &rel, const dev::FilterMultiD
   const bool narrow_ok = !(nenv && atoi(nenv) == 0);
   const char *senv = Knob("MBX_SR_SENT");  // MBX_SR_SENT=0: NULL-able outputs stage validity bytes (A/B)
   const bool sent_off = senv && atoi(senv) == 0;
-  if (const char *c1 = Knob("MBX_SR_COPY1")) S.copy1 = atoi(c1);  // storers: 1 = one row per lane per pass, 2 = byte validity stores (A/B)
+  if (const char *c1 = Knob("MBX_SR_COPY1")) S.copy1 = atoi(c1);
+  if (const char *nt = Knob("MBX_SR_NT_OFF")) S.nt_off = atoi(nt);  // storers: 1 = plain value stores, 2 = plain validity stores (A/B)  // storers: 1 = one row per lane per pass, 2 = byte validity stores (A/B)
   for (auto &x : exprs) {
     const DCol &c = rel.cols[x->col];
     if (c.validity && (mode == 2 || (uintptr_t)c.validity % 16)) return false;
@@ -4146,6 +4147,79 @@ static bool ShardedAggregateRccl(Connection &c, const BoundSelect &s, const Boun
   return true;
 }
 
+// The host merge when every group key is an integer-like column (the C3
+// shape): the partial rows are keyed by their raw int128 keys (NULL last, as
+// the direct-index paths order them), sorted once, and each run of equal keys
+// folded -- no per-row key strings, hash map or Value keys (8 shards x 32
+// groups: see profiles/r04_shard_overhead*.json).  false for other key types
+// (VARCHAR, floating point, INTERVAL) or more than two keys.
+static bool MergeIntKeys(const BoundSelect &s, const std::vector<int> &first, const std::vector<ResultPtr> &partial,
+                         int ng, std::vector<std::vector<Value>> &rows, std::vector<LogicalType> &types) {
+  if (ng < 1 || ng > 2) return false;
+  for (const auto &m : partial)
+    for (int g = 0; g < ng; g++) {
+      const Phys p = m->cols[g].phys;
+      if (p == P_STR || p == P_F32 || p == P_F64 || p == P_INTERVAL) return false;
+    }
+  struct Ent {
+    i128 k[2];
+    uint8_t nul[2];
+    int32_t shard;
+    int64_t row;
+  };
+  std::vector<Ent> ents;
+  size_t total = 0;
+  for (const auto &m : partial) total += (size_t)m->nrows;
+  ents.reserve(total);
+  for (int i = 0; i < (int)partial.size(); i++) {
+    const MaterializedResult &m = *partial[i];
+    for (int64_t row = 0; row < m.nrows; row++) {
+      Ent e;
+      e.k[1] = 0;
+      e.nul[1] = 0;
+      for (int g = 0; g < ng; g++) {
+        const HostColumn &hc = m.cols[g];
+        e.nul[g] = hc.IsNull(row);
+        e.k[g] = e.nul[g] ? 0 : hc.Get(row).i;
+      }
+      e.shard = i;
+      e.row = row;
+      ents.push_back(e);
+    }
+  }
+  auto less = [&](const Ent &a, const Ent &b) {
+    for (int g = 0; g < ng; g++) {
+      if (a.nul[g] != b.nul[g]) return b.nul[g] != 0;  // NULL keys last
+      if (!a.nul[g] && a.k[g] != b.k[g]) return a.k[g] < b.k[g];
+    }
+    return false;
+  };
+  std::stable_sort(ents.begin(), ents.end(), less);
+  types.clear();
+  for (auto &g : s.groups) types.push_back(g->type);
+  for (auto &a : s.aggs) types.push_back(a.type);
+  rows.clear();
+  std::vector<ShardAcc> accs(s.aggs.size());
+  for (size_t i = 0; i < ents.size();) {
+    size_t j = i;
+    for (auto &a : accs) a = ShardAcc();
+    while (j < ents.size() && !less(ents[i], ents[j])) {
+      const MaterializedResult &m = *partial[ents[j].shard];
+      const int64_t row = ents[j].row;
+      FoldPartial(s, first, accs, [&](int col) { return m.cols[col].Get(row); });
+      j++;
+    }
+    std::vector<Value> out;
+    out.reserve(ng + s.aggs.size());
+    const MaterializedResult &m0 = *partial[ents[i].shard];
+    for (int g = 0; g < ng; g++) out.push_back(m0.cols[g].Get(ents[i].row));
+    FinishAccs(s, accs, out);
+    rows.push_back(std::move(out));
+    i = j;
+  }
+  return true;
+}
+
 // The aggregate relation of a sharded aggregate branch (groups in key order,
 // then one column per aggregate) as host rows: every shard computes its
 // decomposable partials (one small D2H each, on its own worker thread), and
@@ -4172,6 +4246,11 @@ static void ShardedAggregateRows(Connection &c, const BoundSelect &s, const Boun
   Eng(c);
   c.shard_stats.last_partials = partial;
   const auto t_merge = std::chrono::steady_clock::now();
+  if (MergeIntKeys(s, first, partial, ng, rows, types)) {
+    c.shard_stats.last_combine_us =
+        std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t_merge).count();
+    return;
+  }
   // merge by group key, exactly (int128 sums)
   size_t total_rows = 0;
   for (int i = 0; i < nsh; i++) total_rows += (size_t)partial[i]->nrows;

@@ -28,10 +28,14 @@
 #include <sys/mman.h>
 
 #include <algorithm>
+#include <atomic>
+#include <chrono>
 #include <condition_variable>
 #include <cstdint>
 #include <cstdlib>
 #include <cstring>
+#include <functional>
+#include <memory>
 #include <mutex>
 #include <thread>
 #include <vector>
@@ -194,6 +198,183 @@ void AdviseHuge(void *p, size_t n) {
   if (e > b) (void)madvise((void *)b, e - b, MADV_HUGEPAGE);
 }
 
+// ---------------------------------------------------------------------------
+// Mid-size copies (2 MiB up to the pool's 32 MiB; the reference's getters hand
+// out 8 MB per 1e6-row INT64 slice, duckdb_native.c:2392-2422).  At this size
+// the per-call machinery is the limit, and which method wins depends on the
+// box's host side, 2-3x apart between boxes of the same pool for the same
+// method (profiles/r03_link8_probe*.log, r04_link8_probe_flags.log):
+//   M_RUNTIME  the runtime's pageable copy (its own staging),
+//   M_REGISTER page-lock the destination (hipHostRegister), one DMA straight
+//              into it, unregister,
+//   M_BOUNCE   one DMA into a per-device pinned bounce, then T host threads
+//              copy their slices out (threads spin between calls, then sleep).
+// So the library measures: per device and power-of-two size class, the first
+// calls rotate through the methods, each timed end to end, and the class then
+// keeps the method with the best median; every kReprobe calls one call tries
+// another method again.  The bytes are the same whichever method runs.
+// MBX_LINK_MID=0 keeps the runtime's copy; MBX_LINK_MID_MODE=0|1|2 pins one.
+enum MidMethod { M_RUNTIME = 0, M_REGISTER = 1, M_BOUNCE = 2, M_COUNT = 3 };
+
+class SpinTeam {  // T-1 helper threads + the caller; helpers spin kSpinUs after a job, then sleep
+ public:
+  explicit SpinTeam(int t) : n_(t) {
+    for (int i = 1; i < n_; i++) std::thread([this, i] { Loop(i); }).detach();
+  }
+  void Run(const std::function<void(int)> &f) {
+    job_ = &f;
+    left_.store(n_ - 1, std::memory_order_release);
+    {
+      std::lock_guard<std::mutex> g(mu_);
+      gen_.fetch_add(1, std::memory_order_acq_rel);
+    }
+    if (sleepers_.load(std::memory_order_acquire)) cv_.notify_all();
+    f(0);
+    while (left_.load(std::memory_order_acquire) > 0) __builtin_ia32_pause();
+  }
+  int size() const { return n_; }
+
+ private:
+  static constexpr int kSpinUs = 2000;
+  void Loop(int i) {
+    uint64_t seen = 0;
+    for (;;) {
+      const auto t0 = std::chrono::steady_clock::now();
+      int k = 0;
+      while (gen_.load(std::memory_order_acquire) == seen) {
+        if ((++k & 255) == 0 && std::chrono::steady_clock::now() - t0 > std::chrono::microseconds(kSpinUs)) {
+          std::unique_lock<std::mutex> lk(mu_);
+          sleepers_.fetch_add(1);
+          cv_.wait(lk, [&] { return gen_.load(std::memory_order_acquire) != seen; });
+          sleepers_.fetch_sub(1);
+          break;
+        }
+        __builtin_ia32_pause();
+      }
+      seen = gen_.load(std::memory_order_acquire);
+      (*job_)(i);
+      left_.fetch_sub(1, std::memory_order_acq_rel);
+    }
+  }
+  const int n_;
+  std::atomic<uint64_t> gen_{0};
+  std::atomic<int> left_{0}, sleepers_{0};
+  const std::function<void(int)> *job_ = nullptr;
+  std::mutex mu_;
+  std::condition_variable cv_;
+};
+
+class MidLink {
+ public:
+  MidLink() {}
+
+  std::string Copy(void *dst, const void *src, size_t n, int forced) {
+    std::lock_guard<std::mutex> call(mu_);
+    int cls = 0;  // 2-4 MiB: 0, 4-8: 1, 8-16: 2, 16-32: 3
+    for (size_t q = n >> 21; q > 1 && cls < kClasses - 1; q >>= 1) cls++;
+    Class &C = cls_[cls];
+    int m = forced >= 0 && forced < M_COUNT ? forced : Pick(C);
+    const auto t0 = std::chrono::steady_clock::now();
+    std::string err = Run(m, dst, src, n);
+    if (!err.empty() && m != M_RUNTIME) {  // a method the box refuses (e.g. registration): never again here
+      C.broken[m] = true;
+      m = M_RUNTIME;
+      err = Run(m, dst, src, n);
+    }
+    const double us = std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0).count();
+    if (err.empty()) C.Record(m, n / us);
+    return err;
+  }
+
+ private:
+  static constexpr int kClasses = 4, kTrials = 3, kReprobe = 64;
+  struct Class {
+    std::vector<double> gbs[M_COUNT];  // (bytes/us = MB/s; only the order matters)
+    bool broken[M_COUNT] = {false, false, false};
+    uint64_t calls = 0;
+    int best = -1;
+    void Record(int m, double rate) {
+      auto &v = gbs[m];
+      v.push_back(rate);
+      if (v.size() > 16) v.erase(v.begin());
+      double bm = -1;
+      best = -1;
+      for (int k = 0; k < M_COUNT; k++) {
+        if (broken[k] || gbs[k].size() < (size_t)kTrials) continue;
+        std::vector<double> s = gbs[k];
+        std::nth_element(s.begin(), s.begin() + s.size() / 2, s.end());
+        if (s[s.size() / 2] > bm) bm = s[s.size() / 2], best = k;
+      }
+    }
+  };
+  int Pick(Class &C) {
+    const uint64_t k = C.calls++;
+    for (int m = 0; m < M_COUNT; m++)  // the trial phase: round-robin until every method has kTrials samples
+      if (!C.broken[(k + m) % M_COUNT] && C.gbs[(k + m) % M_COUNT].size() < (size_t)kTrials) return (int)((k + m) % M_COUNT);
+    if (C.best >= 0 && k % kReprobe == kReprobe - 1) {  // now and then re-time another method
+      const int o = (int)((C.best + 1 + (k / kReprobe) % (M_COUNT - 1)) % M_COUNT);
+      if (!C.broken[o]) return o;
+    }
+    return C.best >= 0 ? C.best : M_RUNTIME;
+  }
+  std::string Run(int m, void *dst, const void *src, size_t n) {
+    if (m == M_REGISTER) {
+      const uintptr_t pg = 4096, b = (uintptr_t)dst & ~(pg - 1), e = ((uintptr_t)dst + n + pg - 1) & ~(pg - 1);
+      hipError_t r = hipHostRegister((void *)b, e - b, hipHostRegisterDefault);
+      if (r != hipSuccess) {
+        (void)hipGetLastError();
+        return HipErr(r, "LinkD2H hipHostRegister");
+      }
+      hipError_t c = hipMemcpy(dst, src, n, hipMemcpyDeviceToHost);
+      r = hipHostUnregister((void *)b);
+      if (c != hipSuccess) return HipErr(c, "LinkD2H registered copy");
+      return r == hipSuccess ? "" : HipErr(r, "LinkD2H hipHostUnregister");
+    }
+    if (m == M_BOUNCE) {
+      if (n > bounce_n_) {
+        if (bounce_) (void)hipHostFree(bounce_);
+        bounce_ = nullptr;
+        bounce_n_ = 0;
+        size_t b = (size_t)4 << 20;
+        while (b < n) b <<= 1;
+        hipError_t r = hipHostMalloc((void **)&bounce_, b, hipHostMallocDefault);
+        if (r != hipSuccess) return HipErr(r, "LinkD2H bounce allocation");
+        bounce_n_ = b;
+        if (!stream_ && hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking) != hipSuccess)
+          return "HIP error: LinkD2H bounce stream";
+      }
+      hipError_t r = hipMemcpyAsync(bounce_, src, n, hipMemcpyDeviceToHost, stream_);
+      if (r == hipSuccess) r = hipStreamSynchronize(stream_);
+      if (r != hipSuccess) return HipErr(r, "LinkD2H bounce DMA");
+      if (!team_) team_.reset(new SpinTeam(8));
+      const int T = team_->size();
+      const size_t part = (n / T + 4095) & ~(size_t)4095;
+      team_->Run([&](int i) {
+        const size_t o = (size_t)i * part;
+        if (o < n) memcpy((uint8_t *)dst + o, bounce_ + o, std::min(part, n - o));
+      });
+      return "";
+    }
+    hipError_t e = hipMemcpy(dst, src, n, hipMemcpyDeviceToHost);
+    return e == hipSuccess ? "" : HipErr(e, "LinkD2H hipMemcpy");
+  }
+  std::mutex mu_;
+  Class cls_[kClasses];
+  uint8_t *bounce_ = nullptr;
+  size_t bounce_n_ = 0;
+  hipStream_t stream_ = nullptr;
+  std::unique_ptr<SpinTeam> team_;
+};
+
+MidLink *g_mid[64] = {};  // never freed, as the pools
+
+MidLink *Mid(int device) {
+  if (device < 0 || device >= 64) return nullptr;
+  std::lock_guard<std::mutex> lk(g_pools_mu);
+  if (!g_mid[device]) g_mid[device] = new MidLink();
+  return g_mid[device];
+}
+
 }  // namespace
 
 std::string LinkD2H(int device, void *dst, const void *src, size_t n) {
@@ -202,6 +383,10 @@ std::string LinkD2H(int device, void *dst, const void *src, size_t n) {
   const long min_bytes = std::max(1, EnvInt("MBX_LINK_MIN", kFreshBytes));
   const bool huge = EnvInt("MBX_LINK_HUGE", 1) != 0;
   if (n == 0) return "";
+  if ((long)n < min_bytes && n >= (size_t)2 << 20 && EnvInt("MBX_LINK_MID", 1) != 0) {
+    MidLink *mid = Mid(device);
+    if (mid) return mid->Copy(dst, src, n, EnvInt("MBX_LINK_MID_MODE", -1));
+  }
   LinkPool *pool = threads > 0 && (long)n >= min_bytes ? Pool(device, threads) : nullptr;
   if (!pool) {
     hipError_t e = hipMemcpy(dst, src, n, hipMemcpyDeviceToHost);

@@ -464,18 +464,27 @@ __device__ __forceinline__ unsigned long long lds_add_rtn(unsigned long long *p,
 // A storer's copy of staged rows t0w .. t0w + c - 1 (ring positions & mask) to
 // dst[0 .. c): 4 rows per lane per pass, so the 4 staging reads share one LDS
 // wait.
+// a storer's output store: non-temporal by default (the rows are written once
+// and not read back by this kernel); MBX_SR_NT_OFF makes them plain (A/B)
+template <typename T>
+__device__ __forceinline__ void sr_store(T v, T *p, bool nt) {
+  if (nt) __builtin_nontemporal_store(v, p);
+  else *p = v;
+}
+
 template <typename TS, typename TD>
 __device__ __forceinline__ void sr_copy(const TS *st, uint32_t t0w, uint32_t mask, uint32_t c, int lane, TD *dst,
-                                        int mode) {
+                                        int mode, int nt_off) {
+  const bool nt = !(nt_off & 1);
   uint32_t i = lane;
   for (; mode != 1 && i + 192 < c; i += 256) {
     TS x[4];
 #pragma unroll
     for (int u = 0; u < 4; u++) x[u] = st[(t0w + i + 64 * u) & mask];
 #pragma unroll
-    for (int u = 0; u < 4; u++) __builtin_nontemporal_store((TD)x[u], dst + i + 64 * u);
+    for (int u = 0; u < 4; u++) sr_store((TD)x[u], dst + i + 64 * u, nt);
   }
-  for (; i < c; i += 64) __builtin_nontemporal_store((TD)st[(t0w + i) & mask], dst + i);
+  for (; i < c; i += 64) sr_store((TD)st[(t0w + i) & mask], dst + i, nt);
 }
 
 // A storer's copy of a sentinel-staged NULL-able output (SelectDesc::col
@@ -484,7 +493,8 @@ __device__ __forceinline__ void sr_copy(const TS *st, uint32_t t0w, uint32_t mas
 template <typename TS, typename TD, bool Z>
 __device__ __forceinline__ void sr_copy_sent(const TS *st, uint32_t t0w, uint32_t mask, uint32_t c, int lane, TD *dst,
                                              uint8_t *vd, TS sent, long long &mn, long long &mx, uint32_t &nv,
-                                             int mode) {
+                                             int mode, int nt_off) {
+  const bool ntv = !(nt_off & 1), ntb = !(nt_off & 2);
   uint32_t b = 0;
   // whole passes of 256 rows, 4 per lane (rows b + lane + 64 u): the 4 staging
   // reads share one LDS wait.  The validity of the pass comes back as 4 ballots
@@ -500,8 +510,8 @@ __device__ __forceinline__ void sr_copy_sent(const TS *st, uint32_t t0w, uint32_
 #pragma unroll
     for (int u = 0; u < 4; u++) {
       const bool ok = x[u] != sent;
-      __builtin_nontemporal_store((TD)(ok ? x[u] : (TS)0), dst + b + lane + 64 * u);
-      if (mode == 2) __builtin_nontemporal_store((uint8_t)ok, vd + b + lane + 64 * u);
+      sr_store((TD)(ok ? x[u] : (TS)0), dst + b + lane + 64 * u, ntv);
+      if (mode == 2) sr_store((uint8_t)ok, vd + b + lane + 64 * u, ntb);
       bal[u] = __ballot(ok);
       if constexpr (Z) {
         mn = ok && (long long)x[u] < mn ? (long long)x[u] : mn;
@@ -517,14 +527,14 @@ __device__ __forceinline__ void sr_copy_sent(const TS *st, uint32_t t0w, uint32_
       const int q = lane >> 4;
       const unsigned long long bw = q == 0 ? bal[0] : q == 1 ? bal[1] : q == 2 ? bal[2] : bal[3];
       const uint32_t nib = (uint32_t)(bw >> ((4 * lane) & 63)) & 0xFu;
-      __builtin_nontemporal_store((nib * 0x00204081u) & 0x01010101u, (uint32_t *)(vd + b + 4 * lane));
+      sr_store((nib * 0x00204081u) & 0x01010101u, (uint32_t *)(vd + b + 4 * lane), ntb);
     }
   }
   for (uint32_t i = b + lane; i < c; i += 64) {
     const TS x = st[(t0w + i) & mask];
     const bool ok = x != sent;
-    __builtin_nontemporal_store((TD)(ok ? x : (TS)0), dst + i);
-    __builtin_nontemporal_store((uint8_t)ok, vd + i);
+    sr_store((TD)(ok ? x : (TS)0), dst + i, ntv);
+    sr_store((uint8_t)ok, vd + i, ntb);
     if constexpr (Z) {
       mn = ok && (long long)x < mn ? (long long)x : mn;
       mx = ok && (long long)x > mx ? (long long)x : mx;
@@ -947,16 +957,16 @@ __global__ __launch_bounds__((NL + 5) * 64) void select_rounds_kernel(SelectDesc
             uint8_t *vd = D.vdst[o] + pos;
             if (s8) {
               const int64_t *st = (const int64_t *)(mystage + so);
-              if (z) sr_copy_sent<int64_t, int64_t, true>(st, t0w, mask, c, lane, (int64_t *)D.dst[o] + pos, vd, D.col[oc].sent, zmn[o], zmx[o], zcnt[o], D.copy1);
-              else sr_copy_sent<int64_t, int64_t, false>(st, t0w, mask, c, lane, (int64_t *)D.dst[o] + pos, vd, D.col[oc].sent, zmn[o], zmx[o], zcnt[o], D.copy1);
+              if (z) sr_copy_sent<int64_t, int64_t, true>(st, t0w, mask, c, lane, (int64_t *)D.dst[o] + pos, vd, D.col[oc].sent, zmn[o], zmx[o], zcnt[o], D.copy1, D.nt_off);
+              else sr_copy_sent<int64_t, int64_t, false>(st, t0w, mask, c, lane, (int64_t *)D.dst[o] + pos, vd, D.col[oc].sent, zmn[o], zmx[o], zcnt[o], D.copy1, D.nt_off);
             } else if (D.col[oc].w == 8) {
               const int32_t *st = (const int32_t *)(mystage + so);
-              if (z) sr_copy_sent<int32_t, int64_t, true>(st, t0w, mask, c, lane, (int64_t *)D.dst[o] + pos, vd, (int32_t)D.col[oc].sent, zmn[o], zmx[o], zcnt[o], D.copy1);
-              else sr_copy_sent<int32_t, int64_t, false>(st, t0w, mask, c, lane, (int64_t *)D.dst[o] + pos, vd, (int32_t)D.col[oc].sent, zmn[o], zmx[o], zcnt[o], D.copy1);
+              if (z) sr_copy_sent<int32_t, int64_t, true>(st, t0w, mask, c, lane, (int64_t *)D.dst[o] + pos, vd, (int32_t)D.col[oc].sent, zmn[o], zmx[o], zcnt[o], D.copy1, D.nt_off);
+              else sr_copy_sent<int32_t, int64_t, false>(st, t0w, mask, c, lane, (int64_t *)D.dst[o] + pos, vd, (int32_t)D.col[oc].sent, zmn[o], zmx[o], zcnt[o], D.copy1, D.nt_off);
             } else {
               const int32_t *st = (const int32_t *)(mystage + so);
-              if (z) sr_copy_sent<int32_t, int32_t, true>(st, t0w, mask, c, lane, (int32_t *)D.dst[o] + pos, vd, (int32_t)D.col[oc].sent, zmn[o], zmx[o], zcnt[o], D.copy1);
-              else sr_copy_sent<int32_t, int32_t, false>(st, t0w, mask, c, lane, (int32_t *)D.dst[o] + pos, vd, (int32_t)D.col[oc].sent, zmn[o], zmx[o], zcnt[o], D.copy1);
+              if (z) sr_copy_sent<int32_t, int32_t, true>(st, t0w, mask, c, lane, (int32_t *)D.dst[o] + pos, vd, (int32_t)D.col[oc].sent, zmn[o], zmx[o], zcnt[o], D.copy1, D.nt_off);
+              else sr_copy_sent<int32_t, int32_t, false>(st, t0w, mask, c, lane, (int32_t *)D.dst[o] + pos, vd, (int32_t)D.col[oc].sent, zmn[o], zmx[o], zcnt[o], D.copy1, D.nt_off);
             }
           } else if ((zsmask >> oc) & 1) {  // the copy also folds the output's zone map (NULL rows skipped)
             long long mn = zmn[o], mx = zmx[o];
@@ -989,16 +999,16 @@ __global__ __launch_bounds__((NL + 5) * 64) void select_rounds_kernel(SelectDesc
             }
             zmn[o] = mn, zmx[o] = mx, zcnt[o] += nv;
           } else if (s8) {
-            sr_copy<int64_t, int64_t>((const int64_t *)(mystage + so), t0w, mask, c, lane, (int64_t *)D.dst[o] + pos, D.copy1);
+            sr_copy<int64_t, int64_t>((const int64_t *)(mystage + so), t0w, mask, c, lane, (int64_t *)D.dst[o] + pos, D.copy1, D.nt_off);
           } else if (D.col[oc].w == 8) {  // staged narrow: sign-extend back to int64
-            sr_copy<int32_t, int64_t>((const int32_t *)(mystage + so), t0w, mask, c, lane, (int64_t *)D.dst[o] + pos, D.copy1);
+            sr_copy<int32_t, int64_t>((const int32_t *)(mystage + so), t0w, mask, c, lane, (int64_t *)D.dst[o] + pos, D.copy1, D.nt_off);
           } else {
-            sr_copy<int32_t, int32_t>((const int32_t *)(mystage + so), t0w, mask, c, lane, (int32_t *)D.dst[o] + pos, D.copy1);
+            sr_copy<int32_t, int32_t>((const int32_t *)(mystage + so), t0w, mask, c, lane, (int32_t *)D.dst[o] + pos, D.copy1, D.nt_off);
           }
           if constexpr (VAL) {
             if (vb) {
               uint8_t *vd = D.vdst[o] + pos;
-              for (uint32_t i = lane; i < c; i += 64) __builtin_nontemporal_store((uint8_t)vb[(t0w + i) & mask], vd + i);
+              for (uint32_t i = lane; i < c; i += 64) sr_store((uint8_t)vb[(t0w + i) & mask], vd + i, !(D.nt_off & 2));
             }
           }
         }
