@@ -477,12 +477,16 @@ __device__ __forceinline__ void sr_copy(const TS *st, uint32_t t0w, uint32_t mas
                                         int mode, int nt_off) {
   const bool nt = !(nt_off & 1);
   uint32_t i = lane;
-  for (; mode != 1 && i + 192 < c; i += 256) {
+  // passes of 256 rows, the last one partial: with one 256-row step per round
+  // (8 loaders, S = 1) a loader's range is ~130 rows, which the whole-pass loop
+  // alone never reached (the staging reads past c stay inside the ring)
+  for (; mode != 1 && i < c; i += 256) {
     TS x[4];
 #pragma unroll
     for (int u = 0; u < 4; u++) x[u] = st[(t0w + i + 64 * u) & mask];
 #pragma unroll
-    for (int u = 0; u < 4; u++) sr_store((TD)x[u], dst + i + 64 * u, nt);
+    for (int u = 0; u < 4; u++)
+      if (i + 64 * u < c) sr_store((TD)x[u], dst + i + 64 * u, nt);
   }
   for (; i < c; i += 64) sr_store((TD)st[(t0w + i) & mask], dst + i, nt);
 }
@@ -496,22 +500,27 @@ __device__ __forceinline__ void sr_copy_sent(const TS *st, uint32_t t0w, uint32_
                                              int mode, int nt_off) {
   const bool ntv = !(nt_off & 1), ntb = !(nt_off & 2);
   uint32_t b = 0;
-  // whole passes of 256 rows, 4 per lane (rows b + lane + 64 u): the 4 staging
-  // reads share one LDS wait.  The validity of the pass comes back as 4 ballots
-  // (bit l of ballot u = row b + 64 u + l), from which lane l writes the bytes
-  // of rows b + 4 l .. b + 4 l + 3 as one 4-byte store (nibble -> bytes by one
-  // multiply), so a pass stores its 256 validity bytes with one instruction
-  // instead of four (mode 2: four byte stores, MBX_SR_COPY1=2)
-  for (; mode != 1 && b + 256 <= c; b += 256) {
+  // passes of 256 rows, 4 per lane (rows b + lane + 64 u), the last one
+  // partial: the 4 staging reads share one LDS wait (reads past c stay inside
+  // the ring and are not used).  The validity of the pass comes back as 4
+  // ballots (bit l of ballot u = row b + 64 u + l), from which lane l writes
+  // the bytes of rows b + 4 l .. b + 4 l + 3 as one 4-byte store (nibble ->
+  // bytes by one multiply; byte stores where the range ends inside them), so a
+  // pass stores its 256 validity bytes with one instruction instead of four
+  // (mode 2: four byte stores, MBX_SR_COPY1=2)
+  for (; mode != 1 && b < c; b += 256) {
     TS x[4];
 #pragma unroll
     for (int u = 0; u < 4; u++) x[u] = st[(t0w + b + lane + 64 * u) & mask];
     unsigned long long bal[4];
 #pragma unroll
     for (int u = 0; u < 4; u++) {
-      const bool ok = x[u] != sent;
-      sr_store((TD)(ok ? x[u] : (TS)0), dst + b + lane + 64 * u, ntv);
-      if (mode == 2) sr_store((uint8_t)ok, vd + b + lane + 64 * u, ntb);
+      const bool in = b + lane + 64 * u < c;
+      const bool ok = in && x[u] != sent;
+      if (in) {
+        sr_store((TD)(ok ? x[u] : (TS)0), dst + b + lane + 64 * u, ntv);
+        if (mode == 2) sr_store((uint8_t)ok, vd + b + lane + 64 * u, ntb);
+      }
       bal[u] = __ballot(ok);
       if constexpr (Z) {
         mn = ok && (long long)x[u] < mn ? (long long)x[u] : mn;
@@ -527,7 +536,14 @@ __device__ __forceinline__ void sr_copy_sent(const TS *st, uint32_t t0w, uint32_
       const int q = lane >> 4;
       const unsigned long long bw = q == 0 ? bal[0] : q == 1 ? bal[1] : q == 2 ? bal[2] : bal[3];
       const uint32_t nib = (uint32_t)(bw >> ((4 * lane) & 63)) & 0xFu;
-      sr_store((nib * 0x00204081u) & 0x01010101u, (uint32_t *)(vd + b + 4 * lane), ntb);
+      const uint32_t r0 = b + 4 * lane;
+      if (r0 + 3 < c) {
+        sr_store((nib * 0x00204081u) & 0x01010101u, (uint32_t *)(vd + r0), ntb);
+      } else {
+#pragma unroll
+        for (int e = 0; e < 4; e++)
+          if (r0 + e < c) sr_store((uint8_t)((nib >> e) & 1u), vd + r0 + e, ntb);
+      }
     }
   }
   for (uint32_t i = b + lane; i < c; i += 64) {

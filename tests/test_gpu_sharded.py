@@ -315,3 +315,40 @@ def test_sharded_rowwise_appender_across_parts(mbx):
     assert np.array_equal(np.frombuffer(bv[4:], dtype=np.int64), v)
     assert np.array_equal(np.frombuffer(bd[4:], dtype=np.float64), np.arange(n) * 0.5)
     c.close()
+
+
+def test_sharded_integer_key_merge_vs_numpy(mbx, oracle):
+    """The host merge's integer-key path (MergeIntKeys): negative keys, NULL
+    keys (last), two keys and a DECIMAL key over 4 shards, each group's
+    COUNT / SUM / MIN / MAX / AVG against numpy, in key order with and without
+    ORDER BY (the direct host result and the re-uploaded relation)."""
+    n = 400_009
+    c = _conn(mbx, "0,0,0,0")
+    q(c, f"CREATE TABLE w AS SELECT CASE WHEN mbx_synth(5, i, 9) = 0 THEN NULL ELSE mbx_synth(7, i, 40) - 20 END AS kn, "
+         f"CAST(mbx_synth(3, i, 3) AS INTEGER) AS k2, mbx_synth(42, i, 50) + 1 AS x, "
+         f"CAST(mbx_synth(11, i, 7) - 3 AS DECIMAL(9,2)) AS dk FROM range({n}) tbl(i)")
+    nul = oracle.synth_i64(n, 5, 0, 9, 0) == 0
+    kn = oracle.synth_i64(n, 7, 0, 40, 0) - 20
+    k2 = oracle.synth_i64(n, 3, 0, 3, 0)
+    x = oracle.synth_i64(n, 42, 0, 50, 1)
+    dk = oracle.synth_i64(n, 11, 0, 7, 0) - 3
+    exp = []
+    for key in list(range(-20, 20)) + [None]:
+        mk = nul if key is None else (~nul) & (kn == key)
+        if mk.any():
+            exp.append(["" if key is None else str(key), str(int(mk.sum())), str(int(x[mk].sum())),
+                        str(int(x[mk].min())), str(int(x[mk].max()))])
+    assert q(c, "SELECT kn, COUNT(*), SUM(x), MIN(x), MAX(x) FROM w GROUP BY kn").rows == exp
+    assert q(c, "SELECT kn, COUNT(*), SUM(x), MIN(x), MAX(x) FROM w GROUP BY kn ORDER BY kn NULLS LAST").rows == exp
+    exp2 = []
+    for key in list(range(-20, 20)) + [None]:
+        for b in range(3):
+            mk = (nul if key is None else (~nul) & (kn == key)) & (k2 == b)
+            if mk.any():
+                exp2.append(["" if key is None else str(key), str(b), str(int(mk.sum()))])
+    assert q(c, "SELECT kn, k2, COUNT(*) FROM w GROUP BY kn, k2").rows == exp2
+    got = q(c, "SELECT dk, COUNT(*), AVG(x) FROM w GROUP BY dk").rows
+    assert [r[:2] for r in got] == [[f"{v}.00", str(int((dk == v).sum()))] for v in range(-3, 4)]
+    for r, v in zip(got, range(-3, 4)):
+        assert abs(float(r[2]) - x[dk == v].mean()) <= 1e-9 * x[dk == v].mean()
+    c.close()
