@@ -1215,7 +1215,7 @@ static bool TrySelectOnePass(Engine &e, const DRel &rel, const dev::FilterMultiD
         // storers busy, so the loaders fold it (SELECT x ... WHERE x > 24:
         // 2.21 ms; storers 2.35)
         const char *zs = Knob("MBX_SR_ZSTORE");
-        S.zstore = zs ? atoi(zs) != 0 : plan.NL == 4;
+        S.zstore = plan.NL == 4 && (zs ? atoi(zs) != 0 : true);  // (8-loader kernels fold it in the loaders only)
         long long *z0 = (long long *)(e.h_pinned + 256);
         for (int c = 0; c < SL_MAX_COL; c++) z0[3 * c] = LLONG_MAX, z0[3 * c + 1] = LLONG_MIN, z0[3 * c + 2] = 0;
         HIPCHK(hipMemcpyAsync(S.zstats, z0, SL_MAX_COL * 3 * sizeof(long long), hipMemcpyHostToDevice, e.stream));
@@ -2024,7 +2024,11 @@ static DRel Aggregate(Engine &e, const DRel &src, const BoundSelect &s);
 // come from one pass with COUNT(arg) in the distinct ones' places; the
 // per-group distinct counts (one row per group) are merged into that relation
 // on the host by group key (KeyBytes, as the sharded combine does) and the
-// relation is uploaded back in the main pass's group order.
+// relation is uploaded back in the main pass's group order.  This merge is a
+// host slow path: it costs a D2H of the main relation and of every distinct
+// count, O(groups log groups) host work and an upload, so a high-cardinality
+// GROUP BY with COUNT(DISTINCT) is bound by the host (and a sharded table
+// gathers its parts first); it is off the measured hot path.
 static DRel DistinctAggregate(Engine &e, const DRel &src, const BoundSelect &s) {
   const int ng = (int)s.groups.size(), na = (int)s.aggs.size();
   BoundSelect m = s;

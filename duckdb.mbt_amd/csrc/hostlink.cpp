@@ -210,9 +210,10 @@ void AdviseHuge(void *p, size_t n) {
 //   M_BOUNCE   one DMA into a per-device pinned bounce, then T host threads
 //              copy their slices out (threads spin between calls, then sleep).
 // So the library measures: per device and power-of-two size class, the first
-// calls rotate through the methods, each timed end to end, and the class then
-// keeps the method with the best median; every kReprobe calls one call tries
-// another method again.  The bytes are the same whichever method runs.
+// calls rotate through the methods, each timed end to end (a method's first
+// call, which pays its setup and cold pages, is not counted), and the class
+// then keeps the method with the best median of its last samples; every
+// kReprobe calls one call tries another method again.  The bytes are the same whichever method runs.
 // MBX_LINK_MID=0 keeps the runtime's copy; MBX_LINK_MID_MODE=0|1|2 pins one.
 enum MidMethod { M_RUNTIME = 0, M_REGISTER = 1, M_BOUNCE = 2, M_COUNT = 3 };
 
@@ -287,14 +288,19 @@ class MidLink {
   }
 
  private:
-  static constexpr int kClasses = 4, kTrials = 3, kReprobe = 64;
+  static constexpr int kClasses = 4, kTrials = 3, kReprobe = 32;
   struct Class {
     std::vector<double> gbs[M_COUNT];  // (bytes/us = MB/s; only the order matters)
     bool broken[M_COUNT] = {false, false, false};
+    bool warmed[M_COUNT] = {false, false, false};
     uint64_t calls = 0;
     int best = -1;
     void Record(int m, double rate) {
       auto &v = gbs[m];
+      if (!warmed[m]) {  // a method's first call pays its setup and cold pages: not a sample
+        warmed[m] = true;
+        return;
+      }
       v.push_back(rate);
       if (v.size() > 16) v.erase(v.begin());
       double bm = -1;
@@ -309,8 +315,10 @@ class MidLink {
   };
   int Pick(Class &C) {
     const uint64_t k = C.calls++;
-    for (int m = 0; m < M_COUNT; m++)  // the trial phase: round-robin until every method has kTrials samples
-      if (!C.broken[(k + m) % M_COUNT] && C.gbs[(k + m) % M_COUNT].size() < (size_t)kTrials) return (int)((k + m) % M_COUNT);
+    for (int m = 0; m < M_COUNT; m++) {  // the trial phase: round-robin until every method has kTrials samples
+      const int t = (int)((k + m) % M_COUNT);
+      if (!C.broken[t] && (!C.warmed[t] || C.gbs[t].size() < (size_t)kTrials)) return t;
+    }
     if (C.best >= 0 && k % kReprobe == kReprobe - 1) {  // now and then re-time another method
       const int o = (int)((C.best + 1 + (k / kReprobe) % (M_COUNT - 1)) % M_COUNT);
       if (!C.broken[o]) return o;

@@ -929,7 +929,10 @@ __global__ __launch_bounds__((NL + 5) * 64) void select_rounds_kernel(SelectDesc
     // SELECT v 3.40 -> 3.30 at 1e9 rows).
     // D.zstore: the zone map of the D.zmask columns is folded here, per
     // output, from the values the copy loads anyway (else by the loaders)
-    const uint32_t zsmask = D.zstats && D.zstore ? (uint32_t)D.zmask & smask : 0u;
+    // (8 loaders: the loaders fold it, so the storer's copy of the map is not
+    // compiled -- its registers pushed the NULL-able 8-loader instances past
+    // 128 VGPRs into scratch)
+    const uint32_t zsmask = NL == 4 && D.zstats && D.zstore ? (uint32_t)D.zmask & smask : 0u;
     long long zmn[SL_MAX_OUT], zmx[SL_MAX_OUT];
     uint32_t zcnt[SL_MAX_OUT];
 #pragma unroll
@@ -945,12 +948,17 @@ __global__ __launch_bounds__((NL + 5) * 64) void select_rounds_kernel(SelectDesc
       if (dbg) d_wait += clock64() - t0;
       if (quit) break;
       int64_t pos = lds_ld(&sm.base[slot]);
+      // the round's loader counts in one LDS read (lane q: loader q's count),
+      // the prefix taken by readlanes: one LDS round trip per round instead of
+      // one per earlier loader (up to 8 waited reads for storer 3's second loader)
+      uint32_t cl;
+      asm volatile("ds_read_b32 %0, %1\n\ts_waitcnt lgkmcnt(0)" : "=v"(cl) : "v"(lds_addr(&sm.cnt[slot][lane & 7])) : "memory");
       int q = 0;
 #pragma unroll
       for (int j = 0; j < PER; j++) {
         const int l = sw + 4 * j;
-        for (; q < l; q++) pos += lds_ld(&sm.cnt[slot][q]);
-        const uint32_t c = lds_ld(&sm.cnt[slot][l]);
+        for (; q < l; q++) pos += (uint32_t)__builtin_amdgcn_readlane((int)cl, q);
+        const uint32_t c = (uint32_t)__builtin_amdgcn_readlane((int)cl, l);
         const unsigned char *mystage = stage0 + (size_t)l * (stg + 64) * rowb;
 #pragma unroll
         for (int o = 0; o < SL_MAX_OUT; o++) {
