@@ -1214,8 +1214,7 @@ static bool TrySelectOnePass(Engine &e, const DRel &rel, const dev::FilterMultiD
         // 4.59 ms, as the selection alone; loaders 5.00); 8 loaders keep their
         // storers busy, so the loaders fold it (SELECT x ... WHERE x > 24:
         // 2.21 ms; storers 2.35)
-        const char *zs = Knob("MBX_SR_ZSTORE");
-        S.zstore = plan.NL == 4 && (zs ? atoi(zs) != 0 : true);  // (8-loader kernels fold it in the loaders only)
+        S.zstore = plan.NL == 4;  // (each kernel instance compiles the map in that role only)
         long long *z0 = (long long *)(e.h_pinned + 256);
         for (int c = 0; c < SL_MAX_COL; c++) z0[3 * c] = LLONG_MAX, z0[3 * c + 1] = LLONG_MIN, z0[3 * c + 2] = 0;
         HIPCHK(hipMemcpyAsync(S.zstats, z0, SL_MAX_COL * 3 * sizeof(long long), hipMemcpyHostToDevice, e.stream));

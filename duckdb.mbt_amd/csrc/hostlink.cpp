@@ -210,10 +210,9 @@ void AdviseHuge(void *p, size_t n) {
 //   M_BOUNCE   one DMA into a per-device pinned bounce, then T host threads
 //              copy their slices out (threads spin between calls, then sleep).
 // So the library measures: per device and power-of-two size class, the first
-// calls rotate through the methods, each timed end to end (a method's first
-// call, which pays its setup and cold pages, is not counted), and the class
-// then keeps the method with the best median of its last samples; every
-// kReprobe calls one call tries another method again.  The bytes are the same whichever method runs.
+// calls run each method for a block of kBlock calls, timed end to end (a
+// block's first call, which pays the method's setup and cold pages, is not
+// counted), and the class then keeps the method with the best median.  The bytes are the same whichever method runs.
 // MBX_LINK_MID=0 keeps the runtime's copy; MBX_LINK_MID_MODE=0|1|2 pins one.
 enum MidMethod { M_RUNTIME = 0, M_REGISTER = 1, M_BOUNCE = 2, M_COUNT = 3 };
 
@@ -274,7 +273,8 @@ class MidLink {
     int cls = 0;  // 2-4 MiB: 0, 4-8: 1, 8-16: 2, 16-32: 3
     for (size_t q = n >> 21; q > 1 && cls < kClasses - 1; q >>= 1) cls++;
     Class &C = cls_[cls];
-    int m = forced >= 0 && forced < M_COUNT ? forced : Pick(C);
+    bool sample = false;
+    int m = forced >= 0 && forced < M_COUNT ? forced : Pick(C, &sample);
     const auto t0 = std::chrono::steady_clock::now();
     std::string err = Run(m, dst, src, n);
     if (!err.empty() && m != M_RUNTIME) {  // a method the box refuses (e.g. registration): never again here
@@ -283,45 +283,44 @@ class MidLink {
       err = Run(m, dst, src, n);
     }
     const double us = std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0).count();
-    if (err.empty()) C.Record(m, n / us);
+    if (err.empty()) C.Record(m, n / us, sample);
     return err;
   }
 
  private:
-  static constexpr int kClasses = 4, kTrials = 3, kReprobe = 32;
+  static constexpr int kClasses = 4, kBlock = 5;  // trial calls per method (the first not counted)
   struct Class {
     std::vector<double> gbs[M_COUNT];  // (bytes/us = MB/s; only the order matters)
     bool broken[M_COUNT] = {false, false, false};
-    bool warmed[M_COUNT] = {false, false, false};
     uint64_t calls = 0;
     int best = -1;
-    void Record(int m, double rate) {
-      auto &v = gbs[m];
-      if (!warmed[m]) {  // a method's first call pays its setup and cold pages: not a sample
-        warmed[m] = true;
-        return;
-      }
-      v.push_back(rate);
-      if (v.size() > 16) v.erase(v.begin());
+    // one trial block per method, back to back (alternating methods call by
+    // call disturbed them: on one box the runtime copy ran 6-8 GB/s between
+    // bounce calls and 16 GB/s in a run of its own); a block's first call pays
+    // the method's setup and cold pages and is not a sample
+    void Record(int m, double rate, bool sample) {
+      if (!sample) return;
+      gbs[m].push_back(rate);
       double bm = -1;
       best = -1;
       for (int k = 0; k < M_COUNT; k++) {
-        if (broken[k] || gbs[k].size() < (size_t)kTrials) continue;
+        if (broken[k] || gbs[k].empty()) continue;
         std::vector<double> s = gbs[k];
         std::nth_element(s.begin(), s.begin() + s.size() / 2, s.end());
         if (s[s.size() / 2] > bm) bm = s[s.size() / 2], best = k;
       }
     }
   };
-  int Pick(Class &C) {
+  // the method for call k of a class, and whether its rate is a trial sample
+  int Pick(Class &C, bool *sample) {
     const uint64_t k = C.calls++;
-    for (int m = 0; m < M_COUNT; m++) {  // the trial phase: round-robin until every method has kTrials samples
-      const int t = (int)((k + m) % M_COUNT);
-      if (!C.broken[t] && (!C.warmed[t] || C.gbs[t].size() < (size_t)kTrials)) return t;
-    }
-    if (C.best >= 0 && k % kReprobe == kReprobe - 1) {  // now and then re-time another method
-      const int o = (int)((C.best + 1 + (k / kReprobe) % (M_COUNT - 1)) % M_COUNT);
-      if (!C.broken[o]) return o;
+    *sample = false;
+    if (k < (uint64_t)M_COUNT * kBlock) {
+      const int t = (int)(k / kBlock);
+      if (!C.broken[t]) {
+        *sample = k % kBlock != 0;
+        return t;
+      }
     }
     return C.best >= 0 ? C.best : M_RUNTIME;
   }

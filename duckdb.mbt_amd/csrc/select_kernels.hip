@@ -698,7 +698,7 @@ __global__ __launch_bounds__((NL + 5) * 64) void select_rounds_kernel(SelectDesc
     // folded from the values already in registers (4-byte columns in 32-bit
     // ops); the non-NULL count only for NULL-able columns (otherwise it is the
     // selected count)
-    const uint32_t zmask = D.zstats && !D.zstore ? (uint32_t)D.zmask & smask : 0u;
+    const uint32_t zmask = NL == 8 && D.zstats && !D.zstore ? (uint32_t)D.zmask & smask : 0u;  // (4 loaders: the storers fold it)
     long long zmn[NC], zmx[NC];
     int zmn4[NC], zmx4[NC];
     uint32_t zcnt[NC];
