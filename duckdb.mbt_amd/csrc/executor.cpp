@@ -1233,16 +1233,16 @@ static bool TrySelectOnePass(Engine &e, const DRel &rel, const dev::FilterMultiD
       return false;  // the two-pass form instead
     }
     if (dbgbuf) {
-      unsigned long long h[13];
+      unsigned long long h[14];
       HIPCHK(hipMemcpyAsync(h, dbgbuf->p, sizeof(h), hipMemcpyDeviceToHost, e.stream));
       HIPCHK(hipStreamSynchronize(e.stream));
-      const double L = (double)plan.G * 4, C = (double)plan.G;
+      const double L = (double)plan.G * plan.NL, Ls = (double)plan.G * 4, C = (double)plan.G;
       fprintf(stderr, "[select_rounds] G %d rounds %lld S %d stg %d depth %d | per loader: cycles %.0f dma_wait %.0f "
-              "staging_wait %.0f meta_wait %.0f | per storer: cycles %.0f base_wait %.0f | per coordinator: cycles %.0f "
+              "staging_wait %.0f meta_wait %.0f | per storer: cycles %.0f base_wait %.0f copy %.0f | per coordinator: cycles %.0f "
               "polls %.1f no_progress %.1f poll_load_cycles %.0f (%.0f per poll) rounds %.1f max/poll %llu "
               "publish->resolve %.0f cycles/round\n",
               plan.G, (long long)plan.nrounds, plan.S, plan.stg, plan.depth, h[0] / L, h[1] / L, h[2] / L, h[3] / L,
-              h[4] / L, h[5] / L, h[6] / C, h[7] / C, h[8] / C, h[9] / C, h[7] ? (double)h[9] / h[7] : 0.0, h[10] / C,
+              h[4] / Ls, h[5] / Ls, h[13] / Ls, h[6] / C, h[7] / C, h[8] / C, h[9] / C, h[7] ? (double)h[9] / h[7] : 0.0, h[10] / C,
               h[11], h[10] ? (double)h[12] / h[10] : 0.0);
       if (tsbuf) {  // publish-time spread per round (10 ns ticks): how far the last workgroup trails
         std::vector<unsigned long long> ts((size_t)plan.nrounds * plan.G);

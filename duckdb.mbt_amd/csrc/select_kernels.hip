@@ -450,6 +450,11 @@ __device__ __forceinline__ void lds_st(long long *p, long long v) {
 __device__ __forceinline__ void lds_st(unsigned long long *p, unsigned long long v) {
   asm volatile("ds_write_b64 %0, %1\n\ts_waitcnt lgkmcnt(0)" ::"v"(lds_addr(p)), "v"(v) : "memory");
 }
+// a control-word store whose completion nobody in this wave waits for (the
+// wave's later LDS ops stay in order behind it; the reader polls)
+__device__ __forceinline__ void lds_st_nw(uint32_t *p, uint32_t v) {
+  asm volatile("ds_write_b32 %0, %1" ::"v"(lds_addr(p)), "v"(v) : "memory");
+}
 template <int N>
 __device__ __forceinline__ void sr_wait() {
   asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
@@ -477,16 +482,16 @@ __device__ __forceinline__ void sr_copy(const TS *st, uint32_t t0w, uint32_t mas
                                         int mode, int nt_off) {
   const bool nt = !(nt_off & 1);
   uint32_t i = lane;
-  // passes of 256 rows, the last one partial: with one 256-row step per round
-  // (8 loaders, S = 1) a loader's range is ~130 rows, which the whole-pass loop
-  // alone never reached (the staging reads past c stay inside the ring)
-  for (; mode != 1 && i < c; i += 256) {
+  // whole 4-row groups only: with one 256-row step per round (8 loaders,
+  // S = 1) a loader's range is ~130 rows, and guarded 4-row passes over such
+  // ranges measured slower than the one-row loop (SELECT v ... WHERE xn > 24
+  // 3.70 vs 3.57 ms, profiles/r04_storer_copy_ab.log)
+  for (; mode != 1 && i + 192 < c; i += 256) {
     TS x[4];
 #pragma unroll
     for (int u = 0; u < 4; u++) x[u] = st[(t0w + i + 64 * u) & mask];
 #pragma unroll
-    for (int u = 0; u < 4; u++)
-      if (i + 64 * u < c) sr_store((TD)x[u], dst + i + 64 * u, nt);
+    for (int u = 0; u < 4; u++) sr_store((TD)x[u], dst + i + 64 * u, nt);
   }
   for (; i < c; i += 64) sr_store((TD)st[(t0w + i) & mask], dst + i, nt);
 }
@@ -500,27 +505,25 @@ __device__ __forceinline__ void sr_copy_sent(const TS *st, uint32_t t0w, uint32_
                                              int mode, int nt_off) {
   const bool ntv = !(nt_off & 1), ntb = !(nt_off & 2);
   uint32_t b = 0;
-  // passes of 256 rows, 4 per lane (rows b + lane + 64 u), the last one
-  // partial: the 4 staging reads share one LDS wait (reads past c stay inside
-  // the ring and are not used).  The validity of the pass comes back as 4
-  // ballots (bit l of ballot u = row b + 64 u + l), from which lane l writes
-  // the bytes of rows b + 4 l .. b + 4 l + 3 as one 4-byte store (nibble ->
-  // bytes by one multiply; byte stores where the range ends inside them), so a
-  // pass stores its 256 validity bytes with one instruction instead of four
-  // (mode 2: four byte stores, MBX_SR_COPY1=2)
-  for (; mode != 1 && b < c; b += 256) {
+  // whole passes of 256 rows, 4 per lane (rows b + lane + 64 u): the 4 staging
+  // reads share one LDS wait.  The validity of the pass comes back as 4 ballots
+  // (bit l of ballot u = row b + 64 u + l), from which lane l writes the bytes
+  // of rows b + 4 l .. b + 4 l + 3 as one 4-byte store (nibble -> bytes by one
+  // multiply), so a pass stores its 256 validity bytes with one instruction
+  // instead of four (mode 2: four byte stores, MBX_SR_COPY1=2).  The rows after
+  // the last whole pass take the one-row loop: guarded partial passes measured
+  // slower on ~130-row ranges (SELECT vn ... WHERE x > 24 4.81 vs 4.06 ms,
+  // profiles/r04_storer_copy_ab.log)
+  for (; mode != 1 && b + 256 <= c; b += 256) {
     TS x[4];
 #pragma unroll
     for (int u = 0; u < 4; u++) x[u] = st[(t0w + b + lane + 64 * u) & mask];
     unsigned long long bal[4];
 #pragma unroll
     for (int u = 0; u < 4; u++) {
-      const bool in = b + lane + 64 * u < c;
-      const bool ok = in && x[u] != sent;
-      if (in) {
-        sr_store((TD)(ok ? x[u] : (TS)0), dst + b + lane + 64 * u, ntv);
-        if (mode == 2) sr_store((uint8_t)ok, vd + b + lane + 64 * u, ntb);
-      }
+      const bool ok = x[u] != sent;
+      sr_store((TD)(ok ? x[u] : (TS)0), dst + b + lane + 64 * u, ntv);
+      if (mode == 2) sr_store((uint8_t)ok, vd + b + lane + 64 * u, ntb);
       bal[u] = __ballot(ok);
       if constexpr (Z) {
         mn = ok && (long long)x[u] < mn ? (long long)x[u] : mn;
@@ -536,14 +539,7 @@ __device__ __forceinline__ void sr_copy_sent(const TS *st, uint32_t t0w, uint32_
       const int q = lane >> 4;
       const unsigned long long bw = q == 0 ? bal[0] : q == 1 ? bal[1] : q == 2 ? bal[2] : bal[3];
       const uint32_t nib = (uint32_t)(bw >> ((4 * lane) & 63)) & 0xFu;
-      const uint32_t r0 = b + 4 * lane;
-      if (r0 + 3 < c) {
-        sr_store((nib * 0x00204081u) & 0x01010101u, (uint32_t *)(vd + r0), ntb);
-      } else {
-#pragma unroll
-        for (int e = 0; e < 4; e++)
-          if (r0 + e < c) sr_store((uint8_t)((nib >> e) & 1u), vd + r0 + e, ntb);
-      }
+      sr_store((nib * 0x00204081u) & 0x01010101u, (uint32_t *)(vd + b + 4 * lane), ntb);
     }
   }
   for (uint32_t i = b + lane; i < c; i += 64) {
@@ -923,7 +919,7 @@ __global__ __launch_bounds__((NL + 5) * 64) void select_rounds_kernel(SelectDesc
 #pragma unroll
     for (int j = 0; j < PER; j++) tail[j] = 0;
     const bool dbg = D.dbg != nullptr;
-    unsigned long long t_all = dbg ? clock64() : 0, d_wait = 0, t0 = 0;
+    unsigned long long t_all = dbg ? clock64() : 0, d_wait = 0, d_copy = 0, t0 = 0, t1 = 0;
     // Output stores are non-temporal: the rows are written once and not read
     // back by this kernel (sel 2.055 -> 2.025 ms, SELECT k, v 4.61 -> 4.44,
     // SELECT v 3.40 -> 3.30 at 1e9 rows).
@@ -953,6 +949,7 @@ __global__ __launch_bounds__((NL + 5) * 64) void select_rounds_kernel(SelectDesc
       // one per earlier loader (up to 8 waited reads for storer 3's second loader)
       uint32_t cl;
       asm volatile("ds_read_b32 %0, %1\n\ts_waitcnt lgkmcnt(0)" : "=v"(cl) : "v"(lds_addr(&sm.cnt[slot][lane & 7])) : "memory");
+      if (dbg) t1 = clock64();
       int q = 0;
 #pragma unroll
       for (int j = 0; j < PER; j++) {
@@ -1038,10 +1035,12 @@ __global__ __launch_bounds__((NL + 5) * 64) void select_rounds_kernel(SelectDesc
         }
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // staging read before it is freed
         tail[j] += c;
-        if (lane == 0) lds_st(&sm.tail[l], tail[j]);
+        if (lane == 0) lds_st_nw(&sm.tail[l], tail[j]);
       }
-      if (lane == 0) lds_st(&sm.sdone[sw], (uint32_t)(r + 1));
+      if (dbg) d_copy += clock64() - t1;
+      if (lane == 0) lds_st_nw(&sm.sdone[sw], (uint32_t)(r + 1));
     }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the last control stores land before the wave ends
     if (zsmask) {
 #pragma unroll
       for (int o = 0; o < SL_MAX_OUT; o++) {
@@ -1067,6 +1066,7 @@ __global__ __launch_bounds__((NL + 5) * 64) void select_rounds_kernel(SelectDesc
     if (dbg && lane == 0) {
       atomicAdd(&D.dbg[4], clock64() - t_all);
       atomicAdd(&D.dbg[5], d_wait);
+      atomicAdd(&D.dbg[13], d_copy);
     }
     return;
   }
