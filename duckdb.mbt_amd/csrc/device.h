@@ -367,7 +367,19 @@ struct SelectDesc {
   int32_t zstore;  // 1: the storers fold the zone maps while copying, 0: the loaders
   int32_t nt_off;  // select_rounds storers (MBX_SR_NT_OFF, A/B): bit 0 = plain value stores, bit 1 = plain validity stores (default: non-temporal)
   int32_t copy1;   // select_rounds storers (MBX_SR_COPY1, A/B): 0 = 4 rows per lane per pass, 1 = one, 2 = 4 with byte validity stores
-  unsigned long long *dbg;     // nullptr, or 9 counters (MBX_SL_DEBUG) / 13 (MBX_SR_DEBUG)
+  // select_rounds, 8 loaders: the validity of ONE NULL-able output (index vbo,
+  // -1: none) leaves as ballots instead of bytes.  Loaders write, per 256-row
+  // sub-step gs of the input, 8 words at vball[8 gs]: the 4 selection ballots,
+  // then the 4 ballots of selected-and-valid rows (bit l of word e = row
+  // 256 gs + 4 l + e); the staged value of a NULL row is 0.  Storers write
+  // vpos[range] = the output row of each loader range's first row (range =
+  // ((round G + workgroup) NL + loader); S steps each), workgroup 0's tail loop
+  // the sub-steps after nsteps H and vpos[nrounds G NL].  PackValidityBallots
+  // then builds the bitmap, one thread per output word.
+  unsigned long long *vball;
+  int64_t *vpos;
+  int32_t vbo;
+  unsigned long long *dbg;     // nullptr, or 9 counters (MBX_SL_DEBUG) / 14 (MBX_SR_DEBUG)
   unsigned long long *dbg_ts;  // MBX_SR_DEBUG=2: s_memrealtime of every (round, workgroup) publish
 };
 size_t SelectStatusBytes(int64_t nrows, int ni);
@@ -396,6 +408,14 @@ hipError_t SelectRounds(const SelectDesc &d, const SelectRoundsPlan &p, int64_t 
                   uint32_t epoch, hipStream_t s);
 // bits[i / 64] bit i % 64 = bytes[i] (0/1), for the n output rows of a NULL-able select_rounds output
 void PackValidityBytes(const uint8_t *bytes, int64_t n, uint64_t *bits, hipStream_t s);
+// the bitmap of the ballot-mode output (SelectDesc::vbo) of a finished launch
+// of plan p over nrows input rows with n selected rows
+void PackValidityBallots(const unsigned long long *vball, const int64_t *vpos, const SelectRoundsPlan &p,
+                         int64_t nrows, int64_t n, uint64_t *bits, hipStream_t s);
+// words of vball / vpos a launch of plan p over nrows rows writes (+ the dump
+// slot of dead steps)
+size_t SelectBallotWords(const SelectRoundsPlan &p, int64_t nrows);
+size_t SelectRangeCount(const SelectRoundsPlan &p);
 
 }  // namespace dev
 }  // namespace mbx

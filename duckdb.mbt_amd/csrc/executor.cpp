@@ -1087,6 +1087,7 @@ static bool TrySelectOnePass(Engine &e, const DRel &rel, const dev::FilterMultiD
   if ((int)exprs.size() > SL_MAX_OUT) return false;
   dev::SelectDesc S;
   memset(&S, 0, sizeof(S));
+  S.vbo = -1;
   auto slot_of = [&](const void *data, int w) -> int {
     for (int i = 0; i < S.ncol; i++)
       if (S.col[i].data == data) return S.col[i].w == w ? i : -2;
@@ -1153,17 +1154,53 @@ static bool TrySelectOnePass(Engine &e, const DRel &rel, const dev::FilterMultiD
   const int64_t n = rel.n;
   dev::SelectRoundsPlan plan;
   memset(&plan, 0, sizeof(plan));
+  // Ballot-mode validity for one NULL-able output (SelectDesc::vbo): with 8
+  // loaders the storers were the bottleneck of NULL-able outputs (busy ~90 %,
+  // profiles/r04_select_rounds_role_split.log); in this mode they copy the
+  // values like a NULL-free output, the loaders store each step's ballots,
+  // and PackValidityBallots builds the bitmap.  Only when the planner gives
+  // the 8-loader H = 1 form, and the column feeds no other output.
+  // MBX_SR_VBALL=0 keeps the sentinel / byte forms (A/B).
+  int vb_k = -1;
   if (mode != 2) {
+    const char *vbk = Knob("MBX_SR_VBALL");
+    if (!(vbk && atoi(vbk) == 0))
+      for (int k = 0; k < S.nout && vb_k < 0; k++) {
+        const int i = S.out_col[k];
+        if (!S.col[i].valid) continue;
+        int uses = 0;
+        for (int k2 = 0; k2 < S.nout; k2++) uses += S.out_col[k2] == i;
+        if (uses == 1) vb_k = k;
+      }
+    int32_t save_vsent = 0;
+    int64_t save_sent = 0;
+    const int vb_i = vb_k >= 0 ? S.out_col[vb_k] : -1;
+    if (vb_i >= 0) {
+      save_vsent = S.col[vb_i].vsent, save_sent = S.col[vb_i].sent;
+      S.col[vb_i].vsent = 2, S.col[vb_i].sent = 0;  // a NULL row is staged as 0, with no byte of its own
+    }
     plan = dev::PlanSelectRounds(S, n);
+    if (vb_i >= 0 && !(plan.ok && plan.NL == 8 && plan.H == 1)) {
+      S.col[vb_i].vsent = save_vsent, S.col[vb_i].sent = save_sent;
+      vb_k = -1;
+      plan = dev::PlanSelectRounds(S, n);
+    }
     if (!plan.ok) return false;
   }
   std::vector<DCol> cols;
   std::vector<DevBufPtr> vbytes(exprs.size());  // NULL-able outputs: one validity byte per output row
+  DevBufPtr vball, vpos;                         // ballot mode: per-step ballots, per-range output rows
   for (int k = 0; k < (int)exprs.size(); k++) {
     const bool nullable = rel.cols[exprs[k]->col].validity != nullptr;
     cols.push_back(AllocOut(e, exprs[k]->type, n, nullable, false));
     S.dst[k] = cols[k].data;
-    if (nullable) {  // (released to the engine's pool when this returns: later users run after the pack on e.stream)
+    if (nullable && k == vb_k) {  // (released to the engine's pool when this returns: later users run after the pack on e.stream)
+      vball = Alloc(e, dev::SelectBallotWords(plan, n) * 8);
+      vpos = Alloc(e, (dev::SelectRangeCount(plan) + 1) * 8);
+      S.vball = (unsigned long long *)vball->p;
+      S.vpos = (int64_t *)vpos->p;
+      S.vbo = k;
+    } else if (nullable) {
       vbytes[k] = Alloc(e, (size_t)std::max<int64_t>(n, 1) + 64);
       S.vdst[k] = (uint8_t *)vbytes[k]->p;
     }
@@ -1328,6 +1365,12 @@ static bool TrySelectOnePass(Engine &e, const DRel &rel, const dev::FilterMultiD
     e.events.back().bytes += ob;
   }
   for (int k = 0; k < S.nout; k++) {
+    if (k == S.vbo) {
+      const int64_t nsub = (int64_t)dev::SelectBallotWords(plan, n) / 8;
+      ProfScope ps(e, "pack_validity", (double)nsub * 64 + (double)dev::SelectRangeCount(plan) * 8 + nsel / 8.0, nsel);
+      dev::PackValidityBallots(S.vball, S.vpos, plan, n, nsel, (uint64_t *)cols[k].validity, e.stream);
+      continue;
+    }
     if (!S.vdst[k]) continue;
     ProfScope ps(e, "pack_validity", (double)nsel + nsel / 8.0, nsel);
     dev::PackValidityBytes(S.vdst[k], nsel, cols[k].validity, e.stream);
@@ -1336,7 +1379,7 @@ static bool TrySelectOnePass(Engine &e, const DRel &rel, const dev::FilterMultiD
   out.n = nsel;
   out.cols = cols;
   bool packed = false;
-  for (int k = 0; k < S.nout; k++) packed |= S.vdst[k] != nullptr;
+  for (int k = 0; k < S.nout; k++) packed |= S.vdst[k] != nullptr || k == S.vbo;
   if (rounds_err >= 0 && !packed) RaiseDeviceError(e, rounds_err);  // nothing ran after that read
   else CheckError(e);
   return true;

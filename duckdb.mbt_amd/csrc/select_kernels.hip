@@ -680,8 +680,20 @@ __global__ __launch_bounds__((NL + 5) * 64) void select_rounds_kernel(SelectDesc
                                                (void *)(vring + slot * VSB + h * NC * 32 + voff[c]), 16, 0, 2);
       }
     };
+    // ballot-mode validity (SelectDesc::vbo; 8 loaders, H = 1): every step
+    // stores its 8 ballot words (one instruction, counted in the waits below;
+    // a dead step's go to the dump slot past the live ones).  So that every
+    // wait counts the same instructions, the prologue puts one store of the
+    // dump slot in front of each slot after the first.
+    const int vbm = VAL && NL == 8 && H == 1 && D.vbo >= 0 ? 1 : 0;
+    const int vbc = vbm ? D.out_col[D.vbo] : -1;
+    const int64_t vdump = (nsteps + (n - nsteps * 256 + 255) / 256) * 8;
 #pragma unroll
-    for (int d = 0; d < DEPTH; d++) issue(d);
+    for (int d = 0; d < DEPTH; d++) {
+      if (vbm && d > 0 && lane < 8) D.vball[vdump + lane] = 0ull;
+      asm volatile("" ::: "memory");  // (issue order is what the counted waits count)
+      issue(d);
+    }
     int k = 0;
     uint32_t head = 0, tail_seen = 0;
     bool quit = false;
@@ -722,11 +734,15 @@ __global__ __launch_bounds__((NL + 5) * 64) void select_rounds_kernel(SelectDesc
       for (int s = 0; s < S; s++) {
         if (dbg) t0 = clock64();
         if constexpr (VAL) {
-          switch (nv) {  // wave-uniform: the exact count of the instructions issued after this slot's
+          switch (nv + 4 * vbm) {  // wave-uniform: the exact count of the instructions issued after this slot's
             case 1: sr_wait<(NI + H) * (DEPTH - 1)>(); break;
             case 2: sr_wait<(NI + 2 * H) * (DEPTH - 1)>(); break;
             case 3: sr_wait<(NI + 3 * H) * (DEPTH - 1)>(); break;
-            default: sr_wait<(NI + 4 * H) * (DEPTH - 1)>(); break;
+            case 4: sr_wait<(NI + 4 * H) * (DEPTH - 1)>(); break;
+            case 5: sr_wait<(NI + H + 1) * (DEPTH - 1)>(); break;  // (+ the step's ballot store)
+            case 6: sr_wait<(NI + 2 * H + 1) * (DEPTH - 1)>(); break;
+            case 7: sr_wait<(NI + 3 * H + 1) * (DEPTH - 1)>(); break;
+            default: sr_wait<(NI + 4 * H + 1) * (DEPTH - 1)>(); break;
           }
         } else {
           asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NI * (DEPTH - 1)) : "memory");
@@ -785,6 +801,22 @@ __global__ __launch_bounds__((NL + 5) * 64) void select_rounds_kernel(SelectDesc
             hc[h] += (uint32_t)__popcll(b[h][e]);
           }
           cnt += hc[h];
+        }
+        if constexpr (VAL && NL == 8 && H == 1) {
+          if (vbm) {  // the step's selection ballots and its selected-and-valid ballots of the output column
+            uint32_t vm = 0xFu;
+#pragma unroll
+            for (int c = 0; c < NC; c++)
+              if (c == vbc) vm = vmc[0][c];
+            unsigned long long vb[4];
+#pragma unroll
+            for (int e = 0; e < 4; e++) vb[e] = __ballot(ok[0][e] && ((vm >> e) & 1u));
+            const int le = lane & 3;
+            const unsigned long long wb = le == 0 ? b[0][0] : le == 1 ? b[0][1] : le == 2 ? b[0][2] : b[0][3];
+            const unsigned long long wv = le == 0 ? vb[0] : le == 1 ? vb[1] : le == 2 ? vb[2] : vb[3];
+            unsigned long long *vp = D.vball + (live ? 8 * (qb + s) : vdump);
+            if (lane < 8) vp[lane] = lane < 4 ? wb : wv;
+          }
         }
         if (cnt) {
           if (head + 256u * H - tail_seen > (uint32_t)stg) {  // staging full: wait for the storer
@@ -956,6 +988,7 @@ __global__ __launch_bounds__((NL + 5) * 64) void select_rounds_kernel(SelectDesc
         const int l = sw + 4 * j;
         for (; q < l; q++) pos += (uint32_t)__builtin_amdgcn_readlane((int)cl, q);
         const uint32_t c = (uint32_t)__builtin_amdgcn_readlane((int)cl, l);
+        if (VAL && NL == 8 && D.vball && lane == 0) D.vpos[(r * G + g) * NL + l] = pos;  // ballot mode: the range's first output row
         const unsigned char *mystage = stage0 + (size_t)l * (stg + 64) * rowb;
 #pragma unroll
         for (int o = 0; o < SL_MAX_OUT; o++) {
@@ -1175,6 +1208,10 @@ __global__ __launch_bounds__((NL + 5) * 64) void select_rounds_kernel(SelectDesc
 #pragma unroll
   for (int c = 0; c < NC; c++) tmn[c] = LLONG_MAX, tmx[c] = LLONG_MIN, tnv[c] = 0;
   int64_t tcnt = 0;
+  // ballot mode: the tail's 256-row passes are sub-steps nsteps H, ... of the
+  // ballot array, all in one range after the last round's
+  const int tvb = VAL && NL == 8 && H == 1 && D.vbo >= 0 ? D.out_col[D.vbo] : -1;
+  if (tvb >= 0 && lane == 0) D.vpos[nrounds * G * NL] = running;
   for (int64_t base = nsteps * 256 * H; base < n; base += 256) {
     bool ok[4];
     const int64_t i0 = base + 4 * lane;
@@ -1193,14 +1230,25 @@ __global__ __launch_bounds__((NL + 5) * 64) void select_rounds_kernel(SelectDesc
     unsigned long long bb[4];
 #pragma unroll
     for (int e = 0; e < 4; e++) bb[e] = __ballot(ok[e]);
+    if (tvb >= 0) {
+      unsigned long long vb[4];
+#pragma unroll
+      for (int e = 0; e < 4; e++)
+        vb[e] = __ballot(ok[e] && ((D.col[tvb].valid[(i0 + e) >> 6] >> ((i0 + e) & 63)) & 1));
+      const int le = lane & 3;
+      const unsigned long long wb = le == 0 ? bb[0] : le == 1 ? bb[1] : le == 2 ? bb[2] : bb[3];
+      const unsigned long long wv = le == 0 ? vb[0] : le == 1 ? vb[1] : le == 2 ? vb[2] : vb[3];
+      if (lane < 8) D.vball[8 * (base / 256) + lane] = lane < 4 ? wb : wv;
+    }
     int64_t pos = running + tcnt + __popcll(bb[0] & lt) + __popcll(bb[1] & lt) + __popcll(bb[2] & lt) +
                   __popcll(bb[3] & lt);
     for (int e = 0; e < 4; e++) {
       if (!ok[e]) continue;
       for (int o = 0; o < D.nout; o++) {
         const int c = D.out_col[o];
-        if (D.col[c].w == 8) ((int64_t *)D.dst[o])[pos] = ((const int64_t *)D.col[c].data)[i0 + e];
-        else ((int32_t *)D.dst[o])[pos] = ((const int32_t *)D.col[c].data)[i0 + e];
+        const bool zn = c == tvb && !((D.col[c].valid[(i0 + e) >> 6] >> ((i0 + e) & 63)) & 1);  // (0 under NULL)
+        if (D.col[c].w == 8) ((int64_t *)D.dst[o])[pos] = zn ? 0 : ((const int64_t *)D.col[c].data)[i0 + e];
+        else ((int32_t *)D.dst[o])[pos] = zn ? 0 : ((const int32_t *)D.col[c].data)[i0 + e];
         if (VAL && D.vdst[o]) D.vdst[o][pos] = (uint8_t)((D.col[c].valid[(i0 + e) >> 6] >> ((i0 + e) & 63)) & 1);
       }
       pos++;
@@ -1431,6 +1479,144 @@ void PackValidityBytes(const uint8_t *bytes, int64_t n, uint64_t *bits, hipStrea
   const int64_t words = (n + 63) / 64;
   hipLaunchKernelGGL(pack_validity_bytes_kernel, dim3((unsigned)((words * 4 + 255) / 256)), dim3(256), 0, s, bytes, n,
                      bits);
+}
+
+// Ballot-mode validity (SelectDesc::vbo): output word w of the bitmap from
+// the per-step ballots and the per-range first output rows, one thread per
+// word, each word written once (no shared partial words, no atomics).
+//   * the range holding output row 64 w: the last range R with vpos[R] <= 64 w
+//     (vpos is non-decreasing in range order, which is output order), found
+//     by galloping from the range a uniform spread would put it in;
+//   * inside R, the sub-steps in order (S H per range; the tail range holds
+//     the passes after nsteps H), each one's rows in row order: lane-major
+//     ballot words (bit l of word e = row 4 l + e) are interleaved into four
+//     64-row words (row 4 l + e of word k = bit 16 k + l of word e);
+//   * then the validity bits of the next 64 selected rows, in order.
+__device__ __forceinline__ uint64_t pv_spread16(uint64_t x) {  // bit i -> bit 4 i (16 bits)
+  x &= 0xFFFFull;
+  x = (x | (x << 24)) & 0x000000FF000000FFull;
+  x = (x | (x << 12)) & 0x000F000F000F000Full;
+  x = (x | (x << 6)) & 0x0303030303030303ull;
+  x = (x | (x << 3)) & 0x1111111111111111ull;
+  return x;
+}
+struct PvDesc {
+  const unsigned long long *vball;
+  const int64_t *vpos;
+  int64_t nranges;   // ranges of the rounds (the tail range is index nranges)
+  int64_t sub_per_range;  // S H
+  int64_t nsub_main;      // nsteps H: sub-steps of the rounds
+  int64_t nsub_tail;      // 256-row passes after them
+  int64_t n;              // selected rows
+};
+__global__ __launch_bounds__(256) void pack_validity_ballots_kernel(PvDesc d, uint64_t *__restrict__ bits) {
+  const int64_t w = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int64_t target = w * 64;
+  if (target >= d.n) return;
+  // the range: last R in [0, nranges] with vpos[R] <= target
+  const int64_t nr = d.nranges + 1;
+  int64_t lo = (int64_t)((double)target / (double)d.n * (double)nr);
+  lo = lo < 0 ? 0 : lo >= nr ? nr - 1 : lo;
+  int64_t hi;
+  if (d.vpos[lo] <= target) {  // gallop up: vpos[lo] <= target < vpos[hi] (hi = nr: past the end)
+    int64_t step = 1;
+    hi = lo + 1;
+    while (hi < nr && d.vpos[hi] <= target) {
+      lo = hi;
+      step <<= 1;
+      hi = lo + step;
+    }
+    if (hi > nr) hi = nr;
+  } else {  // gallop down
+    int64_t step = 1;
+    hi = lo;
+    lo = hi - 1;
+    while (lo > 0 && d.vpos[lo] > target) {
+      hi = lo;
+      step <<= 1;
+      lo = hi - step;
+    }
+    if (lo < 0) lo = 0;
+  }
+  while (hi - lo > 1) {  // vpos[lo] <= target < vpos[hi]
+    const int64_t m = (lo + hi) >> 1;
+    if (d.vpos[m] <= target) lo = m;
+    else hi = m;
+  }
+  int64_t R = lo, cur = d.vpos[R], j = 0;
+  // sub-step gs of (range R, index j), or -1 past the range's live sub-steps
+  auto sub = [&](int64_t RR, int64_t jj) -> int64_t {
+    if (RR < d.nranges) {
+      const int64_t gs = RR * d.sub_per_range + jj;
+      return jj < d.sub_per_range && gs < d.nsub_main ? gs : -1;
+    }
+    return jj < d.nsub_tail ? d.nsub_main + jj : -1;
+  };
+  uint64_t out = 0;
+  int got = 0;
+  const int want = (int)(d.n - target < 64 ? d.n - target : 64);
+  int64_t skip = target - cur;  // selected rows of R before the word's first
+  while (got < want) {
+    const int64_t gs = sub(R, j);
+    if (gs < 0) {  // next range
+      R++;
+      j = 0;
+      if (R > d.nranges) break;  // (cannot happen for a consistent launch)
+      continue;
+    }
+    const unsigned long long *bw = d.vball + 8 * gs;
+    const uint64_t s0 = bw[0], s1 = bw[1], s2 = bw[2], s3 = bw[3];
+    const int cnt = __popcll(s0) + __popcll(s1) + __popcll(s2) + __popcll(s3);
+    if (skip >= cnt) {
+      skip -= cnt;
+      j++;
+      continue;
+    }
+    const uint64_t v0 = bw[4], v1 = bw[5], v2 = bw[6], v3 = bw[7];
+    for (int k = 0; k < 4 && got < want; k++) {  // row-order word k: rows 64 k .. 64 k + 63 of the sub-step
+      const int sh = 16 * k;
+      uint64_t sel = pv_spread16(s0 >> sh) | (pv_spread16(s1 >> sh) << 1) | (pv_spread16(s2 >> sh) << 2) |
+                     (pv_spread16(s3 >> sh) << 3);
+      const uint64_t val = pv_spread16(v0 >> sh) | (pv_spread16(v1 >> sh) << 1) | (pv_spread16(v2 >> sh) << 2) |
+                           (pv_spread16(v3 >> sh) << 3);
+      const int pc = __popcll(sel);
+      if (skip >= pc) {
+        skip -= pc;
+        continue;
+      }
+      for (; skip > 0; skip--) sel &= sel - 1;  // drop the rows before the word's first
+      while (sel && got < want) {
+        const int t = __ffsll((unsigned long long)sel) - 1;
+        out |= ((val >> t) & 1ull) << got;
+        got++;
+        sel &= sel - 1;
+      }
+    }
+    j++;
+  }
+  bits[w] = out;
+}
+
+size_t SelectRangeCount(const SelectRoundsPlan &p) { return (size_t)p.nrounds * p.G * p.NL; }
+size_t SelectBallotWords(const SelectRoundsPlan &p, int64_t nrows) {
+  const int64_t nsteps = nrows / (256 * p.H);
+  return (size_t)(nsteps * p.H + (nrows - nsteps * 256 * p.H + 255) / 256) * 8 + 8;  // + the dump slot
+}
+
+void PackValidityBallots(const unsigned long long *vball, const int64_t *vpos, const SelectRoundsPlan &p,
+                         int64_t nrows, int64_t n, uint64_t *bits, hipStream_t s) {
+  if (n <= 0) return;
+  PvDesc d;
+  const int64_t nsteps = nrows / (256 * p.H);
+  d.vball = vball;
+  d.vpos = vpos;
+  d.nranges = (int64_t)SelectRangeCount(p);
+  d.sub_per_range = (int64_t)p.S * p.H;
+  d.nsub_main = nsteps * p.H;
+  d.nsub_tail = (nrows - nsteps * 256 * p.H + 255) / 256;
+  d.n = n;
+  const int64_t words = (n + 63) / 64;
+  hipLaunchKernelGGL(pack_validity_ballots_kernel, dim3((unsigned)((words + 255) / 256)), dim3(256), 0, s, d, bits);
 }
 
 hipError_t SelectRounds(const SelectDesc &d, const SelectRoundsPlan &p, int64_t nrows, unsigned long long *ctl,
