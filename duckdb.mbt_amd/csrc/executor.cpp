@@ -1160,11 +1160,11 @@ static bool TrySelectOnePass(Engine &e, const DRel &rel, const dev::FilterMultiD
   // values like a NULL-free output, the loaders store each step's ballots,
   // and PackValidityBallots builds the bitmap.  Only when the planner gives
   // the 8-loader H = 1 form, and the column feeds no other output.
-  // MBX_SR_VBALL=0 keeps the sentinel / byte forms (A/B).
+  // MBX_SR_VBALL=1 turns it on (default off until measured on the GPU).
   int vb_k = -1;
   if (mode != 2) {
     const char *vbk = Knob("MBX_SR_VBALL");
-    if (!(vbk && atoi(vbk) == 0))
+    if (vbk && atoi(vbk) == 1)
       for (int k = 0; k < S.nout && vb_k < 0; k++) {
         const int i = S.out_col[k];
         if (!S.col[i].valid) continue;
