@@ -411,7 +411,7 @@ void PackValidityBytes(const uint8_t *bytes, int64_t n, uint64_t *bits, hipStrea
 // the bitmap of the ballot-mode output (SelectDesc::vbo) of a finished launch
 // of plan p over nrows input rows with n selected rows
 void PackValidityBallots(const unsigned long long *vball, const int64_t *vpos, const SelectRoundsPlan &p,
-                         int64_t nrows, int64_t n, uint64_t *bits, hipStream_t s);
+                         int64_t nrows, int64_t n, uint64_t *bits, int64_t *wmap, hipStream_t s);  // wmap: (n + 63) / 64 words of scratch
 // words of vball / vpos a launch of plan p over nrows rows writes (+ the dump
 // slot of dead steps)
 size_t SelectBallotWords(const SelectRoundsPlan &p, int64_t nrows);

@@ -1368,7 +1368,9 @@ static bool TrySelectOnePass(Engine &e, const DRel &rel, const dev::FilterMultiD
     if (k == S.vbo) {
       const int64_t nsub = (int64_t)dev::SelectBallotWords(plan, n) / 8;
       ProfScope ps(e, "pack_validity", (double)nsub * 64 + (double)dev::SelectRangeCount(plan) * 8 + nsel / 8.0, nsel);
-      dev::PackValidityBallots(S.vball, S.vpos, plan, n, nsel, (uint64_t *)cols[k].validity, e.stream);
+      auto wmap = Alloc(e, (size_t)((nsel + 63) / 64) * 8 + 8);
+      dev::PackValidityBallots(S.vball, S.vpos, plan, n, nsel, (uint64_t *)cols[k].validity, (int64_t *)wmap->p,
+                               e.stream);
       continue;
     }
     if (!S.vdst[k]) continue;

@@ -469,12 +469,12 @@ __device__ __forceinline__ unsigned long long lds_add_rtn(unsigned long long *p,
 // A storer's copy of staged rows t0w .. t0w + c - 1 (ring positions & mask) to
 // dst[0 .. c): 4 rows per lane per pass, so the 4 staging reads share one LDS
 // wait.
-// a storer's output store: non-temporal by default (the rows are written once
-// and not read back by this kernel); MBX_SR_NT_OFF makes them plain (A/B)
+// a storer's output store: non-temporal (the rows are written once and not
+// read back by this kernel; plain stores measured the same time and the same
+// WRITE_SIZE, profiles/r04_shapes_store_flavour_ab.log)
 template <typename T>
-__device__ __forceinline__ void sr_store(T v, T *p, bool nt) {
-  if (nt) __builtin_nontemporal_store(v, p);
-  else *p = v;
+__device__ __forceinline__ void sr_store(T v, T *p, bool) {
+  __builtin_nontemporal_store(v, p);
 }
 
 template <typename TS, typename TD>
@@ -1481,17 +1481,23 @@ void PackValidityBytes(const uint8_t *bytes, int64_t n, uint64_t *bits, hipStrea
                      bits);
 }
 
-// Ballot-mode validity (SelectDesc::vbo): output word w of the bitmap from
-// the per-step ballots and the per-range first output rows, one thread per
-// word, each word written once (no shared partial words, no atomics).
-//   * the range holding output row 64 w: the last range R with vpos[R] <= 64 w
-//     (vpos is non-decreasing in range order, which is output order), found
-//     by galloping from the range a uniform spread would put it in;
-//   * inside R, the sub-steps in order (S H per range; the tail range holds
-//     the passes after nsteps H), each one's rows in row order: lane-major
-//     ballot words (bit l of word e = row 4 l + e) are interleaved into four
-//     64-row words (row 4 l + e of word k = bit 16 k + l of word e);
-//   * then the validity bits of the next 64 selected rows, in order.
+// Ballot-mode validity (SelectDesc::vbo): the output bitmap from the
+// per-step ballots and the per-range first output rows, in two kernels.
+//  * ballot_word_map, one thread per 256-row sub-step gs: its first output row
+//    p (the range's row + the selected rows of the range's earlier
+//    sub-steps) and its count c; for every output word w whose first row 64 w
+//    falls in [p, p + c) it records (gs, 64 w - p) -- each word is recorded by
+//    exactly one sub-step.  Sub-step order is output order (ranges in order,
+//    sub-steps within a range, then the tail), so a word's later rows are in
+//    gs + 1, gs + 2, ...
+//  * pack_validity_ballots, one thread per output word: from (gs, rank) it
+//    interleaves each sub-step's lane-major ballots into row order (bit l of
+//    word e = row 4 l + e; row-order word k = rows 64 k .. 64 k + 63) and
+//    compresses the validity bits of the selected rows (a 6-step software
+//    pext), until it has the word's 64 rows.  Every word is written once: no
+//    atomics, no shared partial words.  (A first form, one thread per word
+//    with a galloping search over the range rows and a bit-serial gather,
+//    took 1.02 ms at 1e9 rows: profiles/r04_vball_kernel_stats.csv.)
 __device__ __forceinline__ uint64_t pv_spread16(uint64_t x) {  // bit i -> bit 4 i (16 bits)
   x &= 0xFFFFull;
   x = (x | (x << 24)) & 0x000000FF000000FFull;
@@ -1500,99 +1506,82 @@ __device__ __forceinline__ uint64_t pv_spread16(uint64_t x) {  // bit i -> bit 4
   x = (x | (x << 3)) & 0x1111111111111111ull;
   return x;
 }
+__device__ __forceinline__ uint64_t pv_compress(uint64_t x, uint64_t m) {  // the bits of x at m's set bits, packed low
+  x &= m;
+  uint64_t mk = ~m << 1;
+#pragma unroll
+  for (int i = 0; i < 6; i++) {
+    uint64_t mp = mk ^ (mk << 1);
+    mp ^= mp << 2;
+    mp ^= mp << 4;
+    mp ^= mp << 8;
+    mp ^= mp << 16;
+    mp ^= mp << 32;
+    const uint64_t mv = mp & m;
+    m = (m ^ mv) | (mv >> (1 << i));
+    const uint64_t t = x & mv;
+    x = (x ^ t) | (t >> (1 << i));
+    mk &= ~mp;
+  }
+  return x;
+}
 struct PvDesc {
   const unsigned long long *vball;
   const int64_t *vpos;
-  int64_t nranges;   // ranges of the rounds (the tail range is index nranges)
-  int64_t sub_per_range;  // S H
-  int64_t nsub_main;      // nsteps H: sub-steps of the rounds
-  int64_t nsub_tail;      // 256-row passes after them
-  int64_t n;              // selected rows
+  int64_t *wmap;           // per output word: (gs << 8) | rank of its first row in gs
+  int64_t nranges;         // ranges of the rounds (the tail range is index nranges)
+  int64_t sub_per_range;   // S H
+  int64_t nsub_main;       // nsteps H: sub-steps of the rounds
+  int64_t nsub_tail;       // 256-row passes after them
+  int64_t n;               // selected rows
 };
+__device__ __forceinline__ int pv_count(const unsigned long long *bw) {
+  return __popcll(bw[0]) + __popcll(bw[1]) + __popcll(bw[2]) + __popcll(bw[3]);
+}
+__global__ __launch_bounds__(256) void ballot_word_map_kernel(PvDesc d) {
+  const int64_t gs = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (gs >= d.nsub_main + d.nsub_tail) return;
+  int64_t R, j0;
+  if (gs < d.nsub_main) R = gs / d.sub_per_range, j0 = R * d.sub_per_range;
+  else R = d.nranges, j0 = d.nsub_main;
+  int64_t p = d.vpos[R];
+  for (int64_t q = j0; q < gs; q++) p += pv_count(d.vball + 8 * q);
+  const int64_t c = pv_count(d.vball + 8 * gs);
+  for (int64_t w = (p + 63) >> 6; 64 * w < p + c; w++) d.wmap[w] = (gs << 8) | (64 * w - p);
+}
 __global__ __launch_bounds__(256) void pack_validity_ballots_kernel(PvDesc d, uint64_t *__restrict__ bits) {
   const int64_t w = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   const int64_t target = w * 64;
   if (target >= d.n) return;
-  // the range: last R in [0, nranges] with vpos[R] <= target
-  const int64_t nr = d.nranges + 1;
-  int64_t lo = (int64_t)((double)target / (double)d.n * (double)nr);
-  lo = lo < 0 ? 0 : lo >= nr ? nr - 1 : lo;
-  int64_t hi;
-  if (d.vpos[lo] <= target) {  // gallop up: vpos[lo] <= target < vpos[hi] (hi = nr: past the end)
-    int64_t step = 1;
-    hi = lo + 1;
-    while (hi < nr && d.vpos[hi] <= target) {
-      lo = hi;
-      step <<= 1;
-      hi = lo + step;
-    }
-    if (hi > nr) hi = nr;
-  } else {  // gallop down
-    int64_t step = 1;
-    hi = lo;
-    lo = hi - 1;
-    while (lo > 0 && d.vpos[lo] > target) {
-      hi = lo;
-      step <<= 1;
-      lo = hi - step;
-    }
-    if (lo < 0) lo = 0;
-  }
-  while (hi - lo > 1) {  // vpos[lo] <= target < vpos[hi]
-    const int64_t m = (lo + hi) >> 1;
-    if (d.vpos[m] <= target) lo = m;
-    else hi = m;
-  }
-  int64_t R = lo, cur = d.vpos[R], j = 0;
-  // sub-step gs of (range R, index j), or -1 past the range's live sub-steps
-  auto sub = [&](int64_t RR, int64_t jj) -> int64_t {
-    if (RR < d.nranges) {
-      const int64_t gs = RR * d.sub_per_range + jj;
-      return jj < d.sub_per_range && gs < d.nsub_main ? gs : -1;
-    }
-    return jj < d.nsub_tail ? d.nsub_main + jj : -1;
-  };
+  const int64_t m = d.wmap[w];
+  int64_t gs = m >> 8;
+  int off = (int)(m & 255);
+  const int want = (int)(d.n - target < 64 ? d.n - target : 64);
+  const int64_t nsub = d.nsub_main + d.nsub_tail;
   uint64_t out = 0;
   int got = 0;
-  const int want = (int)(d.n - target < 64 ? d.n - target : 64);
-  int64_t skip = target - cur;  // selected rows of R before the word's first
-  while (got < want) {
-    const int64_t gs = sub(R, j);
-    if (gs < 0) {  // next range
-      R++;
-      j = 0;
-      if (R > d.nranges) break;  // (cannot happen for a consistent launch)
-      continue;
-    }
+  for (; got < want && gs < nsub; gs++, off = 0) {
     const unsigned long long *bw = d.vball + 8 * gs;
     const uint64_t s0 = bw[0], s1 = bw[1], s2 = bw[2], s3 = bw[3];
-    const int cnt = __popcll(s0) + __popcll(s1) + __popcll(s2) + __popcll(s3);
-    if (skip >= cnt) {
-      skip -= cnt;
-      j++;
-      continue;
-    }
+    if (__popcll(s0) + __popcll(s1) + __popcll(s2) + __popcll(s3) <= off) continue;  // (only an empty sub-step)
     const uint64_t v0 = bw[4], v1 = bw[5], v2 = bw[6], v3 = bw[7];
-    for (int k = 0; k < 4 && got < want; k++) {  // row-order word k: rows 64 k .. 64 k + 63 of the sub-step
+    for (int k = 0; k < 4 && got < want; k++) {
       const int sh = 16 * k;
-      uint64_t sel = pv_spread16(s0 >> sh) | (pv_spread16(s1 >> sh) << 1) | (pv_spread16(s2 >> sh) << 2) |
-                     (pv_spread16(s3 >> sh) << 3);
-      const uint64_t val = pv_spread16(v0 >> sh) | (pv_spread16(v1 >> sh) << 1) | (pv_spread16(v2 >> sh) << 2) |
-                           (pv_spread16(v3 >> sh) << 3);
-      const int pc = __popcll(sel);
-      if (skip >= pc) {
-        skip -= pc;
+      const uint64_t sel = pv_spread16(s0 >> sh) | (pv_spread16(s1 >> sh) << 1) | (pv_spread16(s2 >> sh) << 2) |
+                           (pv_spread16(s3 >> sh) << 3);
+      const int c = __popcll(sel);
+      if (off >= c) {
+        off -= c;
         continue;
       }
-      for (; skip > 0; skip--) sel &= sel - 1;  // drop the rows before the word's first
-      while (sel && got < want) {
-        const int t = __ffsll((unsigned long long)sel) - 1;
-        out |= ((val >> t) & 1ull) << got;
-        got++;
-        sel &= sel - 1;
-      }
+      const uint64_t val = pv_spread16(v0 >> sh) | (pv_spread16(v1 >> sh) << 1) | (pv_spread16(v2 >> sh) << 2) |
+                           (pv_spread16(v3 >> sh) << 3);
+      const uint64_t b = pv_compress(val, sel) >> off;
+      const int take = c - off < want - got ? c - off : want - got;
+      out |= (take >= 64 ? b : (b & ((1ull << take) - 1))) << got;
+      got += take;
+      off = 0;
     }
-    j++;
   }
   bits[w] = out;
 }
@@ -1604,18 +1593,20 @@ size_t SelectBallotWords(const SelectRoundsPlan &p, int64_t nrows) {
 }
 
 void PackValidityBallots(const unsigned long long *vball, const int64_t *vpos, const SelectRoundsPlan &p,
-                         int64_t nrows, int64_t n, uint64_t *bits, hipStream_t s) {
+                         int64_t nrows, int64_t n, uint64_t *bits, int64_t *wmap, hipStream_t s) {
   if (n <= 0) return;
   PvDesc d;
   const int64_t nsteps = nrows / (256 * p.H);
   d.vball = vball;
   d.vpos = vpos;
+  d.wmap = wmap;
   d.nranges = (int64_t)SelectRangeCount(p);
   d.sub_per_range = (int64_t)p.S * p.H;
   d.nsub_main = nsteps * p.H;
   d.nsub_tail = (nrows - nsteps * 256 * p.H + 255) / 256;
   d.n = n;
-  const int64_t words = (n + 63) / 64;
+  const int64_t nsub = d.nsub_main + d.nsub_tail, words = (n + 63) / 64;
+  hipLaunchKernelGGL(ballot_word_map_kernel, dim3((unsigned)((nsub + 255) / 256)), dim3(256), 0, s, d);
   hipLaunchKernelGGL(pack_validity_ballots_kernel, dim3((unsigned)((words + 255) / 256)), dim3(256), 0, s, d, bits);
 }
 
