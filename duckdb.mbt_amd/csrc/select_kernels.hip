@@ -555,6 +555,41 @@ __device__ __forceinline__ void sr_copy_sent(const TS *st, uint32_t t0w, uint32_
   }
 }
 
+// A storer's copy of its two loaders' ranges of a round as one stream (8
+// loaders, one output): rows i < cA come from loader A's staging and go to
+// dA + i, the rest from B's to dB + i - cA.  4 rows per lane per pass over the
+// joined ranges, so the ~2 x 130 rows of a one-step round take 2 LDS waits
+// instead of 6 (each range's last pass was mostly empty).  SENT: a
+// sentinel-staged NULL-able output (0 and a validity byte of 0 under NULL).
+template <typename TS, typename TD, bool SENT>
+__device__ __forceinline__ void sr_copy2(const TS *stA, uint32_t tA, TD *dA, uint8_t *vA, uint32_t cA, const TS *stB,
+                                         uint32_t tB, TD *dB, uint8_t *vB, uint32_t cB, uint32_t mask, int lane, TS sent) {
+  const uint32_t c = cA + cB;
+  for (uint32_t i = lane; i < c; i += 256) {
+    TS x[4];
+#pragma unroll
+    for (int u = 0; u < 4; u++) {  // (reads past c stay inside the staging ring and are not used)
+      const uint32_t r = i + 64 * u;
+      x[u] = r < cA ? stA[(tA + r) & mask] : stB[(tB + r - cA) & mask];
+    }
+#pragma unroll
+    for (int u = 0; u < 4; u++) {
+      const uint32_t r = i + 64 * u;
+      if (r < c) {
+        const bool a = r < cA;
+        TD *d = a ? dA + r : dB + (r - cA);
+        if constexpr (SENT) {
+          const bool ok = x[u] != sent;
+          __builtin_nontemporal_store((TD)(ok ? x[u] : (TS)0), d);
+          __builtin_nontemporal_store((uint8_t)ok, a ? vA + r : vB + (r - cA));
+        } else {
+          __builtin_nontemporal_store((TD)x[u], d);
+        }
+      }
+    }
+  }
+}
+
 // NC loaded columns; bit c of WM: column c is 8 bytes wide (else 4).
 template <int NC, int WM>
 struct SrCols {
@@ -983,8 +1018,58 @@ __global__ __launch_bounds__((NL + 5) * 64) void select_rounds_kernel(SelectDesc
       asm volatile("ds_read_b32 %0, %1\n\ts_waitcnt lgkmcnt(0)" : "=v"(cl) : "v"(lds_addr(&sm.cnt[slot][lane & 7])) : "memory");
       if (dbg) t1 = clock64();
       int q = 0;
+      // 8 loaders, one output without staged validity bytes: both loaders'
+      // ranges in one stream (sr_copy2; MBX_SR_COPY1 != 0 keeps the per-range copies)
+      bool merged = false;
+      if constexpr (PER == 2) {
+        const int oc = D.out_col[0];
+        bool vs = false, vbyte = false;
+        if constexpr (VAL) {
+          vs = D.vdst[0] && D.col[oc].vsent;
+          vbyte = D.vdst[0] && !D.col[oc].vsent;
+        }
+        if (D.nout == 1 && D.copy1 == 0 && !vbyte && !((zsmask >> oc) & 1)) {
+          merged = true;
+          const int lA = sw, lB = sw + 4;
+          int64_t pA = pos, pB;
+          for (int qq = 0; qq < lA; qq++) pA += (uint32_t)__builtin_amdgcn_readlane((int)cl, qq);
+          pB = pA;
+          for (int qq = lA; qq < lB; qq++) pB += (uint32_t)__builtin_amdgcn_readlane((int)cl, qq);
+          const uint32_t cA = (uint32_t)__builtin_amdgcn_readlane((int)cl, lA);
+          const uint32_t cB = (uint32_t)__builtin_amdgcn_readlane((int)cl, lB);
+          if (VAL && NL == 8 && D.vball && lane == 0) {  // ballot mode: the ranges' first output rows
+            D.vpos[(r * G + g) * NL + lA] = pA;
+            D.vpos[(r * G + g) * NL + lB] = pB;
+          }
+          int so = 0;
+          bool s8 = false;
 #pragma unroll
-      for (int j = 0; j < PER; j++) {
+          for (int cc = 0; cc < NC; cc++)
+            if (cc == oc) so = soff[cc], s8 = st8[cc];
+          const unsigned char *sA = stage0 + (size_t)lA * (stg + 64) * rowb + so;
+          const unsigned char *sB = stage0 + (size_t)lB * (stg + 64) * rowb + so;
+          uint8_t *vA = vs ? D.vdst[0] + pA : nullptr, *vB = vs ? D.vdst[0] + pB : nullptr;
+          if (s8) {
+            if (vs) sr_copy2<int64_t, int64_t, true>((const int64_t *)sA, tail[0], (int64_t *)D.dst[0] + pA, vA, cA, (const int64_t *)sB, tail[1], (int64_t *)D.dst[0] + pB, vB, cB, mask, lane, D.col[oc].sent);
+            else sr_copy2<int64_t, int64_t, false>((const int64_t *)sA, tail[0], (int64_t *)D.dst[0] + pA, vA, cA, (const int64_t *)sB, tail[1], (int64_t *)D.dst[0] + pB, vB, cB, mask, lane, 0);
+          } else if (D.col[oc].w == 8) {  // staged narrow: sign-extend back to int64
+            if (vs) sr_copy2<int32_t, int64_t, true>((const int32_t *)sA, tail[0], (int64_t *)D.dst[0] + pA, vA, cA, (const int32_t *)sB, tail[1], (int64_t *)D.dst[0] + pB, vB, cB, mask, lane, (int32_t)D.col[oc].sent);
+            else sr_copy2<int32_t, int64_t, false>((const int32_t *)sA, tail[0], (int64_t *)D.dst[0] + pA, vA, cA, (const int32_t *)sB, tail[1], (int64_t *)D.dst[0] + pB, vB, cB, mask, lane, 0);
+          } else {
+            if (vs) sr_copy2<int32_t, int32_t, true>((const int32_t *)sA, tail[0], (int32_t *)D.dst[0] + pA, vA, cA, (const int32_t *)sB, tail[1], (int32_t *)D.dst[0] + pB, vB, cB, mask, lane, (int32_t)D.col[oc].sent);
+            else sr_copy2<int32_t, int32_t, false>((const int32_t *)sA, tail[0], (int32_t *)D.dst[0] + pA, vA, cA, (const int32_t *)sB, tail[1], (int32_t *)D.dst[0] + pB, vB, cB, mask, lane, 0);
+          }
+          asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // staging read before it is freed
+          tail[0] += cA;
+          tail[1] += cB;
+          if (lane == 0) {
+            lds_st_nw(&sm.tail[lA], tail[0]);
+            lds_st_nw(&sm.tail[lB], tail[1]);
+          }
+        }
+      }
+#pragma unroll
+      for (int j = 0; j < PER && !merged; j++) {
         const int l = sw + 4 * j;
         for (; q < l; q++) pos += (uint32_t)__builtin_amdgcn_readlane((int)cl, q);
         const uint32_t c = (uint32_t)__builtin_amdgcn_readlane((int)cl, l);
