@@ -556,7 +556,7 @@ __device__ __forceinline__ void sr_copy_sent(const TS *st, uint32_t t0w, uint32_
 }
 
 // A storer's copy of its two loaders' ranges of a round as one stream (8
-// loaders, one output): rows i < cA come from loader A's staging and go to
+// loaders, one sentinel-staged NULL-able output): rows i < cA come from loader A's staging and go to
 // dA + i, the rest from B's to dB + i - cA.  4 rows per lane per pass over the
 // joined ranges, so the ~2 x 130 rows of a one-step round take 2 LDS waits
 // instead of 6 (each range's last pass was mostly empty).  SENT: a
@@ -568,9 +568,10 @@ __device__ __forceinline__ void sr_copy2(const TS *stA, uint32_t tA, TD *dA, uin
   for (uint32_t i = lane; i < c; i += 256) {
     TS x[4];
 #pragma unroll
-    for (int u = 0; u < 4; u++) {  // (reads past c stay inside the staging ring and are not used)
+    for (int u = 0; u < 4; u++) {  // one LDS read per row (reads past c stay inside the staging ring, unused)
       const uint32_t r = i + 64 * u;
-      x[u] = r < cA ? stA[(tA + r) & mask] : stB[(tB + r - cA) & mask];
+      const TS *p = r < cA ? stA + ((tA + r) & mask) : stB + ((tB + r - cA) & mask);
+      x[u] = *p;
     }
 #pragma unroll
     for (int u = 0; u < 4; u++) {
@@ -1028,7 +1029,9 @@ __global__ __launch_bounds__((NL + 5) * 64) void select_rounds_kernel(SelectDesc
           vs = D.vdst[0] && D.col[oc].vsent;
           vbyte = D.vdst[0] && !D.col[oc].vsent;
         }
-        if (D.nout == 1 && D.copy1 == 0 && !vbyte && !((zsmask >> oc) & 1)) {
+        // (sentinel-staged NULL-able outputs only: SELECT vn ... WHERE x > 24 3.91 -> 3.62 ms, but the
+        // NULL-free SELECT v ... WHERE x > 24 3.27 -> 3.46, profiles/r04_storer_merged_ab.log)
+        if (D.nout == 1 && D.copy1 == 0 && vs && !vbyte && !((zsmask >> oc) & 1)) {
           merged = true;
           const int lA = sw, lB = sw + 4;
           int64_t pA = pos, pB;
