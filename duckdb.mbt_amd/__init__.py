@@ -88,6 +88,7 @@ _sig("duckdb_mbx_shard_partial", _P, _P, _I)
 _sig("duckdb_mbx_rccl_stats", _I, _P, ctypes.POINTER(ctypes.c_int64), ctypes.POINTER(ctypes.c_double))
 _sig("duckdb_mbx_rccl_note", ctypes.c_void_p, _P)
 _sig("duckdb_mbx_set_combine", _I, _P, _I)
+_sig("duckdb_mbx_rccl_stats_ex", _I, _P, ctypes.POINTER(ctypes.c_int64), _I)
 _sig("duckdb_mbx_combine_lanes", _I, ctypes.POINTER(ctypes.c_int64), _I, _I, ctypes.POINTER(ctypes.c_int8),
      ctypes.POINTER(ctypes.c_int64))
 
@@ -627,14 +628,21 @@ class Connection:
         out = (ctypes.c_int64 * 2)()
         us = (ctypes.c_double * 1)()
         lib.duckdb_mbx_rccl_stats(self._h, out, us)
+        ex = (ctypes.c_int64 * 4)()
+        lib.duckdb_mbx_rccl_stats_ex(self._h, ex, 4)
         p = lib.duckdb_mbx_rccl_note(self._h)
         note = ctypes.string_at(p).decode()
         lib.duckdb_mbx_free(p)
-        return {"rccl_combines": out[0], "rccl_fallbacks": out[1], "last_rccl_us": us[0], "note": note}
+        return {"rccl_combines": out[0], "rccl_fallbacks": out[1], "rccl_loopbacks": ex[2], "rccl_errors": ex[3],
+                "last_rccl_us": us[0], "note": note}
 
-    def set_combine(self, rccl: bool) -> None:
-        """Host merge (False) or RCCL combine (True) from the next statement on."""
-        lib.duckdb_mbx_set_combine(self._h, 1 if rccl else 0)
+    def set_combine(self, rccl) -> None:
+        """Host merge (False / "host"), RCCL combine (True / "rccl") or, in tests
+        with MBX_EXPERIMENTS=1, the RCCL combine over device copies instead of
+        the collectives ("rccl_loopback"), from the next statement on."""
+        mode = {"host": 0, "rccl": 1, "rccl_loopback": 2}[rccl] if isinstance(rccl, str) else (1 if rccl else 0)
+        if not lib.duckdb_mbx_set_combine(self._h, mode):
+            raise ValueError(f"mbx_combine mode {rccl!r} refused (the loopback needs MBX_EXPERIMENTS=1)")
 
     def profile_drain(self) -> list:
         import json

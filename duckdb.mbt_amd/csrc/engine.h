@@ -129,6 +129,10 @@ struct Options {
   // distinct devices combines its partials with RCCL collectives on the shard
   // devices (rccl_combine.h) instead of the host merge
   bool combine_rccl = false;
+  // "mbx_combine" = "rccl_loopback" (tests only, MBX_EXPERIMENTS=1): the RCCL
+  // combine with its two collectives replaced by device copies between the
+  // shards' lane buffers, so it runs over same-device shards on one GPU
+  bool rccl_loopback = false;
   std::map<std::string, std::string> raw;
 };
 
@@ -161,6 +165,8 @@ struct ShardStats {
   // mbx_combine=rccl: sharded global aggregates combined by RCCL collectives
   // on the shard devices instead of the host merge
   int64_t rccl_combines = 0, rccl_fallbacks = 0;
+  int64_t rccl_loopbacks = 0;  // of rccl_combines, through the test loopback
+  int64_t rccl_errors = 0;     // combines that raised a shard's device error
   double last_rccl_us = 0;
   std::string rccl_note;  // why the last rccl request fell back (empty: it ran)
 };

@@ -4117,28 +4117,36 @@ static bool ShardedAggregateRccl(Connection &c, const BoundSelect &s, const Boun
       default: return fallback("aggregate without an integer partial: host merge");
     }
   }
+  if (c.rccl && rc::IsLoopback(*c.rccl) != c.opts.rccl_loopback) c.rccl.reset(), c.rccl_tried = false;
   if (!c.rccl_tried) {
     c.rccl_tried = true;
     std::string note;
-    c.rccl = rc::Open(c.opts.devices, &note);
+    c.rccl = rc::Open(c.opts.devices, c.opts.rccl_loopback, &note);
     if (!c.rccl) st.rccl_note = note;
   }
   if (!c.rccl) return fallback(st.rccl_note.empty() ? "RCCL unavailable" : st.rccl_note);
   const Table &t = *s.src.table;
   const int nsh = (int)t.parts.size();
+  if (nsh != (int)c.rccl->devs.size()) return fallback("table parts do not match the shard devices: host merge");
   const int P = rc::LanesPerRank(ncols, counts_only);
   const size_t recv_lanes = counts_only ? (size_t)P : (size_t)nsh * P;
   cd.ncols = ncols;
   cd.nranks = nsh;
   Engine &e = *c.engine;
   std::vector<int64_t> host(recv_lanes + 3 * ncols);
-  double t_coll = 0;
+  // Phase 1, on every shard at once: the partial row, its shape checks, the
+  // lane buffers and the pack.  Anything that can fail happens here, before
+  // any rank enters the collective, so an error cannot leave the other ranks
+  // waiting inside it (ForShards re-raises it naming the shard).
+  std::vector<DRel> rel(nsh);
+  std::vector<DevBufPtr> sendb(nsh), recvb(nsh), scrb(nsh);
   ForShards(c, [&](int i) {
     Connection &sc = *c.shards[i];
     Engine &se = ShardEngine(c, sc);
     BoundSelect pi = p;
     pi.src.table = t.parts[i];
-    DRel r = RunBranch(se, sc, pi);
+    rel[i] = RunBranch(se, sc, pi);
+    const DRel &r = rel[i];
     if (r.n != 1 || (int)r.cols.size() < ncols) ThrowError("Internal", "RCCL combine: partial row shape");
     rc::PackDesc pd;
     memset(&pd, 0, sizeof(pd));
@@ -4153,67 +4161,91 @@ static bool ShardedAggregateRccl(Connection &c, const BoundSelect &s, const Boun
     pd.ncols = ncols;
     pd.counts_only = counts_only;
     pd.err = se.d_err;
-    auto send = Alloc(se, (size_t)P * 8);
-    auto recv = Alloc(se, recv_lanes * 8);
-    rc::Pack(pd, (int64_t *)send->p, se.stream);
+    sendb[i] = Alloc(se, (size_t)P * 8);
+    recvb[i] = Alloc(se, recv_lanes * 8);
+    if (counts_only && c.rccl->loopback) scrb[i] = Alloc(se, (size_t)nsh * P * 8);
+    if (i == 0 && !se.EnsurePinned(host.size() * 8)) ThrowError("IO", "RCCL combine: pinned staging");
+    rc::Pack(pd, (int64_t *)sendb[i]->p, se.stream);
+    HIPCHK(hipGetLastError());
     MarkLaunched(c, i);
-    const auto tc0 = std::chrono::steady_clock::now();
-    std::string err;
-    const bool ok = counts_only ? rc::AllReduceSum(*c.rccl, i, (const int64_t *)send->p, (int64_t *)recv->p, P,
-                                                   se.stream, &err)
-                                : rc::AllGather(*c.rccl, i, (const int64_t *)send->p, (int64_t *)recv->p, P,
-                                                se.stream, &err);
-    if (!ok) ThrowError("IO", err);
-    if (i == 0) {
-      DevBufPtr out;
-      if (!counts_only) {
-        out = Alloc(se, (size_t)3 * ncols * 8);
-        rc::Combine(cd, (const int64_t *)recv->p, (int64_t *)out->p, se.stream);
-      }
-      const size_t need = host.size() * 8;
-      if (!se.EnsurePinned(need)) ThrowError("IO", "RCCL combine: pinned staging");
-      HIPCHK(hipMemcpyAsync(se.h_pinned, recv->p, recv_lanes * 8, hipMemcpyDeviceToHost, se.stream));
-      if (out)
-        HIPCHK(hipMemcpyAsync(se.h_pinned + recv_lanes * 8, out->p, (size_t)3 * ncols * 8, hipMemcpyDeviceToHost,
-                              se.stream));
-      HIPCHK(hipStreamSynchronize(se.stream));  // every rank's part of the collective has landed
-      memcpy(host.data(), se.h_pinned, need);
-      t_coll = std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - tc0).count();
-    } else if (se.profile) {
-      HIPCHK(hipStreamSynchronize(se.stream));  // (the kernel events must have completed)
-    }
-    ShardCollect(e, se, i, true);
   });
-  Eng(c);
-  const auto t_merge = std::chrono::steady_clock::now();
-  // every rank's device error word, raised as that shard's error
-  for (int i = 0; i < (counts_only ? 1 : nsh); i++) {
-    const int64_t err = host[(size_t)i * P + P - 1];
-    if (!err) continue;
-    if (counts_only) {  // the summed words only say some shard failed: ask each one
-      for (int k = 0; k < nsh; k++) {
-        Engine &se = Eng(*c.shards[k]);
-        try {
-          CheckError(se);
-        } catch (std::exception &ex) {
-          Eng(c);
-          throw EngineError(std::string(ex.what()) + " (shard " + std::to_string(k) + " of " + std::to_string(nsh) +
-                            ", device " + std::to_string(c.shards[k]->opts.device) + ")");
+  // Phase 2, on this thread: the one collective over every rank's stream
+  const auto tc0 = std::chrono::steady_clock::now();
+  std::vector<const int64_t *> sp(nsh);
+  std::vector<int64_t *> rp(nsh), xp(nsh);
+  std::vector<hipStream_t> streams(nsh);
+  for (int i = 0; i < nsh; i++) {
+    sp[i] = (const int64_t *)sendb[i]->p;
+    rp[i] = (int64_t *)recvb[i]->p;
+    xp[i] = scrb[i] ? (int64_t *)scrb[i]->p : nullptr;
+    streams[i] = c.shards[i]->engine->stream;
+  }
+  std::string cerr;
+  const bool cok = rc::Collective(*c.rccl, counts_only, sp, rp, xp, streams, (size_t)P, &cerr);
+  // Phase 3: device 0 finishes (combine kernel, one D2H); every rank's stream
+  // is drained before its lane buffers go back to its pool
+  std::exception_ptr first_err;
+  for (int i = 0; i < nsh; i++) {
+    Engine &se = Eng(*c.shards[i]);
+    try {
+      if (cok && i == 0) {
+        DevBufPtr out;
+        if (!counts_only) {
+          out = Alloc(se, (size_t)3 * ncols * 8);
+          rc::Combine(cd, (const int64_t *)recvb[0]->p, (int64_t *)out->p, se.stream);
+          HIPCHK(hipGetLastError());
         }
+        HIPCHK(hipMemcpyAsync(se.h_pinned, recvb[0]->p, recv_lanes * 8, hipMemcpyDeviceToHost, se.stream));
+        if (out)
+          HIPCHK(hipMemcpyAsync(se.h_pinned + recv_lanes * 8, out->p, (size_t)3 * ncols * 8, hipMemcpyDeviceToHost,
+                                se.stream));
+        HIPCHK(hipStreamSynchronize(se.stream));  // every rank's part of the collective has landed
+        memcpy(host.data(), se.h_pinned, host.size() * 8);
+        out.reset();
+      } else {
+        HIPCHK(hipStreamSynchronize(se.stream));
       }
-      Eng(c);
-      ThrowError("Internal", "RCCL combine: a shard reported a device error");
+      ShardCollect(e, se, i, true);
+    } catch (...) {
+      if (!first_err) first_err = std::current_exception();
     }
+    sendb[i].reset(), recvb[i].reset(), scrb[i].reset();
+    rel[i] = DRel();
+  }
+  Eng(c);
+  const double t_coll = std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - tc0).count();
+  if (first_err) std::rethrow_exception(first_err);
+  if (!cok) ThrowError("IO", cerr);
+  const auto t_merge = std::chrono::steady_clock::now();
+  // every rank's device error word, raised as that shard's error; every
+  // shard that reported one is cleared, so no stale error reaches its next query
+  std::vector<int32_t> errs(nsh, 0);
+  if (counts_only) {
+    if (host[(size_t)P - 1]) {  // the summed words only say some shard failed: read each one
+      for (int k = 0; k < nsh; k++) errs[k] = ReadDev<int32_t>(Eng(*c.shards[k]), c.shards[k]->engine->d_err);
+      Eng(c);
+    }
+  } else {
+    for (int i = 0; i < nsh; i++) errs[i] = (int32_t)host[(size_t)i * P + P - 1];
+  }
+  int bad = -1;
+  for (int i = 0; i < nsh; i++) {
+    if (!errs[i]) continue;
+    if (bad < 0) bad = i;
     Engine &se = Eng(*c.shards[i]);
     HIPCHK(hipMemsetAsync(se.d_err, 0, sizeof(int32_t), se.stream));
     HIPCHK(hipStreamSynchronize(se.stream));
-    Eng(c);
+  }
+  Eng(c);
+  if (bad >= 0) {
+    st.rccl_errors++;
     try {
-      RaiseDeviceError(e, (int32_t)err);
+      RaiseDeviceError(e, errs[bad]);
     } catch (std::exception &ex) {
-      throw EngineError(std::string(ex.what()) + " (shard " + std::to_string(i) + " of " + std::to_string(nsh) +
-                        ", device " + std::to_string(c.shards[i]->opts.device) + ")");
+      throw EngineError(std::string(ex.what()) + " (shard " + std::to_string(bad) + " of " + std::to_string(nsh) +
+                        ", device " + std::to_string(c.shards[bad]->opts.device) + ")");
     }
+    ThrowError("Internal", "RCCL combine: a shard reported a device error");
   }
   // the combined partial row, then the aggregates finished as the host merge does
   std::vector<Value> part(ncols);
@@ -4250,6 +4282,7 @@ static bool ShardedAggregateRccl(Connection &c, const BoundSelect &s, const Boun
     }
   }
   st.rccl_combines++;
+  if (c.rccl->loopback) st.rccl_loopbacks++;
   st.rccl_note.clear();
   st.last_rccl_us = t_coll;
   st.last_combine_us = std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t_merge).count();

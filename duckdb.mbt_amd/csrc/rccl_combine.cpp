@@ -22,6 +22,8 @@ struct Api {
   decltype(&ncclAllGather) allgather = nullptr;
   decltype(&ncclAllReduce) allreduce = nullptr;
   decltype(&ncclGetErrorString) errstr = nullptr;
+  decltype(&ncclGroupStart) gstart = nullptr;
+  decltype(&ncclGroupEnd) gend = nullptr;
 };
 
 const Api &GetApi() {
@@ -43,7 +45,9 @@ const Api &GetApi() {
     api.allgather = (decltype(api.allgather))dlsym(h, "ncclAllGather");
     api.allreduce = (decltype(api.allreduce))dlsym(h, "ncclAllReduce");
     api.errstr = (decltype(api.errstr))dlsym(h, "ncclGetErrorString");
-    api.ok = api.init && api.destroy && api.allgather && api.allreduce && api.errstr;
+    api.gstart = (decltype(api.gstart))dlsym(h, "ncclGroupStart");
+    api.gend = (decltype(api.gend))dlsym(h, "ncclGroupEnd");
+    api.ok = api.init && api.destroy && api.allgather && api.allreduce && api.errstr && api.gstart && api.gend;
     if (!api.ok) api.why = "librccl lacks an entry point";
   });
   return api;
@@ -54,17 +58,20 @@ std::string ErrText(const Api &a, ncclResult_t r) {
 }
 }  // namespace
 
-struct Comms {
-  std::vector<int> devs;
-  std::vector<ncclComm_t> comms;
-  ~Comms() {
-    const Api &a = GetApi();
-    for (auto c : comms)
-      if (c && a.destroy) a.destroy(c);
-  }
-};
+Comms::~Comms() {
+  if (comms.empty()) return;
+  const Api &a = GetApi();
+  for (auto c : comms)
+    if (c && a.destroy) a.destroy(c);
+}
 
-std::shared_ptr<Comms> Open(const std::vector<int> &devs, std::string *note) {
+std::shared_ptr<Comms> Open(const std::vector<int> &devs, bool loopback, std::string *note) {
+  auto c = std::make_shared<Comms>();
+  c->devs = devs;
+  if (loopback) {  // test stand-in: no communicator, the collectives become copies
+    c->loopback = true;
+    return c;
+  }
   const Api &a = GetApi();
   if (!a.ok) {
     *note = a.why;
@@ -78,8 +85,6 @@ std::shared_ptr<Comms> Open(const std::vector<int> &devs, std::string *note) {
       }
   int cur = 0;
   (void)hipGetDevice(&cur);
-  auto c = std::make_shared<Comms>();
-  c->devs = devs;
   c->comms.assign(devs.size(), nullptr);
   const ncclResult_t r = a.init(c->comms.data(), (int)devs.size(), devs.data());
   (void)hipSetDevice(cur);
@@ -91,20 +96,73 @@ std::shared_ptr<Comms> Open(const std::vector<int> &devs, std::string *note) {
   return c;
 }
 
-bool AllGather(Comms &c, int rank, const int64_t *send, int64_t *recv, size_t count, hipStream_t s,
-               std::string *err) {
-  const Api &a = GetApi();
-  const ncclResult_t r = a.allgather(send, recv, count, ncclInt64, c.comms[rank], s);
-  if (r != ncclSuccess) *err = "ncclAllGather: " + ErrText(a, r);
-  return r == ncclSuccess;
+bool IsLoopback(const Comms &c) { return c.loopback; }
+
+__global__ void sum_lanes_kernel(const int64_t *g, int nranks, int lanes, int64_t *out) {
+  for (int j = threadIdx.x; j < lanes; j += blockDim.x) {
+    int64_t s = 0;
+    for (int r = 0; r < nranks; r++) s += g[(int64_t)r * lanes + j];
+    out[j] = s;
+  }
 }
 
-bool AllReduceSum(Comms &c, int rank, const int64_t *send, int64_t *recv, size_t count, hipStream_t s,
-                  std::string *err) {
+bool Collective(Comms &c, bool all_reduce, const std::vector<const int64_t *> &send, const std::vector<int64_t *> &recv,
+                const std::vector<int64_t *> &scratch, const std::vector<hipStream_t> &streams, size_t count,
+                std::string *err) {
+  const int n = (int)c.devs.size();
+  if (c.loopback) {
+    // every rank's send block lands in every rank's receive (or scratch)
+    // block after the sender's pack: the data movement of the all-gather, the
+    // all-reduce summed by one small kernel per rank
+    std::vector<hipEvent_t> ev(n, nullptr);
+    bool ok = true;
+    for (int i = 0; i < n && ok; i++) {
+      ok = hipSetDevice(c.devs[i]) == hipSuccess &&
+           hipEventCreateWithFlags(&ev[i], hipEventDisableTiming) == hipSuccess &&
+           hipEventRecord(ev[i], streams[i]) == hipSuccess;
+    }
+    for (int j = 0; j < n && ok; j++) {
+      ok = hipSetDevice(c.devs[j]) == hipSuccess;
+      int64_t *dst = all_reduce ? scratch[j] : recv[j];
+      for (int i = 0; i < n && ok; i++)
+        ok = hipStreamWaitEvent(streams[j], ev[i], 0) == hipSuccess &&
+             hipMemcpyAsync(dst + (size_t)i * count, send[i], count * 8, hipMemcpyDeviceToDevice, streams[j]) ==
+                 hipSuccess;
+      if (ok && all_reduce) {
+        hipLaunchKernelGGL(sum_lanes_kernel, dim3(1), dim3(64), 0, streams[j], (const int64_t *)dst, n, (int)count,
+                           recv[j]);
+        ok = hipGetLastError() == hipSuccess;
+      }
+    }
+    for (int i = 0; i < n; i++)
+      if (ev[i]) (void)hipEventDestroy(ev[i]);
+    if (!ok) *err = "RCCL loopback: a HIP call failed";
+    return ok;
+  }
+  // one thread drives every rank: the calls are fused into one group, so no
+  // rank's collective waits for a call that is never made
   const Api &a = GetApi();
-  const ncclResult_t r = a.allreduce(send, recv, count, ncclInt64, ncclSum, c.comms[rank], s);
-  if (r != ncclSuccess) *err = "ncclAllReduce: " + ErrText(a, r);
-  return r == ncclSuccess;
+  ncclResult_t r = a.gstart();
+  if (r != ncclSuccess) {
+    *err = "ncclGroupStart: " + ErrText(a, r);
+    return false;
+  }
+  ncclResult_t first = ncclSuccess;
+  for (int i = 0; i < n; i++) {
+    const ncclResult_t ri = all_reduce ? a.allreduce(send[i], recv[i], count, ncclInt64, ncclSum, c.comms[i], streams[i])
+                                       : a.allgather(send[i], recv[i], count, ncclInt64, c.comms[i], streams[i]);
+    if (ri != ncclSuccess && first == ncclSuccess) first = ri;
+  }
+  r = a.gend();
+  if (first != ncclSuccess) {
+    *err = std::string(all_reduce ? "ncclAllReduce: " : "ncclAllGather: ") + ErrText(a, first);
+    return false;
+  }
+  if (r != ncclSuccess) {
+    *err = "ncclGroupEnd: " + ErrText(a, r);
+    return false;
+  }
+  return true;
 }
 
 // one lane group per column: row 0's value widened to int128, its validity

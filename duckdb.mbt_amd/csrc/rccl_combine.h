@@ -15,20 +15,36 @@
 
 #include "combine.h"
 
+struct ncclComm;  // RCCL's communicator (ncclComm_t)
+
 namespace mbx {
 namespace rc {
 
-struct Comms;  // one ncclComm_t per shard device (rank i = devs[i])
+// one communicator per shard device (rank i = devs[i]); none in loopback
+struct Comms {
+  std::vector<int> devs;
+  std::vector<ncclComm *> comms;
+  bool loopback = false;
+  ~Comms();
+};
 
 // ncclCommInitAll over devs (distinct devices, one rank each); nullptr and a
-// reason in *note when librccl is missing or the init fails.
-std::shared_ptr<Comms> Open(const std::vector<int> &devs, std::string *note);
+// reason in *note when librccl is missing or the init fails.  loopback (tests
+// only, MBX_EXPERIMENTS=1): no communicator; Collective moves the same lanes
+// with device copies, so the pack / combine kernels and the host decode run on
+// a box with one GPU (same-device shards).
+std::shared_ptr<Comms> Open(const std::vector<int> &devs, bool loopback, std::string *note);
+bool IsLoopback(const Comms &c);
 
-// rank's part of the collective on its device's stream (the caller keeps that
-// device current); false and *err on an RCCL error
-bool AllGather(Comms &c, int rank, const int64_t *send, int64_t *recv, size_t count, hipStream_t s, std::string *err);
-bool AllReduceSum(Comms &c, int rank, const int64_t *send, int64_t *recv, size_t count, hipStream_t s,
-                  std::string *err);
+// One collective over every rank, driven from the calling thread: rank i's
+// count int64 lanes send[i] on streams[i] -> recv[i] (all-gather: n * count
+// lanes in rank order; all-reduce: count summed lanes).  The RCCL calls are
+// fused in one ncclGroupStart/End, so no rank can be left inside a collective
+// that another rank never joined.  scratch[i] (n * count lanes) is used by the
+// loopback all-reduce only.  false and *err on an RCCL / HIP error.
+bool Collective(Comms &c, bool all_reduce, const std::vector<const int64_t *> &send, const std::vector<int64_t *> &recv,
+                const std::vector<int64_t *> &scratch, const std::vector<hipStream_t> &streams, size_t count,
+                std::string *err);
 
 // the lanes of a one-row partial relation (row 0 of every column) and the
 // device error word, written to dst by one small kernel

@@ -446,8 +446,9 @@ int32_t duckdb_mb_config_set(duckdb_mb_config *c, moonbit_bytes_t key, moonbit_b
     ok = IsInt(v, &x) && x >= 0;
     if (ok) c->opts.shard_rows = x;
   } else if (kl == "mbx_combine") {
-    ok = v == "host" || v == "rccl";
-    if (ok) c->opts.combine_rccl = v == "rccl";
+    // rccl_loopback: the test-only stand-in for the collectives (rccl_combine.h)
+    ok = v == "host" || v == "rccl" || (v == "rccl_loopback" && mbx::Knob("MBX_EXPERIMENTS"));
+    if (ok) c->opts.combine_rccl = v != "host", c->opts.rccl_loopback = v == "rccl_loopback";
   } else if (kl == "mbx_force_peer") {
     c->opts.force_peer = v == "true" || v == "1";
   } else if (kl == "mbx_profile") {
@@ -1741,11 +1742,26 @@ char *duckdb_mbx_rccl_note(duckdb_mb_connection *h) {
   return strdup(h ? h->conn.shard_stats.rccl_note.c_str() : "");
 }
 
+// mbx_combine counters, up to cap of {RCCL combines, fallbacks to the host
+// merge, combines through the test loopback, combines that raised a shard's
+// device error}; returns how many were written.
+int32_t duckdb_mbx_rccl_stats_ex(duckdb_mb_connection *h, int64_t *out, int32_t cap) {
+  if (!h || !out) return 0;
+  const ShardStats &st = h->conn.shard_stats;
+  const int64_t v[4] = {st.rccl_combines, st.rccl_fallbacks, st.rccl_loopbacks, st.rccl_errors};
+  int32_t n = 0;
+  for (; n < cap && n < 4; n++) out[n] = v[n];
+  return n;
+}
+
 // Switches a connection's combine between the host merge (0) and RCCL (1), as
-// Config::set("mbx_combine", ...) at connect would.  Returns 1.
-int32_t duckdb_mbx_set_combine(duckdb_mb_connection *h, int32_t rccl) {
-  if (!h) return 0;
-  h->conn.opts.combine_rccl = rccl != 0;
+// Config::set("mbx_combine", ...) at connect would; 2 is the test loopback
+// (accepted only with MBX_EXPERIMENTS=1).  Returns 1 (0: refused).
+int32_t duckdb_mbx_set_combine(duckdb_mb_connection *h, int32_t mode) {
+  if (!h || mode < 0 || mode > 2) return 0;
+  if (mode == 2 && !mbx::Knob("MBX_EXPERIMENTS")) return 0;
+  h->conn.opts.combine_rccl = mode != 0;
+  h->conn.opts.rccl_loopback = mode == 2;
   return 1;
 }
 

@@ -313,8 +313,15 @@ duckdb_mb_result *duckdb_mbx_shard_partial(duckdb_mb_connection *connection, int
 int32_t duckdb_mbx_rccl_stats(duckdb_mb_connection *connection, int64_t *out2, double *out_us1);
 /* Why the last RCCL request fell back ("" if it ran); free with duckdb_mbx_free. */
 char *duckdb_mbx_rccl_note(duckdb_mb_connection *connection);
-/* 1: RCCL combine, 0: host merge, from the next statement on.  Returns 1. */
-int32_t duckdb_mbx_set_combine(duckdb_mb_connection *connection, int32_t rccl);
+/* Up to cap of {RCCL combines, host-merge fallbacks, combines through the test
+ * loopback, combines that raised a shard's device error}; returns the count
+ * written. */
+int32_t duckdb_mbx_rccl_stats_ex(duckdb_mb_connection *connection, int64_t *out, int32_t cap);
+/* 1: RCCL combine, 0: host merge, from the next statement on; 2: the RCCL
+ * combine with its collectives replaced by device copies (tests only: refused
+ * without MBX_EXPERIMENTS=1), so it runs over same-device shards.  Returns 1
+ * (0: refused). */
+int32_t duckdb_mbx_set_combine(duckdb_mb_connection *connection, int32_t mode);
 /* The RCCL combine's lane arithmetic on the host (tests): gathered holds
  * nranks x (3 ncols + 1) int64 lanes ({lo, hi, non-NULL} per column, then the
  * rank's error word); kinds[j] = 0 sum / 1 min / 2 max; out = 3 ncols lanes.

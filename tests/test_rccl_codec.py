@@ -72,3 +72,26 @@ def test_bad_arguments(mbx):
         mbx.combine_lanes([], ["sum"])
     with pytest.raises(ValueError):
         mbx.combine_lanes([[1] * 33], ["sum"] * 33)
+
+
+def test_loopback_combine_needs_the_experiments_opt_in(mbx):
+    """mbx_combine=rccl_loopback (the test stand-in for the collectives) is a
+    config value only under MBX_EXPERIMENTS=1: a MoonBit program's environment
+    cannot turn the product's RCCL combine into device copies."""
+    import os
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    code = (
+        "import importlib.util, sys\n"
+        f"spec = importlib.util.spec_from_file_location('m', {os.path.join(root, 'duckdb.mbt_amd', '__init__.py')!r})\n"
+        "m = importlib.util.module_from_spec(spec); sys.modules['m'] = m; spec.loader.exec_module(m)\n"
+        "cfg = m.Config.create()\n"
+        "print(type(cfg.set('mbx_combine', 'rccl_loopback')).__name__, type(cfg.set('mbx_combine', 'rccl')).__name__)\n"
+    )
+    env = {k: v for k, v in os.environ.items() if k != "MBX_EXPERIMENTS"}
+    out = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=120)
+    assert out.returncode == 0, out.stderr
+    assert out.stdout.split() == ["Err", "Ok"], out.stdout
+    cfg = mbx.Config.create()  # this process has the opt-in (conftest)
+    assert isinstance(cfg.set("mbx_combine", "rccl_loopback"), mbx.Ok)
