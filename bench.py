@@ -12,8 +12,11 @@ Multi-GPU (default): the product's own path.  One process opens devices
 0..N-1 through the library's `gpu_devices` Config::set key (what a MoonBit
 caller gets from duckdb_mb_query); the library shards the table by row range,
 runs every shard's fused kernel on its own device and stream from a
-persistent host worker, and merges the partial aggregates exactly (int128) on
-the host.  Under the driver's `torch.distributed.run --nproc-per-node N`
+persistent host worker, and combines the partial aggregates with RCCL on the
+shard devices (all-reduce for COUNT, all-gather + carry-correct int128 combine
+kernel for SUM; the library's default `mbx_combine`), or exactly on the host
+where RCCL does not apply (same-device shards, GROUP BY).  The other combine
+is timed right after the headline (`multi_device.combine_ab`).  Under the driver's `torch.distributed.run --nproc-per-node N`
 launch, rank 0 drives all N devices and the other ranks only join the gloo
 barriers.  `--ranks` keeps the one-process-per-GPU form (each rank its own
 connection and 1e9-row shard, combined by an RCCL all-reduce / all-gather
@@ -175,7 +178,9 @@ def inlib_plan(args, world):
     nshards = len(devices)
     par = (f"in-library row-range shards: gpu_devices={','.join(map(str, devices))} "
            f"({ngpu} GPU x {spg} shard(s), one engine + stream + persistent host worker per shard), "
-           f"per-shard partial aggregates merged exactly on the host (int128)") if nshards > 1 \
+           f"per-shard partial aggregates combined by the library's default: an RCCL all-reduce (COUNT) / "
+           f"all-gather + int128 combine kernel (SUM) over the shard devices when they are distinct, else an exact "
+           f"host merge") if nshards > 1 \
         else "row-range shards x1"
     return {"ngpu": ngpu, "shards_per_gpu": spg, "devices": devices, "nshards": nshards,
             "rows_total": args.rows * ngpu, "parallelism": par}
@@ -367,9 +372,14 @@ def run_inlib(args, world, rank, vote=None):
         conn.profile_drain()
         barrier = dist.barrier if dist else None
         sr0 = conn.engine_stats()
+        cb0 = conn.rccl_stats()
         elapsed, out = time_steps(step, args.steps, 0, barrier,
                                   torch.cuda.synchronize if torch.cuda.is_available() else None)
         sr_out = sel_outcomes(conn, sr0)
+        cb1 = conn.rccl_stats()
+        cb_out = {"ran_rccl_steps": cb1["rccl_combines"] - cb0["rccl_combines"],
+                  "host_merge_steps": cb1["rccl_fallbacks"] - cb0["rccl_fallbacks"], "note": cb1["note"],
+                  "rccl_timeouts": cb1["rccl_timeouts"], "last_collective_d2h_us": cb1["last_rccl_us"]}
     except Exception as ex:  # noqa: BLE001 - a shard's error names the shard and its device
         fail(dist, f"query failed: {ex}")
     kern = conn.profile_drain()
@@ -410,8 +420,13 @@ def run_inlib(args, world, rank, vote=None):
         if shard_par is not None:
             md["shard_parity"] = shard_par
         if args.config in ("c2", "c2d", "c5"):
-            md["rccl_combine"] = guarded(lambda: rccl_leg(conn, step, args, w, n_total, plan), RCCL_LEG_TIMEOUT_S)
-            stuck = md["rccl_combine"].get("error", "").startswith("timeout")
+            # the timed loop ran the library's default combine (RCCL over the
+            # shard devices when they are distinct); the other mode is timed after
+            md["combine"] = {"timed_loop": cb_out, "mode": "rccl" if cb_out["ran_rccl_steps"] else "host merge"}
+            md["combine_ab"] = guarded(
+                lambda: combine_leg(conn, step, args, n_total, "host" if cb_out["ran_rccl_steps"] else "rccl"),
+                RCCL_LEG_TIMEOUT_S)
+            stuck = md["combine_ab"].get("error", "").startswith("timeout")
         result["multi_device"] = md
     calibrate_into(conn, result, args.config)
     if args.config == "sel":
@@ -426,8 +441,16 @@ def run_inlib(args, world, rank, vote=None):
         extras = "c3,sel" if (args.config == "c2" and plan["nshards"] == 1) else ""
     if extras:
         result["extra"] = {}
+        ceil = result["roofline"].get("measured_ceilings_gbs", {})
         for ex in [e for e in extras.split(",") if e]:
-            result["extra"][ex] = sub_bench(conn, ex, plan, args)
+            r = result["extra"][ex] = sub_bench(conn, ex, plan, args)
+            # against this box's ceiling of the same shape: C3's two-array ring read
+            # (4 + 8 B per row, 2-deep 3 KiB slots); sel's half-writing ring copy
+            shape = {"c3": "ring_read2_gbs", "sel": "ring_copy_half_gbs"}.get(ex)
+            if shape and isinstance(ceil.get(shape), float) and r.get("achieved_gbs"):
+                r["measured_ceiling_gbs"] = ceil[shape]
+                r["ceiling_shape"] = shape
+                r["frac_of_measured"] = r["achieved_gbs"] / ceil[shape]
     if not args.no_cpu and plan["nshards"] == 1 and args.config in ("c2", "c2d", "c3", "c5", "sel"):
         result["cpu_baseline"] = cpu_baseline(args.cpu_seconds, "c2" if args.config == "c2d" else args.config)
     if dist:
@@ -441,12 +464,13 @@ def run_inlib(args, world, rank, vote=None):
         log("[bench] PARITY FAILURE: " + json.dumps(result["parity"]) +
             (" shards: " + json.dumps([p for p in shard_par if not p["match"]]) if shard_par else ""))
     if stuck:
-        # the RCCL leg's thread is still inside a collective: the headline line
+        # the second leg's thread is still inside the library: the headline line
         # is out, so leave without joining it (interpreter teardown would wait)
-        log("[bench] RCCL combine leg did not finish; exiting without closing the connection")
+        # a hung leg is a failed run even when the headline's parity matched
+        log("[bench] the second combine leg did not finish; exiting (status 4) without closing the connection")
         sys.stdout.flush()
         sys.stderr.flush()
-        os._exit(3 if bad else 0)
+        os._exit(3 if bad else 4)
     if bad:
         raise SystemExit(3)
     return result
@@ -541,6 +565,15 @@ def sharded_parity(conn, config, out, n_total, nshards, threads):
     from oracle import Oracle
     orc = Oracle()
     shard_par, g_cnt, g_sum, g_groups = [], 0, 0, {}
+    probe = conn.shard_partial(0)
+    if probe is None:
+        # the RCCL all-reduce (COUNT-only rows) leaves no per-shard partials on
+        # the host: one more step with the host merge brings them back
+        conn.set_combine("host")
+        conn.query_raw(f"SELECT COUNT(*) FROM t WHERE x > 24").close()
+        conn.set_combine("rccl")
+    else:
+        probe.close()
     for i in range(nshards):
         lo, hi = n_total * i // nshards, n_total * (i + 1) // nshards
         rr = conn.shard_partial(i)
@@ -582,15 +615,16 @@ def sharded_parity(conn, config, out, n_total, nshards, threads):
     return par, shard_par
 
 
-def rccl_leg(conn, step, args, w, n_total, plan):
-    """The same query with the library's RCCL combine (mbx_combine=rccl), timed
-    with the same discipline right after the host-merge headline: warmup (the
-    communicators are created on first use), K timed steps, the global answer
-    vs the headline's.  On same-device shards RCCL cannot run (one rank per
-    device) and the library falls back to the host merge: reported as such."""
+def combine_leg(conn, step, args, n_total, mode):
+    """The same query with the other combine (`mode`: "host" after an RCCL
+    headline, "rccl" after a host-merge one), timed with the same discipline
+    right after the headline: warmup (RCCL communicators are created on first
+    use), K timed steps, the global answer vs the headline mode's.  On
+    same-device shards RCCL cannot run (one rank per device) and the library
+    falls back to the host merge: reported as such."""
     import torch
     try:
-        conn.set_combine(True)
+        conn.set_combine(mode)
         for _ in range(max(1, args.warmup)):
             step()
         st0 = conn.rccl_stats()
@@ -598,17 +632,17 @@ def rccl_leg(conn, step, args, w, n_total, plan):
         elapsed, out = time_steps(step, args.steps, 0, None, torch.cuda.synchronize)
         st1 = conn.rccl_stats()
         conn.profile_drain()
-        conn.set_combine(False)
-        ran = st1["rccl_combines"] - st0["rccl_combines"]
-        exp = step()  # host merge again: the reference answer of the same rows
-        return {"ran_rccl_steps": ran, "fell_back_steps": st1["rccl_fallbacks"] - st0["rccl_fallbacks"],
+        conn.set_combine("rccl")
+        exp = step()  # the product default again: the headline mode's answer over the same rows
+        return {"mode": mode, "ran_rccl_steps": st1["rccl_combines"] - st0["rccl_combines"],
+                "fell_back_steps": st1["rccl_fallbacks"] - st0["rccl_fallbacks"],
                 "note": st1["note"], "ms_per_step": elapsed / args.steps * 1e3,
                 "value": n_total * args.steps / elapsed, "unit": "rows/s",
                 "last_collective_d2h_us": st1["last_rccl_us"],
-                "parity": {"rccl": [str(x) for x in out], "host_merge": [str(x) for x in exp],
+                "parity": {mode: [str(x) for x in out], "default": [str(x) for x in exp],
                            "match": [str(x) for x in out] == [str(x) for x in exp]}}
-    except Exception as ex:  # noqa: BLE001 - the RCCL leg must not lose the headline line
-        conn.set_combine(False)
+    except Exception as ex:  # noqa: BLE001 - the second leg must not lose the headline line
+        conn.set_combine("rccl")
         return {"error": str(ex)}
 
 

@@ -80,6 +80,7 @@ _sig("duckdb_mbx_append_column", _I, _P, _I, _P, _P, _L)
 _sig("duckdb_mbx_append_commit", _I, _P, _L)
 _sig("duckdb_mbx_hbm_calibrate", _I, _P, _L, _I, ctypes.POINTER(ctypes.c_double))
 _sig("duckdb_mbx_hbm_calibrate_ex", _I, _P, _L, _I, ctypes.POINTER(ctypes.c_double), _I)
+_sig("duckdb_mbx_clock_stamps", _I, _P, ctypes.POINTER(ctypes.c_uint64), _I)
 _sig("duckdb_mbx_statement_plan_stats", _I, _P, ctypes.POINTER(ctypes.c_int64))
 _sig("duckdb_mbx_shard_stats", _I, _P, ctypes.POINTER(ctypes.c_int64), ctypes.POINTER(ctypes.c_double))
 _sig("duckdb_mbx_engine_stats", _I, _P, ctypes.POINTER(ctypes.c_int64))
@@ -584,11 +585,26 @@ class Connection:
 
     def hbm_calibrate(self, nbytes: int = 2 << 30, iters: int = 5) -> dict:
         """This device's measured HBM ceilings (GB/s; a copy counts read + write)."""
-        out = (ctypes.c_double * 7)()
-        if lib.duckdb_mbx_hbm_calibrate_ex(self._h, nbytes, iters, out, 7) != 7:
+        out = (ctypes.c_double * 8)()
+        if lib.duckdb_mbx_hbm_calibrate_ex(self._h, nbytes, iters, out, 8) != 8:
             raise DuckDBError(_last_error("hbm_calibrate failed"))
         return {"copy_gbs": out[0], "read_nt_gbs": out[1], "read_gbs": out[2], "ring_read_gbs": out[3],
-                "copy_nt4_gbs": out[4], "ring_copy_gbs": out[5], "ring_copy_half_gbs": out[6], "bytes": nbytes}
+                "copy_nt4_gbs": out[4], "ring_copy_gbs": out[5], "ring_copy_half_gbs": out[6],
+                "ring_read2_gbs": out[7], "bytes": nbytes}
+
+    def clock_stamps(self, nwg: int) -> list:
+        """In-kernel clock of each of the first `nwg` workgroups of the last
+        filter_agg_lds / group_direct_lds / two-array ring launch, in GHz
+        (d s_memtime / d s_memrealtime x 100 MHz around its main loop).  Only
+        the diagnostic build (libduckdb_mb_amd_clk.so) stamps; [] otherwise."""
+        out = (ctypes.c_uint64 * (4 * nwg))()
+        n = lib.duckdb_mbx_clock_stamps(self._h, out, nwg)
+        res = []
+        for i in range(n):
+            c0, r0, c1, r1 = out[4 * i], out[4 * i + 1], out[4 * i + 2], out[4 * i + 3]
+            if r1 > r0 and c1 > c0:
+                res.append({"ghz": (c1 - c0) / (r1 - r0) * 0.1, "loop_us": (r1 - r0) / 100.0, "r0": r0})
+        return res
 
     def shard_stats(self) -> dict:
         """Counters of the in-library multi-device path (gpu_devices; extension)."""
@@ -628,12 +644,12 @@ class Connection:
         out = (ctypes.c_int64 * 2)()
         us = (ctypes.c_double * 1)()
         lib.duckdb_mbx_rccl_stats(self._h, out, us)
-        ex = (ctypes.c_int64 * 4)()
-        lib.duckdb_mbx_rccl_stats_ex(self._h, ex, 4)
+        ex = (ctypes.c_int64 * 5)()
+        lib.duckdb_mbx_rccl_stats_ex(self._h, ex, 5)
         p = lib.duckdb_mbx_rccl_note(self._h)
         note = ctypes.string_at(p).decode()
         lib.duckdb_mbx_free(p)
-        return {"rccl_combines": out[0], "rccl_fallbacks": out[1], "rccl_loopbacks": ex[2], "rccl_errors": ex[3],
+        return {"rccl_combines": out[0], "rccl_fallbacks": out[1], "rccl_loopbacks": ex[2], "rccl_errors": ex[3], "rccl_timeouts": ex[4],
                 "last_rccl_us": us[0], "note": note}
 
     def set_combine(self, rccl) -> None:

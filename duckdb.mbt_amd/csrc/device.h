@@ -162,7 +162,10 @@ void BitmapAppend(uint64_t *dst, int64_t dst_off, const uint64_t *src, int64_t n
 // HBM calibration: out = in (float4 copy), nbytes multiple of 16
 void CopyKernel(const void *in, void *out, int64_t nbytes, hipStream_t s);
 // best-of-iters GB/s of {float4 copy (read+write bytes), nt int64 read, plain int64 read}
-void HbmCalibrate(void *buf_a, void *buf_b, int64_t bytes, int iters, double out[7], hipStream_t s);
+constexpr int kCalibrateShapes = 8;  // HbmCalibrate's measured shapes (kernels.hip)
+void HbmCalibrate(void *buf_a, void *buf_b, int64_t bytes, int iters, double out[kCalibrateShapes], hipStream_t s);
+// clock stamps of the last stamped launch (libduckdb_mb_amd_clk.so only; 0 otherwise)
+int ReadClockStamps(uint64_t *out, int cap, hipStream_t s);
 
 int NumCUs();
 

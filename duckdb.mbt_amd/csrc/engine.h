@@ -125,10 +125,12 @@ struct Options {
   // "mbx_force_peer" (tests): shards on the same device still exchange row
   // results by peer DMA (hipMemcpyPeerAsync), as distinct devices do
   bool force_peer = false;
-  // "mbx_combine" = "host" (default) | "rccl": a sharded global aggregate over
+  // "mbx_combine" = "rccl" (default) | "host": a sharded global aggregate over
   // distinct devices combines its partials with RCCL collectives on the shard
-  // devices (rccl_combine.h) instead of the host merge
-  bool combine_rccl = false;
+  // devices (rccl_combine.h); "host" (and every shape or device list RCCL does
+  // not cover: GROUP BY, floating-point partials, same-device shards) merges
+  // the partials on the host
+  bool combine_rccl = true;
   // "mbx_combine" = "rccl_loopback" (tests only, MBX_EXPERIMENTS=1): the RCCL
   // combine with its two collectives replaced by device copies between the
   // shards' lane buffers, so it runs over same-device shards on one GPU
@@ -167,6 +169,7 @@ struct ShardStats {
   int64_t rccl_combines = 0, rccl_fallbacks = 0;
   int64_t rccl_loopbacks = 0;  // of rccl_combines, through the test loopback
   int64_t rccl_errors = 0;     // combines that raised a shard's device error
+  int64_t rccl_timeouts = 0;   // collectives aborted after MBX_RCCL_TIMEOUT_MS (then host merge)
   double last_rccl_us = 0;
   std::string rccl_note;  // why the last rccl request fell back (empty: it ran)
 };
@@ -255,7 +258,9 @@ void AppendRawColumns(Connection &c, Table &t, const std::vector<const void *> &
 // waits for in-flight appends and folds their zone-map statistics
 void SettleAppends(Connection &c);
 void HostColumnPush(HostColumn &col, const Value &v);  // v already of col.type (or NULL)
-void HbmCalibrateConn(Connection &c, int64_t bytes, int iters, double out[7]);
+void HbmCalibrateConn(Connection &c, int64_t bytes, int iters, double out[8]);
+// in-kernel clock stamps of the last stamped launch (libduckdb_mb_amd_clk.so)
+int ClockStampsConn(Connection &c, uint64_t *out, int cap);
 // adds this connection's (and its shards') select_rounds counters to out:
 // launches, aborts (a workgroup never scheduled: the two-pass form reran), launch failures
 void EngineCounters(const Connection &c, int64_t out[3]);

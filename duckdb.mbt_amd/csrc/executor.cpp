@@ -4182,6 +4182,40 @@ static bool ShardedAggregateRccl(Connection &c, const BoundSelect &s, const Boun
   }
   std::string cerr;
   const bool cok = rc::Collective(*c.rccl, counts_only, sp, rp, xp, streams, (size_t)P, &cerr);
+  // A collective that does not complete in time (a rank that cannot reach the
+  // others, a broken link) must not hang the connection: the communicators
+  // are aborted, this connection keeps the host merge from then on, and the
+  // host merge answers this statement.
+  if (cok && !c.rccl->loopback) {
+    static const int timeout_ms = [] {
+      const char *v = Knob("MBX_RCCL_TIMEOUT_MS");
+      return v ? std::max(1, atoi(v)) : 20000;
+    }();
+    const auto deadline = tc0 + std::chrono::milliseconds(timeout_ms);
+    for (int i = 0; i < nsh;) {
+      const hipError_t q = hipStreamQuery(streams[i]);
+      if (q != hipErrorNotReady) {  // done (or an error, raised by the synchronisation below)
+        i++;
+        continue;
+      }
+      if (std::chrono::steady_clock::now() > deadline) {
+        rc::Abort(*c.rccl);
+        for (int k = 0; k < nsh; k++) {
+          Eng(*c.shards[k]);
+          (void)hipStreamSynchronize(streams[k]);
+          sendb[k].reset(), recvb[k].reset(), scrb[k].reset();
+          rel[k] = DRel();
+        }
+        Eng(c);
+        c.rccl.reset();  // rccl_tried stays set: no new communicators on this connection
+        st.rccl_timeouts++;
+        st.rccl_note = "an RCCL collective did not complete within " + std::to_string(timeout_ms) +
+                       " ms: communicators aborted, host merge from now on";
+        return fallback(st.rccl_note);
+      }
+      __builtin_ia32_pause();
+    }
+  }
   // Phase 3: device 0 finishes (combine kernel, one D2H); every rank's stream
   // is drained before its lane buffers go back to its pool
   std::exception_ptr first_err;
@@ -4655,7 +4689,7 @@ void EngineCounters(const Connection &c, int64_t out[3]) {
   for (auto &sc : c.shards) EngineCounters(*sc, out);
 }
 
-void HbmCalibrateConn(Connection &c, int64_t bytes, int iters, double out[7]) {
+void HbmCalibrateConn(Connection &c, int64_t bytes, int iters, double out[8]) {
   Engine &e = Eng(c);
   bytes &= ~(int64_t)1023;  // whole 1 KiB ring slots
   void *a = nullptr, *b = nullptr;
@@ -4667,6 +4701,11 @@ void HbmCalibrateConn(Connection &c, int64_t bytes, int iters, double out[7]) {
   HIPCHK(hipStreamSynchronize(e.stream));
   HIPCHK(hipFree(a));
   HIPCHK(hipFree(b));
+}
+
+int ClockStampsConn(Connection &c, uint64_t *out, int cap) {
+  Engine &e = Eng(c);
+  return dev::ReadClockStamps(out, cap, e.stream);
 }
 
 // memcpy split over a few host threads (one thread tops out near 10 GB/s)

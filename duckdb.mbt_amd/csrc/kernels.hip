@@ -18,6 +18,36 @@
 
 #include "device.h"
 #include "types.h"
+
+// ---------------------------------------------------------------------------
+// In-kernel clock stamps (diagnostic build only: make clockdiag compiles this
+// file with MBX_CLOCK_STAMPS=1 into libduckdb_mb_amd_clk.so; in the product
+// library no stamp instruction exists).  Thread 0 of each of the first
+// kClkSlots workgroups of filter_agg_lds, group_direct_lds and the two-array
+// ring read records the shader-clock counter (s_memtime) and the 100 MHz
+// reference counter (s_memrealtime) once when its main loop starts and once
+// when it has drained, with ordinary vector stores.  Clock of a workgroup =
+// d(memtime) / d(realtime) x 100 MHz (MI355X_MICROARCH.md, DVFS item 6).
+// ---------------------------------------------------------------------------
+namespace mbx {
+namespace dev {
+constexpr int kClkSlots = 1024;
+}
+}  // namespace mbx
+#if MBX_CLOCK_STAMPS
+__device__ unsigned long long g_clk_stamps[mbx::dev::kClkSlots * 4];
+__device__ __forceinline__ void clk_stamp(int part) {
+  if (threadIdx.x == 0 && blockIdx.x < mbx::dev::kClkSlots) {
+    const unsigned long long c = __builtin_amdgcn_s_memtime();
+    const unsigned long long r = __builtin_amdgcn_s_memrealtime();
+    g_clk_stamps[blockIdx.x * 4 + part * 2] = c;
+    g_clk_stamps[blockIdx.x * 4 + part * 2 + 1] = r;
+  }
+}
+#define MBX_CLK(part) clk_stamp(part)
+#else
+#define MBX_CLK(part)
+#endif
 #include "vm.h"
 #include "vm_device.h"
 #include "knobs.h"
@@ -586,6 +616,7 @@ __global__ __launch_bounds__(256) void filter_agg_lds_kernel(const T *__restrict
     }
   }
   int k = 0;
+  MBX_CLK(0);
   for (; pc < npieces; pc += nw) {
     asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NS * (DEPTH - 1)) : "memory");
     v2i64 x = slot0[k * 64 + lane];
@@ -618,6 +649,7 @@ __global__ __launch_bounds__(256) void filter_agg_lds_kernel(const T *__restrict
     k = k + 1 == DEPTH ? 0 : k + 1;
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  MBX_CLK(1);
   if (blockIdx.x == 0 && w == 0) {
     for (int64_t i = npieces * RP + lane; i < n; i += 64) {
       int64_t xv = p[i];
@@ -1339,6 +1371,45 @@ __global__ __launch_bounds__(256) void ring_read_kernel(const unsigned char *__r
   if (acc == 0x123456789) atomicAdd(flag, 1ull);
 }
 
+// the read shape of C3's group_direct_lds (d2_g1): one workgroup of 4 waves
+// per CU; a wave step pulls 256 rows of a 4-byte column (1 KiB) and of an
+// 8-byte column (2 KiB) into a DEPTH-deep ring of 3 KiB slots; no atomics
+template <int DEPTH>
+__global__ __launch_bounds__(256) void ring_read2_kernel(const unsigned char *__restrict__ k4,
+                                                         const unsigned char *__restrict__ v8, int64_t nsteps,
+                                                         unsigned long long *flag) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char r2_lds[];
+  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  unsigned char *ring = r2_lds + w * DEPTH * 3072;
+  const int64_t nw = (int64_t)gridDim.x * 4;
+  int64_t st = (int64_t)blockIdx.x * 4 + w;
+  auto issue = [&](int64_t q, int d) {
+    unsigned char *dst = ring + d * 3072;
+    __builtin_amdgcn_global_load_lds((const void *)(k4 + q * 1024 + lane * 16), (void *)dst, 16, 0, 2);
+    __builtin_amdgcn_global_load_lds((const void *)(v8 + q * 2048 + lane * 16), (void *)(dst + 1024), 16, 0, 2);
+    __builtin_amdgcn_global_load_lds((const void *)(v8 + q * 2048 + 1024 + lane * 16), (void *)(dst + 2048), 16, 0, 2);
+  };
+#pragma unroll
+  for (int d = 0; d < DEPTH; d++) issue(st + d * nw < nsteps ? st + d * nw : 0, d);
+  long long acc = 0;
+  int k = 0;
+  MBX_CLK(0);
+  for (; st < nsteps; st += nw) {
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(3 * (DEPTH - 1)) : "memory");
+    const unsigned char *src = ring + k * 3072;
+    v4i32 a = *(const v4i32 *)(src + lane * 16);
+    v2i64 b = *(const v2i64 *)(src + 1024 + lane * 32), c = *(const v2i64 *)(src + 1024 + lane * 32 + 16);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    const int64_t q = st + DEPTH * nw;
+    issue(q < nsteps ? q : st, k);
+    acc += (a.x ^ a.w) + (b.x ^ c.y);
+    k = k + 1 == DEPTH ? 0 : k + 1;
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  MBX_CLK(1);
+  if (acc == 0x123456789) atomicAdd(flag, 1ull);
+}
+
 // 16-B copy with 4 independent loads in flight per lane, non-temporal both ways
 __global__ __launch_bounds__(256) void copy_nt4_kernel(const v4i32 *__restrict__ in, v4i32 *__restrict__ out, int64_t n) {
   const int64_t stride = (int64_t)gridDim.x * blockDim.x;
@@ -1388,9 +1459,10 @@ __global__ __launch_bounds__(256) void ring_copy_kernel(const unsigned char *__r
 
 // out: [0] float4 copy, [1] non-temporal int64 read, [2] plain read, [3] the
 // hot kernels' LDS-DMA ring read, [4] unrolled non-temporal 16-B copy, [5] the
-// LDS-DMA ring copy, [6] the ring copy writing half of what it reads (GB/s;
-// a copy counts its read and its write)
-void HbmCalibrate(void *buf_a, void *buf_b, int64_t bytes, int iters, double out[7], hipStream_t s) {
+// LDS-DMA ring copy, [6] the ring copy writing half of what it reads, [7] C3's
+// two-array ring read (a 4-byte and an 8-byte column, 2-deep 3 KiB slots)
+// (GB/s; a copy counts its read and its write)
+void HbmCalibrate(void *buf_a, void *buf_b, int64_t bytes, int iters, double out[kCalibrateShapes], hipStream_t s) {
   hipEvent_t e0, e1;
   (void)hipEventCreate(&e0);
   (void)hipEventCreate(&e1);
@@ -1398,7 +1470,8 @@ void HbmCalibrate(void *buf_a, void *buf_b, int64_t bytes, int iters, double out
   int64_t n16 = bytes / 16;
   int grid = NumCUs() * 8;
   const int64_t nsteps = bytes / 1024;
-  for (int k = 0; k < 7; k++) {
+  const int64_t nsteps3 = bytes / 3072;  // [7]: 256-row steps of 4 + 8 bytes per row
+  for (int k = 0; k < kCalibrateShapes; k++) {
     float best = 1e30f;
     for (int it = 0; it < iters + 1; it++) {
       (void)hipEventRecord(e0, s);
@@ -1413,6 +1486,9 @@ void HbmCalibrate(void *buf_a, void *buf_b, int64_t bytes, int iters, double out
       else if (k == 5)
         hipLaunchKernelGGL((ring_copy_kernel<6, false>), dim3(NumCUs()), dim3(256), 4 * 6 * 1024, s,
                            (const unsigned char *)buf_a, (unsigned char *)buf_b, nsteps);
+      else if (k == 7)
+        hipLaunchKernelGGL(ring_read2_kernel<2>, dim3(NumCUs()), dim3(256), 4 * 2 * 3072, s,
+                           (const unsigned char *)buf_a, (const unsigned char *)buf_a + nsteps3 * 1024, nsteps3, flag);
       else
         hipLaunchKernelGGL((ring_copy_kernel<6, true>), dim3(NumCUs()), dim3(256), 4 * 6 * 1024, s,
                            (const unsigned char *)buf_a, (unsigned char *)buf_b, nsteps);
@@ -1422,11 +1498,29 @@ void HbmCalibrate(void *buf_a, void *buf_b, int64_t bytes, int iters, double out
       (void)hipEventElapsedTime(&ms, e0, e1);
       if (it > 0 && ms < best) best = ms;  // first launch is a warm-up
     }
-    double moved = (k == 6 ? 1.5 : k == 0 || k >= 4 ? 2.0 : 1.0) * (double)bytes;
+    double moved = (k == 7 ? (double)nsteps3 * 3072 / (double)bytes : k == 6 ? 1.5 : k == 0 || (k >= 4 && k < 7) ? 2.0 : 1.0) *
+                   (double)bytes;
     out[k] = moved / (best * 1e-3) / 1e9;
   }
   (void)hipEventDestroy(e0);
   (void)hipEventDestroy(e1);
+}
+
+// The clock stamps of the last stamped launch (diagnostic build): up to cap
+// workgroups' {memtime start, realtime start, memtime end, realtime end};
+// returns the count copied, 0 in the product library (no stamps compiled).
+int ReadClockStamps(uint64_t *out, int cap, hipStream_t s) {
+#if MBX_CLOCK_STAMPS
+  const int n = std::min(cap, kClkSlots);
+  if (n <= 0) return 0;
+  if (hipStreamSynchronize(s) != hipSuccess) return 0;
+  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_clk_stamps), (size_t)n * 4 * 8, 0, hipMemcpyDeviceToHost) != hipSuccess)
+    return 0;
+  return n;
+#else
+  (void)out, (void)cap, (void)s;
+  return 0;
+#endif
 }
 
 // ---------------------------------------------------------------------------
@@ -1748,6 +1842,7 @@ __global__ __launch_bounds__(256) void group_direct_lds_kernel(const TK *__restr
     }
   }
   int k = 0;
+  MBX_CLK(0);
   for (; st < nsteps; st += nw) {
     asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NLD * (DEPTH - 1)) : "memory");
     const unsigned char *src = ring + k * SB;
@@ -1810,6 +1905,7 @@ __global__ __launch_bounds__(256) void group_direct_lds_kernel(const TK *__restr
     }
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  MBX_CLK(1);
   if (blockIdx.x == 0) {
     for (int64_t i = (nsteps << 8) + t; i < n; i += blockDim.x) {
       int64_t kv = (int64_t)keys[i], av = NV >= 1 ? (int64_t)v0[i] : 0;

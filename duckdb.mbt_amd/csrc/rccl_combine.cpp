@@ -24,6 +24,7 @@ struct Api {
   decltype(&ncclGetErrorString) errstr = nullptr;
   decltype(&ncclGroupStart) gstart = nullptr;
   decltype(&ncclGroupEnd) gend = nullptr;
+  decltype(&ncclCommAbort) abort = nullptr;
 };
 
 const Api &GetApi() {
@@ -47,6 +48,7 @@ const Api &GetApi() {
     api.errstr = (decltype(api.errstr))dlsym(h, "ncclGetErrorString");
     api.gstart = (decltype(api.gstart))dlsym(h, "ncclGroupStart");
     api.gend = (decltype(api.gend))dlsym(h, "ncclGroupEnd");
+    api.abort = (decltype(api.abort))dlsym(h, "ncclCommAbort");
     api.ok = api.init && api.destroy && api.allgather && api.allreduce && api.errstr && api.gstart && api.gend;
     if (!api.ok) api.why = "librccl lacks an entry point";
   });
@@ -97,6 +99,12 @@ std::shared_ptr<Comms> Open(const std::vector<int> &devs, bool loopback, std::st
 }
 
 bool IsLoopback(const Comms &c) { return c.loopback; }
+
+void Abort(Comms &c) {
+  const Api &a = GetApi();
+  for (auto &x : c.comms)
+    if (x && a.abort) a.abort(x), x = nullptr;
+}
 
 __global__ void sum_lanes_kernel(const int64_t *g, int nranks, int lanes, int64_t *out) {
   for (int j = threadIdx.x; j < lanes; j += blockDim.x) {

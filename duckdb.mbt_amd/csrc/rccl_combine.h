@@ -35,6 +35,9 @@ struct Comms {
 // a box with one GPU (same-device shards).
 std::shared_ptr<Comms> Open(const std::vector<int> &devs, bool loopback, std::string *note);
 bool IsLoopback(const Comms &c);
+// ncclCommAbort on every rank (a collective that never completed); the
+// communicators are gone afterwards
+void Abort(Comms &c);
 
 // One collective over every rank, driven from the calling thread: rank i's
 // count int64 lanes send[i] on streams[i] -> recv[i] (all-gather: n * count

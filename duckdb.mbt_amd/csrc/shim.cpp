@@ -1584,11 +1584,24 @@ char *duckdb_mbx_jit_selftest(void) {
 int32_t duckdb_mbx_hbm_calibrate_ex(duckdb_mb_connection *h, int64_t bytes, int32_t iters, double *out, int32_t nout) {
   if (!h || !out || nout <= 0) return 0;
   try {
-    double all[7] = {0, 0, 0, 0, 0, 0, 0};
+    double all[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     HbmCalibrateConn(h->conn, bytes, iters, all);
-    const int k = nout < 7 ? nout : 7;
+    const int k = nout < 8 ? nout : 8;
     for (int i = 0; i < k; i++) out[i] = all[i];
     return k;
+  } catch (std::exception &e) {
+    SetError(e.what());
+    return 0;
+  }
+}
+// In-kernel clock stamps of the last filter_agg_lds / group_direct_lds /
+// two-array ring launch: {memtime, realtime} at the start and the end of each
+// of the first cap workgroups' main loop (libduckdb_mb_amd_clk.so, `make
+// clockdiag`); returns the workgroups copied, 0 from the product library.
+int32_t duckdb_mbx_clock_stamps(duckdb_mb_connection *h, uint64_t *out4, int32_t cap) {
+  if (!h || !out4 || cap <= 0) return 0;
+  try {
+    return ClockStampsConn(h->conn, out4, cap);
   } catch (std::exception &e) {
     SetError(e.what());
     return 0;
@@ -1744,13 +1757,14 @@ char *duckdb_mbx_rccl_note(duckdb_mb_connection *h) {
 
 // mbx_combine counters, up to cap of {RCCL combines, fallbacks to the host
 // merge, combines through the test loopback, combines that raised a shard's
-// device error}; returns how many were written.
+// device error, collectives aborted after the timeout}; returns how many were
+// written.
 int32_t duckdb_mbx_rccl_stats_ex(duckdb_mb_connection *h, int64_t *out, int32_t cap) {
   if (!h || !out) return 0;
   const ShardStats &st = h->conn.shard_stats;
-  const int64_t v[4] = {st.rccl_combines, st.rccl_fallbacks, st.rccl_loopbacks, st.rccl_errors};
+  const int64_t v[5] = {st.rccl_combines, st.rccl_fallbacks, st.rccl_loopbacks, st.rccl_errors, st.rccl_timeouts};
   int32_t n = 0;
-  for (; n < cap && n < 4; n++) out[n] = v[n];
+  for (; n < cap && n < 5; n++) out[n] = v[n];
   return n;
 }
 

@@ -214,12 +214,20 @@ char *duckdb_mbx_profile_drain(duckdb_mb_connection *handle);
  * float4 copy (read+write bytes), a non-temporal int64 read and a plain int64
  * read over `bytes`-sized buffers -> out3[0..2].  Returns 1 on success. */
 int32_t duckdb_mbx_hbm_calibrate(duckdb_mb_connection *handle, int64_t bytes, int32_t iters, double *out3);
-/* the same plus the hot kernels' shapes: out[0..6] = copy, nt read, read,
+/* the same plus the hot kernels' shapes: out[0..7] = copy, nt read, read,
  * LDS-DMA ring read, unrolled nt copy, LDS-DMA ring copy, ring copy writing
- * half of what it reads (GB/s; a copy counts read + write); returns how many
+ * half of what it reads, C3's two-array ring read (4-byte + 8-byte column,
+ * 2-deep 3 KiB slots) (GB/s; a copy counts read + write); returns how many
  * were written (<= nout), 0 on error */
 int32_t duckdb_mbx_hbm_calibrate_ex(duckdb_mb_connection *handle, int64_t bytes, int32_t iters, double *out,
                                     int32_t nout);
+/* Diagnostic build only (`make -C duckdb.mbt_amd clockdiag` ->
+ * libduckdb_mb_amd_clk.so): the in-kernel clock stamps of the last
+ * filter_agg_lds / group_direct_lds / two-array ring launch, 4 values per
+ * workgroup {s_memtime, s_memrealtime at the main loop's start, the same at
+ * its end}; clock = d(memtime) / d(realtime) x 100 MHz.  Returns the
+ * workgroups copied (<= cap); 0 from the product library, which has no stamps. */
+int32_t duckdb_mbx_clock_stamps(duckdb_mb_connection *handle, uint64_t *out4, int32_t cap);
 
 /* ---- DataChunk / Vector / LogicalType (ref src/duckdb_native.c:1926-2132) ----
  * The reference wraps libduckdb's data-chunk API; these handles keep its C
@@ -304,7 +312,7 @@ int32_t duckdb_mbx_shard_timings(duckdb_mb_connection *connection, double *out, 
  * accessors and free it with duckdb_mb_result_destroy; NULL if none. */
 duckdb_mb_result *duckdb_mbx_shard_partial(duckdb_mb_connection *connection, int32_t shard);
 
-/* mbx_combine=rccl (Config::set key, ref src/duckdb_native.c:714-747): a
+/* mbx_combine=rccl (the default; Config::set key, ref src/duckdb_native.c:714-747): a
  * sharded global aggregate over distinct devices is combined by RCCL on the
  * shard devices (ncclInt64 all-reduce for COUNT-only rows; all-gather of int128
  * lanes + a carry-correct combine on device 0 otherwise).  out2 = {RCCL
@@ -314,8 +322,9 @@ int32_t duckdb_mbx_rccl_stats(duckdb_mb_connection *connection, int64_t *out2, d
 /* Why the last RCCL request fell back ("" if it ran); free with duckdb_mbx_free. */
 char *duckdb_mbx_rccl_note(duckdb_mb_connection *connection);
 /* Up to cap of {RCCL combines, host-merge fallbacks, combines through the test
- * loopback, combines that raised a shard's device error}; returns the count
- * written. */
+ * loopback, combines that raised a shard's device error, collectives aborted
+ * after MBX_RCCL_TIMEOUT_MS (default 20 s; the host merge answers)}; returns
+ * the count written. */
 int32_t duckdb_mbx_rccl_stats_ex(duckdb_mb_connection *connection, int64_t *out, int32_t cap);
 /* 1: RCCL combine, 0: host merge, from the next statement on; 2: the RCCL
  * combine with its collectives replaced by device copies (tests only: refused
