@@ -106,7 +106,7 @@ struct GroupPreds {
 bool GroupByDirectStates(const void *kcol, int kphys, int64_t kmin, int nk, const void *v0, const void *v1, int vphys,
                          int nv, bool mm, int64_t nrows, int64_t seg_rows, int R, unsigned long long *cstar,
                          AggState *st0, AggState *st1, int grid_blocks, hipStream_t s,
-                         const GroupPreds *pred = nullptr, uint64_t vmaxabs = ~0ull,
+                         const GroupPreds *pred = nullptr, uint64_t vmaxabs = ~0ull /* (unused) */,
                          const uint64_t *v0valid = nullptr);  // v0's validity words (nv == 1): false if unsupported
 
 // --- generic aggregation over compacted columns ---------------------------
@@ -332,12 +332,10 @@ int64_t CountEntries(int64_t nrows);  // pass-1 count entries (the count array h
 void FilterCountChunks(const FilterMultiDesc &d, int64_t nrows, uint32_t *counts, hipStream_t s);
 void CompactRecompute(const CompactDesc &d, int64_t nrows, const int64_t *chunk_offsets, hipStream_t s);
 
-// One-pass filter -> compaction (select_kernels.hip): every loaded column (the
-// union of the predicate and output columns, 4 or 8 bytes, no NULLs) is read
-// from HBM once; tiles are claimed by an atomic ticket and ordered by a
-// decoupled look-back over per-tile status words.  Outputs must have room for
-// every row (the selected count is not known up front); the count lands in
-// *total.  status_buf: SelectStatusBytes(nrows, ni) bytes (ni = Σ w / 4).
+// One-pass filter -> compaction (select_kernels.hip, select_rounds): every
+// loaded column (the union of the predicate and output columns, 4 or 8 bytes)
+// is read from HBM once.  Outputs must have room for every row (the selected
+// count is not known up front).
 #define SL_MAX_COL 4
 #define SL_MAX_OUT 4
 struct SelectDesc {
@@ -368,29 +366,12 @@ struct SelectDesc {
   long long *zstats;
   int32_t zmask;
   int32_t zstore;  // 1: the storers fold the zone maps while copying, 0: the loaders
-  int32_t nt_off;  // select_rounds storers (MBX_SR_NT_OFF, A/B): bit 0 = plain value stores, bit 1 = plain validity stores (default: non-temporal)
-  int32_t copy1;   // select_rounds storers (MBX_SR_COPY1, A/B): 0 = 4 rows per lane per pass, 1 = one, 2 = 4 with byte validity stores
-  // select_rounds, 8 loaders: the validity of ONE NULL-able output (index vbo,
-  // -1: none) leaves as ballots instead of bytes.  Loaders write, per 256-row
-  // sub-step gs of the input, 8 words at vball[8 gs]: the 4 selection ballots,
-  // then the 4 ballots of selected-and-valid rows (bit l of word e = row
-  // 256 gs + 4 l + e); the staged value of a NULL row is 0.  Storers write
-  // vpos[range] = the output row of each loader range's first row (range =
-  // ((round G + workgroup) NL + loader); S steps each), workgroup 0's tail loop
-  // the sub-steps after nsteps H and vpos[nrounds G NL].  PackValidityBallots
-  // then builds the bitmap, one thread per output word.
-  unsigned long long *vball;
-  int64_t *vpos;
-  int32_t vbo;
-  unsigned long long *dbg;     // nullptr, or 9 counters (MBX_SL_DEBUG) / 14 (MBX_SR_DEBUG)
+  unsigned long long *dbg;     // nullptr, or 14 counters (MBX_SR_DEBUG)
   unsigned long long *dbg_ts;  // MBX_SR_DEBUG=2: s_memrealtime of every (round, workgroup) publish
 };
-size_t SelectStatusBytes(int64_t nrows, int ni);
-void SelectCompact(const SelectDesc &d, int64_t nrows, void *status_buf, int64_t *total, hipStream_t s);
 
 // Round-synchronous one-pass filter -> compaction (select_kernels.hip,
-// select_rounds): the same shapes and output contract as SelectCompact, one
-// persistent workgroup per CU.  Round r's tile of workgroup g is 4 S steps; a
+// select_rounds), one persistent workgroup per CU.  Round r's tile of workgroup g is 4 S steps; a
 // workgroup's round count is published as an 8-byte {count, epoch} granule
 // and every workgroup reads each round's G granules to place its tile.  ctl:
 // SelectRoundsCtlBytes(plan) bytes, zeroed once when allocated and reused
@@ -411,14 +392,6 @@ hipError_t SelectRounds(const SelectDesc &d, const SelectRoundsPlan &p, int64_t 
                   uint32_t epoch, hipStream_t s);
 // bits[i / 64] bit i % 64 = bytes[i] (0/1), for the n output rows of a NULL-able select_rounds output
 void PackValidityBytes(const uint8_t *bytes, int64_t n, uint64_t *bits, hipStream_t s);
-// the bitmap of the ballot-mode output (SelectDesc::vbo) of a finished launch
-// of plan p over nrows input rows with n selected rows
-void PackValidityBallots(const unsigned long long *vball, const int64_t *vpos, const SelectRoundsPlan &p,
-                         int64_t nrows, int64_t n, uint64_t *bits, int64_t *wmap, hipStream_t s);  // wmap: (n + 63) / 64 words of scratch
-// words of vball / vpos a launch of plan p over nrows rows writes (+ the dump
-// slot of dead steps)
-size_t SelectBallotWords(const SelectRoundsPlan &p, int64_t nrows);
-size_t SelectRangeCount(const SelectRoundsPlan &p);
 
 }  // namespace dev
 }  // namespace mbx

@@ -62,60 +62,7 @@ struct DevicePool {
   size_t cached = 0;
   hipStream_t s = nullptr;
   int device = 0;
-  // MBX_VMM_MIN_MB (experiment, off by default): blocks of at least that many
-  // MiB come from the virtual memory API (hipMemCreate + hipMemMap at the
-  // recommended granularity) instead of hipMalloc -- the round-3 verdict's
-  // idea for the C3 placement effect (profiles/r04_c3_*)
-  struct Vmm {
-    hipMemGenericAllocationHandle_t h;
-    size_t size;
-  };
-  std::map<void *, Vmm> vmm_;
-  size_t vmm_min = [] {
-    const char *e = Knob("MBX_VMM_MIN_MB");
-    return e ? (size_t)atoll(e) << 20 : (size_t)0;
-  }();
-  void *VmmAlloc(size_t b) {
-    hipMemAllocationProp prop;
-    memset(&prop, 0, sizeof(prop));
-    prop.type = hipMemAllocationTypePinned;
-    prop.location.type = hipMemLocationTypeDevice;
-    prop.location.id = device;
-    size_t gran = 0;
-    if (hipMemGetAllocationGranularity(&gran, &prop, hipMemAllocationGranularityRecommended) != hipSuccess || !gran)
-      return nullptr;
-    const size_t size = (b + gran - 1) / gran * gran;
-    void *p = nullptr;
-    if (hipMemAddressReserve(&p, size, gran, nullptr, 0) != hipSuccess) return nullptr;
-    hipMemGenericAllocationHandle_t h;
-    if (hipMemCreate(&h, size, &prop, 0) != hipSuccess) {
-      (void)hipMemAddressFree(p, size);
-      return nullptr;
-    }
-    hipMemAccessDesc acc;
-    memset(&acc, 0, sizeof(acc));
-    acc.location = prop.location;
-    acc.flags = hipMemAccessFlagsProtReadWrite;
-    if (hipMemMap(p, size, 0, h, 0) != hipSuccess || hipMemSetAccess(p, size, &acc, 1) != hipSuccess) {
-      (void)hipMemUnmap(p, size);
-      (void)hipMemRelease(h);
-      (void)hipMemAddressFree(p, size);
-      return nullptr;
-    }
-    vmm_[p] = {h, size};
-    return p;
-  }
-  void Free(void *p) {
-    auto it = vmm_.find(p);
-    if (it == vmm_.end()) {
-      (void)hipFree(p);
-      return;
-    }
-    (void)hipMemUnmap(p, it->second.size);
-    (void)hipMemRelease(it->second.h);
-    (void)hipMemAddressFree(p, it->second.size);
-    vmm_.erase(it);
-  }
+  void Free(void *p) { (void)hipFree(p); }
   static size_t Bucket(size_t bytes) {
     if (bytes <= 256) return 256;
     size_t p2 = 256;
@@ -140,11 +87,6 @@ struct DevicePool {
       return p;
     }
     void *p = nullptr;
-    if (vmm_min && b >= vmm_min) {
-      p = VmmAlloc(b);
-      if (p) return p;
-      (void)hipGetLastError();
-    }
     if (hipMalloc(&p, b) != hipSuccess) {
       (void)hipGetLastError();
       ReleaseAll();  // give cached blocks back and retry once
@@ -1132,9 +1074,9 @@ static bool FastIntCol(const DRel &rel, int c) {
 //    two persistent grids never compete for the CUs; should a workgroup never
 //    be scheduled anyway, the kernel gives up after 100 ms without progress
 //    and the two-pass form runs instead.
-//  * MBX_SL=2: dev::SelectCompact, the decoupled look-back kernel (measured
-//    2-9x slower than the two-pass forms, profiles/r02_select_onepass.log).
-//  * MBX_SL=0: never (the count-first / ballot-bits two-pass forms).
+//  * MBX_SL=0: never (the count-first / ballot-bits two-pass forms).  (A
+//    decoupled look-back one-pass kernel measured 2-9x slower than the
+//    two-pass forms and was removed, profiles/r02_select_onepass.log.)
 static std::mutex g_rounds_mu[64];
 
 static bool TrySelectOnePass(Engine &e, const DRel &rel, const dev::FilterMultiDesc &F,
@@ -1144,11 +1086,10 @@ static bool TrySelectOnePass(Engine &e, const DRel &rel, const dev::FilterMultiD
   if (mode == 0) return false;
   int64_t min_rows = (int64_t)1 << 22;
   if (const char *m = Knob("MBX_SR_MIN_ROWS")) min_rows = atoll(m);
-  if (mode == 1 && rel.n < min_rows) return false;
+  if (rel.n < min_rows) return false;
   if ((int)exprs.size() > SL_MAX_OUT) return false;
   dev::SelectDesc S;
   memset(&S, 0, sizeof(S));
-  S.vbo = -1;
   auto slot_of = [&](const void *data, int w) -> int {
     for (int i = 0; i < S.ncol; i++)
       if (S.col[i].data == data) return S.col[i].w == w ? i : -2;
@@ -1159,7 +1100,7 @@ static bool TrySelectOnePass(Engine &e, const DRel &rel, const dev::FilterMultiD
   };
   bool any_valid = false;
   for (int j = 0; j < F.ncol; j++) {
-    if (F.col[j].valid && (mode == 2 || (uintptr_t)F.col[j].valid % 16)) return false;
+    if (F.col[j].valid && (uintptr_t)F.col[j].valid % 16) return false;
     const int i = slot_of(F.col[j].data, F.col[j].phys == P_I64 ? 8 : 4);
     if (i < 0) return false;
     S.col[i].valid = F.col[j].valid;
@@ -1173,11 +1114,9 @@ static bool TrySelectOnePass(Engine &e, const DRel &rel, const dev::FilterMultiD
   const bool narrow_ok = !(nenv && atoi(nenv) == 0);
   const char *senv = Knob("MBX_SR_SENT");  // MBX_SR_SENT=0: NULL-able outputs stage validity bytes (A/B)
   const bool sent_off = senv && atoi(senv) == 0;
-  if (const char *c1 = Knob("MBX_SR_COPY1")) S.copy1 = atoi(c1);
-  if (const char *nt = Knob("MBX_SR_NT_OFF")) S.nt_off = atoi(nt);  // storers: 1 = plain value stores, 2 = plain validity stores (A/B)  // storers: 1 = one row per lane per pass, 2 = byte validity stores (A/B)
   for (auto &x : exprs) {
     const DCol &c = rel.cols[x->col];
-    if (c.validity && (mode == 2 || (uintptr_t)c.validity % 16)) return false;
+    if (c.validity && (uintptr_t)c.validity % 16) return false;
     const int w = PhysSize(c.phys);
     if (w != 4 && w != 8) return false;
     const int i = slot_of(c.data, w);
@@ -1213,55 +1152,15 @@ static bool TrySelectOnePass(Engine &e, const DRel &rel, const dev::FilterMultiD
   if (const char *c = Knob("MBX_SL_MAX_GB")) cap_gb = atof(c);
   if (out_bytes > cap_gb * 1e9) return false;
   const int64_t n = rel.n;
-  dev::SelectRoundsPlan plan;
-  memset(&plan, 0, sizeof(plan));
-  // Ballot-mode validity for one NULL-able output (SelectDesc::vbo): with 8
-  // loaders the storers were the bottleneck of NULL-able outputs (busy ~90 %,
-  // profiles/r04_select_rounds_role_split.log); in this mode they copy the
-  // values like a NULL-free output, the loaders store each step's ballots,
-  // and PackValidityBallots builds the bitmap.  Only when the planner gives
-  // the 8-loader H = 1 form, and the column feeds no other output.
-  // MBX_SR_VBALL=1 turns it on (default off until measured on the GPU).
-  int vb_k = -1;
-  if (mode != 2) {
-    const char *vbk = Knob("MBX_SR_VBALL");
-    if (vbk && atoi(vbk) == 1)
-      for (int k = 0; k < S.nout && vb_k < 0; k++) {
-        const int i = S.out_col[k];
-        if (!S.col[i].valid) continue;
-        int uses = 0;
-        for (int k2 = 0; k2 < S.nout; k2++) uses += S.out_col[k2] == i;
-        if (uses == 1) vb_k = k;
-      }
-    int32_t save_vsent = 0;
-    int64_t save_sent = 0;
-    const int vb_i = vb_k >= 0 ? S.out_col[vb_k] : -1;
-    if (vb_i >= 0) {
-      save_vsent = S.col[vb_i].vsent, save_sent = S.col[vb_i].sent;
-      S.col[vb_i].vsent = 2, S.col[vb_i].sent = 0;  // a NULL row is staged as 0, with no byte of its own
-    }
-    plan = dev::PlanSelectRounds(S, n);
-    if (vb_i >= 0 && !(plan.ok && plan.NL == 8 && plan.H == 1)) {
-      S.col[vb_i].vsent = save_vsent, S.col[vb_i].sent = save_sent;
-      vb_k = -1;
-      plan = dev::PlanSelectRounds(S, n);
-    }
-    if (!plan.ok) return false;
-  }
+  const dev::SelectRoundsPlan plan = dev::PlanSelectRounds(S, n);
+  if (!plan.ok) return false;
   std::vector<DCol> cols;
   std::vector<DevBufPtr> vbytes(exprs.size());  // NULL-able outputs: one validity byte per output row
-  DevBufPtr vball, vpos;                         // ballot mode: per-step ballots, per-range output rows
   for (int k = 0; k < (int)exprs.size(); k++) {
     const bool nullable = rel.cols[exprs[k]->col].validity != nullptr;
     cols.push_back(AllocOut(e, exprs[k]->type, n, nullable, false));
     S.dst[k] = cols[k].data;
-    if (nullable && k == vb_k) {  // (released to the engine's pool when this returns: later users run after the pack on e.stream)
-      vball = Alloc(e, dev::SelectBallotWords(plan, n) * 8);
-      vpos = Alloc(e, (dev::SelectRangeCount(plan) + 1) * 8);
-      S.vball = (unsigned long long *)vball->p;
-      S.vpos = (int64_t *)vpos->p;
-      S.vbo = k;
-    } else if (nullable) {
+    if (nullable) {
       vbytes[k] = Alloc(e, (size_t)std::max<int64_t>(n, 1) + 64);
       S.vdst[k] = (uint8_t *)vbytes[k]->p;
     }
@@ -1270,7 +1169,7 @@ static bool TrySelectOnePass(Engine &e, const DRel &rel, const dev::FilterMultiD
   for (int i = 0; i < S.ncol; i++) bytes += (double)n * S.col[i].w + (S.col[i].valid ? n / 8.0 : 0);
   int64_t nsel = 0;
   int32_t rounds_err = -1;  // the error word read with the round total (-1: not read)
-  if (mode != 2) {
+  {
     std::unique_lock<std::mutex> lk(g_rounds_mu[e.device & 63]);
     const size_t need = dev::SelectRoundsCtlBytes(plan);
     if (need > e.rounds_bytes) {
@@ -1400,40 +1299,13 @@ static bool TrySelectOnePass(Engine &e, const DRel &rel, const dev::FilterMultiD
       return false;
     }
     nsel = (int64_t)h[1];
-  } else {
-    auto status = Alloc(e, dev::SelectStatusBytes(n, ni));
-    DevBufPtr dbgbuf;
-    if (Knob("MBX_SL_DEBUG")) {
-      dbgbuf = Alloc(e, 128, true);
-      S.dbg = (unsigned long long *)dbgbuf->p;
-    }
-    {
-      ProfScope ps(e, "select", bytes, n);
-      dev::SelectCompact(S, n, status->p, e.d_scratch, e.stream);
-    }
-    if (dbgbuf) {
-      unsigned long long h[9];
-      HIPCHK(hipMemcpyAsync(h, dbgbuf->p, sizeof(h), hipMemcpyDeviceToHost, e.stream));
-      HIPCHK(hipStreamSynchronize(e.stream));
-      fprintf(stderr, "[select] dma_wait %llu b1b2 %llu lookback %llu ticket %llu compact %llu windows %llu spins %llu "
-              "tiles %llu total %llu (cycles summed over workgroups)\n", h[0], h[1], h[2], h[3], h[4], h[5], h[6], h[7], h[8]);
-    }
-    nsel = ReadDev<int64_t>(e, e.d_scratch);
   }
-  if (e.profile && !e.events.empty() && (e.events.back().name == "select" || e.events.back().name == "select_rounds")) {
+  if (e.profile && !e.events.empty() && e.events.back().name == "select_rounds") {
     double ob = 0;
     for (int k = 0; k < S.nout; k++) ob += (double)nsel * (S.col[S.out_col[k]].w + (S.vdst[k] ? 1 : 0));
     e.events.back().bytes += ob;
   }
   for (int k = 0; k < S.nout; k++) {
-    if (k == S.vbo) {
-      const int64_t nsub = (int64_t)dev::SelectBallotWords(plan, n) / 8;
-      ProfScope ps(e, "pack_validity", (double)nsub * 64 + (double)dev::SelectRangeCount(plan) * 8 + nsel / 8.0, nsel);
-      auto wmap = Alloc(e, (size_t)((nsel + 63) / 64) * 8 + 8);
-      dev::PackValidityBallots(S.vball, S.vpos, plan, n, nsel, (uint64_t *)cols[k].validity, (int64_t *)wmap->p,
-                               e.stream);
-      continue;
-    }
     if (!S.vdst[k]) continue;
     ProfScope ps(e, "pack_validity", (double)nsel + nsel / 8.0, nsel);
     dev::PackValidityBytes(S.vdst[k], nsel, cols[k].validity, e.stream);
@@ -1442,7 +1314,7 @@ static bool TrySelectOnePass(Engine &e, const DRel &rel, const dev::FilterMultiD
   out.n = nsel;
   out.cols = cols;
   bool packed = false;
-  for (int k = 0; k < S.nout; k++) packed |= S.vdst[k] != nullptr || k == S.vbo;
+  for (int k = 0; k < S.nout; k++) packed |= S.vdst[k] != nullptr;
   if (rounds_err >= 0 && !packed) RaiseDeviceError(e, rounds_err);  // nothing ran after that read
   else CheckError(e);
   return true;

@@ -1661,15 +1661,12 @@ __global__ __launch_bounds__(256) void group_direct_kernel(const TK *__restrict_
 // 16-B/lane global_load_lds (1 KiB per instruction, no VGPR staging); each
 // lane then owns 4 consecutive rows.  Waves walk steps grid-stride.  The
 // replicated LDS tables and the rings share ONE dynamic __shared__ array.
-//
-// PK (packed count): the row's COUNT rides in the low PKB bits of its SUM
-// atomic — one ds_add_u64 of (v << PKB) + 1 per row instead of a ds_add_u32
-// plus a ds_add_u64.  That bounded this kernel while the compiler drained the
-// ring before every LDS atomic; with the asm atomics below the plain form is
-// faster, and PK stays behind MBX_GD_PACK=1.
-// Every PKF wave steps the block drains the packed table into per-thread
-// register partials (slot t + 256 j), before a count can reach 2^PKB or the
-// shifted sum can leave int64; the host derives PKB/PKF from the zone maps.
+// Each row takes a ds_add_u32 for its COUNT and a ds_add_u64 for its SUM.  (A
+// packed form -- the COUNT in the low bits of one ds_add_u64 per row, drained
+// into registers every few thousand steps -- bounded this kernel while the
+// compiler drained the ring before every LDS atomic; with the asm atomics
+// below the plain form is faster: C3 1.684 vs 1.744 ms,
+// profiles/r02_group_unpacked.log, so it was removed.)
 // LDS atomics of the table as inline-asm ds_* ops that return nothing: the
 // compiler puts an s_waitcnt vmcnt(0) in front of every atomic LDS access
 // while LDS-DMA is in flight (it cannot prove the table and the ring do not
@@ -1694,15 +1691,14 @@ __device__ __forceinline__ void gd_max_i64(long long *p, long long v) {
 // VV (NV = 1): the value column has NULLs.  Its step's 32 B of validity
 // words ride the ring slot after the value slice (one exec-masked glds);
 // COUNT(*) takes its own ds_add_u32 per row, the valid rows are counted in
-// vcnt (a ds_add_u32 of their own, or the packed count of the SUM atomic
-// drained into vcnt under PK), and SUM / MIN / MAX see the valid rows only; a
-// predicate on the value column fails on NULL.
-template <typename TK, typename TV, int NV, bool MM, int DEPTH, bool PK, bool VV = false>
+// vcnt (a ds_add_u32 of their own), and SUM / MIN / MAX see the valid rows
+// only; a predicate on the value column fails on NULL.
+template <typename TK, typename TV, int NV, bool MM, int DEPTH, bool VV = false>
 __global__ __launch_bounds__(256) void group_direct_lds_kernel(const TK *__restrict__ keys, const TV *__restrict__ v0,
                                                                const TV *__restrict__ v1, int64_t n, int64_t kmin,
                                                                int nk, int R, size_t ring_off,
                                                                unsigned long long *cstar, AggState *st0,
-                                                               AggState *st1, GroupPreds pr, int PKB, int PKF,
+                                                               AggState *st1, GroupPreds pr,
                                                                const uint64_t *__restrict__ vvalid) {
   static_assert(!VV || NV == 1, "validity: one value column");
   extern __shared__ __attribute__((aligned(16))) unsigned char lds_raw[];
@@ -1749,44 +1745,17 @@ __global__ __launch_bounds__(256) void group_direct_lds_kernel(const TK *__restr
     int sl = (int)(k - kmin) * R + rep;
     if (VV) {
       gd_add_u32(&cnt[sl], 1u);
-      if (valid && PK) gd_add_u64(&sum0[sl], ((unsigned long long)a << PKB) + 1ull);
-      if (valid && !PK) { gd_add_u32(&vcnt[sl], 1u); gd_add_u64(&sum0[sl], (unsigned long long)a); }
+      if (valid) { gd_add_u32(&vcnt[sl], 1u); gd_add_u64(&sum0[sl], (unsigned long long)a); }
       if (MM && valid) { gd_min_i64(&mn0[sl], (long long)a); gd_max_i64(&mx0[sl], (long long)a); }
       return;
     }
-    if (PK) {
-      gd_add_u64(&sum0[sl], ((unsigned long long)a << PKB) + 1ull);
-    } else {
-      gd_add_u32(&cnt[sl], 1u);
-      if (NV >= 1) gd_add_u64(&sum0[sl], (unsigned long long)a);
-    }
+    gd_add_u32(&cnt[sl], 1u);
+    if (NV >= 1) gd_add_u64(&sum0[sl], (unsigned long long)a);
     if (NV >= 2) gd_add_u64(&sum1[sl], (unsigned long long)b);
     if (MM) {
       gd_min_i64(&mn0[sl], (long long)a); gd_max_i64(&mx0[sl], (long long)a);
       if (NV >= 2) { gd_min_i64(&mn1[sl], (long long)b); gd_max_i64(&mx1[sl], (long long)b); }
     }
-  };
-  // PK: register partials of slots t + 256 j (nslot <= 256 * PK_J, checked by the host)
-  constexpr int PK_J = 8;
-  unsigned int rc[PK_J];
-  long long rs[PK_J];
-#pragma unroll
-  for (int j = 0; j < PK_J; j++) { rc[j] = 0; rs[j] = 0; }
-  auto pk_drain = [&]() {
-    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
-    const unsigned long long m = (1ull << PKB) - 1;
-#pragma unroll
-    for (int j = 0; j < PK_J; j++) {
-      int sl = t + 256 * j;
-      if (sl < nslot) {
-        unsigned long long p = (unsigned long long)sum0[sl];
-        unsigned long long c = p & m;
-        rc[j] += (unsigned int)c;
-        rs[j] += (long long)(p - c) >> PKB;
-        sum0[sl] = 0;
-      }
-    }
-    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
   };
   const int64_t nsteps = n >> 8;
   const int64_t nw = (int64_t)gridDim.x * 4;
@@ -1796,11 +1765,6 @@ __global__ __launch_bounds__(256) void group_direct_lds_kernel(const TK *__restr
   int64_t bl = blockIdx.x;
   if (pr.xcd && (gridDim.x & 7) == 0) bl = (int64_t)(blockIdx.x & 7) * (gridDim.x >> 3) + (blockIdx.x >> 3);
   int64_t st = bl * 4 + w;
-  // steps of the block's last wave (the fewest): in-loop drains happen only
-  // while every wave of the block still iterates, so all reach the barrier
-  const int64_t last_w = bl * 4 + 3;
-  const int64_t min_steps = last_w < nsteps ? (nsteps - 1 - last_w) / nw + 1 : 0;
-  int64_t it = 0;
   // issue one step's glds into slot d: key slice, then each value slice
   auto issue = [&](int64_t q, int d) {
     unsigned char *dst = ring + d * SB;
@@ -1899,10 +1863,6 @@ __global__ __launch_bounds__(256) void group_direct_lds_kernel(const TK *__restr
     for (int e = 0; e < 4; e++)
       if (ok[e]) row(kk[e], NV >= 1 ? a[e] : 0, NV >= 2 ? b[e] : 0, ((vm >> e) & 1u) != 0);
     k = k + 1 == DEPTH ? 0 : k + 1;
-    if (PK) {
-      ++it;
-      if (it % PKF == 0 && it <= min_steps) pk_drain();
-    }
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   MBX_CLK(1);
@@ -1921,18 +1881,6 @@ __global__ __launch_bounds__(256) void group_direct_lds_kernel(const TK *__restr
     }
   }
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // this thread's table atomics (asm) have landed
-  if (PK) {
-    pk_drain();
-#pragma unroll
-    for (int j = 0; j < PK_J; j++) {
-      int sl = t + 256 * j;
-      if (sl < nslot) {
-        if (VV) vcnt[sl] = rc[j];  // cnt[] keeps COUNT(*) from its own atomics
-        else cnt[sl] = rc[j];
-        sum0[sl] = rs[j];
-      }
-    }
-  }
   __syncthreads();
   for (int kq = t; kq < nk; kq += blockDim.x) {
     unsigned long long c = 0, vc = 0;
@@ -1986,26 +1934,6 @@ size_t GroupDirectLds(int nk, int R, int nv, bool mm, bool vv) {
   if (mm) b += nslot * 8 * 2 * (size_t)(nv >= 2 ? 2 : 1);
   if (vv) b += (nslot * 4 + 15) & ~(size_t)15;  // valid-row counts
   return b;
-}
-
-// Packed-count parameters for group_direct_lds (PK): the largest drain period
-// (wave steps) such that between drains no replica slot's count reaches 2^PKB
-// and |sum| << PKB stays inside int64.  A slot absorbs at most 1024/R rows per
-// block step (64/R lanes x 4 rows x 4 waves), plus 256 tail rows in block 0.
-// Returns false when no period of at least 16 steps exists.
-static bool PackedCountParams(uint64_t vmaxabs, int R, int &pkb, int &pkf) {
-  if (vmaxabs >= (1ull << 50)) return false;
-  const uint64_t ma = vmaxabs ? vmaxabs : 1;
-  int64_t best = 0;
-  for (int b = 8; b <= 40; b++) {
-    uint64_t m = std::min<uint64_t>((1ull << b) - 1, ((1ull << (63 - b)) - 1) / ma);  // rows per slot per period
-    if (m <= 256) continue;
-    int64_t f = (int64_t)((m - 256) * (uint64_t)R / 1024);
-    if (f > best) { best = f; pkb = b; }
-  }
-  if (best < 16) return false;
-  pkf = (int)std::min<int64_t>(best, 1 << 20);
-  return true;
 }
 
 bool GroupByDirectStates(const void *kcol, int kphys, int64_t kmin, int nk, const void *v0, const void *v1, int vphys,
@@ -2066,34 +1994,18 @@ bool GroupByDirectStates(const void *kcol, int kphys, int64_t kmin, int nk, cons
         ring_off = (tab + 15) & ~(size_t)15;
         lds = ring_off + 4 * (size_t)depth * slot;
       }
-      // packed count: needs a value column, the register partials (nslot <=
-      // 2048) and a zone-map bound on |v|.  Since the table atomics stopped
-      // draining the DMA ring, two plain atomics per row beat one packed atomic
-      // plus the periodic drains (C3 1.744 -> 1.684 ms, with MIN/MAX 2.12 ->
-      // 1.87; profiles/r02_group_unpacked.log).  Both forms need the one flush
-      // at the end to be overflow-safe (else the segmented kernel), so packing
-      // is now used only for MBX_GD_PACK=1 (the NULL-able value form included:
-      // c3n 2.18 ms packed, profiles/r02_group_unpacked.log).
-      int pkb = 0, pkf = 0;
-      bool pk = nv >= 1 && (int64_t)nk * R <= 2048 && PackedCountParams(vmaxabs, R, pkb, pkf);
+      // one flush at the end must be overflow-safe (else the segmented kernel)
       const bool one_flush = seg_rows <= 0 || seg_rows >= rows_per_block;
-      if (one_flush) pk = false;
-      if (const char *ep = Knob("MBX_GD_PACK"))
-        pk = atoi(ep) != 0 && nv >= 1 && (int64_t)nk * R <= 2048 && PackedCountParams(vmaxabs, R, pkb, pkf);
-      // MBX_GD_PKF=<steps>: drain more often than needed (tests exercise the drains)
-      if (const char *ef = Knob("MBX_GD_PKF")) pkf = std::max(1, std::min(pkf, atoi(ef)));
-      if (vv) {  // NULL-able value column: packed counts and one flush only
+      if (vv) {  // NULL-able value column: one flush only
         if (!one_flush || lds > lds_cap) return false;
-#define GLVV1(TK, TV, MM, D, P)                                                                                     \
+#define GLVV(TK, TV, MM, D)                                                                                         \
   {                                                                                                                 \
-    (void)hipFuncSetAttribute((const void *)group_direct_lds_kernel<TK, TV, 1, MM, D, P, true>,                     \
+    (void)hipFuncSetAttribute((const void *)group_direct_lds_kernel<TK, TV, 1, MM, D, true>,                        \
                               hipFuncAttributeMaxDynamicSharedMemorySize, 150 * 1024);                              \
-    hipLaunchKernelGGL((group_direct_lds_kernel<TK, TV, 1, MM, D, P, true>), dim3(grid), dim3(256), lds, s,        \
+    hipLaunchKernelGGL((group_direct_lds_kernel<TK, TV, 1, MM, D, true>), dim3(grid), dim3(256), lds, s,           \
                        (const TK *)kcol, (const TV *)v0, (const TV *)v1, nrows, kmin, nk, R, ring_off, cstar, st0,  \
-                       st1, pr, pk ? pkb : 0, pk ? pkf : 1, v0valid);                                               \
+                       st1, pr, v0valid);                                                                           \
   }
-#define GLVV(TK, TV, MM, D) \
-  if (pk) GLVV1(TK, TV, MM, D, true) else GLVV1(TK, TV, MM, D, false)
 #define GLVVD(TK, TV)                                                                                             \
   if (mm) { if (depth == 2) GLVV(TK, TV, true, 2) else GLVV(TK, TV, true, 3) }                                      \
   else { if (depth == 2) GLVV(TK, TV, false, 2) else GLVV(TK, TV, false, 3) }
@@ -2104,26 +2016,17 @@ bool GroupByDirectStates(const void *kcol, int kphys, int64_t kmin, int nk, cons
         }
 #undef GLVVD
 #undef GLVV
-#undef GLVV1
         CHECK_LAUNCH();
         return true;
       }
-      if ((seg_rows <= 0 || seg_rows >= rows_per_block) && lds <= lds_cap) {
+      if (one_flush && lds <= lds_cap) {
 #define GL(TK, TV, NV, MM, D)                                                                                      \
-  if (lds > 64 * 1024) { /* deep rings at one or two blocks per CU */                                             \
-    (void)hipFuncSetAttribute((const void *)group_direct_lds_kernel<TK, TV, NV, MM, D, NV >= 1>,                   \
-                              hipFuncAttributeMaxDynamicSharedMemorySize, 150 * 1024);                             \
+  if (lds > 64 * 1024) /* deep rings at one or two blocks per CU */                                               \
     (void)hipFuncSetAttribute((const void *)group_direct_lds_kernel<TK, TV, NV, MM, D, false>,                     \
                               hipFuncAttributeMaxDynamicSharedMemorySize, 150 * 1024);                             \
-  }                                                                                                                \
-  if (pk && NV >= 1)                                                                                               \
-    hipLaunchKernelGGL((group_direct_lds_kernel<TK, TV, NV, MM, D, NV >= 1>), dim3(grid), dim3(256), lds, s,       \
-                       (const TK *)kcol, (const TV *)v0, (const TV *)v1, nrows, kmin, nk, R, ring_off, cstar, st0, \
-                       st1, pr, pkb, pkf, (const uint64_t *)nullptr);                                              \
-  else                                                                                                             \
-    hipLaunchKernelGGL((group_direct_lds_kernel<TK, TV, NV, MM, D, false>), dim3(grid), dim3(256), lds, s,         \
-                       (const TK *)kcol, (const TV *)v0, (const TV *)v1, nrows, kmin, nk, R, ring_off, cstar, st0, \
-                       st1, pr, 0, 1, (const uint64_t *)nullptr);
+  hipLaunchKernelGGL((group_direct_lds_kernel<TK, TV, NV, MM, D, false>), dim3(grid), dim3(256), lds, s,           \
+                     (const TK *)kcol, (const TV *)v0, (const TV *)v1, nrows, kmin, nk, R, ring_off, cstar, st0,   \
+                     st1, pr, (const uint64_t *)nullptr);
 #define GLD(TK, TV, NV, MM)                                                                     \
   if (depth == 2) { GL(TK, TV, NV, MM, 2) } else if (depth == 3) { GL(TK, TV, NV, MM, 3) }      \
   else if (depth == 4) { GL(TK, TV, NV, MM, 4) } else if (depth == 6) { GL(TK, TV, NV, MM, 6) } \

@@ -4,34 +4,10 @@
 // Why one pass: the two-pass form (kernels.hip: filter_bits_lds -> scan ->
 // compact_lds) reads every predicate column twice when the predicate column
 // is also an output (SELECT x FROM t WHERE x > 24: 16 GB read + 4.2 GB
-// written per 1e9 rows).  Here each needed column is read from HBM once:
-//
-//  * A tile is 4 waves x S steps x 256 rows.  Workgroups claim tiles with an
-//    atomic ticket (claim order == output order), and every wave pulls its S
-//    steps of every loaded column into its own LDS region by LDS-DMA
-//    (global_load_lds_dwordx4), NBUF tiles in flight per workgroup.
-//  * When a tile has landed, each wave evaluates the predicates (each lane
-//    owns rows 4 lane + e of a step) into ballot words; the tile's count is
-//    published at once as an aggregate (flag AGG) in a per-tile status word.
-//  * Wave 0 then resolves the tile's exclusive prefix by a decoupled
-//    look-back over the predecessors' status words, 64 at a time (one lane
-//    per predecessor, a ballot finds the nearest inclusive prefix), and
-//    publishes the inclusive prefix (flag INC).  Meanwhile the next tiles'
-//    DMA keeps streaming, and the tile itself stays in LDS: nothing is
-//    re-read.
-//  * Each wave then compacts its steps out of LDS: selected values go to a
-//    per-wave staging row at their rank (popcounts of the ballot words below
-//    the lane), and consecutive lanes store consecutive output rows.
-//
-// Progress: a tile is claimed only by a running workgroup, and a workgroup
-// finishes its claimed tiles in claim order, so the lowest unfinished tile
-// always has all its predecessors published or being published by running
-// workgroups: no residency assumption, no deadlock with other kernels sharing
-// the GPU.  Status words are 8-byte agent-scope atomics on both sides.
-//
-// The final partial step (n % 256 rows) follows the last tile: the workgroup
-// that resolved the last tile's inclusive prefix handles it with guarded
-// loads and writes the selected-row total.
+// written per 1e9 rows).  select_rounds (below) reads each needed column from
+// HBM once and places every workgroup's rows by a round-synchronous prefix.
+// The count-first two-pass form (filter_count_lds -> scan ->
+// compact_recomp_lds, at the end of this file) serves small inputs.
 #include <hip/hip_runtime.h>
 
 #include <atomic>
@@ -65,8 +41,6 @@ namespace {
 typedef long long sl_v2i64 __attribute__((ext_vector_type(2)));
 typedef int sl_v4i32 __attribute__((ext_vector_type(4)));
 
-constexpr unsigned long long SL_AGG = 1ull << 62, SL_INC = 2ull << 62, SL_VAL = (1ull << 62) - 1;
-
 __device__ __forceinline__ int64_t sl_wave_sum(int64_t v) {
 #pragma unroll
   for (int m = 32; m >= 1; m >>= 1) v += __shfl_xor(v, m, 64);
@@ -94,281 +68,6 @@ __device__ __forceinline__ int64_t sl_uni(int64_t x) {
 }
 
 }  // namespace
-
-// NI: LDS-DMA instructions (KiB) per 256-row step over all loaded columns;
-// S: steps per wave per tile; NBUF: tiles in flight per workgroup.
-template <int NI, int S, int NBUF>
-__global__ __launch_bounds__(256) void select_lds_kernel(SelectDesc D, int64_t n, int64_t ntiles,
-                                                         unsigned long long *status, unsigned int *ticket,
-                                                         int64_t *total) {
-  extern __shared__ __attribute__((aligned(16))) unsigned char sl_lds[];
-  __shared__ int64_t s_tick[NBUF];
-  __shared__ int64_t s_excl[2];
-  __shared__ uint32_t s_wcnt[2][4];
-  constexpr int SB = NI * 1024;  // one step of every loaded column
-  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  unsigned char *ring = sl_lds + (size_t)w * NBUF * S * SB;
-  unsigned char *stage = sl_lds + (size_t)4 * NBUF * S * SB + (size_t)w * 2048;  // 256 rows x 8 B
-  const int64_t nsteps = n >> 8;
-  const uint64_t lt = (1ull << lane) - 1;
-  int off[SL_MAX_COL];
-  {
-    int o = 0;
-#pragma unroll
-    for (int c = 0; c < SL_MAX_COL; c++) {
-      off[c] = o;
-      if (c < D.ncol) o += D.col[c].w * 256;
-    }
-  }
-  // this wave's S steps of tile T into buffer b (a dummy re-load of step 0
-  // for steps past the end, so every tile is exactly S * NI loads per wave)
-  auto issue = [&](int64_t T, int b) {
-#pragma unroll
-    for (int s = 0; s < S; s++) {
-      int64_t q = (T * 4 + w) * S + s;
-      if (T >= ntiles || q >= nsteps) q = 0;
-      unsigned char *dst = ring + (size_t)(b * S + s) * SB;
-#pragma unroll
-      for (int c = 0; c < SL_MAX_COL; c++) {
-        if (c >= D.ncol) break;
-        const int B = D.col[c].w * 256;
-        const unsigned char *src = (const unsigned char *)D.col[c].data + q * B;
-        __builtin_amdgcn_global_load_lds((const void *)(src + lane * 16), (void *)(dst + off[c]), 16, 0, 2);
-        if (B == 2048)
-          __builtin_amdgcn_global_load_lds((const void *)(src + 1024 + lane * 16), (void *)(dst + off[c] + 1024), 16, 0,
-                                           2);
-      }
-    }
-  };
-
-  if (threadIdx.x == 0)
-    for (int i = 0; i < NBUF; i++) s_tick[i] = (int64_t)atomicAdd(ticket, 1u);
-  __syncthreads();
-#pragma unroll
-  for (int i = 0; i < NBUF - 1; i++) issue(sl_uni(s_tick[i]), i);
-
-  int64_t last_incl = -1;  // wave 0: inclusive prefix of the last tile, if this workgroup resolved it
-  // MBX_SL_DEBUG: wave 0's cycle split (D.dbg: dma wait, barrier 1 -> 2,
-  // look-back loop, ticket, compaction, windows, spins, tiles, total)
-  unsigned long long dg[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
-  const bool dbg = D.dbg != nullptr && w == 0;
-  unsigned long long t_start = dbg ? clock64() : 0, t0 = 0;
-  for (int j = 0;; j++) {
-    const int b = j % NBUF, par = j & 1;
-    const int64_t T = sl_uni(s_tick[b]);
-    if (T >= ntiles) break;  // workgroup-uniform
-    {
-      const int nb = (j + NBUF - 1) % NBUF;
-      issue(sl_uni(s_tick[nb]), nb);
-    }
-    if (dbg) t0 = clock64();
-    asm volatile("s_waitcnt vmcnt(%0)" ::"n"((NBUF - 1) * S * NI) : "memory");
-    if (dbg) dg[0] += clock64() - t0;
-    // --- count: ballots of this wave's S steps
-    unsigned long long bal[S][4];
-    int cnt[S];
-    int cw = 0;
-#pragma unroll
-    for (int s = 0; s < S; s++) {
-      const unsigned char *slot = ring + (size_t)(b * S + s) * SB;
-      const bool live = (T * 4 + w) * S + s < nsteps;
-      bool ok[4] = {live, live, live, live};
-#pragma unroll
-      for (int c = 0; c < SL_MAX_COL; c++) {
-        if (c >= D.ncol) break;
-        if (!D.col[c].is_pred) continue;
-        int64_t v[4];
-        sl_read4(slot + off[c], D.col[c].w, lane, v);
-#pragma unroll
-        for (int e = 0; e < 4; e++) ok[e] = ok[e] && (uint64_t)(v[e]) - (uint64_t)(D.col[c].lo) <= D.col[c].span;
-      }
-      int cs = 0;
-#pragma unroll
-      for (int e = 0; e < 4; e++) {
-        bal[s][e] = __ballot(ok[e]);
-        cs += __popcll(bal[s][e]);
-      }
-      cnt[s] = cs;
-      cw += cs;
-    }
-    if (lane == 0) s_wcnt[par][w] = (uint32_t)cw;
-    __syncthreads();
-    if (dbg) t0 = clock64();
-    // --- wave 0: publish the aggregate, look back, publish the inclusive prefix
-    if (w == 0) {
-      const int64_t A = sl_uni((int64_t)s_wcnt[par][0] + s_wcnt[par][1] + s_wcnt[par][2] + s_wcnt[par][3]);
-      if (lane == 0) __hip_atomic_store(&status[T], SL_AGG | (unsigned long long)A, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      int64_t excl = 0;
-      int64_t base = T - 1;
-      const unsigned long long tl = dbg ? clock64() : 0;
-      while (base >= 0) {
-        if (dbg) dg[5]++;
-        const int64_t idx = base - lane;
-        const unsigned long long v =
-            idx >= 0 ? __hip_atomic_load(&status[idx], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : SL_INC;
-        const unsigned long long incl = __ballot((v >> 62) == 2);
-        const unsigned long long none = __ballot((v >> 62) == 0);
-        // lanes up to and including the nearest inclusive prefix
-        const unsigned long long upto = incl ? (((incl & (~incl + 1)) << 1) - 1) : ~0ull;
-        if (none & upto) {  // a predecessor has not published yet
-          if (dbg) dg[6]++;
-          __builtin_amdgcn_s_sleep(1);
-          continue;
-        }
-        excl += sl_wave_sum(((upto >> lane) & 1) ? (int64_t)(v & SL_VAL) : 0);
-        if (incl) break;
-        base -= 64;
-      }
-      if (dbg) dg[2] += clock64() - tl;
-      const unsigned long long tt = dbg ? clock64() : 0;
-      if (lane == 0) {
-        __hip_atomic_store(&status[T], SL_INC | (unsigned long long)(excl + A), __ATOMIC_RELAXED,
-                           __HIP_MEMORY_SCOPE_AGENT);
-        s_excl[par] = excl;
-        s_tick[b] = (int64_t)atomicAdd(ticket, 1u);  // the tile this buffer takes next
-      }
-      if (T == ntiles - 1) last_incl = excl + A;
-      if (dbg) { __builtin_amdgcn_s_waitcnt(0); dg[3] += clock64() - tt; }
-    }
-    __syncthreads();
-    if (dbg) { dg[1] += clock64() - t0; dg[7]++; t0 = clock64(); }
-    // --- compaction of this wave's steps straight out of LDS
-    int64_t o = s_excl[par];
-    for (int q = 0; q < w; q++) o += s_wcnt[par][q];
-    o = sl_uni(o);
-#pragma unroll
-    for (int s = 0; s < S; s++) {
-      if (cnt[s] == 0) continue;  // wave-uniform
-      const unsigned char *slot = ring + (size_t)(b * S + s) * SB;
-      const unsigned m = (unsigned)((bal[s][0] >> lane) & 1) | (unsigned)((bal[s][1] >> lane) & 1) << 1 |
-                         (unsigned)((bal[s][2] >> lane) & 1) << 2 | (unsigned)((bal[s][3] >> lane) & 1) << 3;
-      const int r0 = __popcll(bal[s][0] & lt) + __popcll(bal[s][1] & lt) + __popcll(bal[s][2] & lt) +
-                     __popcll(bal[s][3] & lt);
-#pragma unroll
-      for (int k = 0; k < SL_MAX_OUT; k++) {
-        if (k >= D.nout) break;
-        const int c = D.out_col[k];
-        int64_t v[4];
-        sl_read4(slot + off[c], D.col[c].w, lane, v);
-        int r = r0;
-        if (D.col[c].w == 8) {
-#pragma unroll
-          for (int e = 0; e < 4; e++)
-            if ((m >> e) & 1u) ((int64_t *)stage)[r++] = v[e];
-          asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-          int64_t *dst = (int64_t *)D.dst[k] + o;
-          for (int i = lane; i < cnt[s]; i += 64) dst[i] = ((const int64_t *)stage)[i];
-        } else {
-#pragma unroll
-          for (int e = 0; e < 4; e++)
-            if ((m >> e) & 1u) ((int32_t *)stage)[r++] = (int32_t)v[e];
-          asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-          int32_t *dst = (int32_t *)D.dst[k] + o;
-          for (int i = lane; i < cnt[s]; i += 64) dst[i] = ((const int32_t *)stage)[i];
-        }
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // staging reads done before it is rewritten
-      }
-      o += cnt[s];
-    }
-    if (dbg) dg[4] += clock64() - t0;
-  }
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  if (dbg && lane == 0) {
-    dg[8] = clock64() - t_start;
-    for (int i = 0; i < 9; i++) atomicAdd(&D.dbg[i], dg[i]);
-  }
-  // --- the partial last step and the total, by the resolver of the last tile
-  // (or block 0 when there is no full tile)
-  if (w == 0 && (last_incl >= 0 || (ntiles == 0 && blockIdx.x == 0))) {
-    const int64_t prefix = last_incl >= 0 ? last_incl : 0;
-    int64_t tcnt = 0;
-    if (n & 255) {
-      bool ok[4];
-      int64_t i0 = (nsteps << 8) + 4 * lane;
-#pragma unroll
-      for (int e = 0; e < 4; e++) {
-        const int64_t i = i0 + e;
-        ok[e] = i < n;
-        for (int c = 0; c < D.ncol && ok[e]; c++) {
-          if (!D.col[c].is_pred) continue;
-          const int64_t x = D.col[c].w == 8 ? ((const int64_t *)D.col[c].data)[i]
-                                            : (int64_t)((const int32_t *)D.col[c].data)[i];
-          ok[e] = (uint64_t)(x) - (uint64_t)(D.col[c].lo) <= D.col[c].span;
-        }
-      }
-      unsigned long long bb[4];
-      for (int e = 0; e < 4; e++) bb[e] = __ballot(ok[e]);
-      int64_t pos = prefix + __popcll(bb[0] & lt) + __popcll(bb[1] & lt) + __popcll(bb[2] & lt) + __popcll(bb[3] & lt);
-      for (int e = 0; e < 4; e++) {
-        if (!ok[e]) continue;
-        for (int k = 0; k < D.nout; k++) {
-          const int c = D.out_col[k];
-          if (D.col[c].w == 8) ((int64_t *)D.dst[k])[pos] = ((const int64_t *)D.col[c].data)[i0 + e];
-          else ((int32_t *)D.dst[k])[pos] = ((const int32_t *)D.col[c].data)[i0 + e];
-        }
-        pos++;
-      }
-      tcnt = __popcll(bb[0]) + __popcll(bb[1]) + __popcll(bb[2]) + __popcll(bb[3]);
-    }
-    if (lane == 0) *total = prefix + tcnt;
-  }
-}
-
-int SelectSteps(int ni) { return ni <= 2 ? 4 : ni <= 4 ? 2 : 1; }
-
-size_t SelectStatusBytes(int64_t nrows, int ni) {
-  const int64_t tile_steps = 4 * (int64_t)SelectSteps(ni);
-  const int64_t ntiles = ((nrows >> 8) + tile_steps - 1) / tile_steps;
-  return (size_t)(ntiles + 2) * 8;  // status words + the ticket
-}
-
-void SelectCompact(const SelectDesc &d, int64_t nrows, void *status_buf, int64_t *total, hipStream_t s) {
-  int ni = 0;
-  for (int c = 0; c < d.ncol; c++) {
-    if (d.col[c].w != 4 && d.col[c].w != 8) throw std::runtime_error("SelectCompact: columns must be 4 or 8 bytes");
-    ni += d.col[c].w / 4;
-  }
-  if (ni < 1 || ni > 8 || d.nout < 1 || d.nout > SL_MAX_OUT)
-    throw std::runtime_error("SelectCompact: unsupported shape");
-  const int S = SelectSteps(ni);
-  const int64_t tile_steps = 4 * (int64_t)S;
-  const int64_t ntiles = ((nrows >> 8) + tile_steps - 1) / tile_steps;
-  unsigned long long *status = (unsigned long long *)status_buf;
-  unsigned int *ticket = (unsigned int *)(status + ntiles + 1);
-  (void)hipMemsetAsync(status, 0, (size_t)(ntiles + 2) * 8, s);
-  int nbuf = 3;
-  if (const char *e = Knob("MBX_SL_NBUF")) nbuf = atoi(e) == 2 ? 2 : atoi(e) >= 4 ? 4 : 3;
-  int gpc = 1;
-  if (const char *e = Knob("MBX_SL_BLOCKS_PER_CU")) gpc = atoi(e) > 0 ? atoi(e) : 1;
-  int64_t grid = (int64_t)NumCUs() * gpc;
-  if (grid > ntiles) grid = ntiles > 0 ? ntiles : 1;
-  const size_t lds = (size_t)4 * nbuf * S * ni * 1024 + 4 * 2048;
-#define SL(NI_, S_, NB_)                                                                                       \
-  do {                                                                                                         \
-    static std::atomic<uint64_t> attr{0};                                                                      \
-    EnsureMaxLds((const void *)select_lds_kernel<NI_, S_, NB_>, attr, 160 * 1024 - 256);                      \
-    hipLaunchKernelGGL((select_lds_kernel<NI_, S_, NB_>), dim3((unsigned)grid), dim3(256), lds, s, d, nrows,  \
-                       ntiles, status, ticket, total);                                                         \
-  } while (0)
-#define SLN(NI_, S_)                   \
-  if (nbuf == 2) SL(NI_, S_, 2);       \
-  else if (nbuf == 4) SL(NI_, S_, 4);  \
-  else SL(NI_, S_, 3)
-  switch (ni) {
-    case 1: SLN(1, 4); break;
-    case 2: SLN(2, 4); break;
-    case 3: SLN(3, 2); break;
-    case 4: SLN(4, 2); break;
-    case 5: SLN(5, 1); break;
-    case 6: SLN(6, 1); break;
-    case 7: SLN(7, 1); break;
-    default: SLN(8, 1); break;
-  }
-#undef SLN
-#undef SL
-  (void)hipGetLastError();
-}
-
 
 // ---------------------------------------------------------------------------
 // Round-synchronous one-pass compaction (select_rounds; see device.h).
@@ -473,27 +172,25 @@ __device__ __forceinline__ unsigned long long lds_add_rtn(unsigned long long *p,
 // read back by this kernel; plain stores measured the same time and the same
 // WRITE_SIZE, profiles/r04_shapes_store_flavour_ab.log)
 template <typename T>
-__device__ __forceinline__ void sr_store(T v, T *p, bool) {
+__device__ __forceinline__ void sr_store(T v, T *p) {
   __builtin_nontemporal_store(v, p);
 }
 
 template <typename TS, typename TD>
-__device__ __forceinline__ void sr_copy(const TS *st, uint32_t t0w, uint32_t mask, uint32_t c, int lane, TD *dst,
-                                        int mode, int nt_off) {
-  const bool nt = !(nt_off & 1);
+__device__ __forceinline__ void sr_copy(const TS *st, uint32_t t0w, uint32_t mask, uint32_t c, int lane, TD *dst) {
   uint32_t i = lane;
   // whole 4-row groups only: with one 256-row step per round (8 loaders,
   // S = 1) a loader's range is ~130 rows, and guarded 4-row passes over such
   // ranges measured slower than the one-row loop (SELECT v ... WHERE xn > 24
   // 3.70 vs 3.57 ms, profiles/r04_storer_copy_ab.log)
-  for (; mode != 1 && i + 192 < c; i += 256) {
+  for (; i + 192 < c; i += 256) {
     TS x[4];
 #pragma unroll
     for (int u = 0; u < 4; u++) x[u] = st[(t0w + i + 64 * u) & mask];
 #pragma unroll
-    for (int u = 0; u < 4; u++) sr_store((TD)x[u], dst + i + 64 * u, nt);
+    for (int u = 0; u < 4; u++) sr_store((TD)x[u], dst + i + 64 * u);
   }
-  for (; i < c; i += 64) sr_store((TD)st[(t0w + i) & mask], dst + i, nt);
+  for (; i < c; i += 64) sr_store((TD)st[(t0w + i) & mask], dst + i);
 }
 
 // A storer's copy of a sentinel-staged NULL-able output (SelectDesc::col
@@ -501,20 +198,18 @@ __device__ __forceinline__ void sr_copy(const TS *st, uint32_t t0w, uint32_t mas
 // of the valid rows.
 template <typename TS, typename TD, bool Z>
 __device__ __forceinline__ void sr_copy_sent(const TS *st, uint32_t t0w, uint32_t mask, uint32_t c, int lane, TD *dst,
-                                             uint8_t *vd, TS sent, long long &mn, long long &mx, uint32_t &nv,
-                                             int mode, int nt_off) {
-  const bool ntv = !(nt_off & 1), ntb = !(nt_off & 2);
+                                             uint8_t *vd, TS sent, long long &mn, long long &mx, uint32_t &nv) {
   uint32_t b = 0;
   // whole passes of 256 rows, 4 per lane (rows b + lane + 64 u): the 4 staging
   // reads share one LDS wait.  The validity of the pass comes back as 4 ballots
   // (bit l of ballot u = row b + 64 u + l), from which lane l writes the bytes
   // of rows b + 4 l .. b + 4 l + 3 as one 4-byte store (nibble -> bytes by one
   // multiply), so a pass stores its 256 validity bytes with one instruction
-  // instead of four (mode 2: four byte stores, MBX_SR_COPY1=2).  The rows after
+  // instead of four (which measured the same).  The rows after
   // the last whole pass take the one-row loop: guarded partial passes measured
   // slower on ~130-row ranges (SELECT vn ... WHERE x > 24 4.81 vs 4.06 ms,
   // profiles/r04_storer_copy_ab.log)
-  for (; mode != 1 && b + 256 <= c; b += 256) {
+  for (; b + 256 <= c; b += 256) {
     TS x[4];
 #pragma unroll
     for (int u = 0; u < 4; u++) x[u] = st[(t0w + b + lane + 64 * u) & mask];
@@ -522,8 +217,7 @@ __device__ __forceinline__ void sr_copy_sent(const TS *st, uint32_t t0w, uint32_
 #pragma unroll
     for (int u = 0; u < 4; u++) {
       const bool ok = x[u] != sent;
-      sr_store((TD)(ok ? x[u] : (TS)0), dst + b + lane + 64 * u, ntv);
-      if (mode == 2) sr_store((uint8_t)ok, vd + b + lane + 64 * u, ntb);
+      sr_store((TD)(ok ? x[u] : (TS)0), dst + b + lane + 64 * u);
       bal[u] = __ballot(ok);
       if constexpr (Z) {
         mn = ok && (long long)x[u] < mn ? (long long)x[u] : mn;
@@ -531,22 +225,22 @@ __device__ __forceinline__ void sr_copy_sent(const TS *st, uint32_t t0w, uint32_
         nv += ok;
       }
     }
-    if (mode != 2) {
+    {
       // vd = D.vdst[o] + pos with pos any prefix count, so this dword store is
       // generally not 4-byte aligned: it relies on the unaligned global access
       // mode the ROCm runtime configures for gfx9 (SH_MEM_CONFIG alignment_mode
-      // UNALIGNED, ROCm's default); MBX_SR_COPY1=2 is the byte-store form
+      // UNALIGNED, ROCm's default)
       const int q = lane >> 4;
       const unsigned long long bw = q == 0 ? bal[0] : q == 1 ? bal[1] : q == 2 ? bal[2] : bal[3];
       const uint32_t nib = (uint32_t)(bw >> ((4 * lane) & 63)) & 0xFu;
-      sr_store((nib * 0x00204081u) & 0x01010101u, (uint32_t *)(vd + b + 4 * lane), ntb);
+      sr_store((nib * 0x00204081u) & 0x01010101u, (uint32_t *)(vd + b + 4 * lane));
     }
   }
   for (uint32_t i = b + lane; i < c; i += 64) {
     const TS x = st[(t0w + i) & mask];
     const bool ok = x != sent;
-    sr_store((TD)(ok ? x : (TS)0), dst + i, ntv);
-    sr_store((uint8_t)ok, vd + i, ntb);
+    sr_store((TD)(ok ? x : (TS)0), dst + i);
+    sr_store((uint8_t)ok, vd + i);
     if constexpr (Z) {
       mn = ok && (long long)x < mn ? (long long)x : mn;
       mx = ok && (long long)x > mx ? (long long)x : mx;
@@ -716,20 +410,8 @@ __global__ __launch_bounds__((NL + 5) * 64) void select_rounds_kernel(SelectDesc
                                                (void *)(vring + slot * VSB + h * NC * 32 + voff[c]), 16, 0, 2);
       }
     };
-    // ballot-mode validity (SelectDesc::vbo; 8 loaders, H = 1): every step
-    // stores its 8 ballot words (one instruction, counted in the waits below;
-    // a dead step's go to the dump slot past the live ones).  So that every
-    // wait counts the same instructions, the prologue puts one store of the
-    // dump slot in front of each slot after the first.
-    const int vbm = VAL && NL == 8 && H == 1 && D.vbo >= 0 ? 1 : 0;
-    const int vbc = vbm ? D.out_col[D.vbo] : -1;
-    const int64_t vdump = (nsteps + (n - nsteps * 256 + 255) / 256) * 8;
 #pragma unroll
-    for (int d = 0; d < DEPTH; d++) {
-      if (vbm && d > 0 && lane < 8) D.vball[vdump + lane] = 0ull;
-      asm volatile("" ::: "memory");  // (issue order is what the counted waits count)
-      issue(d);
-    }
+    for (int d = 0; d < DEPTH; d++) issue(d);
     int k = 0;
     uint32_t head = 0, tail_seen = 0;
     bool quit = false;
@@ -770,15 +452,11 @@ __global__ __launch_bounds__((NL + 5) * 64) void select_rounds_kernel(SelectDesc
       for (int s = 0; s < S; s++) {
         if (dbg) t0 = clock64();
         if constexpr (VAL) {
-          switch (nv + 4 * vbm) {  // wave-uniform: the exact count of the instructions issued after this slot's
+          switch (nv) {  // wave-uniform: the exact count of the instructions issued after this slot's
             case 1: sr_wait<(NI + H) * (DEPTH - 1)>(); break;
             case 2: sr_wait<(NI + 2 * H) * (DEPTH - 1)>(); break;
             case 3: sr_wait<(NI + 3 * H) * (DEPTH - 1)>(); break;
-            case 4: sr_wait<(NI + 4 * H) * (DEPTH - 1)>(); break;
-            case 5: sr_wait<(NI + H + 1) * (DEPTH - 1)>(); break;  // (+ the step's ballot store)
-            case 6: sr_wait<(NI + 2 * H + 1) * (DEPTH - 1)>(); break;
-            case 7: sr_wait<(NI + 3 * H + 1) * (DEPTH - 1)>(); break;
-            default: sr_wait<(NI + 4 * H + 1) * (DEPTH - 1)>(); break;
+            default: sr_wait<(NI + 4 * H) * (DEPTH - 1)>(); break;
           }
         } else {
           asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NI * (DEPTH - 1)) : "memory");
@@ -837,22 +515,6 @@ __global__ __launch_bounds__((NL + 5) * 64) void select_rounds_kernel(SelectDesc
             hc[h] += (uint32_t)__popcll(b[h][e]);
           }
           cnt += hc[h];
-        }
-        if constexpr (VAL && NL == 8 && H == 1) {
-          if (vbm) {  // the step's selection ballots and its selected-and-valid ballots of the output column
-            uint32_t vm = 0xFu;
-#pragma unroll
-            for (int c = 0; c < NC; c++)
-              if (c == vbc) vm = vmc[0][c];
-            unsigned long long vb[4];
-#pragma unroll
-            for (int e = 0; e < 4; e++) vb[e] = __ballot(ok[0][e] && ((vm >> e) & 1u));
-            const int le = lane & 3;
-            const unsigned long long wb = le == 0 ? b[0][0] : le == 1 ? b[0][1] : le == 2 ? b[0][2] : b[0][3];
-            const unsigned long long wv = le == 0 ? vb[0] : le == 1 ? vb[1] : le == 2 ? vb[2] : vb[3];
-            unsigned long long *vp = D.vball + (live ? 8 * (qb + s) : vdump);
-            if (lane < 8) vp[lane] = lane < 4 ? wb : wv;
-          }
         }
         if (cnt) {
           if (head + 256u * H - tail_seen > (uint32_t)stg) {  // staging full: wait for the storer
@@ -1020,7 +682,7 @@ __global__ __launch_bounds__((NL + 5) * 64) void select_rounds_kernel(SelectDesc
       if (dbg) t1 = clock64();
       int q = 0;
       // 8 loaders, one output without staged validity bytes: both loaders'
-      // ranges in one stream (sr_copy2; MBX_SR_COPY1 != 0 keeps the per-range copies)
+      // ranges in one stream (sr_copy2)
       bool merged = false;
       if constexpr (PER == 2) {
         const int oc = D.out_col[0];
@@ -1031,7 +693,7 @@ __global__ __launch_bounds__((NL + 5) * 64) void select_rounds_kernel(SelectDesc
         }
         // (sentinel-staged NULL-able outputs only: SELECT vn ... WHERE x > 24 3.91 -> 3.62 ms, but the
         // NULL-free SELECT v ... WHERE x > 24 3.27 -> 3.46, profiles/r04_storer_merged_ab.log)
-        if (D.nout == 1 && D.copy1 == 0 && vs && !vbyte && !((zsmask >> oc) & 1)) {
+        if (D.nout == 1 && vs && !vbyte && !((zsmask >> oc) & 1)) {
           merged = true;
           const int lA = sw, lB = sw + 4;
           int64_t pA = pos, pB;
@@ -1040,10 +702,6 @@ __global__ __launch_bounds__((NL + 5) * 64) void select_rounds_kernel(SelectDesc
           for (int qq = lA; qq < lB; qq++) pB += (uint32_t)__builtin_amdgcn_readlane((int)cl, qq);
           const uint32_t cA = (uint32_t)__builtin_amdgcn_readlane((int)cl, lA);
           const uint32_t cB = (uint32_t)__builtin_amdgcn_readlane((int)cl, lB);
-          if (VAL && NL == 8 && D.vball && lane == 0) {  // ballot mode: the ranges' first output rows
-            D.vpos[(r * G + g) * NL + lA] = pA;
-            D.vpos[(r * G + g) * NL + lB] = pB;
-          }
           int so = 0;
           bool s8 = false;
 #pragma unroll
@@ -1076,7 +734,6 @@ __global__ __launch_bounds__((NL + 5) * 64) void select_rounds_kernel(SelectDesc
         const int l = sw + 4 * j;
         for (; q < l; q++) pos += (uint32_t)__builtin_amdgcn_readlane((int)cl, q);
         const uint32_t c = (uint32_t)__builtin_amdgcn_readlane((int)cl, l);
-        if (VAL && NL == 8 && D.vball && lane == 0) D.vpos[(r * G + g) * NL + l] = pos;  // ballot mode: the range's first output row
         const unsigned char *mystage = stage0 + (size_t)l * (stg + 64) * rowb;
 #pragma unroll
         for (int o = 0; o < SL_MAX_OUT; o++) {
@@ -1099,16 +756,16 @@ __global__ __launch_bounds__((NL + 5) * 64) void select_rounds_kernel(SelectDesc
             uint8_t *vd = D.vdst[o] + pos;
             if (s8) {
               const int64_t *st = (const int64_t *)(mystage + so);
-              if (z) sr_copy_sent<int64_t, int64_t, true>(st, t0w, mask, c, lane, (int64_t *)D.dst[o] + pos, vd, D.col[oc].sent, zmn[o], zmx[o], zcnt[o], D.copy1, D.nt_off);
-              else sr_copy_sent<int64_t, int64_t, false>(st, t0w, mask, c, lane, (int64_t *)D.dst[o] + pos, vd, D.col[oc].sent, zmn[o], zmx[o], zcnt[o], D.copy1, D.nt_off);
+              if (z) sr_copy_sent<int64_t, int64_t, true>(st, t0w, mask, c, lane, (int64_t *)D.dst[o] + pos, vd, D.col[oc].sent, zmn[o], zmx[o], zcnt[o]);
+              else sr_copy_sent<int64_t, int64_t, false>(st, t0w, mask, c, lane, (int64_t *)D.dst[o] + pos, vd, D.col[oc].sent, zmn[o], zmx[o], zcnt[o]);
             } else if (D.col[oc].w == 8) {
               const int32_t *st = (const int32_t *)(mystage + so);
-              if (z) sr_copy_sent<int32_t, int64_t, true>(st, t0w, mask, c, lane, (int64_t *)D.dst[o] + pos, vd, (int32_t)D.col[oc].sent, zmn[o], zmx[o], zcnt[o], D.copy1, D.nt_off);
-              else sr_copy_sent<int32_t, int64_t, false>(st, t0w, mask, c, lane, (int64_t *)D.dst[o] + pos, vd, (int32_t)D.col[oc].sent, zmn[o], zmx[o], zcnt[o], D.copy1, D.nt_off);
+              if (z) sr_copy_sent<int32_t, int64_t, true>(st, t0w, mask, c, lane, (int64_t *)D.dst[o] + pos, vd, (int32_t)D.col[oc].sent, zmn[o], zmx[o], zcnt[o]);
+              else sr_copy_sent<int32_t, int64_t, false>(st, t0w, mask, c, lane, (int64_t *)D.dst[o] + pos, vd, (int32_t)D.col[oc].sent, zmn[o], zmx[o], zcnt[o]);
             } else {
               const int32_t *st = (const int32_t *)(mystage + so);
-              if (z) sr_copy_sent<int32_t, int32_t, true>(st, t0w, mask, c, lane, (int32_t *)D.dst[o] + pos, vd, (int32_t)D.col[oc].sent, zmn[o], zmx[o], zcnt[o], D.copy1, D.nt_off);
-              else sr_copy_sent<int32_t, int32_t, false>(st, t0w, mask, c, lane, (int32_t *)D.dst[o] + pos, vd, (int32_t)D.col[oc].sent, zmn[o], zmx[o], zcnt[o], D.copy1, D.nt_off);
+              if (z) sr_copy_sent<int32_t, int32_t, true>(st, t0w, mask, c, lane, (int32_t *)D.dst[o] + pos, vd, (int32_t)D.col[oc].sent, zmn[o], zmx[o], zcnt[o]);
+              else sr_copy_sent<int32_t, int32_t, false>(st, t0w, mask, c, lane, (int32_t *)D.dst[o] + pos, vd, (int32_t)D.col[oc].sent, zmn[o], zmx[o], zcnt[o]);
             }
           } else if ((zsmask >> oc) & 1) {  // the copy also folds the output's zone map (NULL rows skipped)
             long long mn = zmn[o], mx = zmx[o];
@@ -1141,16 +798,16 @@ __global__ __launch_bounds__((NL + 5) * 64) void select_rounds_kernel(SelectDesc
             }
             zmn[o] = mn, zmx[o] = mx, zcnt[o] += nv;
           } else if (s8) {
-            sr_copy<int64_t, int64_t>((const int64_t *)(mystage + so), t0w, mask, c, lane, (int64_t *)D.dst[o] + pos, D.copy1, D.nt_off);
+            sr_copy<int64_t, int64_t>((const int64_t *)(mystage + so), t0w, mask, c, lane, (int64_t *)D.dst[o] + pos);
           } else if (D.col[oc].w == 8) {  // staged narrow: sign-extend back to int64
-            sr_copy<int32_t, int64_t>((const int32_t *)(mystage + so), t0w, mask, c, lane, (int64_t *)D.dst[o] + pos, D.copy1, D.nt_off);
+            sr_copy<int32_t, int64_t>((const int32_t *)(mystage + so), t0w, mask, c, lane, (int64_t *)D.dst[o] + pos);
           } else {
-            sr_copy<int32_t, int32_t>((const int32_t *)(mystage + so), t0w, mask, c, lane, (int32_t *)D.dst[o] + pos, D.copy1, D.nt_off);
+            sr_copy<int32_t, int32_t>((const int32_t *)(mystage + so), t0w, mask, c, lane, (int32_t *)D.dst[o] + pos);
           }
           if constexpr (VAL) {
             if (vb) {
               uint8_t *vd = D.vdst[o] + pos;
-              for (uint32_t i = lane; i < c; i += 64) sr_store((uint8_t)vb[(t0w + i) & mask], vd + i, !(D.nt_off & 2));
+              for (uint32_t i = lane; i < c; i += 64) sr_store((uint8_t)vb[(t0w + i) & mask], vd + i);
             }
           }
         }
@@ -1296,10 +953,6 @@ __global__ __launch_bounds__((NL + 5) * 64) void select_rounds_kernel(SelectDesc
 #pragma unroll
   for (int c = 0; c < NC; c++) tmn[c] = LLONG_MAX, tmx[c] = LLONG_MIN, tnv[c] = 0;
   int64_t tcnt = 0;
-  // ballot mode: the tail's 256-row passes are sub-steps nsteps H, ... of the
-  // ballot array, all in one range after the last round's
-  const int tvb = VAL && NL == 8 && H == 1 && D.vbo >= 0 ? D.out_col[D.vbo] : -1;
-  if (tvb >= 0 && lane == 0) D.vpos[nrounds * G * NL] = running;
   for (int64_t base = nsteps * 256 * H; base < n; base += 256) {
     bool ok[4];
     const int64_t i0 = base + 4 * lane;
@@ -1318,25 +971,14 @@ __global__ __launch_bounds__((NL + 5) * 64) void select_rounds_kernel(SelectDesc
     unsigned long long bb[4];
 #pragma unroll
     for (int e = 0; e < 4; e++) bb[e] = __ballot(ok[e]);
-    if (tvb >= 0) {
-      unsigned long long vb[4];
-#pragma unroll
-      for (int e = 0; e < 4; e++)
-        vb[e] = __ballot(ok[e] && ((D.col[tvb].valid[(i0 + e) >> 6] >> ((i0 + e) & 63)) & 1));
-      const int le = lane & 3;
-      const unsigned long long wb = le == 0 ? bb[0] : le == 1 ? bb[1] : le == 2 ? bb[2] : bb[3];
-      const unsigned long long wv = le == 0 ? vb[0] : le == 1 ? vb[1] : le == 2 ? vb[2] : vb[3];
-      if (lane < 8) D.vball[8 * (base / 256) + lane] = lane < 4 ? wb : wv;
-    }
     int64_t pos = running + tcnt + __popcll(bb[0] & lt) + __popcll(bb[1] & lt) + __popcll(bb[2] & lt) +
                   __popcll(bb[3] & lt);
     for (int e = 0; e < 4; e++) {
       if (!ok[e]) continue;
       for (int o = 0; o < D.nout; o++) {
         const int c = D.out_col[o];
-        const bool zn = c == tvb && !((D.col[c].valid[(i0 + e) >> 6] >> ((i0 + e) & 63)) & 1);  // (0 under NULL)
-        if (D.col[c].w == 8) ((int64_t *)D.dst[o])[pos] = zn ? 0 : ((const int64_t *)D.col[c].data)[i0 + e];
-        else ((int32_t *)D.dst[o])[pos] = zn ? 0 : ((const int32_t *)D.col[c].data)[i0 + e];
+        if (D.col[c].w == 8) ((int64_t *)D.dst[o])[pos] = ((const int64_t *)D.col[c].data)[i0 + e];
+        else ((int32_t *)D.dst[o])[pos] = ((const int32_t *)D.col[c].data)[i0 + e];
         if (VAL && D.vdst[o]) D.vdst[o][pos] = (uint8_t)((D.col[c].valid[(i0 + e) >> 6] >> ((i0 + e) & 63)) & 1);
       }
       pos++;
@@ -1567,135 +1209,6 @@ void PackValidityBytes(const uint8_t *bytes, int64_t n, uint64_t *bits, hipStrea
   const int64_t words = (n + 63) / 64;
   hipLaunchKernelGGL(pack_validity_bytes_kernel, dim3((unsigned)((words * 4 + 255) / 256)), dim3(256), 0, s, bytes, n,
                      bits);
-}
-
-// Ballot-mode validity (SelectDesc::vbo): the output bitmap from the
-// per-step ballots and the per-range first output rows, in two kernels.
-//  * ballot_word_map, one thread per 256-row sub-step gs: its first output row
-//    p (the range's row + the selected rows of the range's earlier
-//    sub-steps) and its count c; for every output word w whose first row 64 w
-//    falls in [p, p + c) it records (gs, 64 w - p) -- each word is recorded by
-//    exactly one sub-step.  Sub-step order is output order (ranges in order,
-//    sub-steps within a range, then the tail), so a word's later rows are in
-//    gs + 1, gs + 2, ...
-//  * pack_validity_ballots, one thread per output word: from (gs, rank) it
-//    interleaves each sub-step's lane-major ballots into row order (bit l of
-//    word e = row 4 l + e; row-order word k = rows 64 k .. 64 k + 63) and
-//    compresses the validity bits of the selected rows (a 6-step software
-//    pext), until it has the word's 64 rows.  Every word is written once: no
-//    atomics, no shared partial words.  (A first form, one thread per word
-//    with a galloping search over the range rows and a bit-serial gather,
-//    took 1.02 ms at 1e9 rows: profiles/r04_vball_kernel_stats.csv.)
-__device__ __forceinline__ uint64_t pv_spread16(uint64_t x) {  // bit i -> bit 4 i (16 bits)
-  x &= 0xFFFFull;
-  x = (x | (x << 24)) & 0x000000FF000000FFull;
-  x = (x | (x << 12)) & 0x000F000F000F000Full;
-  x = (x | (x << 6)) & 0x0303030303030303ull;
-  x = (x | (x << 3)) & 0x1111111111111111ull;
-  return x;
-}
-__device__ __forceinline__ uint64_t pv_compress(uint64_t x, uint64_t m) {  // the bits of x at m's set bits, packed low
-  x &= m;
-  uint64_t mk = ~m << 1;
-#pragma unroll
-  for (int i = 0; i < 6; i++) {
-    uint64_t mp = mk ^ (mk << 1);
-    mp ^= mp << 2;
-    mp ^= mp << 4;
-    mp ^= mp << 8;
-    mp ^= mp << 16;
-    mp ^= mp << 32;
-    const uint64_t mv = mp & m;
-    m = (m ^ mv) | (mv >> (1 << i));
-    const uint64_t t = x & mv;
-    x = (x ^ t) | (t >> (1 << i));
-    mk &= ~mp;
-  }
-  return x;
-}
-struct PvDesc {
-  const unsigned long long *vball;
-  const int64_t *vpos;
-  int64_t *wmap;           // per output word: (gs << 8) | rank of its first row in gs
-  int64_t nranges;         // ranges of the rounds (the tail range is index nranges)
-  int64_t sub_per_range;   // S H
-  int64_t nsub_main;       // nsteps H: sub-steps of the rounds
-  int64_t nsub_tail;       // 256-row passes after them
-  int64_t n;               // selected rows
-};
-__device__ __forceinline__ int pv_count(const unsigned long long *bw) {
-  return __popcll(bw[0]) + __popcll(bw[1]) + __popcll(bw[2]) + __popcll(bw[3]);
-}
-__global__ __launch_bounds__(256) void ballot_word_map_kernel(PvDesc d) {
-  const int64_t gs = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (gs >= d.nsub_main + d.nsub_tail) return;
-  int64_t R, j0;
-  if (gs < d.nsub_main) R = gs / d.sub_per_range, j0 = R * d.sub_per_range;
-  else R = d.nranges, j0 = d.nsub_main;
-  int64_t p = d.vpos[R];
-  for (int64_t q = j0; q < gs; q++) p += pv_count(d.vball + 8 * q);
-  const int64_t c = pv_count(d.vball + 8 * gs);
-  for (int64_t w = (p + 63) >> 6; 64 * w < p + c; w++) d.wmap[w] = (gs << 8) | (64 * w - p);
-}
-__global__ __launch_bounds__(256) void pack_validity_ballots_kernel(PvDesc d, uint64_t *__restrict__ bits) {
-  const int64_t w = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  const int64_t target = w * 64;
-  if (target >= d.n) return;
-  const int64_t m = d.wmap[w];
-  int64_t gs = m >> 8;
-  int off = (int)(m & 255);
-  const int want = (int)(d.n - target < 64 ? d.n - target : 64);
-  const int64_t nsub = d.nsub_main + d.nsub_tail;
-  uint64_t out = 0;
-  int got = 0;
-  for (; got < want && gs < nsub; gs++, off = 0) {
-    const unsigned long long *bw = d.vball + 8 * gs;
-    const uint64_t s0 = bw[0], s1 = bw[1], s2 = bw[2], s3 = bw[3];
-    if (__popcll(s0) + __popcll(s1) + __popcll(s2) + __popcll(s3) <= off) continue;  // (only an empty sub-step)
-    const uint64_t v0 = bw[4], v1 = bw[5], v2 = bw[6], v3 = bw[7];
-    for (int k = 0; k < 4 && got < want; k++) {
-      const int sh = 16 * k;
-      const uint64_t sel = pv_spread16(s0 >> sh) | (pv_spread16(s1 >> sh) << 1) | (pv_spread16(s2 >> sh) << 2) |
-                           (pv_spread16(s3 >> sh) << 3);
-      const int c = __popcll(sel);
-      if (off >= c) {
-        off -= c;
-        continue;
-      }
-      const uint64_t val = pv_spread16(v0 >> sh) | (pv_spread16(v1 >> sh) << 1) | (pv_spread16(v2 >> sh) << 2) |
-                           (pv_spread16(v3 >> sh) << 3);
-      const uint64_t b = pv_compress(val, sel) >> off;
-      const int take = c - off < want - got ? c - off : want - got;
-      out |= (take >= 64 ? b : (b & ((1ull << take) - 1))) << got;
-      got += take;
-      off = 0;
-    }
-  }
-  bits[w] = out;
-}
-
-size_t SelectRangeCount(const SelectRoundsPlan &p) { return (size_t)p.nrounds * p.G * p.NL; }
-size_t SelectBallotWords(const SelectRoundsPlan &p, int64_t nrows) {
-  const int64_t nsteps = nrows / (256 * p.H);
-  return (size_t)(nsteps * p.H + (nrows - nsteps * 256 * p.H + 255) / 256) * 8 + 8;  // + the dump slot
-}
-
-void PackValidityBallots(const unsigned long long *vball, const int64_t *vpos, const SelectRoundsPlan &p,
-                         int64_t nrows, int64_t n, uint64_t *bits, int64_t *wmap, hipStream_t s) {
-  if (n <= 0) return;
-  PvDesc d;
-  const int64_t nsteps = nrows / (256 * p.H);
-  d.vball = vball;
-  d.vpos = vpos;
-  d.wmap = wmap;
-  d.nranges = (int64_t)SelectRangeCount(p);
-  d.sub_per_range = (int64_t)p.S * p.H;
-  d.nsub_main = nsteps * p.H;
-  d.nsub_tail = (nrows - nsteps * 256 * p.H + 255) / 256;
-  d.n = n;
-  const int64_t nsub = d.nsub_main + d.nsub_tail, words = (n + 63) / 64;
-  hipLaunchKernelGGL(ballot_word_map_kernel, dim3((unsigned)((nsub + 255) / 256)), dim3(256), 0, s, d);
-  hipLaunchKernelGGL(pack_validity_ballots_kernel, dim3((unsigned)((words + 255) / 256)), dim3(256), 0, s, d, bits);
 }
 
 hipError_t SelectRounds(const SelectDesc &d, const SelectRoundsPlan &p, int64_t nrows, unsigned long long *ctl,

@@ -4,8 +4,7 @@ MBX_SR_MIN_ROWS rows, forced at every size with MBX_SR_MIN_ROWS=0), the
 count-first two-pass form (dev::FilterCountChunks + scan +
 dev::CompactRecompute, when every predicate column is an output; MBX_SL=0),
 the ballot-bits two-pass form (dev::FilterBits + scan + dev::CompactColumns;
-MBX_SL=0 MBX_CC=0), the one-pass look-back kernel (dev::SelectCompact;
-MBX_SL=2) and the VM path (MBX_FC=0) must all give the selected rows of every
+MBX_SL=0 MBX_CC=0) and the VM path (MBX_FC=0) must all give the selected rows of every
 output column, in row order, bit for bit.  Sizes straddle the 256-row step,
 the one-pass tiles (4 S steps per workgroup and round) and the grid-stride
 (partial last step, one-row tail, many rounds per workgroup)."""
@@ -54,7 +53,7 @@ def test_filter_compact_parity(conn, oracle, monkeypatch, n):
             got = _col(conn, sql, kind, i)
             assert np.array_equal(got, arr[m].astype(got.dtype)), (n, sql, i)
         # every other form: the same rows
-        for envs in ({"MBX_SR_MIN_ROWS": "0"}, {"MBX_SL": "0"}, {"MBX_SL": "0", "MBX_CC": "0"}, {"MBX_SL": "2"},
+        for envs in ({"MBX_SR_MIN_ROWS": "0"}, {"MBX_SL": "0"}, {"MBX_SL": "0", "MBX_CC": "0"},
                      {"MBX_FC": "0"}):
             for env, val in envs.items():
                 monkeypatch.setenv(env, val)
@@ -112,41 +111,6 @@ def test_filter_compact_runs_the_hip_passes(mbx, oracle, monkeypatch):
         names = [kk["name"] for kk in c.last_profile()["kernels"]]
         assert "select_rounds" in names and "filter_bits" not in names and "filter_count" not in names, names
         assert np.array_equal(got, col[m])
-    monkeypatch.setenv("MBX_SL", "2")
-    got = _col(c, "SELECT v, k FROM fc WHERE x > 24 AND k < 16", "int64")
-    names = [kk["name"] for kk in c.last_profile()["kernels"]]
-    assert "select" in names and "filter_bits" not in names, names  # one pass, look-back (opt-in)
-    assert np.array_equal(got, v[(x > 24) & (k < 16)])
-    c.close()
-
-
-@pytest.mark.parametrize("nbuf,gpc", [(2, 1), (3, 1), (4, 1), (2, 2), (3, 4)])
-def test_select_one_pass_launch_shapes(mbx, oracle, monkeypatch, nbuf, gpc):
-    """Every ring depth / workgroups-per-CU shape of the one-pass kernel over
-    many tiles per workgroup (ticket reuse, look-back windows longer than 64
-    tiles) and the 1..4-column loaded sets (NI 1..8): exact rows in order."""
-    monkeypatch.setenv("MBX_SL", "2")
-    monkeypatch.setenv("MBX_SL_NBUF", str(nbuf))
-    monkeypatch.setenv("MBX_SL_BLOCKS_PER_CU", str(gpc))
-    cfg = mbx.Config.create()
-    cfg.set("mbx_profile", "true")
-    c = mbx.connect_with_config(cfg).value
-    n = 20_000_077
-    x, k, v, s = _table(c, oracle, n)
-    cases = [
-        ("SELECT k FROM fc WHERE k < 5", k < 5, [("int32", k)]),
-        ("SELECT x FROM fc WHERE x > 24", x > 24, [("int64", x)]),
-        ("SELECT x, k FROM fc WHERE x > 24 AND k <= 16", (x > 24) & (k <= 16), [("int64", x), ("int32", k)]),
-        ("SELECT v, x, k FROM fc WHERE v > 0 AND x < 30", (v > 0) & (x < 30),
-         [("int64", v), ("int64", x), ("int32", k)]),
-        ("SELECT k, v FROM fc WHERE x BETWEEN 10 AND 40 AND k >= 3 AND v > 0",
-         (x >= 10) & (x <= 40) & (k >= 3) & (v > 0), [("int32", k), ("int64", v)]),
-    ]
-    for sql, m, cols in cases:
-        for i, (kind, arr) in enumerate(cols):
-            got = _col(c, sql, kind, i)
-            assert "select" in [kk["name"] for kk in c.last_profile()["kernels"]], sql
-            assert np.array_equal(got, arr[m].astype(got.dtype)), (sql, i)
     c.close()
 
 

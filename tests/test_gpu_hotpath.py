@@ -258,17 +258,13 @@ def test_filter_agg_variants_parity(conn, oracle, monkeypatch, variant):
 
 
 # ---- every fused GROUP BY launch shape gives the same bits ------------------
-# "+p0"/"+p1": separate COUNT atomics (the default) / packed counts;
-# "+f<k>": packed-count drains every k wave steps
-GD_VARIANTS = ["", "seg", "d2_g1", "d3_g2", "d4_g2", "+p0", "+p1", "d2_g1+p1+f1", "d3_g2+p1+f2"]
+GD_VARIANTS = ["", "seg", "d2_g1", "d3_g2", "d4_g2", "d6_g1", "d8_g1"]
 
 
 @pytest.mark.parametrize("variant", GD_VARIANTS)
 def test_group_direct_variants_parity(conn, oracle, monkeypatch, variant):
     base, *opts = variant.split("+")
     monkeypatch.setenv("MBX_GD_VARIANT", base)
-    for o in opts:
-        monkeypatch.setenv({"p": "MBX_GD_PACK", "f": "MBX_GD_PKF"}[o[0]], o[1:])
     for n in (1, 255, 256, 257, 1023, 70_001, 1_000_003):
         k = oracle.synth_i64(n, 7, 0, 40, -20)           # keys -20..19
         v = oracle.synth_i64(n, 9, 0, 2**40, -2**39)
@@ -737,18 +733,14 @@ def test_hbm_calibrate_reports_every_shape(mbx):
     c.close()
 
 
-@pytest.mark.parametrize("pack", ["0", "1"])
 @pytest.mark.parametrize("n", [1, 257, 100_003, 1_000_003])
-def test_group_direct_nullable_value(mbx, oracle, monkeypatch, n, pack):
+def test_group_direct_nullable_value(mbx, oracle, monkeypatch, n):
     """F2's group_direct_lds with a NULL-able value column (VV: validity words
     in the ring, COUNT(*) apart from the value's count): COUNT(*), COUNT(vn),
     SUM, MIN, MAX, AVG per key, a key whose values are all NULL (SUM / MIN /
     MAX / AVG NULL, COUNT(vn) 0), with and without a fused WHERE, exact vs
-    numpy and equal to the generic path (MBX_GD_NULLS=0); plain valid-row
-    counts (the default) and packed counts with drains forced often."""
+    numpy and equal to the generic path (MBX_GD_NULLS=0)."""
     import numpy as np
-    monkeypatch.setenv("MBX_GD_PACK", pack)
-    monkeypatch.setenv("MBX_GD_PKF", "16")
     cfg = mbx.Config.create()
     cfg.set("mbx_profile", "true")
     c = mbx.connect_with_config(cfg).value

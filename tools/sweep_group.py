@@ -2,8 +2,8 @@
 """A/B sweep of the fused GROUP BY (group_direct) launch variants on the C3
 table in ONE process: interleaved rounds, median/min kernel time.  GPU only.
 Variants: MBX_GD_VARIANT = "d<depth>_g<blocks per CU>" (LDS-DMA) or "seg",
-with options "+r<replicas>", "+p0" (separate COUNT atomics instead of packed)
-"+f<n>" (drain the packed counts at least every n steps), "+h2" (two 256-row sub-steps per wave step) and "+x1" (XCD-grouped step
+with options "+r<replicas>",
+"+h2" (two 256-row sub-steps per wave step) and "+x1" (XCD-grouped step
 windows)."""
 import json
 import os
@@ -34,21 +34,15 @@ for name, sql in sqls.items():
         for v in (variants if rnd % 2 == 0 else variants[::-1]):
             os.environ["MBX_GD_VARIANT"] = v.split("+")[0]
             os.environ.pop("MBX_GD_R", None)
-            os.environ.pop("MBX_GD_PACK", None)
             os.environ.pop("MBX_GD_H", None)
             os.environ.pop("MBX_GD_XCD", None)
-            os.environ.pop("MBX_GD_PKF", None)
             for opt in v.split("+")[1:]:
                 if opt.startswith("h"):
                     os.environ["MBX_GD_H"] = opt[1:]  # h2: two 256-row sub-steps per wave step
-                if opt.startswith("f"):
-                    os.environ["MBX_GD_PKF"] = opt[1:]  # f<n>: packed-count drain every n wave steps (at most)
                 if opt.startswith("x"):
                     os.environ["MBX_GD_XCD"] = opt[1:]  # x1: XCD-grouped step windows
                 if opt.startswith("r"):
                     os.environ["MBX_GD_R"] = opt[1:]
-                elif opt.startswith("p"):
-                    os.environ["MBX_GD_PACK"] = opt[1:]  # p0: unpacked count atomics
             r = c.query(sql)
             assert isinstance(r, m.Ok), r
             rows = sorted(r.value.rows)
