@@ -81,6 +81,8 @@ _sig("duckdb_mbx_append_commit", _I, _P, _L)
 _sig("duckdb_mbx_hbm_calibrate", _I, _P, _L, _I, ctypes.POINTER(ctypes.c_double))
 _sig("duckdb_mbx_hbm_calibrate_ex", _I, _P, _L, _I, ctypes.POINTER(ctypes.c_double), _I)
 _sig("duckdb_mbx_clock_stamps", _I, _P, ctypes.POINTER(ctypes.c_uint64), _I)
+_sig("duckdb_mbx_set_link_mode", _I, _I)
+_sig("duckdb_mbx_link_stats", ctypes.c_void_p)
 _sig("duckdb_mbx_statement_plan_stats", _I, _P, ctypes.POINTER(ctypes.c_int64))
 _sig("duckdb_mbx_shard_stats", _I, _P, ctypes.POINTER(ctypes.c_int64), ctypes.POINTER(ctypes.c_double))
 _sig("duckdb_mbx_engine_stats", _I, _P, ctypes.POINTER(ctypes.c_int64))
@@ -713,6 +715,23 @@ class RawResult:
         buf = ctypes.create_string_buffer(16)
         n = lib.duckdb_mbx_result_raw(self._h, c, r, buf, 16)
         return buf.raw[:n]
+
+
+def set_link_mode(mode: int) -> None:
+    """Arrow getter copies of 2-32 MiB, process-wide (extension): -1 the measured
+    choice (default), 0 the runtime's copy, 1 a registered destination, 2 the
+    pinned bounce."""
+    lib.duckdb_mbx_set_link_mode(mode)
+
+
+def link_stats() -> list:
+    """Per device and size class of the 2-32 MiB getter copies: each method's
+    trial medians (GB/s), the method kept, the calls served (extension)."""
+    import json
+    p = lib.duckdb_mbx_link_stats()
+    s = ctypes.string_at(p).decode()
+    lib.duckdb_mbx_free(p)
+    return json.loads(s)
 
 
 def connect(on_ready: Callable = None, path: str = ":memory:"):

@@ -382,6 +382,7 @@ struct SelectDesc {
 struct SelectRoundsPlan {
   bool ok;
   int nc, wm, ni, depth, S, H, NL, stg, G, sleep, test_stall, pw;  // wm: bit c = column c is 8 bytes; H: 256-row sub-steps per step
+  int NS;  // storer waves (4; 6 with 6 loaders)
   int nv;  // loaded columns with validity words (their 32 B per step ride a second ring)
   int64_t nrounds;
   size_t lds;

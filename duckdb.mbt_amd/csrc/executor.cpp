@@ -1233,7 +1233,7 @@ static bool TrySelectOnePass(Engine &e, const DRel &rel, const dev::FilterMultiD
       unsigned long long h[14];
       HIPCHK(hipMemcpyAsync(h, dbgbuf->p, sizeof(h), hipMemcpyDeviceToHost, e.stream));
       HIPCHK(hipStreamSynchronize(e.stream));
-      const double L = (double)plan.G * plan.NL, Ls = (double)plan.G * 4, C = (double)plan.G;
+      const double L = (double)plan.G * plan.NL, Ls = (double)plan.G * plan.NS, C = (double)plan.G;
       fprintf(stderr, "[select_rounds] G %d rounds %lld S %d stg %d depth %d | per loader: cycles %.0f dma_wait %.0f "
               "staging_wait %.0f meta_wait %.0f | per storer: cycles %.0f base_wait %.0f copy %.0f | per coordinator: cycles %.0f "
               "polls %.1f no_progress %.1f poll_load_cycles %.0f (%.0f per poll) rounds %.1f max/poll %llu "

@@ -213,7 +213,9 @@ void AdviseHuge(void *p, size_t n) {
 // calls run each method for a block of kBlock calls, timed end to end (a
 // block's first call, which pays the method's setup and cold pages, is not
 // counted), and the class then keeps the method with the best median.  The bytes are the same whichever method runs.
-// MBX_LINK_MID=0 keeps the runtime's copy; MBX_LINK_MID_MODE=0|1|2 pins one.
+// MBX_LINK_MID=0 keeps the runtime's copy; MBX_LINK_MID_MODE=0|1|2 (or
+// duckdb_mbx_set_link_mode) pins one.  The mid path is part of the host copy
+// machinery, so MBX_LINK_THREADS=0 turns it off too.
 enum MidMethod { M_RUNTIME = 0, M_REGISTER = 1, M_BOUNCE = 2, M_COUNT = 3 };
 
 class SpinTeam {  // T-1 helper threads + the caller; helpers spin kSpinUs after a job, then sleep
@@ -267,6 +269,35 @@ class SpinTeam {  // T-1 helper threads + the caller; helpers spin kSpinUs after
 class MidLink {
  public:
   MidLink() {}
+
+  // {"class_mib": [lo, hi], "calls": c, "kept": method, "trial_median_gbs": {...}} per class with calls
+  std::string StatsJson() {
+    std::lock_guard<std::mutex> call(mu_);
+    static const char *names[M_COUNT] = {"runtime", "register", "bounce"};
+    std::string j = "[";
+    for (int c = 0; c < kClasses; c++) {
+      Class &C = cls_[c];
+      if (!C.calls) continue;
+      if (j.size() > 1) j += ",";
+      j += "{\"class_mib\":[" + std::to_string(2 << c) + "," + std::to_string(4 << c) + "],\"calls\":" +
+           std::to_string(C.calls) + ",\"kept\":\"" + (C.best >= 0 ? names[C.best] : "runtime (no trial yet)") +
+           "\",\"trial_median_gbs\":{";
+      bool first = true;
+      for (int m = 0; m < M_COUNT; m++) {
+        if (C.gbs[m].empty() && !C.broken[m]) continue;
+        std::vector<double> v = C.gbs[m];
+        double med = 0;
+        if (!v.empty()) {
+          std::nth_element(v.begin(), v.begin() + v.size() / 2, v.end());
+          med = v[v.size() / 2] / 1e3;  // MB/s -> GB/s
+        }
+        j += std::string(first ? "" : ",") + "\"" + names[m] + "\":" + (C.broken[m] ? "\"refused\"" : std::to_string(med));
+        first = false;
+      }
+      j += "}}";
+    }
+    return j + "]";
+  }
 
   std::string Copy(void *dst, const void *src, size_t n, int forced) {
     std::lock_guard<std::mutex> call(mu_);
@@ -384,15 +415,36 @@ MidLink *Mid(int device) {
 
 }  // namespace
 
+static std::atomic<int> g_link_mode{-1};
+
+void SetLinkMode(int mode) { g_link_mode.store(mode >= 0 && mode < M_COUNT ? mode : -1); }
+
+std::string LinkStatsJson() {
+  std::string j = "[";
+  for (int d = 0; d < 64; d++) {
+    MidLink *m = nullptr;
+    {
+      std::lock_guard<std::mutex> lk(g_pools_mu);
+      m = g_mid[d];
+    }
+    if (!m) continue;
+    if (j.size() > 1) j += ",";
+    j += "{\"device\":" + std::to_string(d) + ",\"mode\":" + std::to_string(g_link_mode.load()) +
+         ",\"classes\":" + m->StatsJson() + "}";
+  }
+  return j + "]";
+}
+
 std::string LinkD2H(int device, void *dst, const void *src, size_t n) {
   // read per call (tests flip them); a device's pool keeps its first thread count
   const int threads = std::min(64, std::max(0, EnvInt("MBX_LINK_THREADS", 8)));
   const long min_bytes = std::max(1, EnvInt("MBX_LINK_MIN", kFreshBytes));
   const bool huge = EnvInt("MBX_LINK_HUGE", 1) != 0;
   if (n == 0) return "";
-  if ((long)n < min_bytes && n >= (size_t)2 << 20 && EnvInt("MBX_LINK_MID", 1) != 0) {
+  if (threads > 0 && (long)n < min_bytes && n >= (size_t)2 << 20 && EnvInt("MBX_LINK_MID", 1) != 0) {
     MidLink *mid = Mid(device);
-    if (mid) return mid->Copy(dst, src, n, EnvInt("MBX_LINK_MID_MODE", -1));
+    const int mode = g_link_mode.load();
+    if (mid) return mid->Copy(dst, src, n, mode >= 0 ? mode : EnvInt("MBX_LINK_MID_MODE", -1));
   }
   LinkPool *pool = threads > 0 && (long)n >= min_bytes ? Pool(device, threads) : nullptr;
   if (!pool) {

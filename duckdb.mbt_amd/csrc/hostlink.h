@@ -13,4 +13,12 @@ namespace mbx {
 // Returns "" or the HIP error text.
 std::string LinkD2H(int device, void *dst, const void *src, size_t n);
 
+// The mid-size (2-32 MiB) copy method for every device from now on: -1 the
+// measured choice (default), 0 the runtime's copy, 1 a registered
+// destination, 2 the pinned bounce (duckdb_mbx_set_link_mode; A/B legs).
+void SetLinkMode(int mode);
+// Per device and size class: each method's trial medians (GB/s), the method
+// kept, and the calls served -- JSON text.
+std::string LinkStatsJson();
+
 }  // namespace mbx

@@ -116,7 +116,7 @@ struct SrShared {
   long long base[SR_MR];          // output row of the workgroup's tile of the round
   uint32_t btag[SR_MR];           // round + 1 once base is set
   uint32_t tail[8];               // staging rows freed, per loader (monotonic)
-  uint32_t sdone[4];              // rounds finished, per storer
+  uint32_t sdone[8];              // rounds finished, per storer
   uint32_t abort_;
   unsigned long long pubt[SR_MR];  // MBX_SR_DEBUG: clock64 when the round's granule was published
 };
@@ -310,8 +310,8 @@ struct SrCols {
 // the staged bytes; bits ORed into an LDS ring by the loaders) measured 5.5-6.5
 // ms against 4.25 + 0.14-0.22 ms for this form on `SELECT vn ... WHERE x > 24`
 // at 1e9 rows: the storers of this shape are nearly as busy as the loaders.
-template <int NC, int WM, int DEPTH, int H, int NL, bool VAL>
-__global__ __launch_bounds__((NL + 5) * 64) void select_rounds_kernel(SelectDesc D, int64_t n, int64_t nrounds, int S, int stg,
+template <int NC, int WM, int DEPTH, int H, int NL, bool VAL, int NS = 4>
+__global__ __launch_bounds__((NL + NS + 1) * 64) void select_rounds_kernel(SelectDesc D, int64_t n, int64_t nrounds, int S, int stg,
                                                             unsigned long long *ctl, uint32_t epoch, int sleep_,
                                                             int test_stall, int pwmax) {
   typedef SrCols<NC, WM> L;
@@ -437,9 +437,8 @@ __global__ __launch_bounds__((NL + 5) * 64) void select_rounds_kernel(SelectDesc
         if (dbg) t0 = clock64();
         while (true) {
           uint32_t m = lds_ld(&sm.sdone[0]);
-          m = min(m, lds_ld(&sm.sdone[1]));
-          m = min(m, lds_ld(&sm.sdone[2]));
-          m = min(m, lds_ld(&sm.sdone[3]));
+#pragma unroll
+          for (int q = 1; q < NS; q++) m = min(m, lds_ld(&sm.sdone[q]));
           if (__builtin_amdgcn_readfirstlane(m) >= need) break;
           if (lds_ld(&sm.abort_)) { quit = true; break; }
           __builtin_amdgcn_s_sleep(1);
@@ -641,10 +640,10 @@ __global__ __launch_bounds__((NL + 5) * 64) void select_rounds_kernel(SelectDesc
     }
     return;
   }
-  if (w < NL + 4) {
+  if (w < NL + NS) {
     // ------------------------------------------------------------ storer
     const int sw = w - NL;
-    constexpr int PER = NL / 4;  // loaders per storer: sw, sw + 4, ...
+    constexpr int PER = NL / NS;  // loaders per storer: sw, sw + NS, ...
     uint32_t tail[PER];
 #pragma unroll
     for (int j = 0; j < PER; j++) tail[j] = 0;
@@ -659,6 +658,7 @@ __global__ __launch_bounds__((NL + 5) * 64) void select_rounds_kernel(SelectDesc
     // compiled -- its registers pushed the NULL-able 8-loader instances past
     // 128 VGPRs into scratch)
     const uint32_t zsmask = NL == 4 && D.zstats && D.zstore ? (uint32_t)D.zmask & smask : 0u;
+    static_assert(NL % NS == 0, "every storer drains the same number of loaders");
     long long zmn[SL_MAX_OUT], zmx[SL_MAX_OUT];
     uint32_t zcnt[SL_MAX_OUT];
 #pragma unroll
@@ -695,7 +695,7 @@ __global__ __launch_bounds__((NL + 5) * 64) void select_rounds_kernel(SelectDesc
         // NULL-free SELECT v ... WHERE x > 24 3.27 -> 3.46, profiles/r04_storer_merged_ab.log)
         if (D.nout == 1 && vs && !vbyte && !((zsmask >> oc) & 1)) {
           merged = true;
-          const int lA = sw, lB = sw + 4;
+          const int lA = sw, lB = sw + NS;
           int64_t pA = pos, pB;
           for (int qq = 0; qq < lA; qq++) pA += (uint32_t)__builtin_amdgcn_readlane((int)cl, qq);
           pB = pA;
@@ -731,7 +731,7 @@ __global__ __launch_bounds__((NL + 5) * 64) void select_rounds_kernel(SelectDesc
       }
 #pragma unroll
       for (int j = 0; j < PER && !merged; j++) {
-        const int l = sw + 4 * j;
+        const int l = sw + NS * j;
         for (; q < l; q++) pos += (uint32_t)__builtin_amdgcn_readlane((int)cl, q);
         const uint32_t c = (uint32_t)__builtin_amdgcn_readlane((int)cl, l);
         const unsigned char *mystage = stage0 + (size_t)l * (stg + 64) * rowb;
@@ -1068,6 +1068,7 @@ static SelectRoundsPlan PlanSelectRoundsNL(const SelectDesc &d, int64_t nrows, i
   p.NL = (p.nc == 1 && rowb <= 4 + p.nv * SR_VB) || (p.nc == 2 && !vout) ? 8 : 4;
   if (const char *e = Knob("MBX_SR_NL")) p.NL = atoi(e) == 8 && p.nc <= 2 ? 8 : 4;
   if (force_nl) p.NL = force_nl;
+  p.NS = 4;  // storer waves (every instance has 4; the kernel takes NS as a parameter)
   if (p.NL == 8) want_h = 1, want_depth = p.nc == 1 || p.ni <= 2 ? 3 : 2;  // (the depths SrDepth instantiates)
   if (const char *e = Knob("MBX_SR_H")) want_h = atoi(e) == 1 ? 1 : 2;
   if (p.nv && p.NL == 8) want_h = 1;  // the 8-loader NULL-able form is H = 1 only
@@ -1121,15 +1122,17 @@ static SelectRoundsPlan PlanSelectRoundsNL(const SelectDesc &d, int64_t nrows, i
 size_t SelectRoundsCtlBytes(const SelectRoundsPlan &p) { return (size_t)(8 + p.nrounds * p.G) * 8; }
 
 namespace {
-template <int NC, int WM, int DP, int H, int NL, bool VAL = false>
+template <int NC, int WM, int DP, int H, int NL, bool VAL = false, int NS = 4>
 void SrLaunchNL(const SelectDesc &d, const SelectRoundsPlan &p, int64_t nrows, unsigned long long *ctl, uint32_t epoch,
                 hipStream_t s) {
   // the plan's layout must be this instance's: a mismatch (a planner rule
   // without a matching instance) would place rows wrongly, so it never launches
-  if (p.NL != NL || p.H != H || p.depth != DP) throw std::logic_error("select_rounds: plan has no matching kernel");
+  if (p.NL != NL || p.NS != NS || p.H != H || p.depth != DP)
+    throw std::logic_error("select_rounds: plan has no matching kernel");
   static std::atomic<uint64_t> attr{0};
-  EnsureMaxLds((const void *)select_rounds_kernel<NC, WM, DP, H, NL, VAL>, attr, 160 * 1024 - 2048);
-  hipLaunchKernelGGL((select_rounds_kernel<NC, WM, DP, H, NL, VAL>), dim3((unsigned)p.G), dim3((NL + 5) * 64), p.lds, s,
+  EnsureMaxLds((const void *)select_rounds_kernel<NC, WM, DP, H, NL, VAL, NS>, attr, 160 * 1024 - 2048);
+  hipLaunchKernelGGL((select_rounds_kernel<NC, WM, DP, H, NL, VAL, NS>), dim3((unsigned)p.G), dim3((NL + NS + 1) * 64),
+                     p.lds, s,
                      d, nrows, p.nrounds, p.S, p.stg, ctl, epoch, p.sleep, p.test_stall, p.pw);
 }
 template <int NC, int WM, int DP, int H>
@@ -1150,6 +1153,10 @@ void SrDepth(const SelectDesc &d, const SelectRoundsPlan &p, int64_t nrows, unsi
     }
     if constexpr (NC == 2) {  // two columns: 8 loaders with H = 1 (the planner's ring depth for ni)
       if (p.NL == 8) return SrLaunchNL<NC, WM, (ni <= 2 ? 3 : 2), 1, 8, true>(d, p, nrows, ctl, epoch, s);
+      // (6 loaders + 6 storers, one loader range per storer, measured no better
+      // for SELECT vn ... WHERE x > 24 -- 3.57-3.61 vs 3.61-3.65 ms -- and
+      // slower for SELECT v ... WHERE xn > 24, 3.49-3.51 vs 3.31-3.40 ms:
+      // profiles/r05_seln_ab/; the instance was removed, NS stays a parameter)
     }
     if (p.H == 2) return SrLaunchNL<NC, WM, 2, 2, 4, true>(d, p, nrows, ctl, epoch, s);
     if (ni <= 2) return SrLaunchNL<NC, WM, 3, 1, 4, true>(d, p, nrows, ctl, epoch, s);

@@ -26,6 +26,7 @@
 #include "engine.h"
 #include "jit.h"
 #include "knobs.h"
+#include "hostlink.h"
 
 using namespace mbx;
 
@@ -1594,6 +1595,19 @@ int32_t duckdb_mbx_hbm_calibrate_ex(duckdb_mb_connection *h, int64_t bytes, int3
     return 0;
   }
 }
+// Arrow getter copies of 2-32 MiB (an 8 MB 1e6-row INT64 slice is one): the
+// method from now on, process-wide -- -1 the measured choice (default), 0 the
+// runtime's copy, 1 a registered destination, 2 the pinned bounce.  Returns 1.
+int32_t duckdb_mbx_set_link_mode(int32_t mode) {
+  mbx::SetLinkMode(mode);
+  return 1;
+}
+
+// Per device and power-of-two size class of those copies: each method's trial
+// medians (GB/s), the method kept and the calls served, as JSON (malloc'd;
+// free with duckdb_mbx_free).
+char *duckdb_mbx_link_stats(void) { return strdup(mbx::LinkStatsJson().c_str()); }
+
 // In-kernel clock stamps of the last filter_agg_lds / group_direct_lds /
 // two-array ring launch: {memtime, realtime} at the start and the end of each
 // of the first cap workgroups' main loop (libduckdb_mb_amd_clk.so, `make

@@ -221,6 +221,16 @@ int32_t duckdb_mbx_hbm_calibrate(duckdb_mb_connection *handle, int64_t bytes, in
  * were written (<= nout), 0 on error */
 int32_t duckdb_mbx_hbm_calibrate_ex(duckdb_mb_connection *handle, int64_t bytes, int32_t iters, double *out,
                                     int32_t nout);
+/* Arrow getter copies of 2-32 MiB (ref src/duckdb_native.c:2392-2422 fills
+ * an 8 MB Bytes per 1e6-row INT64 slice): by default, per device and size
+ * class, the first calls try the runtime's copy, a registered destination
+ * and a pinned bounce (5 calls each) and the class keeps the fastest median.
+ * duckdb_mbx_set_link_mode pins one method process-wide from now on (-1 the
+ * measured choice, 0 runtime, 1 register, 2 bounce; returns 1);
+ * duckdb_mbx_link_stats reports each class's trial medians (GB/s), the method
+ * kept and the calls served, as JSON (free with duckdb_mbx_free). */
+int32_t duckdb_mbx_set_link_mode(int32_t mode);
+char *duckdb_mbx_link_stats(void);
 /* Diagnostic build only (`make -C duckdb.mbt_amd clockdiag` ->
  * libduckdb_mb_amd_clk.so): the in-kernel clock stamps of the last
  * filter_agg_lds / group_direct_lds / two-array ring launch, 4 values per

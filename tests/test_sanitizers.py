@@ -30,8 +30,9 @@ MALFORMED = [
 
 
 def _ensure_asan():
-    if not os.path.exists(ASAN_LIB):
-        subprocess.run(["make", "-s", "-j8", "-C", LIBDIR, "asan"], check=True, capture_output=True)
+    # always through make: a library older than its sources (e.g. lacking a
+    # symbol the header gained) is rebuilt; an up-to-date one costs nothing
+    subprocess.run(["make", "-s", "-j8", "-C", LIBDIR, "asan"], check=True, capture_output=True)
 
 
 def _rt_dir():

@@ -7,14 +7,31 @@ gfx950 correction (MI355X_MICROARCH.md §HBM): FETCH_SIZE is reported in KB and
 counts exactly half the bytes of a wide (16 B/lane) coalesced streaming read,
 so hbm_bytes = FETCH_SIZE * 1024 * 2.  WRITE_SIZE is exact for 16 B/lane
 stores (x1024).  Usage: pmc_traffic.py <counter_collection.csv> <kernel-key=substring> ...
+
+Every entry it writes carries its provenance: the sha256 of the kernel and
+executor sources it was measured with (csrc_digest(), the same digest
+bench.py computes at run time), the git commit and the date.  bench.py
+reports an entry's bytes as roofline.traffic only while the sources still
+hash to that digest; otherwise traffic is null and traffic_source says why.
 """
 import collections
 import csv
+import datetime
 import json
 import os
+import subprocess
 import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+from bench import csrc_digest  # noqa: E402  (one definition of the digest)
+
+
+def git_head():
+    try:
+        return subprocess.check_output(["git", "-C", ROOT, "rev-parse", "--short", "HEAD"], text=True).strip()
+    except Exception:  # noqa: BLE001
+        return None
 
 
 def main():
@@ -41,6 +58,9 @@ def main():
             e["hbm_write_bytes_per_launch"] = w * 1024
         e["hbm_bytes_per_launch"] = e.get("hbm_read_bytes_per_launch", 0) + e.get("hbm_write_bytes_per_launch", 0)
         e["correction"] = "FETCH_SIZE x1024 x2 (gfx950 half-count of 16B/lane streaming reads), WRITE_SIZE x1024"
+        e["csrc_sha256"] = csrc_digest()
+        e["git_head"] = git_head()
+        e["date"] = datetime.date.today().isoformat()
         data[key] = e
     json.dump(data, open(out_path, "w"), indent=1)
     print(json.dumps(data, indent=1))
