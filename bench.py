@@ -909,10 +909,12 @@ def run_ranks(args, world, rank, local_rank, vote=None):
         parity["match"] = parity["match"] and gcount == g_oracle
         if args.config == "c5":
             parity["global_sum"] = gsum
+            parity["global_oracle_sum"] = g_osum
             parity["match"] = parity["match"] and gsum == g_osum
     if world > 1 and args.config == "c3":
         g_exp = mbx_dist.global_group_count_sum(orc, device=coll_dev, group=group)
         parity["global_groups"] = len(ggroups)
+        parity["global_oracle_groups"] = len(g_exp)
         parity["match"] = parity["match"] and ggroups == g_exp
     # every rank's own line items, gathered to rank 0 (gloo)
     mine = {"rank": rank, "device": device, "kernel_ms_avg": avg_k, "elapsed_s": elapsed,
