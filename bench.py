@@ -13,7 +13,7 @@ Multi-GPU (default): the product's own path.  One process opens devices
 caller gets from duckdb_mb_query); the library shards the table by row range,
 runs every shard's fused kernel on its own device and stream from a
 persistent host worker, and combines the partial aggregates with RCCL on the
-shard devices (all-reduce for COUNT, all-gather + carry-correct int128 combine
+shard devices (a reduce to device 0 for COUNT, all-gather + carry-correct int128 combine
 kernel for SUM; the library's default `mbx_combine`), or exactly on the host
 where RCCL does not apply (same-device shards, GROUP BY).  The other combine
 is timed right after the headline (`multi_device.combine_ab`).  Under the driver's `torch.distributed.run --nproc-per-node N`
@@ -178,7 +178,7 @@ def inlib_plan(args, world):
     nshards = len(devices)
     par = (f"in-library row-range shards: gpu_devices={','.join(map(str, devices))} "
            f"({ngpu} GPU x {spg} shard(s), one engine + stream + persistent host worker per shard), "
-           f"per-shard partial aggregates combined by the library's default: an RCCL all-reduce (COUNT) / "
+           f"per-shard partial aggregates combined by the library's default: an RCCL reduce to device 0 (COUNT) / "
            f"all-gather + int128 combine kernel (SUM) over the shard devices when they are distinct, else an exact "
            f"host merge") if nshards > 1 \
         else "row-range shards x1"
@@ -604,7 +604,7 @@ def sharded_parity(conn, config, out, n_total, nshards, threads):
     shard_par, g_cnt, g_sum, g_groups = [], 0, 0, {}
     probe = conn.shard_partial(0)
     if probe is None:
-        # the RCCL all-reduce (COUNT-only rows) leaves no per-shard partials on
+        # the RCCL reduce (COUNT-only rows) leaves no per-shard partials on
         # the host: one more step with the host merge brings them back
         conn.set_combine("host")
         conn.query_raw(f"SELECT COUNT(*) FROM t WHERE x > 24").close()

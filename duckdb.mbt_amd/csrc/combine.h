@@ -8,7 +8,7 @@
 // gathered lanes are combined carry-correct afterwards (CombineColumn, on
 // device 0 by the combine kernel, and on the host by the CPU tests through
 // duckdb_mbx_combine_lanes).  A COUNT-only row needs no int128: its lanes are
-// the counts themselves, summed by one ncclInt64 all-reduce.  Every rank
+// the counts themselves, summed into device 0 by one ncclInt64 reduce.  Every rank
 // appends its device error word, so a shard's overflow is raised as on one
 // device.  Shared by the kernels (rccl_combine.cpp) and the host (shim.cpp).
 #pragma once

@@ -3949,7 +3949,7 @@ static Value LanesValue(const LogicalType &t, int64_t lo, int64_t hi, bool valid
 // (COUNT, SUM as HUGEINT / DECIMAL(38,s), integer MIN / MAX; AVG over
 // integers) is combined by RCCL on the shard devices: every shard packs its
 // one partial row into int64 lanes (combine.h) and takes part in one
-// collective on its own stream -- an ncclInt64 all-reduce when every partial
+// collective on its own stream -- an ncclInt64 reduce to device 0 when every partial
 // is a COUNT, else an all-gather finished by the carry-correct combine kernel
 // on device 0 -- and device 0's answer (with every rank's error word) comes
 // back in one small D2H.  false (the host merge runs instead, the reason in
@@ -4035,7 +4035,7 @@ static bool ShardedAggregateRccl(Connection &c, const BoundSelect &s, const Boun
     pd.err = se.d_err;
     sendb[i] = Alloc(se, (size_t)P * 8);
     recvb[i] = Alloc(se, recv_lanes * 8);
-    if (counts_only && c.rccl->loopback) scrb[i] = Alloc(se, (size_t)nsh * P * 8);
+    if (counts_only && c.rccl->loopback && i == 0) scrb[i] = Alloc(se, (size_t)nsh * P * 8);
     if (i == 0 && !se.EnsurePinned(host.size() * 8)) ThrowError("IO", "RCCL combine: pinned staging");
     rc::Pack(pd, (int64_t *)sendb[i]->p, se.stream);
     HIPCHK(hipGetLastError());

@@ -5,7 +5,12 @@
 #include <dlfcn.h>
 #include <rccl/rccl.h>
 
+#include <chrono>
+#include <condition_variable>
 #include <mutex>
+#include <thread>
+
+#include "knobs.h"
 
 #include "phys.h"
 
@@ -20,7 +25,7 @@ struct Api {
   decltype(&ncclCommInitAll) init = nullptr;
   decltype(&ncclCommDestroy) destroy = nullptr;
   decltype(&ncclAllGather) allgather = nullptr;
-  decltype(&ncclAllReduce) allreduce = nullptr;
+  decltype(&ncclReduce) reduce = nullptr;
   decltype(&ncclGetErrorString) errstr = nullptr;
   decltype(&ncclGroupStart) gstart = nullptr;
   decltype(&ncclGroupEnd) gend = nullptr;
@@ -44,12 +49,12 @@ const Api &GetApi() {
     api.init = (decltype(api.init))dlsym(h, "ncclCommInitAll");
     api.destroy = (decltype(api.destroy))dlsym(h, "ncclCommDestroy");
     api.allgather = (decltype(api.allgather))dlsym(h, "ncclAllGather");
-    api.allreduce = (decltype(api.allreduce))dlsym(h, "ncclAllReduce");
+    api.reduce = (decltype(api.reduce))dlsym(h, "ncclReduce");
     api.errstr = (decltype(api.errstr))dlsym(h, "ncclGetErrorString");
     api.gstart = (decltype(api.gstart))dlsym(h, "ncclGroupStart");
     api.gend = (decltype(api.gend))dlsym(h, "ncclGroupEnd");
     api.abort = (decltype(api.abort))dlsym(h, "ncclCommAbort");
-    api.ok = api.init && api.destroy && api.allgather && api.allreduce && api.errstr && api.gstart && api.gend;
+    api.ok = api.init && api.destroy && api.allgather && api.reduce && api.errstr && api.gstart && api.gend;
     if (!api.ok) api.why = "librccl lacks an entry point";
   });
   return api;
@@ -85,16 +90,39 @@ std::shared_ptr<Comms> Open(const std::vector<int> &devs, bool loopback, std::st
         *note = "shard devices are not distinct (RCCL takes one rank per device): host merge";
         return nullptr;
       }
-  int cur = 0;
-  (void)hipGetDevice(&cur);
-  c->comms.assign(devs.size(), nullptr);
-  const ncclResult_t r = a.init(c->comms.data(), (int)devs.size(), devs.data());
-  (void)hipSetDevice(cur);
-  if (r != ncclSuccess) {
-    c->comms.clear();
-    *note = "ncclCommInitAll: " + ErrText(a, r);
+  // the communicators are built on a helper thread, given a bounded time: an
+  // init that never completes (a bootstrap that cannot reach itself, a link
+  // down) leaves the host merge in charge instead of hanging the statement
+  struct Init {
+    std::mutex mu;
+    std::condition_variable cv;
+    bool done = false;
+    ncclResult_t r = ncclInternalError;
+    std::vector<ncclComm_t> comms;
+  };
+  auto st = std::make_shared<Init>();
+  st->comms.assign(devs.size(), nullptr);
+  std::thread([st, devs, &a] {
+    const ncclResult_t r = a.init(st->comms.data(), (int)devs.size(), devs.data());
+    std::lock_guard<std::mutex> g(st->mu);
+    st->r = r;
+    st->done = true;
+    st->cv.notify_all();
+  }).detach();
+  static const int timeout_ms = [] {
+    const char *v = Knob("MBX_RCCL_INIT_TIMEOUT_MS");
+    return v ? std::max(1, atoi(v)) : 60000;
+  }();
+  std::unique_lock<std::mutex> lk(st->mu);
+  if (!st->cv.wait_for(lk, std::chrono::milliseconds(timeout_ms), [&] { return st->done; })) {
+    *note = "ncclCommInitAll did not complete within " + std::to_string(timeout_ms) + " ms: host merge";
+    return nullptr;  // (the init thread keeps its communicators if it ever finishes)
+  }
+  if (st->r != ncclSuccess) {
+    *note = "ncclCommInitAll: " + ErrText(a, st->r);
     return nullptr;
   }
+  c->comms.assign(st->comms.begin(), st->comms.end());
   return c;
 }
 
@@ -114,14 +142,15 @@ __global__ void sum_lanes_kernel(const int64_t *g, int nranks, int lanes, int64_
   }
 }
 
-bool Collective(Comms &c, bool all_reduce, const std::vector<const int64_t *> &send, const std::vector<int64_t *> &recv,
+bool Collective(Comms &c, bool reduce, const std::vector<const int64_t *> &send, const std::vector<int64_t *> &recv,
                 const std::vector<int64_t *> &scratch, const std::vector<hipStream_t> &streams, size_t count,
                 std::string *err) {
   const int n = (int)c.devs.size();
   if (c.loopback) {
-    // every rank's send block lands in every rank's receive (or scratch)
-    // block after the sender's pack: the data movement of the all-gather, the
-    // all-reduce summed by one small kernel per rank
+    // the data movement of the collective as device copies after every
+    // sender's pack: the all-gather lands every rank's block in every rank's
+    // receive buffer; the reduce lands them in rank 0's scratch, summed there
+    // by one small kernel
     std::vector<hipEvent_t> ev(n, nullptr);
     bool ok = true;
     for (int i = 0; i < n && ok; i++) {
@@ -129,14 +158,14 @@ bool Collective(Comms &c, bool all_reduce, const std::vector<const int64_t *> &s
            hipEventCreateWithFlags(&ev[i], hipEventDisableTiming) == hipSuccess &&
            hipEventRecord(ev[i], streams[i]) == hipSuccess;
     }
-    for (int j = 0; j < n && ok; j++) {
+    for (int j = 0; j < (reduce ? 1 : n) && ok; j++) {
       ok = hipSetDevice(c.devs[j]) == hipSuccess;
-      int64_t *dst = all_reduce ? scratch[j] : recv[j];
+      int64_t *dst = reduce ? scratch[j] : recv[j];
       for (int i = 0; i < n && ok; i++)
         ok = hipStreamWaitEvent(streams[j], ev[i], 0) == hipSuccess &&
              hipMemcpyAsync(dst + (size_t)i * count, send[i], count * 8, hipMemcpyDeviceToDevice, streams[j]) ==
                  hipSuccess;
-      if (ok && all_reduce) {
+      if (ok && reduce) {
         hipLaunchKernelGGL(sum_lanes_kernel, dim3(1), dim3(64), 0, streams[j], (const int64_t *)dst, n, (int)count,
                            recv[j]);
         ok = hipGetLastError() == hipSuccess;
@@ -157,13 +186,13 @@ bool Collective(Comms &c, bool all_reduce, const std::vector<const int64_t *> &s
   }
   ncclResult_t first = ncclSuccess;
   for (int i = 0; i < n; i++) {
-    const ncclResult_t ri = all_reduce ? a.allreduce(send[i], recv[i], count, ncclInt64, ncclSum, c.comms[i], streams[i])
-                                       : a.allgather(send[i], recv[i], count, ncclInt64, c.comms[i], streams[i]);
+    const ncclResult_t ri = reduce ? a.reduce(send[i], recv[i], count, ncclInt64, ncclSum, 0, c.comms[i], streams[i])
+                                   : a.allgather(send[i], recv[i], count, ncclInt64, c.comms[i], streams[i]);
     if (ri != ncclSuccess && first == ncclSuccess) first = ri;
   }
   r = a.gend();
   if (first != ncclSuccess) {
-    *err = std::string(all_reduce ? "ncclAllReduce: " : "ncclAllGather: ") + ErrText(a, first);
+    *err = std::string(reduce ? "ncclReduce: " : "ncclAllGather: ") + ErrText(a, first);
     return false;
   }
   if (r != ncclSuccess) {

@@ -2,7 +2,7 @@
 // the two small kernels around the collective (mbx_combine=rccl).
 //
 // one process, ncclCommInitAll over the shard devices, COUNT
-// as an ncclInt64 all-reduce, SUM int128 as an all-gather of 16-byte partials
+// as an ncclInt64 reduce to device 0, SUM int128 as an all-gather of 16-byte partials
 // with a carry-correct combine on device 0.  librccl is opened with dlopen on
 // first use, so the library loads (and the host merge runs) where it is
 // absent.  Lane layout: combine.h.
@@ -41,11 +41,12 @@ void Abort(Comms &c);
 
 // One collective over every rank, driven from the calling thread: rank i's
 // count int64 lanes send[i] on streams[i] -> recv[i] (all-gather: n * count
-// lanes in rank order; all-reduce: count summed lanes).  The RCCL calls are
-// fused in one ncclGroupStart/End, so no rank can be left inside a collective
-// that another rank never joined.  scratch[i] (n * count lanes) is used by the
-// loopback all-reduce only.  false and *err on an RCCL / HIP error.
-bool Collective(Comms &c, bool all_reduce, const std::vector<const int64_t *> &send, const std::vector<int64_t *> &recv,
+// lanes in rank order on every rank; reduce: count lanes summed into rank 0's
+// recv).  The RCCL calls are fused in one ncclGroupStart/End, so no rank can
+// be left inside a collective that another rank never joined.  scratch[0]
+// (n * count lanes) is used by the loopback reduce only.  false and *err on
+// an RCCL / HIP error.
+bool Collective(Comms &c, bool reduce, const std::vector<const int64_t *> &send, const std::vector<int64_t *> &recv,
                 const std::vector<int64_t *> &scratch, const std::vector<hipStream_t> &streams, size_t count,
                 std::string *err);
 

@@ -324,7 +324,7 @@ duckdb_mb_result *duckdb_mbx_shard_partial(duckdb_mb_connection *connection, int
 
 /* mbx_combine=rccl (the default; Config::set key, ref src/duckdb_native.c:714-747): a
  * sharded global aggregate over distinct devices is combined by RCCL on the
- * shard devices (ncclInt64 all-reduce for COUNT-only rows; all-gather of int128
+ * shard devices (ncclInt64 reduce to device 0 for COUNT-only rows; all-gather of int128
  * lanes + a carry-correct combine on device 0 otherwise).  out2 = {RCCL
  * combines, requests that fell back to the host merge}; out_us1 = the last
  * combine's collective + D2H wall us.  Returns 2 (0: no handle). */

@@ -7,7 +7,7 @@ each shard's lane block into every rank's receive buffer.  Everything around
 them is the product code that a multi-GPU node runs:
   * pack_lanes_kernel on every shard's stream (COUNT as one lane; SUM / MIN /
     MAX as {lo, hi, valid} of the int128 value; the device error word last);
-  * the all-gather / all-reduce data movement, ordered after each pack;
+  * the all-gather / reduce data movement, ordered after each pack;
   * combine_lanes_kernel on device 0 (carry-correct int128 sum, signed
     min/max, validity OR) and the one D2H;
   * the host decode (LanesValue, AVG finished as the emit kernel does) and the
@@ -59,7 +59,7 @@ def test_rccl_loopback_count_sum_minmax_avg(mbx, oracle, devices):
     x = oracle.synth_i64(n, 42, 0, 50, 1)
     v = oracle.synth_i64(n, 9, 0, 1 << 40, -(1 << 39))
     cnt, s = oracle.synth_filter_count(42, 0, n, 50, 1, 25, 2**63 - 1, 8)
-    # COUNT only: the all-reduce form (one lane per column + the error word)
+    # COUNT only: the reduce form (one lane per column + the error word)
     assert _both(c, "SELECT COUNT(*) FROM t WHERE x > 24") == [str(cnt)]
     assert _both(c, "SELECT COUNT(*), COUNT(x) FROM t") == [str(n), str(n)]
     # COUNT + SUM(BIGINT) -> HUGEINT: the all-gather form and the combine kernel
@@ -152,7 +152,7 @@ def test_rccl_loopback_c5_shape(mbx, oracle):
         assert one(c, "SELECT COUNT(*) FROM t WHERE x > 24") == [str(cnt)]
         assert _ran(c, st0) == 1
     # per-shard partials as the all-gather delivered them (the COUNT-only
-    # all-reduce keeps none), each against its shard's row range
+    # reduce keeps none), each against its shard's row range
     one(c, "SELECT COUNT(*), SUM(x) FROM t WHERE x > 24")
     for i in range(2):
         p = c.shard_partial(i)
