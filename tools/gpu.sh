@@ -10,6 +10,12 @@
 #   pmc       rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes of bench.py (one counter set per run)
 #   link      tools/link8_probe (8 MB D2H variants; build it first: see its header)
 #   pmcshape  rocprofv3 kernel trace + FETCH_SIZE / WRITE_SIZE of tools/shape_bench.py (PMC_SHAPES)
+#   clock     C3 / C2 / two-array ring with in-kernel clock stamps at 4 launch cadences (tools/c3_clock.py;
+#             needs libduckdb_mb_amd_clk.so: make -C duckdb.mbt_amd clockdiag), then a GRBM_GUI_ACTIVE pass
+#   seln      NULL-able selection A/B: the default plan vs MBX_SR_NL=$SELN_NL (rocprofv3 stats, alternated twice)
+#   apitrace  HIP API + kernel trace of the C2 query loop at 1e6 rows (tools/query_overhead.py)
+#   rccl      the RCCL-combine loopback tests and the sharded tests
+#   gpuonly   the -m gpu suite alone (as tests, no smoke)
 # Results go to gpurun_out/ (merged back by gpurun); copy what is judged into profiles/.
 set -o pipefail
 mkdir -p gpurun_out
@@ -70,6 +76,30 @@ if has pmcshape; then  # kernel trace + FETCH_SIZE / WRITE_SIZE passes of tools/
   for ctr in FETCH_SIZE WRITE_SIZE; do
     ( cd /tmp && export TMPDIR=/tmp && timeout -s KILL 300 rocprofv3 --pmc $ctr --output-format csv -d $R/gpurun_out/pmcshape/$ctr -o $ctr -- python3 $R/tools/shape_bench.py 1000000000 > $R/gpurun_out/pmcshape_$ctr.log 2>&1 ) || exit 26
   done
+fi
+if has clock; then
+  mkdir -p gpurun_out/clock
+  DUCKDB_MB_AMD_LIB=$R/duckdb.mbt_amd/libduckdb_mb_amd_clk.so timeout -k 10 300 python -u tools/c3_clock.py 15 > gpurun_out/clock/c3_clock.jsonl 2> gpurun_out/clock/c3_clock.err || exit 27
+  ( cd /tmp && export TMPDIR=/tmp && timeout -s KILL 200 rocprofv3 --pmc GRBM_GUI_ACTIVE --kernel-trace --output-format csv -d $R/gpurun_out/clock/grbm -o grbm -- python3 $R/tools/c3_clock.py pmc 15 > $R/gpurun_out/clock/grbm.log 2>&1 ) || exit 28
+fi
+if has seln; then
+  mkdir -p gpurun_out/seln
+  for rep in 1 2; do
+    for nl in default ${SELN_NL:-4}; do
+      ( cd /tmp && export TMPDIR=/tmp MBX_EXPERIMENTS=1 NULLABLE=1 SHAPES=${SHAPES:-seln_out,seln_pred} REPS=7 && if [ $nl != default ]; then export MBX_SR_NL=$nl; fi && timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $R/gpurun_out/seln/nl${nl}_$rep -o t -- python3 $R/tools/shape_bench.py 1000000000 > $R/gpurun_out/seln/nl${nl}_$rep.log 2>&1 ) || exit 29
+      rm -f $R/gpurun_out/seln/nl${nl}_$rep/*kernel_trace.csv
+    done
+  done
+fi
+if has apitrace; then
+  mkdir -p gpurun_out/apitrace
+  ( cd /tmp && export TMPDIR=/tmp && timeout -k 10 300 rocprofv3 --hip-trace --kernel-trace --output-format csv -d $R/gpurun_out/apitrace/tr -o tr -- python3 $R/tools/query_overhead.py 1000000 > $R/gpurun_out/apitrace/qo.log 2>&1 ) || exit 30
+fi
+if has rccl; then
+  timeout -k 10 500 python -u -m pytest tests/test_gpu_rccl_loopback.py tests/test_gpu_sharded.py -m gpu -x -q --timeout 200 --timeout-method thread > gpurun_out/rccl_tests.log 2>&1 || exit 31
+fi
+if has gpuonly; then
+  timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > gpurun_out/gpu_tests.log 2>&1 || exit 32
 fi
 if has link; then
   timeout -k 10 200 ./tools/link8_probe ${LINK_MB:-8} 200 > gpurun_out/link8_probe.log 2>&1 || exit 23
