@@ -488,6 +488,13 @@ def run_inlib(args, world, rank, vote=None):
                 r["measured_ceiling_gbs"] = ceil[shape]
                 r["ceiling_shape"] = shape
                 r["frac_of_measured"] = r["achieved_gbs"] / ceil[shape]
+    if plan["nshards"] == 1 and args.config == "c2" and extras:
+        # the RCCL calls of the in-library combine, on this one-GPU box: a one-rank
+        # communicator, a grouped reduce and all-gather (outside the timed loop)
+        try:
+            result["extra"]["rccl_selftest"] = mbx.rccl_selftest(0)
+        except Exception as ex:  # noqa: BLE001
+            result["extra"]["rccl_selftest"] = {"ok": False, "error": str(ex)}
     if not args.no_cpu and plan["nshards"] == 1 and args.config in ("c2", "c2d", "c3", "c5", "sel"):
         result["cpu_baseline"] = cpu_baseline(args.cpu_seconds, "c2" if args.config == "c2d" else args.config)
     if dist:

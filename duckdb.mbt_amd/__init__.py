@@ -82,6 +82,7 @@ _sig("duckdb_mbx_hbm_calibrate", _I, _P, _L, _I, ctypes.POINTER(ctypes.c_double)
 _sig("duckdb_mbx_hbm_calibrate_ex", _I, _P, _L, _I, ctypes.POINTER(ctypes.c_double), _I)
 _sig("duckdb_mbx_clock_stamps", _I, _P, ctypes.POINTER(ctypes.c_uint64), _I)
 _sig("duckdb_mbx_set_link_mode", _I, _I)
+_sig("duckdb_mbx_rccl_selftest", _I, _I, ctypes.POINTER(ctypes.c_double))
 _sig("duckdb_mbx_link_stats", ctypes.c_void_p)
 _sig("duckdb_mbx_statement_plan_stats", _I, _P, ctypes.POINTER(ctypes.c_int64))
 _sig("duckdb_mbx_shard_stats", _I, _P, ctypes.POINTER(ctypes.c_int64), ctypes.POINTER(ctypes.c_double))
@@ -715,6 +716,14 @@ class RawResult:
         buf = ctypes.create_string_buffer(16)
         n = lib.duckdb_mbx_result_raw(self._h, c, r, buf, 16)
         return buf.raw[:n]
+
+
+def rccl_selftest(device: int = 0) -> dict:
+    """The RCCL calls of the combine on hardware with one GPU (extension): a
+    one-rank communicator, one grouped reduce and one all-gather, checked."""
+    us = (ctypes.c_double * 1)()
+    ok = lib.duckdb_mbx_rccl_selftest(device, us) == 1
+    return {"ok": ok, "us": us[0], "error": "" if ok else _last_error("rccl self-test failed")}
 
 
 def set_link_mode(mode: int) -> None:

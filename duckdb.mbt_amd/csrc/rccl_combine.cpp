@@ -202,6 +202,44 @@ bool Collective(Comms &c, bool reduce, const std::vector<const int64_t *> &send,
   return true;
 }
 
+std::string SelfTest(int device, double *us) {
+  std::string note;
+  const auto t0 = std::chrono::steady_clock::now();
+  auto c = Open({device}, false, &note);
+  if (!c) return note.empty() ? "RCCL unavailable" : note;
+  int cur = 0;
+  (void)hipGetDevice(&cur);
+  std::string err;
+  hipStream_t s = nullptr;
+  int64_t *buf = nullptr;
+  constexpr int kLanes = 97;  // an odd lane count: 3 columns x 32 + the error word
+  int64_t host[3 * kLanes];
+  for (int i = 0; i < kLanes; i++) host[i] = (int64_t)0x123456789abcdefLL * (i + 1) - (int64_t)i * i;
+  if (hipSetDevice(device) != hipSuccess || hipStreamCreateWithFlags(&s, hipStreamNonBlocking) != hipSuccess ||
+      hipMalloc((void **)&buf, sizeof(host)) != hipSuccess ||
+      hipMemsetAsync(buf, 0xff, sizeof(host), s) != hipSuccess ||
+      hipMemcpyAsync(buf, host, kLanes * 8, hipMemcpyHostToDevice, s) != hipSuccess) {
+    err = "RCCL self-test: HIP setup failed";
+  }
+  // one rank: the reduce and the all-gather each return the send lanes
+  if (err.empty() && !Collective(*c, true, {buf}, {buf + kLanes}, {nullptr}, {s}, kLanes, &err)) {
+  } else if (err.empty() && !Collective(*c, false, {buf}, {buf + 2 * kLanes}, {nullptr}, {s}, kLanes, &err)) {
+  }
+  int64_t back[3 * kLanes];
+  if (err.empty() && (hipMemcpyAsync(back, buf, sizeof(back), hipMemcpyDeviceToHost, s) != hipSuccess ||
+                      hipStreamSynchronize(s) != hipSuccess))
+    err = "RCCL self-test: HIP copy-back failed";
+  if (err.empty())
+    for (int i = 0; i < kLanes && err.empty(); i++)
+      if (back[kLanes + i] != host[i] || back[2 * kLanes + i] != host[i])
+        err = "RCCL self-test: lane " + std::to_string(i) + " differs after the collectives";
+  if (s) (void)hipStreamSynchronize(s), (void)hipStreamDestroy(s);
+  if (buf) (void)hipFree(buf);
+  (void)hipSetDevice(cur);
+  *us = std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0).count();
+  return err;
+}
+
 // one lane group per column: row 0's value widened to int128, its validity
 __global__ void pack_lanes_kernel(PackDesc d, int64_t *dst) {
   const int j = threadIdx.x;

@@ -50,6 +50,12 @@ bool Collective(Comms &c, bool reduce, const std::vector<const int64_t *> &send,
                 const std::vector<int64_t *> &scratch, const std::vector<hipStream_t> &streams, size_t count,
                 std::string *err);
 
+// Hardware check of the RCCL calls the combine makes, for a box with one GPU:
+// a one-rank communicator on `device` (ncclCommInitAll on the helper thread),
+// one grouped reduce and one grouped all-gather of 97 int64 lanes, the lanes
+// checked.  Returns "" (and the wall time in *us) or what failed.
+std::string SelfTest(int device, double *us);
+
 // the lanes of a one-row partial relation (row 0 of every column) and the
 // device error word, written to dst by one small kernel
 struct PackDesc {

@@ -1793,6 +1793,28 @@ int32_t duckdb_mbx_set_combine(duckdb_mb_connection *h, int32_t mode) {
   return 1;
 }
 
+// The RCCL library calls of the combine on hardware with one GPU (the combine
+// itself needs one device per rank): a one-rank communicator on `device`, one
+// grouped ncclReduce and one ncclAllGather of 97 int64 lanes, checked.  Returns
+// 1 and the wall us in *us_out; 0 and the reason via duckdb_mb_last_error.
+extern "C++" {
+namespace mbx {
+namespace rc {
+std::string SelfTest(int device, double *us);  // rccl_combine.cpp
+}
+}  // namespace mbx
+}
+int32_t duckdb_mbx_rccl_selftest(int32_t device, double *us_out) {
+  double us = 0;
+  const std::string err = mbx::rc::SelfTest(device, &us);
+  if (us_out) *us_out = us;
+  if (!err.empty()) {
+    SetError(err.c_str());
+    return 0;
+  }
+  return 1;
+}
+
 // The RCCL combine's lane arithmetic on the host (combine.h; CPU tests):
 // gathered = nranks x (3 ncols + 1) lanes, kinds[ncols] (0 sum, 1 min, 2 max);
 // out = 3 ncols lanes {lo, hi, non-NULL}.  Returns 1 (0: bad arguments).

@@ -341,6 +341,12 @@ int32_t duckdb_mbx_rccl_stats_ex(duckdb_mb_connection *connection, int64_t *out,
  * without MBX_EXPERIMENTS=1), so it runs over same-device shards.  Returns 1
  * (0: refused). */
 int32_t duckdb_mbx_set_combine(duckdb_mb_connection *connection, int32_t mode);
+/* The RCCL calls the combine makes, checked on hardware with one GPU (the
+ * combine needs one device per rank): a one-rank communicator on `device`, one
+ * grouped ncclReduce and one ncclAllGather of 97 int64 lanes.  Returns 1 and
+ * the wall microseconds in *us_out (may be NULL); 0 with the reason in
+ * duckdb_mb_last_error(). */
+int32_t duckdb_mbx_rccl_selftest(int32_t device, double *us_out);
 /* The RCCL combine's lane arithmetic on the host (tests): gathered holds
  * nranks x (3 ncols + 1) int64 lanes ({lo, hi, non-NULL} per column, then the
  * rank's error word); kinds[j] = 0 sum / 1 min / 2 max; out = 3 ncols lanes.

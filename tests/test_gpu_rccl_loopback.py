@@ -183,3 +183,15 @@ def test_rccl_without_distinct_devices_falls_back_with_note(mbx, oracle):
     q(c, "SELECT SUM(x / 2) FROM t")
     assert "floating-point" in c.rccl_stats()["note"]
     c.close()
+
+
+def test_rccl_library_calls_on_one_gpu(mbx):
+    """The real RCCL calls the combine makes -- librccl opened by dlopen,
+    ncclCommInitAll (on its helper thread, bounded), one ncclReduce and one
+    ncclAllGather inside ncclGroupStart/End on a stream of the device -- on a
+    one-rank communicator, the only one a one-GPU box allows; the lanes come
+    back unchanged.  (Distinct-device ranks exchange data the same way.)"""
+    r = mbx.rccl_selftest(0)
+    assert r["ok"], r
+    # twice: a second communicator in the same process
+    assert mbx.rccl_selftest(0)["ok"]
