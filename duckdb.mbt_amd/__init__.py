@@ -647,12 +647,12 @@ class Connection:
         out = (ctypes.c_int64 * 2)()
         us = (ctypes.c_double * 1)()
         lib.duckdb_mbx_rccl_stats(self._h, out, us)
-        ex = (ctypes.c_int64 * 5)()
-        lib.duckdb_mbx_rccl_stats_ex(self._h, ex, 5)
+        ex = (ctypes.c_int64 * 6)()
+        lib.duckdb_mbx_rccl_stats_ex(self._h, ex, 6)
         p = lib.duckdb_mbx_rccl_note(self._h)
         note = ctypes.string_at(p).decode()
         lib.duckdb_mbx_free(p)
-        return {"rccl_combines": out[0], "rccl_fallbacks": out[1], "rccl_loopbacks": ex[2], "rccl_errors": ex[3], "rccl_timeouts": ex[4],
+        return {"rccl_combines": out[0], "rccl_fallbacks": out[1], "rccl_loopbacks": ex[2], "rccl_errors": ex[3], "rccl_timeouts": ex[4], "rccl_group_combines": ex[5],
                 "last_rccl_us": us[0], "note": note}
 
     def set_combine(self, rccl) -> None:

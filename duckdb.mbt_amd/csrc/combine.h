@@ -35,6 +35,9 @@ enum Kind : int8_t {
 // int64 lanes per rank: 3 per column (or 1 per column for a COUNT-only row), then the error word
 MBX_HD inline int LanesPerRank(int ncols, bool counts_only) { return (counts_only ? ncols : 3 * ncols) + 1; }
 
+// int64 lanes per dense GROUP BY slot: presence, then {lo, hi, flags} per column
+MBX_HD inline int SlotLanes(int ncols) { return 1 + 3 * ncols; }
+
 MBX_HD inline int Cmp128(int64_t alo, int64_t ahi, int64_t blo, int64_t bhi) {
   if (ahi != bhi) return ahi < bhi ? -1 : 1;
   const uint64_t a = (uint64_t)alo, b = (uint64_t)blo;

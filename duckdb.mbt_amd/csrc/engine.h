@@ -168,6 +168,7 @@ struct ShardStats {
   // on the shard devices instead of the host merge
   int64_t rccl_combines = 0, rccl_fallbacks = 0;
   int64_t rccl_loopbacks = 0;  // of rccl_combines, through the test loopback
+  int64_t rccl_group_combines = 0;  // of rccl_combines, GROUP BY relations
   int64_t rccl_errors = 0;     // combines that raised a shard's device error
   int64_t rccl_timeouts = 0;   // collectives aborted after MBX_RCCL_TIMEOUT_MS (then host merge)
   double last_rccl_us = 0;

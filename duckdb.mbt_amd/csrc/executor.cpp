@@ -10,6 +10,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <array>
 #include <atomic>
 #include <chrono>
 #include <type_traits>
@@ -3954,6 +3955,87 @@ static Value LanesValue(const LogicalType &t, int64_t lo, int64_t hi, bool valid
 // on device 0 -- and device 0's answer (with every rank's error word) comes
 // back in one small D2H.  false (the host merge runs instead, the reason in
 // shard_stats.rccl_note) for other shapes or without distinct devices.
+// How each partial column of p combines across ranks (combine.h kinds) and
+// whether every one is a COUNT; false and *why for partials RCCL does not
+// combine (floating point, non-integer MIN/MAX, too many columns).
+static bool RcclKinds(const BoundSelect &p, rc::CombineDesc &cd, bool &counts_only, std::string *why) {
+  const int ncols = (int)p.aggs.size();
+  if (ncols < 1 || ncols > rc::kMaxCols) return *why = "partial row wider than the RCCL lane block", false;
+  memset(&cd, 0, sizeof(cd));
+  counts_only = true;
+  for (int k = 0; k < ncols; k++) {
+    const AggSpec &a = p.aggs[k];
+    const VClass vc = ClassOf(a.type);
+    switch (a.kind) {
+      case A_COUNT_STAR:
+      case A_COUNT: cd.kind[k] = rc::K_SUM; break;
+      case A_SUM:
+        if (vc != VC_I64 && vc != VC_I128) return *why = "floating-point SUM: host merge", false;
+        cd.kind[k] = rc::K_SUM, counts_only = false;
+        break;
+      case A_MIN:
+      case A_MAX:
+        if ((vc != VC_I64 && vc != VC_I128) || PhysOf(a.type) == P_STR || PhysOf(a.type) == P_INTERVAL)
+          return *why = "non-integer MIN/MAX: host merge", false;
+        cd.kind[k] = a.kind == A_MIN ? rc::K_MIN : rc::K_MAX, counts_only = false;
+        break;
+      default: return *why = "aggregate without an integer partial: host merge", false;
+    }
+  }
+  cd.ncols = ncols;
+  return true;
+}
+
+// the connection's communicators (opened on first use; the loopback when the
+// test mode asks for it); false and the reason in shard_stats.rccl_note
+static bool RcclReady(Connection &c) {
+  ShardStats &st = c.shard_stats;
+  if (c.rccl && rc::IsLoopback(*c.rccl) != c.opts.rccl_loopback) c.rccl.reset(), c.rccl_tried = false;
+  if (!c.rccl_tried) {
+    c.rccl_tried = true;
+    std::string note;
+    c.rccl = rc::Open(c.opts.devices, c.opts.rccl_loopback, &note);
+    if (!c.rccl) st.rccl_note = note;
+  }
+  if (!c.rccl && st.rccl_note.empty()) st.rccl_note = "RCCL unavailable";
+  return c.rccl != nullptr;
+}
+
+// Waits (bounded) for every rank's stream after a collective; false when it
+// timed out, after the communicators were aborted (this connection keeps the
+// host merge from then on: rccl_tried stays set).
+static bool RcclWait(Connection &c, const std::vector<hipStream_t> &streams,
+                     std::chrono::steady_clock::time_point t0) {
+  if (c.rccl->loopback) return true;
+  static const int timeout_ms = [] {
+    const char *v = Knob("MBX_RCCL_TIMEOUT_MS");
+    return v ? std::max(1, atoi(v)) : 20000;
+  }();
+  const auto deadline = t0 + std::chrono::milliseconds(timeout_ms);
+  for (size_t i = 0; i < streams.size();) {
+    const hipError_t q = hipStreamQuery(streams[i]);
+    if (q != hipErrorNotReady) {  // done (or an error, raised by the synchronisation after)
+      i++;
+      continue;
+    }
+    if (std::chrono::steady_clock::now() > deadline) {
+      rc::Abort(*c.rccl);
+      for (size_t k = 0; k < streams.size(); k++) {
+        Eng(*c.shards[k]);
+        (void)hipStreamSynchronize(streams[k]);
+      }
+      Eng(c);
+      c.rccl.reset();
+      c.shard_stats.rccl_timeouts++;
+      c.shard_stats.rccl_note = "an RCCL collective did not complete within " + std::to_string(timeout_ms) +
+                                " ms: communicators aborted, host merge from now on";
+      return false;
+    }
+    __builtin_ia32_pause();
+  }
+  return true;
+}
+
 static bool ShardedAggregateRccl(Connection &c, const BoundSelect &s, const BoundSelect &p,
                                  const std::vector<int> &first, std::vector<std::vector<Value>> &rows,
                                  std::vector<LogicalType> &types) {
@@ -3964,39 +4046,13 @@ static bool ShardedAggregateRccl(Connection &c, const BoundSelect &s, const Boun
     st.rccl_note = why;
     return false;
   };
-  if (!s.groups.empty()) return fallback("GROUP BY: host merge (the RCCL combine covers global aggregates)");
+  if (!s.groups.empty()) return false;  // (GROUP BY: ShardedAggregateRows, GroupRcclCombine)
   const int ncols = (int)p.aggs.size();
-  if (ncols < 1 || ncols > rc::kMaxCols) return fallback("partial row wider than the RCCL lane block");
   rc::CombineDesc cd;
-  memset(&cd, 0, sizeof(cd));
   bool counts_only = true;
-  for (int k = 0; k < ncols; k++) {
-    const AggSpec &a = p.aggs[k];
-    const VClass vc = ClassOf(a.type);
-    switch (a.kind) {
-      case A_COUNT_STAR:
-      case A_COUNT: cd.kind[k] = rc::K_SUM; break;
-      case A_SUM:
-        if (vc != VC_I64 && vc != VC_I128) return fallback("floating-point SUM: host merge");
-        cd.kind[k] = rc::K_SUM, counts_only = false;
-        break;
-      case A_MIN:
-      case A_MAX:
-        if ((vc != VC_I64 && vc != VC_I128) || PhysOf(a.type) == P_STR || PhysOf(a.type) == P_INTERVAL)
-          return fallback("non-integer MIN/MAX: host merge");
-        cd.kind[k] = a.kind == A_MIN ? rc::K_MIN : rc::K_MAX, counts_only = false;
-        break;
-      default: return fallback("aggregate without an integer partial: host merge");
-    }
-  }
-  if (c.rccl && rc::IsLoopback(*c.rccl) != c.opts.rccl_loopback) c.rccl.reset(), c.rccl_tried = false;
-  if (!c.rccl_tried) {
-    c.rccl_tried = true;
-    std::string note;
-    c.rccl = rc::Open(c.opts.devices, c.opts.rccl_loopback, &note);
-    if (!c.rccl) st.rccl_note = note;
-  }
-  if (!c.rccl) return fallback(st.rccl_note.empty() ? "RCCL unavailable" : st.rccl_note);
+  std::string why;
+  if (!RcclKinds(p, cd, counts_only, &why)) return fallback(why);
+  if (!RcclReady(c)) return fallback(st.rccl_note);
   const Table &t = *s.src.table;
   const int nsh = (int)t.parts.size();
   if (nsh != (int)c.rccl->devs.size()) return fallback("table parts do not match the shard devices: host merge");
@@ -4056,37 +4112,10 @@ static bool ShardedAggregateRccl(Connection &c, const BoundSelect &s, const Boun
   const bool cok = rc::Collective(*c.rccl, counts_only, sp, rp, xp, streams, (size_t)P, &cerr);
   // A collective that does not complete in time (a rank that cannot reach the
   // others, a broken link) must not hang the connection: the communicators
-  // are aborted, this connection keeps the host merge from then on, and the
-  // host merge answers this statement.
-  if (cok && !c.rccl->loopback) {
-    static const int timeout_ms = [] {
-      const char *v = Knob("MBX_RCCL_TIMEOUT_MS");
-      return v ? std::max(1, atoi(v)) : 20000;
-    }();
-    const auto deadline = tc0 + std::chrono::milliseconds(timeout_ms);
-    for (int i = 0; i < nsh;) {
-      const hipError_t q = hipStreamQuery(streams[i]);
-      if (q != hipErrorNotReady) {  // done (or an error, raised by the synchronisation below)
-        i++;
-        continue;
-      }
-      if (std::chrono::steady_clock::now() > deadline) {
-        rc::Abort(*c.rccl);
-        for (int k = 0; k < nsh; k++) {
-          Eng(*c.shards[k]);
-          (void)hipStreamSynchronize(streams[k]);
-          sendb[k].reset(), recvb[k].reset(), scrb[k].reset();
-          rel[k] = DRel();
-        }
-        Eng(c);
-        c.rccl.reset();  // rccl_tried stays set: no new communicators on this connection
-        st.rccl_timeouts++;
-        st.rccl_note = "an RCCL collective did not complete within " + std::to_string(timeout_ms) +
-                       " ms: communicators aborted, host merge from now on";
-        return fallback(st.rccl_note);
-      }
-      __builtin_ia32_pause();
-    }
+  // are aborted and the host merge answers this statement and the next ones.
+  if (cok && !RcclWait(c, streams, tc0)) {
+    for (int k = 0; k < nsh; k++) sendb[k].reset(), recvb[k].reset(), scrb[k].reset(), rel[k] = DRel();
+    return fallback(st.rccl_note);
   }
   // Phase 3: device 0 finishes (combine kernel, one D2H); every rank's stream
   // is drained before its lane buffers go back to its pool
@@ -4195,6 +4224,221 @@ static bool ShardedAggregateRccl(Connection &c, const BoundSelect &s, const Boun
   return true;
 }
 
+// mbx_combine=rccl for a sharded GROUP BY on one integer key (SURVEY.md
+// §8(e): the GROUP BY partials travel by the same all-gather).  Each shard's
+// partial relation (its groups, already on its device) is packed into dense
+// key slots -- slot = key - kmin over the union of the shards' key ranges,
+// the NULL key last -- with {lo, hi, valid} lanes per partial column
+// (PackRows); one all-gather of the blocks; combine_slots_kernel on device 0
+// ORs presence and combines each column as the global combine does; one D2H
+// of the combined slots (and of the gathered blocks, for the per-shard
+// partials).  Groups come out in key order, NULL last, as the direct-index
+// paths emit them.  false (the caller merges the same partials on the host)
+// when the key range is wider than kMaxGroupSlots or a collective fails.
+static constexpr int64_t kMaxGroupSlots = 4096;
+static bool GroupRcclEligible(Connection &c, const BoundSelect &s, const BoundSelect &p, rc::CombineDesc &cd) {
+  ShardStats &st = c.shard_stats;
+  if (!c.opts.combine_rccl || s.groups.size() != 1) return false;
+  auto fallback = [&](const std::string &why) {
+    st.rccl_fallbacks++;
+    st.rccl_note = why;
+    return false;
+  };
+  const LogicalType &kt = s.groups[0]->type;
+  const Phys kp = PhysOf(kt);
+  if (kp != P_I8 && kp != P_I16 && kp != P_I32 && kp != P_I64 && kp != P_U8 && kp != P_U16 && kp != P_U32)
+    return fallback("GROUP BY key is not an integer column of <= 64 bits: host merge");
+  bool counts_only = false;
+  std::string why;
+  if (!RcclKinds(p, cd, counts_only, &why)) return fallback(why);
+  if (!RcclReady(c)) return fallback(st.rccl_note);
+  if ((int)s.src.table->parts.size() != (int)c.rccl->devs.size())
+    return fallback("table parts do not match the shard devices: host merge");
+  return true;
+}
+
+static bool GroupRcclCombine(Connection &c, const BoundSelect &s, const BoundSelect &p, const std::vector<int> &first,
+                             rc::CombineDesc cd, std::vector<DRel> &rel, const std::vector<std::array<long long, 3>> &kr,
+                             std::vector<std::vector<Value>> &rows, std::vector<LogicalType> &types) {
+  ShardStats &st = c.shard_stats;
+  auto fallback = [&](const std::string &why) {
+    st.rccl_fallbacks++;
+    st.rccl_note = why;
+    return false;
+  };
+  const int nsh = (int)rel.size(), ncols = cd.ncols;
+  // the union of the shards' key ranges, and whether any shard has the NULL group
+  bool any = false, has_null = false;
+  i128 kmin = 0, kmax = 0;
+  for (int i = 0; i < nsh; i++) {
+    if (kr[i][2] > 0) {
+      if (!any || (i128)kr[i][0] < kmin) kmin = kr[i][0];
+      if (!any || (i128)kr[i][1] > kmax) kmax = kr[i][1];
+      any = true;
+    }
+    has_null |= kr[i][2] < rel[i].n;
+  }
+  const i128 range = any ? kmax - kmin + 1 : 0;
+  if (range > kMaxGroupSlots) return fallback("GROUP BY key range wider than 4096: host merge");
+  const int64_t nslot = (int64_t)range + 1;  // + the NULL key's slot
+  const int64_t SL = rc::SlotLanes(ncols), P = nslot * SL + 1, recv_lanes = (int64_t)nsh * P;
+  const int64_t out_lanes = nslot * SL + nsh;
+  cd.nranks = nsh;
+  Engine &e = *c.engine;
+  std::vector<DevBufPtr> sendb(nsh), recvb(nsh);
+  std::vector<const int64_t *> sp(nsh);
+  std::vector<int64_t *> rp(nsh), xp(nsh, nullptr);
+  std::vector<hipStream_t> streams(nsh);
+  // pack every rank's block (the partial relations are on their devices)
+  for (int i = 0; i < nsh; i++) {
+    Engine &se = Eng(*c.shards[i]);
+    const DRel &r = rel[i];
+    rc::PackRowsDesc pd;
+    memset(&pd, 0, sizeof(pd));
+    pd.key = r.cols[0].data;
+    pd.key_valid = r.cols[0].validity;
+    pd.key_phys = (uint8_t)r.cols[0].phys;
+    for (int k = 0; k < ncols; k++) {
+      const DCol &d = r.cols[1 + k];
+      if (d.phys == P_STR || d.phys == P_F32 || d.phys == P_F64 || d.phys == P_INTERVAL || !d.data)
+        ThrowError("Internal", "RCCL combine: partial column type");
+      pd.data[k] = d.data;
+      pd.valid[k] = d.validity;
+      pd.phys[k] = (uint8_t)d.phys;
+    }
+    pd.ncols = ncols;
+    pd.nrows = r.n;
+    pd.kmin = (int64_t)kmin;
+    pd.nslot = nslot;
+    pd.err = se.d_err;
+    sendb[i] = Alloc(se, (size_t)P * 8);
+    recvb[i] = Alloc(se, (size_t)recv_lanes * 8);
+    rc::PackRows(pd, (int64_t *)sendb[i]->p, se.stream);
+    HIPCHK(hipGetLastError());
+    sp[i] = (const int64_t *)sendb[i]->p;
+    rp[i] = (int64_t *)recvb[i]->p;
+    streams[i] = se.stream;
+  }
+  const auto tc0 = std::chrono::steady_clock::now();
+  std::string cerr;
+  const bool cok = rc::Collective(*c.rccl, false, sp, rp, xp, streams, (size_t)P, &cerr);
+  if (cok && !RcclWait(c, streams, tc0)) return fallback(st.rccl_note);
+  // device 0 combines; one D2H of the combined slots and of the gathered blocks
+  const bool keep_parts = recv_lanes * 8 <= ((int64_t)4 << 20);  // the per-shard partials, when small
+  std::vector<int64_t> host((size_t)out_lanes + (keep_parts ? (size_t)recv_lanes : 0));
+  std::exception_ptr first_err;
+  for (int i = 0; i < nsh; i++) {
+    Engine &se = Eng(*c.shards[i]);
+    try {
+      if (cok && i == 0) {
+        DevBufPtr out = Alloc(se, (size_t)out_lanes * 8);
+        rc::CombineSlots(cd, nslot, (const int64_t *)recvb[0]->p, (int64_t *)out->p, se.stream);
+        HIPCHK(hipGetLastError());
+        if (!se.EnsurePinned(host.size() * 8)) ThrowError("IO", "RCCL combine: pinned staging");
+        HIPCHK(hipMemcpyAsync(se.h_pinned, out->p, (size_t)out_lanes * 8, hipMemcpyDeviceToHost, se.stream));
+        if (keep_parts)
+          HIPCHK(hipMemcpyAsync(se.h_pinned + out_lanes * 8, recvb[0]->p, (size_t)recv_lanes * 8,
+                                hipMemcpyDeviceToHost, se.stream));
+        HIPCHK(hipStreamSynchronize(se.stream));
+        memcpy(host.data(), se.h_pinned, host.size() * 8);
+      } else {
+        HIPCHK(hipStreamSynchronize(se.stream));
+      }
+      ShardCollect(e, se, i, true);
+    } catch (...) {
+      if (!first_err) first_err = std::current_exception();
+    }
+    sendb[i].reset(), recvb[i].reset();
+  }
+  Eng(c);
+  const double t_coll = std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - tc0).count();
+  if (first_err) std::rethrow_exception(first_err);
+  if (!cok) return fallback("RCCL all-gather failed (" + cerr + "): host merge");
+  const auto t_merge = std::chrono::steady_clock::now();
+  // every rank's device error word: the first raised naming its shard, all cleared
+  int bad = -1;
+  std::vector<int32_t> errs(nsh);
+  for (int i = 0; i < nsh; i++) {
+    errs[i] = (int32_t)host[(size_t)nslot * SL + i];
+    if (!errs[i]) continue;
+    if (bad < 0) bad = i;
+    Engine &se = Eng(*c.shards[i]);
+    HIPCHK(hipMemsetAsync(se.d_err, 0, sizeof(int32_t), se.stream));
+    HIPCHK(hipStreamSynchronize(se.stream));
+  }
+  Eng(c);
+  if (bad >= 0) {
+    st.rccl_errors++;
+    try {
+      RaiseDeviceError(e, errs[bad]);
+    } catch (std::exception &ex) {
+      throw EngineError(std::string(ex.what()) + " (shard " + std::to_string(bad) + " of " + std::to_string(nsh) +
+                        ", device " + std::to_string(c.shards[bad]->opts.device) + ")");
+    }
+    ThrowError("Internal", "RCCL combine: a shard reported a device error");
+  }
+  // the merged groups in key order (the NULL key last), aggregates finished as the host merge does
+  const LogicalType &kt = s.groups[0]->type;
+  auto key_value = [&](int64_t sl) {
+    if (sl == nslot - 1) return Value::Null(kt);
+    const i128 k = kmin + sl;
+    return LanesValue(kt, (int64_t)k, (int64_t)(k >> 64), true);
+  };
+  types.clear();
+  types.push_back(kt);
+  for (auto &a : s.aggs) types.push_back(a.type);
+  rows.clear();
+  std::vector<Value> part(1 + ncols);
+  for (int64_t sl = 0; sl < nslot; sl++) {
+    const int64_t *o = host.data() + sl * SL;
+    if (!o[0]) continue;
+    part[0] = key_value(sl);
+    for (int k = 0; k < ncols; k++) part[1 + k] = LanesValue(p.aggs[k].type, o[1 + 3 * k], o[2 + 3 * k], o[3 + 3 * k] & 1);
+    std::vector<ShardAcc> accs(s.aggs.size());
+    FoldPartial(s, first, accs, [&](int col) { return part[col]; });
+    std::vector<Value> row;
+    row.push_back(part[0]);
+    FinishAccs(s, accs, row);
+    rows.push_back(std::move(row));
+  }
+  // each rank's partial groups as they were gathered
+  st.last_partials.clear();
+  if (keep_parts) {
+    for (int i = 0; i < nsh; i++) {
+      const int64_t *g = host.data() + out_lanes + (size_t)i * P;
+      auto res = std::make_shared<MaterializedResult>();
+      HostColumn kc;
+      kc.name = p.names[0];
+      kc.type = kt;
+      kc.phys = PhysOf(kt);
+      std::vector<HostColumn> vc(ncols);
+      for (int k = 0; k < ncols; k++) {
+        vc[k].name = p.names[1 + k];
+        vc[k].type = p.aggs[k].type;
+        vc[k].phys = PhysOf(vc[k].type);
+      }
+      for (int64_t sl = 0; sl < nslot; sl++) {
+        const int64_t *o = g + sl * SL;
+        if (!o[0]) continue;
+        HostColumnPush(kc, key_value(sl));
+        for (int k = 0; k < ncols; k++)
+          HostColumnPush(vc[k], LanesValue(vc[k].type, o[1 + 3 * k], o[2 + 3 * k], o[3 + 3 * k] & 1));
+        res->nrows++;
+      }
+      res->cols.push_back(std::move(kc));
+      for (auto &h : vc) res->cols.push_back(std::move(h));
+      st.last_partials.push_back(res);
+    }
+  }
+  st.rccl_combines++;
+  st.rccl_group_combines++;
+  if (c.rccl->loopback) st.rccl_loopbacks++;
+  st.rccl_note.clear();
+  st.last_rccl_us = t_coll;
+  st.last_combine_us = std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t_merge).count();
+  return true;
+}
+
 // The host merge when every group key is an integer-like column (the C3
 // shape): the partial rows are keyed by their raw int128 keys (NULL last, as
 // the direct-index paths order them), sorted once, and each run of equal keys
@@ -4281,6 +4525,12 @@ static void ShardedAggregateRows(Connection &c, const BoundSelect &s, const Boun
   const int nsh = (int)t.parts.size(), ng = (int)s.groups.size();
   std::vector<ResultPtr> partial(nsh);
   Engine &e = *c.engine;
+  // mbx_combine=rccl over a GROUP BY on one integer key: the partials stay on
+  // their devices for GroupRcclCombine (each shard reads back only its key range)
+  rc::CombineDesc gcd;
+  const bool grp_rccl = GroupRcclEligible(c, s, p, gcd);
+  std::vector<DRel> rel(grp_rccl ? nsh : 0);
+  std::vector<std::array<long long, 3>> kr(nsh, std::array<long long, 3>{0, 0, 0});
   ForShards(c, [&](int i) {
     Connection &sc = *c.shards[i];
     Engine &se = ShardEngine(c, sc);
@@ -4288,10 +4538,31 @@ static void ShardedAggregateRows(Connection &c, const BoundSelect &s, const Boun
     pi.src.table = t.parts[i];
     DRel r = RunBranch(se, sc, pi);
     MarkLaunched(c, i);
+    if (grp_rccl) {
+      if (r.n > 0) {
+        long long *o3 = (long long *)((char *)se.d_small + 3072);
+        dev::KeyRange(r.cols[0].data, r.cols[0].phys, r.cols[0].validity, r.n, o3, se.stream);
+        HIPCHK(hipMemcpyAsync(se.h_pinned, o3, 24, hipMemcpyDeviceToHost, se.stream));
+        HIPCHK(hipStreamSynchronize(se.stream));
+        memcpy(kr[i].data(), se.h_pinned, 24);
+      }
+      rel[i] = std::move(r);
+      return;
+    }
     partial[i] = ToHost(se, r, pi.names, 0, -1, pi.names.size());  // synchronises and raises device errors
     ShardCollect(e, se, i, true);
   });
   Eng(c);
+  if (grp_rccl) {
+    if (GroupRcclCombine(c, s, p, first, gcd, rel, kr, rows, types)) return;
+    // the host merge of the same partials
+    ForShards(c, [&](int i) {
+      Engine &se = Eng(*c.shards[i]);
+      partial[i] = ToHost(se, rel[i], p.names, 0, -1, p.names.size());
+      ShardCollect(e, se, i, true);
+    });
+    Eng(c);
+  }
   c.shard_stats.last_partials = partial;
   const auto t_merge = std::chrono::steady_clock::now();
   if (MergeIntKeys(s, first, partial, ng, rows, types)) {

@@ -14,6 +14,8 @@
 
 #include "phys.h"
 
+#include <algorithm>
+
 namespace mbx {
 namespace rc {
 
@@ -240,25 +242,31 @@ std::string SelfTest(int device, double *us) {
   return err;
 }
 
+// element i of an integer column widened to int128 {lo, hi}
+__device__ __forceinline__ void widen(uint8_t phys, const void *p, int64_t i, int64_t &lo, int64_t &hi) {
+  bool unsigned_ = false;
+  switch (phys) {
+    case P_U8: lo = ((const uint8_t *)p)[i], unsigned_ = true; break;
+    case P_I8: lo = ((const int8_t *)p)[i]; break;
+    case P_I16: lo = ((const int16_t *)p)[i]; break;
+    case P_U16: lo = ((const uint16_t *)p)[i], unsigned_ = true; break;
+    case P_I32: lo = ((const int32_t *)p)[i]; break;
+    case P_U32: lo = ((const uint32_t *)p)[i], unsigned_ = true; break;
+    case P_U64: lo = ((const int64_t *)p)[i], unsigned_ = true; break;  // (zero-extended below)
+    case P_I128:
+      lo = ((const int64_t *)p)[2 * i], hi = ((const int64_t *)p)[2 * i + 1];
+      return;
+    default: lo = ((const int64_t *)p)[i]; break;
+  }
+  hi = unsigned_ ? 0 : (lo < 0 ? -1 : 0);
+}
+
 // one lane group per column: row 0's value widened to int128, its validity
 __global__ void pack_lanes_kernel(PackDesc d, int64_t *dst) {
   const int j = threadIdx.x;
   if (j < d.ncols) {
-    const void *p = d.data[j];
     int64_t lo = 0, hi = 0;
-    switch (d.phys[j]) {
-      case P_U8: lo = *(const uint8_t *)p; break;
-      case P_I8: lo = *(const int8_t *)p; break;
-      case P_I16: lo = *(const int16_t *)p; break;
-      case P_U16: lo = *(const uint16_t *)p; break;
-      case P_I32: lo = *(const int32_t *)p; break;
-      case P_U32: lo = *(const uint32_t *)p; break;
-      case P_U64: lo = *(const int64_t *)p; break;  // (zero-extended below)
-      case P_I128: lo = ((const int64_t *)p)[0], hi = ((const int64_t *)p)[1]; break;
-      default: lo = *(const int64_t *)p; break;
-    }
-    if (d.phys[j] != P_I128 && d.phys[j] != P_U64 && d.phys[j] != P_U8 && d.phys[j] != P_U16 && d.phys[j] != P_U32)
-      hi = lo < 0 ? -1 : 0;
+    widen(d.phys[j], d.data[j], 0, lo, hi);
     const bool ok = !d.valid[j] || (d.valid[j][0] & 1);
     if (d.counts_only) {
       dst[j] = ok ? lo : 0;
@@ -282,6 +290,58 @@ __global__ void combine_lanes_kernel(CombineDesc d, const int64_t *g, int64_t *o
 
 void Combine(const CombineDesc &d, const int64_t *gathered, int64_t *out, hipStream_t s) {
   hipLaunchKernelGGL(combine_lanes_kernel, dim3(1), dim3(64), 0, s, d, gathered, out);
+}
+
+// one thread per partial GROUP BY row: its slot's presence lane and column
+// lanes (the block was zeroed, so absent slots stay {0, 0, invalid})
+__global__ void pack_rows_kernel(PackRowsDesc d, int64_t *dst) {
+  const int64_t sl_lanes = SlotLanes(d.ncols);
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < d.nrows; i += (int64_t)gridDim.x * blockDim.x) {
+    int64_t klo = 0, khi = 0;
+    widen(d.key_phys, d.key, i, klo, khi);
+    const bool knull = d.key_valid && !((d.key_valid[i >> 6] >> (i & 63)) & 1);
+    const int64_t slot = knull ? d.nslot - 1 : klo - d.kmin;
+    if (slot < 0 || slot >= d.nslot) continue;  // (the host derived kmin / nslot from these keys)
+    int64_t *o = dst + slot * sl_lanes;
+    o[0] = 1;
+    for (int j = 0; j < d.ncols; j++) {
+      int64_t lo = 0, hi = 0;
+      widen(d.phys[j], d.data[j], i, lo, hi);
+      const bool ok = !d.valid[j] || ((d.valid[j][i >> 6] >> (i & 63)) & 1);
+      o[1 + 3 * j] = ok ? lo : 0;
+      o[2 + 3 * j] = ok ? hi : 0;
+      o[3 + 3 * j] = ok ? 1 : 0;
+    }
+  }
+  if (blockIdx.x == 0 && threadIdx.x == 0) dst[d.nslot * sl_lanes] = d.err ? *d.err : 0;
+}
+
+void PackRows(const PackRowsDesc &d, int64_t *dst, hipStream_t s) {
+  const int64_t lanes = d.nslot * SlotLanes(d.ncols) + 1;
+  (void)hipMemsetAsync(dst, 0, (size_t)lanes * 8, s);
+  const int64_t blocks = std::max<int64_t>(1, std::min<int64_t>((d.nrows + 255) / 256, 1024));
+  hipLaunchKernelGGL(pack_rows_kernel, dim3((unsigned)blocks), dim3(256), 0, s, d, dst);
+}
+
+// one thread per slot: presence ORed over the ranks, every column combined as
+// the global combine does; then every rank's error word after the slots
+__global__ void combine_slots_kernel(CombineDesc d, int64_t nslot, const int64_t *g, int64_t *out) {
+  const int64_t sl_lanes = SlotLanes(d.ncols), stride = nslot * sl_lanes + 1;
+  for (int64_t sl = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; sl < nslot; sl += (int64_t)gridDim.x * blockDim.x) {
+    int64_t present = 0;
+    for (int r = 0; r < d.nranks; r++) present |= g[(int64_t)r * stride + sl * sl_lanes];
+    int64_t *o = out + sl * sl_lanes;
+    o[0] = present;
+    for (int j = 0; j < d.ncols; j++)
+      CombineColumn(g + sl * sl_lanes + 1, d.nranks, (int)stride, j, d.kind[j], o + 1 + 3 * j);
+  }
+  if (blockIdx.x == 0 && threadIdx.x < d.nranks)
+    out[nslot * sl_lanes + threadIdx.x] = g[(int64_t)threadIdx.x * stride + stride - 1];
+}
+
+void CombineSlots(const CombineDesc &d, int64_t nslot, const int64_t *gathered, int64_t *out, hipStream_t s) {
+  const int64_t blocks = std::max<int64_t>(1, std::min<int64_t>((nslot + 255) / 256, 64));
+  hipLaunchKernelGGL(combine_slots_kernel, dim3((unsigned)blocks), dim3(256), 0, s, d, nslot, gathered, out);
 }
 
 }  // namespace rc

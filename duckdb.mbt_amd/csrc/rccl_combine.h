@@ -76,5 +76,26 @@ struct CombineDesc {
 };
 void Combine(const CombineDesc &d, const int64_t *gathered, int64_t *out, hipStream_t s);
 
+// GROUP BY on one integer key: a rank's partial relation (nrows groups) packed
+// into dense key slots -- slot = key - kmin, the NULL key in slot nslot - 1 --
+// each SlotLanes(ncols) lanes {present, then {lo, hi, valid} per column}, the
+// device error word after the last slot (nslot * SlotLanes + 1 lanes; PackRows
+// zeroes the block first, so a group the rank lacks stays absent)
+struct PackRowsDesc {
+  const void *key;
+  const uint64_t *key_valid;
+  const void *data[kMaxCols];
+  const uint64_t *valid[kMaxCols];
+  uint8_t phys[kMaxCols];
+  uint8_t key_phys;
+  int ncols;
+  int64_t nrows, kmin, nslot;
+  const int32_t *err;
+};
+void PackRows(const PackRowsDesc &d, int64_t *dst, hipStream_t s);
+// out[slot * SlotLanes ..] = the slot over the nranks gathered blocks (presence
+// ORed, columns as CombineColumn), then every rank's error word
+void CombineSlots(const CombineDesc &d, int64_t nslot, const int64_t *gathered, int64_t *out, hipStream_t s);
+
 }  // namespace rc
 }  // namespace mbx

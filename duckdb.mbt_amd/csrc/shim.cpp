@@ -1771,14 +1771,15 @@ char *duckdb_mbx_rccl_note(duckdb_mb_connection *h) {
 
 // mbx_combine counters, up to cap of {RCCL combines, fallbacks to the host
 // merge, combines through the test loopback, combines that raised a shard's
-// device error, collectives aborted after the timeout}; returns how many were
-// written.
+// device error, collectives aborted after the timeout, combines of GROUP BY
+// relations}; returns how many were written.
 int32_t duckdb_mbx_rccl_stats_ex(duckdb_mb_connection *h, int64_t *out, int32_t cap) {
   if (!h || !out) return 0;
   const ShardStats &st = h->conn.shard_stats;
-  const int64_t v[5] = {st.rccl_combines, st.rccl_fallbacks, st.rccl_loopbacks, st.rccl_errors, st.rccl_timeouts};
+  const int64_t v[6] = {st.rccl_combines,  st.rccl_fallbacks, st.rccl_loopbacks,
+                        st.rccl_errors,    st.rccl_timeouts,  st.rccl_group_combines};
   int32_t n = 0;
-  for (; n < cap && n < 5; n++) out[n] = v[n];
+  for (; n < cap && n < 6; n++) out[n] = v[n];
   return n;
 }
 

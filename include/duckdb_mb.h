@@ -333,8 +333,9 @@ int32_t duckdb_mbx_rccl_stats(duckdb_mb_connection *connection, int64_t *out2, d
 char *duckdb_mbx_rccl_note(duckdb_mb_connection *connection);
 /* Up to cap of {RCCL combines, host-merge fallbacks, combines through the test
  * loopback, combines that raised a shard's device error, collectives aborted
- * after MBX_RCCL_TIMEOUT_MS (default 20 s; the host merge answers)}; returns
- * the count written. */
+ * after MBX_RCCL_TIMEOUT_MS (default 20 s; the host merge answers), combines
+ * of GROUP BY relations (one integer key: dense key slots all-gathered)};
+ * returns the count written. */
 int32_t duckdb_mbx_rccl_stats_ex(duckdb_mb_connection *connection, int64_t *out, int32_t cap);
 /* 1: RCCL combine, 0: host merge, from the next statement on; 2: the RCCL
  * combine with its collectives replaced by device copies (tests only: refused

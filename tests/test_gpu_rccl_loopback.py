@@ -176,10 +176,10 @@ def test_rccl_without_distinct_devices_falls_back_with_note(mbx, oracle):
     assert st["rccl_combines"] == st0["rccl_combines"]
     assert st["rccl_fallbacks"] == st0["rccl_fallbacks"] + 1
     assert "not distinct" in st["note"] or "librccl" in st["note"], st
-    # shapes the RCCL combine does not cover say so too (GROUP BY, DOUBLE SUM)
+    # shapes the RCCL combine does not cover say so too (a DOUBLE key, DOUBLE SUM)
     c.set_combine("rccl_loopback")
-    q(c, "SELECT x % 3 AS g, COUNT(*) FROM t GROUP BY g")
-    assert "GROUP BY" in c.rccl_stats()["note"]
+    q(c, "SELECT x / 2 AS g, COUNT(*) FROM t GROUP BY g")
+    assert "not an integer" in c.rccl_stats()["note"], c.rccl_stats()
     q(c, "SELECT SUM(x / 2) FROM t")
     assert "floating-point" in c.rccl_stats()["note"]
     c.close()
@@ -195,3 +195,101 @@ def test_rccl_library_calls_on_one_gpu(mbx):
     assert r["ok"], r
     # twice: a second communicator in the same process
     assert mbx.rccl_selftest(0)["ok"]
+
+
+def _group_both(c, sql):
+    """A GROUP BY under the loopback RCCL combine (dense key slots) and under
+    the host merge of the same connection: the same rows, in key order."""
+    st0 = c.rccl_stats()
+    got = q(c, sql).rows
+    st = c.rccl_stats()
+    assert st["note"] == "" and st["rccl_group_combines"] - st0["rccl_group_combines"] == 1, (sql, st)
+    c.set_combine("host")
+    ref = q(c, sql).rows
+    c.set_combine("rccl_loopback")
+    assert got == ref, (sql, got[:5], ref[:5])
+    return got
+
+
+@pytest.mark.parametrize("devices", ["0,0", "0,0,0"])
+def test_rccl_loopback_group_by_c3_shape(mbx, oracle, devices):
+    """C3 over sharded parts: each shard's 32 groups packed into dense key
+    slots, all-gathered, combined on device 0; every group's COUNT and exact
+    int128 SUM against the oracle, and every shard's partial against its range."""
+    n = 40_000_003
+    c = _conn(mbx, devices)
+    q(c, f"CREATE TABLE g AS SELECT CAST(mbx_synth(7, i, 32) AS INTEGER) AS k, "
+         f"mbx_synth(9, i, 1099511627776) - 549755813888 AS v FROM range({n}) tbl(i)")
+    oc, osum = oracle.synth_groupby(7, 9, 0, n, 32, 1 << 40, -(1 << 39), 8)
+    rows = _group_both(c, "SELECT k, SUM(v), COUNT(*) FROM g GROUP BY k")
+    assert rows == [[str(k), str(osum[k]), str(oc[k])] for k in range(32) if oc[k]]
+    nsh = devices.count(",") + 1
+    for i in range(nsh):
+        lo, hi = n * i // nsh, n * (i + 1) // nsh
+        pc, ps = oracle.synth_groupby(7, 9, lo, hi - lo, 32, 1 << 40, -(1 << 39), 8)
+        part = c.shard_partial(i)
+        got, _ = part.cells()
+        part.close()
+        assert sorted((int(r[0]), int(r[1]), int(r[2])) for r in got) == \
+            [(k, int(ps[k]), int(pc[k])) for k in range(32) if pc[k]], i
+    # HAVING / ORDER BY / LIMIT over the combined groups
+    top = q(c, "SELECT k, COUNT(*) AS n FROM g GROUP BY k HAVING COUNT(*) > 0 ORDER BY n DESC, k LIMIT 3").rows
+    exp = sorted(((int(oc[k]), k) for k in range(32)), key=lambda t: (-t[0], t[1]))[:3]
+    assert top == [[str(k), str(cn)] for cn, k in exp]
+    c.close()
+
+
+def test_rccl_loopback_group_by_nulls_sparse_keys(mbx):
+    """Negative keys, a NULL key group, keys present on one shard only,
+    MIN / MAX / AVG / COUNT(col) with NULL values, DECIMAL sums; against numpy
+    and the host merge."""
+    n = 3_000_000
+    c = _conn(mbx, "0,0,0")
+    q(c, f"CREATE TABLE s AS SELECT CASE WHEN i % 97 = 0 THEN NULL "
+         f"WHEN i >= 2000000 THEN 100 + i % 5 ELSE i % 13 - 6 END AS k, "
+         f"CASE WHEN i % 11 = 0 THEN NULL ELSE i - 1500000 END AS v, "
+         f"CAST(i % 1000 AS DECIMAL(12,2)) AS d FROM range({n}) tbl(i)")
+    i = np.arange(n, dtype=np.int64)
+    knull = i % 97 == 0
+    k = np.where(i >= 2_000_000, 100 + i % 5, i % 13 - 6)
+    vnull = i % 11 == 0
+    v = i - 1_500_000
+    d = i % 1000
+    rows = _group_both(c, "SELECT k, COUNT(*), COUNT(v), SUM(v), MIN(v), MAX(v), SUM(d) FROM s GROUP BY k")
+    keys = sorted(set(k[~knull].tolist()))
+    exp = []
+    for kk in keys + [None]:
+        m = knull if kk is None else (~knull & (k == kk))
+        mv = m & ~vnull
+        vs = v[mv]
+        exp.append(["" if kk is None else str(kk), str(int(m.sum())), str(int(mv.sum())),
+                    str(int(vs.sum())) if vs.size else "", str(vs.min()) if vs.size else "",
+                    str(vs.max()) if vs.size else "", f"{int(d[m].sum())}.00"])
+    assert rows == exp
+    avg = _group_both(c, "SELECT k, AVG(v) FROM s GROUP BY k")
+    for row, kk in zip(avg, keys + [None]):
+        m = (knull if kk is None else (~knull & (k == kk))) & ~vnull
+        assert abs(float(row[1]) - v[m].mean()) <= 1e-9 * max(1.0, abs(v[m].mean())), (kk, row)
+    c.close()
+
+
+def test_rccl_loopback_group_by_wide_keys_and_errors(mbx):
+    """A key range wider than 4096 slots takes the host merge of the same
+    partials (with its note); an overflow on one shard's partial is raised
+    naming the shard, and the next GROUP BY on the connection is exact."""
+    c = _conn(mbx, "0,0")
+    q(c, "CREATE TABLE w AS SELECT i * 7 AS k, i AS x FROM range(10000) tbl(i)")
+    st0 = c.rccl_stats()
+    rows = q(c, "SELECT k, COUNT(*) FROM w GROUP BY k").rows
+    assert len(rows) == 10000 and rows[0] == ["0", "1"] and rows[-1] == [str(9999 * 7), "1"]
+    st = c.rccl_stats()
+    assert "wider than 4096" in st["note"] and st["rccl_group_combines"] == st0["rccl_group_combines"], st
+    m = 9_220_000_000_000_000
+    q(c, "CREATE TABLE o AS SELECT i % 4 AS k, i AS x FROM range(2000) tbl(i)")
+    r = c.query(f"SELECT k, SUM(x * {m}) FROM o GROUP BY k")
+    assert not hasattr(r, "value"), r
+    assert "Overflow" in r.error.message and "shard 1" in r.error.message, r.error.message
+    got = q(c, "SELECT k, SUM(x), COUNT(*) FROM o GROUP BY k").rows
+    assert got == [[str(kk), str(sum(range(kk, 2000, 4))), "500"] for kk in range(4)]
+    assert c.rccl_stats()["note"] == ""
+    c.close()
