@@ -508,6 +508,66 @@ int main(int argc, char **argv) {
     RUN2(2, 0, 1)
     return 0;
   }
+  if (argc > 2 && (argv[2][0] == 'c' || argv[2][0] == 'g')) {
+    // round 5: GB-scale offsets of the value array from the key array inside
+    // ONE allocation -- physically contiguous ('c', hipDeviceMallocContiguous)
+    // or a plain hipMalloc ('g') -- each delta timed twice, interleaved
+    unsigned char *big;
+    const size_t kb = (size_t)nsteps * 1024, vb = (size_t)nsteps * 2048, slack = (size_t)4 << 30;
+    if (argv[2][0] == 'c') CK(hipExtMallocWithFlags((void **)&big, kb + vb + slack, hipDeviceMallocContiguous));
+    else CK(hipMalloc((void **)&big, kb + vb + slack));
+    hipLaunchKernelGGL(fill_keys, dim3(4096), dim3(256), 0, 0, (int *)big, nsteps * 256);
+    const size_t M = 1 << 20;
+    const size_t deltas[] = {0, 4096, 64 << 10, 1 * M, 2 * M, 6 * M, 64 * M, 96 * M, 256 * M, 512 * M + 4 * M,
+                             1024 * M, 1536 * M, 2048 * M, 3072 * M + 2 * M, 4095 * M};
+    size_t lds = 24576 + 4 * 2 * 3072;
+    CK(hipFuncSetAttribute((const void *)two_stream<2, 0>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+    CK(hipFuncSetAttribute((const void *)two_stream<2, 1>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+    for (int rep = 0; rep < 2; rep++)
+      for (size_t dv : deltas) {
+        long long *vv = (long long *)(big + kb + dv);
+        CK(hipMemset(vv, 2, vb));
+        float ms = TimeIt([&] { hipLaunchKernelGGL((two_stream<2, 0>), dim3(cus), dim3(256), lds, 0, (int *)big, vv, nsteps, out); }, 9);
+        float ma = TimeIt([&] { hipLaunchKernelGGL((two_stream<2, 1>), dim3(cus), dim3(256), lds, 0, (int *)big, vv, nsteps, out); }, 9);
+        printf("%s rep %d delta_MiB %9.3f  stream %.4f ms  with_atomics %.4f ms  %.0f GB/s\n", argv[2][0] == 'c' ? "contig" : "malloc",
+               rep, dv / (double)M, ms, ma, bytes / ms / 1e6);
+        fflush(stdout);
+      }
+    return 0;
+  }
+  if (argc > 2 && argv[2][0] == 'r') {
+    // round 5: separate allocations as the engine makes them, re-made 8 times
+    // with a filler of varying size allocated first (placement varies)
+    size_t lds = 24576 + 4 * 2 * 3072;
+    CK(hipFuncSetAttribute((const void *)two_stream<2, 0>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+    CK(hipFree(k));
+    CK(hipFree(v));
+    CK(hipFree(one));
+    for (int rep = 0; rep < 8; rep++) {
+      void *fill = nullptr;
+      const size_t fb = ((size_t)(rep * 3 % 8) << 30) + ((size_t)rep << 21);
+      if (fb) CK(hipMalloc(&fill, fb));
+      int *k2;
+      long long *v2;
+      if (rep & 1) {
+        CK(hipMalloc(&v2, nsteps * 2048));
+        CK(hipMalloc(&k2, nsteps * 1024));
+      } else {
+        CK(hipMalloc(&k2, nsteps * 1024));
+        CK(hipMalloc(&v2, nsteps * 2048));
+      }
+      hipLaunchKernelGGL(fill_keys, dim3(4096), dim3(256), 0, 0, k2, nsteps * 256);
+      CK(hipMemset(v2, 2, nsteps * 2048));
+      float ms = TimeIt([&] { hipLaunchKernelGGL((two_stream<2, 0>), dim3(cus), dim3(256), lds, 0, k2, v2, nsteps, out); }, 9);
+      printf("separate rep %d filler_GiB %.3f order %s  k %p v %p  stream %.4f ms  %.0f GB/s\n", rep, fb / 1073741824.0,
+             rep & 1 ? "v,k" : "k,v", (void *)k2, (void *)v2, ms, bytes / ms / 1e6);
+      fflush(stdout);
+      CK(hipFree(k2));
+      CK(hipFree(v2));
+      if (fill) CK(hipFree(fill));
+    }
+    return 0;
+  }
   if (argc > 2 && argv[2][0] == 'l') {
     RUNLC(4, 4) RUNLC(6, 4) RUNLC(4, 8) RUNLC(6, 8) RUNLC(8, 8) RUNLC(6, 12)
     RUN2(2, 0, 1) RUN2(2, 2, 3)
