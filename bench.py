@@ -60,7 +60,20 @@ def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
+def guard_stdout():
+    """The contract's stdout carries the JSON line only.  Libraries in this
+    process may write to file descriptor 1 themselves (RCCL prints its version
+    banner when a communicator is created, e.g. by the in-library combine); so
+    fd 1 is pointed at stderr, and Python's sys.stdout -- where the JSON line is
+    printed -- keeps a private duplicate of the original stdout."""
+    sys.stdout.flush()
+    out = os.fdopen(os.dup(1), "w", buffering=1)
+    os.dup2(2, 1)
+    sys.stdout = out
+
+
 def main():
+    guard_stdout()
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--shards-per-gpu", type=int, default=1,

@@ -173,3 +173,15 @@ def test_guarded_leg_times_out_and_reports():
     assert bench.guarded(lambda: {"ok": 1}, 5) == {"ok": 1}
     r = bench.guarded(lambda: 1 // 0, 5)
     assert "division" in r["error"]
+
+
+def test_stdout_carries_only_the_json_line():
+    """Anything a library in the bench process writes to fd 1 (RCCL prints its
+    version banner when a communicator is created) lands on stderr; the JSON
+    line printed through sys.stdout is the only thing on stdout."""
+    code = ("import os, sys, json; sys.path.insert(0, %r); import bench; bench.guard_stdout(); "
+            "os.write(1, b'RCCL version : x\\n'); print(json.dumps({'metric': 'm', 'value': 1}), flush=True)" % ROOT)
+    p = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=120)
+    assert p.returncode == 0, p.stderr
+    assert p.stdout.strip().splitlines() == ['{"metric": "m", "value": 1}'], p.stdout
+    assert "RCCL version" in p.stderr
