@@ -1,3 +1,6 @@
+# Round-5 A/B of the C2 emit folded into filter_agg_lds (HISTORY.md, Round 5): the
+# build under test had MBX_FA_NOFUSE (experiments only) to switch the fold off; the fold
+# was reverted after this A/B, so on the current tree both modes run the same code.
 set -o pipefail
 mkdir -p gpurun_out/fuse
 timeout -k 10 600 python -u -m pytest tests/test_gpu_hotpath.py tests/test_gpu_fixtures.py tests/test_gpu_sharded.py tests/test_gpu_rccl_loopback.py -m gpu -x -q --timeout 300 --timeout-method thread > gpurun_out/fuse/tests.log 2>&1 || exit 11
