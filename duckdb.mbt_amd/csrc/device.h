@@ -102,12 +102,31 @@ struct GroupPreds {
   int32_t xcd;  // group_direct_lds: 1 = XCD-grouped step windows (blocks b, b+8, ... share an XCD)
   GroupPred p[GROUP_MAX_PRED];
 };
-// false only when a predicate was given and the shape needs the segmented kernel
+// Per-workgroup partial records of group_direct_lds (key-major, GroupPartialWords
+// u64 each: COUNT(*), valid-row count, then per value column sum lo / hi and,
+// with MIN/MAX, min / max), reduced by GroupPartialsCompact.
+constexpr int kGroupPartialKeys = 128;
+__host__ __device__ constexpr int GroupPartialWords(int nv, bool mm) { return 2 + nv * (mm ? 4 : 2); }
+struct GroupPartialsOut {
+  void *buf;            // room for the records
+  size_t bytes;
+  int64_t state_slots;  // AggStates at st0 (st1 follows st0) that the call initialises when it uses atomics
+  bool used;            // set: the records were written (GroupPartialsCompact must follow)
+  int blocks;           // set: workgroups that wrote records
+};
+// The records reduced into cstar / st0 / st1 for every key (empty keys as
+// initialised), then the non-empty keys compacted as CompactSlots does.
+void GroupPartialsCompact(const GroupPartialsOut &po, int nv, bool mm, int nk, unsigned long long *count_star,
+                          AggState *st0, AggState *st1, int32_t *slot_list, int64_t *n_out, hipStream_t s);
+// false only when a predicate was given and the shape needs the segmented kernel.
+// po: the caller did not initialise cstar / st0 / st1: the call does (atomic
+// forms) or writes per-workgroup records instead (po->used).
 bool GroupByDirectStates(const void *kcol, int kphys, int64_t kmin, int nk, const void *v0, const void *v1, int vphys,
                          int nv, bool mm, int64_t nrows, int64_t seg_rows, int R, unsigned long long *cstar,
                          AggState *st0, AggState *st1, int grid_blocks, hipStream_t s,
                          const GroupPreds *pred = nullptr, uint64_t vmaxabs = ~0ull /* (unused) */,
-                         const uint64_t *v0valid = nullptr);  // v0's validity words (nv == 1): false if unsupported
+                         const uint64_t *v0valid = nullptr,   // v0's validity words (nv == 1): false if unsupported
+                         GroupPartialsOut *po = nullptr);
 
 // --- generic aggregation over compacted columns ---------------------------
 // vclass: VC_I64 / VC_I128 / VC_F64 of the input column (phys given)

@@ -2237,7 +2237,18 @@ static DRel Aggregate(Engine &e, const DRel &src, const BoundSelect &s) {
           auto cs = Alloc(e, nslots * 8);
           auto sb = Alloc(e, 2 * st_bytes);
           dev::AggState *const s0p = (dev::AggState *)sb->p, *const s1p = s0p + nslots;
-          dev::InitAggStatesCounts(s0p, 2 * nslots, (unsigned long long *)cs->p, nslots, e.stream);
+          // GroupByDirectStates initialises the states for its atomic forms, or
+          // has every workgroup write a record of its table (up to
+          // kGroupPartialKeys keys) that GroupPartialsCompact reduces
+          DevBufPtr gparts;
+          dev::GroupPartialsOut po;
+          memset(&po, 0, sizeof(po));
+          po.state_slots = 2 * nslots;
+          if (nk <= dev::kGroupPartialKeys) {
+            po.bytes = (size_t)nk * dev::NumCUs() * 3 * dev::GroupPartialWords(2, true) * 8;
+            gparts = Alloc(e, po.bytes);
+            po.buf = gparts->p;
+          }
           Phys vphys = nv ? src.cols[vcols[0]].phys : P_I64;
           double bytes = (double)src.n * PhysSize(K.phys);
           for (int c : vcols) bytes += (double)src.n * PhysSize(src.cols[c].phys);
@@ -2262,11 +2273,15 @@ static DRel Aggregate(Engine &e, const DRel &src, const BoundSelect &s) {
                                                 nv > 1 ? src.cols[vcols[1]].data : nullptr, vphys, nv, mm, src.n, seg,
                                                 R, (unsigned long long *)cs->p, s0p,
                                                 s1p, 0, e.stream, gp.n ? &gp : nullptr,
-                                                maxabs < ((i128)1 << 62) ? (uint64_t)maxabs : ~0ull, vvalid);
+                                                maxabs < ((i128)1 << 62) ? (uint64_t)maxabs : ~0ull, vvalid, &po);
           }
           if (!launched) goto generic;
           auto list = Alloc(e, nslots * 4);
-          dev::CompactSlots((const unsigned long long *)cs->p, nslots, (int32_t *)list->p, e.d_scratch, e.stream);
+          if (po.used)
+            dev::GroupPartialsCompact(po, nv, mm, nk, (unsigned long long *)cs->p, s0p, s1p, (int32_t *)list->p,
+                                      e.d_scratch, e.stream);
+          else
+            dev::CompactSlots((const unsigned long long *)cs->p, nslots, (int32_t *)list->p, e.d_scratch, e.stream);
           // outputs sized for every slot (<= 1024 rows): the emit reads the group
           // count from the device, so the query waits on the stream once, after it
           dev::EmitDesc D;

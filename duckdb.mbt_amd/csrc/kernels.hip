@@ -1699,7 +1699,8 @@ __global__ __launch_bounds__(256) void group_direct_lds_kernel(const TK *__restr
                                                                int nk, int R, size_t ring_off,
                                                                unsigned long long *cstar, AggState *st0,
                                                                AggState *st1, GroupPreds pr,
-                                                               const uint64_t *__restrict__ vvalid) {
+                                                               const uint64_t *__restrict__ vvalid,
+                                                               unsigned long long *gpart) {
   static_assert(!VV || NV == 1, "validity: one value column");
   extern __shared__ __attribute__((aligned(16))) unsigned char lds_raw[];
   constexpr int KB = 256 * (int)sizeof(TK), VB = 256 * (int)sizeof(TV);  // bytes per step
@@ -1898,6 +1899,27 @@ __global__ __launch_bounds__(256) void group_direct_lds_kernel(const TK *__restr
       }
     }
     if (!VV) vc = c;
+    if (gpart) {
+      // this workgroup's record of key kq (key-major: group_partials_compact
+      // reads one key's records contiguously); no global atomics
+      unsigned long long *o = gpart + ((size_t)kq * gridDim.x + blockIdx.x) * GroupPartialWords(NV, MM);
+      o[0] = c;
+      o[1] = vc;
+      int f = 2;
+      if (NV >= 1) {
+        int64_t lo, hi;
+        sp128(s0, lo, hi);
+        o[f++] = (unsigned long long)lo; o[f++] = (unsigned long long)hi;
+        if (MM) { o[f++] = (unsigned long long)a0; o[f++] = (unsigned long long)b0; }
+      }
+      if (NV >= 2) {
+        int64_t lo, hi;
+        sp128(s1, lo, hi);
+        o[f++] = (unsigned long long)lo; o[f++] = (unsigned long long)hi;
+        if (MM) { o[f++] = (unsigned long long)a1; o[f++] = (unsigned long long)b1; }
+      }
+      continue;
+    }
     if (c) atomicAdd(&cstar[kq], c);
     if (vc) {
       Acc A;
@@ -1939,10 +1961,19 @@ size_t GroupDirectLds(int nk, int R, int nv, bool mm, bool vv) {
 bool GroupByDirectStates(const void *kcol, int kphys, int64_t kmin, int nk, const void *v0, const void *v1, int vphys,
                          int nv, bool mm, int64_t nrows, int64_t seg_rows, int R, unsigned long long *cstar,
                          AggState *st0, AggState *st1, int grid_blocks, hipStream_t s, const GroupPreds *pred,
-                         uint64_t vmaxabs, const uint64_t *v0valid) {
+                         uint64_t vmaxabs, const uint64_t *v0valid, GroupPartialsOut *po) {
   const bool vv = v0valid != nullptr;
   if (vv && nv != 1) return false;
-  if (nrows <= 0) return true;
+  if (po) po->used = false;
+  // with po, the states are this call's to initialise: the atomic forms below
+  // need them zeroed first, the partials form writes every one at the end
+  auto init_states = [&] {
+    if (po) InitAggStatesCounts(st0, po->state_slots, cstar, nk, s);
+  };
+  if (nrows <= 0) {
+    init_states();
+    return true;
+  }
   GroupPreds pr;
   memset(&pr, 0, sizeof(pr));
   if (pred) pr = *pred;
@@ -1996,15 +2027,26 @@ bool GroupByDirectStates(const void *kcol, int kphys, int64_t kmin, int nk, cons
       }
       // one flush at the end must be overflow-safe (else the segmented kernel)
       const bool one_flush = seg_rows <= 0 || seg_rows >= rows_per_block;
+      // per-workgroup records reduced by group_partials_compact instead of the
+      // flush's global atomics (every workgroup hitting the same nk states at
+      // once): up to kGroupPartialKeys keys, when the caller gave room
+      unsigned long long *gpart = nullptr;
+      if (po && one_flush && lds <= lds_cap && nk <= kGroupPartialKeys &&
+          (size_t)nk * grid * GroupPartialWords(nv, mm) * 8 <= po->bytes && !Knob("MBX_GD_ATOMIC_FLUSH")) {
+        gpart = (unsigned long long *)po->buf;
+        po->used = true;
+        po->blocks = grid;
+      }
       if (vv) {  // NULL-able value column: one flush only
         if (!one_flush || lds > lds_cap) return false;
+        if (!gpart) init_states();
 #define GLVV(TK, TV, MM, D)                                                                                         \
   {                                                                                                                 \
     (void)hipFuncSetAttribute((const void *)group_direct_lds_kernel<TK, TV, 1, MM, D, true>,                        \
                               hipFuncAttributeMaxDynamicSharedMemorySize, 150 * 1024);                              \
     hipLaunchKernelGGL((group_direct_lds_kernel<TK, TV, 1, MM, D, true>), dim3(grid), dim3(256), lds, s,           \
                        (const TK *)kcol, (const TV *)v0, (const TV *)v1, nrows, kmin, nk, R, ring_off, cstar, st0,  \
-                       st1, pr, v0valid);                                                                           \
+                       st1, pr, v0valid, gpart);                                                                    \
   }
 #define GLVVD(TK, TV)                                                                                             \
   if (mm) { if (depth == 2) GLVV(TK, TV, true, 2) else GLVV(TK, TV, true, 3) }                                      \
@@ -2020,13 +2062,14 @@ bool GroupByDirectStates(const void *kcol, int kphys, int64_t kmin, int nk, cons
         return true;
       }
       if (one_flush && lds <= lds_cap) {
+        if (!gpart) init_states();
 #define GL(TK, TV, NV, MM, D)                                                                                      \
   if (lds > 64 * 1024) /* deep rings at one or two blocks per CU */                                               \
     (void)hipFuncSetAttribute((const void *)group_direct_lds_kernel<TK, TV, NV, MM, D, false>,                     \
                               hipFuncAttributeMaxDynamicSharedMemorySize, 150 * 1024);                             \
   hipLaunchKernelGGL((group_direct_lds_kernel<TK, TV, NV, MM, D, false>), dim3(grid), dim3(256), lds, s,           \
                      (const TK *)kcol, (const TV *)v0, (const TV *)v1, nrows, kmin, nk, R, ring_off, cstar, st0,   \
-                     st1, pr, (const uint64_t *)nullptr);
+                     st1, pr, (const uint64_t *)nullptr, gpart);
 #define GLD(TK, TV, NV, MM)                                                                     \
   if (depth == 2) { GL(TK, TV, NV, MM, 2) } else if (depth == 3) { GL(TK, TV, NV, MM, 3) }      \
   else if (depth == 4) { GL(TK, TV, NV, MM, 4) } else if (depth == 6) { GL(TK, TV, NV, MM, 6) } \
@@ -2049,6 +2092,7 @@ bool GroupByDirectStates(const void *kcol, int kphys, int64_t kmin, int nk, cons
     }
   }
   if (pr.n) return false;  // a predicate needs the LDS-DMA kernel
+  init_states();
   int grid = grid_blocks > 0 ? grid_blocks : NumCUs() * 4;
   int64_t chunk = (nrows + grid - 1) / grid;
   chunk = (chunk + 3) & ~(int64_t)3;
@@ -2422,6 +2466,89 @@ __global__ void slot_scatter_kernel(const int32_t *flag, const int32_t *pos, int
 
 // Ordered list of the non-empty slots.  One workgroup for small tables; a
 // device-wide scan (flags -> hipCUB exclusive sum -> scatter) for large ones.
+// The group_direct_lds partials of nb workgroups reduced per key (one wave per
+// key at a time, its lanes over the records, carry-correct int128 sums), every
+// key's state and COUNT(*) slot written (empty keys as the initialisation
+// leaves them), then the non-empty keys compacted in key order as
+// compact_slots_kernel does, from the counts kept in LDS.
+template <int NV, bool MM>
+__global__ __launch_bounds__(1024) void group_partials_compact_kernel(const unsigned long long *gpart, int nb, int nk,
+                                                                      unsigned long long *count_star, AggState *st0,
+                                                                      AggState *st1, int32_t *slot_list,
+                                                                      int64_t *n_out) {
+  constexpr int W = GroupPartialWords(NV, MM);
+  __shared__ unsigned long long kc[kGroupPartialKeys];
+  __shared__ int wsum[16];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, nw = blockDim.x >> 6;
+  for (int kq = w; kq < nk; kq += nw) {
+    unsigned long long c = 0;
+    Acc A[NV > 0 ? NV : 1];
+    for (int j = 0; j < (NV > 0 ? NV : 1); j++) {
+      A[j].cnt = 0; A[j].slo = 0; A[j].shi = 0; A[j].mn = INT64_MAX; A[j].mx = INT64_MIN;
+    }
+    for (int b = lane; b < nb; b += 64) {
+      const unsigned long long *o = gpart + ((size_t)kq * nb + b) * W;
+      c += o[0];
+      int f = 2;
+#pragma unroll
+      for (int j = 0; j < NV; j++) {
+        Acc B;
+        B.cnt = o[1]; B.slo = o[f]; B.shi = (int64_t)o[f + 1];
+        B.mn = MM ? (int64_t)o[f + 2] : INT64_MAX;
+        B.mx = MM ? (int64_t)o[f + 3] : INT64_MIN;
+        f += MM ? 4 : 2;
+        acc_merge(A[j], B);
+      }
+    }
+#pragma unroll
+    for (int m = 32; m >= 1; m >>= 1) c += shfl_xor_u64(c, m);
+#pragma unroll
+    for (int j = 0; j < NV; j++) acc_wave_reduce(A[j]);
+    if (lane == 0) {
+      kc[kq] = c;
+      count_star[kq] = c;
+      for (int j = 0; j < 2; j++) {
+        AggState z;
+        z.count = 0; z.sum_lo = 0; z.sum_hi = 0;
+        z.min_i = INT64_MAX; z.max_i = INT64_MIN;
+        z.sum_f = 0; z.min_f = 0xFFFFFFFFFFFFFFFFull; z.max_f = 0;
+        if (j < NV && A[j].cnt) {
+          z.count = A[j].cnt; z.sum_lo = A[j].slo; z.sum_hi = A[j].shi;
+          if (MM) { z.min_i = A[j].mn; z.max_i = A[j].mx; }
+        }
+        (j == 0 ? st0 : st1)[kq] = z;
+      }
+    }
+  }
+  __syncthreads();
+  // compaction of the non-empty keys (one pass: nk <= blockDim.x)
+  const int i = threadIdx.x;
+  const bool f = i < nk && kc[i] > 0;
+  const uint64_t m = __ballot(f);
+  if (lane == 0) wsum[w] = __popcll(m);
+  __syncthreads();
+  int before = 0, total = 0;
+  for (int k = 0; k < nw; k++) {
+    before += k < w ? wsum[k] : 0;
+    total += wsum[k];
+  }
+  const uint64_t lt = lane ? (m & ((1ull << lane) - 1ull)) : 0ull;
+  if (f) slot_list[before + __popcll(lt)] = (int32_t)i;
+  if (threadIdx.x == 0) *n_out = total;
+}
+
+void GroupPartialsCompact(const GroupPartialsOut &po, int nv, bool mm, int nk, unsigned long long *count_star,
+                          AggState *st0, AggState *st1, int32_t *slot_list, int64_t *n_out, hipStream_t s) {
+#define GPC(NV, MM)                                                                                               \
+  hipLaunchKernelGGL((group_partials_compact_kernel<NV, MM>), dim3(1), dim3(1024), 0, s,                          \
+                     (const unsigned long long *)po.buf, po.blocks, nk, count_star, st0, st1, slot_list, n_out)
+  if (nv == 0) GPC(0, false);
+  else if (nv == 1) { if (mm) GPC(1, true); else GPC(1, false); }
+  else { if (mm) GPC(2, true); else GPC(2, false); }
+#undef GPC
+  CHECK_LAUNCH();
+}
+
 void CompactSlots(const unsigned long long *count_star, int64_t nslots, int32_t *slot_list, int64_t *n_out,
                   hipStream_t s) {
   if (nslots <= (1 << 16)) {

@@ -258,13 +258,17 @@ def test_filter_agg_variants_parity(conn, oracle, monkeypatch, variant):
 
 
 # ---- every fused GROUP BY launch shape gives the same bits ------------------
-GD_VARIANTS = ["", "seg", "d2_g1", "d3_g2", "d4_g2", "d6_g1", "d8_g1"]
+# (+atomic: the table flush through global atomics instead of the per-workgroup
+# records that group_partials_compact reduces)
+GD_VARIANTS = ["", "seg", "d2_g1", "d3_g2", "d4_g2", "d6_g1", "d8_g1", "+atomic", "d3_g2+atomic"]
 
 
 @pytest.mark.parametrize("variant", GD_VARIANTS)
 def test_group_direct_variants_parity(conn, oracle, monkeypatch, variant):
     base, *opts = variant.split("+")
     monkeypatch.setenv("MBX_GD_VARIANT", base)
+    if "atomic" in opts:
+        monkeypatch.setenv("MBX_GD_ATOMIC_FLUSH", "1")
     for n in (1, 255, 256, 257, 1023, 70_001, 1_000_003):
         k = oracle.synth_i64(n, 7, 0, 40, -20)           # keys -20..19
         v = oracle.synth_i64(n, 9, 0, 2**40, -2**39)

@@ -29,6 +29,18 @@ for prof in ("false", "true"):
             rr.close()
             ts.append(time.perf_counter() - t0)
         out[f"profile={prof} {sql}"] = {"median_us": statistics.median(ts[50:]) * 1e6, "min_us": min(ts) * 1e6}
+    # the C3 shape: a 32-key GROUP BY whose 96 cells come back as text in one call
+    c.query(f"CREATE TABLE t3 AS SELECT CAST(mbx_synth(7, i, 32) AS INTEGER) AS k, "
+            f"mbx_synth(9, i, 1099511627776) - 549755813888 AS v FROM range({n}) tbl(i)")
+    for sql in ("SELECT k, SUM(v), COUNT(*) FROM t3 GROUP BY k",):
+        ts = []
+        for i in range(300):
+            t0 = time.perf_counter()
+            rr = c.query_raw(sql)
+            rr.cells()
+            rr.close()
+            ts.append(time.perf_counter() - t0)
+        out[f"profile={prof} {sql}"] = {"median_us": statistics.median(ts[50:]) * 1e6, "min_us": min(ts) * 1e6}
     if prof == "false":
         # prepared re-execution: bound-plan cache on / off (MBX_PLAN_CACHE=0)
         st = c.prepare("SELECT COUNT(*) FROM t WHERE x > ?").value
