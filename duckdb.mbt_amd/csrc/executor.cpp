@@ -124,6 +124,7 @@ struct Engine {
   uint32_t rounds_epoch = 0;
   void *d_small = nullptr;       // 64 KB scratch for small states
   dev::AggPartial *d_partials = nullptr;  // per-workgroup partials of the fused filter-aggregate
+  const void *defer_count_for = nullptr;  // the top-level BoundSelect whose GROUP BY count may stay on the device
   // pinned host staging for small results: every D2H of a query lands here
   // and the query pays ONE stream synchronisation
   // set around the query of CREATE TABLE AS / INSERT ... SELECT: select_rounds
@@ -376,6 +377,11 @@ struct DRel {
   int64_t n = 0;
   bool range = false;  // column 0 is the virtual range column
   int64_t rs = 0, rstep = 1;
+  // the row count is still on the device (n is its upper bound; the columns
+  // hold n rows): only the top-level aggregate of ExecuteSelect leaves it so,
+  // for ToHost to read with the rows in one copy; SettleCount otherwise
+  const int64_t *n_dev = nullptr;
+  std::shared_ptr<void> n_owner;
 };
 
 static DCol ColFromTable(const DevColumn &c) {
@@ -431,6 +437,14 @@ static T ReadDev(Engine &e, const void *p) {
   T v;
   memcpy(&v, e.h_pinned, sizeof(T));
   return v;
+}
+
+// a row count left on the device (DRel::n_dev) read back
+static void SettleCount(Engine &e, DRel &r) {
+  if (!r.n_dev) return;
+  r.n = ReadDev<int64_t>(e, r.n_dev);
+  r.n_dev = nullptr;
+  r.n_owner.reset();
 }
 
 // ---------------------------------------------------------------------------
@@ -877,6 +891,11 @@ static bool TryFilterCompact(Engine &e, const DRel &rel, const BExpr &pred, cons
 // projected relation of the selected rows.
 static DRel FilterProject(Engine &e, const DRel &rel, const BExprPtr &pred, const std::vector<BExprPtr> &exprs) {
   const int64_t n = rel.n;
+  if (rel.n_dev) {  // only a column passthrough may carry a row count still on the device
+    bool pt = !pred;
+    for (auto &x : exprs) pt &= x->kind == BExpr::COL && !(rel.range && x->col == 0);
+    if (!pt) ThrowError("Internal", "a relation with its row count on the device reached a projection");
+  }
   {
     DRel fused;
     if (pred && pred->kind != BExpr::CONST && TryFilterCompact(e, rel, *pred, exprs, fused)) return fused;
@@ -888,9 +907,12 @@ static DRel FilterProject(Engine &e, const DRel &rel, const BExprPtr &pred, cons
   if (passthrough) {
     DRel out;
     out.n = n;
+    out.n_dev = rel.n_dev;
+    out.n_owner = rel.n_owner;
     for (auto &x : exprs) out.cols.push_back(rel.cols[x->col]);
     return out;
   }
+
   const int64_t ntiles = (n + VM_TILE - 1) / VM_TILE;
   DevBufPtr bits, offs;
   int64_t nsel = n;
@@ -2067,6 +2089,19 @@ static DRel DistinctAggregate(Engine &e, const DRel &src, const BoundSelect &s) 
   return UploadRows(e, rows, types);
 }
 
+// The top-level SELECT of ExecuteSelect whose relation goes to the host
+// unchanged (no HAVING, ORDER BY, LIMIT / OFFSET or UNION; every output a
+// column of the aggregate): its GROUP BY may leave the group count on the
+// device, so the rows and the count come back in one copy (DRel::n_dev).
+static bool CountMayStayOnDevice(const Engine &e, const BoundSelect &s) {
+  if (e.defer_count_for != (const void *)&s || s.having || !s.union_all.empty() || !s.order.empty() ||
+      s.limit >= 0 || s.offset > 0)
+    return false;
+  for (auto &x : s.outputs)
+    if (x->kind != BExpr::COL) return false;
+  return true;
+}
+
 static DRel Aggregate(Engine &e, const DRel &src, const BoundSelect &s) {
   const int ng = (int)s.groups.size();
   const int na = (int)s.aggs.size();
@@ -2277,11 +2312,16 @@ static DRel Aggregate(Engine &e, const DRel &src, const BoundSelect &s) {
           }
           if (!launched) goto generic;
           auto list = Alloc(e, nslots * 4);
+          // the group count: left on the device for ToHost when this is the
+          // statement's own result (CountMayStayOnDevice), else read below
+          const bool defer = CountMayStayOnDevice(e, s);
+          DevBufPtr nbuf = defer ? Alloc(e, 8) : nullptr;
+          int64_t *const n_out = defer ? (int64_t *)nbuf->p : e.d_scratch;
           if (po.used)
             dev::GroupPartialsCompact(po, nv, mm, nk, (unsigned long long *)cs->p, s0p, s1p, (int32_t *)list->p,
-                                      e.d_scratch, e.stream);
+                                      n_out, e.stream);
           else
-            dev::CompactSlots((const unsigned long long *)cs->p, nslots, (int32_t *)list->p, e.d_scratch, e.stream);
+            dev::CompactSlots((const unsigned long long *)cs->p, nslots, (int32_t *)list->p, n_out, e.stream);
           // outputs sized for every slot (<= 1024 rows): the emit reads the group
           // count from the device, so the query waits on the stream once, after it
           dev::EmitDesc D;
@@ -2289,7 +2329,7 @@ static DRel Aggregate(Engine &e, const DRel &src, const BoundSelect &s) {
           D.nagg = na;
           D.cstar = (const unsigned long long *)cs->p;
           D.slot_list = (const int32_t *)list->p;
-          D.n_list = e.d_scratch;
+          D.n_list = n_out;
           D.nslots = nslots;
           D.has_key = 1;
           D.key_phys = PhysOf(s.groups[0]->type);
@@ -2310,7 +2350,13 @@ static DRel Aggregate(Engine &e, const DRel &src, const BoundSelect &s) {
             out.cols.push_back(oc);
           }
           dev::EmitAggRelation(D, e.stream);
-          out.n = ReadDev<int64_t>(e, e.d_scratch);  // its synchronisation also covers the emit (state buffers)
+          if (defer) {
+            out.n = nslots;  // the columns hold every slot; the count follows the rows to the host
+            out.n_dev = n_out;
+            out.n_owner = nbuf;
+          } else {
+            out.n = ReadDev<int64_t>(e, n_out);
+          }
           return out;
         }
       }
@@ -2661,8 +2707,12 @@ static bool TextCol(const DCol &d, int64_t start, dev::TextCol &tc) {
 }
 
 static ResultPtr ToHostPinned(Engine &e, const DRel &r, const std::vector<std::string> &names, size_t ncols,
-                              int64_t start, int64_t n, bool text = false) {
-  size_t need = 64;
+                              int64_t start, int64_t n, bool text = false, const int64_t *count_dev = nullptr) {
+  // count_dev: the true row count (<= n) is on the device: it rides the one
+  // mapped copy with the n rows, which are trimmed to it (nullptr when that copy
+  // does not apply, before anything is launched)
+  if (count_dev && (start != 0 || (text && n >= kTextRows))) return nullptr;
+  size_t need = count_dev ? 128 : 64;
   const int64_t w0 = start >> 6, w1 = (start + n + 63) >> 6;
   for (size_t c = 0; c < ncols; c++) {
     const DCol &d = r.cols[c];
@@ -2711,7 +2761,9 @@ static ResultPtr ToHostPinned(Engine &e, const DRel &r, const std::vector<std::s
   }
   // small results: one copy kernel into the coherent mapped buffer instead of
   // one DMA per buffer; larger ones: DMA into the (growable) pinned arena
-  const bool mapped = tj.empty() && need <= Engine::kMappedBytes && ncols * 2 <= HOSTCOPY_MAX && !Knob("MBX_NO_HOSTCOPY");
+  const bool mapped = tj.empty() && need <= Engine::kMappedBytes && ncols * 2 + 1 <= HOSTCOPY_MAX &&
+                      !Knob("MBX_NO_HOSTCOPY");
+  if (count_dev && !mapped) return nullptr;
   if (!mapped && !e.EnsurePinned(need)) return nullptr;
   uint8_t *const H = mapped ? e.h_mapped : e.h_pinned;
   std::vector<size_t> data_off(ncols), valid_off(ncols, 0);
@@ -2721,8 +2773,12 @@ static ResultPtr ToHostPinned(Engine &e, const DRel &r, const std::vector<std::s
     if (mapped) hd.seg[hd.nseg++] = dev::HostCopySeg{src, H + off, (int64_t)bytes};
     else HIPCHK(hipMemcpyAsync(H + off, src, bytes, hipMemcpyDeviceToHost, e.stream));
   };
-  size_t at = 64;  // [0, 4): error word
+  size_t at = 64;  // [0, 4): error word; [64, 72): the device row count (count_dev)
   if (!mapped) HIPCHK(hipMemcpyAsync(H, e.d_err, 4, hipMemcpyDeviceToHost, e.stream));
+  if (count_dev) {
+    seg(count_dev, at, 8);
+    at += 64;
+  }
   for (size_t c = 0; c < ncols; c++) {
     const DCol &d = r.cols[c];
     const int sz = PhysSize(d.phys);
@@ -2754,6 +2810,12 @@ static ResultPtr ToHostPinned(Engine &e, const DRel &r, const std::vector<std::s
   int32_t err;
   memcpy(&err, (const void *)H, 4);
   RaiseDeviceError(e, err);
+  if (count_dev) {
+    int64_t cnt;
+    memcpy(&cnt, (const void *)(H + 64), 8);
+    if (cnt < 0 || cnt > n) ThrowError("Internal", "device row count out of range");
+    n = cnt;
+  }
   auto res = std::make_shared<MaterializedResult>();
   res->nrows = n;
   for (size_t c = 0; c < ncols; c++) {
@@ -2789,6 +2851,14 @@ static ResultPtr ToHostPinned(Engine &e, const DRel &r, const std::vector<std::s
 
 static ResultPtr ToHost(Engine &e, const DRel &r, const std::vector<std::string> &names, int64_t offset, int64_t limit,
                         size_t ncols, bool text) {
+  if (r.n_dev) {
+    // the rows (all n of the upper bound) and the count in one copy; else read the count first
+    if (offset <= 0 && limit < 0)
+      if (ResultPtr p = ToHostPinned(e, r, names, ncols, 0, r.n, text, r.n_dev)) return p;
+    DRel settled = r;
+    SettleCount(e, settled);
+    return ToHost(e, settled, names, offset, limit, ncols, text);
+  }
   int64_t start = std::min(std::max<int64_t>(offset, 0), r.n);
   int64_t n = r.n - start;
   if (limit >= 0) n = std::min(n, limit);
@@ -2914,6 +2984,7 @@ static size_t VisibleCols(const BoundSelect &s) {
 // result), not a subquery's or an INSERT's input
 static DRel RunSelectDev(Engine &e, Connection &c, const BoundSelect &s, bool top) {
   DRel r = RunBranch(e, c, s);
+  if (!top || !s.union_all.empty() || !s.order.empty() || s.limit >= 0 || s.offset > 0) SettleCount(e, r);
   if (!s.union_all.empty()) {
     std::vector<DRel> parts;
     parts.push_back(r);
@@ -3093,6 +3164,11 @@ ResultPtr ExecuteSelect(Connection &c, const BoundSelect &s) {
       return hr;
     }
   }
+  struct DeferScope {  // the statement's own aggregate may leave its group count on the device
+    Engine &e;
+    DeferScope(Engine &en, const BoundSelect &s) : e(en) { e.defer_count_for = &s; }
+    ~DeferScope() { e.defer_count_for = nullptr; }
+  } defer(e, s);
   DRel r = RunSelectDev(e, c, s, true);
   std::vector<std::string> names(s.names.begin(), s.names.begin() + VisibleCols(s));
   ResultPtr res = ToHost(e, r, names, 0, -1, names.size(), true);  // raises pending device errors

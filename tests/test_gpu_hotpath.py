@@ -473,6 +473,56 @@ def test_groupby_direct_wide_slot_table(conn):
     assert res.rows == [[str(k), str(c), str(s)] for k, (c, s) in sorted(exp.items())]
 
 
+def test_groupby_direct_sparse_keys_count_on_device(mbx, oracle, monkeypatch):
+    """The direct GROUP BY of the statement's own result leaves its group count on
+    the device and ToHost trims the slot rows to it in the same copy; sparse keys
+    (3 of 16 slots present) make the count smaller than the slot table.  HAVING,
+    ORDER BY, LIMIT, a projection, a stream and the Arrow path read the count
+    first; each must give the same groups."""
+    cfg = mbx.Config.create()
+    cfg.set("mbx_profile", "true")
+    c = mbx.connect_with_config(cfg).value
+    try:
+        for flush in ("", "1"):
+            monkeypatch.setenv("MBX_GD_ATOMIC_FLUSH", flush)
+            for n in (3, 1000, 1_000_003):
+                q(c, "DROP TABLE IF EXISTS sk")
+                # keys -3, 7, 12 (range 16), values i - 500
+                q(c, f"CREATE TABLE sk AS SELECT CASE WHEN i % 3 = 0 THEN -3 WHEN i % 3 = 1 THEN 7 ELSE 12 END AS k, "
+                     f"i - 500 AS v FROM range({n}) tbl(i)")
+                exp = {}
+                for kk, r in ((-3, 0), (7, 1), (12, 2)):
+                    vals = [i - 500 for i in range(r, n, 3)]
+                    if vals:
+                        exp[kk] = (sum(vals), len(vals), min(vals), max(vals))
+                got = q(c, "SELECT k, SUM(v), COUNT(*), MIN(v), MAX(v) FROM sk GROUP BY k").rows
+                assert "group_direct" in [x["name"] for x in c.last_profile()["kernels"]], n
+                assert sorted((int(r[0]), int(r[1]), int(r[2]), int(r[3]), int(r[4])) for r in got) == \
+                    sorted((kk,) + t for kk, t in exp.items()), (flush, n)
+                assert [r[0] for r in got] == [str(kk) for kk in sorted(exp)]  # key order
+                keys = sorted(exp)
+                r = q(c, "SELECT k, COUNT(*) FROM sk GROUP BY k HAVING COUNT(*) > 0 ORDER BY k DESC").rows
+                assert [int(x[0]) for x in r] == keys[::-1]
+                r = q(c, "SELECT k, COUNT(*) FROM sk GROUP BY k LIMIT 2").rows
+                assert [int(x[0]) for x in r] == keys[:2]
+                r = q(c, "SELECT k + 1, COUNT(*) FROM sk GROUP BY k").rows
+                assert sorted(int(x[0]) for x in r) == [kk + 1 for kk in keys]
+                st = c.query_stream("SELECT k, COUNT(*) FROM sk GROUP BY k").value
+                rows = []
+                while True:
+                    ch = st.next().value
+                    if ch is None or not ch.rows:
+                        break
+                    rows += ch.rows
+                st.close()
+                assert [int(x[0]) for x in rows] == keys
+                a = c.query_arrow("SELECT k, COUNT(*) FROM sk GROUP BY k").value
+                assert a.row_count() == len(keys)
+                a.close()
+    finally:
+        c.close()
+
+
 # ---- multi-column conjunctions fused into one LDS-DMA pass ----------------------
 def test_filter_multi_parity(mbx, oracle):
     cfg = mbx.Config.create()
