@@ -115,9 +115,13 @@ struct GroupPartialsOut {
   int blocks;           // set: workgroups that wrote records
 };
 // The records reduced into cstar / st0 / st1 for every key (empty keys as
-// initialised), then the non-empty keys compacted as CompactSlots does.
+// initialised), then the non-empty keys compacted as CompactSlots does; with
+// emit, the same launch then writes that relation as EmitAggRelation would
+// (emit->slot_list / n_list: slot_list / n_out).
+struct EmitDesc;
 void GroupPartialsCompact(const GroupPartialsOut &po, int nv, bool mm, int nk, unsigned long long *count_star,
-                          AggState *st0, AggState *st1, int32_t *slot_list, int64_t *n_out, hipStream_t s);
+                          AggState *st0, AggState *st1, int32_t *slot_list, int64_t *n_out, hipStream_t s,
+                          const EmitDesc *emit = nullptr);
 // false only when a predicate was given and the shape needs the segmented kernel.
 // po: the caller did not initialise cstar / st0 / st1: the call does (atomic
 // forms) or writes per-workgroup records instead (po->used).

@@ -2317,10 +2317,7 @@ static DRel Aggregate(Engine &e, const DRel &src, const BoundSelect &s) {
           const bool defer = CountMayStayOnDevice(e, s);
           DevBufPtr nbuf = defer ? Alloc(e, 8) : nullptr;
           int64_t *const n_out = defer ? (int64_t *)nbuf->p : e.d_scratch;
-          if (po.used)
-            dev::GroupPartialsCompact(po, nv, mm, nk, (unsigned long long *)cs->p, s0p, s1p, (int32_t *)list->p,
-                                      n_out, e.stream);
-          else
+          if (!po.used)
             dev::CompactSlots((const unsigned long long *)cs->p, nslots, (int32_t *)list->p, n_out, e.stream);
           // outputs sized for every slot (<= 1024 rows): the emit reads the group
           // count from the device, so the query waits on the stream once, after it
@@ -2349,7 +2346,11 @@ static DRel Aggregate(Engine &e, const DRel &src, const BoundSelect &s) {
             D.a[j] = EmitFor(s.aggs[j], VC_I64, stp, oc);
             out.cols.push_back(oc);
           }
-          dev::EmitAggRelation(D, e.stream);
+          if (po.used)  // records reduced, keys compacted and the relation written by one launch
+            dev::GroupPartialsCompact(po, nv, mm, nk, (unsigned long long *)cs->p, s0p, s1p, (int32_t *)list->p,
+                                      n_out, e.stream, &D);
+          else
+            dev::EmitAggRelation(D, e.stream);
           if (defer) {
             out.n = nslots;  // the columns hold every slot; the count follows the rows to the host
             out.n_dev = n_out;

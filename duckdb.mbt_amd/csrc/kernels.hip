@@ -2466,6 +2466,133 @@ __global__ void slot_scatter_kernel(const int32_t *flag, const int32_t *pos, int
 
 // Ordered list of the non-empty slots.  One workgroup for small tables; a
 // device-wide scan (flags -> hipCUB exclusive sum -> scatter) for large ones.
+// Writes the aggregate relation [key?, agg0, agg1, ...] from per-slot states,
+// as workgroup `bid` of `nb` (emit_agg_kernel; the one workgroup of
+// group_partials_compact_kernel).  Validity bitmaps are written as whole 64-bit
+// words from a wave ballot (each wave owns 64 consecutive output rows), so the
+// output bitmaps need no zeroing and no atomics.  part: LDS room for one Acc
+// per wave (the partials reduction).
+__device__ __forceinline__ void emit_agg_body(const EmitDesc &D, Acc *part, int64_t bid, int64_t nb) {
+  if (D.npartials > 0) {
+    // slot 0 from the filter-aggregate's per-workgroup partials (one workgroup)
+    Acc A;
+    A.cnt = 0; A.slo = 0; A.shi = 0; A.mn = INT64_MAX; A.mx = INT64_MIN;
+    for (int i = threadIdx.x; i < D.npartials; i += blockDim.x) {
+      const AggPartial &q = D.partials[i];
+      Acc B;
+      B.cnt = q.cnt; B.slo = q.slo; B.shi = q.shi; B.mn = q.mn; B.mx = q.mx;
+      acc_merge(A, B);
+    }
+    acc_wave_reduce(A);
+    if ((threadIdx.x & 63) == 0) part[threadIdx.x >> 6] = A;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      Acc T0 = part[0];
+      for (int i = 1; i < (int)(blockDim.x >> 6); i++) acc_merge(T0, part[i]);
+      unsigned long long *cs = (unsigned long long *)D.cstar;
+      cs[0] = T0.cnt;
+      for (int j = 0; j < D.nagg; j++) {
+        AggState *S = D.a[j].states;
+        if (!S) continue;
+        S->count = T0.cnt;
+        S->sum_lo = T0.slo;
+        S->sum_hi = T0.shi;
+        S->min_i = T0.mn;
+        S->max_i = T0.mx;
+      }
+      __threadfence_block();
+    }
+    __syncthreads();
+  }
+  const int64_t n = D.slot_list ? *D.n_list : D.nslots;
+  const int lane = threadIdx.x & 63;
+  const int64_t stride = nb * blockDim.x;
+  for (int64_t base = bid * blockDim.x + (threadIdx.x & ~63); base < n; base += stride) {
+    const int64_t i = base + lane;
+    const bool in = i < n;
+    const int64_t sl = in ? (D.slot_list ? D.slot_list[i] : i) : 0;
+    if (D.has_key) {
+      bool kv = in && sl != D.null_slot;
+      if (in) {
+        int64_t k = D.kmin + sl;
+        if (kv) store_phys(D.key_out, D.key_phys, i, k, k >> 63);
+        else store_phys(D.key_out, D.key_phys, i, 0, 0);
+      }
+      uint64_t m = __ballot(kv);
+      if (lane == 0) {
+        D.key_valid[base >> 5] = (uint32_t)m;
+        if (base + 32 < n) D.key_valid[(base >> 5) + 1] = (uint32_t)(m >> 32);
+      }
+    }
+    for (int q = 0; q < D.nkeys_c; q++) {
+      const auto &K = D.kc[q];
+      bool kv = in;
+      if (in) {
+        const int64_t dg = (sl / K.stride) % K.radix;
+        kv = !(K.nullable && dg == K.radix - 1);
+        const int64_t k = kv ? K.kmin + dg : 0;
+        store_phys(K.out, K.phys, i, k, k >> 63);
+      }
+      uint64_t m = __ballot(kv);
+      if (lane == 0) {
+        K.valid[base >> 5] = (uint32_t)m;
+        if (base + 32 < n) K.valid[(base >> 5) + 1] = (uint32_t)(m >> 32);
+      }
+    }
+    for (int j = 0; j < D.nagg; j++) {
+      const EmitAgg &A = D.a[j];
+      bool valid = in;
+      int64_t lo = 0, hi = 0;
+      if (in) {
+        if (A.kind == 0 /*COUNT_STAR*/) {
+          lo = (int64_t)D.cstar[sl];
+        } else {
+          const AggState &S = A.states[sl];
+          switch (A.kind) {
+            case 1: /*COUNT*/ lo = (int64_t)S.count; break;
+            case 2: /*SUM*/
+              if (!S.count) { valid = false; break; }
+              if (A.in_class == VC_F64) lo = __double_as_longlong(S.sum_f);
+              else { lo = (int64_t)S.sum_lo; hi = S.sum_hi; }
+              break;
+            case 3: /*MIN*/
+            case 4: /*MAX*/
+              if (!S.count) { valid = false; break; }
+              if (A.in_class == VC_F64) lo = __double_as_longlong(f64_unorder(A.kind == 3 ? S.min_f : S.max_f));
+              else { lo = A.kind == 3 ? S.min_i : S.max_i; hi = lo >> 63; }
+              break;
+            default: /*AVG*/ {
+              if (!S.count) { valid = false; break; }
+              double v;
+              if (A.in_class == VC_F64) v = S.sum_f / (double)S.count;
+              else {
+                double sum = i128_to_double(mk128((int64_t)S.sum_lo, S.sum_hi));
+                double div = (double)S.count;
+                for (int k = 0; k < A.avg_scale; k++) div *= 10.0;
+                v = sum / div;
+              }
+              lo = __double_as_longlong(v);
+              break;
+            }
+          }
+        }
+        if (valid) store_phys(A.out, A.out_phys, i, lo, hi);
+        else store_phys(A.out, A.out_phys, i, 0, 0);
+      }
+      uint64_t m = __ballot(valid);
+      if (lane == 0) {
+        A.valid[base >> 5] = (uint32_t)m;
+        if (base + 32 < n) A.valid[(base >> 5) + 1] = (uint32_t)(m >> 32);
+      }
+    }
+  }
+}
+
+__global__ __launch_bounds__(256) void emit_agg_kernel(EmitDesc D) {
+  __shared__ Acc part[4];
+  emit_agg_body(D, part, blockIdx.x, gridDim.x);
+}
+
 // The group_direct_lds partials of nb workgroups reduced per key (one wave per
 // key at a time, its lanes over the records, carry-correct int128 sums), every
 // key's state and COUNT(*) slot written (empty keys as the initialisation
@@ -2475,10 +2602,11 @@ template <int NV, bool MM>
 __global__ __launch_bounds__(1024) void group_partials_compact_kernel(const unsigned long long *gpart, int nb, int nk,
                                                                       unsigned long long *count_star, AggState *st0,
                                                                       AggState *st1, int32_t *slot_list,
-                                                                      int64_t *n_out) {
+                                                                      int64_t *n_out, EmitDesc D, int emit) {
   constexpr int W = GroupPartialWords(NV, MM);
   __shared__ unsigned long long kc[kGroupPartialKeys];
   __shared__ int wsum[16];
+  __shared__ Acc part[16];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, nw = blockDim.x >> 6;
   for (int kq = w; kq < nk; kq += nw) {
     unsigned long long c = 0;
@@ -2535,13 +2663,24 @@ __global__ __launch_bounds__(1024) void group_partials_compact_kernel(const unsi
   const uint64_t lt = lane ? (m & ((1ull << lane) - 1ull)) : 0ull;
   if (f) slot_list[before + __popcll(lt)] = (int32_t)i;
   if (threadIdx.x == 0) *n_out = total;
+  if (!emit) return;
+  // the relation of the compacted keys (D reads the states, slot list and
+  // count just written by this workgroup)
+  __threadfence_block();
+  __syncthreads();
+  emit_agg_body(D, part, 0, 1);
 }
 
 void GroupPartialsCompact(const GroupPartialsOut &po, int nv, bool mm, int nk, unsigned long long *count_star,
-                          AggState *st0, AggState *st1, int32_t *slot_list, int64_t *n_out, hipStream_t s) {
+                          AggState *st0, AggState *st1, int32_t *slot_list, int64_t *n_out, hipStream_t s,
+                          const EmitDesc *emit) {
+  EmitDesc D;
+  if (emit) D = *emit;
+  else memset(&D, 0, sizeof(D));
 #define GPC(NV, MM)                                                                                               \
   hipLaunchKernelGGL((group_partials_compact_kernel<NV, MM>), dim3(1), dim3(1024), 0, s,                          \
-                     (const unsigned long long *)po.buf, po.blocks, nk, count_star, st0, st1, slot_list, n_out)
+                     (const unsigned long long *)po.buf, po.blocks, nk, count_star, st0, st1, slot_list, n_out, D, \
+                     emit ? 1 : 0)
   if (nv == 0) GPC(0, false);
   else if (nv == 1) { if (mm) GPC(1, true); else GPC(1, false); }
   else { if (mm) GPC(2, true); else GPC(2, false); }
@@ -2859,127 +2998,6 @@ void CopyKernel(const void *in, void *out, int64_t nbytes, hipStream_t s) {
 
 namespace mbx {
 namespace dev {
-
-// Writes the aggregate relation [key?, agg0, agg1, ...] from per-slot states.
-// Writes the aggregate relation.  Validity bitmaps are written as whole
-// 64-bit words from a wave ballot (each wave owns 64 consecutive output rows),
-// so the output bitmaps need no zeroing and no atomics.
-__global__ __launch_bounds__(256) void emit_agg_kernel(EmitDesc D) {
-  if (D.npartials > 0) {
-    // slot 0 from the filter-aggregate's per-workgroup partials (one workgroup)
-    __shared__ Acc part[4];
-    Acc A;
-    A.cnt = 0; A.slo = 0; A.shi = 0; A.mn = INT64_MAX; A.mx = INT64_MIN;
-    for (int i = threadIdx.x; i < D.npartials; i += blockDim.x) {
-      const AggPartial &q = D.partials[i];
-      Acc B;
-      B.cnt = q.cnt; B.slo = q.slo; B.shi = q.shi; B.mn = q.mn; B.mx = q.mx;
-      acc_merge(A, B);
-    }
-    acc_wave_reduce(A);
-    if ((threadIdx.x & 63) == 0) part[threadIdx.x >> 6] = A;
-    __syncthreads();
-    if (threadIdx.x == 0) {
-      Acc T0 = part[0];
-      for (int i = 1; i < (int)(blockDim.x >> 6); i++) acc_merge(T0, part[i]);
-      unsigned long long *cs = (unsigned long long *)D.cstar;
-      cs[0] = T0.cnt;
-      for (int j = 0; j < D.nagg; j++) {
-        AggState *S = D.a[j].states;
-        if (!S) continue;
-        S->count = T0.cnt;
-        S->sum_lo = T0.slo;
-        S->sum_hi = T0.shi;
-        S->min_i = T0.mn;
-        S->max_i = T0.mx;
-      }
-      __threadfence_block();
-    }
-    __syncthreads();
-  }
-  const int64_t n = D.slot_list ? *D.n_list : D.nslots;
-  const int lane = threadIdx.x & 63;
-  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
-  for (int64_t base = (int64_t)blockIdx.x * blockDim.x + (threadIdx.x & ~63); base < n; base += stride) {
-    const int64_t i = base + lane;
-    const bool in = i < n;
-    const int64_t sl = in ? (D.slot_list ? D.slot_list[i] : i) : 0;
-    if (D.has_key) {
-      bool kv = in && sl != D.null_slot;
-      if (in) {
-        int64_t k = D.kmin + sl;
-        if (kv) store_phys(D.key_out, D.key_phys, i, k, k >> 63);
-        else store_phys(D.key_out, D.key_phys, i, 0, 0);
-      }
-      uint64_t m = __ballot(kv);
-      if (lane == 0) {
-        D.key_valid[base >> 5] = (uint32_t)m;
-        if (base + 32 < n) D.key_valid[(base >> 5) + 1] = (uint32_t)(m >> 32);
-      }
-    }
-    for (int q = 0; q < D.nkeys_c; q++) {
-      const auto &K = D.kc[q];
-      bool kv = in;
-      if (in) {
-        const int64_t dg = (sl / K.stride) % K.radix;
-        kv = !(K.nullable && dg == K.radix - 1);
-        const int64_t k = kv ? K.kmin + dg : 0;
-        store_phys(K.out, K.phys, i, k, k >> 63);
-      }
-      uint64_t m = __ballot(kv);
-      if (lane == 0) {
-        K.valid[base >> 5] = (uint32_t)m;
-        if (base + 32 < n) K.valid[(base >> 5) + 1] = (uint32_t)(m >> 32);
-      }
-    }
-    for (int j = 0; j < D.nagg; j++) {
-      const EmitAgg &A = D.a[j];
-      bool valid = in;
-      int64_t lo = 0, hi = 0;
-      if (in) {
-        if (A.kind == 0 /*COUNT_STAR*/) {
-          lo = (int64_t)D.cstar[sl];
-        } else {
-          const AggState &S = A.states[sl];
-          switch (A.kind) {
-            case 1: /*COUNT*/ lo = (int64_t)S.count; break;
-            case 2: /*SUM*/
-              if (!S.count) { valid = false; break; }
-              if (A.in_class == VC_F64) lo = __double_as_longlong(S.sum_f);
-              else { lo = (int64_t)S.sum_lo; hi = S.sum_hi; }
-              break;
-            case 3: /*MIN*/
-            case 4: /*MAX*/
-              if (!S.count) { valid = false; break; }
-              if (A.in_class == VC_F64) lo = __double_as_longlong(f64_unorder(A.kind == 3 ? S.min_f : S.max_f));
-              else { lo = A.kind == 3 ? S.min_i : S.max_i; hi = lo >> 63; }
-              break;
-            default: /*AVG*/ {
-              if (!S.count) { valid = false; break; }
-              double v;
-              if (A.in_class == VC_F64) v = S.sum_f / (double)S.count;
-              else {
-                double sum = i128_to_double(mk128((int64_t)S.sum_lo, S.sum_hi));
-                double div = (double)S.count;
-                for (int k = 0; k < A.avg_scale; k++) div *= 10.0;
-                v = sum / div;
-              }
-              lo = __double_as_longlong(v);
-              break;
-            }
-          }
-        }
-        if (valid) store_phys(A.out, A.out_phys, i, lo, hi);
-        else store_phys(A.out, A.out_phys, i, 0, 0);
-      }
-      uint64_t m = __ballot(valid);
-      if (lane == 0) {
-        A.valid[base >> 5] = (uint32_t)m;
-        if (base + 32 < n) A.valid[(base >> 5) + 1] = (uint32_t)(m >> 32);
-      }
-    }
-  }
-}
 
 void EmitAggRelation(const EmitDesc &d, hipStream_t s) {
   hipLaunchKernelGGL(emit_agg_kernel, dim3(d.npartials > 0 ? 1 : GridFor(d.nslots, 256, 1024)), dim3(256), 0, s, d);
