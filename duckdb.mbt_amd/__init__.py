@@ -207,17 +207,20 @@ def _result_text(res):
         lib.duckdb_mbx_free(ctypes.c_void_p(p))
     nr, nc = struct.unpack_from("<qq", data, 0)
     ncell = nr * nc
+    if ncell == 0:
+        return [[] for _ in range(nr)], [[] for _ in range(nr)]
     head = 16 + ((ncell + 7) & ~7)
     offs = struct.unpack_from(f"<{ncell + 1}q", data, head)
     base = head + 8 * (ncell + 1)
-    flags = data[16:16 + ncell]
-    rows, nulls = [], []
-    for r in range(nr):
-        i0 = r * nc
-        rn = [f == 1 for f in flags[i0:i0 + nc]]
-        rv = [data[base + offs[i]:base + offs[i + 1]].decode("utf-8", errors="replace") for i in range(i0, i0 + nc)]
-        rows.append(rv)
-        nulls.append(rn)
+    raw = data[base:base + offs[ncell]]
+    if raw.isascii():  # one decode; byte offsets are then character offsets
+        txt = raw.decode("ascii")
+        vals = [txt[a:b] for a, b in zip(offs, offs[1:])]
+    else:
+        vals = [raw[a:b].decode("utf-8", errors="replace") for a, b in zip(offs, offs[1:])]
+    fl = [f == 1 for f in data[16:16 + ncell]]
+    rows = [vals[i:i + nc] for i in range(0, ncell, nc)]
+    nulls = [fl[i:i + nc] for i in range(0, ncell, nc)]
     return rows, nulls
 
 
