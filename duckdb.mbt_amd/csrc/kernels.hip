@@ -2614,7 +2614,8 @@ __global__ __launch_bounds__(1024) void group_partials_compact_kernel(const unsi
     for (int j = 0; j < (NV > 0 ? NV : 1); j++) {
       A[j].cnt = 0; A[j].slo = 0; A[j].shi = 0; A[j].mn = INT64_MAX; A[j].mx = INT64_MIN;
     }
-    for (int b = lane; b < nb; b += 64) {
+#pragma unroll 4
+    for (int b = lane; b < nb; b += 64) {  // (unrolled: a lane's records load together)
       const unsigned long long *o = gpart + ((size_t)kq * nb + b) * W;
       c += o[0];
       int f = 2;
