@@ -3195,8 +3195,7 @@ DeviceResultPtr ExecuteSelectDevice(Connection &c, const BoundSelect &s, StreamS
   auto d = std::make_shared<DeviceResult>();
   d->r = RunSelectDev(e, c, s, true);
   d->names.assign(s.names.begin(), s.names.begin() + VisibleCols(s));
-  HIPCHK(hipStreamSynchronize(e.stream));
-  CheckError(e);
+  CheckError(e);  // (its copy of the error word waits for the whole stream)
   meta->names = d->names;
   meta->types.clear();
   for (size_t i = 0; i < d->names.size(); i++) meta->types.push_back(d->r.cols[i].type);
