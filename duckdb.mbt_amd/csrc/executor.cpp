@@ -4204,7 +4204,9 @@ static bool ShardedAggregateRccl(Connection &c, const BoundSelect &s, const Boun
   // A collective that does not complete in time (a rank that cannot reach the
   // others, a broken link) must not hang the connection: the communicators
   // are aborted and the host merge answers this statement and the next ones.
-  if (cok && !RcclWait(c, streams, tc0)) {
+  // The wait is bounded also when the group reported an error: some ranks'
+  // parts may have been enqueued before it.
+  if (!RcclWait(c, streams, tc0)) {
     for (int k = 0; k < nsh; k++) sendb[k].reset(), recvb[k].reset(), scrb[k].reset(), rel[k] = DRel();
     return fallback(st.rccl_note);
   }
@@ -4241,7 +4243,10 @@ static bool ShardedAggregateRccl(Connection &c, const BoundSelect &s, const Boun
   Eng(c);
   const double t_coll = std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - tc0).count();
   if (first_err) std::rethrow_exception(first_err);
-  if (!cok) ThrowError("IO", cerr);
+  if (!cok) {  // the host merge recomputes the partials, for this statement and the next ones
+    c.rccl.reset();
+    return fallback("RCCL collective failed (" + cerr + "): communicators dropped, host merge from now on");
+  }
   const auto t_merge = std::chrono::steady_clock::now();
   // every rank's device error word, raised as that shard's error; every
   // shard that reported one is cleared, so no stale error reaches its next query
@@ -4413,7 +4418,7 @@ static bool GroupRcclCombine(Connection &c, const BoundSelect &s, const BoundSel
   const auto tc0 = std::chrono::steady_clock::now();
   std::string cerr;
   const bool cok = rc::Collective(*c.rccl, false, sp, rp, xp, streams, (size_t)P, &cerr);
-  if (cok && !RcclWait(c, streams, tc0)) return fallback(st.rccl_note);
+  if (!RcclWait(c, streams, tc0)) return fallback(st.rccl_note);  // (bounded also after a reported error)
   // device 0 combines; one D2H of the combined slots and of the gathered blocks
   const bool keep_parts = recv_lanes * 8 <= ((int64_t)4 << 20);  // the per-shard partials, when small
   std::vector<int64_t> host((size_t)out_lanes + (keep_parts ? (size_t)recv_lanes : 0));
@@ -4444,7 +4449,10 @@ static bool GroupRcclCombine(Connection &c, const BoundSelect &s, const BoundSel
   Eng(c);
   const double t_coll = std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - tc0).count();
   if (first_err) std::rethrow_exception(first_err);
-  if (!cok) return fallback("RCCL all-gather failed (" + cerr + "): host merge");
+  if (!cok) {
+    c.rccl.reset();
+    return fallback("RCCL all-gather failed (" + cerr + "): communicators dropped, host merge from now on");
+  }
   const auto t_merge = std::chrono::steady_clock::now();
   // every rank's device error word: the first raised naming its shard, all cleared
   int bad = -1;

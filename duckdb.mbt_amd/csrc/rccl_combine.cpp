@@ -148,6 +148,10 @@ bool Collective(Comms &c, bool reduce, const std::vector<const int64_t *> &send,
                 const std::vector<int64_t *> &scratch, const std::vector<hipStream_t> &streams, size_t count,
                 std::string *err) {
   const int n = (int)c.devs.size();
+  if (Knob("MBX_RCCL_TEST_FAIL")) {  // tests: a collective that reports an error before any rank's part runs
+    *err = "injected collective failure (MBX_RCCL_TEST_FAIL)";
+    return false;
+  }
   if (c.loopback) {
     // the data movement of the collective as device copies after every
     // sender's pack: the all-gather lands every rank's block in every rank's

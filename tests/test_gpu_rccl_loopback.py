@@ -185,6 +185,35 @@ def test_rccl_without_distinct_devices_falls_back_with_note(mbx, oracle):
     c.close()
 
 
+def test_rccl_collective_failure_falls_back_to_host_merge(mbx, oracle, monkeypatch):
+    """A collective that reports an error (injected, MBX_RCCL_TEST_FAIL): the
+    statement is answered exactly by the host merge, the communicators are
+    dropped, and the connection keeps the host merge for the next statements;
+    the GROUP BY combine the same."""
+    n = 2_000_003
+    for sql, group in (("SELECT COUNT(*), SUM(x) FROM t WHERE x > 24", False),
+                       ("SELECT k, COUNT(*), SUM(x) FROM t GROUP BY k", True)):
+        c = _conn(mbx, "0,0")
+        q(c, f"CREATE TABLE t AS SELECT mbx_synth(42, i, 50) + 1 AS x, CAST(mbx_synth(7, i, 32) AS INTEGER) AS k "
+             f"FROM range({n}) tbl(i)")
+        c.set_combine("host")
+        ref = q(c, sql).rows
+        c.set_combine("rccl_loopback")
+        monkeypatch.setenv("MBX_RCCL_TEST_FAIL", "1")
+        st0 = c.rccl_stats()
+        assert q(c, sql).rows == ref, sql
+        st = c.rccl_stats()
+        assert st["rccl_fallbacks"] > st0["rccl_fallbacks"], st
+        assert st["rccl_loopbacks"] == st0["rccl_loopbacks"] and "host merge from now on" in st["note"], st
+        monkeypatch.delenv("MBX_RCCL_TEST_FAIL")
+        assert q(c, sql).rows == ref, sql
+        assert c.rccl_stats()["rccl_loopbacks"] == st0["rccl_loopbacks"], c.rccl_stats()  # communicators dropped
+        if not group:
+            cnt, s = oracle.synth_filter_count(42, 0, n, 50, 1, 25, 2**63 - 1, 8)
+            assert ref == [[str(cnt), str(s)]]
+        c.close()
+
+
 def test_rccl_library_calls_on_one_gpu(mbx):
     """The real RCCL calls the combine makes -- librccl opened by dlopen,
     ncclCommInitAll (on its helper thread, bounded), one ncclReduce and one
