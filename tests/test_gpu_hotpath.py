@@ -489,7 +489,7 @@ def test_groupby_direct_sparse_keys_count_on_device(mbx, oracle, monkeypatch):
                 q(c, "DROP TABLE IF EXISTS sk")
                 # keys -3, 7, 12 (range 16), values i - 500
                 q(c, f"CREATE TABLE sk AS SELECT CASE WHEN i % 3 = 0 THEN -3 WHEN i % 3 = 1 THEN 7 ELSE 12 END AS k, "
-                     f"i - 500 AS v FROM range({n}) tbl(i)")
+                     f"i - 500 AS v, CAST(i - 500 AS DECIMAL(15,2)) AS d FROM range({n}) tbl(i)")
                 exp = {}
                 for kk, r in ((-3, 0), (7, 1), (12, 2)):
                     vals = [i - 500 for i in range(r, n, 3)]
@@ -519,6 +519,12 @@ def test_groupby_direct_sparse_keys_count_on_device(mbx, oracle, monkeypatch):
                 a = c.query_arrow("SELECT k, COUNT(*) FROM sk GROUP BY k").value
                 assert a.row_count() == len(keys)
                 a.close()
+                # no group at all (a fused predicate no row passes): the count 0 trims every slot
+                r = q(c, "SELECT k, COUNT(*), SUM(v) FROM sk WHERE v > 1000000000000 GROUP BY k")
+                assert r.rows == [] and len(r.columns) == 3
+                # DECIMAL sums (16-byte results) through the same trimmed copy
+                r = q(c, "SELECT k, SUM(d) FROM sk GROUP BY k").rows
+                assert [(int(x[0]), x[1]) for x in r] == [(kk, f"{exp[kk][0]}.00") for kk in keys]
     finally:
         c.close()
 
