@@ -330,10 +330,15 @@ def pmc_traffic_entry(kernel, n):
     pmc = os.path.join(HERE, "profiles", "pmc_traffic.json")
     src = {"file": "profiles/pmc_traffic.json", "entry": kernel}
     try:
-        ent = json.load(open(pmc)).get(kernel)
+        table = json.load(open(pmc))
     except Exception as ex:  # noqa: BLE001
         src["why_null"] = f"unreadable: {ex}"
         return None, src
+    # a row count other than the default 1e9 has its own entry ("<kernel>@<rows>", e.g. C5's shard)
+    if n != 1_000_000_000 and f"{kernel}@{n}" in table:
+        kernel = f"{kernel}@{n}"
+        src["entry"] = kernel
+    ent = table.get(kernel)
     if not ent:
         src["why_null"] = "no entry for this kernel"
         return None, src

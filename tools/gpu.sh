@@ -8,6 +8,7 @@
 #   layout    tools/c3_layout_probe.py                     rehearse  2 gloo ranks on one GPU (--ranks)
 #   prof      rocprofv3 --kernel-trace --stats of bench.py (c2 line with extras)
 #   pmc       rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes of bench.py (one counter set per run)
+#   pmc5      the same passes of bench.py --config c5 (1.25e9 rows per launch)
 #   link      tools/link8_probe (8 MB D2H variants; build it first: see its header)
 #   pmcshape  rocprofv3 kernel trace + FETCH_SIZE / WRITE_SIZE of tools/shape_bench.py (PMC_SHAPES)
 #   clock     C3 / C2 / two-array ring with in-kernel clock stamps at 4 launch cadences (tools/c3_clock.py;
@@ -67,6 +68,12 @@ if has pmc; then
   mkdir -p gpurun_out/pmc
   for ctr in FETCH_SIZE WRITE_SIZE; do
     ( cd /tmp && export TMPDIR=/tmp && timeout -s KILL 300 rocprofv3 --pmc $ctr --output-format csv -d $R/gpurun_out/pmc/$ctr -o $ctr -- python3 $R/bench.py --steps 5 --warmup 1 --no-cpu > $R/gpurun_out/pmc_$ctr.log 2>&1 ) || exit 22
+  done
+fi
+if has pmc5; then  # the same two passes of the C5 line (1.25e9 rows per launch: the filter_agg@1250000000 entry)
+  mkdir -p gpurun_out/pmc5
+  for ctr in FETCH_SIZE WRITE_SIZE; do
+    ( cd /tmp && export TMPDIR=/tmp && timeout -s KILL 300 rocprofv3 --pmc $ctr --output-format csv -d $R/gpurun_out/pmc5/$ctr -o $ctr -- python3 $R/bench.py --config c5 --steps 5 --warmup 1 --no-cpu > $R/gpurun_out/pmc5_$ctr.log 2>&1 ) || exit 33
   done
 fi
 if has pmcshape; then  # kernel trace + FETCH_SIZE / WRITE_SIZE passes of tools/shape_bench.py (PMC_SHAPES, 1e9 rows)

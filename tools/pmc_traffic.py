@@ -7,6 +7,8 @@ gfx950 correction (MI355X_MICROARCH.md §HBM): FETCH_SIZE is reported in KB and
 counts exactly half the bytes of a wide (16 B/lane) coalesced streaming read,
 so hbm_bytes = FETCH_SIZE * 1024 * 2.  WRITE_SIZE is exact for 16 B/lane
 stores (x1024).  Usage: pmc_traffic.py <counter_collection.csv> <kernel-key=substring> ...
+A key "<kernel>@<rows>" records a launch over that many rows (bench.py reads it
+for lines at that size, e.g. filter_agg@1250000000 for C5).
 
 Every entry it writes carries its provenance: the sha256 of the kernel and
 executor sources it was measured with (csrc_digest(), the same digest
@@ -58,6 +60,8 @@ def main():
             e["hbm_write_bytes_per_launch"] = w * 1024
         e["hbm_bytes_per_launch"] = e.get("hbm_read_bytes_per_launch", 0) + e.get("hbm_write_bytes_per_launch", 0)
         e["correction"] = "FETCH_SIZE x1024 x2 (gfx950 half-count of 16B/lane streaming reads), WRITE_SIZE x1024"
+        if "@" in key:  # "<kernel>@<rows>": measured at that row count per launch
+            e["rows"] = int(key.split("@", 1)[1])
         e["csrc_sha256"] = csrc_digest()
         e["git_head"] = git_head()
         e["date"] = datetime.date.today().isoformat()
