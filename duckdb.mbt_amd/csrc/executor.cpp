@@ -183,11 +183,15 @@ struct Engine {
   std::vector<QueryProfile::Kernel> shard_kernels;
   std::vector<std::pair<hipEvent_t, hipEvent_t>> ev_pool;  // reused across queries
   size_t ev_used = 0;
+  // The per-kernel profile's event pairs: timing only (FinishProfile reads them
+  // after a stream synchronisation), so without the system-scope fence a
+  // recorded event otherwise performs (an L2 writeback and invalidate around
+  // each timestamp, which also delays the next launch on the stream)
   std::pair<hipEvent_t, hipEvent_t> NextEvents() {
     if (ev_used == ev_pool.size()) {
       hipEvent_t a, b;
-      (void)hipEventCreate(&a);
-      (void)hipEventCreate(&b);
+      (void)hipEventCreateWithFlags(&a, hipEventDisableSystemFence);
+      (void)hipEventCreateWithFlags(&b, hipEventDisableSystemFence);
       ev_pool.push_back({a, b});
     }
     return ev_pool[ev_used++];
