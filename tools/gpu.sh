@@ -17,6 +17,9 @@
 #   apitrace  HIP API + kernel trace of the C2 query loop at 1e6 rows (tools/query_overhead.py)
 #   rccl      the RCCL-combine loopback tests and the sharded tests
 #   gpuonly   the -m gpu suite alone (as tests, no smoke)
+#   gdab      C3 table flush A/B (records vs global atomics), alone and in the C2 line
+#   overheadq per-query overhead of the C2 / C3 shapes at 1e6 rows (tools/query_overhead.py)
+#   profcost  the per-kernel event profile's cost on the C2 query (tools/profile_cost.py)
 # Results go to gpurun_out/ (merged back by gpurun); copy what is judged into profiles/.
 set -o pipefail
 mkdir -p gpurun_out
@@ -107,6 +110,26 @@ if has rccl; then
 fi
 if has gpuonly; then
   timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > gpurun_out/gpu_tests.log 2>&1 || exit 32
+fi
+if has gdab; then  # C3 table flush A/B: per-workgroup records (default) vs global atomics (MBX_GD_ATOMIC_FLUSH=1),
+  # alternated, alone (--config c3) and inside the C2 line; results in gpurun_out/gd/
+  mkdir -p gpurun_out/gd
+  for rep in 1 2; do
+    for m in parts atomic; do
+      if [ $m = atomic ]; then X="MBX_EXPERIMENTS=1 MBX_GD_ATOMIC_FLUSH=1"; else X=""; fi
+      env $X timeout -k 10 200 python bench.py --config c3 --steps 60 --warmup 5 --no-cpu --extra "" > gpurun_out/gd/c3_${m}_$rep.json 2> gpurun_out/gd/c3_${m}_$rep.err || exit 34
+      env $X timeout -k 10 300 python bench.py --no-cpu --steps 20 > gpurun_out/gd/c2line_${m}_$rep.json 2> gpurun_out/gd/c2line_${m}_$rep.err || exit 35
+    done
+  done
+fi
+if has overheadq; then  # per-query overhead of the C2 and C3 shapes at 1e6 rows (tools/query_overhead.py), twice
+  mkdir -p gpurun_out/qo
+  for rep in 1 2; do
+    timeout -k 10 100 python tools/query_overhead.py 1000000 > gpurun_out/qo/qo_$rep.json 2> gpurun_out/qo/qo_$rep.err || exit 36
+  done
+fi
+if has profcost; then  # what the per-kernel event profile costs the C2 query (tools/profile_cost.py)
+  timeout -k 10 300 python tools/profile_cost.py > gpurun_out/profile_cost.json 2> gpurun_out/profile_cost.err || exit 37
 fi
 if has link; then
   timeout -k 10 200 ./tools/link8_probe ${LINK_MB:-8} 200 > gpurun_out/link8_probe.log 2>&1 || exit 23
