@@ -2,9 +2,8 @@
 """A/B sweep of the fused GROUP BY (group_direct) launch variants on the C3
 table in ONE process: interleaved rounds, median/min kernel time.  GPU only.
 Variants: MBX_GD_VARIANT = "d<depth>_g<blocks per CU>" (LDS-DMA) or "seg",
-with options "+r<replicas>",
-"+h2" (two 256-row sub-steps per wave step) and "+x1" (XCD-grouped step
-windows)."""
+with options "+r<replicas>", "+x1" (XCD-grouped step windows) and "+atomic"
+(the table flush through global atomics instead of per-workgroup records)."""
 import json
 import os
 import statistics
@@ -34,11 +33,11 @@ for name, sql in sqls.items():
         for v in (variants if rnd % 2 == 0 else variants[::-1]):
             os.environ["MBX_GD_VARIANT"] = v.split("+")[0]
             os.environ.pop("MBX_GD_R", None)
-            os.environ.pop("MBX_GD_H", None)
             os.environ.pop("MBX_GD_XCD", None)
+            os.environ.pop("MBX_GD_ATOMIC_FLUSH", None)
             for opt in v.split("+")[1:]:
-                if opt.startswith("h"):
-                    os.environ["MBX_GD_H"] = opt[1:]  # h2: two 256-row sub-steps per wave step
+                if opt == "atomic":
+                    os.environ["MBX_GD_ATOMIC_FLUSH"] = "1"  # the table flush through global atomics
                 if opt.startswith("x"):
                     os.environ["MBX_GD_XCD"] = opt[1:]  # x1: XCD-grouped step windows
                 if opt.startswith("r"):
