@@ -415,6 +415,13 @@ def run_inlib(args, world, rank, vote=None):
             return None
     import torch
     mbx = load_mbx()
+    selftest = None
+    if plan["ngpu"] > 1:
+        # the RCCL calls of the combine over every GPU of the run, before any
+        # table exists: a fresh ncclCommInitAll over devices 0..N-1 and the
+        # multi-rank reduce / all-gather check, with what RCCL reports per rank
+        selftest = guarded(lambda: mbx.rccl_selftest(list(range(plan["ngpu"]))), RCCL_LEG_TIMEOUT_S)
+        log(f"[bench] rccl self-test over devices 0..{plan['ngpu'] - 1}: {json.dumps(selftest)}")
     cfg = mbx.Config.create()
     if plan["nshards"] > 1:
         cfg.set("gpu_devices", ",".join(map(str, plan["devices"])))
@@ -445,9 +452,7 @@ def run_inlib(args, world, rank, vote=None):
         out = decode_c3(out)
         sr_out = sel_outcomes(conn, sr0)
         cb1 = conn.rccl_stats()
-        cb_out = {"ran_rccl_steps": cb1["rccl_combines"] - cb0["rccl_combines"],
-                  "host_merge_steps": cb1["rccl_fallbacks"] - cb0["rccl_fallbacks"], "note": cb1["note"],
-                  "rccl_timeouts": cb1["rccl_timeouts"], "last_collective_d2h_us": cb1["last_rccl_us"]}
+        cb_out = combine_delta(cb0, cb1)
     except Exception as ex:  # noqa: BLE001 - a shard's error names the shard and its device
         fail(dist, f"query failed: {ex}")
     kern = conn.profile_drain()
@@ -486,15 +491,24 @@ def run_inlib(args, world, rank, vote=None):
                      if plan["shards_per_gpu"] > 1 else "one shard per device")}
         md["split_us"] = overhead_split(conn, step, 10)
         if shard_par is not None:
-            md["shard_parity"] = shard_par
-        if args.config in ("c2", "c2d", "c5"):
-            # the timed loop ran the library's default combine (RCCL over the
-            # shard devices when they are distinct); the other mode is timed after
-            md["combine"] = {"timed_loop": cb_out, "mode": "rccl" if cb_out["ran_rccl_steps"] else "host merge"}
+            md["shard_parity"] = [{k: v for k, v in e.items() if k != "oracle"} for e in shard_par]
+        # the timed loop ran the library's default combine (RCCL over the shard
+        # devices when they are distinct): which collective every step ran, and
+        # the communicators as RCCL reports them (rank count and rank of each)
+        md["combine"] = {"timed_loop": cb_out, "mode": "rccl" if cb_out["ran_rccl_steps"] else "host merge",
+                         "rccl": rccl_evidence(conn.rccl_info(), plan["devices"])}
+        if selftest is not None:
+            md["rccl_selftest"] = selftest
+        if args.config in ("c2", "c2d", "c5", "c3"):
+            # the other mode, timed right after
             md["combine_ab"] = guarded(
                 lambda: combine_leg(conn, step, args, n_total, "host" if cb_out["ran_rccl_steps"] else "rccl"),
                 RCCL_LEG_TIMEOUT_S)
             stuck = md["combine_ab"].get("error", "").startswith("timeout")
+        if not stuck and plan["ngpu"] > 1 and args.config in ("c2", "c2d", "c5", "c3") and shard_par is not None:
+            # the 1 -> N curve from this one run: the same query over device
+            # prefixes 1, 2, 4 ... of 0..N-1, each its own connection and table
+            md["curve"] = guarded(lambda: curve_legs(mbx, args, plan, result, shard_par), CURVE_TIMEOUT_S)
         result["multi_device"] = md
     calibrate_into(conn, result, args.config)
     if args.config == "sel":
@@ -523,7 +537,7 @@ def run_inlib(args, world, rank, vote=None):
         # the RCCL calls of the in-library combine, on this one-GPU box: a one-rank
         # communicator, a grouped reduce and all-gather (outside the timed loop)
         try:
-            result["extra"]["rccl_selftest"] = mbx.rccl_selftest(0)
+            result["extra"]["rccl_selftest"] = mbx.rccl_selftest([0])
         except Exception as ex:  # noqa: BLE001
             result["extra"]["rccl_selftest"] = {"ok": False, "error": str(ex)}
     if not args.no_cpu and plan["nshards"] == 1 and args.config in ("c2", "c2d", "c3", "c5", "sel"):
@@ -552,6 +566,153 @@ def run_inlib(args, world, rank, vote=None):
 
 
 RCCL_LEG_TIMEOUT_S = float(os.environ.get("MBX_BENCH_RCCL_TIMEOUT_S", "120"))
+CURVE_TIMEOUT_S = float(os.environ.get("MBX_BENCH_CURVE_TIMEOUT_S", "300"))
+
+
+ZERO_RCCL_STATS = {"rccl_combines": 0, "rccl_reduces": 0, "rccl_allgathers": 0, "rccl_fallbacks": 0,
+                   "rccl_unsupported": 0, "rccl_timeouts": 0, "last_rccl_us": 0.0, "note": ""}
+
+
+def combine_delta(cb0, cb1):
+    """What the combine did between two rccl_stats() snapshots: steps RCCL
+    combined (and with which collective), steps that fell back to the host
+    merge (RCCL should have run) and steps whose shape RCCL never covers."""
+    d = lambda k: cb1[k] - cb0[k]  # noqa: E731
+    return {"ran_rccl_steps": d("rccl_combines"), "ncclReduce_steps": d("rccl_reduces"),
+            "ncclAllGather_steps": d("rccl_allgathers"), "host_merge_steps": d("rccl_fallbacks") + d("rccl_unsupported"),
+            "fallback_steps": d("rccl_fallbacks"), "unsupported_steps": d("rccl_unsupported"),
+            "note": cb1["note"], "rccl_timeouts": cb1["rccl_timeouts"],
+            "last_collective_d2h_us": cb1["last_rccl_us"]}
+
+
+def rccl_evidence(info, devices):
+    """The connection's communicators as RCCL reports them (duckdb_mbx_rccl_info)
+    and whether they prove an N-rank RCCL: every rank's ncclCommCount equal to
+    the number of distinct shard devices and its ncclCommUserRank its index."""
+    ranks = info.get("ranks") or []
+    n = len(devices)
+    info = dict(info)
+    info["saw_nranks"] = sorted({r["count"] for r in ranks}) if ranks else []
+    info["proves_n_ranks"] = (len(ranks) == n and len(set(devices)) == n and
+                              all(r["count"] == n and r["user_rank"] == i for i, r in enumerate(ranks)))
+    return info
+
+
+def curve_legs(mbx, args, plan, result, shard_par):
+    """The 1 -> N scaling points from one N-GPU process: for every power-of-two
+    prefix p < N of devices 0..N-1 (each listed --shards-per-gpu times), its
+    own connection and a table of p x rows-per-GPU rows (the same rows as the
+    headline's first p x S shards), warmup, K timed steps, the kernel's HIP
+    events, and parity: the global answer and every shard's partial against
+    the oracle values the headline's shard parity already computed over those
+    same row ranges.  The headline's own N point closes the curve."""
+    import torch
+    curve = []
+    for p, devices in curve_points(plan["ngpu"], plan["shards_per_gpu"]):
+        nsh = len(devices)
+        n = args.rows * p
+        cfg = mbx.Config.create()
+        if nsh > 1:
+            cfg.set("gpu_devices", ",".join(map(str, devices)))
+        else:
+            cfg.set("gpu_device", "0")
+        cfg.set("mbx_profile", "true")
+        r = mbx.connect_with_config(cfg)
+        if isinstance(r, mbx.Err):
+            curve.append({"gpus": p, "error": r.error.message})
+            continue
+        conn = r.value
+        try:
+            w = workload(args.config, 0, n)
+            res = conn.query(w["setup"])
+            if isinstance(res, mbx.Err):
+                raise RuntimeError(res.error.message)
+            step = make_step(conn, args.config, w["sql"], decode=False)
+            for _ in range(args.warmup):
+                step()
+            conn.profile_drain()
+            cb0 = conn.rccl_stats()
+            elapsed, out = time_steps(step, args.steps, 0, None, torch.cuda.synchronize)
+            out = decode_c3(out)
+            cb1 = conn.rccl_stats()
+            avg_k, step_k, _ = kernel_stats(conn, w["kernel"], nsh, args.steps)
+            exp = shard_par[:nsh]
+            if args.config == "c3":
+                groups = {}
+                for e in exp:
+                    for k, c_, s_ in e["oracle"]:
+                        gc, gs = groups.get(k, (0, 0))
+                        groups[k] = (gc + c_, gs + s_)
+                want = [(k, groups[k][0], groups[k][1]) for k in sorted(groups)]
+                got = sorted(out, key=lambda g: (g[0] is None, g[0]))
+                par = {"groups": len(got), "oracle_groups": len(want), "match": got == want}
+            else:
+                oc = sum(e["oracle_count"] for e in exp)
+                par = {"gpu_count": int(out[0]), "oracle_count": oc, "match": int(out[0]) == oc}
+                if args.config == "c5":
+                    osum = sum(e["oracle_sum"] for e in exp)
+                    par.update({"gpu_sum": int(out[1]), "oracle_sum": osum,
+                                "match": par["match"] and int(out[1]) == osum})
+            if nsh > 1:
+                sp = shard_partials_vs(conn, args.config, exp)
+                par["shards_match"] = all(x["match"] for x in sp)
+                par["match"] = par["match"] and par["shards_match"]
+            pt = {"gpus": p, "shards": nsh, "devices": devices, "rows": n, "ms_per_step": elapsed / args.steps * 1e3,
+                  "value": n * args.steps / elapsed, "unit": "rows/s", "kernel_ms_avg": avg_k,
+                  "slowest_shard_kernel_ms_per_step": step_k, "parity": par,
+                  "combine": combine_delta(cb0, cb1)}
+            if nsh > 1:
+                pt["rccl"] = rccl_evidence(conn.rccl_info(), devices)
+            curve.append(pt)
+        except Exception as ex:  # noqa: BLE001 - one point must not lose the others
+            curve.append({"gpus": p, "error": str(ex)})
+        finally:
+            conn.close()
+    curve.append({"gpus": plan["ngpu"], "shards": plan["nshards"], "devices": plan["devices"],
+                  "rows": plan["rows_total"], "ms_per_step": result["ms_per_step"], "value": result["value"],
+                  "unit": "rows/s", "kernel_ms_avg": result["roofline"]["kernel_ms_avg"],
+                  "parity": {"match": result["parity"].get("match")}, "the_headline": True})
+    base = next((c["value"] for c in curve if c.get("gpus") == 1 and c.get("value")), None)
+    for c in curve:
+        if base and c.get("value"):
+            c["speedup_vs_1"] = c["value"] / base
+    return {"points": curve, "scaling": "weak (rows per GPU fixed)",
+            "definition": "one process; each point its own connection over devices 0..p-1 and table of p x rows "
+                          "per GPU, the same clock discipline as the headline (warmup, K timed steps, "
+                          "synchronised); parity against the headline's per-shard oracle values"}
+
+
+def curve_points(ngpu, spg):
+    """The curve's prefixes below the headline's N: (p, gpu_devices list) for
+    p = 1, 2, 4, ... < N, each device listed spg times."""
+    pts, p = [], 1
+    while p < ngpu:
+        pts.append((p, [d for d in range(p) for _ in range(spg)]))
+        p *= 2
+    return pts
+
+
+def shard_partials_vs(conn, config, exp):
+    """Every shard's partial (duckdb_mbx_shard_partial) of the last sharded
+    aggregate against its oracle entry (sharded_parity's)."""
+    outp = []
+    for i, e in enumerate(exp):
+        rr = conn.shard_partial(i)
+        if rr is None:
+            outp.append({"shard": i, "match": False, "error": "no partial"})
+            continue
+        if config == "c3":
+            rows, nulls = rr.cells()
+            got = sorted((None if nl[0] else int(rw[0]), int(rw[2]), None if nl[1] else int(rw[1]))
+                         for rw, nl in zip(rows, nulls))
+            ok = got == e["oracle"]
+        else:
+            ok = int(rr.value(0, 0)) == e["oracle_count"]
+            if config == "c5":
+                ok = ok and int(rr.value(1, 0)) == e["oracle_sum"]
+        rr.close()
+        outp.append({"shard": i, "match": ok})
+    return outp
 
 
 def guarded(fn, timeout_s):
@@ -640,15 +801,6 @@ def sharded_parity(conn, config, out, n_total, nshards, threads):
     from oracle import Oracle
     orc = Oracle()
     shard_par, g_cnt, g_sum, g_groups = [], 0, 0, {}
-    probe = conn.shard_partial(0)
-    if probe is None:
-        # the RCCL reduce (COUNT-only rows) leaves no per-shard partials on
-        # the host: one more step with the host merge brings them back
-        conn.set_combine("host")
-        conn.query_raw(f"SELECT COUNT(*) FROM t WHERE x > 24").close()
-        conn.set_combine("rccl")
-    else:
-        probe.close()
     for i in range(nshards):
         lo, hi = n_total * i // nshards, n_total * (i + 1) // nshards
         rr = conn.shard_partial(i)
@@ -663,7 +815,8 @@ def sharded_parity(conn, config, out, n_total, nshards, threads):
                 rows, nulls = rr.cells()
                 got = sorted((None if nl[0] else int(rw[0]), int(rw[2]), None if nl[1] else int(rw[1]))
                              for rw, nl in zip(rows, nulls))
-            shard_par.append({"shard": i, "rows": [lo, hi], "groups": len(got or []), "match": got == exp})
+            shard_par.append({"shard": i, "rows": [lo, hi], "groups": len(got or []), "match": got == exp,
+                              "oracle": exp})
         else:
             oc, osum = orc.synth_filter_count(42, lo, hi - lo, 50, 1, 25, 2**63 - 1, threads)
             g_cnt += oc
@@ -698,6 +851,7 @@ def combine_leg(conn, step, args, n_total, mode):
     same-device shards RCCL cannot run (one rank per device) and the library
     falls back to the host merge: reported as such."""
     import torch
+    before = conn.rccl_info().get("mode", "rccl")
     try:
         conn.set_combine(mode)
         for _ in range(max(1, args.warmup)):
@@ -708,17 +862,16 @@ def combine_leg(conn, step, args, n_total, mode):
         out = decode_c3(out)
         st1 = conn.rccl_stats()
         conn.profile_drain()
-        conn.set_combine("rccl")
-        exp = decode_c3(step())  # the product default again: the headline mode's answer over the same rows
-        return {"mode": mode, "ran_rccl_steps": st1["rccl_combines"] - st0["rccl_combines"],
-                "fell_back_steps": st1["rccl_fallbacks"] - st0["rccl_fallbacks"],
-                "note": st1["note"], "ms_per_step": elapsed / args.steps * 1e3,
+        conn.set_combine(before)
+        exp = decode_c3(step())  # the headline mode again: its answer over the same rows
+        return {"mode": mode, "headline_mode": before, **combine_delta(st0, st1),
+                "ms_per_step": elapsed / args.steps * 1e3,
                 "value": n_total * args.steps / elapsed, "unit": "rows/s",
                 "last_collective_d2h_us": st1["last_rccl_us"],
                 "parity": {mode: [str(x) for x in out], "default": [str(x) for x in exp],
                            "match": [str(x) for x in out] == [str(x) for x in exp]}}
     except Exception as ex:  # noqa: BLE001 - the second leg must not lose the headline line
-        conn.set_combine("rccl")
+        conn.set_combine(before)
         return {"error": str(ex)}
 
 
@@ -1008,15 +1161,30 @@ def dry_run(args, world, rank, form=None, vote=None):
             par = f"row-range shards x{world}" + (" + RCCL all-reduce/all-gather" if world > 1 else "")
             if vote:
                 par += " [one process per GPU: " + vote["reason"] + "]"
+            md = None
         else:
             plan = inlib_plan(args, world)
             mode, ngpu, devices, par = "in-library", plan["ngpu"], plan["devices"], plan["parallelism"]
+            md = None
+            if ngpu > 1:
+                # what the real N > 1 line adds under multi_device (filled by a GPU run)
+                md = {"rccl_selftest": {"devices": list(range(ngpu)), "before": "the connection and the timed loop"},
+                      "combine": {"timed_loop": sorted(combine_delta(ZERO_RCCL_STATS, ZERO_RCCL_STATS)),
+                                  "rccl": ["state", "prepared_at_connect", "init_s", "check_us", "first_wait_ms",
+                                           "ranks[].count", "ranks[].user_rank", "ranks[].cu_device",
+                                           "saw_nranks", "proves_n_ranks", "last_collective"]},
+                      "curve": {"points": [{"gpus": p, "devices": d} for p, d in
+                                           curve_points(ngpu, plan["shards_per_gpu"])]
+                                + [{"gpus": ngpu, "devices": plan["devices"], "the_headline": True}]}}
         cfg = {"workload": args.config, "rows_per_gpu": args.rows, "parallelism": par}
         if vote:
             cfg["form"] = vote
-        print(json.dumps({"metric": METRIC, "value": None, "unit": "rows/s", "n_gpus": ngpu,
-                          "dry_run": True, "mode": mode, "processes": world, "rank_id_sum": int(t.item()),
-                          "gpu_devices": devices, "config": cfg}), flush=True)
+        line = {"metric": METRIC, "value": None, "unit": "rows/s", "n_gpus": ngpu,
+                "dry_run": True, "mode": mode, "processes": world, "rank_id_sum": int(t.item()),
+                "gpu_devices": devices, "config": cfg}
+        if md:
+            line["multi_device_plan"] = md
+        print(json.dumps(line), flush=True)
 
 
 def free_port():

@@ -83,6 +83,8 @@ _sig("duckdb_mbx_hbm_calibrate_ex", _I, _P, _L, _I, ctypes.POINTER(ctypes.c_doub
 _sig("duckdb_mbx_clock_stamps", _I, _P, ctypes.POINTER(ctypes.c_uint64), _I)
 _sig("duckdb_mbx_set_link_mode", _I, _I)
 _sig("duckdb_mbx_rccl_selftest", _I, _I, ctypes.POINTER(ctypes.c_double))
+_sig("duckdb_mbx_rccl_selftest_ex", ctypes.c_void_p, ctypes.POINTER(ctypes.c_int32), _I)
+_sig("duckdb_mbx_rccl_info", ctypes.c_void_p, _P)
 _sig("duckdb_mbx_link_stats", ctypes.c_void_p)
 _sig("duckdb_mbx_statement_plan_stats", _I, _P, ctypes.POINTER(ctypes.c_int64))
 _sig("duckdb_mbx_shard_stats", _I, _P, ctypes.POINTER(ctypes.c_int64), ctypes.POINTER(ctypes.c_double))
@@ -650,13 +652,25 @@ class Connection:
         out = (ctypes.c_int64 * 2)()
         us = (ctypes.c_double * 1)()
         lib.duckdb_mbx_rccl_stats(self._h, out, us)
-        ex = (ctypes.c_int64 * 6)()
-        lib.duckdb_mbx_rccl_stats_ex(self._h, ex, 6)
+        ex = (ctypes.c_int64 * 9)()
+        lib.duckdb_mbx_rccl_stats_ex(self._h, ex, 9)
         p = lib.duckdb_mbx_rccl_note(self._h)
         note = ctypes.string_at(p).decode()
         lib.duckdb_mbx_free(p)
-        return {"rccl_combines": out[0], "rccl_fallbacks": out[1], "rccl_loopbacks": ex[2], "rccl_errors": ex[3], "rccl_timeouts": ex[4], "rccl_group_combines": ex[5],
-                "last_rccl_us": us[0], "note": note}
+        return {"rccl_combines": out[0], "rccl_fallbacks": out[1], "rccl_loopbacks": ex[2], "rccl_errors": ex[3],
+                "rccl_timeouts": ex[4], "rccl_group_combines": ex[5], "rccl_unsupported": ex[6],
+                "rccl_reduces": ex[7], "rccl_allgathers": ex[8], "last_rccl_us": us[0], "note": note}
+
+    def rccl_info(self) -> dict:
+        """The RCCL combine's communicators (extension): state, whether their
+        open started at connect, its ncclCommInitAll seconds and check us, the
+        first combine's wait, every rank's ncclCommCount / ncclCommUserRank /
+        ncclCommCuDevice, the counters and the last collective."""
+        import json
+        p = lib.duckdb_mbx_rccl_info(self._h)
+        s = ctypes.string_at(p).decode()
+        lib.duckdb_mbx_free(p)
+        return json.loads(s)
 
     def set_combine(self, rccl) -> None:
         """Host merge (False / "host"), RCCL combine (True / "rccl") or, in tests
@@ -721,12 +735,24 @@ class RawResult:
         return buf.raw[:n]
 
 
-def rccl_selftest(device: int = 0) -> dict:
-    """The RCCL calls of the combine on hardware with one GPU (extension): a
-    one-rank communicator, one grouped reduce and one all-gather, checked."""
-    us = (ctypes.c_double * 1)()
-    ok = lib.duckdb_mbx_rccl_selftest(device, us) == 1
-    return {"ok": ok, "us": us[0], "error": "" if ok else _last_error("rccl self-test failed")}
+def rccl_selftest(device=0) -> dict:
+    """The RCCL calls of the combine on hardware (extension): a fresh
+    ncclCommInitAll over `device` (an int: one rank) or a list of distinct
+    devices (one rank each), then the multi-rank check the combine is gated on
+    (one grouped reduce and one all-gather, verified on every rank).  The dict
+    has ok, error, us, and for a device list init_us / check_us and every
+    rank's ncclCommCount / ncclCommUserRank / ncclCommCuDevice."""
+    import json
+    if isinstance(device, int):
+        us = (ctypes.c_double * 1)()
+        ok = lib.duckdb_mbx_rccl_selftest(device, us) == 1
+        return {"ok": ok, "us": us[0], "error": "" if ok else _last_error("rccl self-test failed")}
+    devs = (ctypes.c_int32 * max(1, len(device)))(*device)
+    p = lib.duckdb_mbx_rccl_selftest_ex(devs, len(device))
+    r = json.loads(ctypes.string_at(p).decode())
+    lib.duckdb_mbx_free(p)
+    r["us"] = r.get("total_us")
+    return r
 
 
 def set_link_mode(mode: int) -> None:

@@ -125,11 +125,13 @@ struct Options {
   // "mbx_force_peer" (tests): shards on the same device still exchange row
   // results by peer DMA (hipMemcpyPeerAsync), as distinct devices do
   bool force_peer = false;
-  // "mbx_combine" = "rccl" (default) | "host": a sharded global aggregate over
-  // distinct devices combines its partials with RCCL collectives on the shard
-  // devices (rccl_combine.h); "host" (and every shape or device list RCCL does
-  // not cover: GROUP BY, floating-point partials, same-device shards) merges
-  // the partials on the host
+  // "mbx_combine" = "rccl" (default) | "host": a sharded global aggregate, or
+  // a GROUP BY on one integer key, over distinct devices combines its partials
+  // with RCCL collectives on the shard devices (rccl_combine.h), once the
+  // communicators opened at connect have passed their multi-rank check;
+  // "host" (and every shape or device list RCCL does not cover: floating-point
+  // partials, non-integer or several keys, same-device shards) merges the
+  // partials on the host
   bool combine_rccl = true;
   // "mbx_combine" = "rccl_loopback" (tests only, MBX_EXPERIMENTS=1): the RCCL
   // combine with its two collectives replaced by device copies between the
@@ -141,6 +143,7 @@ struct Options {
 struct Engine;        // per-connection executor state (device stream, scratch)
 namespace rc {
 struct Comms;  // RCCL communicators over the shard devices (rccl_combine.h)
+struct Init;   // their open, in flight on a helper thread
 }
 struct ShardWorkers;  // persistent per-shard host threads (executor.cpp)
 
@@ -164,9 +167,15 @@ struct ShardStats {
   // the per-shard partial relations of the last sharded aggregate, as they
   // came back from each device before the merge (duckdb_mbx_shard_partial)
   std::vector<ResultPtr> last_partials;
-  // mbx_combine=rccl: sharded global aggregates combined by RCCL collectives
-  // on the shard devices instead of the host merge
-  int64_t rccl_combines = 0, rccl_fallbacks = 0;
+  // mbx_combine=rccl: sharded aggregates combined by RCCL collectives on the
+  // shard devices instead of the host merge; fallbacks = combines RCCL should
+  // have run but could not (communicators unavailable, a collective failed or
+  // timed out); unsupported = shapes / layouts it never covers (host merge)
+  int64_t rccl_combines = 0, rccl_fallbacks = 0, rccl_unsupported = 0;
+  int64_t rccl_reduces = 0, rccl_allgathers = 0;  // the collective each combine ran
+  std::string last_collective;
+  bool rccl_prepared_at_connect = false;  // the open started at connect (helper thread)
+  double rccl_first_wait_ms = -1;         // how long the first combine waited for it (-1: not yet)
   int64_t rccl_loopbacks = 0;  // of rccl_combines, through the test loopback
   int64_t rccl_group_combines = 0;  // of rccl_combines, GROUP BY relations
   int64_t rccl_errors = 0;     // combines that raised a shard's device error
@@ -186,7 +195,8 @@ struct Connection {
   // combines their results
   std::vector<std::unique_ptr<Connection>> shards;
   std::shared_ptr<ShardWorkers> workers;  // declared after shards: stopped before they go
-  std::shared_ptr<rc::Comms> rccl;        // mbx_combine=rccl, opened on first use
+  std::shared_ptr<rc::Comms> rccl;        // mbx_combine=rccl: the communicators, once waited for
+  std::shared_ptr<rc::Init> rccl_init;    // their open (started at connect over distinct devices)
   bool rccl_tried = false;
   ShardStats shard_stats;
   int64_t shard_stats_t0 = 0;  // steady-clock ns at the start of the current ForShards
@@ -262,6 +272,11 @@ void HostColumnPush(HostColumn &col, const Value &v);  // v already of col.type 
 void HbmCalibrateConn(Connection &c, int64_t bytes, int iters, double out[8]);
 // in-kernel clock stamps of the last stamped launch (libduckdb_mb_amd_clk.so)
 int ClockStampsConn(Connection &c, uint64_t *out, int cap);
+// the connection's RCCL combine as JSON (duckdb_mbx_rccl_info)
+std::string RcclInfoJson(Connection &c);
+// rc::SelfTest over devs as JSON (duckdb_mbx_rccl_selftest_ex); *err ("" when
+// it passed) and the wall us in *us
+std::string RcclSelfTestJson(const std::vector<int> &devs, std::string *err, double *us);
 // adds this connection's (and its shards') select_rounds counters to out:
 // launches, aborts (a workgroup never scheduled: the two-pass form reran), launch failures
 void EngineCounters(const Connection &c, int64_t out[3]);

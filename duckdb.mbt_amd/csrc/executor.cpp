@@ -4081,19 +4081,70 @@ static bool RcclKinds(const BoundSelect &p, rc::CombineDesc &cd, bool &counts_on
   return true;
 }
 
-// the connection's communicators (opened on first use; the loopback when the
-// test mode asks for it); false and the reason in shard_stats.rccl_note
+static bool DistinctDevices(const std::vector<int> &devs) {
+  for (size_t i = 0; i < devs.size(); i++)
+    for (size_t j = i + 1; j < devs.size(); j++)
+      if (devs[i] == devs[j]) return false;
+  return true;
+}
+
+// Whether the RCCL combine can run over c's shard layout at all (one rank per
+// device: distinct devices, unless the test loopback stands in); false and the
+// reason in shard_stats.rccl_note (counted as rccl_unsupported)
+static bool RcclLayout(Connection &c) {
+  if (c.opts.rccl_loopback || DistinctDevices(c.opts.devices)) return true;
+  c.shard_stats.rccl_note = "shard devices are not distinct (RCCL takes one rank per device): host merge";
+  return false;
+}
+
+// Starts opening the communicators of a sharded connection over distinct
+// devices at connect (mbx_combine=rccl): ncclCommInitAll and its check run on
+// a helper thread while the tables are built, so the first aggregate waits
+// only for what is left (rc::Prepare)
+static void RcclPrepare(Connection &c) {
+  if (!c.opts.combine_rccl || c.opts.rccl_loopback || !DistinctDevices(c.opts.devices)) return;
+  if (!rc::ApiProblem().empty()) return;  // (RcclReady reports it)
+  c.rccl_init = rc::Prepare(c.opts.devices);
+  c.shard_stats.rccl_prepared_at_connect = true;
+}
+
+// the connection's communicators (the open started at connect, or now; the
+// loopback when the test mode asks for it); false and the reason in
+// shard_stats.rccl_note
 static bool RcclReady(Connection &c) {
   ShardStats &st = c.shard_stats;
   if (c.rccl && rc::IsLoopback(*c.rccl) != c.opts.rccl_loopback) c.rccl.reset(), c.rccl_tried = false;
+  if (c.rccl && c.rccl->dead) {  // failed on another connection sharing them: host merge from now on
+    c.rccl.reset();
+    st.rccl_note = "RCCL communicators of these devices failed earlier in this process: host merge";
+    return false;
+  }
   if (!c.rccl_tried) {
     c.rccl_tried = true;
     std::string note;
-    c.rccl = rc::Open(c.opts.devices, c.opts.rccl_loopback, &note);
+    if (c.opts.rccl_loopback) {
+      c.rccl = rc::OpenLoopback(c.opts.devices);
+    } else {
+      note = rc::ApiProblem();
+      if (note.empty()) {
+        if (!c.rccl_init) c.rccl_init = rc::Prepare(c.opts.devices);
+        double waited = 0;
+        c.rccl = rc::Wait(c.rccl_init, &note, &waited);
+        st.rccl_first_wait_ms = waited;
+      }
+    }
     if (!c.rccl) st.rccl_note = note;
   }
   if (!c.rccl && st.rccl_note.empty()) st.rccl_note = "RCCL unavailable";
   return c.rccl != nullptr;
+}
+
+// what the last combine ran (duckdb_mbx_rccl_info)
+static void CountCollective(Connection &c, bool reduce) {
+  ShardStats &st = c.shard_stats;
+  (reduce ? st.rccl_reduces : st.rccl_allgathers)++;
+  st.last_collective = std::string(c.rccl->loopback ? "loopback " : "") +
+                       (reduce ? "ncclReduce (int64 sum to device 0)" : "ncclAllGather");
 }
 
 // Waits (bounded) for every rank's stream after a collective; false when it
@@ -4114,7 +4165,7 @@ static bool RcclWait(Connection &c, const std::vector<hipStream_t> &streams,
       continue;
     }
     if (std::chrono::steady_clock::now() > deadline) {
-      rc::Abort(*c.rccl);
+      rc::Abort(*c.rccl, "an RCCL collective did not complete within " + std::to_string(timeout_ms) + " ms");
       for (size_t k = 0; k < streams.size(); k++) {
         Eng(*c.shards[k]);
         (void)hipStreamSynchronize(streams[k]);
@@ -4141,12 +4192,18 @@ static bool ShardedAggregateRccl(Connection &c, const BoundSelect &s, const Boun
     st.rccl_note = why;
     return false;
   };
+  auto unsupported = [&](const std::string &why) {  // a shape or layout RCCL never combines
+    st.rccl_unsupported++;
+    st.rccl_note = why;
+    return false;
+  };
   if (!s.groups.empty()) return false;  // (GROUP BY: ShardedAggregateRows, GroupRcclCombine)
   const int ncols = (int)p.aggs.size();
   rc::CombineDesc cd;
   bool counts_only = true;
   std::string why;
-  if (!RcclKinds(p, cd, counts_only, &why)) return fallback(why);
+  if (!RcclLayout(c)) return unsupported(st.rccl_note);
+  if (!RcclKinds(p, cd, counts_only, &why)) return unsupported(why);
   if (!RcclReady(c)) return fallback(st.rccl_note);
   const Table &t = *s.src.table;
   const int nsh = (int)t.parts.size();
@@ -4187,7 +4244,9 @@ static bool ShardedAggregateRccl(Connection &c, const BoundSelect &s, const Boun
     sendb[i] = Alloc(se, (size_t)P * 8);
     recvb[i] = Alloc(se, recv_lanes * 8);
     if (counts_only && c.rccl->loopback && i == 0) scrb[i] = Alloc(se, (size_t)nsh * P * 8);
-    if (i == 0 && !se.EnsurePinned(host.size() * 8)) ThrowError("IO", "RCCL combine: pinned staging");
+    // shard 0: the combined lanes (+ its own counts); every other shard: its counts (reduce form)
+    if (!se.EnsurePinned(i == 0 ? (host.size() + P) * 8 : (size_t)P * 8))
+      ThrowError("IO", "RCCL combine: pinned staging");
     rc::Pack(pd, (int64_t *)sendb[i]->p, se.stream);
     HIPCHK(hipGetLastError());
     MarkLaunched(c, i);
@@ -4204,18 +4263,27 @@ static bool ShardedAggregateRccl(Connection &c, const BoundSelect &s, const Boun
     streams[i] = c.shards[i]->engine->stream;
   }
   std::string cerr;
-  const bool cok = rc::Collective(*c.rccl, counts_only, sp, rp, xp, streams, (size_t)P, &cerr);
+  // connections over the same devices share the communicators: one collective
+  // (and its wait) at a time; `comms` keeps them alive if RcclWait drops them
+  const std::shared_ptr<rc::Comms> comms = c.rccl;
+  std::unique_lock<std::mutex> coll_lock(comms->mu);
+  const bool cok = rc::Collective(*comms, counts_only, sp, rp, xp, streams, (size_t)P, &cerr);
   // A collective that does not complete in time (a rank that cannot reach the
   // others, a broken link) must not hang the connection: the communicators
   // are aborted and the host merge answers this statement and the next ones.
   // The wait is bounded also when the group reported an error: some ranks'
   // parts may have been enqueued before it.
   if (!RcclWait(c, streams, tc0)) {
+    coll_lock.unlock();
     for (int k = 0; k < nsh; k++) sendb[k].reset(), recvb[k].reset(), scrb[k].reset(), rel[k] = DRel();
     return fallback(st.rccl_note);
   }
+  coll_lock.unlock();
   // Phase 3: device 0 finishes (combine kernel, one D2H); every rank's stream
-  // is drained before its lane buffers go back to its pool
+  // is drained before its lane buffers go back to its pool.  The reduce form
+  // also reads back each rank's own counts (its partial row), in the D2H that
+  // drains it.
+  std::vector<int64_t> own(counts_only ? (size_t)nsh * P : 0);
   std::exception_ptr first_err;
   for (int i = 0; i < nsh; i++) {
     Engine &se = Eng(*c.shards[i]);
@@ -4231,11 +4299,18 @@ static bool ShardedAggregateRccl(Connection &c, const BoundSelect &s, const Boun
         if (out)
           HIPCHK(hipMemcpyAsync(se.h_pinned + recv_lanes * 8, out->p, (size_t)3 * ncols * 8, hipMemcpyDeviceToHost,
                                 se.stream));
+        if (counts_only)
+          HIPCHK(hipMemcpyAsync(se.h_pinned + host.size() * 8, sendb[0]->p, (size_t)P * 8, hipMemcpyDeviceToHost,
+                                se.stream));
         HIPCHK(hipStreamSynchronize(se.stream));  // every rank's part of the collective has landed
         memcpy(host.data(), se.h_pinned, host.size() * 8);
+        if (counts_only) memcpy(own.data(), se.h_pinned + host.size() * 8, (size_t)P * 8);
         out.reset();
       } else {
+        if (cok && counts_only)
+          HIPCHK(hipMemcpyAsync(se.h_pinned, sendb[i]->p, (size_t)P * 8, hipMemcpyDeviceToHost, se.stream));
         HIPCHK(hipStreamSynchronize(se.stream));
+        if (cok && counts_only) memcpy(own.data() + (size_t)i * P, se.h_pinned, (size_t)P * 8);
       }
       ShardCollect(e, se, i, true);
     } catch (...) {
@@ -4248,18 +4323,18 @@ static bool ShardedAggregateRccl(Connection &c, const BoundSelect &s, const Boun
   const double t_coll = std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - tc0).count();
   if (first_err) std::rethrow_exception(first_err);
   if (!cok) {  // the host merge recomputes the partials, for this statement and the next ones
+    const std::string why = "RCCL collective failed (" + cerr + "): communicators dropped, host merge from now on";
+    rc::MarkDead(*c.rccl, why);
     c.rccl.reset();
-    return fallback("RCCL collective failed (" + cerr + "): communicators dropped, host merge from now on");
+    return fallback(why);
   }
+  CountCollective(c, counts_only);
   const auto t_merge = std::chrono::steady_clock::now();
   // every rank's device error word, raised as that shard's error; every
   // shard that reported one is cleared, so no stale error reaches its next query
   std::vector<int32_t> errs(nsh, 0);
   if (counts_only) {
-    if (host[(size_t)P - 1]) {  // the summed words only say some shard failed: read each one
-      for (int k = 0; k < nsh; k++) errs[k] = ReadDev<int32_t>(Eng(*c.shards[k]), c.shards[k]->engine->d_err);
-      Eng(c);
-    }
+    for (int i = 0; i < nsh; i++) errs[i] = (int32_t)own[(size_t)i * P + P - 1];
   } else {
     for (int i = 0; i < nsh; i++) errs[i] = (int32_t)host[(size_t)i * P + P - 1];
   }
@@ -4298,23 +4373,26 @@ static bool ShardedAggregateRccl(Connection &c, const BoundSelect &s, const Boun
   for (auto &a : s.aggs) types.push_back(a.type);
   rows.assign(1, std::vector<Value>());
   FinishAccs(s, accs, rows[0]);
-  // each rank's partial row, as the host merge keeps them (all-gather only)
+  // each rank's partial row, as the host merge keeps them (the all-gather's
+  // blocks, or each rank's own count lanes of the reduce)
   st.last_partials.clear();
-  if (!counts_only) {
-    for (int i = 0; i < nsh; i++) {
-      auto res = std::make_shared<MaterializedResult>();
-      res->nrows = 1;
-      for (int k = 0; k < ncols; k++) {
-        HostColumn hc;
-        hc.name = p.names[k];
-        hc.type = p.aggs[k].type;
-        hc.phys = PhysOf(hc.type);
+  for (int i = 0; i < nsh; i++) {
+    auto res = std::make_shared<MaterializedResult>();
+    res->nrows = 1;
+    for (int k = 0; k < ncols; k++) {
+      HostColumn hc;
+      hc.name = p.names[k];
+      hc.type = p.aggs[k].type;
+      hc.phys = PhysOf(hc.type);
+      if (counts_only) {
+        HostColumnPush(hc, Value::Int(T_BIGINT, (i128)own[(size_t)i * P + k]));
+      } else {
         const int64_t *x = host.data() + (size_t)i * P + 3 * k;
         HostColumnPush(hc, LanesValue(hc.type, x[0], x[1], x[2] & 1));
-        res->cols.push_back(std::move(hc));
       }
-      st.last_partials.push_back(res);
+      res->cols.push_back(std::move(hc));
     }
+    st.last_partials.push_back(res);
   }
   st.rccl_combines++;
   if (c.rccl->loopback) st.rccl_loopbacks++;
@@ -4338,19 +4416,26 @@ static bool ShardedAggregateRccl(Connection &c, const BoundSelect &s, const Boun
 static constexpr int64_t kMaxGroupSlots = 4096;
 static bool GroupRcclEligible(Connection &c, const BoundSelect &s, const BoundSelect &p, rc::CombineDesc &cd) {
   ShardStats &st = c.shard_stats;
-  if (!c.opts.combine_rccl || s.groups.size() != 1) return false;
+  if (!c.opts.combine_rccl) return false;
   auto fallback = [&](const std::string &why) {
     st.rccl_fallbacks++;
     st.rccl_note = why;
     return false;
   };
+  auto unsupported = [&](const std::string &why) {  // a shape or layout RCCL never combines
+    st.rccl_unsupported++;
+    st.rccl_note = why;
+    return false;
+  };
+  if (s.groups.size() != 1) return unsupported("GROUP BY over several keys: host merge");
   const LogicalType &kt = s.groups[0]->type;
   const Phys kp = PhysOf(kt);
+  if (!RcclLayout(c)) return unsupported(st.rccl_note);
   if (kp != P_I8 && kp != P_I16 && kp != P_I32 && kp != P_I64 && kp != P_U8 && kp != P_U16 && kp != P_U32)
-    return fallback("GROUP BY key is not an integer column of <= 64 bits: host merge");
+    return unsupported("GROUP BY key is not an integer column of <= 64 bits: host merge");
   bool counts_only = false;
   std::string why;
-  if (!RcclKinds(p, cd, counts_only, &why)) return fallback(why);
+  if (!RcclKinds(p, cd, counts_only, &why)) return unsupported(why);
   if (!RcclReady(c)) return fallback(st.rccl_note);
   if ((int)s.src.table->parts.size() != (int)c.rccl->devs.size())
     return fallback("table parts do not match the shard devices: host merge");
@@ -4367,8 +4452,8 @@ static bool GroupRcclCombine(Connection &c, const BoundSelect &s, const BoundSel
     return false;
   };
   const int nsh = (int)rel.size(), ncols = cd.ncols;
-  // the union of the shards' key ranges, and whether any shard has the NULL group
-  bool any = false, has_null = false;
+  // the union of the shards' key ranges (the NULL key always has its slot)
+  bool any = false;
   i128 kmin = 0, kmax = 0;
   for (int i = 0; i < nsh; i++) {
     if (kr[i][2] > 0) {
@@ -4376,10 +4461,13 @@ static bool GroupRcclCombine(Connection &c, const BoundSelect &s, const BoundSel
       if (!any || (i128)kr[i][1] > kmax) kmax = kr[i][1];
       any = true;
     }
-    has_null |= kr[i][2] < rel[i].n;
   }
   const i128 range = any ? kmax - kmin + 1 : 0;
-  if (range > kMaxGroupSlots) return fallback("GROUP BY key range wider than 4096: host merge");
+  if (range > kMaxGroupSlots) {  // a shape the slots do not cover
+    st.rccl_unsupported++;
+    st.rccl_note = "GROUP BY key range wider than 4096: host merge";
+    return false;
+  }
   const int64_t nslot = (int64_t)range + 1;  // + the NULL key's slot
   const int64_t SL = rc::SlotLanes(ncols), P = nslot * SL + 1, recv_lanes = (int64_t)nsh * P;
   const int64_t out_lanes = nslot * SL + nsh;
@@ -4421,8 +4509,11 @@ static bool GroupRcclCombine(Connection &c, const BoundSelect &s, const BoundSel
   }
   const auto tc0 = std::chrono::steady_clock::now();
   std::string cerr;
-  const bool cok = rc::Collective(*c.rccl, false, sp, rp, xp, streams, (size_t)P, &cerr);
+  const std::shared_ptr<rc::Comms> comms = c.rccl;  // (shared: one collective at a time, as above)
+  std::unique_lock<std::mutex> coll_lock(comms->mu);
+  const bool cok = rc::Collective(*comms, false, sp, rp, xp, streams, (size_t)P, &cerr);
   if (!RcclWait(c, streams, tc0)) return fallback(st.rccl_note);  // (bounded also after a reported error)
+  coll_lock.unlock();
   // device 0 combines; one D2H of the combined slots and of the gathered blocks
   const bool keep_parts = recv_lanes * 8 <= ((int64_t)4 << 20);  // the per-shard partials, when small
   std::vector<int64_t> host((size_t)out_lanes + (keep_parts ? (size_t)recv_lanes : 0));
@@ -4454,9 +4545,12 @@ static bool GroupRcclCombine(Connection &c, const BoundSelect &s, const BoundSel
   const double t_coll = std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - tc0).count();
   if (first_err) std::rethrow_exception(first_err);
   if (!cok) {
+    const std::string why = "RCCL all-gather failed (" + cerr + "): communicators dropped, host merge from now on";
+    rc::MarkDead(*c.rccl, why);
     c.rccl.reset();
-    return fallback("RCCL all-gather failed (" + cerr + "): communicators dropped, host merge from now on");
+    return fallback(why);
   }
+  CountCollective(c, false);
   const auto t_merge = std::chrono::steady_clock::now();
   // every rank's device error word: the first raised naming its shard, all cleared
   int bad = -1;
@@ -4924,6 +5018,77 @@ void OpenShards(Connection &c) {
   (void)hipGetLastError();  // "already enabled" is not an error here
   hipSetDevice(c.engine->device);
   c.workers = std::make_shared<ShardWorkers>((int)c.shards.size());
+  RcclPrepare(c);
+}
+
+static std::string JsonStr(const std::string &v) {
+  std::string o = "\"";
+  for (unsigned char ch : v) {
+    if (ch == '"' || ch == '\\') o += '\\', o += (char)ch;
+    else if (ch < 0x20) {
+      char b[8];
+      snprintf(b, sizeof(b), "\\u%04x", ch);
+      o += b;
+    } else o += (char)ch;
+  }
+  return o + "\"";
+}
+
+static std::string JsonRanks(const std::vector<int> &devs, const std::vector<int> &count,
+                             const std::vector<int> &user_rank, const std::vector<int> &cu_device) {
+  std::string j = "[";
+  for (size_t i = 0; i < devs.size(); i++) {
+    auto at = [&](const std::vector<int> &v) { return i < v.size() ? v[i] : -1; };
+    j += std::string(i ? "," : "") + "{\"device\":" + std::to_string(devs[i]) +
+         ",\"count\":" + std::to_string(at(count)) + ",\"user_rank\":" + std::to_string(at(user_rank)) +
+         ",\"cu_device\":" + std::to_string(at(cu_device)) + "}";
+  }
+  return j + "]";
+}
+
+std::string RcclInfoJson(Connection &c) {
+  const ShardStats &st = c.shard_stats;
+  const char *state = "none";
+  if (c.rccl && c.rccl->loopback) state = "loopback";
+  else if (c.rccl) state = c.rccl->dead ? "failed" : "ready";
+  else if (c.rccl_init) state = rc::InitState(*c.rccl_init);
+  else if (c.rccl_tried) state = "failed";
+  std::string j = "{";
+  j += "\"mode\":" + JsonStr(!c.opts.combine_rccl ? "host" : c.opts.rccl_loopback ? "rccl_loopback" : "rccl");
+  j += ",\"state\":" + JsonStr(state);
+  j += ",\"devices\":[";
+  for (size_t i = 0; i < c.opts.devices.size(); i++) j += (i ? "," : "") + std::to_string(c.opts.devices[i]);
+  j += "],\"prepared_at_connect\":" + std::string(st.rccl_prepared_at_connect ? "true" : "false");
+  char b[256];
+  snprintf(b, sizeof(b), ",\"first_wait_ms\":%.3f", st.rccl_first_wait_ms);
+  j += b;
+  if (c.rccl && !c.rccl->loopback) {
+    snprintf(b, sizeof(b), ",\"init_s\":%.6f,\"check_us\":%.1f", c.rccl->init_s, c.rccl->check_us);
+    j += b;
+    j += ",\"ranks\":" + JsonRanks(c.rccl->devs, c.rccl->count, c.rccl->user_rank, c.rccl->cu_device);
+  }
+  j += ",\"combines\":" + std::to_string(st.rccl_combines) + ",\"fallbacks\":" + std::to_string(st.rccl_fallbacks) +
+       ",\"unsupported\":" + std::to_string(st.rccl_unsupported) + ",\"loopbacks\":" +
+       std::to_string(st.rccl_loopbacks) + ",\"group_combines\":" + std::to_string(st.rccl_group_combines) +
+       ",\"timeouts\":" + std::to_string(st.rccl_timeouts) + ",\"errors\":" + std::to_string(st.rccl_errors) +
+       ",\"reduces\":" + std::to_string(st.rccl_reduces) + ",\"allgathers\":" + std::to_string(st.rccl_allgathers);
+  j += ",\"last_collective\":" + JsonStr(st.last_collective) + ",\"note\":" + JsonStr(st.rccl_note) + "}";
+  return j;
+}
+
+std::string RcclSelfTestJson(const std::vector<int> &devs, std::string *err, double *us) {
+  rc::SelfTestInfo info;
+  const auto t0 = std::chrono::steady_clock::now();
+  *err = rc::SelfTest(devs, &info);
+  *us = std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0).count();
+  std::string j = "{\"ok\":" + std::string(err->empty() ? "true" : "false") + ",\"error\":" + JsonStr(*err) +
+                  ",\"devices\":[";
+  for (size_t i = 0; i < devs.size(); i++) j += (i ? "," : "") + std::to_string(devs[i]);
+  char b[160];
+  snprintf(b, sizeof(b), "],\"init_us\":%.1f,\"check_us\":%.1f,\"total_us\":%.1f", info.init_us, info.check_us, *us);
+  j += b;
+  j += ",\"ranks\":" + (err->empty() ? JsonRanks(devs, info.count, info.user_rank, info.cu_device) : "[]") + "}";
+  return j;
 }
 
 void EngineCounters(const Connection &c, int64_t out[3]) {

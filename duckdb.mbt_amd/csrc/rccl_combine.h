@@ -9,7 +9,9 @@
 #pragma once
 #include <hip/hip_runtime.h>
 
+#include <atomic>
 #include <memory>
+#include <mutex>
 #include <string>
 #include <vector>
 
@@ -20,24 +22,53 @@ struct ncclComm;  // RCCL's communicator (ncclComm_t)
 namespace mbx {
 namespace rc {
 
-// one communicator per shard device (rank i = devs[i]); none in loopback
+// one communicator per shard device (rank i = devs[i]); none in loopback.
+// Connections over the same device list share one set (Prepare), so a
+// collective and its bounded wait run under `mu`.
 struct Comms {
   std::vector<int> devs;
   std::vector<ncclComm *> comms;
   bool loopback = false;
+  std::mutex mu;
+  std::atomic<bool> dead{false};  // aborted or failed: never used again
+  // what RCCL reports for each communicator (ncclCommCount / ncclCommUserRank /
+  // ncclCommCuDevice; -1 where librccl lacks the query), and the open's cost
+  std::vector<int> count, user_rank, cu_device;
+  double init_s = 0;     // ncclCommInitAll
+  double check_us = 0;   // the multi-rank check that gates the communicators
   ~Comms();
 };
 
-// ncclCommInitAll over devs (distinct devices, one rank each); nullptr and a
-// reason in *note when librccl is missing or the init fails.  loopback (tests
-// only, MBX_EXPERIMENTS=1): no communicator; Collective moves the same lanes
-// with device copies, so the pack / combine kernels and the host decode run on
-// a box with one GPU (same-device shards).
-std::shared_ptr<Comms> Open(const std::vector<int> &devs, bool loopback, std::string *note);
+// One open of the communicators over a device list, run on a helper thread:
+// ncclCommInitAll, then a check of every rank (one grouped ncclReduce and one
+// ncclAllGather of known lanes, verified on every rank, and the rank count RCCL
+// reports) -- the combine uses the communicators only when that check passed.
+// A failed or timed-out open is remembered for the process, keyed by the
+// device list, so later connections go straight to the host merge.
+struct Init;
+// Starts (or joins) the open for devs; never blocks.  Distinct devices only
+// (the caller checks); a device list that failed before gets a finished Init
+// carrying that failure.
+std::shared_ptr<Init> Prepare(const std::vector<int> &devs);
+// The communicators of an open, waiting for it up to MBX_RCCL_INIT_TIMEOUT_MS
+// (default 30 s) from the open's start; nullptr and *note when unavailable.
+// *waited_ms: how long this call blocked.
+std::shared_ptr<Comms> Wait(const std::shared_ptr<Init> &in, std::string *note, double *waited_ms);
+const char *InitState(const Init &in);  // "pending" / "ready" / "failed"
+// the loopback stand-in (tests only, MBX_EXPERIMENTS=1): no communicator;
+// Collective moves the same lanes with device copies, so the pack / combine
+// kernels and the host decode run on a box with one GPU (same-device shards)
+std::shared_ptr<Comms> OpenLoopback(const std::vector<int> &devs);
 bool IsLoopback(const Comms &c);
-// ncclCommAbort on every rank (a collective that never completed); the
-// communicators are gone afterwards
-void Abort(Comms &c);
+// ncclCommAbort on every rank (a collective that never completed), then as
+// MarkDead; the communicators are gone afterwards
+void Abort(Comms &c, const std::string &why);
+// the communicators failed (a collective error): every connection sharing them,
+// and every later open of this device list in the process, takes the host merge
+void MarkDead(Comms &c, const std::string &why);
+// librccl has what the combine needs (ncclCommAbort included: a collective
+// that cannot be aborted is never started); "" or why not
+std::string ApiProblem();
 
 // One collective over every rank, driven from the calling thread: rank i's
 // count int64 lanes send[i] on streams[i] -> recv[i] (all-gather: n * count
@@ -45,16 +76,20 @@ void Abort(Comms &c);
 // recv).  The RCCL calls are fused in one ncclGroupStart/End, so no rank can
 // be left inside a collective that another rank never joined.  scratch[0]
 // (n * count lanes) is used by the loopback reduce only.  false and *err on
-// an RCCL / HIP error.
+// an RCCL / HIP error.  The caller holds c.mu until the streams have drained.
 bool Collective(Comms &c, bool reduce, const std::vector<const int64_t *> &send, const std::vector<int64_t *> &recv,
                 const std::vector<int64_t *> &scratch, const std::vector<hipStream_t> &streams, size_t count,
                 std::string *err);
 
-// Hardware check of the RCCL calls the combine makes, for a box with one GPU:
-// a one-rank communicator on `device` (ncclCommInitAll on the helper thread),
-// one grouped reduce and one grouped all-gather of 97 int64 lanes, the lanes
-// checked.  Returns "" (and the wall time in *us) or what failed.
-std::string SelfTest(int device, double *us);
+// Hardware check of the RCCL calls the combine makes, over `devs` (distinct
+// devices; one device on a one-GPU box): a fresh ncclCommInitAll (on the
+// helper thread, bounded) and the multi-rank check the combine is gated on.
+// Returns "" or what failed; *info gets what RCCL reported.
+struct SelfTestInfo {
+  double init_us = 0, check_us = 0, total_us = 0;
+  std::vector<int> count, user_rank, cu_device;
+};
+std::string SelfTest(const std::vector<int> &devs, SelfTestInfo *info);
 
 // the lanes of a one-row partial relation (row 0 of every column) and the
 // device error word, written to dst by one small kernel

@@ -15,6 +15,8 @@
 //    (reference int32 overflow at duckdb_native.c:2404).
 #include <hip/hip_runtime_api.h>
 
+#include <emmintrin.h>
+
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
@@ -1067,6 +1069,39 @@ duckdb_vector duckdb_mb_list_vector_get_child(duckdb_vector) {  // ref :2093
 duckdb_state duckdb_mb_list_vector_set_size(duckdb_vector, idx_t) { return DuckDBError; }  // ref :2097
 duckdb_state duckdb_mb_list_vector_reserve(duckdb_vector, idx_t) { return DuckDBError; }   // ref :2101
 
+// A vector's bytes into the pinned staging buffer, which only the DMA engine
+// reads afterwards: 16-byte non-temporal stores (no read-for-ownership of the
+// destination lines, nothing evicted from the caller's cache) when both ends
+// are 16-byte aligned, else memcpy.
+static void StreamToPinned(void *dst, const void *src, size_t bytes) {
+  if (((uintptr_t)dst | (uintptr_t)src) & 15) {
+    memcpy(dst, src, bytes);
+    return;
+  }
+  __m128i *d = (__m128i *)dst;
+  const __m128i *p = (const __m128i *)src;
+  size_t n = bytes / 16;
+  for (; n >= 4; n -= 4, d += 4, p += 4) {
+    const __m128i a = _mm_load_si128(p), b = _mm_load_si128(p + 1), c = _mm_load_si128(p + 2),
+                  e = _mm_load_si128(p + 3);
+    _mm_stream_si128(d, a), _mm_stream_si128(d + 1, b), _mm_stream_si128(d + 2, c), _mm_stream_si128(d + 3, e);
+  }
+  for (; n; n--) _mm_stream_si128(d++, _mm_load_si128(p++));
+  if (bytes & 15) memcpy(d, p, bytes & 15);
+  _mm_sfence();  // the stores are globally visible before the buffer's DMA is queued
+}
+
+// whether rows [lo, hi) of an LSB-first validity bitmap are all valid, a word at a time
+static bool AllValid(const uint64_t *w, int64_t lo, int64_t hi) {
+  while (lo < hi) {
+    const int64_t k = lo >> 6, b = lo & 63, e = std::min<int64_t>(64, b + (hi - lo));
+    const uint64_t mask = (e - b == 64) ? ~0ull : (((1ull << (e - b)) - 1) << b);
+    if ((w[k] & mask) != mask) return false;
+    lo += e - b;
+  }
+  return true;
+}
+
 int32_t duckdb_mb_append_data_chunk(duckdb_mb_appender *a, duckdb_mb_data_chunk *mb) {  // ref :2109-2132
   if (!a) return 0;
   if (!mb || !mb->chunk) {
@@ -1101,10 +1136,9 @@ int32_t duckdb_mb_append_data_chunk(duckdb_mb_appender *a, duckdb_mb_data_chunk 
         const int64_t m = std::min<int64_t>(n - off, a->pcap - a->prow);
         for (size_t c = 0; c < nc; c++) {
           const int w = a->pw[c];
-          memcpy((char *)a->pbuf[a->pcur][c] + (size_t)a->prow * w, (const char *)ch.vecs[c].data.data() + (size_t)off * w,
-                 (size_t)m * w);
-          bool all = true;
-          for (int64_t r = off; r < off + m && all; r++) all = row_valid(c, r);
+          StreamToPinned((char *)a->pbuf[a->pcur][c] + (size_t)a->prow * w,
+                         (const char *)ch.vecs[c].data.data() + (size_t)off * w, (size_t)m * w);
+          const bool all = AllValid(ch.vecs[c].valid.data(), off, off + m);
           auto &pv = a->pvalid[c];
           if (!all || !pv.empty()) {
             if (pv.empty()) pv.assign((size_t)a->prow, 1);
@@ -1776,11 +1810,16 @@ char *duckdb_mbx_rccl_note(duckdb_mb_connection *h) {
 int32_t duckdb_mbx_rccl_stats_ex(duckdb_mb_connection *h, int64_t *out, int32_t cap) {
   if (!h || !out) return 0;
   const ShardStats &st = h->conn.shard_stats;
-  const int64_t v[6] = {st.rccl_combines,  st.rccl_fallbacks, st.rccl_loopbacks,
-                        st.rccl_errors,    st.rccl_timeouts,  st.rccl_group_combines};
+  const int64_t v[9] = {st.rccl_combines,        st.rccl_fallbacks,   st.rccl_loopbacks,
+                        st.rccl_errors,          st.rccl_timeouts,    st.rccl_group_combines,
+                        st.rccl_unsupported,     st.rccl_reduces,     st.rccl_allgathers};
   int32_t n = 0;
-  for (; n < cap && n < 6; n++) out[n] = v[n];
+  for (; n < cap && n < 9; n++) out[n] = v[n];
   return n;
+}
+
+char *duckdb_mbx_rccl_info(duckdb_mb_connection *h) {
+  return strdup(h ? RcclInfoJson(h->conn).c_str() : "{}");
 }
 
 // Switches a connection's combine between the host merge (0) and RCCL (1), as
@@ -1798,22 +1837,24 @@ int32_t duckdb_mbx_set_combine(duckdb_mb_connection *h, int32_t mode) {
 // itself needs one device per rank): a one-rank communicator on `device`, one
 // grouped ncclReduce and one ncclAllGather of 97 int64 lanes, checked.  Returns
 // 1 and the wall us in *us_out; 0 and the reason via duckdb_mb_last_error.
-extern "C++" {
-namespace mbx {
-namespace rc {
-std::string SelfTest(int device, double *us);  // rccl_combine.cpp
-}
-}  // namespace mbx
-}
 int32_t duckdb_mbx_rccl_selftest(int32_t device, double *us_out) {
+  std::string err;
   double us = 0;
-  const std::string err = mbx::rc::SelfTest(device, &us);
+  RcclSelfTestJson({device}, &err, &us);
   if (us_out) *us_out = us;
   if (!err.empty()) {
     SetError(err.c_str());
     return 0;
   }
   return 1;
+}
+
+char *duckdb_mbx_rccl_selftest_ex(const int32_t *devices, int32_t n) {
+  std::vector<int> devs;
+  for (int32_t i = 0; devices && i < n; i++) devs.push_back(devices[i]);
+  std::string err;
+  double us = 0;
+  return strdup(RcclSelfTestJson(devs, &err, &us).c_str());
 }
 
 // The RCCL combine's lane arithmetic on the host (combine.h; CPU tests):

@@ -331,23 +331,40 @@ duckdb_mb_result *duckdb_mbx_shard_partial(duckdb_mb_connection *connection, int
 int32_t duckdb_mbx_rccl_stats(duckdb_mb_connection *connection, int64_t *out2, double *out_us1);
 /* Why the last RCCL request fell back ("" if it ran); free with duckdb_mbx_free. */
 char *duckdb_mbx_rccl_note(duckdb_mb_connection *connection);
-/* Up to cap of {RCCL combines, host-merge fallbacks, combines through the test
- * loopback, combines that raised a shard's device error, collectives aborted
- * after MBX_RCCL_TIMEOUT_MS (default 20 s; the host merge answers), combines
- * of GROUP BY relations (one integer key: dense key slots all-gathered)};
- * returns the count written. */
+/* Up to cap of {RCCL combines, host-merge fallbacks (a combine RCCL should
+ * have run: communicators unavailable, a collective failed or timed out),
+ * combines through the test loopback, combines that raised a shard's device
+ * error, collectives aborted after MBX_RCCL_TIMEOUT_MS (default 20 s; the host
+ * merge answers), combines of GROUP BY relations (one integer key: dense key
+ * slots all-gathered), requests RCCL never covers (floating-point partials,
+ * non-integer or several keys, same-device shards), ncclReduce combines,
+ * ncclAllGather combines}; returns the count written. */
 int32_t duckdb_mbx_rccl_stats_ex(duckdb_mb_connection *connection, int64_t *out, int32_t cap);
 /* 1: RCCL combine, 0: host merge, from the next statement on; 2: the RCCL
  * combine with its collectives replaced by device copies (tests only: refused
  * without MBX_EXPERIMENTS=1), so it runs over same-device shards.  Returns 1
  * (0: refused). */
 int32_t duckdb_mbx_set_combine(duckdb_mb_connection *connection, int32_t mode);
-/* The RCCL calls the combine makes, checked on hardware with one GPU (the
- * combine needs one device per rank): a one-rank communicator on `device`, one
- * grouped ncclReduce and one ncclAllGather of 97 int64 lanes.  Returns 1 and
- * the wall microseconds in *us_out (may be NULL); 0 with the reason in
- * duckdb_mb_last_error(). */
+/* The RCCL calls the combine makes, checked on hardware: a fresh
+ * ncclCommInitAll over `device` alone (one rank), then the multi-rank check the
+ * combine is gated on (one grouped ncclReduce and one ncclAllGather of 97 int64
+ * lanes, verified on every rank).  Returns 1 and the wall microseconds in
+ * *us_out (may be NULL); 0 with the reason in duckdb_mb_last_error(). */
 int32_t duckdb_mbx_rccl_selftest(int32_t device, double *us_out);
+/* The same over n distinct devices (n ranks): a JSON object {"ok", "error",
+ * "devices", "init_us", "check_us", "total_us", "ranks": [{"device", "count",
+ * "user_rank", "cu_device"}]} where count / user_rank / cu_device are what
+ * ncclCommCount / ncclCommUserRank / ncclCommCuDevice report (-1 if librccl
+ * lacks the query).  Free with duckdb_mbx_free. */
+char *duckdb_mbx_rccl_selftest_ex(const int32_t *devices, int32_t n);
+/* The connection's RCCL combine as a JSON object: the combine mode, the
+ * communicators' state ("none" / "pending" / "ready" / "failed" / "loopback"),
+ * whether their open started at connect, its ncclCommInitAll seconds and
+ * check microseconds, how long the first combine waited for it, every rank's
+ * ncclCommCount / ncclCommUserRank / ncclCommCuDevice, the counters of
+ * duckdb_mbx_rccl_stats_ex and the collective the last combine ran.  Free
+ * with duckdb_mbx_free. */
+char *duckdb_mbx_rccl_info(duckdb_mb_connection *connection);
 /* The RCCL combine's lane arithmetic on the host (tests): gathered holds
  * nranks x (3 ncols + 1) int64 lanes ({lo, hi, non-NULL} per column, then the
  * rank's error word); kinds[j] = 0 sum / 1 min / 2 max; out = 3 ncols lanes.

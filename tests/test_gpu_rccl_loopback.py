@@ -151,8 +151,8 @@ def test_rccl_loopback_c5_shape(mbx, oracle):
         st0 = c.rccl_stats()
         assert one(c, "SELECT COUNT(*) FROM t WHERE x > 24") == [str(cnt)]
         assert _ran(c, st0) == 1
-    # per-shard partials as the all-gather delivered them (the COUNT-only
-    # reduce keeps none), each against its shard's row range
+    # per-shard partials as the all-gather delivered them, each against its
+    # shard's row range; and the COUNT-only reduce keeps every rank's own count
     one(c, "SELECT COUNT(*), SUM(x) FROM t WHERE x > 24")
     for i in range(2):
         p = c.shard_partial(i)
@@ -160,6 +160,16 @@ def test_rccl_loopback_c5_shape(mbx, oracle):
         pc, ps = oracle.synth_filter_count(42, lo, hi - lo, 50, 1, 25, 2**63 - 1, 8)
         assert p.value(0, 0) == str(pc) and p.value(1, 0) == str(ps), (i, p.cells())
         p.close()
+    one(c, "SELECT COUNT(*) FROM t WHERE x > 24")
+    for i in range(2):
+        p = c.shard_partial(i)
+        lo, hi = i * n // 2, (i + 1) * n // 2
+        pc, _ = oracle.synth_filter_count(42, lo, hi - lo, 50, 1, 25, 2**63 - 1, 8)
+        assert p is not None and p.value(0, 0) == str(pc), i
+        p.close()
+    info = c.rccl_info()
+    assert info["state"] == "loopback" and info["reduces"] >= 4 and info["allgathers"] >= 4, info
+    assert info["last_collective"] == "loopback ncclReduce (int64 sum to device 0)", info
     c.close()
 
 
@@ -174,8 +184,11 @@ def test_rccl_without_distinct_devices_falls_back_with_note(mbx, oracle):
     assert one(c, "SELECT COUNT(*), SUM(x) FROM t WHERE x > 24") == [str(cnt), str(s)]
     st = c.rccl_stats()
     assert st["rccl_combines"] == st0["rccl_combines"]
-    assert st["rccl_fallbacks"] == st0["rccl_fallbacks"] + 1
-    assert "not distinct" in st["note"] or "librccl" in st["note"], st
+    # a layout RCCL never covers: counted apart from combines that failed
+    assert st["rccl_unsupported"] == st0["rccl_unsupported"] + 1 and st["rccl_fallbacks"] == st0["rccl_fallbacks"]
+    assert "not distinct" in st["note"], st
+    info = c.rccl_info()
+    assert info["state"] == "none" and not info["prepared_at_connect"] and info["mode"] == "rccl", info
     # shapes the RCCL combine does not cover say so too (a DOUBLE key, DOUBLE SUM)
     c.set_combine("rccl_loopback")
     q(c, "SELECT x / 2 AS g, COUNT(*) FROM t GROUP BY g")
@@ -222,8 +235,15 @@ def test_rccl_library_calls_on_one_gpu(mbx):
     back unchanged.  (Distinct-device ranks exchange data the same way.)"""
     r = mbx.rccl_selftest(0)
     assert r["ok"], r
-    # twice: a second communicator in the same process
-    assert mbx.rccl_selftest(0)["ok"]
+    # twice: a second communicator in the same process; the device-list form
+    # reports what RCCL itself says about its one rank
+    r = mbx.rccl_selftest([0])
+    assert r["ok"], r
+    assert r["ranks"] == [{"device": 0, "count": 1, "user_rank": 0, "cu_device": 0}], r
+    assert r["init_us"] > 0 and r["check_us"] > 0 and r["total_us"] >= r["init_us"], r
+    # a device list RCCL cannot take (two ranks on one device) is refused before any RCCL call
+    r = mbx.rccl_selftest([0, 0])
+    assert not r["ok"] and "not distinct" in r["error"], r
 
 
 def _group_both(c, sql):
