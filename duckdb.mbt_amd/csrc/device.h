@@ -83,8 +83,14 @@ int FilterAggStates(const void *pcol, int pphys, int64_t lo, int64_t hi, bool ha
                     bool need_minmax = true, uint64_t sum_maxabs = ~0ull, AggPartial *partials = nullptr);
 
 // --- fused GROUP BY on a small-range integer key (config C3) -------------
-// key in [kmin, kmin + nk), no nulls; up to 2 value columns of one phys.
-size_t GroupDirectLds(int nk, int R, int nv, bool mm, bool vv = false);  // vv: + valid-row counts
+// key in [kmin, kmin + nk) (the NULL group in slot nk - 1 when the key has
+// NULLs); up to 2 value columns of one phys.  vm: NULL-able columns (bit 0
+// value 0, bit 1 value 1, bit 2 the key); any: + the valid-row count tables
+size_t GroupDirectLds(int nk, int R, int nv, bool mm, int vm = 0);
+// validity words (LSB-first, 16-B aligned) of the NULL-able columns, or nullptr
+struct GroupValidity {
+  const uint64_t *key, *v0, *v1;
+};
 // Optional fused range predicates of the direct GROUP BY (a conjunction):
 // rows with lo <= p <= lo + span for every entry.  src: 1 = its own column
 // `col` (int32/int64, loaded as an extra slice), 2 = the key column, 3 = value
@@ -103,10 +109,10 @@ struct GroupPreds {
   GroupPred p[GROUP_MAX_PRED];
 };
 // Per-workgroup partial records of group_direct_lds (key-major, GroupPartialWords
-// u64 each: COUNT(*), valid-row count, then per value column sum lo / hi and,
-// with MIN/MAX, min / max), reduced by GroupPartialsCompact.
+// u64 each: COUNT(*), then per value column its valid-row count, sum lo / hi
+// and, with MIN/MAX, min / max), reduced by GroupPartialsCompact.
 constexpr int kGroupPartialKeys = 128;
-__host__ __device__ constexpr int GroupPartialWords(int nv, bool mm) { return 2 + nv * (mm ? 4 : 2); }
+__host__ __device__ constexpr int GroupPartialWords(int nv, bool mm) { return 1 + nv * (mm ? 5 : 3); }
 struct GroupPartialsOut {
   void *buf;            // room for the records
   size_t bytes;
@@ -129,7 +135,7 @@ bool GroupByDirectStates(const void *kcol, int kphys, int64_t kmin, int nk, cons
                          int nv, bool mm, int64_t nrows, int64_t seg_rows, int R, unsigned long long *cstar,
                          AggState *st0, AggState *st1, int grid_blocks, hipStream_t s,
                          const GroupPreds *pred = nullptr, uint64_t vmaxabs = ~0ull /* (unused) */,
-                         const uint64_t *v0valid = nullptr,   // v0's validity words (nv == 1): false if unsupported
+                         const GroupValidity *valid = nullptr,  // NULL-able key / values: false if unsupported
                          GroupPartialsOut *po = nullptr);
 
 // --- generic aggregation over compacted columns ---------------------------

@@ -2208,18 +2208,24 @@ static DRel Aggregate(Engine &e, const DRel &src, const BoundSelect &s) {
   bool f2_pred_ok = !s.where || (RangeConj(*s.where, f2_ranges) && f2_ranges.size() <= GROUP_MAX_PRED);
   for (auto &kv : f2_ranges)
     if (!FastIntCol(src, kv.first) || kv.second.first > kv.second.second) f2_pred_ok = false;
-  if (ng == 1 && f2_pred_ok && !src.range && s.groups[0]->kind == BExpr::COL && FastIntCol(src, s.groups[0]->col)) {
+  // NULL-able key and value columns ride along: their validity words are loaded
+  // with the step (group_direct_lds VM), a NULL key is its own group
+  auto int_col = [&](int c) {
+    const DCol &d = src.cols[c];
+    return FastIntCol(src, c) ||
+           (!(src.range && c == 0) && d.validity && (d.phys == P_I32 || d.phys == P_I64) && d.data &&
+            (uintptr_t)d.validity % 16 == 0);
+  };
+  const char *gd_nulls = Knob("MBX_GD_NULLS");  // MBX_GD_NULLS=0: NULL-able columns keep the generic paths
+  const bool nulls_ok = !(gd_nulls && atoi(gd_nulls) == 0);
+  if (ng == 1 && f2_pred_ok && !src.range && s.groups[0]->kind == BExpr::COL &&
+      (FastIntCol(src, s.groups[0]->col) || (nulls_ok && int_col(s.groups[0]->col)))) {
     const DCol &K = src.cols[s.groups[0]->col];
     const DevColumn *ks = K.table_col;
     std::vector<int> vcols;
-    bool ok = ks && ks->stats_valid && ks->null_count == 0 && src.n > 0;
+    const bool knull = K.validity != nullptr;
+    bool ok = ks && ks->stats_valid && (knull || ks->null_count == 0) && src.n > 0;
     bool mm = false;
-    // one value column may hold NULLs (group_direct_lds VV: its validity words ride the ring)
-    auto int_col = [&](int c) {
-      const DCol &d = src.cols[c];
-      return FastIntCol(src, c) ||
-             (d.validity && (d.phys == P_I32 || d.phys == P_I64) && d.data && (uintptr_t)d.validity % 16 == 0);
-    };
     for (auto &a : s.aggs) {
       if (a.kind == A_COUNT_STAR) continue;
       if (a.distinct) ok = false;
@@ -2231,13 +2237,15 @@ static DRel Aggregate(Engine &e, const DRel &src, const BoundSelect &s) {
       if (a.kind == A_MIN || a.kind == A_MAX) mm = true;
       if (std::find(vcols.begin(), vcols.end(), x->col) == vcols.end()) vcols.push_back(x->col);
     }
-    const uint64_t *vvalid = nullptr;
-    for (int c : vcols)
-      if (src.cols[c].validity) {
-        const char *gn = Knob("MBX_GD_NULLS");  // MBX_GD_NULLS=0: NULL-able values keep the generic paths
-        if (vcols.size() != 1 || (gn && atoi(gn) == 0)) ok = false;
-        vvalid = src.cols[c].validity;
+    dev::GroupValidity gval;
+    memset(&gval, 0, sizeof(gval));
+    gval.key = knull ? K.validity : nullptr;
+    for (size_t j = 0; j < vcols.size() && j < 2; j++)
+      if (src.cols[vcols[j]].validity) {
+        if (!nulls_ok) ok = false;
+        (j == 0 ? gval.v0 : gval.v1) = src.cols[vcols[j]].validity;
       }
+    const int vm = (gval.v0 ? 1 : 0) | (gval.v1 ? 2 : 0) | (gval.key ? 4 : 0);
     if (ok && vcols.size() <= 2) {
       if (vcols.size() == 2 && src.cols[vcols[0]].phys != src.cols[vcols[1]].phys) ok = false;
       i128 range = ks->imax - ks->imin + 1;
@@ -2250,12 +2258,11 @@ static DRel Aggregate(Engine &e, const DRel &src, const BoundSelect &s) {
         else maxabs = std::max(maxabs, std::max(vs->imax < 0 ? -vs->imax : vs->imax, vs->imin < 0 ? -vs->imin : vs->imin));
       }
       if (ok) {
-        int nk = (int)range;
+        int nk = (int)range + (knull ? 1 : 0);  // + the NULL group's slot, last
         int nv = (int)vcols.size();
         int R = 64;
-        const bool vv = vvalid != nullptr;
-        while (R > 1 && dev::GroupDirectLds(nk, R, nv, mm, vv) > 48 * 1024) R >>= 1;
-        if (dev::GroupDirectLds(nk, R, nv, mm, vv) > 64 * 1024) ok = false;
+        while (R > 1 && dev::GroupDirectLds(nk, R, nv, mm, vm) > 48 * 1024) R >>= 1;
+        if (dev::GroupDirectLds(nk, R, nv, mm, vm) > 64 * 1024) ok = false;
         int64_t seg = 0;  // whole chunk
         if (maxabs > 0) {
           i128 per_rep = ((i128)1 << 62) / maxabs;  // rows one replica may absorb
@@ -2291,7 +2298,7 @@ static DRel Aggregate(Engine &e, const DRel &src, const BoundSelect &s) {
           Phys vphys = nv ? src.cols[vcols[0]].phys : P_I64;
           double bytes = (double)src.n * PhysSize(K.phys);
           for (int c : vcols) bytes += (double)src.n * PhysSize(src.cols[c].phys);
-          if (vvalid) bytes += src.n / 8.0;
+          bytes += __builtin_popcount(vm) * (src.n / 8.0);  // validity words
           dev::GroupPreds gp;
           memset(&gp, 0, sizeof(gp));
           for (auto &kv : f2_ranges) {
@@ -2312,7 +2319,8 @@ static DRel Aggregate(Engine &e, const DRel &src, const BoundSelect &s) {
                                                 nv > 1 ? src.cols[vcols[1]].data : nullptr, vphys, nv, mm, src.n, seg,
                                                 R, (unsigned long long *)cs->p, s0p,
                                                 s1p, 0, e.stream, gp.n ? &gp : nullptr,
-                                                maxabs < ((i128)1 << 62) ? (uint64_t)maxabs : ~0ull, vvalid, &po);
+                                                maxabs < ((i128)1 << 62) ? (uint64_t)maxabs : ~0ull,
+                                                vm ? &gval : nullptr, &po);
           }
           if (!launched) goto generic;
           auto list = Alloc(e, nslots * 4);
@@ -2335,7 +2343,7 @@ static DRel Aggregate(Engine &e, const DRel &src, const BoundSelect &s) {
           D.has_key = 1;
           D.key_phys = PhysOf(s.groups[0]->type);
           D.kmin = (int64_t)ks->imin;
-          D.null_slot = -1;
+          D.null_slot = knull ? nk - 1 : -1;
           DCol kc = AllocOut(e, s.groups[0]->type, nslots, true, false);
           D.key_out = kc.data;
           D.key_valid = (uint32_t *)kc.validity;
@@ -4427,6 +4435,7 @@ static bool GroupRcclEligible(Connection &c, const BoundSelect &s, const BoundSe
     st.rccl_note = why;
     return false;
   };
+  if (s.groups.empty()) return false;  // (a global aggregate: ShardedAggregateRccl)
   if (s.groups.size() != 1) return unsupported("GROUP BY over several keys: host merge");
   const LogicalType &kt = s.groups[0]->type;
   const Phys kp = PhysOf(kt);

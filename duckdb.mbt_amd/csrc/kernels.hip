@@ -1688,27 +1688,34 @@ __device__ __forceinline__ void gd_max_i64(long long *p, long long v) {
   asm volatile("ds_max_i64 %0, %1" ::"v"(gd_lds(p)), "v"(v) : "memory");
 }
 
-// VV (NV = 1): the value column has NULLs.  Its step's 32 B of validity
-// words ride the ring slot after the value slice (one exec-masked glds);
-// COUNT(*) takes its own ds_add_u32 per row, the valid rows are counted in
-// vcnt (a ds_add_u32 of their own), and SUM / MIN / MAX see the valid rows
-// only; a predicate on the value column fails on NULL.
-template <typename TK, typename TV, int NV, bool MM, int DEPTH, bool VV = false>
+// VN: some of the key and value columns hold NULLs (gv says which; the
+// choice is wave-uniform, so it costs scalar branches, not one kernel per
+// mask).  Three 32-B steps of validity words (key, value 0, value 1: 256 rows
+// each) ride the ring slot after the value slices, one exec-masked glds each;
+// a column without NULLs re-reads a present column's words (an L2 hit, no HBM
+// bytes), so every step issues the same count of loads for the counted wait.
+// COUNT(*) takes one ds_add_u32 per row; a NULL-able value column's valid rows
+// are counted in its own vcnt table, and its SUM / MIN / MAX see the valid rows
+// only; a row whose key is NULL goes to the last key slot (nk - 1, the NULL
+// group); a predicate on a NULL-able column fails on NULL.
+template <typename TK, typename TV, int NV, bool MM, int DEPTH, bool VN = false>
 __global__ __launch_bounds__(256) void group_direct_lds_kernel(const TK *__restrict__ keys, const TV *__restrict__ v0,
                                                                const TV *__restrict__ v1, int64_t n, int64_t kmin,
                                                                int nk, int R, size_t ring_off,
                                                                unsigned long long *cstar, AggState *st0,
-                                                               AggState *st1, GroupPreds pr,
-                                                               const uint64_t *__restrict__ vvalid,
+                                                               AggState *st1, GroupPreds pr, GroupValidity gv,
                                                                unsigned long long *gpart) {
-  static_assert(!VV || NV == 1, "validity: one value column");
+  const bool KN = VN && gv.key, V0N = VN && NV >= 1 && gv.v0, V1N = VN && NV >= 2 && gv.v1;
+  constexpr int NVW = VN ? 3 : 0;  // validity steps per ring slot
+  const uint64_t *const anyv = VN ? (gv.key ? gv.key : gv.v0 ? gv.v0 : gv.v1) : nullptr;
   extern __shared__ __attribute__((aligned(16))) unsigned char lds_raw[];
   constexpr int KB = 256 * (int)sizeof(TK), VB = 256 * (int)sizeof(TV);  // bytes per step
   constexpr int SBD = KB + NV * VB;                                        // key + value slices
-  constexpr int SB0 = SBD + (VV ? 32 : 0);                                 // + validity words
+  constexpr int OKV = SBD, OV0 = OKV + 32, OV1 = OV0 + 32;  // validity words
+  constexpr int SB0 = SBD + 32 * NVW;
   // NLD counts the glds of a step without the optional predicate slice: with
   // one, the counted wait below is merely conservative (loads retire in order)
-  constexpr int NLD = SBD / 1024 + (VV ? 1 : 0);
+  constexpr int NLD = SBD / 1024 + NVW;
   // extra slices for predicate columns of their own, after the key/value slices
   int poff[GROUP_MAX_PRED];
   int PB = 0;
@@ -1719,6 +1726,7 @@ __global__ __launch_bounds__(256) void group_direct_lds_kernel(const TK *__restr
   }
   const int SB = SB0 + PB;
   const int nslot = nk * R;
+  const int null_key = (nk - 1) * R;  // KN: the NULL group's slots
   unsigned int *cnt = (unsigned int *)lds_raw;
   long long *sum0 = (long long *)(lds_raw + ((nslot * 4 + 15) & ~15));
   long long *sum1 = sum0 + nslot;
@@ -1726,14 +1734,17 @@ __global__ __launch_bounds__(256) void group_direct_lds_kernel(const TK *__restr
   long long *mx0 = mn0 + nslot;
   long long *mn1 = mx0 + nslot;
   long long *mx1 = mn1 + nslot;
-  // VV: valid-row counts per slot, after the table (GroupDirectLds sizes it)
-  unsigned int *vcnt = (unsigned int *)(sum0 + (NV >= 2 ? 2 : 1) * nslot + (MM ? 2 * (NV >= 2 ? 2 : 1) * nslot : 0));
+  // valid-row counts per slot of the NULL-able value columns, after the table
+  // (GroupDirectLds sizes them)
+  unsigned int *vcnt0 = (unsigned int *)(sum0 + (NV >= 2 ? 2 : 1) * nslot + (MM ? 2 * (NV >= 2 ? 2 : 1) * nslot : 0));
+  unsigned int *vcnt1 = vcnt0 + ((nslot + 3) & ~3);
   const int t = threadIdx.x, lane = t & 63, w = t >> 6;
   const int rep = lane % R;
   unsigned char *ring = lds_raw + ring_off + (size_t)w * DEPTH * SB;
   for (int i = t; i < nslot; i += blockDim.x) {
     cnt[i] = 0;
-    if (VV) vcnt[i] = 0;
+    if (V0N) vcnt0[i] = 0;
+    if (V1N) vcnt1[i] = 0;
     if (NV >= 1) sum0[i] = 0;
     if (NV >= 2) sum1[i] = 0;
     if (MM) {
@@ -1742,20 +1753,20 @@ __global__ __launch_bounds__(256) void group_direct_lds_kernel(const TK *__restr
     }
   }
   __syncthreads();
-  auto row = [&](int64_t k, int64_t a, int64_t b, bool valid) {
-    int sl = (int)(k - kmin) * R + rep;
-    if (VV) {
-      gd_add_u32(&cnt[sl], 1u);
-      if (valid) { gd_add_u32(&vcnt[sl], 1u); gd_add_u64(&sum0[sl], (unsigned long long)a); }
-      if (MM && valid) { gd_min_i64(&mn0[sl], (long long)a); gd_max_i64(&mx0[sl], (long long)a); }
-      return;
-    }
+  // one row: its key slot (the NULL group's when kv is false), COUNT(*), and
+  // each value column's sum / min / max over its valid rows
+  auto row = [&](int64_t k, int64_t a, int64_t b, bool kv, bool va, bool vb) {
+    const int sl = (KN && !kv) ? null_key + rep : (int)(k - kmin) * R + rep;
     gd_add_u32(&cnt[sl], 1u);
-    if (NV >= 1) gd_add_u64(&sum0[sl], (unsigned long long)a);
-    if (NV >= 2) gd_add_u64(&sum1[sl], (unsigned long long)b);
-    if (MM) {
-      gd_min_i64(&mn0[sl], (long long)a); gd_max_i64(&mx0[sl], (long long)a);
-      if (NV >= 2) { gd_min_i64(&mn1[sl], (long long)b); gd_max_i64(&mx1[sl], (long long)b); }
+    if (NV >= 1 && (!V0N || va)) {
+      if (V0N) gd_add_u32(&vcnt0[sl], 1u);
+      gd_add_u64(&sum0[sl], (unsigned long long)a);
+      if (MM) { gd_min_i64(&mn0[sl], (long long)a); gd_max_i64(&mx0[sl], (long long)a); }
+    }
+    if (NV >= 2 && (!V1N || vb)) {
+      if (V1N) gd_add_u32(&vcnt1[sl], 1u);
+      gd_add_u64(&sum1[sl], (unsigned long long)b);
+      if (MM) { gd_min_i64(&mn1[sl], (long long)b); gd_max_i64(&mx1[sl], (long long)b); }
     }
   };
   const int64_t nsteps = n >> 8;
@@ -1766,7 +1777,7 @@ __global__ __launch_bounds__(256) void group_direct_lds_kernel(const TK *__restr
   int64_t bl = blockIdx.x;
   if (pr.xcd && (gridDim.x & 7) == 0) bl = (int64_t)(blockIdx.x & 7) * (gridDim.x >> 3) + (blockIdx.x >> 3);
   int64_t st = bl * 4 + w;
-  // issue one step's glds into slot d: key slice, then each value slice
+  // issue one step's glds into slot d: key slice, each value slice, the validity words
   auto issue = [&](int64_t q, int d) {
     unsigned char *dst = ring + d * SB;
     const unsigned char *kp = (const unsigned char *)keys + q * KB;
@@ -1786,8 +1797,14 @@ __global__ __launch_bounds__(256) void group_direct_lds_kernel(const TK *__restr
         __builtin_amdgcn_global_load_lds((const void *)(vp + j * 1024 + lane * 16), (void *)(dst + KB + VB + j * 1024), 16,
                                          0, 2);
     }
-    if (VV && lane < 2)
-      __builtin_amdgcn_global_load_lds((const void *)(vvalid + q * 4 + lane * 2), (void *)(dst + SBD), 16, 0, 2);
+    if (VN && lane < 2) {
+      __builtin_amdgcn_global_load_lds((const void *)((KN ? gv.key : anyv) + q * 4 + lane * 2), (void *)(dst + OKV), 16,
+                                       0, 2);
+      __builtin_amdgcn_global_load_lds((const void *)((V0N ? gv.v0 : anyv) + q * 4 + lane * 2), (void *)(dst + OV0), 16,
+                                       0, 2);
+      __builtin_amdgcn_global_load_lds((const void *)((V1N ? gv.v1 : anyv) + q * 4 + lane * 2), (void *)(dst + OV1), 16,
+                                       0, 2);
+    }
 #pragma unroll
     for (int j = 0; j < GROUP_MAX_PRED; j++) {
       if (j >= pr.n || pr.p[j].src != 1) continue;
@@ -1808,6 +1825,10 @@ __global__ __launch_bounds__(256) void group_direct_lds_kernel(const TK *__restr
   }
   int k = 0;
   MBX_CLK(0);
+  // this lane's 4 rows' bits of a step's validity words at byte offset o
+  auto vbits = [&](const unsigned char *src, int o) {
+    return (unsigned)(*(const uint64_t *)(src + o + (lane >> 4) * 8) >> (4 * (lane & 15))) & 0xFu;
+  };
   for (; st < nsteps; st += nw) {
     asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NLD * (DEPTH - 1)) : "memory");
     const unsigned char *src = ring + k * SB;
@@ -1832,8 +1853,8 @@ __global__ __launch_bounds__(256) void group_direct_lds_kernel(const TK *__restr
       }
     }
     bool ok[4] = {true, true, true, true};
-    unsigned vm = 0xFu;  // VV: validity of this lane's 4 rows
-    if (VV) vm = (unsigned)(*(const uint64_t *)(src + SBD + (lane >> 4) * 8) >> (4 * (lane & 15))) & 0xFu;
+    const unsigned km = KN ? vbits(src, OKV) : 0xFu, am = V0N ? vbits(src, OV0) : 0xFu,
+                   bm = V1N ? vbits(src, OV1) : 0xFu;
 #pragma unroll
     for (int j = 0; j < GROUP_MAX_PRED; j++) {
       if (j >= pr.n) break;
@@ -1852,45 +1873,49 @@ __global__ __launch_bounds__(256) void group_direct_lds_kernel(const TK *__restr
       }
 #pragma unroll
       for (int e = 0; e < 4; e++) ok[e] = ok[e] && (uint64_t)(pv[e]) - (uint64_t)(g.lo) <= g.span;
-      if (VV && g.src == 3) {  // a predicate on the NULL-able value column
+      // a predicate on a NULL-able key / value column fails on NULL
+      const unsigned pm = g.src == 2 ? km : g.src == 3 ? am : 0xFu;
 #pragma unroll
-        for (int e = 0; e < 4; e++) ok[e] = ok[e] && ((vm >> e) & 1u);
-      }
+      for (int e = 0; e < 4; e++) ok[e] = ok[e] && ((pm >> e) & 1u);
     }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     int64_t q = st + DEPTH * nw;
     issue(q < nsteps ? q : st, k);
 #pragma unroll
     for (int e = 0; e < 4; e++)
-      if (ok[e]) row(kk[e], NV >= 1 ? a[e] : 0, NV >= 2 ? b[e] : 0, ((vm >> e) & 1u) != 0);
+      if (ok[e])
+        row(kk[e], NV >= 1 ? a[e] : 0, NV >= 2 ? b[e] : 0, ((km >> e) & 1u) != 0, ((am >> e) & 1u) != 0,
+            ((bm >> e) & 1u) != 0);
     k = k + 1 == DEPTH ? 0 : k + 1;
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   MBX_CLK(1);
   if (blockIdx.x == 0) {
+    auto bit = [](const uint64_t *v, int64_t i) { return ((v[i >> 6] >> (i & 63)) & 1) != 0; };
     for (int64_t i = (nsteps << 8) + t; i < n; i += blockDim.x) {
       int64_t kv = (int64_t)keys[i], av = NV >= 1 ? (int64_t)v0[i] : 0;
-      const bool vr = !VV || ((vvalid[i >> 6] >> (i & 63)) & 1);
+      const bool kr = !KN || bit(gv.key, i), ar = !V0N || bit(gv.v0, i), br = !V1N || bit(gv.v1, i);
       bool okr = true;
       for (int j = 0; j < pr.n; j++) {
         const GroupPred &g = pr.p[j];
         int64_t pv = g.src == 2 ? kv : g.src == 3 ? av
                    : (g.phys == P_I64 ? ((const int64_t *)g.col)[i] : (int64_t)((const int32_t *)g.col)[i]);
-        okr = okr && (uint64_t)(pv) - (uint64_t)(g.lo) <= g.span && (g.src != 3 || vr);
+        okr = okr && (uint64_t)(pv) - (uint64_t)(g.lo) <= g.span && (g.src != 3 || ar) && (g.src != 2 || kr);
       }
-      if (okr) row(kv, av, NV >= 2 ? (int64_t)v1[i] : 0, vr);
+      if (okr) row(kv, av, NV >= 2 ? (int64_t)v1[i] : 0, kr, ar, br);
     }
   }
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // this thread's table atomics (asm) have landed
   __syncthreads();
   for (int kq = t; kq < nk; kq += blockDim.x) {
-    unsigned long long c = 0, vc = 0;
+    unsigned long long c = 0, vc0 = 0, vc1 = 0;
     i128 s0 = 0, s1 = 0;
     long long a0 = INT64_MAX, b0 = INT64_MIN, a1 = INT64_MAX, b1 = INT64_MIN;
     for (int r = 0; r < R; r++) {
       int sl = kq * R + r;
       c += cnt[sl];
-      if (VV) vc += vcnt[sl];
+      if (V0N) vc0 += vcnt0[sl];
+      if (V1N) vc1 += vcnt1[sl];
       if (NV >= 1) s0 += (i128)sum0[sl];
       if (NV >= 2) s1 += (i128)sum1[sl];
       if (MM) {
@@ -1898,44 +1923,44 @@ __global__ __launch_bounds__(256) void group_direct_lds_kernel(const TK *__restr
         if (NV >= 2) { a1 = mn1[sl] < a1 ? mn1[sl] : a1; b1 = mx1[sl] > b1 ? mx1[sl] : b1; }
       }
     }
-    if (!VV) vc = c;
+    if (!V0N) vc0 = c;
+    if (!V1N) vc1 = c;
     if (gpart) {
       // this workgroup's record of key kq (key-major: group_partials_compact
       // reads one key's records contiguously); no global atomics
       unsigned long long *o = gpart + ((size_t)kq * gridDim.x + blockIdx.x) * GroupPartialWords(NV, MM);
       o[0] = c;
-      o[1] = vc;
-      int f = 2;
+      int f = 1;
       if (NV >= 1) {
         int64_t lo, hi;
         sp128(s0, lo, hi);
+        o[f++] = vc0;
         o[f++] = (unsigned long long)lo; o[f++] = (unsigned long long)hi;
         if (MM) { o[f++] = (unsigned long long)a0; o[f++] = (unsigned long long)b0; }
       }
       if (NV >= 2) {
         int64_t lo, hi;
         sp128(s1, lo, hi);
+        o[f++] = vc1;
         o[f++] = (unsigned long long)lo; o[f++] = (unsigned long long)hi;
         if (MM) { o[f++] = (unsigned long long)a1; o[f++] = (unsigned long long)b1; }
       }
       continue;
     }
     if (c) atomicAdd(&cstar[kq], c);
-    if (vc) {
+    if (NV >= 1 && vc0) {
       Acc A;
-      A.cnt = vc;
-      if (NV >= 1) {
-        int64_t lo, hi;
-        sp128(s0, lo, hi);
-        A.slo = (uint64_t)lo; A.shi = hi; A.mn = MM ? a0 : INT64_MAX; A.mx = MM ? b0 : INT64_MIN;
-        agg_state_atomic(&st0[kq], A);
-      }
-      if (NV >= 2) {
-        int64_t lo, hi;
-        sp128(s1, lo, hi);
-        A.slo = (uint64_t)lo; A.shi = hi; A.mn = MM ? a1 : INT64_MAX; A.mx = MM ? b1 : INT64_MIN;
-        agg_state_atomic(&st1[kq], A);
-      }
+      int64_t lo, hi;
+      sp128(s0, lo, hi);
+      A.cnt = vc0; A.slo = (uint64_t)lo; A.shi = hi; A.mn = MM ? a0 : INT64_MAX; A.mx = MM ? b0 : INT64_MIN;
+      agg_state_atomic(&st0[kq], A);
+    }
+    if (NV >= 2 && vc1) {
+      Acc A;
+      int64_t lo, hi;
+      sp128(s1, lo, hi);
+      A.cnt = vc1; A.slo = (uint64_t)lo; A.shi = hi; A.mn = MM ? a1 : INT64_MAX; A.mx = MM ? b1 : INT64_MIN;
+      agg_state_atomic(&st1[kq], A);
     }
   }
 }
@@ -1949,21 +1974,25 @@ static void LaunchGroupDirect(const void *k, const void *v0, const void *v1, int
   CHECK_LAUNCH();
 }
 
-size_t GroupDirectLds(int nk, int R, int nv, bool mm, bool vv) {
+size_t GroupDirectLds(int nk, int R, int nv, bool mm, int vm) {
   size_t nslot = (size_t)nk * R;
   size_t b = (nslot * 4 + 15) & ~(size_t)15;
   b += nslot * 8 * (size_t)(nv >= 2 ? 2 : 1);
   if (mm) b += nslot * 8 * 2 * (size_t)(nv >= 2 ? 2 : 1);
-  if (vv) b += (nslot * 4 + 15) & ~(size_t)15;  // valid-row counts
-  return b;
+  if (vm) b += 2 * 4 * ((nslot + 3) & ~(size_t)3);  // valid-row counts of value columns 0 and 1
+  return (b + 15) & ~(size_t)15;
 }
 
 bool GroupByDirectStates(const void *kcol, int kphys, int64_t kmin, int nk, const void *v0, const void *v1, int vphys,
                          int nv, bool mm, int64_t nrows, int64_t seg_rows, int R, unsigned long long *cstar,
                          AggState *st0, AggState *st1, int grid_blocks, hipStream_t s, const GroupPreds *pred,
-                         uint64_t vmaxabs, const uint64_t *v0valid, GroupPartialsOut *po) {
-  const bool vv = v0valid != nullptr;
-  if (vv && nv != 1) return false;
+                         uint64_t vmaxabs, const GroupValidity *gvp, GroupPartialsOut *po) {
+  GroupValidity gv;
+  memset(&gv, 0, sizeof(gv));
+  if (gvp) gv = *gvp;
+  const int vm = (gv.v0 ? 1 : 0) | (gv.v1 ? 2 : 0) | (gv.key ? 4 : 0);
+  const bool vv = vm != 0;
+  if ((gv.v0 && nv < 1) || (gv.v1 && nv < 2)) return false;
   if (po) po->used = false;
   // with po, the states are this call's to initialise: the atomic forms below
   // need them zeroed first, the partials form writes every one at the end
@@ -2008,9 +2037,10 @@ bool GroupByDirectStates(const void *kcol, int kphys, int64_t kmin, int nk, cons
       int64_t waves = (int64_t)grid * 4;
       int64_t rows_per_block = ((nsteps + waves - 1) / waves) * 4 * 256 + 256;
       if (vv && depth > 3) depth = 3;  // the validity form is built for 2- and 3-deep rings
-      size_t tab = GroupDirectLds(nk, R, nv, mm, vv);
+      size_t tab = GroupDirectLds(nk, R, nv, mm, vm);
       size_t ring_off = (tab + 15) & ~(size_t)15;
-      size_t slot = 256 * (size_t)(kphys == P_I64 ? 8 : 4) + (size_t)nv * 256 * (vphys == P_I64 ? 8 : 4) + (vv ? 32 : 0);
+      size_t slot = 256 * (size_t)(kphys == P_I64 ? 8 : 4) + (size_t)nv * 256 * (vphys == P_I64 ? 8 : 4) +
+                    (vv ? 3 * 32 : 0);
       for (int j = 0; j < pr.n; j++)
         if (pr.p[j].src == 1) slot += 256 * (size_t)(pr.p[j].phys == P_I64 ? 8 : 4);
       depth = depth <= 2 ? 2 : depth <= 3 ? 3 : depth <= 4 ? 4 : depth <= 6 ? 6 : 8;
@@ -2021,7 +2051,7 @@ bool GroupByDirectStates(const void *kcol, int kphys, int64_t kmin, int nk, cons
       while (lds > lds_cap && R > 1) {
         R >>= 1;
         if (seg_rows > 0) seg_rows >>= 1;
-        tab = GroupDirectLds(nk, R, nv, mm, vv);
+        tab = GroupDirectLds(nk, R, nv, mm, vm);
         ring_off = (tab + 15) & ~(size_t)15;
         lds = ring_off + 4 * (size_t)depth * slot;
       }
@@ -2037,26 +2067,31 @@ bool GroupByDirectStates(const void *kcol, int kphys, int64_t kmin, int nk, cons
         po->used = true;
         po->blocks = grid;
       }
-      if (vv) {  // NULL-able value column: one flush only
+      if (vv) {  // NULL-able columns: one flush only
         if (!one_flush || lds > lds_cap) return false;
         if (!gpart) init_states();
-#define GLVV(TK, TV, MM, D)                                                                                         \
+#define GLVV(TK, TV, NV, MM, D)                                                                                     \
   {                                                                                                                 \
-    (void)hipFuncSetAttribute((const void *)group_direct_lds_kernel<TK, TV, 1, MM, D, true>,                        \
+    (void)hipFuncSetAttribute((const void *)group_direct_lds_kernel<TK, TV, NV, MM, D, true>,                      \
                               hipFuncAttributeMaxDynamicSharedMemorySize, 150 * 1024);                              \
-    hipLaunchKernelGGL((group_direct_lds_kernel<TK, TV, 1, MM, D, true>), dim3(grid), dim3(256), lds, s,           \
+    hipLaunchKernelGGL((group_direct_lds_kernel<TK, TV, NV, MM, D, true>), dim3(grid), dim3(256), lds, s,         \
                        (const TK *)kcol, (const TV *)v0, (const TV *)v1, nrows, kmin, nk, R, ring_off, cstar, st0,  \
-                       st1, pr, v0valid, gpart);                                                                    \
+                       st1, pr, gv, gpart);                                                                         \
   }
+#define GLVN(TK, TV, MM, D)                                                                                       \
+  if (nv == 0) { GLVV(TK, TV, 0, false, D) }                                                                        \
+  else if (nv == 1) { GLVV(TK, TV, 1, MM, D) }                                                                      \
+  else { GLVV(TK, TV, 2, MM, D) }
 #define GLVVD(TK, TV)                                                                                             \
-  if (mm) { if (depth == 2) GLVV(TK, TV, true, 2) else GLVV(TK, TV, true, 3) }                                      \
-  else { if (depth == 2) GLVV(TK, TV, false, 2) else GLVV(TK, TV, false, 3) }
+  if (mm) { if (depth == 2) { GLVN(TK, TV, true, 2) } else { GLVN(TK, TV, true, 3) } }                              \
+  else { if (depth == 2) { GLVN(TK, TV, false, 2) } else { GLVN(TK, TV, false, 3) } }
         if (kphys == P_I32) {
           if (vphys == P_I64) { GLVVD(int32_t, int64_t) } else { GLVVD(int32_t, int32_t) }
         } else {
           if (vphys == P_I64) { GLVVD(int64_t, int64_t) } else { GLVVD(int64_t, int32_t) }
         }
 #undef GLVVD
+#undef GLVN
 #undef GLVV
         CHECK_LAUNCH();
         return true;
@@ -2065,11 +2100,11 @@ bool GroupByDirectStates(const void *kcol, int kphys, int64_t kmin, int nk, cons
         if (!gpart) init_states();
 #define GL(TK, TV, NV, MM, D)                                                                                      \
   if (lds > 64 * 1024) /* deep rings at one or two blocks per CU */                                               \
-    (void)hipFuncSetAttribute((const void *)group_direct_lds_kernel<TK, TV, NV, MM, D, false>,                     \
+    (void)hipFuncSetAttribute((const void *)group_direct_lds_kernel<TK, TV, NV, MM, D, 0>,                         \
                               hipFuncAttributeMaxDynamicSharedMemorySize, 150 * 1024);                             \
-  hipLaunchKernelGGL((group_direct_lds_kernel<TK, TV, NV, MM, D, false>), dim3(grid), dim3(256), lds, s,           \
+  hipLaunchKernelGGL((group_direct_lds_kernel<TK, TV, NV, MM, D, 0>), dim3(grid), dim3(256), lds, s,               \
                      (const TK *)kcol, (const TV *)v0, (const TV *)v1, nrows, kmin, nk, R, ring_off, cstar, st0,   \
-                     st1, pr, (const uint64_t *)nullptr, gpart);
+                     st1, pr, gv, gpart);
 #define GLD(TK, TV, NV, MM)                                                                     \
   if (depth == 2) { GL(TK, TV, NV, MM, 2) } else if (depth == 3) { GL(TK, TV, NV, MM, 3) }      \
   else if (depth == 4) { GL(TK, TV, NV, MM, 4) } else if (depth == 6) { GL(TK, TV, NV, MM, 6) } \
@@ -2618,14 +2653,14 @@ __global__ __launch_bounds__(1024) void group_partials_compact_kernel(const unsi
     for (int b = lane; b < nb; b += 64) {  // (unrolled: a lane's records load together)
       const unsigned long long *o = gpart + ((size_t)kq * nb + b) * W;
       c += o[0];
-      int f = 2;
+      int f = 1;
 #pragma unroll
       for (int j = 0; j < NV; j++) {
         Acc B;
-        B.cnt = o[1]; B.slo = o[f]; B.shi = (int64_t)o[f + 1];
-        B.mn = MM ? (int64_t)o[f + 2] : INT64_MAX;
-        B.mx = MM ? (int64_t)o[f + 3] : INT64_MIN;
-        f += MM ? 4 : 2;
+        B.cnt = o[f]; B.slo = o[f + 1]; B.shi = (int64_t)o[f + 2];
+        B.mn = MM ? (int64_t)o[f + 3] : INT64_MAX;
+        B.mx = MM ? (int64_t)o[f + 4] : INT64_MIN;
+        f += MM ? 5 : 3;
         acc_merge(A[j], B);
       }
     }

@@ -47,6 +47,7 @@ def load():
     lib.orc_synth_filter_count.argtypes = [u64, i64, i64, u64, i64, i64, i64, ctypes.c_int, vp, vp]
     lib.orc_groupby_sum_i32_i64.argtypes = [vp, vp, i64, i32, ctypes.c_int, ctypes.c_int, vp, vp]
     lib.orc_synth_groupby.argtypes = [u64, u64, i64, i64, ctypes.c_int, u64, i64, ctypes.c_int, vp, vp]
+    lib.orc_synth_groupby_nulls.argtypes = [vp, vp, vp, i64, i64, ctypes.c_int, vp, vp, vp]
     lib.orc_range_mod_select.restype = i64
     lib.orc_range_mod_select.argtypes = [i64, i64, i64, i64, vp, i64]
     lib.orc_select_i64.restype = i64
@@ -106,6 +107,35 @@ class Oracle:
         sums = ctypes.create_string_buffer(16 * nk)
         self.lib.orc_synth_groupby(seed_k, seed_v, start, n, nk, vm, vadd, threads, counts.ctypes.data, sums)
         return [int(c) for c in counts], [i128_from(sums.raw[16 * i:16 * i + 16]) for i in range(nk)]
+
+    def synth_groupby_nulls(self, seeds, mods, adds, start, n, threads=1):
+        """The C3 GROUP BY with NULL keys and two NULL-able value columns over
+        the generator (oracle.c orc_synth_groupby_nulls): a list of groups in
+        key order, the NULL key last, each (key or None, COUNT(*), COUNT(v),
+        SUM(v) or None, MIN(v), MAX(v), COUNT(w), SUM(w), MIN(w), MAX(w))."""
+        import numpy as np
+        sd = np.array(seeds, dtype=np.uint64)
+        md = np.array(mods, dtype=np.uint64)
+        ad = np.array(adds, dtype=np.int64)
+        nk = int(mods[0])
+        ng = nk + 1
+        counts = np.zeros(3 * ng, dtype=np.uint64)
+        sums = ctypes.create_string_buffer(2 * ng * 16)
+        mm = np.zeros(4 * ng, dtype=np.int64)
+        self.lib.orc_synth_groupby_nulls(sd.ctypes.data, md.ctypes.data, ad.ctypes.data, start, n, threads,
+                                         counts.ctypes.data, sums, mm.ctypes.data)
+        out = []
+        for g in range(ng):
+            if not counts[3 * g]:
+                continue
+            row = [None if g == nk else g, int(counts[3 * g])]
+            for c in range(2):
+                cv = int(counts[3 * g + 1 + c])
+                s = i128_from(sums.raw[16 * (2 * g + c):16 * (2 * g + c) + 16])
+                row += [cv, s if cv else None, int(mm[4 * g + 2 * c]) if cv else None,
+                        int(mm[4 * g + 2 * c + 1]) if cv else None]
+            out.append(tuple(row))
+        return out
 
     def range_mod_select(self, n, k, c, mul):
         import numpy as np

@@ -323,6 +323,89 @@ void orc_synth_groupby(uint64_t seed_k, uint64_t seed_v, int64_t start, int64_t 
   free(acc);
 }
 
+/* ---- the C3 GROUP BY with NULL keys and two NULL-able value columns ----
+ * Over the generator, row r = start + i:
+ *   k = splitmix64(sd[0] + r) mod md[0] (INT32), NULL when md[1] && splitmix64(sd[1] + r) mod md[1] == 0;
+ *   v = splitmix64(sd[2] + r) mod md[2] + ad[0], NULL when md[3] && splitmix64(sd[3] + r) mod md[3] == 0;
+ *   w = splitmix64(sd[4] + r) mod md[4] + ad[1], NULL when md[5] && splitmix64(sd[5] + r) mod md[5] == 0.
+ * DuckDB's rules (GROUP BY puts every NULL key in one group; COUNT(col), SUM,
+ * MIN, MAX skip NULLs): per group g in 0..nk (g = nk: the NULL key),
+ * counts[3g..] = {COUNT(*), COUNT(v), COUNT(w)}, sums16[2g..] = {SUM(v), SUM(w)}
+ * as int128, mm[4g..] = {MIN(v), MAX(v), MIN(w), MAX(w)} (INT64_MAX / MIN when
+ * the group has no valid value). */
+typedef struct {
+  const uint64_t *sd, *md;
+  const int64_t *ad;
+  int64_t start, n;
+  int nk;
+  uint64_t *cnt;
+  i128 *sum;
+  int64_t *mm;
+} sgn_job;
+
+static void *sgn_run(void *p) {
+  sgn_job *j = (sgn_job *)p;
+  const int ng = j->nk + 1;
+  for (int64_t i = 0; i < j->n; i++) {
+    const uint64_t r = (uint64_t)(j->start + i);
+    int g = (int)(orc_splitmix64(j->sd[0] + r) % j->md[0]);
+    if (j->md[1] && orc_splitmix64(j->sd[1] + r) % j->md[1] == 0) g = j->nk;
+    j->cnt[3 * g]++;
+    for (int c = 0; c < 2; c++) {
+      const uint64_t *sd = j->sd + 2 + 2 * c, *md = j->md + 2 + 2 * c;
+      if (md[1] && orc_splitmix64(sd[1] + r) % md[1] == 0) continue;
+      const int64_t v = (int64_t)(orc_splitmix64(sd[0] + r) % md[0]) + j->ad[c];
+      j->cnt[3 * g + 1 + c]++;
+      j->sum[2 * g + c] += v;
+      int64_t *m = j->mm + 4 * g + 2 * c;
+      if (v < m[0]) m[0] = v;
+      if (v > m[1]) m[1] = v;
+    }
+  }
+  (void)ng;
+  return NULL;
+}
+
+void orc_synth_groupby_nulls(const uint64_t *sd, const uint64_t *md, const int64_t *ad, int64_t start, int64_t n,
+                             int threads, uint64_t *counts, void *sums16, int64_t *mm) {
+  if (threads < 1) threads = 1;
+  if (threads > MAXT) threads = MAXT;
+  const int nk = (int)md[0], ng = nk + 1;
+  sgn_job jobs[MAXT];
+  pthread_t th[MAXT];
+  int64_t chunk = (n + threads - 1) / threads;
+  for (int t = 0; t < threads; t++) {
+    int64_t b = t * chunk, e = b + chunk < n ? b + chunk : n;
+    if (b > n) b = n;
+    jobs[t].sd = sd, jobs[t].md = md, jobs[t].ad = ad;
+    jobs[t].start = start + b;
+    jobs[t].n = e - b;
+    jobs[t].nk = nk;
+    jobs[t].cnt = (uint64_t *)calloc((size_t)3 * ng, sizeof(uint64_t));
+    jobs[t].sum = (i128 *)calloc((size_t)2 * ng, sizeof(i128));
+    jobs[t].mm = (int64_t *)malloc((size_t)4 * ng * sizeof(int64_t));
+    for (int q = 0; q < 4 * ng; q++) jobs[t].mm[q] = (q & 1) ? INT64_MIN : INT64_MAX;
+    pthread_create(&th[t], NULL, sgn_run, &jobs[t]);
+  }
+  i128 *acc = (i128 *)calloc((size_t)2 * ng, sizeof(i128));
+  memset(counts, 0, (size_t)3 * ng * sizeof(uint64_t));
+  for (int q = 0; q < 4 * ng; q++) mm[q] = (q & 1) ? INT64_MIN : INT64_MAX;
+  for (int t = 0; t < threads; t++) {
+    pthread_join(th[t], NULL);
+    for (int q = 0; q < 3 * ng; q++) counts[q] += jobs[t].cnt[q];
+    for (int q = 0; q < 2 * ng; q++) acc[q] += jobs[t].sum[q];
+    for (int q = 0; q < 4 * ng; q++) {
+      const int64_t x = jobs[t].mm[q];
+      if ((q & 1) ? x > mm[q] : x < mm[q]) mm[q] = x;
+    }
+    free(jobs[t].cnt);
+    free(jobs[t].sum);
+    free(jobs[t].mm);
+  }
+  memcpy(sums16, acc, (size_t)2 * ng * 16);
+  free(acc);
+}
+
 /* ---- range(N) WHERE i % k = c, projected i*mul (config C1) ------------- */
 int64_t orc_range_mod_select(int64_t n, int64_t k, int64_t c, int64_t mul, int64_t *out, int64_t cap) {
   int64_t w = 0;

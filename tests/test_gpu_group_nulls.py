@@ -1,0 +1,171 @@
+"""GROUP BY with NULL keys and NULL-able value columns on the device-native
+direct-index kernel (group_direct_lds, validity mask VM): a NULL key is its
+own group (the last key slot, emitted last), COUNT(*) counts every row of a
+group, COUNT(col) / SUM / MIN / MAX / AVG skip the column's NULLs, and a group
+whose values are all NULL has SUM / MIN / MAX / AVG NULL and COUNT(col) 0.
+The reference's NULL semantics: src/duckdb_fixture_cases.mbt:125-145 ("null
+handling"), :223-228 ("null in values"); DuckDB puts all NULL keys in one
+group.  Every answer is checked against the oracle's restatement over the same
+generator (oracle.c orc_synth_groupby_nulls), and the kernel that ran is read
+from the query profile: the run-time compiled jit_group no longer takes these
+shapes."""
+import pytest
+
+from conftest import q
+
+pytestmark = pytest.mark.gpu
+
+SEEDS = [7, 19, 9, 23, 31, 29]  # k, k NULL, v, v NULL, w, w NULL
+MODS = [32, 7, 1 << 40, 7, 1 << 40, 7]  # 32 keys, 1/7 NULL keys, values, 1/7 NULL values
+ADDS = [-(1 << 39), -(1 << 39)]
+
+
+def _setup(c, n, name="gnn", mods=MODS):
+    kn = f"mbx_synth({SEEDS[1]}, i, {mods[1]}) = 0" if mods[1] else "false"
+    vn = f"mbx_synth({SEEDS[3]}, i, {mods[3]}) = 0" if mods[3] else "false"
+    wn = f"mbx_synth({SEEDS[5]}, i, {mods[5]}) = 0" if mods[5] else "false"
+    q(c, f"CREATE TABLE {name} AS SELECT "
+         f"CASE WHEN {kn} THEN NULL ELSE CAST(mbx_synth({SEEDS[0]}, i, {mods[0]}) AS INTEGER) END AS k, "
+         f"CASE WHEN {vn} THEN NULL ELSE mbx_synth({SEEDS[2]}, i, {mods[2]}) + ({ADDS[0]}) END AS v, "
+         f"CASE WHEN {wn} THEN NULL ELSE mbx_synth({SEEDS[4]}, i, {mods[4]}) + ({ADDS[1]}) END AS w, "
+         f"mbx_synth(42, i, 50) + 1 AS x FROM range({n}) tbl(i)")
+
+
+def _kernels(c):
+    return [kk["name"] for kk in c.last_profile()["kernels"]]
+
+
+def _cell(x):
+    return "" if x is None else str(x)
+
+
+def _conn(mbx, devices=None, combine=None):
+    cfg = mbx.Config.create()
+    cfg.set("mbx_profile", "true")
+    if devices:
+        assert isinstance(cfg.set("gpu_devices", devices), mbx.Ok)
+    if combine:
+        assert isinstance(cfg.set("mbx_combine", combine), mbx.Ok)
+    r = mbx.connect_with_config(cfg)
+    assert isinstance(r, mbx.Ok), r.error.message
+    return r.value
+
+
+SQL = "SELECT k, COUNT(*), COUNT(v), SUM(v), MIN(v), MAX(v), COUNT(w), SUM(w), MIN(w), MAX(w) FROM gnn GROUP BY k"
+
+
+def _expect(groups, cols=(0, 1, 2, 3, 4, 5, 6, 7, 8, 9)):
+    return [[_cell(g[i]) for i in cols] for g in groups]
+
+
+@pytest.mark.parametrize("n", [1, 255, 257, 100_003, 1_000_003])
+def test_null_keys_two_nullable_values(mbx, oracle, monkeypatch, n):
+    c = _conn(mbx)
+    _setup(c, n)
+    exp = _expect(oracle.synth_groupby_nulls(SEEDS, MODS, ADDS, 0, n, 8))
+    got = q(c, SQL).rows
+    ks = _kernels(c)
+    assert "group_direct" in ks and "jit_group" not in ks, ks
+    assert got == exp, (n, got[-2:], exp[-2:])
+    # the generic path (MBX_GD_NULLS=0: jit_group / compaction) agrees
+    monkeypatch.setenv("MBX_GD_NULLS", "0")
+    ref = q(c, SQL + " ORDER BY k").rows
+    monkeypatch.delenv("MBX_GD_NULLS")
+    assert "group_direct" not in _kernels(c)
+    assert ref == got
+    c.close()
+
+
+def test_null_key_shapes_and_avg(mbx, oracle):
+    """Every validity mask the kernel takes: the key alone (with COUNT(*) only,
+    and with one value), one value alone, two values with either or both
+    NULL-able; AVG over NULL-able values; a fused predicate on another column."""
+    n = 300_007
+    c = _conn(mbx)
+    # k NULL-able; v, w never NULL
+    _setup(c, n, "gk", [32, 7, 1 << 40, 0, 1 << 40, 0])
+    g = oracle.synth_groupby_nulls(SEEDS, [32, 7, 1 << 40, 0, 1 << 40, 0], ADDS, 0, n, 8)
+    for sql, cols in (("SELECT k, COUNT(*) FROM gk GROUP BY k", (0, 1)),
+                      ("SELECT k, COUNT(*), SUM(v), MIN(v), MAX(v) FROM gk GROUP BY k", (0, 1, 3, 4, 5)),
+                      ("SELECT k, SUM(v), SUM(w), COUNT(w) FROM gk GROUP BY k", (0, 3, 7, 6))):
+        assert q(c, sql).rows == _expect(g, cols), sql
+        assert "group_direct" in _kernels(c), (sql, _kernels(c))
+    # v NULL-able, k and w not; and only w NULL-able
+    for mods in ([32, 0, 1 << 40, 7, 1 << 40, 0], [32, 0, 1 << 40, 0, 1 << 40, 7], [32, 5, 1 << 40, 3, 1 << 40, 11]):
+        q(c, "DROP TABLE IF EXISTS gm")
+        _setup(c, n, "gm", mods)
+        g = oracle.synth_groupby_nulls(SEEDS, mods, ADDS, 0, n, 8)
+        sql = "SELECT k, COUNT(*), COUNT(v), SUM(v), MIN(v), MAX(v), COUNT(w), SUM(w), MIN(w), MAX(w) FROM gm GROUP BY k"
+        assert q(c, sql).rows == _expect(g), mods
+        assert "group_direct" in _kernels(c), (mods, _kernels(c))
+        # AVG: DOUBLE of the exact sum / count, NULL for a group of NULLs
+        for row, e in zip(q(c, "SELECT k, AVG(v), AVG(w) FROM gm GROUP BY k").rows, g):
+            for cell, cnt, s in ((row[1], e[2], e[3]), (row[2], e[6], e[7])):
+                if not cnt:
+                    assert cell == ""
+                else:
+                    assert abs(float(cell) - s / cnt) <= 1e-9 * max(1.0, abs(s / cnt)), (mods, row, e)
+    # a fused range predicate on a column of its own (x, never NULL)
+    import numpy as np
+    mods = [32, 7, 1 << 40, 7, 1 << 40, 7]
+    q(c, "DROP TABLE IF EXISTS gm")
+    _setup(c, n, "gm", mods)
+    rows = q(c, "SELECT k, COUNT(*), COUNT(v), SUM(v) FROM gm WHERE x > 24 GROUP BY k").rows
+    assert "group_direct" in _kernels(c), _kernels(c)
+    k = oracle.synth_i64(n, 7, 0, 32, 0)
+    kn = oracle.synth_i64(n, 19, 0, 7, 0) == 0
+    v = oracle.synth_i64(n, 9, 0, 1 << 40, -(1 << 39))
+    vn = oracle.synth_i64(n, 23, 0, 7, 0) == 0
+    x = oracle.synth_i64(n, 42, 0, 50, 1)
+    want = []
+    for kk in list(range(32)) + [None]:
+        m = (x > 24) & (kn if kk is None else (~kn & (k == kk)))
+        if not m.any():
+            continue
+        vs = v[m & ~vn]
+        want.append([_cell(kk), str(int(m.sum())), str(len(vs)), str(int(vs.astype(object).sum())) if len(vs) else ""])
+    assert rows == want
+    # every key NULL: one group
+    q(c, f"CREATE TABLE an AS SELECT CAST(NULL AS INTEGER) AS k, i AS v FROM range(1000) tbl(i)")
+    assert q(c, "SELECT k, COUNT(*), SUM(v) FROM an GROUP BY k").rows == [["", "1000", str(sum(range(1000)))]]
+    c.close()
+
+
+def test_null_keys_1e9_rows(mbx, oracle):
+    """The shape at 1e9 rows (14 % NULL keys, 14 % NULL values in each of two
+    INT64 columns): every group against the oracle over all rows."""
+    import os
+    n = 1_000_000_000
+    c = _conn(mbx)
+    _setup(c, n)
+    got = q(c, SQL).rows
+    assert "group_direct" in _kernels(c), _kernels(c)
+    exp = _expect(oracle.synth_groupby_nulls(SEEDS, MODS, ADDS, 0, n, max(8, len(os.sched_getaffinity(0)))))
+    assert got == exp
+    c.close()
+
+
+@pytest.mark.parametrize("combine", ["host", "rccl_loopback"])
+def test_null_keys_sharded(mbx, oracle, combine):
+    """The same GROUP BY over 3 row-range shards: each shard's partial groups
+    (the NULL key among them) combined by the host merge or by the RCCL
+    combine's dense key slots (loopback on one GPU); against the oracle, and
+    every shard's partial against its own row range."""
+    n = 3_000_017
+    c = _conn(mbx, "0,0,0", combine)
+    _setup(c, n)
+    got = q(c, SQL).rows
+    assert got == _expect(oracle.synth_groupby_nulls(SEEDS, MODS, ADDS, 0, n, 8))
+    if combine == "rccl_loopback":
+        st = c.rccl_stats()
+        assert st["note"] == "" and st["rccl_group_combines"] >= 1, st
+    for i in range(3):
+        lo, hi = n * i // 3, n * (i + 1) // 3
+        part = c.shard_partial(i)
+        rows, _ = part.cells()
+        part.close()
+        exp = oracle.synth_groupby_nulls(SEEDS, MODS, ADDS, lo, hi - lo, 8)
+        # partial columns: key, COUNT(*), then per value COUNT / SUM / MIN / MAX in the plan's order
+        assert len(rows) == len(exp), i
+        assert [r[0] for r in rows] == [_cell(e[0]) for e in exp], i
+    c.close()
