@@ -86,7 +86,9 @@ def main():
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--rows", type=int, default=None,
                     help="rows per GPU (default 1e9; 1.25e9 for c5 = 1e10 over 8 GPUs)")
-    ap.add_argument("--config", default="c2", choices=["c1", "c2", "c2d", "c3", "c4", "c5", "sel"])
+    ap.add_argument("--config", default="c2", choices=["c1", "c2", "c2d", "c3", "c3n", "c3h", "c4", "c5", "sel"])
+    ap.add_argument("--groups", type=int, default=100_000,
+                    help="c3h: distinct INT64 keys of the hash GROUP BY (1e5 and 1e6 are the measured points)")
     ap.add_argument("--extra", default="auto",
                     help="comma-separated sub-benchmarks (c3, sel) reported under the headline line's "
                          "\"extra\" key; auto = c3,sel for the 1-GPU C2 line, none otherwise")
@@ -199,9 +201,43 @@ def inlib_plan(args, world):
             "rows_total": args.rows * ngpu, "parallelism": par}
 
 
-def workload(config, start, n):
+# c3n: C3 with NULLs -- 1/7 of the keys and 1/7 of the values NULL (the
+# generator of tests/test_gpu_group_nulls.py and oracle.c orc_synth_groupby_nulls)
+C3N_SEEDS = [7, 19, 9, 23, 31, 29]
+C3N_MODS = [32, 7, 1 << 40, 7, 1 << 40, 0]
+C3N_ADDS = [-(1 << 39), -(1 << 39)]
+
+
+def workload(config, start, n, groups=100_000):
     """SQL and accounting of one bench config over rows [start, start + n)."""
     w = {"c2like": config in ("c2", "c2d")}
+    if config == "c3n":
+        w["table"] = "t3n"
+        w["setup"] = (f"CREATE TABLE t3n AS SELECT CASE WHEN mbx_synth(19, i, 7) = 0 THEN NULL "
+                      f"ELSE CAST(mbx_synth(7, i, 32) AS INTEGER) END AS k, "
+                      f"CASE WHEN mbx_synth(23, i, 7) = 0 THEN NULL ELSE mbx_synth(9, i, 1099511627776) - 549755813888 "
+                      f"END AS v FROM range({start}, {start + n}) tbl(i)")
+        w["sql"] = "SELECT k, SUM(v), COUNT(*) FROM t3n GROUP BY k"
+        w["kernel"] = "group_direct"
+        w["bytes_per_row"] = 12.25  # 4 B key + 8 B value + the two columns' validity bits
+        w["workload"] = ("C3 with NULLs: SELECT k, SUM(v), COUNT(*) FROM t GROUP BY k over 1e9 rows (INT32 key, 32 "
+                         "groups + the NULL group; 1/7 of keys and 1/7 of values NULL)")
+        w["data"] = ("synthetic: k = splitmix64(7 + i) mod 32 (INT32, NULL where splitmix64(19 + i) mod 7 = 0), "
+                     "v = splitmix64(9 + i) mod 2^40 - 2^39 (INT64, NULL where splitmix64(23 + i) mod 7 = 0), "
+                     "generated on device (no dataset)")
+        return w
+    if config == "c3h":
+        w["table"] = "th"
+        w["setup"] = (f"CREATE TABLE th AS SELECT mbx_synth(7, i, {groups}) AS k, "
+                      f"mbx_synth(9, i, 1099511627776) - 549755813888 AS v FROM range({start}, {start + n}) tbl(i)")
+        w["sql"] = "SELECT k, SUM(v), COUNT(*) FROM th GROUP BY k"
+        w["kernel"] = "*"  # every kernel of the statement: the hash GROUP BY is a pipeline
+        w["bytes_per_row"] = 16
+        w["workload"] = (f"hash GROUP BY: SELECT k, SUM(v), COUNT(*) FROM t GROUP BY k over 1e9 rows "
+                         f"({groups} distinct INT64 keys, INT64 value)")
+        w["data"] = (f"synthetic: k = splitmix64(7 + i) mod {groups} (INT64), v = splitmix64(9 + i) mod 2^40 - 2^39 "
+                     f"(INT64), generated on device (no dataset)")
+        return w
     if config in ("c2", "c2d", "c5", "sel"):
         # c2d: C2 over DECIMAL(15,2) (raw = 100 x; x > 24 is raw > 2400)
         xexpr = "CAST(mbx_synth(42, i, 50) + 1 AS DECIMAL(15,2))" if config == "c2d" else "mbx_synth(42, i, 50) + 1"
@@ -255,7 +291,15 @@ def make_step(conn, config, sql, decode=True):
             a.close()
             return [rows]
         rr = conn.query_raw(sql)
-        if config == "c3":
+        if config == "c3h" and not decode:
+            # 1e5+ groups: the step ends at the materialised result (the
+            # library's D2H and cell text); the cells are pulled once after
+            # the timed loop for parity (a Python list of 3e5 strings per
+            # step would time the interpreter, not the query)
+            rows = rr.row_count()
+            rr.close()
+            return ("c3hrows", rows)
+        if config in ("c3", "c3n", "c3h"):
             rows, nulls = rr.cells()
             cells = ("c3cells", rows, nulls)
             if decode:
@@ -267,7 +311,7 @@ def make_step(conn, config, sql, decode=True):
     return step
 
 
-def parity_check(conn, config, sql, out, start, n, threads):
+def parity_check(conn, config, sql, out, start, n, threads, groups=100_000):
     """The GPU answer over rows [start, start + n) against the CPU oracle at full
     size (test infrastructure: checker only, outside the timed loop)."""
     sys.path.insert(0, HERE)
@@ -285,6 +329,19 @@ def parity_check(conn, config, sql, out, start, n, threads):
         got = sorted(out, key=lambda g: (g[0] is None, g[0]))
         return {"groups": len(got), "oracle_groups": len(exp), "match": got == exp,
                 "checked": "every group's COUNT and exact int128 SUM over all rows"}, exp
+    if config == "c3n":
+        g = orc.synth_groupby_nulls(C3N_SEEDS, C3N_MODS, C3N_ADDS, start, n, threads)
+        exp = [(e[0], e[1], e[3]) for e in g]  # (key or None, COUNT(*), SUM(v) or None)
+        got = sorted(out, key=lambda x: (x[0] is None, x[0] if x[0] is not None else 0))
+        return {"groups": len(got), "oracle_groups": len(exp), "match": got == exp,
+                "checked": "every group's COUNT(*) and exact int128 SUM over the valid values, the NULL key's "
+                           "group included, over all rows (oracle.c orc_synth_groupby_nulls)"}, exp
+    if config == "c3h":
+        oc, osum = orc.synth_groupby(7, 9, start, n, groups, 1 << 40, -(1 << 39), min(threads, 32))
+        exp = [(k, oc[k], osum[k]) for k in range(groups) if oc[k]]
+        got = sorted(out, key=lambda g: (g[0] is None, g[0]))
+        return {"groups": len(got), "oracle_groups": len(exp), "match": got == exp,
+                "checked": f"every one of the {len(exp)} groups' COUNT and exact int128 SUM over all rows"}, exp
     # sel: the full compacted column (one more query, pulled through the int64
     # Arrow getter in slices) against the oracle's order-preserving selection
     import numpy as np
@@ -385,6 +442,10 @@ def kernel_stats(kern, kernel, nshards, steps):
     mean per launch and, per step, the slowest shard."""
     if not isinstance(kern, list):
         kern = kern.profile_drain()
+    if kernel == "*":  # a multi-kernel pipeline: every kernel of the statement, per step
+        ks = [k["ms"] for k in kern]
+        per = sum(ks) / steps if steps and ks else None
+        return per, per, ks
     ks = [k["ms"] for k in kern if k["name"] == kernel]
     if not ks:
         return None, None, []
@@ -433,7 +494,7 @@ def run_inlib(args, world, rank, vote=None):
         fail(dist, f"connect over gpu_devices={plan['devices']} failed: {r.error.message}")
     conn = r.value
     n_total = plan["rows_total"]
-    w = workload(args.config, 0, n_total)
+    w = workload(args.config, 0, n_total, args.groups)
     t0 = time.time()
     res = conn.query(w["setup"])
     if isinstance(res, mbx.Err):
@@ -449,14 +510,20 @@ def run_inlib(args, world, rank, vote=None):
         cb0 = conn.rccl_stats()
         elapsed, out = time_steps(step, args.steps, 0, barrier,
                                   torch.cuda.synchronize if torch.cuda.is_available() else None)
+        kern_timed = None
+        if isinstance(out, tuple) and out[0] == "c3hrows":  # the cells of the same query, pulled once
+            kern_timed = conn.profile_drain()
+            out = make_step(conn, args.config, w["sql"], decode=True)()
+            conn.profile_drain()
         out = decode_c3(out)
         sr_out = sel_outcomes(conn, sr0)
         cb1 = conn.rccl_stats()
         cb_out = combine_delta(cb0, cb1)
     except Exception as ex:  # noqa: BLE001 - a shard's error names the shard and its device
         fail(dist, f"query failed: {ex}")
-    kern = conn.profile_drain()
+    kern = conn.profile_drain() if kern_timed is None else kern_timed
     avg_k, step_k, _ = kernel_stats(kern, w["kernel"], plan["nshards"], args.steps)
+    split = kernel_split(kern, args.steps)
     sstats = conn.shard_stats() if plan["nshards"] > 1 else None
     if dist:
         t_all = torch.tensor([elapsed], dtype=torch.float64)
@@ -467,7 +534,7 @@ def run_inlib(args, world, rank, vote=None):
     if sstats and args.config in ("c2", "c2d", "c5", "c3"):
         parity, shard_par = sharded_parity(conn, args.config, out, n_total, plan["nshards"], threads)
     else:
-        parity, _ = parity_check(conn, args.config, w["sql"], out, 0, n_total, threads)
+        parity, _ = parity_check(conn, args.config, w["sql"], out, 0, n_total, threads, args.groups)
     if sstats:
         parity["checked"] = (f"the global answer over all {n_total} rows ({plan['nshards']} shards, merged in the "
                              f"library) vs the oracle over the same rows"
@@ -477,6 +544,9 @@ def run_inlib(args, world, rank, vote=None):
                       sel_rows=int(out[0]) if args.config == "sel" else None)
     if vote:
         result["config"]["form"] = vote
+    if args.config in ("c3h", "c3n"):
+        # the statement's kernels, ms per step (HIP events per profiled scope)
+        result["kernel_split_ms_per_step"] = split
     stuck = False
     if sstats:
         ms = elapsed / args.steps * 1e3
@@ -540,8 +610,9 @@ def run_inlib(args, world, rank, vote=None):
             result["extra"]["rccl_selftest"] = mbx.rccl_selftest([0])
         except Exception as ex:  # noqa: BLE001
             result["extra"]["rccl_selftest"] = {"ok": False, "error": str(ex)}
-    if not args.no_cpu and plan["nshards"] == 1 and args.config in ("c2", "c2d", "c3", "c5", "sel"):
-        result["cpu_baseline"] = cpu_baseline(args.cpu_seconds, "c2" if args.config == "c2d" else args.config)
+    if not args.no_cpu and plan["nshards"] == 1 and args.config in ("c2", "c2d", "c3", "c3n", "c3h", "c5", "sel"):
+        result["cpu_baseline"] = cpu_baseline(args.cpu_seconds, {"c2d": "c2", "c3n": "c3"}.get(args.config, args.config),
+                                              args.groups)
     if dist:
         dist.barrier()
         dist.destroy_process_group()
@@ -745,6 +816,14 @@ def fail(dist, msg):
         except Exception:  # noqa: BLE001
             pass
     raise SystemExit(2)
+
+
+def kernel_split(kern, steps):
+    """ms per step of every profiled kernel scope of the timed loop, by name."""
+    acc = {}
+    for k in kern:
+        acc[k["name"]] = acc.get(k["name"], 0.0) + k["ms"]
+    return {n: v / steps for n, v in sorted(acc.items(), key=lambda t: -t[1])} if steps else {}
 
 
 def per_shard_kernel_ms(kern, kernel, nshards):
@@ -1395,7 +1474,7 @@ def cgroup_cpus():
         return None
 
 
-def cpu_baseline(seconds, config="c2"):
+def cpu_baseline(seconds, config="c2", groups=100_000):
     """The oracle's multi-threaded C scan over a materialised sample of the same
     column(s): orc_filter_agg_i64 (C2/C5: COUNT/SUM/MIN/MAX WHERE x > 24),
     orc_groupby_sum_i32_i64 (C3: per-key COUNT and int128 SUM) or
@@ -1413,13 +1492,15 @@ def cpu_baseline(seconds, config="c2"):
     quota = cgroup_cpus()
     qthreads = min(aff, max(1, math.ceil(quota))) if quota else aff
     l3 = l3_bytes()
-    bpr = 12 if config == "c3" else 8
+    bpr = 12 if config in ("c3", "c3h") else 8
     sample = max(250_000_000, -(-4 * l3 // bpr))
-    if config == "c3":
-        k = orc.synth_i32(sample, 7, 0, 32, 0)
+    if config in ("c3", "c3h"):
+        nk = 32 if config == "c3" else groups
+        k = orc.synth_i32(sample, 7, 0, nk, 0)
         v = orc.synth_i64(sample, 9, 0, 1 << 40, -(1 << 39))
-        mk = lambda th: (lambda: orc.groupby_sum(k, v, 0, 32, th))  # noqa: E731
-        what = "GROUP BY k: COUNT(*), SUM(v) (int128), 32 keys"
+        mk = lambda th: (lambda: orc.groupby_sum(k, v, 0, nk, th))  # noqa: E731
+        what = f"GROUP BY k: COUNT(*), SUM(v) (int128), {nk} keys" + \
+            (" (direct-indexed per-thread tables of the oracle; INT32 keys)" if config == "c3h" else "")
     elif config == "sel":
         import numpy as np
         x = orc.synth_i64(sample, 42, 0, 50, 1)

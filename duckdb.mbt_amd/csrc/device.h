@@ -138,6 +138,35 @@ bool GroupByDirectStates(const void *kcol, int kphys, int64_t kmin, int nk, cons
                          const GroupValidity *valid = nullptr,  // NULL-able key / values: false if unsupported
                          GroupPartialsOut *po = nullptr);
 
+// --- GROUP BY one integer key over a wide range (group_part.hip) ----------
+// Keys in [kmin, kmin + range) without NULLs, up to 2 value columns of one
+// phys without NULLs; rows partitioned by key range (hist, scan, scatter),
+// each partition reduced in an LDS table.  Writes COUNT(*) into cstar[range]
+// and the states of value column j into st0[j * range ..] (every key: empty
+// keys as InitAggStatesCounts leaves them).  false: the shape does not fit
+// (range above PartGroupMaxRange, n >= 2^32, a value bound that would make the
+// pieces too small).
+constexpr int kPartGroupMaxParts = 4096;
+int PartGroupShift(int nv, bool mm);          // log2 keys per partition
+int64_t PartGroupMaxRange(int nv, bool mm);
+struct PartGroupDesc {
+  const void *key;
+  int kphys;
+  int64_t kmin, range;
+  const void *v0, *v1;
+  int vphys, nv;
+  bool mm;
+  int64_t n;
+  uint64_t vmaxabs;  // max |value| (zone maps); 0 = no value columns
+  unsigned long long *cstar;
+  AggState *st0;  // [nv >= 2 ? 2 * range : range]
+  void *scratch_hist, *scratch_start, *scratch_rows, *scratch_scan;
+  size_t scratch_scan_bytes;
+};
+void PartGroupScratch(int64_t n, int64_t range, int nv, bool mm, int vphys, size_t *hist_bytes, size_t *start_bytes,
+                      size_t *rows_bytes, size_t *scan_bytes);
+bool PartGroup(const PartGroupDesc &d, hipStream_t s);
+
 // --- generic aggregation over compacted columns ---------------------------
 // vclass: VC_I64 / VC_I128 / VC_F64 of the input column (phys given)
 void ReduceColumn(const void *col, int phys, const uint64_t *valid, int64_t n, AggState *out, hipStream_t s);

@@ -2106,6 +2106,114 @@ static bool CountMayStayOnDevice(const Engine &e, const BoundSelect &s) {
   return true;
 }
 
+// F3: GROUP BY one integer key (no NULLs) whose zone-map range is too wide for
+// F2's LDS tables but dense enough for per-key state arrays (1024 < range <=
+// PartGroupMaxRange, range <= 4 n), no WHERE, COUNT / SUM / MIN / MAX / AVG over
+// <= 2 integer columns of one phys without NULLs: rows partitioned by key
+// range, each partition reduced in LDS (group_part.hip), then the non-empty
+// keys compacted and emitted in key order as F2 does.  false: the shape does
+// not fit (the hash path or the run-time compiled kernel takes it).
+static bool PartGroupAggregate(Engine &e, const DRel &src, const BoundSelect &s, DRel &out) {
+  const int na = (int)s.aggs.size();
+  if (s.groups.size() != 1 || s.where || src.range || src.n <= 0 || src.n >= ((int64_t)1 << 32)) return false;
+  if (s.groups[0]->kind != BExpr::COL || !FastIntCol(src, s.groups[0]->col)) return false;
+  const DCol &K = src.cols[s.groups[0]->col];
+  const DevColumn *ks = K.table_col;
+  if (!ks || !ks->stats_valid || ks->null_count != 0) return false;
+  const i128 range = ks->imax - ks->imin + 1;
+  std::vector<int> vcols;
+  bool mm = false;
+  for (auto &a : s.aggs) {
+    if (a.kind == A_COUNT_STAR) continue;
+    if (a.distinct) return false;
+    const BExpr *x = a.arg ? StripWidening(a.arg.get()) : nullptr;
+    if (!x || x->kind != BExpr::COL || !FastIntCol(src, x->col) || a.arg->type.id == T_DOUBLE ||
+        a.arg->type.id == T_FLOAT)
+      return false;
+    if (a.kind == A_MIN || a.kind == A_MAX) mm = true;
+    if (std::find(vcols.begin(), vcols.end(), x->col) == vcols.end()) vcols.push_back(x->col);
+  }
+  const int nv = (int)vcols.size();
+  if (nv > 2 || (nv == 2 && src.cols[vcols[0]].phys != src.cols[vcols[1]].phys)) return false;
+  if (range <= 1024 || range > dev::PartGroupMaxRange(nv, mm) || range > 4 * (i128)src.n) return false;
+  i128 maxabs = 0;
+  for (int c : vcols) {
+    const DevColumn *vs = src.cols[c].table_col;
+    if (!vs || !vs->stats_valid) return false;
+    maxabs = std::max(maxabs, std::max(vs->imax < 0 ? -vs->imax : vs->imax, vs->imin < 0 ? -vs->imin : vs->imin));
+  }
+  if (maxabs >= ((i128)1 << 62)) return false;
+  const int64_t nslots = (int64_t)range;
+  const Phys vphys = nv ? src.cols[vcols[0]].phys : P_I64;
+  size_t hb = 0, sb = 0, rb = 0, cb = 0;
+  dev::PartGroupScratch(src.n, nslots, nv, mm, vphys, &hb, &sb, &rb, &cb);
+  auto cs = Alloc(e, nslots * 8);
+  auto stb = Alloc(e, (size_t)(nv >= 2 ? 2 : 1) * nslots * sizeof(dev::AggState));
+  auto hist = Alloc(e, hb), startb = Alloc(e, sb), rows = Alloc(e, rb), scan = Alloc(e, cb);
+  dev::PartGroupDesc d;
+  memset(&d, 0, sizeof(d));
+  d.key = K.data;
+  d.kphys = K.phys;
+  d.kmin = (int64_t)ks->imin;
+  d.range = nslots;
+  d.v0 = nv > 0 ? src.cols[vcols[0]].data : nullptr;
+  d.v1 = nv > 1 ? src.cols[vcols[1]].data : nullptr;
+  d.vphys = vphys;
+  d.nv = nv;
+  d.mm = mm;
+  d.n = src.n;
+  d.vmaxabs = nv ? (uint64_t)std::max<i128>(maxabs, 1) : 0;
+  d.cstar = (unsigned long long *)cs->p;
+  d.st0 = (dev::AggState *)stb->p;
+  d.scratch_hist = hist->p, d.scratch_start = startb->p, d.scratch_rows = rows->p, d.scratch_scan = scan->p;
+  d.scratch_scan_bytes = cb;
+  // algorithmic bytes: the key and value columns once
+  double bytes = (double)src.n * PhysSize(K.phys);
+  for (int c : vcols) bytes += (double)src.n * PhysSize(src.cols[c].phys);
+  {
+    ProfScope ps(e, "group_part", bytes, src.n);
+    if (!dev::PartGroup(d, e.stream)) return false;
+  }
+  dev::AggState *const s0p = d.st0, *const s1p = d.st0 + nslots;
+  auto list = Alloc(e, nslots * 4);
+  const bool defer = CountMayStayOnDevice(e, s);
+  DevBufPtr nbuf = defer ? Alloc(e, 8) : nullptr;
+  int64_t *const n_out = defer ? (int64_t *)nbuf->p : e.d_scratch;
+  dev::CompactSlots((const unsigned long long *)cs->p, nslots, (int32_t *)list->p, n_out, e.stream);
+  dev::EmitDesc D;
+  memset(&D, 0, sizeof(D));
+  D.nagg = na;
+  D.cstar = (const unsigned long long *)cs->p;
+  D.slot_list = (const int32_t *)list->p;
+  D.n_list = n_out;
+  D.nslots = nslots;
+  D.has_key = 1;
+  D.key_phys = PhysOf(s.groups[0]->type);
+  D.kmin = (int64_t)ks->imin;
+  D.null_slot = -1;
+  DCol kc = AllocOut(e, s.groups[0]->type, nslots, true, false);
+  D.key_out = kc.data;
+  D.key_valid = (uint32_t *)kc.validity;
+  out.cols.clear();
+  out.cols.push_back(kc);
+  for (int j = 0; j < na; j++) {
+    DCol oc = AllocOut(e, s.aggs[j].type, nslots, true, false);
+    dev::AggState *stp = nullptr;
+    if (s.aggs[j].kind != A_COUNT_STAR) stp = StripWidening(s.aggs[j].arg.get())->col == vcols[0] ? s0p : s1p;
+    D.a[j] = EmitFor(s.aggs[j], VC_I64, stp, oc);
+    out.cols.push_back(oc);
+  }
+  dev::EmitAggRelation(D, e.stream);
+  if (defer) {
+    out.n = nslots;  // the columns hold every slot; the count follows the rows to the host
+    out.n_dev = n_out;
+    out.n_owner = nbuf;
+  } else {
+    out.n = ReadDev<int64_t>(e, n_out);
+  }
+  return true;
+}
+
 static DRel Aggregate(Engine &e, const DRel &src, const BoundSelect &s) {
   const int ng = (int)s.groups.size();
   const int na = (int)s.aggs.size();
@@ -2374,6 +2482,11 @@ static DRel Aggregate(Engine &e, const DRel &src, const BoundSelect &s) {
         }
       }
     }
+  }
+  // ---- fast path F3: one integer key over a wide range, partitioned
+  if (ng == 1) {
+    DRel part_out;
+    if (PartGroupAggregate(e, src, s, part_out)) return part_out;
   }
 generic:
   // ---- generic path: compact [groups..., agg args...] then reduce

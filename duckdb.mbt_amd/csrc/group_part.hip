@@ -1,0 +1,296 @@
+// group_part.hip — GROUP BY one integer key over a key range too wide for
+// one LDS table (the zone map bounds it to (1024, PartGroupMaxRange]): rows are
+// partitioned by key range, then every partition is reduced in LDS.
+//
+// Why not per-row global atomics (the hash path's group_reduce): on MI355X a
+// global atomic executes at the memory side, one request per lane when the
+// lanes hit scattered rows (MI355X_MICROARCH.md §Global float atomics; the
+// integer form behaves alike), so a row-at-a-time reduction of 1e9 rows into
+// 1e5 groups ran 205 ms for its atomics alone (profiles/r06_hash/).  Here
+// every row's aggregate update is an LDS atomic, and HBM sees three streams:
+//   1. pg_hist     each workgroup counts its contiguous row chunk's rows per
+//                  partition (partition = (key - kmin) >> shift) in LDS;
+//                  keys only;
+//   2. (scan)      exclusive prefix over [partition][workgroup] counts:
+//                  partition p's rows land in one contiguous run, every
+//                  workgroup its own sub-run;
+//   3. pg_scatter  the same chunks again: each row takes its slot from an LDS
+//                  cursor of its partition and is written as (key - kmin) u32
+//                  + its value columns; a workgroup keeps a few hundred open
+//                  write streams, so lines fill in L2 before they leave;
+//   4. pg_reduce   the partitioned rows in fixed-size pieces (grid = pieces):
+//                  each piece walks the partitions it overlaps, adds its rows
+//                  into an LDS table of the partition's keys (COUNT, int64
+//                  sums made overflow-free by the piece size, MIN / MAX), and
+//                  flushes the non-empty keys with one carry-correct int128
+//                  atomic set per key into the dense per-key states.
+// HBM bytes per row: key (hist) + key + values (scatter in) + 4 + values
+// (scatter out) + 4 + values (reduce in); INT64 key and value: 48 B against
+// the 16 B the query names.
+#include <hip/hip_runtime.h>
+#include <hipcub/hipcub.hpp>
+#include <stdint.h>
+
+#include <algorithm>
+#include <stdexcept>
+
+#include "device.h"
+#include "phys.h"
+
+namespace mbx {
+namespace dev {
+
+namespace {
+constexpr int kPassThreads = 1024;  // one workgroup of 16 waves per CU in the hist / scatter passes
+constexpr int kReduceThreads = 1024;  // the reduce pass: one 16-wave workgroup per CU (its LDS table bounds it)
+
+__device__ __forceinline__ void state_add(AggState *st, unsigned long long cnt, long long sum, long long mn,
+                                          long long mx, bool mm) {
+  atomicAdd(&st->count, cnt);
+  const unsigned long long lo = (unsigned long long)sum;
+  const unsigned long long old = atomicAdd(&st->sum_lo, lo);
+  const unsigned long long carry = old + lo < old ? 1ull : 0ull;
+  const unsigned long long hi = (unsigned long long)(sum >> 63) + carry;
+  if (hi) atomicAdd((unsigned long long *)&st->sum_hi, hi);
+  if (mm) {
+    atomicMin(&st->min_i, mn);
+    atomicMax(&st->max_i, mx);
+  }
+}
+}  // namespace
+
+// rows [w * chunk, min(n, (w + 1) * chunk)) of workgroup w
+template <typename TK>
+__global__ __launch_bounds__(1024) void pg_hist_kernel(const TK *__restrict__ key, int64_t n, int64_t chunk,
+                                                      int64_t kmin, int shift, int np,
+                                                      unsigned int *__restrict__ hist /* [np][grid] */) {
+  extern __shared__ unsigned int h[];
+  for (int p = threadIdx.x; p < np; p += blockDim.x) h[p] = 0;
+  __syncthreads();
+  const int64_t b = (int64_t)blockIdx.x * chunk, e = min(n, b + chunk);
+  const int64_t B = blockDim.x;
+  int64_t i = b + threadIdx.x;
+  for (; i + 3 * B < e; i += 4 * B) {  // four rows in flight per lane
+    int64_t k[4];
+#pragma unroll
+    for (int u = 0; u < 4; u++) k[u] = (int64_t)key[i + u * B];
+#pragma unroll
+    for (int u = 0; u < 4; u++) atomicAdd(&h[(int)((uint64_t)(k[u] - kmin) >> shift)], 1u);
+  }
+  for (; i < e; i += B) atomicAdd(&h[(int)((uint64_t)((int64_t)key[i] - kmin) >> shift)], 1u);
+  __syncthreads();
+  for (int p = threadIdx.x; p < np; p += blockDim.x) hist[(size_t)p * gridDim.x + blockIdx.x] = h[p];
+}
+
+template <typename TK, typename TV, int NV>
+__global__ __launch_bounds__(1024) void pg_scatter_kernel(const TK *__restrict__ key, const TV *__restrict__ v0,
+                                                         const TV *__restrict__ v1, int64_t n, int64_t chunk,
+                                                         int64_t kmin, int shift, int np,
+                                                         const unsigned int *__restrict__ off /* [np][grid] */,
+                                                         uint32_t *__restrict__ ok, TV *__restrict__ ov0,
+                                                         TV *__restrict__ ov1) {
+  extern __shared__ unsigned int cur[];
+  for (int p = threadIdx.x; p < np; p += blockDim.x) cur[p] = off[(size_t)p * gridDim.x + blockIdx.x];
+  __syncthreads();
+  const int64_t b = (int64_t)blockIdx.x * chunk, e = min(n, b + chunk);
+  auto put = [&](int64_t k, TV a, TV c) {
+    const uint32_t rel = (uint32_t)(k - kmin);
+    const unsigned int pos = atomicAdd(&cur[rel >> shift], 1u);
+    ok[pos] = rel;
+    if (NV >= 1) ov0[pos] = a;
+    if (NV >= 2) ov1[pos] = c;
+  };
+  const int64_t B = blockDim.x;
+  int64_t i = b + threadIdx.x;
+  for (; i + 3 * B < e; i += 4 * B) {
+    int64_t k[4];
+    TV a[4], c[4];
+#pragma unroll
+    for (int u = 0; u < 4; u++) {
+      k[u] = (int64_t)key[i + u * B];
+      if (NV >= 1) a[u] = v0[i + u * B];
+      if (NV >= 2) c[u] = v1[i + u * B];
+    }
+#pragma unroll
+    for (int u = 0; u < 4; u++) put(k[u], NV >= 1 ? a[u] : (TV)0, NV >= 2 ? c[u] : (TV)0);
+  }
+  for (; i < e; i += B) put((int64_t)key[i], NV >= 1 ? v0[i] : (TV)0, NV >= 2 ? v1[i] : (TV)0);
+}
+
+// Piece q = rows [q * piece, min(n, (q + 1) * piece)) of the partitioned
+// arrays; start[p] = first row of partition p (start[np] = n).  LDS: the
+// partition's table of KP keys -- COUNT(*) u32, then per value column its int64
+// sum (and min / max).
+template <typename TV, int NV, bool MM>
+__global__ __launch_bounds__(1024) void pg_reduce_kernel(const uint32_t *__restrict__ rk, const TV *__restrict__ rv0,
+                                                        const TV *__restrict__ rv1, int64_t n, int64_t piece,
+                                                        const unsigned int *__restrict__ start, int np, int shift,
+                                                        int64_t range, unsigned long long *__restrict__ cstar,
+                                                        AggState *__restrict__ st0, AggState *__restrict__ st1) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
+  const int KP = 1 << shift;
+  unsigned int *cnt = (unsigned int *)lds;
+  long long *sum0 = (long long *)(lds + (size_t)KP * 4);
+  long long *sum1 = sum0 + KP;
+  long long *mn0 = sum0 + (NV >= 2 ? 2 : 1) * KP, *mx0 = mn0 + KP, *mn1 = mx0 + KP, *mx1 = mn1 + KP;
+  const int64_t a = (int64_t)blockIdx.x * piece, z = min(n, a + piece);
+  if (a >= z) return;
+  // the first partition that ends after a (start is ascending; np <= 4096)
+  int lo = 0, hi = np - 1;
+  while (lo < hi) {
+    const int mid = (lo + hi) >> 1;
+    if ((int64_t)start[mid + 1] <= a) lo = mid + 1;
+    else hi = mid;
+  }
+  for (int p = lo; p < np && (int64_t)start[p] < z; p++) {
+    const int64_t s0 = max(a, (int64_t)start[p]), s1 = min(z, (int64_t)start[p + 1]);
+    if (s0 >= s1) continue;
+    for (int j = threadIdx.x; j < KP; j += blockDim.x) {
+      cnt[j] = 0;
+      if (NV >= 1) sum0[j] = 0;
+      if (NV >= 2) sum1[j] = 0;
+      if (MM) {
+        mn0[j] = INT64_MAX, mx0[j] = INT64_MIN;
+        if (NV >= 2) mn1[j] = INT64_MAX, mx1[j] = INT64_MIN;
+      }
+    }
+    __syncthreads();
+    const uint32_t base = (uint32_t)p << shift;
+    auto add = [&](uint32_t k, TV x, TV y) {
+      const int j = (int)(k - base);
+      atomicAdd(&cnt[j], 1u);
+      if (NV >= 1) atomicAdd((unsigned long long *)&sum0[j], (unsigned long long)(long long)x);
+      if (NV >= 2) atomicAdd((unsigned long long *)&sum1[j], (unsigned long long)(long long)y);
+      if (MM) {
+        atomicMin(&mn0[j], (long long)x), atomicMax(&mx0[j], (long long)x);
+        if (NV >= 2) atomicMin(&mn1[j], (long long)y), atomicMax(&mx1[j], (long long)y);
+      }
+    };
+    const int64_t B = blockDim.x;
+    int64_t i = s0 + threadIdx.x;
+    for (; i + 3 * B < s1; i += 4 * B) {
+      uint32_t k[4];
+      TV x[4], y[4];
+#pragma unroll
+      for (int u = 0; u < 4; u++) {
+        k[u] = rk[i + u * B];
+        if (NV >= 1) x[u] = rv0[i + u * B];
+        if (NV >= 2) y[u] = rv1[i + u * B];
+      }
+#pragma unroll
+      for (int u = 0; u < 4; u++) add(k[u], NV >= 1 ? x[u] : (TV)0, NV >= 2 ? y[u] : (TV)0);
+    }
+    for (; i < s1; i += B) add(rk[i], NV >= 1 ? rv0[i] : (TV)0, NV >= 2 ? rv1[i] : (TV)0);
+    __syncthreads();
+    for (int j = threadIdx.x; j < KP; j += blockDim.x) {
+      const unsigned int c = cnt[j];
+      const int64_t key = (int64_t)base + j;
+      if (!c || key >= range) continue;
+      atomicAdd(&cstar[key], (unsigned long long)c);
+      if (NV >= 1) state_add(&st0[key], c, sum0[j], MM ? mn0[j] : 0, MM ? mx0[j] : 0, MM);
+      if (NV >= 2) state_add(&st1[key], c, sum1[j], MM ? mn1[j] : 0, MM ? mx1[j] : 0, MM);
+    }
+    __syncthreads();
+  }
+}
+
+int PartGroupShift(int nv, bool mm) {
+  // the largest partition table (power of two) that fits the LDS budget
+  const int per_key = 4 + 8 * nv + (mm ? 16 * nv : 0);
+  int shift = 15;
+  while (shift > 10 && ((size_t)per_key << shift) > (size_t)128 * 1024) shift--;
+  return shift;
+}
+
+int64_t PartGroupMaxRange(int nv, bool mm) { return (int64_t)kPartGroupMaxParts << PartGroupShift(nv, mm); }
+
+bool PartGroup(const PartGroupDesc &d, hipStream_t s) {
+  if (d.range <= 0 || d.range > PartGroupMaxRange(d.nv, d.mm) || d.n <= 0 || d.n >= ((int64_t)1 << 32)) return false;
+  if (d.nv < 0 || d.nv > 2 || (d.kphys != P_I32 && d.kphys != P_I64)) return false;
+  if (d.nv > 0 && d.vphys != P_I32 && d.vphys != P_I64) return false;
+  const int shift = PartGroupShift(d.nv, d.mm);
+  const int np = (int)((d.range + (1 << shift) - 1) >> shift);
+  // int64 LDS sums stay exact over a piece: piece x max|v| < 2^62
+  int64_t piece = (int64_t)1 << 20;
+  if (d.nv > 0 && d.vmaxabs > 0) {
+    const uint64_t cap = ((uint64_t)1 << 62) / d.vmaxabs;
+    if (cap < 4096) return false;
+    piece = std::min<int64_t>(piece, (int64_t)cap);
+  }
+  const int grid = NumCUs();
+  const int64_t chunk = (d.n + grid - 1) / grid;
+  const int vb = d.vphys == P_I64 ? 8 : 4;
+  unsigned int *hist = (unsigned int *)d.scratch_hist;  // [np][grid] counts
+  unsigned int *off = hist + (size_t)np * grid;         // ... and their exclusive scan
+  unsigned int *start = (unsigned int *)d.scratch_start;  // [np + 1]
+  uint32_t *rk = (uint32_t *)d.scratch_rows;
+  void *rv0 = (char *)d.scratch_rows + (((size_t)d.n * 4 + 255) & ~(size_t)255);
+  void *rv1 = (char *)rv0 + (((size_t)d.n * vb + 255) & ~(size_t)255);
+  const size_t hl = (size_t)np * 4;
+  if (d.kphys == P_I64)
+    hipLaunchKernelGGL(pg_hist_kernel<int64_t>, dim3(grid), dim3(kPassThreads), hl, s, (const int64_t *)d.key, d.n,
+                       chunk, d.kmin, shift, np, hist);
+  else
+    hipLaunchKernelGGL(pg_hist_kernel<int32_t>, dim3(grid), dim3(kPassThreads), hl, s, (const int32_t *)d.key, d.n,
+                       chunk, d.kmin, shift, np, hist);
+  // partition p starts at the offset of its first workgroup's sub-run
+  size_t tmp = 0;
+  const int nh = np * grid;
+  (void)hipcub::DeviceScan::ExclusiveSum(nullptr, tmp, hist, off, nh, s);
+  if (tmp > d.scratch_scan_bytes) throw std::runtime_error("PartGroup: scan scratch too small");
+  (void)hipcub::DeviceScan::ExclusiveSum(d.scratch_scan, tmp, hist, off, nh, s);
+  (void)hipMemcpy2DAsync(start, 4, off, (size_t)grid * 4, 4, np, hipMemcpyDeviceToDevice, s);
+  (void)hipMemsetD32Async((hipDeviceptr_t)(start + np), (int)(unsigned int)d.n, 1, s);
+#define PGS(TK, TV, NV)                                                                                             \
+  hipLaunchKernelGGL((pg_scatter_kernel<TK, TV, NV>), dim3(grid), dim3(kPassThreads), hl, s, (const TK *)d.key,   \
+                     (const TV *)d.v0, (const TV *)d.v1, d.n, chunk, d.kmin, shift, np, off, rk, (TV *)rv0,       \
+                     (TV *)rv1)
+#define PGSV(TK)                                                                                                    \
+  if (d.vphys == P_I64) {                                                                                           \
+    if (d.nv == 0) PGS(TK, int64_t, 0); else if (d.nv == 1) PGS(TK, int64_t, 1); else PGS(TK, int64_t, 2);          \
+  } else {                                                                                                          \
+    if (d.nv == 0) PGS(TK, int32_t, 0); else if (d.nv == 1) PGS(TK, int32_t, 1); else PGS(TK, int32_t, 2);          \
+  }
+  if (d.kphys == P_I64) { PGSV(int64_t) } else { PGSV(int32_t) }
+#undef PGSV
+#undef PGS
+  InitAggStatesCounts(d.st0, d.nv >= 2 ? 2 * d.range : d.range, d.cstar, d.range, s);
+  const int npieces = (int)((d.n + piece - 1) / piece);
+  const size_t rl = ((size_t)4 << shift) +
+                    ((size_t)8 << shift) * (size_t)(d.nv == 0 ? 0 : d.nv + (d.mm ? 2 * d.nv : 0));
+#define PGR(TV, NV, MM)                                                                                             \
+  {                                                                                                                 \
+    (void)hipFuncSetAttribute((const void *)pg_reduce_kernel<TV, NV, MM>, hipFuncAttributeMaxDynamicSharedMemorySize, \
+                              160 * 1024);                                                                          \
+    hipLaunchKernelGGL((pg_reduce_kernel<TV, NV, MM>), dim3(npieces), dim3(kReduceThreads), rl, s, rk,           \
+                       (const TV *)rv0,                                                                             \
+                       (const TV *)rv1, d.n, piece, start, np, shift, d.range, d.cstar, d.st0,                      \
+                       d.st0 + d.range);                                                                            \
+  }
+#define PGRV(TV)                                                                                                    \
+  if (d.nv == 0) PGR(TV, 0, false)                                                                                  \
+  else if (d.nv == 1) { if (d.mm) PGR(TV, 1, true) else PGR(TV, 1, false) }                                          \
+  else { if (d.mm) PGR(TV, 2, true) else PGR(TV, 2, false) }
+  if (d.vphys == P_I64) { PGRV(int64_t) } else { PGRV(int32_t) }
+#undef PGRV
+#undef PGR
+  return hipGetLastError() == hipSuccess;
+}
+
+void PartGroupScratch(int64_t n, int64_t range, int nv, bool mm, int vphys, size_t *hist_bytes, size_t *start_bytes,
+                      size_t *rows_bytes, size_t *scan_bytes) {
+  const int shift = PartGroupShift(nv, mm);
+  const int np = (int)std::max<int64_t>(1, (range + (1 << shift) - 1) >> shift);
+  const int grid = NumCUs();
+  const int vb = vphys == P_I64 ? 8 : 4;
+  *hist_bytes = (size_t)np * grid * 4 * 2;  // counts and their scan
+  *start_bytes = (size_t)(np + 1) * 4;
+  *rows_bytes = (((size_t)n * 4 + 255) & ~(size_t)255) + (size_t)std::max(nv, 0) * (((size_t)n * vb + 255) & ~(size_t)255);
+  size_t tmp = 0;
+  unsigned int *dummy = nullptr;
+  (void)hipcub::DeviceScan::ExclusiveSum(nullptr, tmp, dummy, dummy, np * grid, (hipStream_t)0);
+  *scan_bytes = tmp ? tmp : 16;
+}
+
+}  // namespace dev
+}  // namespace mbx

@@ -1728,7 +1728,8 @@ __global__ __launch_bounds__(256) void group_direct_lds_kernel(const TK *__restr
   const int nslot = nk * R;
   const int null_key = (nk - 1) * R;  // KN: the NULL group's slots
   unsigned int *cnt = (unsigned int *)lds_raw;
-  long long *sum0 = (long long *)(lds_raw + ((nslot * 4 + 15) & ~15));
+  unsigned long long *cnt64 = (unsigned long long *)lds_raw;  // VN: {COUNT(*), valid rows of value 0}
+  long long *sum0 = (long long *)(lds_raw + ((nslot * (VN ? 8 : 4) + 15) & ~15));
   long long *sum1 = sum0 + nslot;
   long long *mn0 = sum0 + (NV >= 2 ? 2 : 1) * nslot;
   long long *mx0 = mn0 + nslot;
@@ -1736,14 +1737,13 @@ __global__ __launch_bounds__(256) void group_direct_lds_kernel(const TK *__restr
   long long *mx1 = mn1 + nslot;
   // valid-row counts per slot of the NULL-able value columns, after the table
   // (GroupDirectLds sizes them)
-  unsigned int *vcnt0 = (unsigned int *)(sum0 + (NV >= 2 ? 2 : 1) * nslot + (MM ? 2 * (NV >= 2 ? 2 : 1) * nslot : 0));
-  unsigned int *vcnt1 = vcnt0 + ((nslot + 3) & ~3);
+  unsigned int *vcnt1 = (unsigned int *)(sum0 + (NV >= 2 ? 2 : 1) * nslot + (MM ? 2 * (NV >= 2 ? 2 : 1) * nslot : 0));
   const int t = threadIdx.x, lane = t & 63, w = t >> 6;
   const int rep = lane % R;
   unsigned char *ring = lds_raw + ring_off + (size_t)w * DEPTH * SB;
   for (int i = t; i < nslot; i += blockDim.x) {
-    cnt[i] = 0;
-    if (V0N) vcnt0[i] = 0;
+    if (VN) cnt64[i] = 0;
+    else cnt[i] = 0;
     if (V1N) vcnt1[i] = 0;
     if (NV >= 1) sum0[i] = 0;
     if (NV >= 2) sum1[i] = 0;
@@ -1757,9 +1757,9 @@ __global__ __launch_bounds__(256) void group_direct_lds_kernel(const TK *__restr
   // each value column's sum / min / max over its valid rows
   auto row = [&](int64_t k, int64_t a, int64_t b, bool kv, bool va, bool vb) {
     const int sl = (KN && !kv) ? null_key + rep : (int)(k - kmin) * R + rep;
-    gd_add_u32(&cnt[sl], 1u);
+    if (VN) gd_add_u64((long long *)&cnt64[sl], 1ull + ((!V0N || va) ? (1ull << 32) : 0ull));
+    else gd_add_u32(&cnt[sl], 1u);
     if (NV >= 1 && (!V0N || va)) {
-      if (V0N) gd_add_u32(&vcnt0[sl], 1u);
       gd_add_u64(&sum0[sl], (unsigned long long)a);
       if (MM) { gd_min_i64(&mn0[sl], (long long)a); gd_max_i64(&mx0[sl], (long long)a); }
     }
@@ -1913,8 +1913,12 @@ __global__ __launch_bounds__(256) void group_direct_lds_kernel(const TK *__restr
     long long a0 = INT64_MAX, b0 = INT64_MIN, a1 = INT64_MAX, b1 = INT64_MIN;
     for (int r = 0; r < R; r++) {
       int sl = kq * R + r;
-      c += cnt[sl];
-      if (V0N) vc0 += vcnt0[sl];
+      if (VN) {
+        c += cnt64[sl] & 0xFFFFFFFFull;
+        vc0 += cnt64[sl] >> 32;
+      } else {
+        c += cnt[sl];
+      }
       if (V1N) vc1 += vcnt1[sl];
       if (NV >= 1) s0 += (i128)sum0[sl];
       if (NV >= 2) s1 += (i128)sum1[sl];
@@ -1976,10 +1980,10 @@ static void LaunchGroupDirect(const void *k, const void *v0, const void *v1, int
 
 size_t GroupDirectLds(int nk, int R, int nv, bool mm, int vm) {
   size_t nslot = (size_t)nk * R;
-  size_t b = (nslot * 4 + 15) & ~(size_t)15;
+  size_t b = (nslot * (vm ? 8 : 4) + 15) & ~(size_t)15;  // COUNT(*) (vm: + value 0's valid rows)
   b += nslot * 8 * (size_t)(nv >= 2 ? 2 : 1);
   if (mm) b += nslot * 8 * 2 * (size_t)(nv >= 2 ? 2 : 1);
-  if (vm) b += 2 * 4 * ((nslot + 3) & ~(size_t)3);  // valid-row counts of value columns 0 and 1
+  if (vm) b += 4 * ((nslot + 3) & ~(size_t)3);  // valid-row counts of value column 1
   return (b + 15) & ~(size_t)15;
 }
 

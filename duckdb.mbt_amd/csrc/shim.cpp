@@ -15,7 +15,7 @@
 //    (reference int32 overflow at duckdb_native.c:2404).
 #include <hip/hip_runtime_api.h>
 
-#include <emmintrin.h>
+#include <immintrin.h>
 
 #include <cmath>
 #include <cstdio>
@@ -1070,12 +1070,43 @@ duckdb_state duckdb_mb_list_vector_set_size(duckdb_vector, idx_t) { return DuckD
 duckdb_state duckdb_mb_list_vector_reserve(duckdb_vector, idx_t) { return DuckDBError; }   // ref :2101
 
 // A vector's bytes into the pinned staging buffer, which only the DMA engine
-// reads afterwards: 16-byte non-temporal stores (no read-for-ownership of the
+// reads afterwards: non-temporal stores (no read-for-ownership of the
 // destination lines, nothing evicted from the caller's cache) when both ends
-// are 16-byte aligned, else memcpy.
+// are 16-byte aligned -- 64-byte AVX-512 stores where the host has them, else
+// 16-byte SSE2 ones -- else memcpy.  MBX_CHUNK_COPY = memcpy / sse / avx512
+// pins one form (experiments).
+__attribute__((target("avx512f"))) static void StreamNt64(void *dst, const void *src, size_t bytes) {
+  char *d = (char *)dst;
+  const char *p = (const char *)src;
+  size_t n = bytes / 64;
+  if (((uintptr_t)d & 63) == 0) {
+    for (; n >= 4; n -= 4, d += 256, p += 256) {
+      const __m512i a = _mm512_loadu_si512(p), b = _mm512_loadu_si512(p + 64), c = _mm512_loadu_si512(p + 128),
+                    e = _mm512_loadu_si512(p + 192);
+      _mm512_stream_si512((__m512i *)d, a), _mm512_stream_si512((__m512i *)(d + 64), b);
+      _mm512_stream_si512((__m512i *)(d + 128), c), _mm512_stream_si512((__m512i *)(d + 192), e);
+    }
+    for (; n; n--, d += 64, p += 64) _mm512_stream_si512((__m512i *)d, _mm512_loadu_si512(p));
+  }
+  const size_t rest = bytes - (size_t)(d - (char *)dst);
+  for (size_t i = 0; i + 16 <= rest; i += 16) _mm_stream_si128((__m128i *)(d + i), _mm_loadu_si128((const __m128i *)(p + i)));
+  if (rest & 15) memcpy(d + (rest & ~(size_t)15), p + (rest & ~(size_t)15), rest & 15);
+  _mm_sfence();
+}
+
 static void StreamToPinned(void *dst, const void *src, size_t bytes) {
-  if (((uintptr_t)dst | (uintptr_t)src) & 15) {
+  static const int mode = [] {
+    const char *m = Knob("MBX_CHUNK_COPY");
+    if (m && !strcmp(m, "memcpy")) return 0;
+    if (m && !strcmp(m, "sse")) return 1;
+    return __builtin_cpu_supports("avx512f") ? 2 : 1;
+  }();
+  if (mode == 0 || (((uintptr_t)dst | (uintptr_t)src) & 15)) {
     memcpy(dst, src, bytes);
+    return;
+  }
+  if (mode == 2) {
+    StreamNt64(dst, src, bytes);
     return;
   }
   __m128i *d = (__m128i *)dst;

@@ -169,3 +169,84 @@ def test_null_keys_sharded(mbx, oracle, combine):
         assert len(rows) == len(exp), i
         assert [r[0] for r in rows] == [_cell(e[0]) for e in exp], i
     c.close()
+
+
+# ---------------------------------------------------------------------------
+# F3: one integer key over a range too wide for the LDS tables (group_part.hip)
+# ---------------------------------------------------------------------------
+def _np_groups(k, cols, aggs):
+    """numpy GROUP BY k (no NULLs): sorted keys and, per (agg, column), the
+    exact per-key result as Python ints."""
+    import numpy as np
+    keys, inv = np.unique(k, return_inverse=True)
+    out = [keys.tolist(), np.bincount(inv).tolist()]
+    for a, x in aggs:
+        v = cols[x]
+        if a == "sum":
+            acc = [0] * len(keys)
+            order = np.argsort(inv, kind="stable")
+            bounds = np.concatenate([[0], np.cumsum(np.bincount(inv))])
+            vs = v[order].astype(object)
+            for g in range(len(keys)):
+                acc[g] = int(vs[bounds[g]:bounds[g + 1]].sum())
+            out.append(acc)
+        elif a == "min":
+            m = np.full(len(keys), np.iinfo(np.int64).max)
+            np.minimum.at(m, inv, v.astype(np.int64))
+            out.append(m.tolist())
+        elif a == "max":
+            m = np.full(len(keys), np.iinfo(np.int64).min)
+            np.maximum.at(m, inv, v.astype(np.int64))
+            out.append(m.tolist())
+    return out
+
+
+@pytest.mark.parametrize("n,groups,ktype,vtype", [
+    (3_000_017, 100_000, "BIGINT", "BIGINT"), (2_000_003, 5_000, "INTEGER", "INTEGER"),
+    (1_000_001, 250_000, "BIGINT", "INTEGER"), (100_000, 60_000, "INTEGER", "BIGINT")])
+def test_partitioned_group_by_wide_key_range(mbx, oracle, n, groups, ktype, vtype):
+    """COUNT(*), SUM, MIN, MAX, AVG of two value columns per key, keys spread
+    over a range wider than the LDS tables (negative minimum included), against
+    numpy; the profile names group_part, not the hash path."""
+    import numpy as np
+    c = _conn(mbx)
+    q(c, f"CREATE TABLE w AS SELECT CAST(mbx_synth(7, i, {groups}) * 3 - {groups} AS {ktype}) AS k, "
+         f"CAST(mbx_synth(9, i, 2000000) - 1000000 AS {vtype}) AS v, "
+         f"CAST(mbx_synth(11, i, 1000) AS {vtype}) AS u FROM range({n}) tbl(i)")
+    k = oracle.synth_i64(n, 7, 0, groups, 0) * 3 - groups
+    v = oracle.synth_i64(n, 9, 0, 2_000_000, -1_000_000)
+    u = oracle.synth_i64(n, 11, 0, 1000, 0)
+    rows = q(c, "SELECT k, COUNT(*), SUM(v), MIN(v), MAX(u), SUM(u) FROM w GROUP BY k").rows
+    assert "group_part" in _kernels(c), _kernels(c)
+    keys, cnt, sv, mnv, mxu, su = _np_groups(k, {"v": v, "u": u},
+                                             [("sum", "v"), ("min", "v"), ("max", "u"), ("sum", "u")])
+    assert rows == [[str(a), str(b), str(c_), str(d_), str(e_), str(f_)]
+                    for a, b, c_, d_, e_, f_ in zip(keys, cnt, sv, mnv, mxu, su)]
+    # COUNT(*) only, and AVG
+    assert q(c, "SELECT k, COUNT(*) FROM w GROUP BY k").rows == [[str(a), str(b)] for a, b in zip(keys, cnt)]
+    assert "group_part" in _kernels(c)
+    for row, s_, n_ in zip(q(c, "SELECT k, AVG(v) FROM w GROUP BY k").rows, sv, cnt):
+        assert abs(float(row[1]) - s_ / n_) <= 1e-9 * max(1.0, abs(s_ / n_)), row
+    # HAVING / ORDER BY / LIMIT over the emitted groups
+    top = q(c, "SELECT k, COUNT(*) AS c FROM w GROUP BY k ORDER BY c DESC, k LIMIT 5").rows
+    want = sorted(zip(keys, cnt), key=lambda t: (-t[1], t[0]))[:5]
+    assert top == [[str(a), str(b)] for a, b in want]
+    c.close()
+
+
+def test_partitioned_group_by_1e9_rows(mbx, oracle):
+    """The c3h shape at 1e9 rows: 1e5 distinct INT64 keys, SUM(v) and COUNT(*)
+    of every group against the oracle over all rows."""
+    import os
+    n, groups = 1_000_000_000, 100_000
+    c = _conn(mbx)
+    q(c, f"CREATE TABLE th AS SELECT mbx_synth(7, i, {groups}) AS k, "
+         f"mbx_synth(9, i, 1099511627776) - 549755813888 AS v FROM range({n}) tbl(i)")
+    rr = c.query_raw("SELECT k, SUM(v), COUNT(*) FROM th GROUP BY k")
+    rows, _ = rr.cells()
+    rr.close()
+    assert "group_part" in _kernels(c), _kernels(c)
+    oc, osum = oracle.synth_groupby(7, 9, 0, n, groups, 1 << 40, -(1 << 39), min(32, max(8, len(os.sched_getaffinity(0)))))
+    assert len(rows) == groups
+    assert all(r[0] == str(g) and r[1] == str(osum[g]) and r[2] == str(oc[g]) for g, r in enumerate(rows))
+    c.close()

@@ -20,6 +20,9 @@
 #   gdab      C3 table flush A/B (records vs global atomics), alone and in the C2 line
 #   overheadq per-query overhead of the C2 / C3 shapes at 1e6 rows (tools/query_overhead.py)
 #   profcost  the per-kernel event profile's cost on the C2 query (tools/profile_cost.py)
+#   chunk     the C harness's append_data_chunk ingest under each pinned-staging copy form (MBX_CHUNK_COPY)
+#   newcfg    bench.py --config c3n (C3 with NULLs) and c3h (hash GROUP BY, HASH_GROUPS distinct keys)
+#   gdvar     c3n / c3 under each group_direct_lds launch shape (GD_VARIANTS)
 # Results go to gpurun_out/ (merged back by gpurun); copy what is judged into profiles/.
 set -o pipefail
 mkdir -p gpurun_out
@@ -130,6 +133,28 @@ if has overheadq; then  # per-query overhead of the C2 and C3 shapes at 1e6 rows
 fi
 if has profcost; then  # what the per-kernel event profile costs the C2 query (tools/profile_cost.py)
   timeout -k 10 300 python tools/profile_cost.py > gpurun_out/profile_cost.json 2> gpurun_out/profile_cost.err || exit 37
+fi
+if has chunk; then  # the reference-ABI chunk ingest (C harness) under each copy form of the pinned staging
+  mkdir -p gpurun_out/chunk
+  gcc -O2 -std=c11 -Iinclude tests/c_harness/mb_harness.c -o gpurun_out/chunk/mbh -Lduckdb.mbt_amd -lduckdb_mb_amd -Wl,-rpath,$R/duckdb.mbt_amd || exit 38
+  for m in default memcpy sse avx512; do
+    if [ $m = default ]; then X=""; else X="MBX_EXPERIMENTS=1 MBX_CHUNK_COPY=$m"; fi
+    env $X timeout -k 10 200 gpurun_out/chunk/mbh c4chunk ${CHUNK_ROWS:-100000000} > gpurun_out/chunk/$m.json 2> gpurun_out/chunk/$m.err || exit 39
+  done
+fi
+if has newcfg; then  # the C3-with-NULLs and hash GROUP BY configs
+  timeout -k 10 300 python bench.py --config c3n --extra "" > gpurun_out/bench_c3n.json 2> gpurun_out/bench_c3n.err || exit 40
+  for g in ${HASH_GROUPS:-100000 1000000}; do
+    timeout -k 10 400 python bench.py --config c3h --groups $g --steps ${HASH_STEPS:-5} --warmup 1 --extra "" --cpu-seconds 4 > gpurun_out/bench_c3h_$g.json 2> gpurun_out/bench_c3h_$g.err || exit 41
+  done
+fi
+if has gdvar; then  # C3 / C3-with-NULLs under group_direct_lds launch shapes (MBX_GD_VARIANT), rocprof stats each
+  mkdir -p gpurun_out/gdvar
+  for v in ${GD_VARIANTS:-d2_g1 d3_g1 d2_g2 d3_g2}; do
+    for c in c3n c3; do
+      ( cd /tmp && export TMPDIR=/tmp MBX_EXPERIMENTS=1 MBX_GD_VARIANT=$v && timeout -k 10 200 python3 $R/bench.py --config $c --extra "" --no-cpu --steps 20 > $R/gpurun_out/gdvar/${c}_$v.json 2> $R/gpurun_out/gdvar/${c}_$v.err ) || exit 42
+    done
+  done
 fi
 if has link; then
   timeout -k 10 200 ./tools/link8_probe ${LINK_MB:-8} 200 > gpurun_out/link8_probe.log 2>&1 || exit 23
