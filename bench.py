@@ -511,10 +511,12 @@ def run_inlib(args, world, rank, vote=None):
         elapsed, out = time_steps(step, args.steps, 0, barrier,
                                   torch.cuda.synchronize if torch.cuda.is_available() else None)
         kern_timed = None
+        log(f"[bench] timed loop done: {elapsed / args.steps * 1e3:.3f} ms/step")
         if isinstance(out, tuple) and out[0] == "c3hrows":  # the cells of the same query, pulled once
             kern_timed = conn.profile_drain()
             out = make_step(conn, args.config, w["sql"], decode=True)()
             conn.profile_drain()
+            log(f"[bench] c3h: {len(out)} groups pulled for parity")
         out = decode_c3(out)
         sr_out = sel_outcomes(conn, sr0)
         cb1 = conn.rccl_stats()
@@ -531,6 +533,7 @@ def run_inlib(args, world, rank, vote=None):
         elapsed = float(t_all.item())
     threads = len(os.sched_getaffinity(0))
     shard_par = None
+    log("[bench] parity check against the oracle")
     if sstats and args.config in ("c2", "c2d", "c5", "c3"):
         parity, shard_par = sharded_parity(conn, args.config, out, n_total, plan["nshards"], threads)
     else:
@@ -610,6 +613,7 @@ def run_inlib(args, world, rank, vote=None):
             result["extra"]["rccl_selftest"] = mbx.rccl_selftest([0])
         except Exception as ex:  # noqa: BLE001
             result["extra"]["rccl_selftest"] = {"ok": False, "error": str(ex)}
+    log("[bench] parity done")
     if not args.no_cpu and plan["nshards"] == 1 and args.config in ("c2", "c2d", "c3", "c3n", "c3h", "c5", "sel"):
         result["cpu_baseline"] = cpu_baseline(args.cpu_seconds, {"c2d": "c2", "c3n": "c3"}.get(args.config, args.config),
                                               args.groups)
@@ -1513,9 +1517,14 @@ def cpu_baseline(seconds, config="c2", groups=100_000):
         mk = lambda th: (lambda: orc.filter_agg_i64(x, 25, 2**63 - 1, th))  # noqa: E731
         what = "COUNT/SUM/MIN/MAX with x > 24"
     counts = sorted({qthreads, aff})
+    if config == "c3h":
+        # per-thread tables of `groups` keys: one thread count (the quota), so
+        # the baseline stays bounded (256 threads x 1e6-key tables take GBs)
+        counts = [qthreads]
     window = seconds / (3 * len(counts))
     per = {}
     for th in counts:
+        log(f"[bench] cpu baseline: {th} threads, {what}")
         run = mk(th)
         run()  # first touch / thread start-up outside the timed windows
         rates = []

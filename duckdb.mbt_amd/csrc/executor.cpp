@@ -2115,6 +2115,8 @@ static bool CountMayStayOnDevice(const Engine &e, const BoundSelect &s) {
 // not fit (the hash path or the run-time compiled kernel takes it).
 static bool PartGroupAggregate(Engine &e, const DRel &src, const BoundSelect &s, DRel &out) {
   const int na = (int)s.aggs.size();
+  if (const char *k = Knob("MBX_PART_GROUP"))  // MBX_PART_GROUP=0: the hash path (A/B)
+    if (atoi(k) == 0) return false;
   if (s.groups.size() != 1 || s.where || src.range || src.n <= 0 || src.n >= ((int64_t)1 << 32)) return false;
   if (s.groups[0]->kind != BExpr::COL || !FastIntCol(src, s.groups[0]->col)) return false;
   const DCol &K = src.cols[s.groups[0]->col];

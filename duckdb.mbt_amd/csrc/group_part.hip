@@ -41,7 +41,6 @@ namespace mbx {
 namespace dev {
 
 namespace {
-constexpr int kPassThreads = 1024;  // one workgroup of 16 waves per CU in the hist / scatter passes
 constexpr int kReduceThreads = 1024;  // the reduce pass: one 16-wave workgroup per CU (its LDS table bounds it)
 
 __device__ __forceinline__ void state_add(AggState *st, unsigned long long cnt, long long sum, long long mn,
@@ -82,47 +81,113 @@ __global__ __launch_bounds__(1024) void pg_hist_kernel(const TK *__restrict__ ke
   for (int p = threadIdx.x; p < np; p += blockDim.x) hist[(size_t)p * gridDim.x + blockIdx.x] = h[p];
 }
 
-template <typename TK, typename TV, int NV>
-__global__ __launch_bounds__(1024) void pg_scatter_kernel(const TK *__restrict__ key, const TV *__restrict__ v0,
-                                                         const TV *__restrict__ v1, int64_t n, int64_t chunk,
-                                                         int64_t kmin, int shift, int np,
-                                                         const unsigned int *__restrict__ off /* [np][grid] */,
-                                                         uint32_t *__restrict__ ok, TV *__restrict__ ov0,
-                                                         TV *__restrict__ ov1) {
-  extern __shared__ unsigned int cur[];
-  for (int p = threadIdx.x; p < np; p += blockDim.x) cur[p] = off[(size_t)p * gridDim.x + blockIdx.x];
-  __syncthreads();
+// Rows of a workgroup's chunk in tiles of kTile: each tile is counting-sorted
+// by partition in LDS (a returning LDS add gives a row its rank in its
+// partition, a block scan the partitions' bases), staged there, and written
+// out in staged order, so consecutive lanes store consecutive slots of one
+// partition's run (coalesced) instead of one scattered 2- and 8-byte store per
+// row.  The key leaves as its index inside the partition (u16) -- or, with
+// PACK (one INT64 value column whose zone map leaves its top bits unused),
+// inside the value's low bits: one 8-byte record per row, (v << shift) | index.
+constexpr int kScatterThreads = 512;  // two workgroups per CU: one stages while the other stores
+constexpr int kTile = 4096;           // rows per tile (8 per thread)
+
+template <typename TK, typename TV, int NV, bool PACK>
+__global__ __launch_bounds__(kScatterThreads) void pg_scatter_kernel(
+    const TK *__restrict__ key, const TV *__restrict__ v0, const TV *__restrict__ v1, int64_t n, int64_t chunk,
+    int64_t kmin, int shift, int np, const unsigned int *__restrict__ off /* [np][grid] */, uint16_t *__restrict__ ok,
+    TV *__restrict__ ov0, TV *__restrict__ ov1) {
+  constexpr int RPT = kTile / kScatterThreads;  // rows per thread and tile
+  extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
+  TV *sv0 = (TV *)lds;                            // staged values
+  TV *sv1 = sv0 + (NV >= 2 ? kTile : 0);
+  uint16_t *sk = (uint16_t *)(sv0 + (size_t)kTile * (NV >= 2 ? 2 : NV));  // staged keys (index in partition)
+  uint16_t *sp = sk + kTile;                      // staged rows' partitions
+  unsigned int *cur = (unsigned int *)(sp + kTile);  // this workgroup's next global slot per partition
+  unsigned int *cnt = cur + np;                   // tile: rows per partition
+  unsigned int *base = cnt + np;                  // tile: exclusive scan of cnt
+  unsigned int *wsum = base + np;                 // scan: per-wave totals
+  const int t = threadIdx.x, lane = t & 63, w = t >> 6, nw = kScatterThreads / 64;
+  for (int p = t; p < np; p += kScatterThreads) cur[p] = off[(size_t)p * gridDim.x + blockIdx.x];
+  const uint32_t lmask = (1u << shift) - 1u;
   const int64_t b = (int64_t)blockIdx.x * chunk, e = min(n, b + chunk);
-  auto put = [&](int64_t k, TV a, TV c) {
-    const uint32_t rel = (uint32_t)(k - kmin);
-    const unsigned int pos = atomicAdd(&cur[rel >> shift], 1u);
-    ok[pos] = rel;
-    if (NV >= 1) ov0[pos] = a;
-    if (NV >= 2) ov1[pos] = c;
-  };
-  const int64_t B = blockDim.x;
-  int64_t i = b + threadIdx.x;
-  for (; i + 3 * B < e; i += 4 * B) {
-    int64_t k[4];
-    TV a[4], c[4];
+  for (int64_t tb = b; tb < e; tb += kTile) {
+    const int tn = (int)min((int64_t)kTile, e - tb);
+    for (int p = t; p < np; p += kScatterThreads) cnt[p] = 0;
+    __syncthreads();
+    uint32_t rel[RPT];
+    unsigned int rank[RPT];
+    TV a[RPT], c[RPT];
 #pragma unroll
-    for (int u = 0; u < 4; u++) {
-      k[u] = (int64_t)key[i + u * B];
-      if (NV >= 1) a[u] = v0[i + u * B];
-      if (NV >= 2) c[u] = v1[i + u * B];
+    for (int u = 0; u < RPT; u++) {
+      const int j = u * kScatterThreads + t;
+      if (j < tn) {
+        rel[u] = (uint32_t)((int64_t)key[tb + j] - kmin);
+        if (NV >= 1) a[u] = v0[tb + j];
+        if (NV >= 2) c[u] = v1[tb + j];
+      }
     }
 #pragma unroll
-    for (int u = 0; u < 4; u++) put(k[u], NV >= 1 ? a[u] : (TV)0, NV >= 2 ? c[u] : (TV)0);
+    for (int u = 0; u < RPT; u++)
+      if (u * kScatterThreads + t < tn) rank[u] = atomicAdd(&cnt[rel[u] >> shift], 1u);
+    __syncthreads();
+    // exclusive scan of cnt[0, np): each thread a run of consecutive entries,
+    // then the runs' totals across the block
+    const int per = (np + kScatterThreads - 1) / kScatterThreads, p0 = min(np, t * per), p1 = min(np, p0 + per);
+    unsigned int run = 0;
+    for (int p = p0; p < p1; p++) run += cnt[p];
+    unsigned int incl = run;
+#pragma unroll
+    for (int m = 1; m < 64; m <<= 1) {
+      const unsigned int y = __shfl_up(incl, m, 64);
+      if (lane >= m) incl += y;
+    }
+    if (lane == 63) wsum[w] = incl;
+    __syncthreads();
+    unsigned int before = incl - run;
+    for (int k = 0; k < w; k++) before += wsum[k];
+    for (int p = p0; p < p1; p++) {
+      base[p] = before;
+      before += cnt[p];
+    }
+    __syncthreads();
+#pragma unroll
+    for (int u = 0; u < RPT; u++) {
+      if (u * kScatterThreads + t >= tn) continue;
+      const int pp = (int)(rel[u] >> shift);
+      const unsigned int pos = base[pp] + rank[u];
+      sp[pos] = (uint16_t)pp;
+      if (PACK) {
+        sv0[pos] = (TV)(((uint64_t)a[u] << shift) | (uint64_t)(rel[u] & lmask));
+        continue;
+      }
+      sk[pos] = (uint16_t)(rel[u] & lmask);
+      if (NV >= 1) sv0[pos] = a[u];
+      if (NV >= 2) sv1[pos] = c[u];
+    }
+    __syncthreads();
+    for (int j = t; j < tn; j += kScatterThreads) {
+      const int pp = sp[j];
+      const unsigned int dst = cur[pp] + (unsigned int)j - base[pp];
+      if (!PACK) ok[dst] = sk[j];
+      if (NV >= 1) ov0[dst] = sv0[j];
+      if (NV >= 2) ov1[dst] = sv1[j];
+    }
+    __syncthreads();
+    for (int p = t; p < np; p += kScatterThreads) cur[p] += cnt[p];
   }
-  for (; i < e; i += B) put((int64_t)key[i], NV >= 1 ? v0[i] : (TV)0, NV >= 2 ? v1[i] : (TV)0);
+}
+
+size_t ScatterLds(int np, int nv, int vb) {
+  return (size_t)kTile * vb * (nv >= 2 ? 2 : nv) + (size_t)kTile * 4 + (size_t)np * 12 + 64;
 }
 
 // Piece q = rows [q * piece, min(n, (q + 1) * piece)) of the partitioned
 // arrays; start[p] = first row of partition p (start[np] = n).  LDS: the
 // partition's table of KP keys -- COUNT(*) u32, then per value column its int64
 // sum (and min / max).
-template <typename TV, int NV, bool MM>
-__global__ __launch_bounds__(1024) void pg_reduce_kernel(const uint32_t *__restrict__ rk, const TV *__restrict__ rv0,
+template <typename TV, int NV, bool MM, bool PACK>
+__global__ __launch_bounds__(1024) void pg_reduce_kernel(const uint16_t *__restrict__ rk, const TV *__restrict__ rv0,
                                                         const TV *__restrict__ rv1, int64_t n, int64_t piece,
                                                         const unsigned int *__restrict__ start, int np, int shift,
                                                         int64_t range, unsigned long long *__restrict__ cstar,
@@ -157,7 +222,7 @@ __global__ __launch_bounds__(1024) void pg_reduce_kernel(const uint32_t *__restr
     __syncthreads();
     const uint32_t base = (uint32_t)p << shift;
     auto add = [&](uint32_t k, TV x, TV y) {
-      const int j = (int)(k - base);
+      const int j = (int)k;  // the key's index inside partition p
       atomicAdd(&cnt[j], 1u);
       if (NV >= 1) atomicAdd((unsigned long long *)&sum0[j], (unsigned long long)(long long)x);
       if (NV >= 2) atomicAdd((unsigned long long *)&sum1[j], (unsigned long long)(long long)y);
@@ -169,10 +234,16 @@ __global__ __launch_bounds__(1024) void pg_reduce_kernel(const uint32_t *__restr
     const int64_t B = blockDim.x;
     int64_t i = s0 + threadIdx.x;
     for (; i + 3 * B < s1; i += 4 * B) {
-      uint32_t k[4];
+      uint32_t k[4];  // (u16 in memory)
       TV x[4], y[4];
 #pragma unroll
       for (int u = 0; u < 4; u++) {
+        if (PACK) {
+          const TV r = rv0[i + u * B];
+          k[u] = (uint32_t)r & (uint32_t)(KP - 1);
+          x[u] = (TV)((int64_t)r >> shift);
+          continue;
+        }
         k[u] = rk[i + u * B];
         if (NV >= 1) x[u] = rv0[i + u * B];
         if (NV >= 2) y[u] = rv1[i + u * B];
@@ -180,7 +251,14 @@ __global__ __launch_bounds__(1024) void pg_reduce_kernel(const uint32_t *__restr
 #pragma unroll
       for (int u = 0; u < 4; u++) add(k[u], NV >= 1 ? x[u] : (TV)0, NV >= 2 ? y[u] : (TV)0);
     }
-    for (; i < s1; i += B) add(rk[i], NV >= 1 ? rv0[i] : (TV)0, NV >= 2 ? rv1[i] : (TV)0);
+    for (; i < s1; i += B) {
+      if (PACK) {
+        const TV r = rv0[i];
+        add((uint32_t)r & (uint32_t)(KP - 1), (TV)((int64_t)r >> shift), (TV)0);
+      } else {
+        add(rk[i], NV >= 1 ? rv0[i] : (TV)0, NV >= 2 ? rv1[i] : (TV)0);
+      }
+    }
     __syncthreads();
     for (int j = threadIdx.x; j < KP; j += blockDim.x) {
       const unsigned int c = cnt[j];
@@ -217,22 +295,26 @@ bool PartGroup(const PartGroupDesc &d, hipStream_t s) {
     if (cap < 4096) return false;
     piece = std::min<int64_t>(piece, (int64_t)cap);
   }
-  const int grid = NumCUs();
+  const int grid = NumCUs() * (kScatterThreads == 512 ? 2 : 1);
   const int64_t chunk = (d.n + grid - 1) / grid;
   const int vb = d.vphys == P_I64 ? 8 : 4;
+  // one INT64 value column whose |v| leaves shift + 1 top bits unused: the
+  // partition index rides in the value's low bits (8-byte records)
+  const bool pack = d.nv == 1 && d.vphys == P_I64 && d.vmaxabs < ((uint64_t)1 << (62 - shift));
   unsigned int *hist = (unsigned int *)d.scratch_hist;  // [np][grid] counts
   unsigned int *off = hist + (size_t)np * grid;         // ... and their exclusive scan
   unsigned int *start = (unsigned int *)d.scratch_start;  // [np + 1]
-  uint32_t *rk = (uint32_t *)d.scratch_rows;
-  void *rv0 = (char *)d.scratch_rows + (((size_t)d.n * 4 + 255) & ~(size_t)255);
+  uint16_t *rk = (uint16_t *)d.scratch_rows;
+  void *rv0 = (char *)d.scratch_rows + (((size_t)d.n * 2 + 255) & ~(size_t)255);
   void *rv1 = (char *)rv0 + (((size_t)d.n * vb + 255) & ~(size_t)255);
   const size_t hl = (size_t)np * 4;
   if (d.kphys == P_I64)
-    hipLaunchKernelGGL(pg_hist_kernel<int64_t>, dim3(grid), dim3(kPassThreads), hl, s, (const int64_t *)d.key, d.n,
-                       chunk, d.kmin, shift, np, hist);
+    hipLaunchKernelGGL(pg_hist_kernel<int64_t>, dim3(grid), dim3(kScatterThreads), hl, s, (const int64_t *)d.key,
+                       d.n, chunk, d.kmin, shift, np, hist);
   else
-    hipLaunchKernelGGL(pg_hist_kernel<int32_t>, dim3(grid), dim3(kPassThreads), hl, s, (const int32_t *)d.key, d.n,
-                       chunk, d.kmin, shift, np, hist);
+    hipLaunchKernelGGL(pg_hist_kernel<int32_t>, dim3(grid), dim3(kScatterThreads), hl, s, (const int32_t *)d.key,
+                       d.n, chunk, d.kmin, shift, np, hist);
+  const size_t sl = ScatterLds(np, d.nv, vb);
   // partition p starts at the offset of its first workgroup's sub-run
   size_t tmp = 0;
   const int nh = np * grid;
@@ -241,15 +323,23 @@ bool PartGroup(const PartGroupDesc &d, hipStream_t s) {
   (void)hipcub::DeviceScan::ExclusiveSum(d.scratch_scan, tmp, hist, off, nh, s);
   (void)hipMemcpy2DAsync(start, 4, off, (size_t)grid * 4, 4, np, hipMemcpyDeviceToDevice, s);
   (void)hipMemsetD32Async((hipDeviceptr_t)(start + np), (int)(unsigned int)d.n, 1, s);
-#define PGS(TK, TV, NV)                                                                                             \
-  hipLaunchKernelGGL((pg_scatter_kernel<TK, TV, NV>), dim3(grid), dim3(kPassThreads), hl, s, (const TK *)d.key,   \
-                     (const TV *)d.v0, (const TV *)d.v1, d.n, chunk, d.kmin, shift, np, off, rk, (TV *)rv0,       \
-                     (TV *)rv1)
+#define PGS(TK, TV, NV, PK)                                                                                         \
+  {                                                                                                                 \
+    (void)hipFuncSetAttribute((const void *)pg_scatter_kernel<TK, TV, NV, PK>,                                      \
+                              hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);                              \
+    hipLaunchKernelGGL((pg_scatter_kernel<TK, TV, NV, PK>), dim3(grid), dim3(kScatterThreads), sl, s,              \
+                       (const TK *)d.key, (const TV *)d.v0, (const TV *)d.v1, d.n, chunk, d.kmin, shift, np, off,  \
+                       rk, (TV *)rv0, (TV *)rv1);                                                                   \
+  }
 #define PGSV(TK)                                                                                                    \
   if (d.vphys == P_I64) {                                                                                           \
-    if (d.nv == 0) PGS(TK, int64_t, 0); else if (d.nv == 1) PGS(TK, int64_t, 1); else PGS(TK, int64_t, 2);          \
+    if (d.nv == 0) PGS(TK, int64_t, 0, false)                                                                       \
+    else if (d.nv == 1) { if (pack) PGS(TK, int64_t, 1, true) else PGS(TK, int64_t, 1, false) }                     \
+    else PGS(TK, int64_t, 2, false)                                                                                 \
   } else {                                                                                                          \
-    if (d.nv == 0) PGS(TK, int32_t, 0); else if (d.nv == 1) PGS(TK, int32_t, 1); else PGS(TK, int32_t, 2);          \
+    if (d.nv == 0) PGS(TK, int32_t, 0, false)                                                                       \
+    else if (d.nv == 1) PGS(TK, int32_t, 1, false)                                                                  \
+    else PGS(TK, int32_t, 2, false)                                                                                 \
   }
   if (d.kphys == P_I64) { PGSV(int64_t) } else { PGSV(int32_t) }
 #undef PGSV
@@ -258,20 +348,28 @@ bool PartGroup(const PartGroupDesc &d, hipStream_t s) {
   const int npieces = (int)((d.n + piece - 1) / piece);
   const size_t rl = ((size_t)4 << shift) +
                     ((size_t)8 << shift) * (size_t)(d.nv == 0 ? 0 : d.nv + (d.mm ? 2 * d.nv : 0));
-#define PGR(TV, NV, MM)                                                                                             \
+#define PGR(TV, NV, MM, PK)                                                                                         \
   {                                                                                                                 \
-    (void)hipFuncSetAttribute((const void *)pg_reduce_kernel<TV, NV, MM>, hipFuncAttributeMaxDynamicSharedMemorySize, \
-                              160 * 1024);                                                                          \
-    hipLaunchKernelGGL((pg_reduce_kernel<TV, NV, MM>), dim3(npieces), dim3(kReduceThreads), rl, s, rk,           \
+    (void)hipFuncSetAttribute((const void *)pg_reduce_kernel<TV, NV, MM, PK>,                                       \
+                              hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);                              \
+    hipLaunchKernelGGL((pg_reduce_kernel<TV, NV, MM, PK>), dim3(npieces), dim3(kReduceThreads), rl, s, rk,       \
                        (const TV *)rv0,                                                                             \
                        (const TV *)rv1, d.n, piece, start, np, shift, d.range, d.cstar, d.st0,                      \
                        d.st0 + d.range);                                                                            \
   }
 #define PGRV(TV)                                                                                                    \
-  if (d.nv == 0) PGR(TV, 0, false)                                                                                  \
-  else if (d.nv == 1) { if (d.mm) PGR(TV, 1, true) else PGR(TV, 1, false) }                                          \
-  else { if (d.mm) PGR(TV, 2, true) else PGR(TV, 2, false) }
-  if (d.vphys == P_I64) { PGRV(int64_t) } else { PGRV(int32_t) }
+  if (d.nv == 0) PGR(TV, 0, false, false)                                                                           \
+  else if (d.nv == 1) { if (d.mm) PGR(TV, 1, true, false) else PGR(TV, 1, false, false) }                            \
+  else { if (d.mm) PGR(TV, 2, true, false) else PGR(TV, 2, false, false) }
+  if (d.vphys == P_I64) {
+    if (pack) {
+      if (d.mm) PGR(int64_t, 1, true, true) else PGR(int64_t, 1, false, true)
+    } else {
+      PGRV(int64_t)
+    }
+  } else {
+    PGRV(int32_t)
+  }
 #undef PGRV
 #undef PGR
   return hipGetLastError() == hipSuccess;
@@ -281,11 +379,11 @@ void PartGroupScratch(int64_t n, int64_t range, int nv, bool mm, int vphys, size
                       size_t *rows_bytes, size_t *scan_bytes) {
   const int shift = PartGroupShift(nv, mm);
   const int np = (int)std::max<int64_t>(1, (range + (1 << shift) - 1) >> shift);
-  const int grid = NumCUs();
+  const int grid = NumCUs() * (kScatterThreads == 512 ? 2 : 1);
   const int vb = vphys == P_I64 ? 8 : 4;
   *hist_bytes = (size_t)np * grid * 4 * 2;  // counts and their scan
   *start_bytes = (size_t)(np + 1) * 4;
-  *rows_bytes = (((size_t)n * 4 + 255) & ~(size_t)255) + (size_t)std::max(nv, 0) * (((size_t)n * vb + 255) & ~(size_t)255);
+  *rows_bytes = (((size_t)n * 2 + 255) & ~(size_t)255) + (size_t)std::max(nv, 0) * (((size_t)n * vb + 255) & ~(size_t)255);
   size_t tmp = 0;
   unsigned int *dummy = nullptr;
   (void)hipcub::DeviceScan::ExclusiveSum(nullptr, tmp, dummy, dummy, np * grid, (hipStream_t)0);

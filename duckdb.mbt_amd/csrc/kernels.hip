@@ -1757,14 +1757,29 @@ __global__ __launch_bounds__(256) void group_direct_lds_kernel(const TK *__restr
   // each value column's sum / min / max over its valid rows
   auto row = [&](int64_t k, int64_t a, int64_t b, bool kv, bool va, bool vb) {
     const int sl = (KN && !kv) ? null_key + rep : (int)(k - kmin) * R + rep;
-    if (VN) gd_add_u64((long long *)&cnt64[sl], 1ull + ((!V0N || va) ? (1ull << 32) : 0ull));
-    else gd_add_u32(&cnt[sl], 1u);
-    if (NV >= 1 && (!V0N || va)) {
+    if (VN) {
+      // branch-free: a NULL value adds 0 to its sum and the neutral element to
+      // its min / max, so every lane issues the same LDS ops (no exec-mask
+      // juggling per row)
+      const bool a_ok = !V0N || va, b_ok = !V1N || vb;
+      gd_add_u64((long long *)&cnt64[sl], 1ull + (a_ok ? (1ull << 32) : 0ull));
+      if (NV >= 1) {
+        gd_add_u64(&sum0[sl], a_ok ? (unsigned long long)a : 0ull);
+        if (MM) { gd_min_i64(&mn0[sl], a_ok ? (long long)a : INT64_MAX); gd_max_i64(&mx0[sl], a_ok ? (long long)a : INT64_MIN); }
+      }
+      if (NV >= 2) {
+        if (V1N) gd_add_u32(&vcnt1[sl], b_ok ? 1u : 0u);
+        gd_add_u64(&sum1[sl], b_ok ? (unsigned long long)b : 0ull);
+        if (MM) { gd_min_i64(&mn1[sl], b_ok ? (long long)b : INT64_MAX); gd_max_i64(&mx1[sl], b_ok ? (long long)b : INT64_MIN); }
+      }
+      return;
+    }
+    gd_add_u32(&cnt[sl], 1u);
+    if (NV >= 1) {
       gd_add_u64(&sum0[sl], (unsigned long long)a);
       if (MM) { gd_min_i64(&mn0[sl], (long long)a); gd_max_i64(&mx0[sl], (long long)a); }
     }
-    if (NV >= 2 && (!V1N || vb)) {
-      if (V1N) gd_add_u32(&vcnt1[sl], 1u);
+    if (NV >= 2) {
       gd_add_u64(&sum1[sl], (unsigned long long)b);
       if (MM) { gd_min_i64(&mn1[sl], (long long)b); gd_max_i64(&mx1[sl], (long long)b); }
     }
@@ -2020,7 +2035,11 @@ bool GroupByDirectStates(const void *kcol, int kphys, int64_t kmin, int nk, cons
   // under d2_g3 on two boxes) and d2_g3 for COUNT-only tables (0.56 ms vs 0.62
   // on the segmented kernel).
   {
-    int depth = 2, gpc = nv > 0 ? 1 : 3;
+    // NULL-able columns (vv): three 2-deep workgroups per CU -- the validity
+    // words' extra LDS reads and selects per step want more waves to hide
+    // them (C3 with NULLs 1.90 ms at d2_g3 vs 2.13 at d2_g2 and 2.32 at d2_g1,
+    // profiles/r06_gd_nulls/)
+    int depth = 2, gpc = nv > 0 ? ((gvp && (gvp->key || gvp->v0 || gvp->v1)) ? 3 : 1) : 3;
     for (int j = 0; j < pr.n; j++)  // predicate slices of their own: a deeper ring (c3_where: d3 3.00 vs d2 3.32 ms)
       if (pr.p[j].src == 1) depth = 3;
     bool use = true;

@@ -98,7 +98,8 @@ class Oracle:
         sums = ctypes.create_string_buffer(16 * nk)
         self.lib.orc_groupby_sum_i32_i64(k.ctypes.data, v.ctypes.data, len(k), kmin, nk, threads,
                                          counts.ctypes.data, sums)
-        return [int(c) for c in counts], [i128_from(sums.raw[16 * i:16 * i + 16]) for i in range(nk)]
+        raw = sums.raw  # (one copy: .raw builds a new bytes object per access)
+        return [int(c) for c in counts], [i128_from(raw[16 * i:16 * i + 16]) for i in range(nk)]
 
     def synth_groupby(self, seed_k, seed_v, start, n, nk, vm, vadd, threads=1):
         """C3 over the generator: per-key COUNT(*) and exact SUM(v) (no arrays)."""
@@ -106,7 +107,8 @@ class Oracle:
         counts = np.zeros(nk, dtype=np.uint64)
         sums = ctypes.create_string_buffer(16 * nk)
         self.lib.orc_synth_groupby(seed_k, seed_v, start, n, nk, vm, vadd, threads, counts.ctypes.data, sums)
-        return [int(c) for c in counts], [i128_from(sums.raw[16 * i:16 * i + 16]) for i in range(nk)]
+        raw = sums.raw  # (one copy: .raw builds a new bytes object per access)
+        return [int(c) for c in counts], [i128_from(raw[16 * i:16 * i + 16]) for i in range(nk)]
 
     def synth_groupby_nulls(self, seeds, mods, adds, start, n, threads=1):
         """The C3 GROUP BY with NULL keys and two NULL-able value columns over
@@ -125,13 +127,14 @@ class Oracle:
         self.lib.orc_synth_groupby_nulls(sd.ctypes.data, md.ctypes.data, ad.ctypes.data, start, n, threads,
                                          counts.ctypes.data, sums, mm.ctypes.data)
         out = []
+        raw = sums.raw
         for g in range(ng):
             if not counts[3 * g]:
                 continue
             row = [None if g == nk else g, int(counts[3 * g])]
             for c in range(2):
                 cv = int(counts[3 * g + 1 + c])
-                s = i128_from(sums.raw[16 * (2 * g + c):16 * (2 * g + c) + 16])
+                s = i128_from(raw[16 * (2 * g + c):16 * (2 * g + c) + 16])
                 row += [cv, s if cv else None, int(mm[4 * g + 2 * c]) if cv else None,
                         int(mm[4 * g + 2 * c + 1]) if cv else None]
             out.append(tuple(row))

@@ -250,3 +250,25 @@ def test_partitioned_group_by_1e9_rows(mbx, oracle):
     assert len(rows) == groups
     assert all(r[0] == str(g) and r[1] == str(osum[g]) and r[2] == str(oc[g]) for g, r in enumerate(rows))
     c.close()
+
+
+def test_partitioned_group_by_unpacked_int64_values(mbx, oracle):
+    """INT64 values whose zone map uses the top bits (|v| up to 2^49): the
+    partition index cannot ride in the value, so keys and values travel as
+    separate arrays; and values wide enough that no overflow-free piece size
+    exists take the other GROUP BY paths -- both exact against numpy."""
+    import numpy as np
+    n, groups = 700_001, 20_000
+    c = _conn(mbx)
+    for span, kern in ((1 << 50, "group_part"), (1 << 60, None)):
+        q(c, "DROP TABLE IF EXISTS wb")
+        q(c, f"CREATE TABLE wb AS SELECT mbx_synth(7, i, {groups}) AS k, "
+             f"mbx_synth(9, i, {span}) - {span // 2} AS v FROM range({n}) tbl(i)")
+        k = oracle.synth_i64(n, 7, 0, groups, 0)
+        v = oracle.synth_i64(n, 9, 0, span, -(span // 2))
+        rows = q(c, "SELECT k, SUM(v), COUNT(*), MIN(v) FROM wb GROUP BY k ORDER BY k").rows
+        if kern:
+            assert kern in _kernels(c), _kernels(c)
+        keys, cnt, sv, mnv = _np_groups(k, {"v": v}, [("sum", "v"), ("min", "v")])
+        assert rows == [[str(a), str(s_), str(b), str(m)] for a, b, s_, m in zip(keys, cnt, sv, mnv)], span
+    c.close()

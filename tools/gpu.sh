@@ -23,6 +23,8 @@
 #   chunk     the C harness's append_data_chunk ingest under each pinned-staging copy form (MBX_CHUNK_COPY)
 #   newcfg    bench.py --config c3n (C3 with NULLs) and c3h (hash GROUP BY, HASH_GROUPS distinct keys)
 #   gdvar     c3n / c3 under each group_direct_lds launch shape (GD_VARIANTS)
+#   profh     rocprofv3 kernel trace + stats of the c3h and c3n lines (PROFH_CONFIGS, PROFH_GROUPS)
+#   hashab    c3h partitioned (default) vs the hash path (MBX_PART_GROUP=0)
 # Results go to gpurun_out/ (merged back by gpurun); copy what is judged into profiles/.
 set -o pipefail
 mkdir -p gpurun_out
@@ -155,6 +157,18 @@ if has gdvar; then  # C3 / C3-with-NULLs under group_direct_lds launch shapes (M
       ( cd /tmp && export TMPDIR=/tmp MBX_EXPERIMENTS=1 MBX_GD_VARIANT=$v && timeout -k 10 200 python3 $R/bench.py --config $c --extra "" --no-cpu --steps 20 > $R/gpurun_out/gdvar/${c}_$v.json 2> $R/gpurun_out/gdvar/${c}_$v.err ) || exit 42
     done
   done
+fi
+if has profh; then  # rocprofv3 kernel trace + stats of the c3h (F3 partitioned GROUP BY) and c3n lines
+  mkdir -p gpurun_out/profh
+  for c in ${PROFH_CONFIGS:-c3h c3n}; do
+    ( cd /tmp && export TMPDIR=/tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $R/gpurun_out/profh/$c -o $c -- python3 $R/bench.py --config $c --groups ${PROFH_GROUPS:-100000} --extra "" --no-cpu --steps 10 > $R/gpurun_out/profh/$c.json 2> $R/gpurun_out/profh/$c.err ) || exit 43
+    python3 $R/tools/rocpd_stats.py $R/gpurun_out/profh/$c/${c}_results.db $R/gpurun_out/profh/${c}_kernel_stats.csv || true
+  done
+fi
+if has hashab; then  # the wide-key GROUP BY: partitioned (default) vs the hash path (MBX_PART_GROUP=0), 1e5 keys
+  mkdir -p gpurun_out/hashab
+  timeout -k 10 300 python bench.py --config c3h --groups 100000 --steps 10 --warmup 2 --extra "" --no-cpu > gpurun_out/hashab/part.json 2> gpurun_out/hashab/part.err || exit 44
+  MBX_EXPERIMENTS=1 MBX_PART_GROUP=0 timeout -k 10 300 python bench.py --config c3h --groups 100000 --steps 3 --warmup 1 --extra "" --no-cpu > gpurun_out/hashab/hash.json 2> gpurun_out/hashab/hash.err || exit 45
 fi
 if has link; then
   timeout -k 10 200 ./tools/link8_probe ${LINK_MB:-8} 200 > gpurun_out/link8_probe.log 2>&1 || exit 23
