@@ -183,13 +183,24 @@ def vote_form(args, world, rank):
                   "reason": reason}
 
 
+def dev_map(devs):
+    """Device ids as the library sees them.  MBX_BENCH_DEVICE_MOD=k (a
+    rehearsal of the N-GPU line on a box with k GPUs) maps device d to d mod k:
+    the shards then share devices, so the combine is the host merge and the
+    RCCL self-test reports the list it refuses -- every other part of the
+    N > 1 line (timed loop, per-shard parity, combine A/B, the 1 -> N curve)
+    runs as on a node with N GPUs."""
+    k = int(os.environ.get("MBX_BENCH_DEVICE_MOD", "0") or 0)
+    return [d % k for d in devs] if k > 0 else list(devs)
+
+
 def inlib_plan(args, world):
     """The in-library layout: the devices (one process, `gpu_devices` through
     Config::set, ref duckdb_native.c:714-747), each listed --shards-per-gpu
     times; rows per GPU fixed (weak scaling)."""
     ngpu = world if world > 1 else args.gpus
     spg = max(1, args.shards_per_gpu)
-    devices = [d for d in range(ngpu) for _ in range(spg)]
+    devices = dev_map([d for d in range(ngpu) for _ in range(spg)])
     nshards = len(devices)
     par = (f"in-library row-range shards: gpu_devices={','.join(map(str, devices))} "
            f"({ngpu} GPU x {spg} shard(s), one engine + stream + persistent host worker per shard), "
@@ -219,6 +230,7 @@ def workload(config, start, n, groups=100_000):
                       f"END AS v FROM range({start}, {start + n}) tbl(i)")
         w["sql"] = "SELECT k, SUM(v), COUNT(*) FROM t3n GROUP BY k"
         w["kernel"] = "group_direct"
+        w["pmc_keys"] = ["group_direct_nulls"]
         w["bytes_per_row"] = 12.25  # 4 B key + 8 B value + the two columns' validity bits
         w["workload"] = ("C3 with NULLs: SELECT k, SUM(v), COUNT(*) FROM t GROUP BY k over 1e9 rows (INT32 key, 32 "
                          "groups + the NULL group; 1/7 of keys and 1/7 of values NULL)")
@@ -231,7 +243,8 @@ def workload(config, start, n, groups=100_000):
         w["setup"] = (f"CREATE TABLE th AS SELECT mbx_synth(7, i, {groups}) AS k, "
                       f"mbx_synth(9, i, 1099511627776) - 549755813888 AS v FROM range({start}, {start + n}) tbl(i)")
         w["sql"] = "SELECT k, SUM(v), COUNT(*) FROM th GROUP BY k"
-        w["kernel"] = "*"  # every kernel of the statement: the hash GROUP BY is a pipeline
+        w["kernel"] = "*"  # every kernel of the statement: the partitioned GROUP BY is a pipeline
+        w["pmc_keys"] = ["pg_hist", "pg_scatter", "pg_reduce"]
         w["bytes_per_row"] = 16
         w["workload"] = (f"hash GROUP BY: SELECT k, SUM(v), COUNT(*) FROM t GROUP BY k over 1e9 rows "
                          f"({groups} distinct INT64 keys, INT64 value)")
@@ -416,6 +429,18 @@ def pmc_traffic(kernel, n):
     return pmc_traffic_entry(kernel, n)[0]
 
 
+def pmc_traffic_keys(keys, n):
+    """The traffic of a statement whose work is several kernels (c3h's three
+    passes): the sum of their stored per-launch bytes, or None if any is
+    missing or stale; the provenance of each."""
+    tot, srcs = 0.0, []
+    for k in keys:
+        b, src = pmc_traffic_entry(k, n)
+        srcs.append(src)
+        tot = None if (tot is None or b is None) else tot + b
+    return tot, (srcs[0] if len(srcs) == 1 else {"entries": srcs})
+
+
 def time_steps(step, steps, warmup, barrier=None, sync=None):
     """W untimed warmup steps, then EXACTLY K steps bracketed by the barrier and
     a device synchronisation on both sides; returns (elapsed s, last output)."""
@@ -481,7 +506,7 @@ def run_inlib(args, world, rank, vote=None):
         # the RCCL calls of the combine over every GPU of the run, before any
         # table exists: a fresh ncclCommInitAll over devices 0..N-1 and the
         # multi-rank reduce / all-gather check, with what RCCL reports per rank
-        selftest = guarded(lambda: mbx.rccl_selftest(list(range(plan["ngpu"]))), RCCL_LEG_TIMEOUT_S)
+        selftest = guarded(lambda: mbx.rccl_selftest(dev_map(range(plan["ngpu"]))), RCCL_LEG_TIMEOUT_S)
         log(f"[bench] rccl self-test over devices 0..{plan['ngpu'] - 1}: {json.dumps(selftest)}")
     cfg = mbx.Config.create()
     if plan["nshards"] > 1:
@@ -762,7 +787,7 @@ def curve_points(ngpu, spg):
     p = 1, 2, 4, ... < N, each device listed spg times."""
     pts, p = [], 1
     while p < ngpu:
-        pts.append((p, [d for d in range(p) for _ in range(spg)]))
+        pts.append((p, dev_map([d for d in range(p) for _ in range(spg)])))
         p *= 2
     return pts
 
@@ -995,8 +1020,8 @@ def headline(args, w, ngpu, elapsed, avg_kernel_ms, n_rows_step, launch_rows, pa
             "peak": HBM_PEAK_GBS,
             "unit": "GB/s",
             "frac": (achieved / HBM_PEAK_GBS) if achieved else None,
-            "traffic": pmc_traffic(w["kernel"], launch_rows),
-            "traffic_source": pmc_traffic_entry(w["kernel"], launch_rows)[1],
+            "traffic": pmc_traffic_keys(w.get("pmc_keys", [w["kernel"]]), launch_rows)[0],
+            "traffic_source": pmc_traffic_keys(w.get("pmc_keys", [w["kernel"]]), launch_rows)[1],
             "algorithmic_bytes_per_launch": alg_bytes,
             "kernel_ms_avg": avg_kernel_ms,
             "timing": "hipEventRecord pairs on the engine stream around every launch in the timed loop",
@@ -1251,7 +1276,7 @@ def dry_run(args, world, rank, form=None, vote=None):
             md = None
             if ngpu > 1:
                 # what the real N > 1 line adds under multi_device (filled by a GPU run)
-                md = {"rccl_selftest": {"devices": list(range(ngpu)), "before": "the connection and the timed loop"},
+                md = {"rccl_selftest": {"devices": dev_map(range(ngpu)), "before": "the connection and the timed loop"},
                       "combine": {"timed_loop": sorted(combine_delta(ZERO_RCCL_STATS, ZERO_RCCL_STATS)),
                                   "rccl": ["state", "prepared_at_connect", "init_s", "check_us", "first_wait_ms",
                                            "ranks[].count", "ranks[].user_rank", "ranks[].cu_device",

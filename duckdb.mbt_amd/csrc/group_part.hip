@@ -66,6 +66,8 @@ __global__ __launch_bounds__(1024) void pg_hist_kernel(const TK *__restrict__ ke
   extern __shared__ unsigned int h[];
   for (int p = threadIdx.x; p < np; p += blockDim.x) h[p] = 0;
   __syncthreads();
+  // (one row per lane per load: 16-byte row pairs measured slower here and in
+  // the scatter -- 1.32 vs 1.23 ms and 6.77 vs 6.15 ms at 1e6 keys)
   const int64_t b = (int64_t)blockIdx.x * chunk, e = min(n, b + chunk);
   const int64_t B = blockDim.x;
   int64_t i = b + threadIdx.x;
@@ -127,9 +129,10 @@ __global__ __launch_bounds__(kScatterThreads) void pg_scatter_kernel(
         if (NV >= 2) c[u] = v1[tb + j];
       }
     }
+    auto row_of = [&](int u) { return u * kScatterThreads + t; };
 #pragma unroll
     for (int u = 0; u < RPT; u++)
-      if (u * kScatterThreads + t < tn) rank[u] = atomicAdd(&cnt[rel[u] >> shift], 1u);
+      if (row_of(u) < tn) rank[u] = atomicAdd(&cnt[rel[u] >> shift], 1u);
     __syncthreads();
     // exclusive scan of cnt[0, np): each thread a run of consecutive entries,
     // then the runs' totals across the block
@@ -153,7 +156,7 @@ __global__ __launch_bounds__(kScatterThreads) void pg_scatter_kernel(
     __syncthreads();
 #pragma unroll
     for (int u = 0; u < RPT; u++) {
-      if (u * kScatterThreads + t >= tn) continue;
+      if (row_of(u) >= tn) continue;
       const int pp = (int)(rel[u] >> shift);
       const unsigned int pos = base[pp] + rank[u];
       sp[pos] = (uint16_t)pp;
@@ -231,6 +234,29 @@ __global__ __launch_bounds__(1024) void pg_reduce_kernel(const uint16_t *__restr
         if (NV >= 2) atomicMin(&mn1[j], (long long)y), atomicMax(&mx1[j], (long long)y);
       }
     };
+    if (PACK) {
+      // 8-byte records two per lane (16-byte loads) from the first even row
+      auto one = [&](TV r) { add((uint32_t)r & (uint32_t)(KP - 1), (TV)((int64_t)r >> shift), (TV)0); };
+      const int64_t ev = (s0 + 1) & ~(int64_t)1;
+      if (threadIdx.x == 0 && ev > s0) one(rv0[s0]);
+      const int64_t B2 = 2 * (int64_t)blockDim.x;
+      int64_t i = ev + 2 * threadIdx.x;
+      typedef TV PV __attribute__((ext_vector_type(2)));
+      for (; i + 3 * B2 + 1 < s1; i += 4 * B2) {
+        PV x[4];
+#pragma unroll
+        for (int u = 0; u < 4; u++) x[u] = *(const PV *)(rv0 + i + u * B2);
+#pragma unroll
+        for (int u = 0; u < 4; u++) one(x[u].x), one(x[u].y);
+      }
+      for (; i < s1; i += B2) {
+        one(rv0[i]);
+        if (i + 1 < s1) one(rv0[i + 1]);
+      }
+      __syncthreads();
+      goto flush;
+    }
+    {
     const int64_t B = blockDim.x;
     int64_t i = s0 + threadIdx.x;
     for (; i + 3 * B < s1; i += 4 * B) {
@@ -251,15 +277,10 @@ __global__ __launch_bounds__(1024) void pg_reduce_kernel(const uint16_t *__restr
 #pragma unroll
       for (int u = 0; u < 4; u++) add(k[u], NV >= 1 ? x[u] : (TV)0, NV >= 2 ? y[u] : (TV)0);
     }
-    for (; i < s1; i += B) {
-      if (PACK) {
-        const TV r = rv0[i];
-        add((uint32_t)r & (uint32_t)(KP - 1), (TV)((int64_t)r >> shift), (TV)0);
-      } else {
-        add(rk[i], NV >= 1 ? rv0[i] : (TV)0, NV >= 2 ? rv1[i] : (TV)0);
-      }
-    }
+    for (; i < s1; i += B) add(rk[i], NV >= 1 ? rv0[i] : (TV)0, NV >= 2 ? rv1[i] : (TV)0);
     __syncthreads();
+    }
+  flush:
     for (int j = threadIdx.x; j < KP; j += blockDim.x) {
       const unsigned int c = cnt[j];
       const int64_t key = (int64_t)base + j;
@@ -296,7 +317,7 @@ bool PartGroup(const PartGroupDesc &d, hipStream_t s) {
     piece = std::min<int64_t>(piece, (int64_t)cap);
   }
   const int grid = NumCUs() * (kScatterThreads == 512 ? 2 : 1);
-  const int64_t chunk = (d.n + grid - 1) / grid;
+  const int64_t chunk = (((d.n + grid - 1) / grid) + 255) & ~(int64_t)255;  // 2-row aligned pairs in every chunk
   const int vb = d.vphys == P_I64 ? 8 : 4;
   // one INT64 value column whose |v| leaves shift + 1 top bits unused: the
   // partition index rides in the value's low bits (8-byte records)

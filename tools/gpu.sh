@@ -25,6 +25,8 @@
 #   gdvar     c3n / c3 under each group_direct_lds launch shape (GD_VARIANTS)
 #   profh     rocprofv3 kernel trace + stats of the c3h and c3n lines (PROFH_CONFIGS, PROFH_GROUPS)
 #   hashab    c3h partitioned (default) vs the hash path (MBX_PART_GROUP=0)
+#   pmcnew    FETCH_SIZE / WRITE_SIZE passes of the c3n and c3h lines
+#   inlibn    the in-library --gpus 8 (c2) / 4 (c5, c3) line on one GPU (MBX_BENCH_DEVICE_MOD=1)
 # Results go to gpurun_out/ (merged back by gpurun); copy what is judged into profiles/.
 set -o pipefail
 mkdir -p gpurun_out
@@ -169,6 +171,21 @@ if has hashab; then  # the wide-key GROUP BY: partitioned (default) vs the hash 
   mkdir -p gpurun_out/hashab
   timeout -k 10 300 python bench.py --config c3h --groups 100000 --steps 10 --warmup 2 --extra "" --no-cpu > gpurun_out/hashab/part.json 2> gpurun_out/hashab/part.err || exit 44
   MBX_EXPERIMENTS=1 MBX_PART_GROUP=0 timeout -k 10 300 python bench.py --config c3h --groups 100000 --steps 3 --warmup 1 --extra "" --no-cpu > gpurun_out/hashab/hash.json 2> gpurun_out/hashab/hash.err || exit 45
+fi
+if has pmcnew; then  # FETCH_SIZE / WRITE_SIZE passes of the c3n and c3h (1e5 keys) lines
+  mkdir -p gpurun_out/pmcnew
+  for c in c3n c3h; do
+    for ctr in FETCH_SIZE WRITE_SIZE; do
+      ( cd /tmp && export TMPDIR=/tmp && timeout -s KILL 300 rocprofv3 --pmc $ctr --output-format csv -d $R/gpurun_out/pmcnew/${c}_$ctr -o $ctr -- python3 $R/bench.py --config $c --extra "" --steps 5 --warmup 1 --no-cpu > $R/gpurun_out/pmcnew/${c}_$ctr.log 2>&1 ) || exit 46
+    done
+  done
+fi
+if has inlibn; then  # the in-library N-GPU line rehearsed on one GPU (MBX_BENCH_DEVICE_MOD=1: all shards on device 0)
+  mkdir -p gpurun_out/inlibn
+  MBX_BENCH_DEVICE_MOD=1 timeout -k 10 400 python bench.py --gpus 8 --no-cpu --steps 10 > gpurun_out/inlibn/c2_n8.json 2> gpurun_out/inlibn/c2_n8.err || exit 47
+  for c in c5 c3; do
+    MBX_BENCH_DEVICE_MOD=1 timeout -k 10 400 python bench.py --gpus 4 --config $c --no-cpu --steps 10 > gpurun_out/inlibn/${c}_n4.json 2> gpurun_out/inlibn/${c}_n4.err || exit 48
+  done
 fi
 if has link; then
   timeout -k 10 200 ./tools/link8_probe ${LINK_MB:-8} 200 > gpurun_out/link8_probe.log 2>&1 || exit 23
