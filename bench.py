@@ -86,7 +86,8 @@ def main():
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--rows", type=int, default=None,
                     help="rows per GPU (default 1e9; 1.25e9 for c5 = 1e10 over 8 GPUs)")
-    ap.add_argument("--config", default="c2", choices=["c1", "c2", "c2d", "c3", "c3n", "c3h", "c4", "c5", "sel"])
+    ap.add_argument("--config", default="c2",
+                    choices=["c1", "c2", "c2d", "c3", "c3n", "c3h", "c3s", "c4", "c5", "sel"])
     ap.add_argument("--groups", type=int, default=100_000,
                     help="c3h: distinct INT64 keys of the hash GROUP BY (1e5 and 1e6 are the measured points)")
     ap.add_argument("--extra", default="auto",
@@ -217,6 +218,7 @@ def inlib_plan(args, world):
 C3N_SEEDS = [7, 19, 9, 23, 31, 29]
 C3N_MODS = [32, 7, 1 << 40, 7, 1 << 40, 0]
 C3N_ADDS = [-(1 << 39), -(1 << 39)]
+C3S_MULT = 2654435761
 
 
 def workload(config, start, n, groups=100_000):
@@ -237,6 +239,20 @@ def workload(config, start, n, groups=100_000):
         w["data"] = ("synthetic: k = splitmix64(7 + i) mod 32 (INT32, NULL where splitmix64(19 + i) mod 7 = 0), "
                      "v = splitmix64(9 + i) mod 2^40 - 2^39 (INT64, NULL where splitmix64(23 + i) mod 7 = 0), "
                      "generated on device (no dataset)")
+        return w
+    if config == "c3s":
+        # the same GROUP BY over sparse keys (g x 2654435761): hashed partitions (F3h)
+        w["table"] = "ts"
+        w["setup"] = (f"CREATE TABLE ts AS SELECT mbx_synth(7, i, {groups}) * {C3S_MULT} AS k, "
+                      f"mbx_synth(9, i, 1099511627776) - 549755813888 AS v FROM range({start}, {start + n}) tbl(i)")
+        w["sql"] = "SELECT k, SUM(v), COUNT(*) FROM ts GROUP BY k"
+        w["kernel"] = "*"
+        w["pmc_keys"] = ["pg_hist_hashed", "pg_hscatter", "pg_hreduce"]
+        w["bytes_per_row"] = 16
+        w["workload"] = (f"sparse-key GROUP BY: SELECT k, SUM(v), COUNT(*) FROM t GROUP BY k over 1e9 rows "
+                         f"({groups} distinct INT64 keys spread over 2.6e14, INT64 value)")
+        w["data"] = (f"synthetic: k = (splitmix64(7 + i) mod {groups}) x {C3S_MULT} (INT64), "
+                     f"v = splitmix64(9 + i) mod 2^40 - 2^39 (INT64), generated on device (no dataset)")
         return w
     if config == "c3h":
         w["table"] = "th"
@@ -304,7 +320,7 @@ def make_step(conn, config, sql, decode=True):
             a.close()
             return [rows]
         rr = conn.query_raw(sql)
-        if config == "c3h" and not decode:
+        if config in ("c3h", "c3s") and not decode:
             # 1e5+ groups: the step ends at the materialised result (the
             # library's D2H and cell text); the cells are pulled once after
             # the timed loop for parity (a Python list of 3e5 strings per
@@ -312,7 +328,7 @@ def make_step(conn, config, sql, decode=True):
             rows = rr.row_count()
             rr.close()
             return ("c3hrows", rows)
-        if config in ("c3", "c3n", "c3h"):
+        if config in ("c3", "c3n", "c3h", "c3s"):
             rows, nulls = rr.cells()
             cells = ("c3cells", rows, nulls)
             if decode:
@@ -349,9 +365,10 @@ def parity_check(conn, config, sql, out, start, n, threads, groups=100_000):
         return {"groups": len(got), "oracle_groups": len(exp), "match": got == exp,
                 "checked": "every group's COUNT(*) and exact int128 SUM over the valid values, the NULL key's "
                            "group included, over all rows (oracle.c orc_synth_groupby_nulls)"}, exp
-    if config == "c3h":
+    if config in ("c3h", "c3s"):
+        mult = C3S_MULT if config == "c3s" else 1
         oc, osum = orc.synth_groupby(7, 9, start, n, groups, 1 << 40, -(1 << 39), min(threads, 32))
-        exp = [(k, oc[k], osum[k]) for k in range(groups) if oc[k]]
+        exp = [(k * mult, oc[k], osum[k]) for k in range(groups) if oc[k]]
         got = sorted(out, key=lambda g: (g[0] is None, g[0]))
         return {"groups": len(got), "oracle_groups": len(exp), "match": got == exp,
                 "checked": f"every one of the {len(exp)} groups' COUNT and exact int128 SUM over all rows"}, exp
@@ -572,7 +589,7 @@ def run_inlib(args, world, rank, vote=None):
                       sel_rows=int(out[0]) if args.config == "sel" else None)
     if vote:
         result["config"]["form"] = vote
-    if args.config in ("c3h", "c3n"):
+    if args.config in ("c3h", "c3n", "c3s"):
         # the statement's kernels, ms per step (HIP events per profiled scope)
         result["kernel_split_ms_per_step"] = split
     stuck = False
@@ -639,8 +656,9 @@ def run_inlib(args, world, rank, vote=None):
         except Exception as ex:  # noqa: BLE001
             result["extra"]["rccl_selftest"] = {"ok": False, "error": str(ex)}
     log("[bench] parity done")
-    if not args.no_cpu and plan["nshards"] == 1 and args.config in ("c2", "c2d", "c3", "c3n", "c3h", "c5", "sel"):
-        result["cpu_baseline"] = cpu_baseline(args.cpu_seconds, {"c2d": "c2", "c3n": "c3"}.get(args.config, args.config),
+    if not args.no_cpu and plan["nshards"] == 1 and args.config in ("c2", "c2d", "c3", "c3n", "c3h", "c3s", "c5", "sel"):
+        result["cpu_baseline"] = cpu_baseline(args.cpu_seconds,
+                                              {"c2d": "c2", "c3n": "c3", "c3s": "c3h"}.get(args.config, args.config),
                                               args.groups)
     if dist:
         dist.barrier()

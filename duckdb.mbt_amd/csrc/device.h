@@ -166,6 +166,16 @@ struct PartGroupDesc {
 void PartGroupScratch(int64_t n, int64_t range, int nv, bool mm, int vphys, size_t *hist_bytes, size_t *start_bytes,
                       size_t *rows_bytes, size_t *scan_bytes);
 bool PartGroup(const PartGroupDesc &d, hipStream_t s);
+// F3h: the same with a hashed partition function, for integer keys too sparse
+// for dense states (<= 1 value column): groups land in a global hash table of
+// PartGroupHashedSlots() slots -- gkeys[slot] = key ^ 2^63 (0: empty, except
+// the last slot, INT64_MIN's group), cstar / st0 per slot.  *overflow (device)
+// becomes non-zero when a table filled up: the result is then incomplete and
+// the caller must answer the query another way.
+bool PartGroupHashed(const PartGroupDesc &d, unsigned long long *gkeys, int *overflow, hipStream_t s);
+int64_t PartGroupHashedSlots();
+void PartGroupHashedScratch(int64_t n, int nv, size_t *hist_bytes, size_t *start_bytes, size_t *rows_bytes,
+                            size_t *scan_bytes);
 
 // --- generic aggregation over compacted columns ---------------------------
 // vclass: VC_I64 / VC_I128 / VC_F64 of the input column (phys given)
@@ -256,6 +266,9 @@ struct EmitDesc {
   int32_t key_phys;
   int64_t kmin;
   int64_t null_slot;  // -1 if none
+  // has_key with key_msb: the key of slot sl is key_msb[sl] ^ 2^63 (the hashed
+  // wide GROUP BY's table) instead of kmin + sl
+  const unsigned long long *key_msb;
   void *key_out;
   uint32_t *key_valid;
   // composite keys (instead of has_key): key q of slot sl is kmin + digit,

@@ -1662,9 +1662,12 @@ static DRel HashAggregate(Engine &e, const DRel &tmp, const BoundSelect &s, cons
     hk.k[g] = dev::HashKeyCol{c.data, c.validity, c.offsets, c.chars, (int32_t)c.phys};
   }
   const int64_t n = tmp.n;
+  // a table of >= 2n entries, at most 2^30 (its scan counts in int32: a 2^31-entry
+  // table silently lost every group above 5.4e8 rows); at most one entry per
+  // row is ever claimed, so n <= 2^30 rows always fit
   int64_t cap = 1024;
-  while (cap < 2 * n) cap <<= 1;
-  if (cap > ((int64_t)1 << 31)) ThrowError("Not implemented", "GROUP BY input above 2^30 rows on the hash path");
+  while (cap < 2 * n && cap < ((int64_t)1 << 30)) cap <<= 1;
+  if (n > ((int64_t)1 << 30)) ThrowError("Not implemented", "GROUP BY input above 2^30 rows on the hash path");
   auto table = Alloc(e, (size_t)cap * 8);
   HIPCHK(hipMemsetAsync(table->p, 0xFF, (size_t)cap * 8, e.stream));
   auto slot_of = Alloc(e, (size_t)std::max<int64_t>(n, 1) * 4);
@@ -2106,6 +2109,84 @@ static bool CountMayStayOnDevice(const Engine &e, const BoundSelect &s) {
   return true;
 }
 
+// F3h: the wide GROUP BY over hashed partitions (group_part.hip); groups come
+// out in hash-table order (DuckDB's hash aggregate order is unspecified too).
+// false: a table filled up (more groups than the tables hold) -- the caller's
+// hash path answers.
+static bool PartGroupHashedAggregate(Engine &e, const DRel &src, const BoundSelect &s, const DCol &K,
+                                     const std::vector<int> &vcols, bool mm, i128 maxabs, DRel &out) {
+  const int na = (int)s.aggs.size(), nv = (int)vcols.size();
+  const int64_t nslots = dev::PartGroupHashedSlots();
+  size_t hb = 0, sb = 0, rb = 0, cb = 0;
+  dev::PartGroupHashedScratch(src.n, nv, &hb, &sb, &rb, &cb);
+  auto cs = Alloc(e, nslots * 8);
+  auto stb = Alloc(e, (size_t)nslots * sizeof(dev::AggState));
+  auto gk = Alloc(e, nslots * 8);
+  auto hist = Alloc(e, hb), startb = Alloc(e, sb), rows = Alloc(e, rb), scan = Alloc(e, cb);
+  dev::PartGroupDesc d;
+  memset(&d, 0, sizeof(d));
+  d.key = K.data;
+  d.kphys = K.phys;
+  d.v0 = nv > 0 ? src.cols[vcols[0]].data : nullptr;
+  d.vphys = nv ? src.cols[vcols[0]].phys : P_I64;
+  d.nv = nv;
+  d.mm = mm;
+  d.n = src.n;
+  d.vmaxabs = nv ? (uint64_t)std::max<i128>(maxabs, 1) : 0;
+  d.cstar = (unsigned long long *)cs->p;
+  d.st0 = (dev::AggState *)stb->p;
+  d.scratch_hist = hist->p, d.scratch_start = startb->p, d.scratch_rows = rows->p, d.scratch_scan = scan->p;
+  d.scratch_scan_bytes = cb;
+  int32_t *ovf = (int32_t *)((char *)e.d_small + 3584);
+  double bytes = (double)src.n * PhysSize(K.phys) + (nv ? (double)src.n * PhysSize((Phys)d.vphys) : 0);
+  {
+    ProfScope ps(e, "group_part_hashed", bytes, src.n);
+    if (!dev::PartGroupHashed(d, (unsigned long long *)gk->p, ovf, e.stream)) {
+      if (Knob("MBX_PG_DEBUG")) fprintf(stderr, "[mbx] F3h: launch refused\n");
+      return false;
+    }
+  }
+  if (const int32_t o = ReadDev<int32_t>(e, ovf)) {  // more groups than the tables hold
+    if (Knob("MBX_PG_DEBUG")) fprintf(stderr, "[mbx] F3h: table overflow flag %d\n", o);
+    return false;
+  }
+  auto list = Alloc(e, nslots * 4);
+  const bool defer = CountMayStayOnDevice(e, s);
+  DevBufPtr nbuf = defer ? Alloc(e, 8) : nullptr;
+  int64_t *const n_out = defer ? (int64_t *)nbuf->p : e.d_scratch;
+  dev::CompactSlots((const unsigned long long *)cs->p, nslots, (int32_t *)list->p, n_out, e.stream);
+  dev::EmitDesc D;
+  memset(&D, 0, sizeof(D));
+  D.nagg = na;
+  D.cstar = (const unsigned long long *)cs->p;
+  D.slot_list = (const int32_t *)list->p;
+  D.n_list = n_out;
+  D.nslots = nslots;
+  D.has_key = 1;
+  D.key_phys = PhysOf(s.groups[0]->type);
+  D.key_msb = (const unsigned long long *)gk->p;
+  D.null_slot = -1;
+  DCol kc = AllocOut(e, s.groups[0]->type, nslots, true, false);
+  D.key_out = kc.data;
+  D.key_valid = (uint32_t *)kc.validity;
+  out.cols.clear();
+  out.cols.push_back(kc);
+  for (int j = 0; j < na; j++) {
+    DCol oc = AllocOut(e, s.aggs[j].type, nslots, true, false);
+    D.a[j] = EmitFor(s.aggs[j], VC_I64, s.aggs[j].kind == A_COUNT_STAR ? nullptr : d.st0, oc);
+    out.cols.push_back(oc);
+  }
+  dev::EmitAggRelation(D, e.stream);
+  if (defer) {
+    out.n = nslots;
+    out.n_dev = n_out;
+    out.n_owner = nbuf;
+  } else {
+    out.n = ReadDev<int64_t>(e, n_out);
+  }
+  return true;
+}
+
 // F3: GROUP BY one integer key (no NULLs) whose zone-map range is too wide for
 // F2's LDS tables but dense enough for per-key state arrays (1024 < range <=
 // PartGroupMaxRange, range <= 4 n), no WHERE, COUNT / SUM / MIN / MAX / AVG over
@@ -2137,7 +2218,7 @@ static bool PartGroupAggregate(Engine &e, const DRel &src, const BoundSelect &s,
   }
   const int nv = (int)vcols.size();
   if (nv > 2 || (nv == 2 && src.cols[vcols[0]].phys != src.cols[vcols[1]].phys)) return false;
-  if (range <= 1024 || range > dev::PartGroupMaxRange(nv, mm) || range > 4 * (i128)src.n) return false;
+  if (range <= 1024) return false;
   i128 maxabs = 0;
   for (int c : vcols) {
     const DevColumn *vs = src.cols[c].table_col;
@@ -2145,6 +2226,10 @@ static bool PartGroupAggregate(Engine &e, const DRel &src, const BoundSelect &s,
     maxabs = std::max(maxabs, std::max(vs->imax < 0 ? -vs->imax : vs->imax, vs->imin < 0 ? -vs->imin : vs->imin));
   }
   if (maxabs >= ((i128)1 << 62)) return false;
+  // keys too sparse for dense per-key states: hashed partitions (F3h), from
+  // 2^16 rows (below, the hash path's table is small) with at most one value column
+  if (range > dev::PartGroupMaxRange(nv, mm) || range > 4 * (i128)src.n)
+    return nv <= 1 && src.n >= ((int64_t)1 << 16) && PartGroupHashedAggregate(e, src, s, K, vcols, mm, maxabs, out);
   const int64_t nslots = (int64_t)range;
   const Phys vphys = nv ? src.cols[vcols[0]].phys : P_I64;
   size_t hb = 0, sb = 0, rb = 0, cb = 0;

@@ -35,7 +35,10 @@
 #include <stdexcept>
 
 #include "device.h"
+#include "knobs.h"
 #include "phys.h"
+
+#include <cstdio>
 
 namespace mbx {
 namespace dev {
@@ -59,7 +62,21 @@ __device__ __forceinline__ void state_add(AggState *st, unsigned long long cnt, 
 }  // namespace
 
 // rows [w * chunk, min(n, (w + 1) * chunk)) of workgroup w
-template <typename TK>
+// a row's partition: (key - kmin) >> shift, or with HASHED the top `shift`
+// bits of the key's hash (F3h)
+__device__ __forceinline__ uint64_t pg_mix(uint64_t x) {  // splitmix64's finaliser
+  x ^= x >> 30;
+  x *= 0xBF58476D1CE4E5B9ull;
+  x ^= x >> 27;
+  x *= 0x94D049BB133111EBull;
+  return x ^ (x >> 31);
+}
+template <bool HASHED>
+__device__ __forceinline__ int pg_part(int64_t k, int64_t kmin, int shift) {
+  return HASHED ? (int)(pg_mix((uint64_t)k) >> (64 - shift)) : (int)((uint64_t)(k - kmin) >> shift);
+}
+
+template <typename TK, bool HASHED = false>
 __global__ __launch_bounds__(1024) void pg_hist_kernel(const TK *__restrict__ key, int64_t n, int64_t chunk,
                                                       int64_t kmin, int shift, int np,
                                                       unsigned int *__restrict__ hist /* [np][grid] */) {
@@ -76,9 +93,9 @@ __global__ __launch_bounds__(1024) void pg_hist_kernel(const TK *__restrict__ ke
 #pragma unroll
     for (int u = 0; u < 4; u++) k[u] = (int64_t)key[i + u * B];
 #pragma unroll
-    for (int u = 0; u < 4; u++) atomicAdd(&h[(int)((uint64_t)(k[u] - kmin) >> shift)], 1u);
+    for (int u = 0; u < 4; u++) atomicAdd(&h[pg_part<HASHED>(k[u], kmin, shift)], 1u);
   }
-  for (; i < e; i += B) atomicAdd(&h[(int)((uint64_t)((int64_t)key[i] - kmin) >> shift)], 1u);
+  for (; i < e; i += B) atomicAdd(&h[pg_part<HASHED>((int64_t)key[i], kmin, shift)], 1u);
   __syncthreads();
   for (int p = threadIdx.x; p < np; p += blockDim.x) hist[(size_t)p * gridDim.x + blockIdx.x] = h[p];
 }
@@ -293,6 +310,275 @@ __global__ __launch_bounds__(1024) void pg_reduce_kernel(const uint16_t *__restr
   }
 }
 
+// ---- F3h: the same over a hashed partition function (sparse integer keys) ----
+// Records are the full key (stored as key ^ 2^63, so that 0 marks an empty
+// table slot and INT64_MIN has a slot of its own) and, with one value column,
+// the value: 16-byte records written by one store each.  The reduce pass keeps
+// an LDS hash table per partition piece (open addressing, kHashSlots slots)
+// and flushes its groups into a global table of kHashGlobal slots per
+// partition; a table that fills up sets *overflow and the caller answers the
+// query on the hash path instead.
+constexpr int kHashParts = 9;      // log2 partitions
+constexpr int kHashSlots = 4096;   // LDS table of a piece
+constexpr int kHashGlobal = 8192;  // global table per partition
+constexpr uint64_t kMsb = 0x8000000000000000ull;
+
+template <typename TK, typename TV, int NV>
+__global__ __launch_bounds__(kScatterThreads) void pg_hscatter_kernel(
+    const TK *__restrict__ key, const TV *__restrict__ v0, int64_t n, int64_t chunk, int pbits, int np,
+    const unsigned int *__restrict__ off, int64_t *__restrict__ rec /* [n][NV + 1] */) {
+  constexpr int RPT = kTile / kScatterThreads, RS = NV + 1;
+  extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
+  int64_t *srec = (int64_t *)lds;                                   // staged records
+  uint16_t *sp = (uint16_t *)(srec + (size_t)kTile * RS);           // staged rows' partitions
+  unsigned int *cur = (unsigned int *)(sp + kTile);
+  unsigned int *cnt = cur + np, *base = cnt + np, *wsum = base + np;
+  const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+  for (int p = t; p < np; p += kScatterThreads) cur[p] = off[(size_t)p * gridDim.x + blockIdx.x];
+  const int64_t b = (int64_t)blockIdx.x * chunk, e = min(n, b + chunk);
+  for (int64_t tb = b; tb < e; tb += kTile) {
+    const int tn = (int)min((int64_t)kTile, e - tb);
+    for (int p = t; p < np; p += kScatterThreads) cnt[p] = 0;
+    __syncthreads();
+    int64_t kk[RPT], vv[RPT];
+    int pp[RPT];
+    unsigned int rank[RPT];
+#pragma unroll
+    for (int u = 0; u < RPT; u++) {
+      const int j = u * kScatterThreads + t;
+      if (j < tn) {
+        kk[u] = (int64_t)key[tb + j];
+        if (NV >= 1) vv[u] = (int64_t)v0[tb + j];
+        pp[u] = pg_part<true>(kk[u], 0, pbits);
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < RPT; u++)
+      if (u * kScatterThreads + t < tn) rank[u] = atomicAdd(&cnt[pp[u]], 1u);
+    __syncthreads();
+    const int per = (np + kScatterThreads - 1) / kScatterThreads, p0 = min(np, t * per), p1 = min(np, p0 + per);
+    unsigned int run = 0;
+    for (int p = p0; p < p1; p++) run += cnt[p];
+    unsigned int incl = run;
+#pragma unroll
+    for (int m = 1; m < 64; m <<= 1) {
+      const unsigned int y = __shfl_up(incl, m, 64);
+      if (lane >= m) incl += y;
+    }
+    if (lane == 63) wsum[w] = incl;
+    __syncthreads();
+    unsigned int before = incl - run;
+    for (int k = 0; k < w; k++) before += wsum[k];
+    for (int p = p0; p < p1; p++) {
+      base[p] = before;
+      before += cnt[p];
+    }
+    __syncthreads();
+#pragma unroll
+    for (int u = 0; u < RPT; u++) {
+      if (u * kScatterThreads + t >= tn) continue;
+      const unsigned int pos = base[pp[u]] + rank[u];
+      sp[pos] = (uint16_t)pp[u];
+      srec[(size_t)pos * RS] = (int64_t)((uint64_t)kk[u] ^ kMsb);
+      if (NV >= 1) srec[(size_t)pos * RS + 1] = vv[u];
+    }
+    __syncthreads();
+    for (int j = t; j < tn; j += kScatterThreads) {
+      const int q = sp[j];
+      const size_t dst = (size_t)(cur[q] + (unsigned int)j - base[q]);
+      if (NV >= 1) {
+        typedef int64_t P __attribute__((ext_vector_type(2)));
+        *(P *)(rec + dst * 2) = *(const P *)(srec + (size_t)j * 2);
+      } else {
+        rec[dst] = srec[j];
+      }
+    }
+    __syncthreads();
+    for (int p = t; p < np; p += kScatterThreads) cur[p] += cnt[p];
+  }
+}
+
+template <int NV, bool MM>
+__global__ __launch_bounds__(1024) void pg_hreduce_kernel(const int64_t *__restrict__ rec, int64_t n, int64_t piece,
+                                                         const unsigned int *__restrict__ start, int np,
+                                                         unsigned long long *__restrict__ gkeys,
+                                                         unsigned long long *__restrict__ gcs,
+                                                         AggState *__restrict__ gst, int *__restrict__ overflow) {
+  constexpr int RS = NV + 1, C = kHashSlots;
+  extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
+  unsigned long long *tk = (unsigned long long *)lds;  // C + 1 slots: key ^ 2^63 (0: empty); slot C: INT64_MIN
+  long long *sum = (long long *)(tk + C + 1);
+  long long *mn = sum + C + 1, *mx = mn + C + 1;
+  unsigned int *cnt = (unsigned int *)(lds + (size_t)(C + 1) * 8 * (NV >= 1 ? (MM ? 4 : 2) : 1));
+  __shared__ int full;
+  const int64_t a = (int64_t)blockIdx.x * piece, z = min(n, a + piece);
+  if (a >= z) return;
+  int lo = 0, hi = np - 1;
+  while (lo < hi) {
+    const int mid = (lo + hi) >> 1;
+    if ((int64_t)start[mid + 1] <= a) lo = mid + 1;
+    else hi = mid;
+  }
+  if (threadIdx.x == 0) full = 0;
+  for (int p = lo; p < np && (int64_t)start[p] < z; p++) {
+    const int64_t s0 = max(a, (int64_t)start[p]), s1 = min(z, (int64_t)start[p + 1]);
+    if (s0 >= s1) continue;
+    for (int j = threadIdx.x; j <= C; j += blockDim.x) {
+      tk[j] = 0, cnt[j] = 0;
+      if (NV >= 1) sum[j] = 0;
+      if (MM) mn[j] = INT64_MAX, mx[j] = INT64_MIN;
+    }
+    __syncthreads();
+    for (int64_t i = s0 + threadIdx.x; i < s1; i += blockDim.x) {
+      typedef int64_t P __attribute__((ext_vector_type(2)));
+      P r;
+      if (NV >= 1) r = *(const P *)(rec + (size_t)i * 2);  // one 16-byte record
+      else r.x = rec[i];
+      const unsigned long long t = (unsigned long long)r.x;
+      int slot = C;
+      if (t) {  // (t == 0: the key INT64_MIN, slot C)
+        int h = (int)(pg_mix(t) & (C - 1)), probes = 0;
+        for (;;) {
+          const unsigned long long c = atomicCAS(&tk[h], 0ull, t);
+          if (c == 0 || c == t) break;
+          h = (h + 1) & (C - 1);
+          if (++probes == C) {
+            h = -1;
+            break;
+          }
+        }
+        if (h < 0) {
+          full = 1;
+          continue;
+        }
+        slot = h;
+      }
+      atomicAdd(&cnt[slot], 1u);
+      if (NV >= 1) {
+        const int64_t v = r.y;
+        atomicAdd((unsigned long long *)&sum[slot], (unsigned long long)v);
+        if (MM) atomicMin(&mn[slot], (long long)v), atomicMax(&mx[slot], (long long)v);
+      }
+    }
+    __syncthreads();
+    if (full) {
+      if (threadIdx.x == 0) atomicOr(overflow, 1);
+      return;  // (uniform: every thread read the same flag after the barrier)
+    }
+    // the piece's groups into partition p's global table (slot p << log2(G);
+    // INT64_MIN's group in the one slot after every partition's)
+    const size_t gb = (size_t)p * kHashGlobal;
+    for (int j = threadIdx.x; j <= C; j += blockDim.x) {
+      const unsigned int c = cnt[j];
+      if (!c) continue;
+      size_t g = (size_t)np * kHashGlobal;
+      if (j < C) {
+        const unsigned long long t = tk[j];
+        int h = (int)((pg_mix(t) >> 20) & (kHashGlobal - 1)), probes = 0;
+        for (;;) {
+          const unsigned long long o = atomicCAS(&gkeys[gb + h], 0ull, t);
+          if (o == 0 || o == t) break;
+          h = (h + 1) & (kHashGlobal - 1);
+          if (++probes == kHashGlobal) {
+            h = -1;
+            break;
+          }
+        }
+        if (h < 0) {
+          atomicOr(overflow, 1);
+          continue;
+        }
+        g = gb + h;
+      }
+      atomicAdd(&gcs[g], (unsigned long long)c);
+      if (NV >= 1) state_add(&gst[g], c, sum[j], MM ? mn[j] : 0, MM ? mx[j] : 0, MM);
+    }
+    __syncthreads();
+  }
+}
+
+bool PartGroupHashed(const PartGroupDesc &d, unsigned long long *gkeys, int *overflow, hipStream_t s) {
+  if (d.n <= 0 || d.n >= ((int64_t)1 << 32) || d.nv < 0 || d.nv > 1) return false;
+  if (d.kphys != P_I32 && d.kphys != P_I64) return false;
+  if (d.nv > 0 && d.vphys != P_I32 && d.vphys != P_I64) return false;
+  const int pbits = kHashParts, np = 1 << pbits;
+  int64_t piece = (int64_t)1 << 20;
+  if (d.nv > 0 && d.vmaxabs > 0) {
+    const uint64_t cap = ((uint64_t)1 << 62) / d.vmaxabs;
+    if (cap < 4096) return false;
+    piece = std::min<int64_t>(piece, (int64_t)cap);
+  }
+  const int grid = NumCUs() * (kScatterThreads == 512 ? 2 : 1);
+  const int64_t chunk = (((d.n + grid - 1) / grid) + 255) & ~(int64_t)255;
+  unsigned int *hist = (unsigned int *)d.scratch_hist, *off = hist + (size_t)np * grid;
+  unsigned int *start = (unsigned int *)d.scratch_start;
+  int64_t *rec = (int64_t *)d.scratch_rows;
+  const size_t hl = (size_t)np * 4;
+  if (d.kphys == P_I64)
+    hipLaunchKernelGGL((pg_hist_kernel<int64_t, true>), dim3(grid), dim3(kScatterThreads), hl, s,
+                       (const int64_t *)d.key, d.n, chunk, (int64_t)0, pbits, np, hist);
+  else
+    hipLaunchKernelGGL((pg_hist_kernel<int32_t, true>), dim3(grid), dim3(kScatterThreads), hl, s,
+                       (const int32_t *)d.key, d.n, chunk, (int64_t)0, pbits, np, hist);
+  size_t tmp = 0;
+  const int nh = np * grid;
+  (void)hipcub::DeviceScan::ExclusiveSum(nullptr, tmp, hist, off, nh, s);
+  if (tmp > d.scratch_scan_bytes) throw std::runtime_error("PartGroupHashed: scan scratch too small");
+  (void)hipcub::DeviceScan::ExclusiveSum(d.scratch_scan, tmp, hist, off, nh, s);
+  (void)hipMemcpy2DAsync(start, 4, off, (size_t)grid * 4, 4, np, hipMemcpyDeviceToDevice, s);
+  (void)hipMemsetD32Async((hipDeviceptr_t)(start + np), (int)(unsigned int)d.n, 1, s);
+  const size_t sl = (size_t)kTile * 8 * (d.nv + 1) + (size_t)kTile * 2 + (size_t)np * 12 + 64;
+#define PHS(TK, TV, NV)                                                                                             \
+  {                                                                                                                 \
+    (void)hipFuncSetAttribute((const void *)pg_hscatter_kernel<TK, TV, NV>,                                         \
+                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)sl);                                 \
+    hipLaunchKernelGGL((pg_hscatter_kernel<TK, TV, NV>), dim3(grid), dim3(kScatterThreads), sl, s,                 \
+                       (const TK *)d.key, (const TV *)d.v0, d.n, chunk, pbits, np, off, rec);                       \
+  }
+#define PHSV(TK)                                                                                                    \
+  if (d.nv == 0) PHS(TK, int64_t, 0)                                                                                \
+  else if (d.vphys == P_I64) PHS(TK, int64_t, 1)                                                                    \
+  else PHS(TK, int32_t, 1)
+  if (d.kphys == P_I64) { PHSV(int64_t) } else { PHSV(int32_t) }
+#undef PHSV
+#undef PHS
+  const int64_t total = (int64_t)np * kHashGlobal + 1;
+  (void)hipMemsetAsync(gkeys, 0, (size_t)total * 8, s);
+  (void)hipMemsetAsync(overflow, 0, 4, s);
+  InitAggStatesCounts(d.st0, total, d.cstar, total, s);
+  const int npieces = (int)((d.n + piece - 1) / piece);
+  const size_t rl = (size_t)(kHashSlots + 1) * (8 * (d.nv >= 1 ? (d.mm ? 4 : 2) : 1) + 4) + 16;
+#define PHR(NV, MM)                                                                                                 \
+  {                                                                                                                 \
+    (void)hipFuncSetAttribute((const void *)pg_hreduce_kernel<NV, MM>, hipFuncAttributeMaxDynamicSharedMemorySize,  \
+                              (int)rl);  /* (the kernel's own static LDS word counts against 160 KiB) */            \
+    hipLaunchKernelGGL((pg_hreduce_kernel<NV, MM>), dim3(npieces), dim3(kReduceThreads), rl, s, rec, d.n, piece,   \
+                       start, np, gkeys, d.cstar, d.st0, overflow);                                                 \
+  }
+  if (d.nv == 0) PHR(0, false)
+  else if (d.mm) PHR(1, true)
+  else PHR(1, false)
+#undef PHR
+  const hipError_t err = hipGetLastError();
+  if (err != hipSuccess && Knob("MBX_PG_DEBUG")) fprintf(stderr, "[mbx] F3h: %s\n", hipGetErrorString(err));
+  return err == hipSuccess;
+}
+
+int64_t PartGroupHashedSlots() { return ((int64_t)1 << kHashParts) * kHashGlobal + 1; }
+
+void PartGroupHashedScratch(int64_t n, int nv, size_t *hist_bytes, size_t *start_bytes, size_t *rows_bytes,
+                            size_t *scan_bytes) {
+  const int np = 1 << kHashParts;
+  const int grid = NumCUs() * (kScatterThreads == 512 ? 2 : 1);
+  *hist_bytes = (size_t)np * grid * 4 * 2;
+  *start_bytes = (size_t)(np + 1) * 4;
+  *rows_bytes = (size_t)n * 8 * (nv + 1) + 256;
+  size_t tmp = 0;
+  unsigned int *dummy = nullptr;
+  (void)hipcub::DeviceScan::ExclusiveSum(nullptr, tmp, dummy, dummy, np * grid, (hipStream_t)0);
+  *scan_bytes = tmp ? tmp : 16;
+}
+
 int PartGroupShift(int nv, bool mm) {
   // the largest partition table (power of two) that fits the LDS budget
   const int per_key = 4 + 8 * nv + (mm ? 16 * nv : 0);
@@ -347,7 +633,7 @@ bool PartGroup(const PartGroupDesc &d, hipStream_t s) {
 #define PGS(TK, TV, NV, PK)                                                                                         \
   {                                                                                                                 \
     (void)hipFuncSetAttribute((const void *)pg_scatter_kernel<TK, TV, NV, PK>,                                      \
-                              hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);                              \
+                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)sl);                                 \
     hipLaunchKernelGGL((pg_scatter_kernel<TK, TV, NV, PK>), dim3(grid), dim3(kScatterThreads), sl, s,              \
                        (const TK *)d.key, (const TV *)d.v0, (const TV *)d.v1, d.n, chunk, d.kmin, shift, np, off,  \
                        rk, (TV *)rv0, (TV *)rv1);                                                                   \
@@ -372,7 +658,7 @@ bool PartGroup(const PartGroupDesc &d, hipStream_t s) {
 #define PGR(TV, NV, MM, PK)                                                                                         \
   {                                                                                                                 \
     (void)hipFuncSetAttribute((const void *)pg_reduce_kernel<TV, NV, MM, PK>,                                       \
-                              hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);                              \
+                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)rl);                                 \
     hipLaunchKernelGGL((pg_reduce_kernel<TV, NV, MM, PK>), dim3(npieces), dim3(kReduceThreads), rl, s, rk,       \
                        (const TV *)rv0,                                                                             \
                        (const TV *)rv1, d.n, piece, start, np, shift, d.range, d.cstar, d.st0,                      \

@@ -2572,7 +2572,7 @@ __device__ __forceinline__ void emit_agg_body(const EmitDesc &D, Acc *part, int6
     if (D.has_key) {
       bool kv = in && sl != D.null_slot;
       if (in) {
-        int64_t k = D.kmin + sl;
+        int64_t k = D.key_msb ? (int64_t)(D.key_msb[sl] ^ 0x8000000000000000ull) : D.kmin + sl;
         if (kv) store_phys(D.key_out, D.key_phys, i, k, k >> 63);
         else store_phys(D.key_out, D.key_phys, i, 0, 0);
       }

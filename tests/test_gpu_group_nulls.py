@@ -272,3 +272,94 @@ def test_partitioned_group_by_unpacked_int64_values(mbx, oracle):
         keys, cnt, sv, mnv = _np_groups(k, {"v": v}, [("sum", "v"), ("min", "v")])
         assert rows == [[str(a), str(s_), str(b), str(m)] for a, b, s_, m in zip(keys, cnt, sv, mnv)], span
     c.close()
+
+
+# ---------------------------------------------------------------------------
+# F3h: integer keys too sparse for dense states, hashed partitions
+# ---------------------------------------------------------------------------
+@pytest.mark.parametrize("n,groups,mult,ktype", [
+    (3_000_017, 100_000, 1_000_003, "BIGINT"), (2_000_003, 60_000, 20_011, "INTEGER"),
+    (500_000, 400_000, -7_919_000_001, "BIGINT")])
+def test_hashed_group_by_sparse_keys(mbx, oracle, n, groups, mult, ktype):
+    """Keys spread over a range far wider than the rows (so no dense per-key
+    states): rows hash-partitioned, each partition reduced in an LDS hash
+    table, groups collected in a global hash table; against numpy, in any
+    order (DuckDB's hash aggregate order is unspecified)."""
+    c = _conn(mbx)
+    q(c, f"CREATE TABLE hs AS SELECT CAST(mbx_synth(7, i, {groups}) * ({mult}) AS {ktype}) AS k, "
+         f"mbx_synth(9, i, 2000000) - 1000000 AS v FROM range({n}) tbl(i)")
+    k = oracle.synth_i64(n, 7, 0, groups, 0) * mult
+    v = oracle.synth_i64(n, 9, 0, 2_000_000, -1_000_000)
+    rows = q(c, "SELECT k, COUNT(*), SUM(v), MIN(v), MAX(v) FROM hs GROUP BY k").rows
+    # F3h answered (no fallback to the hash path)
+    assert "group_part_hashed" in _kernels(c) and "hash_group_assign" not in _kernels(c), _kernels(c)
+    keys, cnt, sv, mnv, mxv = _np_groups(k, {"v": v}, [("sum", "v"), ("min", "v"), ("max", "v")])
+    want = sorted([str(a), str(b), str(c_), str(d_), str(e_)] for a, b, c_, d_, e_ in zip(keys, cnt, sv, mnv, mxv))
+    assert sorted(rows) == want
+    assert sorted(q(c, "SELECT k, COUNT(*) FROM hs GROUP BY k").rows) == sorted([str(a), str(b)] for a, b in zip(keys, cnt))
+    assert "group_part_hashed" in _kernels(c)
+    c.close()
+
+
+def test_hashed_group_by_edge_keys_and_overflow(mbx):
+    """INT64_MIN (the key the tables keep apart), INT64_MAX, 0 and -1 as keys;
+    and more groups than the hashed tables hold: the hash path answers, exact."""
+    import numpy as np
+    c = _conn(mbx)
+    n = 1 << 17
+    q(c, f"CREATE TABLE he AS SELECT CASE WHEN i % 5 = 0 THEN -9223372036854775807 - 1 "
+         f"WHEN i % 5 = 1 THEN 9223372036854775807 WHEN i % 5 = 2 THEN 0 WHEN i % 5 = 3 THEN -1 "
+         f"ELSE i * 1000003 END AS k, i AS v FROM range({n}) tbl(i)")
+    i = np.arange(n, dtype=np.int64)
+    k = np.where(i % 5 == 0, np.iinfo(np.int64).min, np.where(i % 5 == 1, np.iinfo(np.int64).max,
+                 np.where(i % 5 == 2, 0, np.where(i % 5 == 3, -1, i * 1_000_003))))
+    rows = q(c, "SELECT k, COUNT(*), SUM(v) FROM he GROUP BY k").rows
+    assert "group_part_hashed" in _kernels(c) and "hash_group_assign" not in _kernels(c), _kernels(c)
+    keys, cnt, sv = _np_groups(k, {"v": i}, [("sum", "v")])
+    assert sorted(rows) == sorted([str(a), str(b), str(s_)] for a, b, s_ in zip(keys, cnt, sv))
+    # 2.5M distinct sparse keys: beyond the hashed tables -> the hash path, still exact
+    n2 = 2_500_000
+    q(c, f"CREATE TABLE hb AS SELECT i * 1000003 AS k, i % 7 AS v FROM range({n2}) tbl(i)")
+    r = c.query_raw("SELECT COUNT(*), SUM(c) FROM (SELECT k, COUNT(*) AS c FROM hb GROUP BY k) t")
+    assert r.value(0, 0) == str(n2) and r.value(1, 0) == str(n2)
+    r.close()
+    assert "hash_group_assign" in _kernels(c), _kernels(c)  # the fallback answered
+    c.close()
+
+
+def test_hashed_group_by_1e9_rows(mbx, oracle):
+    """1e9 rows, 1e5 distinct sparse INT64 keys (k = g x 2654435761): every
+    group's COUNT and exact SUM against the oracle over all rows."""
+    import os
+    n, groups, mult = 1_000_000_000, 100_000, 2654435761
+    c = _conn(mbx)
+    q(c, f"CREATE TABLE th AS SELECT mbx_synth(7, i, {groups}) * {mult} AS k, "
+         f"mbx_synth(9, i, 1099511627776) - 549755813888 AS v FROM range({n}) tbl(i)")
+    rr = c.query_raw("SELECT k, SUM(v), COUNT(*) FROM th GROUP BY k")
+    rows, _ = rr.cells()
+    rr.close()
+    assert "group_part_hashed" in _kernels(c) and "hash_group_assign" not in _kernels(c), _kernels(c)
+    oc, osum = oracle.synth_groupby(7, 9, 0, n, groups, 1 << 40, -(1 << 39), min(32, max(8, len(os.sched_getaffinity(0)))))
+    got = sorted((int(r[0]), int(r[1]), int(r[2])) for r in rows)
+    assert got == [(g * mult, osum[g], oc[g]) for g in range(groups)]
+    c.close()
+
+
+def test_hash_path_above_5e8_rows(mbx, oracle, monkeypatch):
+    """The hash path itself at 6e8 rows (F3 / F3h off): its table is capped at
+    2^30 entries, so the int32 scan over it holds (a 2^31-entry table returned no
+    groups at all above 5.4e8 rows before round 6)."""
+    import os
+    n, groups = 600_000_000, 1000
+    c = _conn(mbx)
+    q(c, f"CREATE TABLE hp AS SELECT mbx_synth(7, i, {groups}) * 1000003 AS k, "
+         f"mbx_synth(9, i, 1099511627776) - 549755813888 AS v FROM range({n}) tbl(i)")
+    monkeypatch.setenv("MBX_PART_GROUP", "0")
+    rr = c.query_raw("SELECT k, SUM(v), COUNT(*) FROM hp GROUP BY k")
+    rows, _ = rr.cells()
+    rr.close()
+    monkeypatch.delenv("MBX_PART_GROUP")
+    assert "hash_group_assign" in _kernels(c), _kernels(c)
+    oc, osum = oracle.synth_groupby(7, 9, 0, n, groups, 1 << 40, -(1 << 39), min(32, max(8, len(os.sched_getaffinity(0)))))
+    assert sorted((int(r[0]), int(r[1]), int(r[2])) for r in rows) == [(g * 1000003, osum[g], oc[g]) for g in range(groups)]
+    c.close()

@@ -21,7 +21,7 @@
 #   overheadq per-query overhead of the C2 / C3 shapes at 1e6 rows (tools/query_overhead.py)
 #   profcost  the per-kernel event profile's cost on the C2 query (tools/profile_cost.py)
 #   chunk     the C harness's append_data_chunk ingest under each pinned-staging copy form (MBX_CHUNK_COPY)
-#   newcfg    bench.py --config c3n (C3 with NULLs) and c3h (hash GROUP BY, HASH_GROUPS distinct keys)
+#   newcfg    bench.py --config c3n (C3 with NULLs), c3h (wide dense keys) and c3s (sparse keys), HASH_GROUPS keys
 #   gdvar     c3n / c3 under each group_direct_lds launch shape (GD_VARIANTS)
 #   profh     rocprofv3 kernel trace + stats of the c3h and c3n lines (PROFH_CONFIGS, PROFH_GROUPS)
 #   hashab    c3h partitioned (default) vs the hash path (MBX_PART_GROUP=0)
@@ -149,7 +149,9 @@ fi
 if has newcfg; then  # the C3-with-NULLs and hash GROUP BY configs
   timeout -k 10 300 python bench.py --config c3n --extra "" > gpurun_out/bench_c3n.json 2> gpurun_out/bench_c3n.err || exit 40
   for g in ${HASH_GROUPS:-100000 1000000}; do
-    timeout -k 10 400 python bench.py --config c3h --groups $g --steps ${HASH_STEPS:-5} --warmup 1 --extra "" --cpu-seconds 4 > gpurun_out/bench_c3h_$g.json 2> gpurun_out/bench_c3h_$g.err || exit 41
+    for c in c3h c3s; do
+      timeout -k 10 400 python bench.py --config $c --groups $g --steps ${HASH_STEPS:-10} --warmup 2 --extra "" --cpu-seconds 4 > gpurun_out/bench_${c}_$g.json 2> gpurun_out/bench_${c}_$g.err || exit 41
+    done
   done
 fi
 if has gdvar; then  # C3 / C3-with-NULLs under group_direct_lds launch shapes (MBX_GD_VARIANT), rocprof stats each
