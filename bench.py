@@ -32,8 +32,13 @@ x > 24`): the passing rows compacted in row order into a device-resident
 result (the reference's query_arrow path, rows counted through
 duckdb_mb_arrow_row_count), checked row for row against the oracle.
 
+--config c3n is C3 with 1/7 NULL keys and values; c3h the same GROUP BY over
+--groups (1e5) dense INT64 keys (F3, partitioned in LDS); c3s over sparse keys
+(F3h, hashed partitions).
+
 Usage: python bench.py [--gpus N] [--shards-per-gpu S] [--ranks] [--steps K] [--warmup W]
-                       [--rows R] [--config c1|c2|c2d|c3|c4|c5|sel] [--extra c3,sel] [--no-cpu]
+                       [--rows R] [--config c1|c2|c2d|c3|c3n|c3h|c3s|c4|c5|sel] [--groups G]
+                       [--extra c3,sel,c3n,c3h,c3s] [--no-cpu]
 """
 import argparse
 import json
@@ -91,8 +96,8 @@ def main():
     ap.add_argument("--groups", type=int, default=100_000,
                     help="c3h: distinct INT64 keys of the hash GROUP BY (1e5 and 1e6 are the measured points)")
     ap.add_argument("--extra", default="auto",
-                    help="comma-separated sub-benchmarks (c3, sel) reported under the headline line's "
-                         "\"extra\" key; auto = c3,sel for the 1-GPU C2 line, none otherwise")
+                    help="comma-separated sub-benchmarks (c3, sel, c3n, c3h, c3s) reported under the headline "
+                         "line's \"extra\" key; auto = all five for the 1-GPU C2 line, none otherwise")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--dry-run", action="store_true",
@@ -635,7 +640,7 @@ def run_inlib(args, world, rank, vote=None):
             result["parity"]["fallback_error"] = f"select_rounds outcomes in the timed loop: {sr_out}"
     extras = args.extra
     if extras == "auto":
-        extras = "c3,sel" if (args.config == "c2" and plan["nshards"] == 1) else ""
+        extras = "c3,sel,c3n,c3h,c3s" if (args.config == "c2" and plan["nshards"] == 1) else ""
     if extras:
         result["extra"] = {}
         ceil = result["roofline"].get("measured_ceilings_gbs", {})
@@ -643,7 +648,7 @@ def run_inlib(args, world, rank, vote=None):
             r = result["extra"][ex] = sub_bench(conn, ex, plan, args)
             # against this box's ceiling of the same shape: C3's two-array ring read
             # (4 + 8 B per row, 2-deep 3 KiB slots); sel's half-writing ring copy
-            shape = {"c3": "ring_read2_gbs", "sel": "ring_copy_half_gbs"}.get(ex)
+            shape = {"c3": "ring_read2_gbs", "c3n": "ring_read2_gbs", "sel": "ring_copy_half_gbs"}.get(ex)
             if shape and isinstance(ceil.get(shape), float) and r.get("achieved_gbs"):
                 r["measured_ceiling_gbs"] = ceil[shape]
                 r["ceiling_shape"] = shape
@@ -1063,13 +1068,15 @@ def calibrate_into(conn, result, config):
 
 
 def sub_bench(conn, config, plan, args):
-    """A secondary config (C3 / sel) on the same connection and clock
-    discipline as the headline: its own table, warmup, timed steps, kernel
-    HIP events and full-size parity."""
+    """A secondary config (C3, C3 with NULLs, the wide / sparse-key GROUP BYs,
+    sel) on the same connection and clock discipline as the headline: its own
+    table (sel reads the headline's), warmup, timed steps, kernel HIP events and
+    full-size parity."""
     try:
         n_total = plan["rows_total"]
-        w = workload(config, 0, n_total)
-        if config == "c3":
+        w = workload(config, 0, n_total, args.groups)
+        own_table = config != "sel"
+        if own_table:
             res = conn.query(w["setup"])
             if not hasattr(res, "value"):
                 return {"error": str(res.error.message)}
@@ -1080,22 +1087,29 @@ def sub_bench(conn, config, plan, args):
         import torch
         before = conn.engine_stats()
         elapsed, out = time_steps(step, args.steps, 0, None, torch.cuda.synchronize)
+        kern = conn.profile_drain()
+        if isinstance(out, tuple) and out[0] == "c3hrows":  # the cells, pulled once after the timed loop
+            out = make_step(conn, config, w["sql"], decode=True)()
+            conn.profile_drain()
         out = decode_c3(out)
         outcomes = sel_outcomes(conn, before) if config == "sel" else None
-        avg_k, _, _ = kernel_stats(conn, w["kernel"], plan["nshards"], args.steps)
+        avg_k, _, _ = kernel_stats(kern, w["kernel"], plan["nshards"], args.steps)
         launch_rows = n_total // plan["nshards"]
         sel_rows = int(out[0]) if config == "sel" else None
         alg = launch_rows * w["bytes_per_row"] + (sel_rows * 8 if sel_rows is not None else 0)
         ach = alg / (avg_k * 1e-3) / 1e9 if avg_k else None
-        parity, _ = parity_check(conn, config, w["sql"], out, 0, n_total, len(os.sched_getaffinity(0)))
-        if config == "c3":
-            conn.query("DROP TABLE t3")
+        parity, _ = parity_check(conn, config, w["sql"], out, 0, n_total, len(os.sched_getaffinity(0)), args.groups)
+        if own_table:
+            conn.query(f"DROP TABLE {w['table']}")
+        keys = w.get("pmc_keys", [w["kernel"]])
         r = {"workload": w["workload"], "sql": w["sql"], "steps": args.steps, "warmup": args.warmup,
              "ms_per_step": elapsed / args.steps * 1e3, "value": n_total * args.steps / elapsed, "unit": "rows/s",
              "kernel": w["kernel"], "kernel_ms_avg": avg_k, "algorithmic_bytes_per_launch": alg,
              "achieved_gbs": ach, "frac": ach / HBM_PEAK_GBS if ach else None,
-             "traffic": pmc_traffic(w["kernel"], launch_rows),
-             "traffic_source": pmc_traffic_entry(w["kernel"], launch_rows)[1], "parity": parity}
+             "traffic": pmc_traffic_keys(keys, launch_rows)[0],
+             "traffic_source": pmc_traffic_keys(keys, launch_rows)[1], "parity": parity}
+        if config in ("c3h", "c3s", "c3n"):
+            r["kernel_split_ms_per_step"] = kernel_split(kern, args.steps)
         if outcomes is not None:
             # every timed step must have run the one-pass kernel: an abort (a persistent workgroup
             # never scheduled, the two-pass form reran) or a launch failure is a fallback

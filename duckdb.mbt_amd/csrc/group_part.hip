@@ -319,14 +319,19 @@ __global__ __launch_bounds__(1024) void pg_reduce_kernel(const uint16_t *__restr
 // partition; a table that fills up sets *overflow and the caller answers the
 // query on the hash path instead.
 constexpr int kHashParts = 9;      // log2 partitions
+// the hashed scatter: 8192-row tiles in one 16-wave workgroup per CU, so a
+// tile's run per partition averages 16 records (256 B) -- at 4096-row tiles
+// (8-record runs) it ran 11.2 ms for 1e9 rows
+constexpr int kHTile = 8192, kHThreads = 1024;
 constexpr int kHashSlots = 4096;   // LDS table of a piece
 constexpr int kHashGlobal = 8192;  // global table per partition
 constexpr uint64_t kMsb = 0x8000000000000000ull;
 
 template <typename TK, typename TV, int NV>
-__global__ __launch_bounds__(kScatterThreads) void pg_hscatter_kernel(
+__global__ __launch_bounds__(kHThreads) void pg_hscatter_kernel(
     const TK *__restrict__ key, const TV *__restrict__ v0, int64_t n, int64_t chunk, int pbits, int np,
     const unsigned int *__restrict__ off, int64_t *__restrict__ rec /* [n][NV + 1] */) {
+  constexpr int kTile = kHTile, kScatterThreads = kHThreads;
   constexpr int RPT = kTile / kScatterThreads, RS = NV + 1;
   extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
   int64_t *srec = (int64_t *)lds;                                   // staged records
@@ -508,17 +513,17 @@ bool PartGroupHashed(const PartGroupDesc &d, unsigned long long *gkeys, int *ove
     if (cap < 4096) return false;
     piece = std::min<int64_t>(piece, (int64_t)cap);
   }
-  const int grid = NumCUs() * (kScatterThreads == 512 ? 2 : 1);
+  const int grid = NumCUs();  // (one kHThreads workgroup per CU in the hist and scatter passes)
   const int64_t chunk = (((d.n + grid - 1) / grid) + 255) & ~(int64_t)255;
   unsigned int *hist = (unsigned int *)d.scratch_hist, *off = hist + (size_t)np * grid;
   unsigned int *start = (unsigned int *)d.scratch_start;
   int64_t *rec = (int64_t *)d.scratch_rows;
   const size_t hl = (size_t)np * 4;
   if (d.kphys == P_I64)
-    hipLaunchKernelGGL((pg_hist_kernel<int64_t, true>), dim3(grid), dim3(kScatterThreads), hl, s,
+    hipLaunchKernelGGL((pg_hist_kernel<int64_t, true>), dim3(grid), dim3(kHThreads), hl, s,
                        (const int64_t *)d.key, d.n, chunk, (int64_t)0, pbits, np, hist);
   else
-    hipLaunchKernelGGL((pg_hist_kernel<int32_t, true>), dim3(grid), dim3(kScatterThreads), hl, s,
+    hipLaunchKernelGGL((pg_hist_kernel<int32_t, true>), dim3(grid), dim3(kHThreads), hl, s,
                        (const int32_t *)d.key, d.n, chunk, (int64_t)0, pbits, np, hist);
   size_t tmp = 0;
   const int nh = np * grid;
@@ -527,12 +532,12 @@ bool PartGroupHashed(const PartGroupDesc &d, unsigned long long *gkeys, int *ove
   (void)hipcub::DeviceScan::ExclusiveSum(d.scratch_scan, tmp, hist, off, nh, s);
   (void)hipMemcpy2DAsync(start, 4, off, (size_t)grid * 4, 4, np, hipMemcpyDeviceToDevice, s);
   (void)hipMemsetD32Async((hipDeviceptr_t)(start + np), (int)(unsigned int)d.n, 1, s);
-  const size_t sl = (size_t)kTile * 8 * (d.nv + 1) + (size_t)kTile * 2 + (size_t)np * 12 + 64;
+  const size_t sl = (size_t)kHTile * 8 * (d.nv + 1) + (size_t)kHTile * 2 + (size_t)np * 12 + 64;
 #define PHS(TK, TV, NV)                                                                                             \
   {                                                                                                                 \
     (void)hipFuncSetAttribute((const void *)pg_hscatter_kernel<TK, TV, NV>,                                         \
                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)sl);                                 \
-    hipLaunchKernelGGL((pg_hscatter_kernel<TK, TV, NV>), dim3(grid), dim3(kScatterThreads), sl, s,                 \
+    hipLaunchKernelGGL((pg_hscatter_kernel<TK, TV, NV>), dim3(grid), dim3(kHThreads), sl, s,                       \
                        (const TK *)d.key, (const TV *)d.v0, d.n, chunk, pbits, np, off, rec);                       \
   }
 #define PHSV(TK)                                                                                                    \
@@ -569,7 +574,7 @@ int64_t PartGroupHashedSlots() { return ((int64_t)1 << kHashParts) * kHashGlobal
 void PartGroupHashedScratch(int64_t n, int nv, size_t *hist_bytes, size_t *start_bytes, size_t *rows_bytes,
                             size_t *scan_bytes) {
   const int np = 1 << kHashParts;
-  const int grid = NumCUs() * (kScatterThreads == 512 ? 2 : 1);
+  const int grid = NumCUs();
   *hist_bytes = (size_t)np * grid * 4 * 2;
   *start_bytes = (size_t)(np + 1) * 4;
   *rows_bytes = (size_t)n * 8 * (nv + 1) + 256;
