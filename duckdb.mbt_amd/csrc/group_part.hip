@@ -130,13 +130,11 @@ __global__ __launch_bounds__(kScatterThreads) void pg_scatter_kernel(
   for (int p = t; p < np; p += kScatterThreads) cur[p] = off[(size_t)p * gridDim.x + blockIdx.x];
   const uint32_t lmask = (1u << shift) - 1u;
   const int64_t b = (int64_t)blockIdx.x * chunk, e = min(n, b + chunk);
-  for (int64_t tb = b; tb < e; tb += kTile) {
+  // the next tile is loaded into registers while this one's rows are stored
+  uint32_t rel[RPT];
+  TV a[RPT], c[RPT];
+  auto load = [&](int64_t tb) {
     const int tn = (int)min((int64_t)kTile, e - tb);
-    for (int p = t; p < np; p += kScatterThreads) cnt[p] = 0;
-    __syncthreads();
-    uint32_t rel[RPT];
-    unsigned int rank[RPT];
-    TV a[RPT], c[RPT];
 #pragma unroll
     for (int u = 0; u < RPT; u++) {
       const int j = u * kScatterThreads + t;
@@ -146,6 +144,13 @@ __global__ __launch_bounds__(kScatterThreads) void pg_scatter_kernel(
         if (NV >= 2) c[u] = v1[tb + j];
       }
     }
+  };
+  if (b < e) load(b);
+  for (int64_t tb = b; tb < e; tb += kTile) {
+    const int tn = (int)min((int64_t)kTile, e - tb);
+    for (int p = t; p < np; p += kScatterThreads) cnt[p] = 0;
+    __syncthreads();
+    unsigned int rank[RPT];
     auto row_of = [&](int u) { return u * kScatterThreads + t; };
 #pragma unroll
     for (int u = 0; u < RPT; u++)
@@ -186,6 +191,7 @@ __global__ __launch_bounds__(kScatterThreads) void pg_scatter_kernel(
       if (NV >= 2) sv1[pos] = c[u];
     }
     __syncthreads();
+    if (tb + kTile < e) load(tb + kTile);
     for (int j = t; j < tn; j += kScatterThreads) {
       const int pp = sp[j];
       const unsigned int dst = cur[pp] + (unsigned int)j - base[pp];
@@ -202,11 +208,21 @@ size_t ScatterLds(int np, int nv, int vb) {
   return (size_t)kTile * vb * (nv >= 2 ? 2 : nv) + (size_t)kTile * 4 + (size_t)np * 12 + 64;
 }
 
+// PC (value columns with piece x max|v| < 2^41): a row adds 2^42 + v to one
+// 64-bit word, so COUNT and the sum share one LDS atomic (count = the word
+// rounded to a multiple of 2^42, sum = the rest)
+constexpr int kPcShift = 42;
+__device__ __forceinline__ void pc_split(unsigned long long w, unsigned int *c, long long *sum) {
+  const long long q = (long long)(w + (1ull << (kPcShift - 1))) >> kPcShift;
+  *c = (unsigned int)q;
+  *sum = (long long)(w - ((unsigned long long)q << kPcShift));
+}
+
 // Piece q = rows [q * piece, min(n, (q + 1) * piece)) of the partitioned
 // arrays; start[p] = first row of partition p (start[np] = n).  LDS: the
 // partition's table of KP keys -- COUNT(*) u32, then per value column its int64
 // sum (and min / max).
-template <typename TV, int NV, bool MM, bool PACK>
+template <typename TV, int NV, bool MM, bool PACK, bool PC>
 __global__ __launch_bounds__(1024) void pg_reduce_kernel(const uint16_t *__restrict__ rk, const TV *__restrict__ rv0,
                                                         const TV *__restrict__ rv1, int64_t n, int64_t piece,
                                                         const unsigned int *__restrict__ start, int np, int shift,
@@ -243,8 +259,12 @@ __global__ __launch_bounds__(1024) void pg_reduce_kernel(const uint16_t *__restr
     const uint32_t base = (uint32_t)p << shift;
     auto add = [&](uint32_t k, TV x, TV y) {
       const int j = (int)k;  // the key's index inside partition p
-      atomicAdd(&cnt[j], 1u);
-      if (NV >= 1) atomicAdd((unsigned long long *)&sum0[j], (unsigned long long)(long long)x);
+      if (PC) {
+        atomicAdd((unsigned long long *)&sum0[j], (1ull << kPcShift) + (unsigned long long)(long long)x);
+      } else {
+        atomicAdd(&cnt[j], 1u);
+        if (NV >= 1) atomicAdd((unsigned long long *)&sum0[j], (unsigned long long)(long long)x);
+      }
       if (NV >= 2) atomicAdd((unsigned long long *)&sum1[j], (unsigned long long)(long long)y);
       if (MM) {
         atomicMin(&mn0[j], (long long)x), atomicMax(&mx0[j], (long long)x);
@@ -299,11 +319,14 @@ __global__ __launch_bounds__(1024) void pg_reduce_kernel(const uint16_t *__restr
     }
   flush:
     for (int j = threadIdx.x; j < KP; j += blockDim.x) {
-      const unsigned int c = cnt[j];
+      unsigned int c;
+      long long s0j = 0;
+      if (PC) pc_split((unsigned long long)sum0[j], &c, &s0j);
+      else c = cnt[j], s0j = NV >= 1 ? sum0[j] : 0;
       const int64_t key = (int64_t)base + j;
       if (!c || key >= range) continue;
       atomicAdd(&cstar[key], (unsigned long long)c);
-      if (NV >= 1) state_add(&st0[key], c, sum0[j], MM ? mn0[j] : 0, MM ? mx0[j] : 0, MM);
+      if (NV >= 1) state_add(&st0[key], c, s0j, MM ? mn0[j] : 0, MM ? mx0[j] : 0, MM);
       if (NV >= 2) state_add(&st1[key], c, sum1[j], MM ? mn1[j] : 0, MM ? mx1[j] : 0, MM);
     }
     __syncthreads();
@@ -341,22 +364,30 @@ __global__ __launch_bounds__(kHThreads) void pg_hscatter_kernel(
   const int t = threadIdx.x, lane = t & 63, w = t >> 6;
   for (int p = t; p < np; p += kScatterThreads) cur[p] = off[(size_t)p * gridDim.x + blockIdx.x];
   const int64_t b = (int64_t)blockIdx.x * chunk, e = min(n, b + chunk);
-  for (int64_t tb = b; tb < e; tb += kTile) {
+  // the next tile's rows are loaded into registers while the current tile's
+  // staged records are stored, so the read and write streams overlap
+  int64_t kk[RPT], vv[RPT];
+  auto load = [&](int64_t tb) {
     const int tn = (int)min((int64_t)kTile, e - tb);
-    for (int p = t; p < np; p += kScatterThreads) cnt[p] = 0;
-    __syncthreads();
-    int64_t kk[RPT], vv[RPT];
-    int pp[RPT];
-    unsigned int rank[RPT];
 #pragma unroll
     for (int u = 0; u < RPT; u++) {
       const int j = u * kScatterThreads + t;
       if (j < tn) {
         kk[u] = (int64_t)key[tb + j];
         if (NV >= 1) vv[u] = (int64_t)v0[tb + j];
-        pp[u] = pg_part<true>(kk[u], 0, pbits);
       }
     }
+  };
+  if (b < e) load(b);
+  for (int64_t tb = b; tb < e; tb += kTile) {
+    const int tn = (int)min((int64_t)kTile, e - tb);
+    for (int p = t; p < np; p += kScatterThreads) cnt[p] = 0;
+    __syncthreads();
+    int pp[RPT];
+    unsigned int rank[RPT];
+#pragma unroll
+    for (int u = 0; u < RPT; u++)
+      if (u * kScatterThreads + t < tn) pp[u] = pg_part<true>(kk[u], 0, pbits);
 #pragma unroll
     for (int u = 0; u < RPT; u++)
       if (u * kScatterThreads + t < tn) rank[u] = atomicAdd(&cnt[pp[u]], 1u);
@@ -388,6 +419,7 @@ __global__ __launch_bounds__(kHThreads) void pg_hscatter_kernel(
       if (NV >= 1) srec[(size_t)pos * RS + 1] = vv[u];
     }
     __syncthreads();
+    if (tb + kTile < e) load(tb + kTile);
     for (int j = t; j < tn; j += kScatterThreads) {
       const int q = sp[j];
       const size_t dst = (size_t)(cur[q] + (unsigned int)j - base[q]);
@@ -403,7 +435,7 @@ __global__ __launch_bounds__(kHThreads) void pg_hscatter_kernel(
   }
 }
 
-template <int NV, bool MM>
+template <int NV, bool MM, bool PC>
 __global__ __launch_bounds__(1024) void pg_hreduce_kernel(const int64_t *__restrict__ rec, int64_t n, int64_t piece,
                                                          const unsigned int *__restrict__ start, int np,
                                                          unsigned long long *__restrict__ gkeys,
@@ -434,37 +466,70 @@ __global__ __launch_bounds__(1024) void pg_hreduce_kernel(const int64_t *__restr
       if (MM) mn[j] = INT64_MAX, mx[j] = INT64_MIN;
     }
     __syncthreads();
-    for (int64_t i = s0 + threadIdx.x; i < s1; i += blockDim.x) {
-      typedef int64_t P __attribute__((ext_vector_type(2)));
+    typedef int64_t P __attribute__((ext_vector_type(2)));
+    auto load = [&](int64_t i) {
       P r;
       if (NV >= 1) r = *(const P *)(rec + (size_t)i * 2);  // one 16-byte record
-      else r.x = rec[i];
-      const unsigned long long t = (unsigned long long)r.x;
-      int slot = C;
-      if (t) {  // (t == 0: the key INT64_MIN, slot C)
-        int h = (int)(pg_mix(t) & (C - 1)), probes = 0;
-        for (;;) {
-          const unsigned long long c = atomicCAS(&tk[h], 0ull, t);
-          if (c == 0 || c == t) break;
-          h = (h + 1) & (C - 1);
-          if (++probes == C) {
-            h = -1;
-            break;
-          }
-        }
-        if (h < 0) {
-          full = 1;
-          continue;
-        }
-        slot = h;
+      else r.x = rec[i], r.y = 0;
+      return r;
+    };
+    // a row's slot: its key's first probe is a compare-and-swap issued for
+    // every row of the batch at once (their returns overlap), then each row
+    // walks on only if that slot holds another key
+    auto probe = [&](unsigned long long t, int h, unsigned long long c) {
+      int probes = 1;
+      while (c != 0 && c != t) {
+        h = (h + 1) & (C - 1);
+        if (probes++ == C) return -1;
+        c = atomicCAS(&tk[h], 0ull, t);
       }
-      atomicAdd(&cnt[slot], 1u);
-      if (NV >= 1) {
-        const int64_t v = r.y;
-        atomicAdd((unsigned long long *)&sum[slot], (unsigned long long)v);
-        if (MM) atomicMin(&mn[slot], (long long)v), atomicMax(&mx[slot], (long long)v);
+      return h;
+    };
+    auto update = [&](int slot, int64_t v) {
+      if (PC) {
+        atomicAdd((unsigned long long *)&sum[slot], (1ull << kPcShift) + (unsigned long long)v);
+      } else {
+        atomicAdd(&cnt[slot], 1u);
+        if (NV >= 1) atomicAdd((unsigned long long *)&sum[slot], (unsigned long long)v);
+      }
+      if (NV >= 1 && MM) atomicMin(&mn[slot], (long long)v), atomicMax(&mx[slot], (long long)v);
+    };
+    auto first = [&](unsigned long long t) { return (int)(pg_mix(t) & (C - 1)); };
+    auto add = [&](P r) {
+      const unsigned long long t = (unsigned long long)r.x;
+      int slot = C;  // (t == 0: the key INT64_MIN, slot C)
+      if (t) {
+        const int h = first(t);
+        slot = probe(t, h, atomicCAS(&tk[h], 0ull, t));
+      }
+      if (slot < 0) full = 1;
+      else update(slot, r.y);
+    };
+    // four records in flight per lane, and their first probes too: the
+    // compare-and-swap waits on its return
+    const int64_t B = blockDim.x;
+    int64_t i = s0 + threadIdx.x;
+    for (; i + 3 * B < s1; i += 4 * B) {
+      P r[4];
+#pragma unroll
+      for (int u = 0; u < 4; u++) r[u] = load(i + u * B);
+      int h[4];
+      unsigned long long c[4];
+#pragma unroll
+      for (int u = 0; u < 4; u++) {
+        const unsigned long long t = (unsigned long long)r[u].x;
+        h[u] = t ? first(t) : C;
+        c[u] = t ? atomicCAS(&tk[h[u]], 0ull, t) : 0ull;
+      }
+#pragma unroll
+      for (int u = 0; u < 4; u++) {
+        const unsigned long long t = (unsigned long long)r[u].x;
+        const int slot = t ? probe(t, h[u], c[u]) : C;
+        if (slot < 0) full = 1;
+        else update(slot, r[u].y);
       }
     }
+    for (; i < s1; i += B) add(load(i));
     __syncthreads();
     if (full) {
       if (threadIdx.x == 0) atomicOr(overflow, 1);
@@ -474,7 +539,10 @@ __global__ __launch_bounds__(1024) void pg_hreduce_kernel(const int64_t *__restr
     // INT64_MIN's group in the one slot after every partition's)
     const size_t gb = (size_t)p * kHashGlobal;
     for (int j = threadIdx.x; j <= C; j += blockDim.x) {
-      const unsigned int c = cnt[j];
+      unsigned int c;
+      long long sj = 0;
+      if (PC) pc_split((unsigned long long)sum[j], &c, &sj);
+      else c = cnt[j], sj = NV >= 1 ? sum[j] : 0;
       if (!c) continue;
       size_t g = (size_t)np * kHashGlobal;
       if (j < C) {
@@ -496,7 +564,7 @@ __global__ __launch_bounds__(1024) void pg_hreduce_kernel(const int64_t *__restr
         g = gb + h;
       }
       atomicAdd(&gcs[g], (unsigned long long)c);
-      if (NV >= 1) state_add(&gst[g], c, sum[j], MM ? mn[j] : 0, MM ? mx[j] : 0, MM);
+      if (NV >= 1) state_add(&gst[g], c, sj, MM ? mn[j] : 0, MM ? mx[j] : 0, MM);
     }
     __syncthreads();
   }
@@ -553,16 +621,19 @@ bool PartGroupHashed(const PartGroupDesc &d, unsigned long long *gkeys, int *ove
   InitAggStatesCounts(d.st0, total, d.cstar, total, s);
   const int npieces = (int)((d.n + piece - 1) / piece);
   const size_t rl = (size_t)(kHashSlots + 1) * (8 * (d.nv >= 1 ? (d.mm ? 4 : 2) : 1) + 4) + 16;
-#define PHR(NV, MM)                                                                                                 \
+  const bool pc = d.nv == 1 && (unsigned __int128)d.vmaxabs * (uint64_t)piece < ((unsigned __int128)1 << (kPcShift - 1)) &&
+                  !Knob("MBX_PG_NO_PC");
+#define PHR(NV, MM, PC)                                                                                             \
   {                                                                                                                 \
-    (void)hipFuncSetAttribute((const void *)pg_hreduce_kernel<NV, MM>, hipFuncAttributeMaxDynamicSharedMemorySize,  \
+    (void)hipFuncSetAttribute((const void *)pg_hreduce_kernel<NV, MM, PC>,                                          \
+                              hipFuncAttributeMaxDynamicSharedMemorySize,                                           \
                               (int)rl);  /* (the kernel's own static LDS word counts against 160 KiB) */            \
-    hipLaunchKernelGGL((pg_hreduce_kernel<NV, MM>), dim3(npieces), dim3(kReduceThreads), rl, s, rec, d.n, piece,   \
-                       start, np, gkeys, d.cstar, d.st0, overflow);                                                 \
+    hipLaunchKernelGGL((pg_hreduce_kernel<NV, MM, PC>), dim3(npieces), dim3(kReduceThreads), rl, s, rec, d.n,      \
+                       piece, start, np, gkeys, d.cstar, d.st0, overflow);                                          \
   }
-  if (d.nv == 0) PHR(0, false)
-  else if (d.mm) PHR(1, true)
-  else PHR(1, false)
+  if (d.nv == 0) PHR(0, false, false)
+  else if (d.mm) { if (pc) PHR(1, true, true) else PHR(1, true, false) }
+  else { if (pc) PHR(1, false, true) else PHR(1, false, false) }
 #undef PHR
   const hipError_t err = hipGetLastError();
   if (err != hipSuccess && Knob("MBX_PG_DEBUG")) fprintf(stderr, "[mbx] F3h: %s\n", hipGetErrorString(err));
@@ -658,17 +729,21 @@ bool PartGroup(const PartGroupDesc &d, hipStream_t s) {
 #undef PGS
   InitAggStatesCounts(d.st0, d.nv >= 2 ? 2 * d.range : d.range, d.cstar, d.range, s);
   const int npieces = (int)((d.n + piece - 1) / piece);
+  const bool pc = d.nv >= 1 && (unsigned __int128)d.vmaxabs * (uint64_t)piece < ((unsigned __int128)1 << (kPcShift - 1)) &&
+                  !Knob("MBX_PG_NO_PC");
   const size_t rl = ((size_t)4 << shift) +
                     ((size_t)8 << shift) * (size_t)(d.nv == 0 ? 0 : d.nv + (d.mm ? 2 * d.nv : 0));
-#define PGR(TV, NV, MM, PK)                                                                                         \
+#define PGR1(TV, NV, MM, PK, PC)                                                                                    \
   {                                                                                                                 \
-    (void)hipFuncSetAttribute((const void *)pg_reduce_kernel<TV, NV, MM, PK>,                                       \
+    (void)hipFuncSetAttribute((const void *)pg_reduce_kernel<TV, NV, MM, PK, PC>,                                   \
                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)rl);                                 \
-    hipLaunchKernelGGL((pg_reduce_kernel<TV, NV, MM, PK>), dim3(npieces), dim3(kReduceThreads), rl, s, rk,       \
+    hipLaunchKernelGGL((pg_reduce_kernel<TV, NV, MM, PK, PC>), dim3(npieces), dim3(kReduceThreads), rl, s, rk,   \
                        (const TV *)rv0,                                                                             \
                        (const TV *)rv1, d.n, piece, start, np, shift, d.range, d.cstar, d.st0,                      \
                        d.st0 + d.range);                                                                            \
   }
+#define PGR(TV, NV, MM, PK)                                                                                         \
+  if (NV >= 1 && pc) PGR1(TV, NV, MM, PK, true) else PGR1(TV, NV, MM, PK, false)
 #define PGRV(TV)                                                                                                    \
   if (d.nv == 0) PGR(TV, 0, false, false)                                                                           \
   else if (d.nv == 1) { if (d.mm) PGR(TV, 1, true, false) else PGR(TV, 1, false, false) }                            \
@@ -684,6 +759,7 @@ bool PartGroup(const PartGroupDesc &d, hipStream_t s) {
   }
 #undef PGRV
 #undef PGR
+#undef PGR1
   return hipGetLastError() == hipSuccess;
 }
 
