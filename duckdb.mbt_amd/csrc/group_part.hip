@@ -131,18 +131,17 @@ __global__ __launch_bounds__(kScatterThreads) void pg_scatter_kernel(
   const uint32_t lmask = (1u << shift) - 1u;
   const int64_t b = (int64_t)blockIdx.x * chunk, e = min(n, b + chunk);
   // the next tile is loaded into registers while this one's rows are stored
+  // (straight-line loads and stores, as in pg_hscatter: a row past the chunk
+  // loads the chunk's last row and stores into the pad slot after each array)
   uint32_t rel[RPT];
   TV a[RPT], c[RPT];
   auto load = [&](int64_t tb) {
-    const int tn = (int)min((int64_t)kTile, e - tb);
 #pragma unroll
     for (int u = 0; u < RPT; u++) {
-      const int j = u * kScatterThreads + t;
-      if (j < tn) {
-        rel[u] = (uint32_t)((int64_t)key[tb + j] - kmin);
-        if (NV >= 1) a[u] = v0[tb + j];
-        if (NV >= 2) c[u] = v1[tb + j];
-      }
+      const int64_t r = min(tb + u * kScatterThreads + t, e - 1);
+      rel[u] = (uint32_t)((int64_t)key[r] - kmin);
+      if (NV >= 1) a[u] = v0[r];
+      if (NV >= 2) c[u] = v1[r];
     }
   };
   if (b < e) load(b);
@@ -191,18 +190,24 @@ __global__ __launch_bounds__(kScatterThreads) void pg_scatter_kernel(
       if (NV >= 2) sv1[pos] = c[u];
     }
     __syncthreads();
-    if (tb + kTile < e) load(tb + kTile);
-    for (int j = t; j < tn; j += kScatterThreads) {
-      const int pp = sp[j];
-      const unsigned int dst = cur[pp] + (unsigned int)j - base[pp];
-      if (!PACK) ok[dst] = sk[j];
-      if (NV >= 1) ov0[dst] = sv0[j];
-      if (NV >= 2) ov1[dst] = sv1[j];
+    load(min(tb + kTile, e - 1));
+#pragma unroll
+    for (int u = 0; u < RPT; u++) {
+      const int j = u * kScatterThreads + t;
+      const int jj = min(j, tn - 1);
+      const int pp = sp[jj];
+      const size_t dst = j < tn ? (size_t)(cur[pp] + (unsigned int)j - base[pp]) : (size_t)n;  // (n: the pad slot)
+      if (!PACK) ok[dst] = sk[jj];
+      if (NV >= 1) ov0[dst] = sv0[jj];
+      if (NV >= 2) ov1[dst] = sv1[jj];
     }
     __syncthreads();
     for (int p = t; p < np; p += kScatterThreads) cur[p] += cnt[p];
   }
 }
+
+// an array of `bytes` plus one 16-byte pad slot, rounded up to 256 bytes
+static size_t PadUp(size_t bytes) { return (bytes + 16 + 255) & ~(size_t)255; }
 
 size_t ScatterLds(int np, int nv, int vb) {
   return (size_t)kTile * vb * (nv >= 2 ? 2 : nv) + (size_t)kTile * 4 + (size_t)np * 12 + 64;
@@ -366,16 +371,17 @@ __global__ __launch_bounds__(kHThreads) void pg_hscatter_kernel(
   const int64_t b = (int64_t)blockIdx.x * chunk, e = min(n, b + chunk);
   // the next tile's rows are loaded into registers while the current tile's
   // staged records are stored, so the read and write streams overlap
+  // Loads and stores are straight-line (no lane branches), so the compiler's
+  // wait for the prefetched rows counts past the stores issued after them
+  // instead of draining them: a row past the chunk loads the chunk's last row
+  // and stores into the pad slot after the records.
   int64_t kk[RPT], vv[RPT];
   auto load = [&](int64_t tb) {
-    const int tn = (int)min((int64_t)kTile, e - tb);
 #pragma unroll
     for (int u = 0; u < RPT; u++) {
-      const int j = u * kScatterThreads + t;
-      if (j < tn) {
-        kk[u] = (int64_t)key[tb + j];
-        if (NV >= 1) vv[u] = (int64_t)v0[tb + j];
-      }
+      const int64_t r = min(tb + u * kScatterThreads + t, e - 1);
+      kk[u] = (int64_t)key[r];
+      if (NV >= 1) vv[u] = (int64_t)v0[r];
     }
   };
   if (b < e) load(b);
@@ -419,15 +425,18 @@ __global__ __launch_bounds__(kHThreads) void pg_hscatter_kernel(
       if (NV >= 1) srec[(size_t)pos * RS + 1] = vv[u];
     }
     __syncthreads();
-    if (tb + kTile < e) load(tb + kTile);
-    for (int j = t; j < tn; j += kScatterThreads) {
-      const int q = sp[j];
-      const size_t dst = (size_t)(cur[q] + (unsigned int)j - base[q]);
+    load(min(tb + kTile, e - 1));  // (the last tile re-reads a row: no branch)
+#pragma unroll
+    for (int u = 0; u < RPT; u++) {
+      const int j = u * kScatterThreads + t;
+      const int jj = min(j, tn - 1);
+      const int q = sp[jj];
+      const size_t dst = j < tn ? (size_t)(cur[q] + (unsigned int)j - base[q]) : (size_t)n;  // (n: the pad slot)
       if (NV >= 1) {
         typedef int64_t P __attribute__((ext_vector_type(2)));
-        *(P *)(rec + dst * 2) = *(const P *)(srec + (size_t)j * 2);
+        *(P *)(rec + dst * 2) = *(const P *)(srec + (size_t)jj * 2);
       } else {
-        rec[dst] = srec[j];
+        rec[dst] = srec[jj];
       }
     }
     __syncthreads();
@@ -687,9 +696,9 @@ bool PartGroup(const PartGroupDesc &d, hipStream_t s) {
   unsigned int *hist = (unsigned int *)d.scratch_hist;  // [np][grid] counts
   unsigned int *off = hist + (size_t)np * grid;         // ... and their exclusive scan
   unsigned int *start = (unsigned int *)d.scratch_start;  // [np + 1]
-  uint16_t *rk = (uint16_t *)d.scratch_rows;
-  void *rv0 = (char *)d.scratch_rows + (((size_t)d.n * 2 + 255) & ~(size_t)255);
-  void *rv1 = (char *)rv0 + (((size_t)d.n * vb + 255) & ~(size_t)255);
+  uint16_t *rk = (uint16_t *)d.scratch_rows;  // (each array with its pad slot: PartGroupScratch)
+  void *rv0 = (char *)d.scratch_rows + PadUp((size_t)d.n * 2);
+  void *rv1 = (char *)rv0 + PadUp((size_t)d.n * vb);
   const size_t hl = (size_t)np * 4;
   if (d.kphys == P_I64)
     hipLaunchKernelGGL(pg_hist_kernel<int64_t>, dim3(grid), dim3(kScatterThreads), hl, s, (const int64_t *)d.key,
@@ -771,7 +780,7 @@ void PartGroupScratch(int64_t n, int64_t range, int nv, bool mm, int vphys, size
   const int vb = vphys == P_I64 ? 8 : 4;
   *hist_bytes = (size_t)np * grid * 4 * 2;  // counts and their scan
   *start_bytes = (size_t)(np + 1) * 4;
-  *rows_bytes = (((size_t)n * 2 + 255) & ~(size_t)255) + (size_t)std::max(nv, 0) * (((size_t)n * vb + 255) & ~(size_t)255);
+  *rows_bytes = PadUp((size_t)n * 2) + (size_t)std::max(nv, 0) * PadUp((size_t)n * vb);
   size_t tmp = 0;
   unsigned int *dummy = nullptr;
   (void)hipcub::DeviceScan::ExclusiveSum(nullptr, tmp, dummy, dummy, np * grid, (hipStream_t)0);
