@@ -2,8 +2,72 @@
 #include "engine.h"
 
 #include <cstring>
+#include <sys/mman.h>
+
+#include <cstdlib>
+#include <map>
+#include <mutex>
+#include <new>
 
 namespace mbx {
+
+namespace result_blocks {
+// size classes: 1 MiB steps below 16 MiB, then eighths of a power of two
+static size_t ClassOf(size_t b) {
+  const size_t mib = (size_t)1 << 20;
+  if (b <= 16 * mib) return (b + mib - 1) & ~(mib - 1);
+  size_t p = 16 * mib;
+  while (p * 2 < b) p *= 2;
+  const size_t step = p / 8;
+  return (b + step - 1) / step * step;
+}
+constexpr size_t kMinBlock = (size_t)1 << 20;
+constexpr size_t kCacheCap = (size_t)2 << 30;  // bytes kept for reuse, process-wide
+static std::mutex mu;
+static std::multimap<size_t, void *> cache;
+static size_t cached = 0;
+
+void *Get(size_t bytes) {
+  if (bytes < kMinBlock) {
+    void *p = malloc(bytes ? bytes : 1);
+    if (!p) throw std::bad_alloc();
+    return p;
+  }
+  const size_t c = ClassOf(bytes);
+  {
+    std::lock_guard<std::mutex> g(mu);
+    auto it = cache.find(c);
+    if (it != cache.end()) {
+      void *p = it->second;
+      cache.erase(it);
+      cached -= c;
+      return p;
+    }
+  }
+  void *p = mmap(nullptr, c, PROT_READ | PROT_WRITE, MAP_PRIVATE | MAP_ANONYMOUS, -1, 0);
+  if (p == MAP_FAILED) throw std::bad_alloc();
+  (void)madvise(p, c, MADV_HUGEPAGE);
+  return p;
+}
+
+void Put(void *p, size_t bytes) {
+  if (!p) return;
+  if (bytes < kMinBlock) {
+    free(p);
+    return;
+  }
+  const size_t c = ClassOf(bytes);
+  {
+    std::lock_guard<std::mutex> g(mu);
+    if (cached + c <= kCacheCap) {
+      cache.emplace(c, p);
+      cached += c;
+      return;
+    }
+  }
+  munmap(p, c);
+}
+}  // namespace result_blocks
 
 static std::string Lower(std::string s) {
   for (auto &c : s) c = (char)tolower((unsigned char)c);

@@ -66,19 +66,43 @@ struct Catalog {
 };
 
 // Host copy of a result column (after the single D2H of a query).
+// Host buffers of materialized results.  Blocks of 1 MiB and more come from a
+// process-wide cache of recycled blocks (mmap'd with MADV_HUGEPAGE when new):
+// a 1e6-group result is ~60 MB of host columns, and fresh pages from malloc
+// (page faults on first touch, munmap at destroy) cost more than its kernels.
+namespace result_blocks {
+void *Get(size_t bytes);
+void Put(void *p, size_t bytes);
+}  // namespace result_blocks
+template <class T>
+struct ResultAlloc {
+  typedef T value_type;
+  ResultAlloc() = default;
+  template <class U>
+  ResultAlloc(const ResultAlloc<U> &) {}
+  T *allocate(size_t n) { return (T *)result_blocks::Get(n * sizeof(T)); }
+  void deallocate(T *p, size_t n) { result_blocks::Put(p, n * sizeof(T)); }
+  template <class U>
+  bool operator==(const ResultAlloc<U> &) const { return true; }
+  template <class U>
+  bool operator!=(const ResultAlloc<U> &) const { return false; }
+};
+template <class T>
+using ResultVec = std::vector<T, ResultAlloc<T>>;
+
 struct HostColumn {
   std::string name;
   LogicalType type;
   Phys phys = P_I64;
-  std::vector<uint8_t> data;         // fixed-width values
-  std::vector<uint8_t> valid;        // 1 byte per row (1 = valid)
+  ResultVec<uint8_t> data;           // fixed-width values
+  ResultVec<uint8_t> valid;          // 1 byte per row (1 = valid)
   std::vector<int64_t> offsets;      // P_STR
   std::string chars;                 // P_STR
   // cell text formatted on the device (large integer / BOOLEAN / DECIMAL /
   // HUGEINT results of duckdb_mb_query and stream batches): row i's text is
   // text[text_off[i], text_off[i + 1] - 1) (each row's text is followed by a NUL)
-  std::vector<uint32_t> text_off;
-  std::string text;
+  ResultVec<uint32_t> text_off;
+  ResultVec<char> text;
   Value Get(int64_t row) const;
   // Text of a non-NULL integer/BOOLEAN/DECIMAL cell written into out (>= 48
   // bytes), spelled as FormatValue(Get(row)); -1 for the other types.

@@ -3055,7 +3055,7 @@ static ResultPtr ToHostPinned(Engine &e, const DRel &r, const std::vector<std::s
         o += len[i];
       }
       hc.text_off[n] = o;
-      hc.text.assign((const char *)H + j.chr_off, (size_t)j.total);
+      hc.text.assign((const char *)H + j.chr_off, (const char *)H + j.chr_off + (size_t)j.total);
     }
     res->cols.push_back(std::move(hc));
   }

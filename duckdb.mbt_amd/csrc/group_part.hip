@@ -206,6 +206,16 @@ __global__ __launch_bounds__(kScatterThreads) void pg_scatter_kernel(
   }
 }
 
+// the reduce passes' piece: at most 2^20 rows, and the piece count a multiple
+// of the CU count, so the last round of workgroups is not a partial one
+// (1e9 rows: 1024 pieces of 976 563 rows instead of 954 of 2^20)
+static int64_t BalancedPiece(int64_t n) {
+  const int64_t cus = NumCUs(), target = (int64_t)1 << 20;
+  const int64_t rounds = std::max<int64_t>(1, (n + cus * target - 1) / (cus * target));
+  const int64_t pieces = cus * rounds;
+  return std::max<int64_t>(4096, (n + pieces - 1) / pieces);
+}
+
 // an array of `bytes` plus one 16-byte pad slot, rounded up to 256 bytes
 static size_t PadUp(size_t bytes) { return (bytes + 16 + 255) & ~(size_t)255; }
 
@@ -348,9 +358,10 @@ __global__ __launch_bounds__(1024) void pg_reduce_kernel(const uint16_t *__restr
 // query on the hash path instead.
 constexpr int kHashParts = 9;      // log2 partitions
 // the hashed scatter: 8192-row tiles in one 16-wave workgroup per CU, so a
-// tile's run per partition averages 16 records (256 B) -- at 4096-row tiles
-// (8-record runs) it ran 11.2 ms for 1e9 rows
-constexpr int kHTile = 8192, kHThreads = 1024;
+// tile's run per partition averages 16 records (256 B) -- 4096-row tiles
+// (8-record runs) in two workgroups per CU ran 8.70 vs 7.92 ms at 1e6 keys;
+// 256 partitions (32-record runs) 8.42 ms of scatter but a slower reduce
+constexpr int kHTile = 8192, kHThreads = 1024, kHBlocksPerCU = 1;
 constexpr int kHashSlots = 4096;   // LDS table of a piece
 constexpr int kHashGlobal = 8192;  // global table per partition
 constexpr uint64_t kMsb = 0x8000000000000000ull;
@@ -584,13 +595,13 @@ bool PartGroupHashed(const PartGroupDesc &d, unsigned long long *gkeys, int *ove
   if (d.kphys != P_I32 && d.kphys != P_I64) return false;
   if (d.nv > 0 && d.vphys != P_I32 && d.vphys != P_I64) return false;
   const int pbits = kHashParts, np = 1 << pbits;
-  int64_t piece = (int64_t)1 << 20;
+  int64_t piece = BalancedPiece(d.n);
   if (d.nv > 0 && d.vmaxabs > 0) {
     const uint64_t cap = ((uint64_t)1 << 62) / d.vmaxabs;
     if (cap < 4096) return false;
     piece = std::min<int64_t>(piece, (int64_t)cap);
   }
-  const int grid = NumCUs();  // (one kHThreads workgroup per CU in the hist and scatter passes)
+  const int grid = NumCUs() * kHBlocksPerCU;  // (kHThreads workgroups in the hist and scatter passes)
   const int64_t chunk = (((d.n + grid - 1) / grid) + 255) & ~(int64_t)255;
   unsigned int *hist = (unsigned int *)d.scratch_hist, *off = hist + (size_t)np * grid;
   unsigned int *start = (unsigned int *)d.scratch_start;
@@ -654,7 +665,7 @@ int64_t PartGroupHashedSlots() { return ((int64_t)1 << kHashParts) * kHashGlobal
 void PartGroupHashedScratch(int64_t n, int nv, size_t *hist_bytes, size_t *start_bytes, size_t *rows_bytes,
                             size_t *scan_bytes) {
   const int np = 1 << kHashParts;
-  const int grid = NumCUs();
+  const int grid = NumCUs() * kHBlocksPerCU;
   *hist_bytes = (size_t)np * grid * 4 * 2;
   *start_bytes = (size_t)(np + 1) * 4;
   *rows_bytes = (size_t)n * 8 * (nv + 1) + 256;
@@ -681,7 +692,7 @@ bool PartGroup(const PartGroupDesc &d, hipStream_t s) {
   const int shift = PartGroupShift(d.nv, d.mm);
   const int np = (int)((d.range + (1 << shift) - 1) >> shift);
   // int64 LDS sums stay exact over a piece: piece x max|v| < 2^62
-  int64_t piece = (int64_t)1 << 20;
+  int64_t piece = BalancedPiece(d.n);
   if (d.nv > 0 && d.vmaxabs > 0) {
     const uint64_t cap = ((uint64_t)1 << 62) / d.vmaxabs;
     if (cap < 4096) return false;
