@@ -7,7 +7,7 @@
 #   overhead  tools/shard_overhead.py                      shapes  tools/shape_bench.py (SHAPES, NULLABLE)
 #   layout    tools/c3_layout_probe.py                     rehearse  2 gloo ranks on one GPU (--ranks)
 #   prof      rocprofv3 --kernel-trace --stats of bench.py (c2 line with extras)
-#   pmc       rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes of bench.py (one counter set per run)
+#   pmc       rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes of bench.py (C2 line with c3, sel; one counter set per run)
 #   pmc5      the same passes of bench.py --config c5 (1.25e9 rows per launch)
 #   link      tools/link8_probe (8 MB D2H variants; build it first: see its header)
 #   pmcshape  rocprofv3 kernel trace + FETCH_SIZE / WRITE_SIZE of tools/shape_bench.py (PMC_SHAPES)
@@ -25,7 +25,7 @@
 #   gdvar     c3n / c3 under each group_direct_lds launch shape (GD_VARIANTS)
 #   profh     rocprofv3 kernel trace + stats of the c3h and c3n lines (PROFH_CONFIGS, PROFH_GROUPS)
 #   hashab    c3h partitioned (default) vs the hash path (MBX_PART_GROUP=0)
-#   pmcnew    FETCH_SIZE / WRITE_SIZE passes of the c3n and c3h lines
+#   pmcnew    FETCH_SIZE / WRITE_SIZE passes of the c3n, c3h and c3s lines
 #   inlibn    the in-library --gpus 8 (c2) / 4 (c5, c3) line on one GPU (MBX_BENCH_DEVICE_MOD=1)
 # Results go to gpurun_out/ (merged back by gpurun); copy what is judged into profiles/.
 set -o pipefail
@@ -77,7 +77,7 @@ fi
 if has pmc; then
   mkdir -p gpurun_out/pmc
   for ctr in FETCH_SIZE WRITE_SIZE; do
-    ( cd /tmp && export TMPDIR=/tmp && timeout -s KILL 300 rocprofv3 --pmc $ctr --output-format csv -d $R/gpurun_out/pmc/$ctr -o $ctr -- python3 $R/bench.py --steps 5 --warmup 1 --no-cpu > $R/gpurun_out/pmc_$ctr.log 2>&1 ) || exit 22
+    ( cd /tmp && export TMPDIR=/tmp && timeout -s KILL 300 rocprofv3 --pmc $ctr --output-format csv -d $R/gpurun_out/pmc/$ctr -o $ctr -- python3 $R/bench.py --steps 5 --warmup 1 --no-cpu --extra c3,sel > $R/gpurun_out/pmc_$ctr.log 2>&1 ) || exit 22
   done
 fi
 if has pmc5; then  # the same two passes of the C5 line (1.25e9 rows per launch: the filter_agg@1250000000 entry)
@@ -164,7 +164,7 @@ if has gdvar; then  # C3 / C3-with-NULLs under group_direct_lds launch shapes (M
 fi
 if has profh; then  # rocprofv3 kernel trace + stats of the c3h (F3 partitioned GROUP BY) and c3n lines
   mkdir -p gpurun_out/profh
-  for c in ${PROFH_CONFIGS:-c3h c3n}; do
+  for c in ${PROFH_CONFIGS:-c3h c3s c3n}; do
     ( cd /tmp && export TMPDIR=/tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $R/gpurun_out/profh/$c -o $c -- python3 $R/bench.py --config $c --groups ${PROFH_GROUPS:-100000} --extra "" --no-cpu --steps 10 > $R/gpurun_out/profh/$c.json 2> $R/gpurun_out/profh/$c.err ) || exit 43
     python3 $R/tools/rocpd_stats.py $R/gpurun_out/profh/$c/${c}_results.db $R/gpurun_out/profh/${c}_kernel_stats.csv || true
   done
@@ -174,9 +174,9 @@ if has hashab; then  # the wide-key GROUP BY: partitioned (default) vs the hash 
   timeout -k 10 300 python bench.py --config c3h --groups 100000 --steps 10 --warmup 2 --extra "" --no-cpu > gpurun_out/hashab/part.json 2> gpurun_out/hashab/part.err || exit 44
   MBX_EXPERIMENTS=1 MBX_PART_GROUP=0 timeout -k 10 300 python bench.py --config c3h --groups 100000 --steps 3 --warmup 1 --extra "" --no-cpu > gpurun_out/hashab/hash.json 2> gpurun_out/hashab/hash.err || exit 45
 fi
-if has pmcnew; then  # FETCH_SIZE / WRITE_SIZE passes of the c3n and c3h (1e5 keys) lines
+if has pmcnew; then  # FETCH_SIZE / WRITE_SIZE passes of the c3n, c3h and c3s (1e5 keys) lines
   mkdir -p gpurun_out/pmcnew
-  for c in c3n c3h; do
+  for c in c3n c3h c3s; do
     for ctr in FETCH_SIZE WRITE_SIZE; do
       ( cd /tmp && export TMPDIR=/tmp && timeout -s KILL 300 rocprofv3 --pmc $ctr --output-format csv -d $R/gpurun_out/pmcnew/${c}_$ctr -o $ctr -- python3 $R/bench.py --config $c --extra "" --steps 5 --warmup 1 --no-cpu > $R/gpurun_out/pmcnew/${c}_$ctr.log 2>&1 ) || exit 46
     done
