@@ -1070,11 +1070,11 @@ duckdb_state duckdb_mb_list_vector_set_size(duckdb_vector, idx_t) { return DuckD
 duckdb_state duckdb_mb_list_vector_reserve(duckdb_vector, idx_t) { return DuckDBError; }   // ref :2101
 
 // A vector's bytes into the pinned staging buffer, which only the DMA engine
-// reads afterwards: non-temporal stores (no read-for-ownership of the
-// destination lines, nothing evicted from the caller's cache) when both ends
-// are 16-byte aligned -- 64-byte AVX-512 stores where the host has them, else
-// 16-byte SSE2 ones -- else memcpy.  MBX_CHUNK_COPY = memcpy / sse / avx512
-// pins one form (experiments).
+// reads afterwards: memcpy.  Non-temporal stores (no read-for-ownership of the
+// destination lines) measured no better on two boxes -- 1e8-row C4 ingest 17.2
+// (memcpy) vs 17.1 (SSE2 streaming) vs 17.4 GB/s (AVX-512 streaming), then
+// 17.5 vs 16.9 vs 14.1 GB/s (profiles/r06_chunk/, r06_final/chunk/) -- and stay
+// as experiments: MBX_CHUNK_COPY = sse / avx512 (both ends 16-byte aligned).
 __attribute__((target("avx512f"))) static void StreamNt64(void *dst, const void *src, size_t bytes) {
   char *d = (char *)dst;
   const char *p = (const char *)src;
@@ -1097,9 +1097,9 @@ __attribute__((target("avx512f"))) static void StreamNt64(void *dst, const void 
 static void StreamToPinned(void *dst, const void *src, size_t bytes) {
   static const int mode = [] {
     const char *m = Knob("MBX_CHUNK_COPY");
-    if (m && !strcmp(m, "memcpy")) return 0;
     if (m && !strcmp(m, "sse")) return 1;
-    return __builtin_cpu_supports("avx512f") ? 2 : 1;
+    if (m && !strcmp(m, "avx512")) return __builtin_cpu_supports("avx512f") ? 2 : 1;
+    return 0;
   }();
   if (mode == 0 || (((uintptr_t)dst | (uintptr_t)src) & 15)) {
     memcpy(dst, src, bytes);
