@@ -1,6 +1,8 @@
 // engine.cpp — statement dispatch (DDL / DML / SELECT) and host result columns.
 #include "engine.h"
 
+#include <hip/hip_runtime_api.h>
+
 #include <cstring>
 #include <sys/mman.h>
 
@@ -47,6 +49,10 @@ void *Get(size_t bytes) {
   void *p = mmap(nullptr, c, PROT_READ | PROT_WRITE, MAP_PRIVATE | MAP_ANONYMOUS, -1, 0);
   if (p == MAP_FAILED) throw std::bad_alloc();
   (void)madvise(p, c, MADV_HUGEPAGE);
+  // page-locked once for its lifetime in the cache: a result's columns are
+  // DMA targets (a failed registration leaves a pageable block, still valid)
+  (void)hipHostRegister(p, c, hipHostRegisterPortable);
+  (void)hipGetLastError();
   return p;
 }
 
@@ -65,6 +71,8 @@ void Put(void *p, size_t bytes) {
       return;
     }
   }
+  (void)hipHostUnregister(p);
+  (void)hipGetLastError();
   munmap(p, c);
 }
 }  // namespace result_blocks

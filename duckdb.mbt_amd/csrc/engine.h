@@ -7,6 +7,7 @@
 #include <memory>
 #include <mutex>
 #include <string>
+#include <utility>
 #include <vector>
 
 #include "plan.h"
@@ -67,7 +68,8 @@ struct Catalog {
 
 // Host copy of a result column (after the single D2H of a query).
 // Host buffers of materialized results.  Blocks of 1 MiB and more come from a
-// process-wide cache of recycled blocks (mmap'd with MADV_HUGEPAGE when new):
+// process-wide cache of recycled blocks (mmap'd with MADV_HUGEPAGE and
+// page-locked for DMA when new, hipHostRegister):
 // a 1e6-group result is ~60 MB of host columns, and fresh pages from malloc
 // (page faults on first touch, munmap at destroy) cost more than its kernels.
 namespace result_blocks {
@@ -82,6 +84,16 @@ struct ResultAlloc {
   ResultAlloc(const ResultAlloc<U> &) {}
   T *allocate(size_t n) { return (T *)result_blocks::Get(n * sizeof(T)); }
   void deallocate(T *p, size_t n) { result_blocks::Put(p, n * sizeof(T)); }
+  // resize() leaves new elements uninitialised (every caller writes them: a
+  // DMA or a fill loop), so a 32 MB column is not zeroed before its copy
+  template <class U>
+  void construct(U *p) noexcept {
+    ::new ((void *)p) U;
+  }
+  template <class U, class... A>
+  void construct(U *p, A &&...a) {
+    ::new ((void *)p) U(std::forward<A>(a)...);
+  }
   template <class U>
   bool operator==(const ResultAlloc<U> &) const { return true; }
   template <class U>

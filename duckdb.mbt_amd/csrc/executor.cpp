@@ -2979,6 +2979,11 @@ static ResultPtr ToHostPinned(Engine &e, const DRel &r, const std::vector<std::s
   if (count_dev && !mapped) return nullptr;
   if (!mapped && !e.EnsurePinned(need)) return nullptr;
   uint8_t *const H = mapped ? e.h_mapped : e.h_pinned;
+  // large results: the value columns and the device-formatted text go by DMA
+  // straight into the result's own host buffers (page-locked blocks of the
+  // result block cache) instead of through the pinned arena and a host copy
+  const bool direct = !mapped && need >= ((size_t)4 << 20) && !Knob("MBX_RESULT_STAGED");
+  std::vector<HostColumn> dcols(direct ? ncols : 0);
   std::vector<size_t> data_off(ncols), valid_off(ncols, 0);
   dev::HostCopyDesc hd;
   memset(&hd, 0, sizeof(hd));
@@ -2997,7 +3002,13 @@ static ResultPtr ToHostPinned(Engine &e, const DRel &r, const std::vector<std::s
     const int sz = PhysSize(d.phys);
     size_t bytes = (size_t)n * sz;
     data_off[c] = at;
-    if (bytes) seg((const char *)d.data + (size_t)start * sz, at, bytes);
+    if (bytes && direct) {
+      dcols[c].data.resize(bytes);  // (ResultAlloc: no zero fill)
+      HIPCHK(hipMemcpyAsync(dcols[c].data.data(), (const char *)d.data + (size_t)start * sz, bytes,
+                            hipMemcpyDeviceToHost, e.stream));
+    } else if (bytes) {
+      seg((const char *)d.data + (size_t)start * sz, at, bytes);
+    }
     at += (bytes + 63) & ~(size_t)63;
     if (d.validity) {
       valid_off[c] = at;
@@ -3011,7 +3022,12 @@ static ResultPtr ToHostPinned(Engine &e, const DRel &r, const std::vector<std::s
     seg(j.lens->p, at, (size_t)n * 4);
     at += ((size_t)n * 4 + 63) & ~(size_t)63;
     j.chr_off = at;
-    if (j.total) seg(j.chars->p, at, (size_t)j.total);
+    if (j.total && direct) {
+      dcols[j.c].text.resize((size_t)j.total);
+      HIPCHK(hipMemcpyAsync(dcols[j.c].text.data(), j.chars->p, (size_t)j.total, hipMemcpyDeviceToHost, e.stream));
+    } else if (j.total) {
+      seg(j.chars->p, at, (size_t)j.total);
+    }
     at += ((size_t)j.total + 63) & ~(size_t)63;
   }
   if (mapped) {
@@ -3038,7 +3054,12 @@ static ResultPtr ToHostPinned(Engine &e, const DRel &r, const std::vector<std::s
     hc.type = d.type;
     hc.phys = d.phys;
     size_t bytes = (size_t)n * PhysSize(d.phys);
-    hc.data.assign(H + data_off[c], H + data_off[c] + bytes);
+    if (direct) {
+      hc.data = std::move(dcols[c].data);
+      hc.data.resize(bytes);  // (a device row count below n trims)
+    } else {
+      hc.data.assign(H + data_off[c], H + data_off[c] + bytes);
+    }
     if (d.validity && n > 0) {
       const uint64_t *bm = (const uint64_t *)(H + valid_off[c]);
       const int64_t sh = start - (w0 << 6);
@@ -3055,7 +3076,8 @@ static ResultPtr ToHostPinned(Engine &e, const DRel &r, const std::vector<std::s
         o += len[i];
       }
       hc.text_off[n] = o;
-      hc.text.assign((const char *)H + j.chr_off, (const char *)H + j.chr_off + (size_t)j.total);
+      if (direct) hc.text = std::move(dcols[c].text);
+      else hc.text.assign((const char *)H + j.chr_off, (const char *)H + j.chr_off + (size_t)j.total);
     }
     res->cols.push_back(std::move(hc));
   }
