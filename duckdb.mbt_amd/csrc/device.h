@@ -385,6 +385,7 @@ struct TextCol {
 };
 void TextLengths(const TextCol &c, int64_t n, uint32_t *lens, hipStream_t s);
 void TextWrite(const TextCol &c, int64_t n, const int64_t *offsets, char *chars, uint8_t *vbytes, hipStream_t s);
+void OffsetsU32(const int64_t *offsets, uint32_t *out, int64_t m, hipStream_t s);
 
 // Count-first compaction, for a conjunction of range predicates whose columns
 // are all among the (NULL-free, 4/8-byte) outputs, e.g. SELECT x FROM t WHERE

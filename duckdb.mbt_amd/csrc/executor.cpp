@@ -2948,7 +2948,7 @@ static ResultPtr ToHostPinned(Engine &e, const DRel &r, const std::vector<std::s
       TextJob j;
       j.c = c;
       if (!TextCol(r.cols[c], start, j.tc)) continue;
-      j.lens = Alloc(e, (size_t)n * 4);
+      j.lens = Alloc(e, (size_t)n * 4);  // (reused for the 32-bit offsets of a direct copy)
       j.offs = Alloc(e, (size_t)(n + 1) * 8);
       {
         ProfScope ps(e, "text_lengths", (double)n * PhysSize(r.cols[c].phys), n);
@@ -3019,7 +3019,15 @@ static ResultPtr ToHostPinned(Engine &e, const DRel &r, const std::vector<std::s
   }
   for (auto &j : tj) {
     j.len_off = at;
-    seg(j.lens->p, at, (size_t)n * 4);
+    if (direct) {  // the host's 32-bit offsets made on the device, straight into the result
+      // (the scan wrote offsets [0, n); entry n, the total, is set on the host)
+      dev::OffsetsU32((const int64_t *)j.offs->p, (uint32_t *)j.lens->p, n, e.stream);
+      dcols[j.c].text_off.resize((size_t)n + 1);
+      HIPCHK(hipMemcpyAsync(dcols[j.c].text_off.data(), j.lens->p, (size_t)n * 4, hipMemcpyDeviceToHost, e.stream));
+      dcols[j.c].text_off[n] = (uint32_t)j.total;
+    } else {
+      seg(j.lens->p, at, (size_t)n * 4);
+    }
     at += ((size_t)n * 4 + 63) & ~(size_t)63;
     j.chr_off = at;
     if (j.total && direct) {
@@ -3068,6 +3076,11 @@ static ResultPtr ToHostPinned(Engine &e, const DRel &r, const std::vector<std::s
     }
     for (auto &j : tj) {
       if (j.c != c) continue;
+      if (direct) {
+        hc.text_off = std::move(dcols[c].text_off);
+        hc.text = std::move(dcols[c].text);
+        continue;
+      }
       const uint32_t *len = (const uint32_t *)(H + j.len_off);
       hc.text_off.resize((size_t)n + 1);
       uint32_t o = 0;
@@ -3076,8 +3089,7 @@ static ResultPtr ToHostPinned(Engine &e, const DRel &r, const std::vector<std::s
         o += len[i];
       }
       hc.text_off[n] = o;
-      if (direct) hc.text = std::move(dcols[c].text);
-      else hc.text.assign((const char *)H + j.chr_off, (const char *)H + j.chr_off + (size_t)j.total);
+      hc.text.assign((const char *)H + j.chr_off, (const char *)H + j.chr_off + (size_t)j.total);
     }
     res->cols.push_back(std::move(hc));
   }

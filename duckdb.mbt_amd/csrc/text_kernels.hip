@@ -124,7 +124,23 @@ __global__ __launch_bounds__(256) void text_write_kernel(TextCol C, int64_t n, c
   }
 }
 
+// a text column's int64 offsets (the exclusive scan, n + 1 entries) as the
+// host's 32-bit ones (the caller checked the total fits)
+__global__ __launch_bounds__(256) void offsets_u32_kernel(const int64_t *__restrict__ o, uint32_t *__restrict__ out,
+                                                         int64_t m) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < m; i += (int64_t)gridDim.x * blockDim.x)
+    out[i] = (uint32_t)o[i];
+}
+
 }  // namespace
+
+void OffsetsU32(const int64_t *offsets, uint32_t *out, int64_t m, hipStream_t s) {
+  if (m <= 0) return;
+  int64_t blocks = (m + 255) / 256;
+  if (blocks > (int64_t)NumCUs() * 16) blocks = (int64_t)NumCUs() * 16;
+  hipLaunchKernelGGL(offsets_u32_kernel, dim3((unsigned)blocks), dim3(256), 0, s, offsets, out, m);
+  (void)hipGetLastError();
+}
 
 void TextLengths(const TextCol &c, int64_t n, uint32_t *lens, hipStream_t s) {
   if (n <= 0) return;
