@@ -363,3 +363,26 @@ def test_hash_path_above_5e8_rows(mbx, oracle, monkeypatch):
     oc, osum = oracle.synth_groupby(7, 9, 0, n, groups, 1 << 40, -(1 << 39), min(32, max(8, len(os.sched_getaffinity(0)))))
     assert sorted((int(r[0]), int(r[1]), int(r[2])) for r in rows) == [(g * 1000003, osum[g], oc[g]) for g in range(groups)]
     c.close()
+
+
+@pytest.mark.parametrize("n,spread,mult,kern", [
+    (50_001, 150_000, 1, "group_part"), (70_001, 150_000, 1_000_003, "group_part_hashed"),
+    (4_097, 10_000, 1, "group_part"), (65_537, 9_000, -104_729, "group_part_hashed")])
+def test_partitioned_group_by_skew_and_ragged(mbx, n, spread, mult, kern):
+    """One key holding 90 % of the rows (one partition takes almost every row,
+    so one partition spans many reduce pieces) and row counts just past a
+    scatter tile, dense (F3) and sparse (F3h, from 2^16 rows) keys: exact
+    against numpy."""
+    import numpy as np
+    c = _conn(mbx)
+    q(c, f"CREATE TABLE sk AS SELECT CASE WHEN i % 10 = 0 THEN ((i * 7) % {spread}) * ({mult}) "
+         f"ELSE CAST(4242 AS BIGINT) * ({mult}) END AS k, i % 1000 - 500 AS v FROM range({n}) tbl(i)")
+    i = np.arange(n, dtype=np.int64)
+    k = np.where(i % 10 == 0, ((i * 7) % spread) * mult, 4242 * mult)
+    v = i % 1000 - 500
+    rows = q(c, "SELECT k, COUNT(*), SUM(v), MIN(v), MAX(v) FROM sk GROUP BY k").rows
+    assert kern in _kernels(c), _kernels(c)
+    keys, cnt, sv, mnv, mxv = _np_groups(k, {"v": v}, [("sum", "v"), ("min", "v"), ("max", "v")])
+    want = sorted([str(a), str(b), str(c_), str(d_), str(e_)] for a, b, c_, d_, e_ in zip(keys, cnt, sv, mnv, mxv))
+    assert sorted(rows) == want
+    c.close()
