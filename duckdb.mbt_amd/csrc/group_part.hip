@@ -14,31 +14,32 @@
 //   2. (scan)      exclusive prefix over [partition][workgroup] counts:
 //                  partition p's rows land in one contiguous run, every
 //                  workgroup its own sub-run;
-//   3. pg_scatter  the same chunks again: each row takes its slot from an LDS
-//                  cursor of its partition and is written as (key - kmin) u32
-//                  + its value columns; a workgroup keeps a few hundred open
-//                  write streams, so lines fill in L2 before they leave;
+//   3. pg_scatter  the same chunks again, in tiles counting-sorted by
+//                  partition in LDS and stored run by run into the workgroup's
+//                  sub-run of each partition: one 8-byte record per row
+//                  ((v << shift) | index in partition) when the value's zone map
+//                  leaves its top bits free, else a u16 index + the values;
 //   4. pg_reduce   the partitioned rows in fixed-size pieces (grid = pieces):
 //                  each piece walks the partitions it overlaps, adds its rows
 //                  into an LDS table of the partition's keys (COUNT, int64
 //                  sums made overflow-free by the piece size, MIN / MAX), and
 //                  flushes the non-empty keys with one carry-correct int128
 //                  atomic set per key into the dense per-key states.
-// HBM bytes per row: key (hist) + key + values (scatter in) + 4 + values
-// (scatter out) + 4 + values (reduce in); INT64 key and value: 48 B against
-// the 16 B the query names.
+// HBM bytes per row with one INT64 key and value (c3h): 8 (hist) + 16 + 8
+// (scatter) + 8 (reduce) = 40 B against the 16 B the query names.  F3h (the
+// second half of this file) does the same over a hashed partition function
+// for keys too sparse for dense states.
 #include <hip/hip_runtime.h>
 #include <hipcub/hipcub.hpp>
 #include <stdint.h>
 
 #include <algorithm>
+#include <cstdio>
 #include <stdexcept>
 
 #include "device.h"
 #include "knobs.h"
 #include "phys.h"
-
-#include <cstdio>
 
 namespace mbx {
 namespace dev {
