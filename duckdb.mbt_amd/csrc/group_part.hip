@@ -109,14 +109,17 @@ __global__ __launch_bounds__(1024) void pg_hist_kernel(const TK *__restrict__ ke
 // row.  The key leaves as its index inside the partition (u16) -- or, with
 // PACK (one INT64 value column whose zone map leaves its top bits unused),
 // inside the value's low bits: one 8-byte record per row, (v << shift) | index.
-constexpr int kScatterThreads = 512;  // two workgroups per CU: one stages while the other stores
-constexpr int kTile = 4096;           // rows per tile (8 per thread)
+// TILE rows per tile, 8 per thread: 8192-row tiles in one 16-wave workgroup
+// per CU where the staging fits LDS (longer runs per partition), else 4096-row
+// tiles in two 8-wave workgroups per CU (one stages while the other stores)
+constexpr int kScatterThreads = 512, kTile = 4096;
 
-template <typename TK, typename TV, int NV, bool PACK>
-__global__ __launch_bounds__(kScatterThreads) void pg_scatter_kernel(
+template <typename TK, typename TV, int NV, bool PACK, int TILE>
+__global__ __launch_bounds__(TILE / 8) void pg_scatter_kernel(
     const TK *__restrict__ key, const TV *__restrict__ v0, const TV *__restrict__ v1, int64_t n, int64_t chunk,
     int64_t kmin, int shift, int np, const unsigned int *__restrict__ off /* [np][grid] */, uint16_t *__restrict__ ok,
     TV *__restrict__ ov0, TV *__restrict__ ov1) {
+  constexpr int kTile = TILE, kScatterThreads = TILE / 8;
   constexpr int RPT = kTile / kScatterThreads;  // rows per thread and tile
   extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
   TV *sv0 = (TV *)lds;                            // staged values
@@ -220,8 +223,8 @@ static int64_t BalancedPiece(int64_t n) {
 // an array of `bytes` plus one 16-byte pad slot, rounded up to 256 bytes
 static size_t PadUp(size_t bytes) { return (bytes + 16 + 255) & ~(size_t)255; }
 
-size_t ScatterLds(int np, int nv, int vb) {
-  return (size_t)kTile * vb * (nv >= 2 ? 2 : nv) + (size_t)kTile * 4 + (size_t)np * 12 + 64;
+size_t ScatterLds(int np, int nv, int vb, int tile) {
+  return (size_t)tile * vb * (nv >= 2 ? 2 : nv) + (size_t)tile * 4 + (size_t)np * 12 + 64;
 }
 
 // PC (value columns with piece x max|v| < 2^41): a row adds 2^42 + v to one
@@ -699,9 +702,17 @@ bool PartGroup(const PartGroupDesc &d, hipStream_t s) {
     if (cap < 4096) return false;
     piece = std::min<int64_t>(piece, (int64_t)cap);
   }
-  const int grid = NumCUs() * (kScatterThreads == 512 ? 2 : 1);
-  const int64_t chunk = (((d.n + grid - 1) / grid) + 255) & ~(int64_t)255;  // 2-row aligned pairs in every chunk
   const int vb = d.vphys == P_I64 ? 8 : 4;
+  // the scatter's tile: 8192 rows in one 16-wave workgroup per CU where the
+  // staging fits LDS (c3h at 1e6 keys 9.33 vs 10.20 ms of kernels, 1e5 keys
+  // 8.18 vs 8.23: longer runs per partition), else 4096-row tiles in two
+  // workgroups per CU (MBX_PG_TILE=4096 forces these: A/B)
+  int tile = ScatterLds(np, d.nv, vb, 8192) <= (size_t)150 * 1024 ? 8192 : kTile;
+  if (const char *t = Knob("MBX_PG_TILE"))
+    if (atoi(t) == 4096) tile = kTile;
+  const int sthreads = tile / 8;
+  const int grid = NumCUs() * (tile == 4096 ? 2 : 1);
+  const int64_t chunk = (((d.n + grid - 1) / grid) + 255) & ~(int64_t)255;  // 2-row aligned pairs in every chunk
   // one INT64 value column whose |v| leaves shift + 1 top bits unused: the
   // partition index rides in the value's low bits (8-byte records)
   const bool pack = d.nv == 1 && d.vphys == P_I64 && d.vmaxabs < ((uint64_t)1 << (62 - shift));
@@ -713,12 +724,12 @@ bool PartGroup(const PartGroupDesc &d, hipStream_t s) {
   void *rv1 = (char *)rv0 + PadUp((size_t)d.n * vb);
   const size_t hl = (size_t)np * 4;
   if (d.kphys == P_I64)
-    hipLaunchKernelGGL(pg_hist_kernel<int64_t>, dim3(grid), dim3(kScatterThreads), hl, s, (const int64_t *)d.key,
+    hipLaunchKernelGGL(pg_hist_kernel<int64_t>, dim3(grid), dim3(sthreads), hl, s, (const int64_t *)d.key,
                        d.n, chunk, d.kmin, shift, np, hist);
   else
-    hipLaunchKernelGGL(pg_hist_kernel<int32_t>, dim3(grid), dim3(kScatterThreads), hl, s, (const int32_t *)d.key,
+    hipLaunchKernelGGL(pg_hist_kernel<int32_t>, dim3(grid), dim3(sthreads), hl, s, (const int32_t *)d.key,
                        d.n, chunk, d.kmin, shift, np, hist);
-  const size_t sl = ScatterLds(np, d.nv, vb);
+  const size_t sl = ScatterLds(np, d.nv, vb, tile);
   // partition p starts at the offset of its first workgroup's sub-run
   size_t tmp = 0;
   const int nh = np * grid;
@@ -727,14 +738,16 @@ bool PartGroup(const PartGroupDesc &d, hipStream_t s) {
   (void)hipcub::DeviceScan::ExclusiveSum(d.scratch_scan, tmp, hist, off, nh, s);
   (void)hipMemcpy2DAsync(start, 4, off, (size_t)grid * 4, 4, np, hipMemcpyDeviceToDevice, s);
   (void)hipMemsetD32Async((hipDeviceptr_t)(start + np), (int)(unsigned int)d.n, 1, s);
-#define PGS(TK, TV, NV, PK)                                                                                         \
+#define PGS1(TK, TV, NV, PK, T)                                                                                     \
   {                                                                                                                 \
-    (void)hipFuncSetAttribute((const void *)pg_scatter_kernel<TK, TV, NV, PK>,                                      \
+    (void)hipFuncSetAttribute((const void *)pg_scatter_kernel<TK, TV, NV, PK, T>,                                   \
                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)sl);                                 \
-    hipLaunchKernelGGL((pg_scatter_kernel<TK, TV, NV, PK>), dim3(grid), dim3(kScatterThreads), sl, s,              \
-                       (const TK *)d.key, (const TV *)d.v0, (const TV *)d.v1, d.n, chunk, d.kmin, shift, np, off,  \
-                       rk, (TV *)rv0, (TV *)rv1);                                                                   \
+    hipLaunchKernelGGL((pg_scatter_kernel<TK, TV, NV, PK, T>), dim3(grid), dim3(T / 8), sl, s, (const TK *)d.key, \
+                       (const TV *)d.v0, (const TV *)d.v1, d.n, chunk, d.kmin, shift, np, off, rk, (TV *)rv0,      \
+                       (TV *)rv1);                                                                                  \
   }
+#define PGS(TK, TV, NV, PK)                                                                                         \
+  if (tile == 8192) PGS1(TK, TV, NV, PK, 8192) else PGS1(TK, TV, NV, PK, 4096)
 #define PGSV(TK)                                                                                                    \
   if (d.vphys == P_I64) {                                                                                           \
     if (d.nv == 0) PGS(TK, int64_t, 0, false)                                                                       \
@@ -748,6 +761,7 @@ bool PartGroup(const PartGroupDesc &d, hipStream_t s) {
   if (d.kphys == P_I64) { PGSV(int64_t) } else { PGSV(int32_t) }
 #undef PGSV
 #undef PGS
+#undef PGS1
   InitAggStatesCounts(d.st0, d.nv >= 2 ? 2 * d.range : d.range, d.cstar, d.range, s);
   const int npieces = (int)((d.n + piece - 1) / piece);
   const bool pc = d.nv >= 1 && (unsigned __int128)d.vmaxabs * (uint64_t)piece < ((unsigned __int128)1 << (kPcShift - 1)) &&
